@@ -1,0 +1,193 @@
+/*
+ * sfm_amd — MI355X-native bundle-adjustment + feature-tracking core for the
+ * hulop/SfM pipeline.  Plain C ABI: no C++ types, no exceptions, caller-owned
+ * arrays, 0 / negative-errno return codes, sfm_last_error() for the message.
+ *
+ * Drop-in boundary.  Each entry point names the reference
+ * interface it replaces:
+ *
+ *   sfm_ba_solve
+ *     replaces void CTracker::bundleAdjustmentStructAndPose(
+ *         const vector<Point2d>& observations, const vector<int>& camIdx,
+ *         const vector<Matx33d>& K, vector<double*>& R, vector<double*>& t,
+ *         vector<double*>& pts3D, int isStructOrPose)
+ *     declared /root/reference/CTracker.h:65, defined CTracker.cpp:670-702,
+ *     called from CSfM::bundleAdjustment (CSfM.cpp:343).  The reference
+ *     identifies parameter blocks by address (duplicated double* per
+ *     observation); this ABI takes the deduplicated form: pt_idx[i] indexes
+ *     X[n_pts][3] (include/sfm_ctracker_compat.hpp does the address
+ *     dedup and the in-place scatter-back for C++ callers).
+ *     Ceres' ceres::Solver::Summary, which the reference discards
+ *     (CTracker.cpp:700-701), is returned in *summary.
+ *
+ *   sfm_match_features
+ *     replaces CTracker::matchFeatures(pts0, desc0, pts1, desc1, idx0, idx1,
+ *     minDistance, maxDistance)  (CTracker.h:55, CTracker.cpp:211-250) and,
+ *     with min/max = 1.5/40 (CTracker.cpp:30-31), the member-window overload
+ *     (CTracker.h:53, CTracker.cpp:114-149).  The index-subset overload
+ *     (CTracker.h:56, CTracker.cpp:368-417) is the same call on gathered
+ *     rows followed by an index map (sfm_amd/ctracker.py, the compat header).
+ *
+ * Every function is synchronous with respect to the caller's host buffers.
+ */
+#ifndef SFM_AMD_H_
+#define SFM_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFM_ABI_VERSION 1
+
+/* Error codes (negative errno values). */
+#define SFM_OK 0
+#define SFM_EINVAL (-22)   /* bad argument / out-of-range index / non-finite input */
+#define SFM_ENOMEM (-12)   /* device allocation failed */
+#define SFM_ENODEV (-19)   /* no usable HIP device */
+#define SFM_EIO (-5)       /* HIP / RCCL runtime error */
+#define SFM_ENOTSUP (-95)  /* mode not supported by the device path */
+
+/* BA_TYPE (CTracker.h:67). */
+#define SFM_BA_STRUCT_ONLY 0
+#define SFM_BA_POSE_ONLY 1
+#define SFM_BA_STRUCT_AND_POSE 2
+
+/* The Ceres options that matter for the reference's solve.  The reference
+ * sets linear_solver_type = DENSE_SCHUR and silent logging and leaves every
+ * other option at its Ceres default (CTracker.cpp:571-577);
+ * sfm_ba_default_options() returns those defaults. */
+typedef struct sfm_ba_options {
+  int32_t max_num_iterations;                /* 50 */
+  int32_t max_num_consecutive_invalid_steps; /* 5 */
+  int32_t jacobi_scaling;                    /* 1 */
+  int32_t reserved0;
+  double function_tolerance;          /* 1e-6 */
+  double gradient_tolerance;          /* 1e-10 */
+  double parameter_tolerance;         /* 1e-8 */
+  double initial_trust_region_radius; /* 1e4 */
+  double max_trust_region_radius;     /* 1e16 */
+  double min_trust_region_radius;     /* 1e-32 */
+  double min_lm_diagonal;             /* 1e-6 */
+  double max_lm_diagonal;             /* 1e32 */
+  double min_relative_decrease;       /* 1e-3 */
+} sfm_ba_options;
+
+/* termination_type values (ceres::TerminationType subset). */
+#define SFM_CONVERGENCE 0
+#define SFM_NO_CONVERGENCE 1
+#define SFM_FAILURE 2
+
+typedef struct sfm_ba_summary {
+  int32_t termination_type;
+  int32_t num_iterations; /* LM iterations (iteration 0 = initial evaluation not counted) */
+  int32_t num_successful_steps;
+  int32_t num_unsuccessful_steps;
+  int32_t num_invalid_steps;
+  int32_t num_residual_evaluations; /* full residual-vector evaluations (Jacobian passes included) */
+  int32_t num_jacobian_evaluations;
+  int32_t num_linear_solves;
+  double initial_cost;
+  double final_cost;
+  double wall_time_s;
+  double jacobian_time_s;
+  double linear_solver_time_s;
+  double residual_time_s;
+} sfm_ba_summary;
+
+/* One entry per iteration (ceres::IterationSummary subset). */
+typedef struct sfm_ba_iteration {
+  int32_t iteration;
+  int32_t step_is_valid;
+  int32_t step_is_successful;
+  int32_t reserved;
+  double cost;
+  double cost_change;
+  double gradient_max_norm;
+  double step_norm;
+  double relative_decrease;
+  double trust_region_radius;
+} sfm_ba_iteration;
+
+typedef struct sfm_ba_handle sfm_ba_handle;
+
+int32_t sfm_abi_version(void);
+const char* sfm_last_error(void);
+void sfm_ba_default_options(sfm_ba_options* opts);
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int32_t sfm_device_count(void);
+
+/* One-shot drop-in solve (host arrays in, results written in place):
+ *   obs_uv [n_obs][2] undistorted pixel observations (CFrame::_pts, Kopt frame)
+ *   cam_idx[n_obs] in [0, n_cams), pt_idx[n_obs] in [0, n_pts)
+ *   K9 [n_cams][9] row-major Matx33d::val (only [0],[1],[2],[4],[5] are read)
+ *   rot, t [n_cams][3] angle-axis / translation (CFrame::_rot, _t); X [n_pts][3]
+ * mode: SFM_BA_* (any other value adds no residuals: returns 0, no change).
+ * trace (optional): per-iteration records, capacity trace_cap, *trace_len set. */
+int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const double* obs_uv,
+                 const int32_t* cam_idx, const int32_t* pt_idx, int32_t n_cams, const double* K9, double* rot,
+                 double* t, int32_t n_pts, double* X, sfm_ba_summary* summary, sfm_ba_iteration* trace,
+                 int32_t trace_cap, int32_t* trace_len);
+
+/* Resident-problem API (problem uploaded once, solved many times from HBM).
+ * With sfm_ba_set_comm the problem is one landmark shard of a larger one:
+ * every rank passes ALL cameras and its own points / observations. */
+int sfm_ba_create(int32_t device, sfm_ba_handle** out);
+int sfm_ba_destroy(sfm_ba_handle* h);
+int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, const int32_t* cam_idx,
+                       const int32_t* pt_idx, int32_t n_cams, const double* K9, const double* rot, const double* t,
+                       int32_t n_pts, const double* X);
+/* Restore the parameters given to sfm_ba_set_problem (device-to-device). */
+int sfm_ba_reset_parameters(sfm_ba_handle* h);
+int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts, int32_t mode, sfm_ba_summary* summary,
+                          sfm_ba_iteration* trace, int32_t trace_cap, int32_t* trace_len);
+int sfm_ba_get_parameters(sfm_ba_handle* h, double* rot, double* t, double* X);
+/* One residual + Jacobian pass at the current parameters (unscaled J).
+ * res [n_obs][2], jac [n_obs][2][9] (columns dR | dt | dX) in the caller's
+ * observation order; either may be NULL; *cost = 1/2 |r|^2 (may be NULL). */
+int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac);
+/* `reps` back-to-back Jacobian passes on the resident problem (benchmark
+ * of the HBM-bound kernel); *avg_ms = mean duration per pass (HIP events). */
+int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms);
+/* Per-phase device time of the last solve (ms): [jacobian, cam_reduce,
+ * point_eval, point_prep, schur, cholesky, backsolve, backsub, other]. */
+int sfm_ba_phase_times(sfm_ba_handle* h, double* ms9);
+/* Enable per-phase HIP-event timing for subsequent solves (adds syncs). */
+int sfm_ba_set_profiling(sfm_ba_handle* h, int32_t on);
+/* Synchronise the handle's stream. */
+int sfm_ba_sync(sfm_ba_handle* h);
+
+/* Multi-GPU (landmark sharding, RCCL over xGMI).  Rank 0 creates the id,
+ * the caller distributes its 128 bytes (e.g. torch.distributed), every rank
+ * calls sfm_ba_set_comm before sfm_ba_set_problem. */
+int sfm_comm_unique_id(uint8_t out[128]);
+int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_t id[128]);
+
+/* Hamming 2-NN matcher + the reference's sequential acceptance rule.
+ *   pts0/pts1 [n][2] double positions, desc0/desc1 [n][desc_bytes] (BRISK: 64)
+ *   idx0/idx1 capacity >= min(n0, n1); *n_matches = number written.
+ * ratio_test 0.8 and (min,max) = (1.5, 40) px in the reference.
+ * Falls back to no matches when n1 < 2 (reference UB, CTracker.cpp:224). */
+int sfm_match_features(int32_t device, const double* pts0, const uint8_t* desc0, int32_t n0, const double* pts1,
+                       const uint8_t* desc1, int32_t n1, int32_t desc_bytes, double ratio_test, double min_distance,
+                       double max_distance, int32_t* idx0, int32_t* idx1, int32_t* n_matches);
+/* The 2-NN search alone: best/second train index + Hamming distance per query. */
+int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uint8_t* desc1, int32_t n1,
+                     int32_t desc_bytes, int32_t* best_idx, int32_t* best_dist, int32_t* second_idx,
+                     int32_t* second_dist);
+
+/* Synthetic scenes, host-only.  Points [p_begin, p_end) of a
+ * scene with n_pts_total points; every camera is returned.  Observations are
+ * sorted by (point, camera); pt_idx is relative to p_begin.
+ * n_obs = (p_end - p_begin) * views.  NULL *_true / *_init pointers allowed. */
+void sfm_scene_default_intrinsics(double K9[9]);
+int sfm_scene_generate(int32_t n_cams, int32_t n_pts_total, int32_t p_begin, int32_t p_end, int32_t views,
+                       uint64_t seed, double pixel_sigma, double pt_sigma, double rot_sigma, double t_sigma,
+                       double* K9, double* rot_true, double* t_true, double* X_true, double* rot_init,
+                       double* t_init, double* X_init, double* obs_uv, int32_t* cam_idx, int32_t* pt_idx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFM_AMD_H_ */

@@ -1,0 +1,140 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of liboracle.so (the CPU restatement of the reference path,
+see ba_oracle.cpp / match_oracle.cpp headers).  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.
+PARITY UNPINNED: no reference test or fixture pins these results.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("max_num_iterations", c_int32), ("max_num_consecutive_invalid_steps", c_int32),
+                ("jacobi_scaling", c_int32), ("pad_", c_int32)] + [
+        (n, c_double) for n in ("function_tolerance", "gradient_tolerance", "parameter_tolerance",
+                                "initial_trust_region_radius", "max_trust_region_radius", "min_trust_region_radius",
+                                "min_lm_diagonal", "max_lm_diagonal", "min_relative_decrease")]
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("termination_type", "num_iterations", "num_successful_steps",
+                                       "num_unsuccessful_steps", "num_invalid_steps", "num_residual_evaluations",
+                                       "num_jacobian_evaluations", "num_linear_solves")] + [
+        (n, c_double) for n in ("initial_cost", "final_cost", "wall_time_s", "jacobian_time_s",
+                                "linear_solver_time_s", "residual_time_s")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class Iteration(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("iteration", "step_is_valid", "step_is_successful", "pad_")] + [
+        (n, c_double) for n in ("cost", "cost_change", "gradient_max_norm", "step_norm", "relative_decrease",
+                                "trust_region_radius")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "pad_"}
+
+
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_default_options.argtypes = [POINTER(Options)]
+        L.oracle_default_options.restype = None
+        L.oracle_ba_residuals_jacobians.argtypes = [c_int64] + [c_void_p] * 9
+        L.oracle_ba_residuals_jacobians.restype = c_int
+        L.oracle_ba_solve.argtypes = [POINTER(Options), c_int, c_int64, c_void_p, c_void_p, c_void_p, c_int32,
+                                      c_void_p, c_void_p, c_void_p, c_int32, c_void_p, POINTER(Summary), c_void_p,
+                                      c_int32, POINTER(c_int32)]
+        L.oracle_ba_solve.restype = c_int
+        L.oracle_knn2_hamming.argtypes = [c_void_p, c_int32, c_void_p, c_int32, c_int32] + [c_void_p] * 4
+        L.oracle_knn2_hamming.restype = c_int
+        L.oracle_match_features.argtypes = [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                            c_double, c_double, c_double, c_void_p, c_void_p]
+        L.oracle_match_features.restype = c_int
+        _L = L
+    return _L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(c_void_p)
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    lib().oracle_default_options(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def residuals_jacobians(uv, cam_idx, pt_idx, K9, rot, t, X, jacobian=True):
+    uv = np.ascontiguousarray(uv, np.float64)
+    cam_idx = np.ascontiguousarray(cam_idx, np.int32)
+    pt_idx = np.ascontiguousarray(pt_idx, np.int32)
+    K9 = np.ascontiguousarray(K9, np.float64).reshape(-1, 9)
+    rot, t, X = (np.ascontiguousarray(a, np.float64) for a in (rot, t, X))
+    n = uv.shape[0]
+    res = np.zeros((n, 2))
+    jac = np.zeros((n, 2, 9)) if jacobian else None
+    rc = lib().oracle_ba_residuals_jacobians(n, _p(uv), _p(cam_idx), _p(pt_idx), _p(K9), _p(rot), _p(t), _p(X),
+                                             _p(res), _p(jac))
+    assert rc == 0
+    return res, jac
+
+
+def solve(uv, cam_idx, pt_idx, K9, rot, t, X, mode=2, options: Options | None = None, trace_cap=128):
+    """rot, t, X are updated in place (float64, C-contiguous)."""
+    uv = np.ascontiguousarray(uv, np.float64)
+    cam_idx = np.ascontiguousarray(cam_idx, np.int32)
+    pt_idx = np.ascontiguousarray(pt_idx, np.int32)
+    K9 = np.ascontiguousarray(K9, np.float64).reshape(-1, 9)
+    o = options if options is not None else default_options()
+    sm = Summary()
+    tr = (Iteration * trace_cap)()
+    tl = c_int32(0)
+    rc = lib().oracle_ba_solve(ctypes.byref(o), mode, uv.shape[0], _p(uv), _p(cam_idx), _p(pt_idx), rot.shape[0],
+                               _p(K9), _p(rot), _p(t), X.shape[0], _p(X), ctypes.byref(sm), tr, trace_cap,
+                               ctypes.byref(tl))
+    if rc != 0:
+        raise RuntimeError(f"oracle_ba_solve returned {rc}")
+    return sm.as_dict(), [tr[i].as_dict() for i in range(tl.value)]
+
+
+def knn2(desc0, desc1):
+    desc0 = np.ascontiguousarray(desc0, np.uint8)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    n0, n1 = desc0.shape[0], desc1.shape[0]
+    out = [np.zeros(n0, np.int32) for _ in range(4)]
+    lib().oracle_knn2_hamming(_p(desc0), n0, _p(desc1), n1, desc0.shape[1], *map(_p, out))
+    return tuple(out)
+
+
+def match_features(pts0, desc0, pts1, desc1, ratio=0.8, min_distance=1.5, max_distance=40.0):
+    pts0 = np.ascontiguousarray(pts0, np.float64).reshape(-1, 2)
+    pts1 = np.ascontiguousarray(pts1, np.float64).reshape(-1, 2)
+    desc0 = np.ascontiguousarray(desc0, np.uint8)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    n0, n1 = pts0.shape[0], pts1.shape[0]
+    nb = desc0.shape[1] if n0 else 64
+    cap = max(1, min(n0, n1))
+    i0 = np.zeros(cap, np.int32)
+    i1 = np.zeros(cap, np.int32)
+    m = lib().oracle_match_features(_p(pts0), _p(desc0), n0, _p(pts1), _p(desc1), n1, nb, ratio, min_distance,
+                                    max_distance, _p(i0), _p(i1))
+    return i0[:m].copy(), i1[:m].copy()

@@ -1,0 +1,165 @@
+"""ctypes binding of include/sfm_amd.h (libsfm_amd.so, built in-tree).
+
+The product path has no CPU fallback: if the HIP library is missing or a
+call fails, an exception is raised.  Struct layouts mirror the header
+field for field.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8, c_uint64, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsfm_amd.so")
+
+
+class SfmError(RuntimeError):
+    """A C-ABI call returned a negative errno-style code."""
+
+    def __init__(self, code: int, what: str, msg: str):
+        super().__init__(f"{what} failed with {code}: {msg}")
+        self.code = code
+
+
+class BAOptions(ctypes.Structure):
+    _fields_ = [
+        ("max_num_iterations", c_int32),
+        ("max_num_consecutive_invalid_steps", c_int32),
+        ("jacobi_scaling", c_int32),
+        ("reserved0", c_int32),
+        ("function_tolerance", c_double),
+        ("gradient_tolerance", c_double),
+        ("parameter_tolerance", c_double),
+        ("initial_trust_region_radius", c_double),
+        ("max_trust_region_radius", c_double),
+        ("min_trust_region_radius", c_double),
+        ("min_lm_diagonal", c_double),
+        ("max_lm_diagonal", c_double),
+        ("min_relative_decrease", c_double),
+    ]
+
+
+class BASummary(ctypes.Structure):
+    _fields_ = [
+        ("termination_type", c_int32),
+        ("num_iterations", c_int32),
+        ("num_successful_steps", c_int32),
+        ("num_unsuccessful_steps", c_int32),
+        ("num_invalid_steps", c_int32),
+        ("num_residual_evaluations", c_int32),
+        ("num_jacobian_evaluations", c_int32),
+        ("num_linear_solves", c_int32),
+        ("initial_cost", c_double),
+        ("final_cost", c_double),
+        ("wall_time_s", c_double),
+        ("jacobian_time_s", c_double),
+        ("linear_solver_time_s", c_double),
+        ("residual_time_s", c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class BAIteration(ctypes.Structure):
+    _fields_ = [
+        ("iteration", c_int32),
+        ("step_is_valid", c_int32),
+        ("step_is_successful", c_int32),
+        ("reserved", c_int32),
+        ("cost", c_double),
+        ("cost_change", c_double),
+        ("gradient_max_norm", c_double),
+        ("step_norm", c_double),
+        ("relative_decrease", c_double),
+        ("trust_region_radius", c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "sfm_abi_version": (c_int32, []),
+    "sfm_last_error": (c_char_p, []),
+    "sfm_ba_default_options": (None, [POINTER(BAOptions)]),
+    "sfm_device_count": (c_int32, []),
+    "sfm_ba_solve": (c_int, [POINTER(BAOptions), c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                             c_void_p, c_void_p, c_int32, c_void_p, POINTER(BASummary), c_void_p, c_int32,
+                             POINTER(c_int32)]),
+    "sfm_ba_create": (c_int, [c_int32, POINTER(c_void_p)]),
+    "sfm_ba_destroy": (c_int, [c_void_p]),
+    "sfm_ba_set_problem": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_int32, c_void_p]),
+    "sfm_ba_reset_parameters": (c_int, [c_void_p]),
+    "sfm_ba_solve_resident": (c_int, [c_void_p, POINTER(BAOptions), c_int32, POINTER(BASummary), c_void_p, c_int32,
+                                      POINTER(c_int32)]),
+    "sfm_ba_get_parameters": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sfm_ba_evaluate": (c_int, [c_void_p, POINTER(c_double), c_void_p, c_void_p]),
+    "sfm_ba_bench_jacobian": (c_int, [c_void_p, c_int32, POINTER(c_double)]),
+    "sfm_ba_phase_times": (c_int, [c_void_p, c_void_p]),
+    "sfm_ba_set_profiling": (c_int, [c_void_p, c_int32]),
+    "sfm_ba_sync": (c_int, [c_void_p]),
+    "sfm_comm_unique_id": (c_int, [c_void_p]),
+    "sfm_ba_set_comm": (c_int, [c_void_p, c_int32, c_int32, c_void_p]),
+    "sfm_match_features": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                   c_double, c_double, c_double, c_void_p, c_void_p, POINTER(c_int32)]),
+    "sfm_knn2_hamming": (c_int, [c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
+    "sfm_scene_default_intrinsics": (None, [c_void_p]),
+    "sfm_scene_generate": (c_int, [c_int32, c_int32, c_int32, c_int32, c_int32, c_uint64, c_double, c_double,
+                                   c_double, c_double] + [c_void_p] * 10),
+}
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsfm_amd.so once.  Raises if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the HIP path)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGNATURES)
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SfmError(rc, what, lib().sfm_last_error().decode(errors="replace"))
+
+
+def ptr(a: np.ndarray | None) -> c_void_p | None:
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to the C ABI must be C-contiguous"
+    return a.ctypes.data_as(c_void_p)
+
+
+def default_options() -> BAOptions:
+    o = BAOptions()
+    lib().sfm_ba_default_options(ctypes.byref(o))
+    return o
+
+
+def device_count() -> int:
+    return int(lib().sfm_device_count())
+
+
+__all__ = ["lib", "check", "ptr", "BAOptions", "BASummary", "BAIteration", "SfmError", "default_options",
+           "device_count", "exported_symbols", "LIB_PATH", "c_uint8"]

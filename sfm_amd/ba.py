@@ -1,0 +1,139 @@
+"""Device bundle adjuster (resident-problem API of include/sfm_amd.h)."""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_double, c_int32, c_void_p
+
+import numpy as np
+
+from ._ffi import BAIteration, BAOptions, BASummary, check, default_options, lib, ptr
+
+STRUCT_ONLY, POSE_ONLY, STRUCT_AND_POSE = 0, 1, 2   # CTracker::BA_TYPE (CTracker.h:67)
+TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
+PHASES = ["jacobian", "cam_reduce", "point_eval", "point_prep", "schur", "cholesky", "backsolve", "backsub", "other"]
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def make_options(**overrides) -> BAOptions:
+    o = default_options()
+    for k, v in overrides.items():
+        if not hasattr(o, k):
+            raise KeyError(k)
+        setattr(o, k, v)
+    return o
+
+
+class BundleAdjuster:
+    """A problem resident in HBM on one GPU (or one landmark shard of it)."""
+
+    def __init__(self, device: int = 0):
+        h = c_void_p()
+        check(lib().sfm_ba_create(device, ctypes.byref(h)), "sfm_ba_create")
+        self._h = h
+        self.device = device
+        self.n_obs = self.n_cams = self.n_pts = 0
+
+    def close(self) -> None:
+        if self._h:
+            lib().sfm_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- multi-GPU -------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib().sfm_comm_unique_id(buf), "sfm_comm_unique_id")
+        return bytes(buf)
+
+    def set_comm(self, nranks: int, rank: int, uid: bytes) -> None:
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().sfm_ba_set_comm(self._h, nranks, rank, buf), "sfm_ba_set_comm")
+
+    # ---- problem ---------------------------------------------------------
+    def set_problem(self, uv, cam_idx, pt_idx, K9, rot, t, X) -> None:
+        uv, K9, rot, t, X = _f64(uv), _f64(K9), _f64(rot), _f64(t), _f64(X)
+        cam_idx, pt_idx = _i32(cam_idx), _i32(pt_idx)
+        n = int(uv.shape[0])
+        C, P = int(rot.shape[0]), int(X.shape[0])
+        check(lib().sfm_ba_set_problem(self._h, n, ptr(uv), ptr(cam_idx), ptr(pt_idx), C, ptr(K9), ptr(rot),
+                                       ptr(t), P, ptr(X)), "sfm_ba_set_problem")
+        self.n_obs, self.n_cams, self.n_pts = n, C, P
+
+    def reset(self) -> None:
+        check(lib().sfm_ba_reset_parameters(self._h), "sfm_ba_reset_parameters")
+
+    def solve(self, options: BAOptions | None = None, mode: int = STRUCT_AND_POSE, trace_cap: int = 128):
+        opts = options if options is not None else default_options()
+        sm = BASummary()
+        tr = (BAIteration * trace_cap)()
+        tl = c_int32(0)
+        check(lib().sfm_ba_solve_resident(self._h, ctypes.byref(opts), mode, ctypes.byref(sm), tr, trace_cap,
+                                          ctypes.byref(tl)), "sfm_ba_solve_resident")
+        return sm, [tr[i].as_dict() for i in range(tl.value)]
+
+    def parameters(self):
+        rot = np.zeros((self.n_cams, 3))
+        t = np.zeros((self.n_cams, 3))
+        X = np.zeros((self.n_pts, 3))
+        check(lib().sfm_ba_get_parameters(self._h, ptr(rot), ptr(t), ptr(X)), "sfm_ba_get_parameters")
+        return rot, t, X
+
+    def evaluate(self, want_jacobian: bool = True):
+        cost = c_double(0.0)
+        res = np.zeros((self.n_obs, 2))
+        jac = np.zeros((self.n_obs, 2, 9)) if want_jacobian else None
+        check(lib().sfm_ba_evaluate(self._h, ctypes.byref(cost), ptr(res), ptr(jac)), "sfm_ba_evaluate")
+        return cost.value, res, jac
+
+    def bench_jacobian(self, reps: int) -> float:
+        ms = c_double(0.0)
+        check(lib().sfm_ba_bench_jacobian(self._h, reps, ctypes.byref(ms)), "sfm_ba_bench_jacobian")
+        return ms.value
+
+    def set_profiling(self, on: bool) -> None:
+        check(lib().sfm_ba_set_profiling(self._h, 1 if on else 0), "sfm_ba_set_profiling")
+
+    def phase_times(self) -> dict:
+        buf = np.zeros(2 * len(PHASES))
+        check(lib().sfm_ba_phase_times(self._h, ptr(buf)), "sfm_ba_phase_times")
+        return {p: {"ms": float(buf[i]), "count": int(buf[len(PHASES) + i])} for i, p in enumerate(PHASES)}
+
+    def sync(self) -> None:
+        check(lib().sfm_ba_sync(self._h), "sfm_ba_sync")
+
+
+def solve(uv, cam_idx, pt_idx, K9, rot, t, X, options: BAOptions | None = None, mode: int = STRUCT_AND_POSE,
+          trace_cap: int = 128):
+    """One-shot drop-in solve (sfm_ba_solve): rot, t, X are updated in place."""
+    for name, a in (("rot", rot), ("t", t), ("X", X)):
+        if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]):
+            raise TypeError(f"{name} must be a C-contiguous float64 array (updated in place)")
+    uv, K9 = _f64(uv), _f64(K9)
+    cam_idx, pt_idx = _i32(cam_idx), _i32(pt_idx)
+    opts = options if options is not None else default_options()
+    sm = BASummary()
+    tr = (BAIteration * trace_cap)()
+    tl = c_int32(0)
+    check(lib().sfm_ba_solve(ctypes.byref(opts), mode, int(uv.shape[0]), ptr(uv), ptr(cam_idx), ptr(pt_idx),
+                             int(rot.shape[0]), ptr(K9), ptr(rot), ptr(t), int(X.shape[0]), ptr(X),
+                             ctypes.byref(sm), tr, trace_cap, ctypes.byref(tl)), "sfm_ba_solve")
+    return sm, [tr[i].as_dict() for i in range(tl.value)]

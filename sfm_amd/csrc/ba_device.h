@@ -1,0 +1,125 @@
+// Device-side data layout of one bundle-adjustment problem (one rank's shard)
+// and the launchers of the LM-iteration kernels.  See DESIGN.md §3 for the
+// HBM layout and the per-kernel roofline arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace sfm {
+
+// Per-observation Jacobian record written by the Jacobian pass (doubles):
+//   [0..5]  J_X  (2 x 3, row-major)   d r / d X          (scaled)
+//   [6..7]  r    (2)                   residual
+//   [8..19] J_c  (2 x 6, row-major)   d r / d (rot, t)   (scaled)
+constexpr int kJRec = 20;
+constexpr int kJX = 0, kRes = 6, kJC = 8;
+// Per-observation Schur record written every LM iteration:
+//   [0..5] M = J_X L_p^-T (2 x 3)   [6..7] h = M z_p
+constexpr int kMRec = 8;
+// Per-camera rotation data: R (9, row-major) and dR/dw_k (27, k-major).
+constexpr int kCamR = 36;
+// Per-camera reduction record: U (21, packed upper 6x6), b_c (6), pad.
+constexpr int kUcam = 28;
+// Per-point record: V (6 packed lower), b_p (3), pad | L (6), z (3), pad.
+constexpr int kPtV = 10;
+constexpr int kPtL = 10;
+// Cholesky tile size.
+constexpr int kNB = 64;
+
+// Index of scalar results (device array `scal`, doubles).
+enum Scalar {
+  kCost = 0,        // cost at current x (Jacobian pass)
+  kGradMaxCam,      // max |g| over camera params
+  kGradMaxPt,       // max |g| over point params
+  kXNorm2Cam,       // sum x^2 over cameras
+  kXNorm2Pt,        // sum x^2 over points
+  kModelChange,     // model cost change
+  kNewCost,         // cost at the candidate
+  kStep2Pt,         // sum dx^2 over points
+  kStep2Cam,        // sum dx^2 over cameras
+  kBadStep,         // > 0 if the step or candidate is non-finite / V not PD
+  kCholFail,        // reserved (the Cholesky flag is an int, fetched separately)
+  kBadCam,          // > 0 if the camera step is non-finite
+  kBadBack,         // > 0 if the point step is non-finite
+  kNumScalars
+};
+
+struct DevProblem {
+  int32_t C = 0, P = 0;      // cameras (global), points (this shard)
+  int64_t N = 0;             // observations (this shard)
+  // structure (point-major observation order; within a point by camera)
+  double* uv = nullptr;        // [N][2]
+  int32_t* obs_cam = nullptr;  // [N]
+  int32_t* obs_pt = nullptr;   // [N]
+  int32_t* pt_off = nullptr;   // [P+1]
+  int32_t* cam_obs = nullptr;  // [N] observation ids grouped by camera
+  int32_t* cam_off = nullptr;  // [C+1]
+  double* Kc = nullptr;        // [C][5] fx skew cx fy cy
+  // parameters (current and candidate)
+  double* cam = nullptr;      // [C][6] rot(3) t(3)
+  double* cam_new = nullptr;  // [C][6]
+  double* X = nullptr;        // [P][3]
+  double* X_new = nullptr;    // [P][3]
+  double* cam0 = nullptr;     // [C][6] initial (reset)
+  double* X0 = nullptr;       // [P][3]
+  // Jacobi scaling and LM diagonal
+  double* scale_c = nullptr;  // [C][6]
+  double* scale_p = nullptr;  // [P][3]
+  double* diag_c = nullptr;   // [C][6]
+  double* diag_p = nullptr;   // [P][3]
+  // per-iteration work arrays
+  double* camR = nullptr;     // [C][36]
+  double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
+  double* jrec = nullptr;     // [N][20]
+  double* mrec = nullptr;     // [N][8]
+  double* ptV = nullptr;      // [P][10]
+  double* ptL = nullptr;      // [P][10]
+  double* Ucam = nullptr;     // [C][28]
+  // reduced camera system: column-major lower (== row-major upper), ld x ld,
+  // n = 6C unknowns, row n holds the reduced right-hand side (augmented).
+  int32_t n = 0, ld = 0, nblk = 0;
+  double* S = nullptr;
+  double* invL = nullptr;     // [nblk][64][64] inverses of the diagonal tiles
+  double* zwork = nullptr;    // [ld]
+  double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
+  int32_t* fail = nullptr;    // [1] Cholesky failure flag
+  // Schur tasks: (row camera, first column camera, end column camera)
+  int32_t n_tasks = 0;
+  int32_t* tasks = nullptr;   // [n_tasks][3]
+  int32_t tile_cams = 0;      // max column cameras per task (LDS budget)
+  // reductions
+  double* partials = nullptr; // scratch [kNumPartialSlots][max_blocks]
+  int32_t max_blocks = 0;
+  double* scal = nullptr;     // [kNumScalars]
+  double* scal_host = nullptr;  // pinned host mirror
+};
+
+// Partial-sum slots (each max_blocks doubles).
+enum PartialSlot {
+  kPCost = 0, kPXNormCam, kPXNormPt, kPGradCam, kPGradPt, kPModel, kPNewCost, kPStepPt, kPStepCam, kPBad,
+  kPBadCam, kPBadBack,
+  kNumPartialSlots
+};
+
+// ---- launchers (ba_kernels.hip) ----
+void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s);
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s);
+void launch_cam_reduce(const DevProblem& d, hipStream_t s);
+// mode 0: unscaled pass -> compute scale_c from colnorms; mode 1: diag (if !reuse) + gradient
+void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s);
+// mode 0: unscaled pass -> scale_p; mode 1: V, b, diag (if !reuse), gradient, x-norm
+void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s);
+void launch_point_prep(const DevProblem& d, double radius, hipStream_t s);
+void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
+void launch_pad_init(const DevProblem& d, hipStream_t s);
+void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
+void launch_point_backsub(const DevProblem& d, hipStream_t s);
+// sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
+void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
+int blocks_for(int64_t n, int threads);
+
+// ---- dense Cholesky (chol_kernels.hip) ----
+void launch_cholesky(const DevProblem& d, hipStream_t s);
+void launch_backsolve(const DevProblem& d, hipStream_t s);
+
+}  // namespace sfm

@@ -1,0 +1,651 @@
+// Bundle-adjustment LM-iteration kernels for gfx950 (MI355X), fp64.
+//
+// Restates on the GPU the per-iteration work Ceres performs inside
+// ceres::Solve for CTracker::bundleAdjustmentStructAndPose
+// (/root/reference/CTracker.cpp:670-702):
+//   * residual + 2x9 Jacobian of BAStructAndPoseFunctor (CTracker.cpp:585-604)
+//     with ceres::AngleAxisRotatePoint (CTracker.cpp:588), Jacobi-scaled;
+//   * the DENSE_SCHUR normal-equation assembly: per-point 3x3 blocks V_p,
+//     per-camera 6x6 blocks U_c, reduced camera matrix S = U + D^2 - W V^-1 W^T
+//     and its right-hand side;
+//   * point back-substitution, the LM model-cost change and the candidate
+//     residual evaluation.
+// Every reduction is a fixed-order tree (per-block partials, then one
+// ordered pass), so cost / gradient / step norms are bitwise reproducible.
+// The only order-dependent sum is the LDS accumulation of S (ds_add_f64).
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cmath>
+#include "ba_device.h"
+
+namespace sfm {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+
+// Fixed-order block reduction; result valid in thread 0.  `sh` >= 4 doubles.
+__device__ __forceinline__ double block_reduce(double v, double* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    r = sh[0];
+    for (int i = 1; i < nw; ++i) r = is_max ? fmax(r, sh[i]) : r + sh[i];
+  }
+  return r;
+}
+
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ __forceinline__ void st2(double* p, double a, double b) {
+  *reinterpret_cast<double2*>(p) = make_double2(a, b);
+}
+
+// Rotation matrix R(w) with the branch of ceres::AngleAxisRotatePoint:
+// theta^2 > DBL_EPSILON -> Rodrigues; otherwise the first-order map I + [w]x.
+// Optionally dR/dw_k (k-major, 3 x row-major 3x3), differentiated through
+// the same expressions the Jet evaluation of the reference functor uses.
+__device__ void rotation(const double w[3], double R[9], double* dR) {
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (th2 > DBL_EPSILON) {
+    const double th = sqrt(th2);
+    double s, c;
+    sincos(th, &s, &c);
+    const double ith = 1.0 / th;
+    const double u[3] = {w[0] * ith, w[1] * ith, w[2] * ith};
+    const double omc = 1.0 - c;
+    R[0] = c + omc * u[0] * u[0];        R[1] = -s * u[2] + omc * u[0] * u[1]; R[2] = s * u[1] + omc * u[0] * u[2];
+    R[3] = s * u[2] + omc * u[1] * u[0]; R[4] = c + omc * u[1] * u[1];        R[5] = -s * u[0] + omc * u[1] * u[2];
+    R[6] = -s * u[1] + omc * u[2] * u[0]; R[7] = s * u[0] + omc * u[2] * u[1]; R[8] = c + omc * u[2] * u[2];
+    if (dR) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double dc = -s * u[k], ds = c * u[k], domc = s * u[k];
+        double du[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) du[i] = ((i == k ? 1.0 : 0.0) - u[i] * u[k]) * ith;
+        double* D = dR + 9 * k;
+        // d/dw_k of: c I + s [u]x + omc u u^T
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            D[3 * i + j] = (i == j ? dc : 0.0) + domc * u[i] * u[j] + omc * (du[i] * u[j] + u[i] * du[j]);
+        // skew parts: [a]x = [[0,-a2,a1],[a2,0,-a0],[-a1,a0,0]] with a = ds*u + s*du
+        const double a0 = ds * u[0] + s * du[0], a1 = ds * u[1] + s * du[1], a2 = ds * u[2] + s * du[2];
+        D[1] -= a2; D[2] += a1; D[3] += a2; D[5] -= a0; D[6] -= a1; D[7] += a0;
+      }
+    }
+  } else {
+    R[0] = 1.0;   R[1] = -w[2]; R[2] = w[1];
+    R[3] = w[2];  R[4] = 1.0;   R[5] = -w[0];
+    R[6] = -w[1]; R[7] = w[0];  R[8] = 1.0;
+    if (dR) {
+      for (int i = 0; i < 27; ++i) dR[i] = 0.0;
+      // d([w]x)/dw_k = [e_k]x
+      dR[0 * 9 + 5] = -1.0; dR[0 * 9 + 7] = 1.0;
+      dR[1 * 9 + 2] = 1.0;  dR[1 * 9 + 6] = -1.0;
+      dR[2 * 9 + 1] = -1.0; dR[2 * 9 + 3] = 1.0;
+    }
+  }
+}
+
+// Packed upper-triangle index of a 6x6 symmetric matrix.
+__device__ __forceinline__ int up6(int a, int b) {
+  if (a > b) { int t = a; a = b; b = t; }
+  return a * 6 - (a * (a - 1)) / 2 + (b - a);
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __restrict__ cam,
+                                                       double* __restrict__ camR, double* __restrict__ part_xn) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  double xn = 0.0;
+  if (c < C) {
+    const double w[3] = {cam[6 * c], cam[6 * c + 1], cam[6 * c + 2]};
+    double R[9], dR[27];
+    rotation(w, R, dR);
+    double* o = camR + size_t(kCamR) * c;
+    for (int i = 0; i < 9; ++i) o[i] = R[i];
+    for (int i = 0; i < 27; ++i) o[9 + i] = dR[i];
+    for (int k = 0; k < 6; ++k) xn += cam[6 * c + k] * cam[6 * c + k];
+  }
+  const double r = block_reduce(xn, sh, false);
+  if (threadIdx.x == 0 && part_xn) part_xn[blockIdx.x] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Residual + Jacobian, one lane per observation.  Per observation the pass
+// moves 184 B of algorithmic HBM traffic (uv 16, cam/pt index 8, record 160)
+// plus the per-camera (88 B) and per-point (24 B) parameter reads.  Records
+// are staged in LDS so the stores leave as fully coalesced 16-B lanes.
+constexpr int kStage = kJRec + 1;  // odd stride: conflict-light LDS staging
+__global__ __launch_bounds__(kThreads) void k_jacobian(int64_t N, const double* __restrict__ uv,
+                                                       const int32_t* __restrict__ obs_cam,
+                                                       const int32_t* __restrict__ obs_pt,
+                                                       const double* __restrict__ Kc, const double* __restrict__ cam,
+                                                       const double* __restrict__ camR, const double* __restrict__ X,
+                                                       const double* __restrict__ scale_c,
+                                                       const double* __restrict__ scale_p, int scaled,
+                                                       double* __restrict__ jrec, double* __restrict__ part_cost) {
+  __shared__ double stage[kThreads * kStage];
+  __shared__ double sh[4];
+  const int64_t base = int64_t(blockIdx.x) * kThreads;
+  const int64_t o = base + threadIdx.x;
+  double cost = 0.0;
+  if (o < N) {
+    const int c = obs_cam[o], p = obs_pt[o];
+    const double* cr = camR + size_t(kCamR) * c;
+    const double2 uvo = ld2(uv + 2 * o);
+    const double Xp[3] = {X[3 * size_t(p)], X[3 * size_t(p) + 1], X[3 * size_t(p) + 2]};
+    const double* k = Kc + 5 * size_t(c);
+    const double fx = k[0], sk = k[1], cx = k[2], fy = k[3], cy = k[4];
+    double pc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      pc[i] = cr[3 * i] * Xp[0] + cr[3 * i + 1] * Xp[1] + cr[3 * i + 2] * Xp[2] + cam[6 * c + 3 + i];
+    const double xp = pc[0] / pc[2], yp = pc[1] / pc[2];
+    const double r0 = fx * xp + sk * yp + cx - uvo.x;
+    const double r1 = fy * yp + cy - uvo.y;
+    const double iz = 1.0 / pc[2];
+    // d r / d pc
+    const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+    const double b1 = fy * iz, b2 = -fy * yp * iz;
+    double* st = stage + threadIdx.x * kStage;
+    // J_X = dr/dpc * R
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double sj = scaled ? scale_p[3 * size_t(p) + j] : 1.0;
+      st[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sj;
+      st[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sj;
+    }
+    st[kRes] = r0;
+    st[kRes + 1] = r1;
+    // J_w[:,k] = dr/dpc * (dR_k X);  J_t = dr/dpc
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      const double* D = cr + 9 + 9 * kk;
+      const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+      const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+      const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+      const double sk_ = scaled ? scale_c[6 * size_t(c) + kk] : 1.0;
+      st[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sk_;
+      st[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sk_;
+    }
+    const double st0 = scaled ? scale_c[6 * size_t(c) + 3] : 1.0;
+    const double st1 = scaled ? scale_c[6 * size_t(c) + 4] : 1.0;
+    const double st2_ = scaled ? scale_c[6 * size_t(c) + 5] : 1.0;
+    st[kJC + 3] = a0 * st0; st[kJC + 4] = a1 * st1; st[kJC + 5] = a2 * st2_;
+    st[kJC + 9] = 0.0;      st[kJC + 10] = b1 * st1; st[kJC + 11] = b2 * st2_;
+    cost = 0.5 * (r0 * r0 + r1 * r1);
+  }
+  __syncthreads();
+  const int64_t nrec = (N - base) < kThreads ? (N - base) : kThreads;
+  double* dst = jrec + base * kJRec;
+  const int npairs = int(nrec) * (kJRec / 2);
+  for (int e = threadIdx.x; e < npairs; e += kThreads) {
+    const int t = e / (kJRec / 2), f = 2 * (e - t * (kJRec / 2));
+    st2(dst + 2 * e, stage[t * kStage + f], stage[t * kStage + f + 1]);
+  }
+  const double r = block_reduce(cost, sh, false);
+  if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Per-camera normal-equation block U_c = sum J_c^T J_c and b_c = sum J_c^T r,
+// one workgroup per camera, fixed-order reduction.
+__global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_off,
+                                                         const int32_t* __restrict__ cam_obs,
+                                                         const double* __restrict__ jrec, double* __restrict__ Ucam) {
+  __shared__ double sh[4 * 27];
+  const int c = blockIdx.x;
+  double acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+  const int i0 = cam_off[c], i1 = cam_off[c + 1];
+  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
+    const double* J = jrec + size_t(cam_obs[i]) * kJRec;
+    const double2 rr = ld2(J + kRes);
+    double j0[6], j1[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 a = ld2(J + kJC + 2 * k), b = ld2(J + kJC + 6 + 2 * k);
+      j0[2 * k] = a.x; j0[2 * k + 1] = a.y; j1[2 * k] = b.x; j1[2 * k + 1] = b.y;
+    }
+    int q = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = a; b < 6; ++b) acc[q++] += j0[a] * j0[b] + j1[a] * j1[b];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += j0[a] * rr.x + j1[a] * rr.y;
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    const double v = wave_sum(acc[i]);
+    if (l == 0) sh[w * 27 + i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    const double v = sh[threadIdx.x] + sh[27 + threadIdx.x] + sh[54 + threadIdx.x] + sh[81 + threadIdx.x];
+    Ucam[size_t(kUcam) * c + threadIdx.x] = v;
+  }
+}
+
+// mode 0: Jacobi scale from the unscaled column norms (diagonal of U).
+// mode 1: LM diagonal (unless reused) and camera gradient max-norm.
+__global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* __restrict__ Ucam,
+                                                           double* __restrict__ scale_c, double* __restrict__ diag_c,
+                                                           double min_diag, double max_diag, int mode, int reuse,
+                                                           double* __restrict__ part_grad) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  double g = 0.0;
+  if (c < C) {
+    const double* U = Ucam + size_t(kUcam) * c;
+    for (int a = 0; a < 6; ++a) {
+      const double cn = U[up6(a, a)];
+      if (mode == 0) {
+        scale_c[6 * c + a] = 1.0 / (1.0 + sqrt(cn));
+      } else {
+        if (!reuse) diag_c[6 * c + a] = fmin(fmax(cn, min_diag), max_diag);
+        g = fmax(g, fabs(U[21 + a] / scale_c[6 * c + a]));
+      }
+    }
+  }
+  const double r = block_reduce(g, sh, true);
+  if (threadIdx.x == 0 && part_grad) part_grad[blockIdx.x] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Point pass after a Jacobian evaluation (one lane per point):
+// mode 0: Jacobi scale of the point columns; mode 1: V_p, b_p, LM diagonal,
+// gradient max-norm and |X|^2.
+__global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* __restrict__ pt_off,
+                                                         const double* __restrict__ jrec, const double* __restrict__ X,
+                                                         double* __restrict__ scale_p, double* __restrict__ diag_p,
+                                                         double* __restrict__ ptV, double min_diag, double max_diag,
+                                                         int mode, int reuse, double* __restrict__ part_grad,
+                                                         double* __restrict__ part_xn) {
+  __shared__ double sh[4];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double g = 0.0, xn = 0.0;
+  if (p < P) {
+    double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    const int q0 = pt_off[p], q1 = pt_off[p + 1];
+    for (int q = q0; q < q1; ++q) {
+      const double* J = jrec + size_t(q) * kJRec;
+      const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4), rr = ld2(J + kRes);
+      const double u0 = e0.x, u1 = e0.y, u2 = e1.x, v0 = e1.y, v1 = e2.x, v2 = e2.y;
+      V[0] += u0 * u0 + v0 * v0;
+      V[1] += u1 * u0 + v1 * v0; V[2] += u1 * u1 + v1 * v1;
+      V[3] += u2 * u0 + v2 * v0; V[4] += u2 * u1 + v2 * v1; V[5] += u2 * u2 + v2 * v2;
+      b[0] += u0 * rr.x + v0 * rr.y; b[1] += u1 * rr.x + v1 * rr.y; b[2] += u2 * rr.x + v2 * rr.y;
+    }
+    const double cn[3] = {V[0], V[2], V[5]};
+    if (mode == 0) {
+      for (int k = 0; k < 3; ++k) scale_p[3 * size_t(p) + k] = 1.0 / (1.0 + sqrt(cn[k]));
+    } else {
+      for (int k = 0; k < 3; ++k) {
+        if (!reuse) diag_p[3 * size_t(p) + k] = fmin(fmax(cn[k], min_diag), max_diag);
+        g = fmax(g, fabs(b[k] / scale_p[3 * size_t(p) + k]));
+        xn += X[3 * size_t(p) + k] * X[3 * size_t(p) + k];
+      }
+      double* o = ptV + size_t(kPtV) * p;
+      st2(o, V[0], V[1]); st2(o + 2, V[2], V[3]); st2(o + 4, V[4], V[5]); st2(o + 6, b[0], b[1]); st2(o + 8, b[2], 0.0);
+    }
+  }
+  if (mode == 1) {
+    const double rg = block_reduce(g, sh, true);
+    if (threadIdx.x == 0) part_grad[blockIdx.x] = rg;
+    const double rx = block_reduce(xn, sh, false);
+    if (threadIdx.x == 0) part_xn[blockIdx.x] = rx;
+  }
+}
+
+// Per-iteration point factorisation (depends on the trust-region radius):
+// V_p + D_p^2 = L L^T, z = L^-1 b_p, and per observation M = J_X L^-T,
+// h = M z (the ingredients of W V^-1 W^T and W V^-1 b).
+__global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* __restrict__ pt_off,
+                                                         const double* __restrict__ jrec, const double* __restrict__ ptV,
+                                                         const double* __restrict__ diag_p, double radius,
+                                                         double* __restrict__ mrec, double* __restrict__ ptL,
+                                                         double* __restrict__ part_bad) {
+  __shared__ double sh[4];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double bad = 0.0;
+  if (p < P) {
+    const double* v = ptV + size_t(kPtV) * p;
+    double D[3];
+    for (int k = 0; k < 3; ++k) { const double d = sqrt(diag_p[3 * size_t(p) + k] / radius); D[k] = d * d; }
+    const double V00 = v[0] + D[0], V10 = v[1], V11 = v[2] + D[1], V20 = v[3], V21 = v[4], V22 = v[5] + D[2];
+    const double l00 = sqrt(V00);
+    const double l10 = V10 / l00, l20 = V20 / l00;
+    const double l11 = sqrt(V11 - l10 * l10);
+    const double l21 = (V21 - l20 * l10) / l11;
+    const double l22 = sqrt(V22 - l20 * l20 - l21 * l21);
+    if (!(l00 > 0.0) || !(l11 > 0.0) || !(l22 > 0.0)) bad = 1.0;
+    const double z0 = v[6] / l00, z1 = (v[7] - l10 * z0) / l11, z2 = (v[8] - l20 * z0 - l21 * z1) / l22;
+    double* L = ptL + size_t(kPtL) * p;
+    st2(L, l00, l10); st2(L + 2, l11, l20); st2(L + 4, l21, l22); st2(L + 6, z0, z1); st2(L + 8, z2, 0.0);
+    const int q0 = pt_off[p], q1 = pt_off[p + 1];
+    for (int q = q0; q < q1; ++q) {
+      const double* J = jrec + size_t(q) * kJRec;
+      const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
+      const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
+      const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
+      double* M = mrec + size_t(q) * kMRec;
+      st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
+      st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
+    }
+  }
+  const double r = block_reduce(bad, sh, true);
+  if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Reduced camera matrix, one workgroup per task (row camera c1, column
+// cameras [a, b) with a >= c1).  The row's block strip lives in LDS; each
+// lane walks the row camera's observations and, for each, the observations
+// of the same point whose camera falls in [max(a,c1), b) (a contiguous run,
+// since a point's observations are sorted by camera), adding
+//   A_o1 A_o2^T = J_c1^T (M_o1 M_o2^T) J_c2
+// into block (c1, c2).  Written out as S[c1][c2] = [c1==c2](U + D^2) - acc
+// into the row-major upper triangle (== column-major lower) of S; the first
+// task of each row also writes the reduced right-hand side
+//   rhs_c1 = sum_{o in c1} J_c^T (r_o - h_o)
+// into the augmented column n.
+__global__ __launch_bounds__(kThreads) void k_schur(
+    const int32_t* __restrict__ tasks, const int32_t* __restrict__ cam_off, const int32_t* __restrict__ cam_obs,
+    const int32_t* __restrict__ obs_pt, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pt_off,
+    const double* __restrict__ jrec, const double* __restrict__ mrec, const double* __restrict__ Ucam,
+    const double* __restrict__ diag_c, double radius, int add_diag, double* __restrict__ S, int ld, int n) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int c1 = tasks[3 * blockIdx.x], a = tasks[3 * blockIdx.x + 1], b = tasks[3 * blockIdx.x + 2];
+  const int ncol = b - a;
+  double* acc = smem;
+  double* red = smem + ncol * 36;  // 4 waves x 6
+  for (int i = threadIdx.x; i < ncol * 36; i += kThreads) acc[i] = 0.0;
+  __syncthreads();
+  const int lo = a > c1 ? a : c1;
+  const bool own = (a <= c1) && (c1 < b);
+  double rhs[6] = {0, 0, 0, 0, 0, 0};
+  const int i0 = cam_off[c1], i1 = cam_off[c1 + 1];
+  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
+    const int o1 = cam_obs[i];
+    const int p = obs_pt[o1];
+    const double* J1p = jrec + size_t(o1) * kJRec;
+    const double* M1p = mrec + size_t(o1) * kMRec;
+    double J1[12], M1[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { const double2 t = ld2(J1p + kJC + 2 * k); J1[2 * k] = t.x; J1[2 * k + 1] = t.y; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { const double2 t = ld2(M1p + 2 * k); M1[2 * k] = t.x; M1[2 * k + 1] = t.y; }
+    if (own) {
+      const double2 rr = ld2(J1p + kRes), hh = ld2(M1p + 6);
+      const double e0 = rr.x - hh.x, e1 = rr.y - hh.y;
+#pragma unroll
+      for (int u = 0; u < 6; ++u) rhs[u] += J1[u] * e0 + J1[6 + u] * e1;
+    }
+    const int q0 = pt_off[p], q1 = pt_off[p + 1];
+    for (int o2 = q0; o2 < q1; ++o2) {
+      const int c2 = obs_cam[o2];
+      if (c2 < lo) continue;
+      if (c2 >= b) break;
+      const double* J2p = jrec + size_t(o2) * kJRec + kJC;
+      const double* M2p = mrec + size_t(o2) * kMRec;
+      double J2[12], M2[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { const double2 t = ld2(J2p + 2 * k); J2[2 * k] = t.x; J2[2 * k + 1] = t.y; }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { const double2 t = ld2(M2p + 2 * k); M2[2 * k] = t.x; M2[2 * k + 1] = t.y; }
+      const double G00 = M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2];
+      const double G01 = M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5];
+      const double G10 = M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2];
+      const double G11 = M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5];
+      double* blk = acc + (c2 - a) * 36;
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+        const double H0 = J1[u] * G00 + J1[6 + u] * G10;
+        const double H1 = J1[u] * G01 + J1[6 + u] * G11;
+#pragma unroll
+        for (int v = 0; v < 6; ++v) atomicAdd(blk + 6 * u + v, H0 * J2[v] + H1 * J2[6 + v]);
+      }
+    }
+  }
+  __syncthreads();
+  const int W = 6 * ncol;
+  const double* U = Ucam + size_t(kUcam) * c1;
+  for (int e = threadIdx.x; e < 6 * W; e += kThreads) {
+    const int u = e / W, col = e - u * W;
+    const int cb = col / 6, v = col - 6 * cb;
+    double val = -acc[cb * 36 + 6 * u + v];
+    if (add_diag && a + cb == c1) {
+      val += U[up6(u, v)];
+      if (u == v) { const double d = sqrt(diag_c[6 * size_t(c1) + u] / radius); val += d * d; }
+    }
+    S[size_t(6 * c1 + u) * ld + 6 * size_t(a) + col] = val;
+  }
+  if (own) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const double v = wave_sum(rhs[u]);
+      if (l == 0) red[w * 6 + u] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6)
+      S[size_t(6 * c1 + threadIdx.x) * ld + n] =
+          red[threadIdx.x] + red[6 + threadIdx.x] + red[12 + threadIdx.x] + red[18 + threadIdx.x];
+  }
+}
+
+// Identity padding beyond the augmented row n (column-major lower view).
+__global__ void k_pad_init(double* __restrict__ S, int ld, int n) {
+  const int j = blockIdx.x;
+  for (int i = (j > n ? j : n + 1) + threadIdx.x; i < ld; i += blockDim.x) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
+  if (j == n && threadIdx.x == 0) S[size_t(n) * ld + n] = 1.0;
+}
+
+// ---------------------------------------------------------------------------
+// Camera candidate: delta = -y (scaled space), dx = s * delta.
+__global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __restrict__ cam,
+                                                         const double* __restrict__ ysol,
+                                                         const double* __restrict__ scale_c,
+                                                         double* __restrict__ cam_new, double* __restrict__ camRn,
+                                                         double* __restrict__ part_step, double* __restrict__ part_bad) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  double st = 0.0, bad = 0.0;
+  if (c < C) {
+    double xn[6];
+    for (int k = 0; k < 6; ++k) {
+      const double y = ysol[6 * c + k];
+      if (!isfinite(y)) bad = 1.0;
+      const double dx = scale_c[6 * c + k] * (-y);
+      xn[k] = cam[6 * c + k] + dx;
+      const double d = cam[6 * c + k] - xn[k];
+      st += d * d;
+      cam_new[6 * c + k] = xn[k];
+    }
+    double R[9];
+    rotation(xn, R, nullptr);
+    double* o = camRn + 12 * size_t(c);
+    for (int i = 0; i < 9; ++i) o[i] = R[i];
+    o[9] = xn[3]; o[10] = xn[4]; o[11] = xn[5];
+  }
+  const double rs = block_reduce(st, sh, false);
+  if (threadIdx.x == 0 && part_step) part_step[blockIdx.x] = rs;
+  const double rb = block_reduce(bad, sh, true);
+  if (threadIdx.x == 0) part_bad[blockIdx.x] = rb;
+}
+
+// Point back-substitution + model cost change + candidate cost, one lane per
+// point:  y_p = L^-T (z - sum_o M_o^T (J_c,o y_c)),  delta_p = -y_p,
+//   model residual q_o = J_s delta = -(J_c y_c + J_X y_p),
+//   model cost change -= q . (r + q/2)   (ceres trust_region_minimizer),
+//   candidate residual at (cam_new, X + s*delta_p).
+__global__ __launch_bounds__(kThreads) void k_point_backsub(
+    int P, const int32_t* __restrict__ pt_off, const int32_t* __restrict__ obs_cam, const double* __restrict__ uv,
+    const double* __restrict__ Kc, const double* __restrict__ jrec, const double* __restrict__ mrec,
+    const double* __restrict__ ptL, const double* __restrict__ ysol, const double* __restrict__ scale_p,
+    const double* __restrict__ X, double* __restrict__ X_new, const double* __restrict__ camRn,
+    double* __restrict__ part_model, double* __restrict__ part_cost, double* __restrict__ part_step,
+    double* __restrict__ part_bad) {
+  __shared__ double sh[4];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double model = 0.0, ncost = 0.0, st = 0.0, bad = 0.0;
+  if (p < P) {
+    const double* L = ptL + size_t(kPtL) * p;
+    const double l00 = L[0], l10 = L[1], l11 = L[2], l20 = L[3], l21 = L[4], l22 = L[5];
+    double w0 = L[6], w1 = L[7], w2 = L[8];
+    const int q0 = pt_off[p], q1 = pt_off[p + 1];
+    for (int q = q0; q < q1; ++q) {
+      const int c = obs_cam[q];
+      const double* J = jrec + size_t(q) * kJRec + kJC;
+      const double* M = mrec + size_t(q) * kMRec;
+      const double* y = ysol + 6 * size_t(c);
+      double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
+      w0 -= M[0] * e0 + M[3] * e1;
+      w1 -= M[1] * e0 + M[4] * e1;
+      w2 -= M[2] * e0 + M[5] * e1;
+    }
+    const double y2 = w2 / l22;
+    const double y1 = (w1 - l21 * y2) / l11;
+    const double y0 = (w0 - l10 * y1 - l20 * y2) / l00;
+    if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) bad = 1.0;
+    const double yp[3] = {y0, y1, y2};
+    double Xn[3];
+    for (int k = 0; k < 3; ++k) {
+      const double x = X[3 * size_t(p) + k];
+      Xn[k] = x + scale_p[3 * size_t(p) + k] * (-yp[k]);
+      const double d = x - Xn[k];
+      st += d * d;
+      X_new[3 * size_t(p) + k] = Xn[k];
+    }
+    for (int q = q0; q < q1; ++q) {
+      const int c = obs_cam[q];
+      const double* Jr = jrec + size_t(q) * kJRec;
+      const double* y = ysol + 6 * size_t(c);
+      double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { e0 += Jr[kJC + k] * y[k]; e1 += Jr[kJC + 6 + k] * y[k]; }
+      const double m0 = -(e0 + Jr[0] * y0 + Jr[1] * y1 + Jr[2] * y2);
+      const double m1 = -(e1 + Jr[3] * y0 + Jr[4] * y1 + Jr[5] * y2);
+      const double r0 = Jr[kRes], r1 = Jr[kRes + 1];
+      model -= m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
+      // candidate residual
+      const double* Rn = camRn + 12 * size_t(c);
+      double pc[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pc[i] = Rn[3 * i] * Xn[0] + Rn[3 * i + 1] * Xn[1] + Rn[3 * i + 2] * Xn[2] + Rn[9 + i];
+      const double xp = pc[0] / pc[2], ypj = pc[1] / pc[2];
+      const double* k = Kc + 5 * size_t(c);
+      const double2 uvo = ld2(uv + 2 * size_t(q));
+      const double rn0 = k[0] * xp + k[1] * ypj + k[2] - uvo.x;
+      const double rn1 = k[3] * ypj + k[4] - uvo.y;
+      ncost += 0.5 * (rn0 * rn0 + rn1 * rn1);
+    }
+  }
+  double r = block_reduce(model, sh, false);
+  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
+  r = block_reduce(ncost, sh, false);
+  if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
+  r = block_reduce(st, sh, false);
+  if (threadIdx.x == 0) part_step[blockIdx.x] = r;
+  r = block_reduce(bad, sh, true);
+  if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
+}
+
+// Fixed-order final reduction of one partial slot.
+__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ src, int nb, int op,
+                                                 double* __restrict__ dst) {
+  __shared__ double sh[16];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 1024) v = op ? fmax(v, src[i]) : v + src[i];
+  v = op ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = sh[0];
+    for (int i = 1; i < 16; ++i) r = op ? fmax(r, sh[i]) : r + sh[i];
+    *dst = r;
+  }
+}
+
+}  // namespace
+
+int blocks_for(int64_t n, int threads) { return int((n + threads - 1) / threads); }
+
+static inline double* slot(const DevProblem& d, int s) { return d.partials + size_t(s) * d.max_blocks; }
+
+void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s) {
+  k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
+}
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
+  if (d.N == 0) return;
+  k_jacobian<<<blocks_for(d.N, kThreads), kThreads, 0, s>>>(d.N, d.uv, d.obs_cam, d.obs_pt, d.Kc, d.cam, d.camR, d.X,
+                                                           d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
+                                                           slot(d, kPCost));
+}
+void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
+  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_off, d.cam_obs, d.jrec, d.Ucam);
+}
+void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
+  k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, 1e-6, 1e32, mode,
+                                                               reuse_diag ? 1 : 0,
+                                                               count_grad ? slot(d, kPGradCam) : nullptr);
+}
+void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
+  if (d.P == 0) return;
+  k_point_eval<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.jrec, d.X, d.scale_p, d.diag_p, d.ptV,
+                                                             1e-6, 1e32, mode, reuse_diag ? 1 : 0,
+                                                             slot(d, kPGradPt), slot(d, kPXNormPt));
+}
+void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
+  if (d.P == 0) return;
+  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.jrec, d.ptV, d.diag_p, radius, d.mrec,
+                                                             d.ptL, slot(d, kPBad));
+}
+void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
+  const size_t lds = (size_t(d.tile_cams) * 36 + 32) * sizeof(double);
+  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_off, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.jrec,
+                                           d.mrec, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld, d.n);
+}
+void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }
+void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
+  k_cam_update<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.cam, d.ysol, d.scale_c, d.cam_new, d.camRn,
+                                                             count_norm ? slot(d, kPStepCam) : nullptr,
+                                                             slot(d, kPBadCam));
+}
+void launch_point_backsub(const DevProblem& d, hipStream_t s) {
+  if (d.P == 0) return;
+  k_point_backsub<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(
+      d.P, d.pt_off, d.obs_cam, d.uv, d.Kc, d.jrec, d.mrec, d.ptL, d.ysol, d.scale_p, d.X, d.X_new, d.camRn,
+      slot(d, kPModel), slot(d, kPNewCost), slot(d, kPStepPt), slot(d, kPBadBack));
+}
+void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
+  k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);
+}
+
+}  // namespace sfm

@@ -1,0 +1,730 @@
+// Host side of the device bundle adjuster: problem layout, the Levenberg-
+// Marquardt trust-region loop and the C ABI of include/sfm_amd.h.
+//
+// The loop restates Ceres' TrustRegionMinimizer + LevenbergMarquardtStrategy
+// (the solver behind ceres::Solve at /root/reference/CTracker.cpp:700-701,
+// options CTracker.cpp:571-577) step for step; the
+// per-iteration arithmetic runs in the kernels of ba_kernels.hip /
+// chol_kernels.hip and only ~10 scalars cross PCIe per iteration.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+#include <chrono>
+
+#include "ba_device.h"
+#include "../../include/sfm_amd.h"
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace
+
+void sfm_internal_set_error(const std::string& msg) { g_err = msg; }
+
+#define HIPCHK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(SFM_EIO, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCCLCHK(expr)                                                                             \
+  do {                                                                                            \
+    ncclResult_t r_ = (expr);                                                                     \
+    if (r_ != ncclSuccess) return fail(SFM_EIO, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+using namespace sfm;
+
+enum Phase { kPhJac = 0, kPhCamRed, kPhPtEval, kPhPtPrep, kPhSchur, kPhChol, kPhBack, kPhBacksub, kPhOther, kNumPh };
+
+struct sfm_ba_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevProblem d;
+  // host copies needed for reordering / reset
+  std::vector<int64_t> order;  // sorted position -> caller observation index
+  std::vector<void*> allocs;
+  bool has_problem = false;
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // profiling
+  bool profiling = false;
+  std::vector<hipEvent_t> ev;
+  int ev_used = 0;
+  std::vector<std::pair<int, int>> ev_marks;  // (phase, event index of start); end = start + 1
+  double phase_ms[kNumPh] = {0};
+  int phase_count[kNumPh] = {0};
+};
+
+namespace {
+
+template <typename T>
+int dalloc(sfm_ba_handle* h, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) return fail(SFM_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  h->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return 0;
+}
+
+void free_problem(sfm_ba_handle* h) {
+  for (void* p : h->allocs) hipFree(p);
+  h->allocs.clear();
+  if (h->d.scal_host) { hipHostFree(h->d.scal_host); h->d.scal_host = nullptr; }
+  h->d = DevProblem();
+  h->has_problem = false;
+}
+
+// ---- phase timing (HIP events on the solver stream; read at the per-iteration sync)
+void mark_begin(sfm_ba_handle* h, int ph) {
+  if (!h->profiling) return;
+  if (h->ev_used + 2 > int(h->ev.size())) {
+    const size_t old = h->ev.size();
+    h->ev.resize(old + 256);
+    for (size_t i = old; i < h->ev.size(); ++i) hipEventCreate(&h->ev[i]);
+  }
+  h->ev_marks.push_back({ph, h->ev_used});
+  hipEventRecord(h->ev[h->ev_used], h->stream);
+  h->ev_used += 2;
+}
+void mark_end(sfm_ba_handle* h) {
+  if (!h->profiling) return;
+  hipEventRecord(h->ev[h->ev_marks.back().second + 1], h->stream);
+}
+void collect_marks(sfm_ba_handle* h) {
+  if (!h->profiling) return;
+  for (auto& m : h->ev_marks) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ev[m.second], h->ev[m.second + 1]) == hipSuccess) {
+      h->phase_ms[m.first] += ms;
+      h->phase_count[m.first] += 1;
+    }
+  }
+  h->ev_marks.clear();
+  h->ev_used = 0;
+}
+
+int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
+  if (h->nranks <= 1) return 0;
+  NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, op, h->comm, h->stream));
+  return 0;
+}
+
+// D2H of the scalar block + stream sync.
+int fetch_scalars(sfm_ba_handle* h) {
+  HIPCHK(hipMemcpyAsync(h->d.scal_host, h->d.scal, sizeof(double) * kNumScalars, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  collect_marks(h);
+  return 0;
+}
+
+// Evaluate cost, Jacobian, Jacobi scale (first call), per-block normal
+// equations, LM diagonal and gradient at the current parameters.
+int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
+  DevProblem& d = h->d;
+  hipStream_t s = h->stream;
+  int rc;
+  launch_cam_prep(d, d.cam, true, s);
+  mark_begin(h, kPhJac);
+  launch_jacobian(d, !first || !jacobi_scaling ? true : false, s);
+  mark_end(h);
+  if (first && jacobi_scaling) {
+    mark_begin(h, kPhCamRed);
+    launch_cam_reduce(d, s);
+    mark_end(h);
+    if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+    launch_cam_finalize(d, 0, false, false, s);
+    launch_point_eval(d, 0, false, s);
+    mark_begin(h, kPhJac);
+    launch_jacobian(d, true, s);
+    mark_end(h);
+  }
+  mark_begin(h, kPhCamRed);
+  launch_cam_reduce(d, s);
+  mark_end(h);
+  if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+  launch_cam_finalize(d, 1, false, true, s);
+  mark_begin(h, kPhPtEval);
+  launch_point_eval(d, 1, false, s);
+  mark_end(h);
+  const int nbN = std::max(1, blocks_for(d.N, 256)), nbP = std::max(1, blocks_for(d.P, 256)),
+            nbC = std::max(1, blocks_for(d.C, 256));
+  if (d.N == 0) hipMemsetAsync(d.partials + size_t(kPCost) * d.max_blocks, 0, sizeof(double), s);
+  if (d.P == 0) {
+    hipMemsetAsync(d.partials + size_t(kPGradPt) * d.max_blocks, 0, sizeof(double), s);
+    hipMemsetAsync(d.partials + size_t(kPXNormPt) * d.max_blocks, 0, sizeof(double), s);
+  }
+  launch_reduce(d, kPCost, nbN, 0, kCost, s);
+  launch_reduce(d, kPGradCam, nbC, 1, kGradMaxCam, s);
+  launch_reduce(d, kPGradPt, nbP, 1, kGradMaxPt, s);
+  launch_reduce(d, kPXNormCam, nbC, 0, kXNorm2Cam, s);
+  launch_reduce(d, kPXNormPt, nbP, 0, kXNorm2Pt, s);
+  if (h->nranks > 1) {
+    if ((rc = allreduce(h, d.scal + kCost, 1, ncclSum))) return rc;
+    if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
+    if ((rc = allreduce(h, d.scal + kXNorm2Pt, 1, ncclSum))) return rc;
+  }
+  return fetch_scalars(h);
+}
+
+// One trust-region step: factor, Schur, dense Cholesky, back substitution,
+// model cost change and candidate cost.
+int compute_step(sfm_ba_handle* h, double radius) {
+  DevProblem& d = h->d;
+  hipStream_t s = h->stream;
+  int rc;
+  mark_begin(h, kPhPtPrep);
+  launch_point_prep(d, radius, s);
+  mark_end(h);
+  mark_begin(h, kPhSchur);
+  launch_schur(d, radius, h->rank == 0, s);
+  mark_end(h);
+  if ((rc = allreduce(h, d.S, size_t(d.ld) * d.ld, ncclSum))) return rc;
+  launch_pad_init(d, s);
+  mark_begin(h, kPhChol);
+  launch_cholesky(d, s);
+  mark_end(h);
+  mark_begin(h, kPhBack);
+  launch_backsolve(d, s);
+  mark_end(h);
+  launch_cam_update(d, h->rank == 0, s);
+  mark_begin(h, kPhBacksub);
+  launch_point_backsub(d, s);
+  mark_end(h);
+  const int nbP = std::max(1, blocks_for(d.P, 256)), nbC = std::max(1, blocks_for(d.C, 256));
+  if (d.P == 0) {
+    const int slots[] = {kPModel, kPNewCost, kPStepPt, kPBadBack, kPBad};
+    for (int sl : slots) hipMemsetAsync(d.partials + size_t(sl) * d.max_blocks, 0, sizeof(double), s);
+  }
+  if (h->rank != 0) hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
+  launch_reduce(d, kPModel, nbP, 0, kModelChange, s);
+  launch_reduce(d, kPNewCost, nbP, 0, kNewCost, s);
+  launch_reduce(d, kPStepPt, nbP, 0, kStep2Pt, s);
+  launch_reduce(d, kPStepCam, nbC, 0, kStep2Cam, s);
+  // bad-step flags: max over point_prep, cam_update and backsub partials
+  launch_reduce(d, kPBad, nbP, 1, kBadStep, s);
+  launch_reduce(d, kPBadCam, nbC, 1, kBadCam, s);
+  launch_reduce(d, kPBadBack, nbP, 1, kBadBack, s);
+  if (h->nranks > 1) {
+    if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
+    if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
+  }
+  // the Cholesky failure flag is an int on the device: fold it into the block
+  HIPCHK(hipMemcpyAsync(d.scal_host + kNumScalars, d.fail, sizeof(int), hipMemcpyDeviceToHost, s));
+  return fetch_scalars(h);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sfm_abi_version(void) { return SFM_ABI_VERSION; }
+const char* sfm_last_error(void) { return g_err.c_str(); }
+
+void sfm_ba_default_options(sfm_ba_options* o) {
+  o->max_num_iterations = 50;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+  o->reserved0 = 0;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->min_relative_decrease = 1e-3;
+}
+
+int32_t sfm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int sfm_ba_create(int32_t device, sfm_ba_handle** out) {
+  if (!out) return fail(SFM_EINVAL, "out is NULL");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(SFM_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(SFM_EINVAL, "device ordinal out of range");
+  HIPCHK(hipSetDevice(device));
+  auto* h = new sfm_ba_handle();
+  h->device = device;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return fail(SFM_EIO, "hipStreamCreate failed");
+  }
+  *out = h;
+  return 0;
+}
+
+int sfm_ba_destroy(sfm_ba_handle* h) {
+  if (!h) return 0;
+  hipSetDevice(h->device);
+  hipStreamSynchronize(h->stream);
+  free_problem(h);
+  for (auto e : h->ev) hipEventDestroy(e);
+  if (h->comm) ncclCommDestroy(h->comm);
+  hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int sfm_comm_unique_id(uint8_t out[128]) {
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out, &id, 128);
+  return 0;
+}
+
+int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+  if (!h || nranks < 1 || rank < 0 || rank >= nranks) return fail(SFM_EINVAL, "bad communicator arguments");
+  HIPCHK(hipSetDevice(h->device));
+  if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
+  h->nranks = nranks;
+  h->rank = rank;
+  if (nranks == 1) return 0;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
+  return 0;
+}
+
+int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, const int32_t* cam_idx,
+                       const int32_t* pt_idx, int32_t n_cams, const double* K9, const double* rot, const double* t,
+                       int32_t n_pts, const double* X) {
+  if (!h) return fail(SFM_EINVAL, "handle is NULL");
+  if (n_obs < 0 || n_cams < 0 || n_pts < 0) return fail(SFM_EINVAL, "negative size");
+  if (n_obs > 0 && (!obs_uv || !cam_idx || !pt_idx)) return fail(SFM_EINVAL, "observation arrays are NULL");
+  if (n_cams > 0 && (!K9 || !rot || !t)) return fail(SFM_EINVAL, "camera arrays are NULL");
+  if (n_pts > 0 && !X) return fail(SFM_EINVAL, "point array is NULL");
+  if (n_obs > int64_t(INT32_MAX)) return fail(SFM_EINVAL, "more than 2^31-1 observations per shard");
+  for (int64_t i = 0; i < n_obs; ++i) {
+    if (cam_idx[i] < 0 || cam_idx[i] >= n_cams) return fail(SFM_EINVAL, "cam_idx out of range at " + std::to_string(i));
+    if (pt_idx[i] < 0 || pt_idx[i] >= n_pts) return fail(SFM_EINVAL, "pt_idx out of range at " + std::to_string(i));
+    if (!std::isfinite(obs_uv[2 * i]) || !std::isfinite(obs_uv[2 * i + 1]))
+      return fail(SFM_EINVAL, "non-finite observation at " + std::to_string(i));
+  }
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  free_problem(h);
+  DevProblem& d = h->d;
+  const int64_t N = n_obs;
+  const int C = n_cams, P = n_pts;
+  d.C = C; d.P = P; d.N = N;
+  // ---- point-major order, cameras ascending within a point (stable) ----
+  std::vector<int32_t> pt_off(size_t(P) + 1, 0);
+  for (int64_t i = 0; i < N; ++i) pt_off[pt_idx[i] + 1]++;
+  for (int p = 0; p < P; ++p) pt_off[p + 1] += pt_off[p];
+  h->order.assign(N, 0);
+  {
+    std::vector<int32_t> fill(pt_off.begin(), pt_off.end() - 1);
+    for (int64_t i = 0; i < N; ++i) h->order[fill[pt_idx[i]]++] = i;
+    for (int p = 0; p < P; ++p) {
+      int64_t* b = h->order.data() + pt_off[p];
+      int64_t* e = h->order.data() + pt_off[p + 1];
+      std::stable_sort(b, e, [&](int64_t x, int64_t y) { return cam_idx[x] < cam_idx[y]; });
+    }
+  }
+  std::vector<double> uv_s(2 * size_t(N));
+  std::vector<int32_t> cam_s(N), pt_s(N);
+  for (int64_t q = 0; q < N; ++q) {
+    const int64_t i = h->order[q];
+    uv_s[2 * q] = obs_uv[2 * i];
+    uv_s[2 * q + 1] = obs_uv[2 * i + 1];
+    cam_s[q] = cam_idx[i];
+    pt_s[q] = pt_idx[i];
+  }
+  std::vector<int32_t> cam_off(size_t(C) + 1, 0), cam_obs(N);
+  for (int64_t q = 0; q < N; ++q) cam_off[cam_s[q] + 1]++;
+  for (int c = 0; c < C; ++c) cam_off[c + 1] += cam_off[c];
+  {
+    std::vector<int32_t> fill(cam_off.begin(), cam_off.end() - 1);
+    for (int64_t q = 0; q < N; ++q) cam_obs[fill[cam_s[q]]++] = int32_t(q);
+  }
+  std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
+  for (int c = 0; c < C; ++c) {
+    const double* k = K9 + 9 * size_t(c);
+    Kc[5 * c] = k[0]; Kc[5 * c + 1] = k[1]; Kc[5 * c + 2] = k[2]; Kc[5 * c + 3] = k[4]; Kc[5 * c + 4] = k[5];
+    for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
+  }
+  // ---- Schur tasks: (row camera, column range) within the LDS budget ----
+  d.tile_cams = std::max(1, std::min(C, 220));  // (220*36+32)*8 B <= 64 KiB dynamic LDS
+  std::vector<std::array<int32_t, 3>> tasks;
+  std::vector<int64_t> work;
+  for (int c1 = 0; c1 < C; ++c1)
+    for (int a = c1; a < C; a += d.tile_cams) {
+      const int b = std::min(C, a + d.tile_cams);
+      tasks.push_back({c1, a, b});
+      work.push_back(int64_t(cam_off[c1 + 1] - cam_off[c1] + 1) * (b - a));
+    }
+  std::vector<int> tord(tasks.size());
+  for (size_t i = 0; i < tord.size(); ++i) tord[i] = int(i);
+  std::stable_sort(tord.begin(), tord.end(), [&](int x, int y) { return work[x] > work[y]; });
+  std::vector<int32_t> task_flat(3 * tasks.size());
+  for (size_t i = 0; i < tord.size(); ++i)
+    for (int k = 0; k < 3; ++k) task_flat[3 * i + k] = tasks[tord[i]][k];
+  d.n_tasks = int32_t(tasks.size());
+  // ---- dense system geometry ----
+  d.n = 6 * C;
+  d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
+  d.nblk = d.ld / kNB;
+  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256)});
+  // ---- device allocation ----
+  int rc = 0;
+#define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) { free_problem(h); return rc; }
+  ALLOC(d.uv, 2 * size_t(N));
+  ALLOC(d.obs_cam, size_t(N));
+  ALLOC(d.obs_pt, size_t(N));
+  ALLOC(d.pt_off, size_t(P) + 1);
+  ALLOC(d.cam_obs, size_t(N));
+  ALLOC(d.cam_off, size_t(C) + 1);
+  ALLOC(d.Kc, 5 * size_t(C));
+  ALLOC(d.cam, 6 * size_t(C));
+  ALLOC(d.cam_new, 6 * size_t(C));
+  ALLOC(d.cam0, 6 * size_t(C));
+  ALLOC(d.X, 3 * size_t(P));
+  ALLOC(d.X_new, 3 * size_t(P));
+  ALLOC(d.X0, 3 * size_t(P));
+  ALLOC(d.scale_c, 6 * size_t(C));
+  ALLOC(d.scale_p, 3 * size_t(P));
+  ALLOC(d.diag_c, 6 * size_t(C));
+  ALLOC(d.diag_p, 3 * size_t(P));
+  ALLOC(d.camR, size_t(kCamR) * C);
+  ALLOC(d.camRn, 12 * size_t(C));
+  ALLOC(d.jrec, size_t(kJRec) * N);
+  ALLOC(d.mrec, size_t(kMRec) * N);
+  ALLOC(d.ptV, size_t(kPtV) * P);
+  ALLOC(d.ptL, size_t(kPtL) * P);
+  ALLOC(d.Ucam, size_t(kUcam) * C);
+  ALLOC(d.S, size_t(d.ld) * d.ld);
+  ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
+  ALLOC(d.zwork, size_t(d.ld));
+  ALLOC(d.ysol, size_t(d.ld));
+  ALLOC(d.fail, size_t(1));
+  ALLOC(d.tasks, 3 * tasks.size());
+  ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
+  ALLOC(d.scal, size_t(kNumScalars));
+#undef ALLOC
+  if (hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
+    free_problem(h);
+    return fail(SFM_ENOMEM, "hipHostMalloc failed");
+  }
+  hipStream_t s = h->stream;
+#define H2D(dst, src, cnt) HIPCHK(hipMemcpyAsync((dst), (src), sizeof(*(dst)) * (cnt), hipMemcpyHostToDevice, s))
+  if (N) {
+    H2D(d.uv, uv_s.data(), 2 * size_t(N));
+    H2D(d.obs_cam, cam_s.data(), size_t(N));
+    H2D(d.obs_pt, pt_s.data(), size_t(N));
+    H2D(d.cam_obs, cam_obs.data(), size_t(N));
+  }
+  H2D(d.pt_off, pt_off.data(), size_t(P) + 1);
+  H2D(d.cam_off, cam_off.data(), size_t(C) + 1);
+  if (C) {
+    H2D(d.Kc, Kc.data(), 5 * size_t(C));
+    H2D(d.cam, cam.data(), 6 * size_t(C));
+    H2D(d.cam0, cam.data(), 6 * size_t(C));
+  }
+  if (P) {
+    H2D(d.X, X, 3 * size_t(P));
+    H2D(d.X0, X, 3 * size_t(P));
+  }
+  if (!tasks.empty()) H2D(d.tasks, task_flat.data(), task_flat.size());
+#undef H2D
+  HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
+  HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
+  HIPCHK(hipStreamSynchronize(s));
+  h->has_problem = true;
+  return 0;
+}
+
+int sfm_ba_reset_parameters(sfm_ba_handle* h) {
+  if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->d.cam, h->d.cam0, sizeof(double) * 6 * size_t(h->d.C), hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.X, h->d.X0, sizeof(double) * 3 * size_t(h->d.P), hipMemcpyDeviceToDevice, h->stream));
+  return 0;
+}
+
+int sfm_ba_get_parameters(sfm_ba_handle* h, double* rot, double* t, double* X) {
+  if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  const DevProblem& d = h->d;
+  std::vector<double> cam(6 * size_t(d.C));
+  if (d.C) HIPCHK(hipMemcpyAsync(cam.data(), d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToHost, h->stream));
+  if (X && d.P) HIPCHK(hipMemcpyAsync(X, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int c = 0; c < d.C; ++c)
+    for (int j = 0; j < 3; ++j) {
+      if (rot) rot[3 * c + j] = cam[6 * c + j];
+      if (t) t[3 * c + j] = cam[6 * c + 3 + j];
+    }
+  return 0;
+}
+
+int sfm_ba_set_profiling(sfm_ba_handle* h, int32_t on) {
+  if (!h) return fail(SFM_EINVAL, "handle is NULL");
+  h->profiling = on != 0;
+  for (int i = 0; i < kNumPh; ++i) { h->phase_ms[i] = 0; h->phase_count[i] = 0; }
+  return 0;
+}
+
+int sfm_ba_phase_times(sfm_ba_handle* h, double* ms) {
+  if (!h || !ms) return fail(SFM_EINVAL, "bad arguments");
+  for (int i = 0; i < kNumPh; ++i) ms[i] = h->phase_ms[i];
+  for (int i = 0; i < kNumPh; ++i) ms[kNumPh + i] = h->phase_count[i];
+  return 0;
+}
+
+int sfm_ba_sync(sfm_ba_handle* h) {
+  if (!h) return fail(SFM_EINVAL, "handle is NULL");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32_t mode, sfm_ba_summary* summary,
+                          sfm_ba_iteration* trace, int32_t trace_cap, int32_t* trace_len) {
+  const auto t_start = std::chrono::steady_clock::now();
+  auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
+  if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
+  sfm_ba_options opts;
+  if (opts_in) opts = *opts_in; else sfm_ba_default_options(&opts);
+  sfm_ba_summary sm;
+  std::memset(&sm, 0, sizeof(sm));
+  int tl = 0;
+  if (trace_len) *trace_len = 0;
+  auto push = [&](const sfm_ba_iteration& it) {
+    if (trace && tl < trace_cap) trace[tl] = it;
+    ++tl;
+    if (trace_len) *trace_len = std::min(tl, trace_cap);
+  };
+  if (mode < 0 || mode > 2 || h->d.N == 0) {
+    // the reference adds no residual blocks for other modes (CTracker.cpp:692-693)
+    sm.termination_type = SFM_CONVERGENCE;
+    if (summary) *summary = sm;
+    return 0;
+  }
+  if (mode != SFM_BA_STRUCT_AND_POSE)
+    return fail(SFM_ENOTSUP, "STRUCT_ONLY / POSE_ONLY are not implemented on the device path yet");
+  HIPCHK(hipSetDevice(h->device));
+  DevProblem& d = h->d;
+  int rc;
+  if (!opts.jacobi_scaling) {
+    std::vector<double> ones(std::max(6 * size_t(d.C), 3 * size_t(d.P)), 1.0);
+    HIPCHK(hipMemcpyAsync(d.scale_c, ones.data(), sizeof(double) * 6 * d.C, hipMemcpyHostToDevice, h->stream));
+    if (d.P) HIPCHK(hipMemcpyAsync(d.scale_p, ones.data(), sizeof(double) * 3 * d.P, hipMemcpyHostToDevice, h->stream));
+  }
+  double* sc = d.scal_host;
+  double tj = now_s();
+  if ((rc = evaluate(h, true, opts.jacobi_scaling != 0))) return rc;
+  sm.jacobian_time_s += now_s() - tj;
+  sm.num_jacobian_evaluations++;
+  sm.num_residual_evaluations++;
+  double cost = sc[kCost];
+  sm.initial_cost = cost;
+  if (!std::isfinite(cost)) {
+    sm.termination_type = SFM_FAILURE;
+    sm.final_cost = cost;
+    if (summary) *summary = sm;
+    return fail(SFM_EIO, "initial residual evaluation is not finite");
+  }
+  double grad_max = std::max(sc[kGradMaxCam], sc[kGradMaxPt]);
+  double x_norm = std::sqrt(sc[kXNorm2Cam] + sc[kXNorm2Pt]);
+  {
+    sfm_ba_iteration it0;
+    std::memset(&it0, 0, sizeof(it0));
+    it0.cost = cost;
+    it0.gradient_max_norm = grad_max;
+    it0.trust_region_radius = opts.initial_trust_region_radius;
+    it0.step_is_valid = 1;
+    it0.step_is_successful = 1;
+    push(it0);
+  }
+  if (grad_max <= opts.gradient_tolerance) {
+    sm.termination_type = SFM_CONVERGENCE;
+  } else {
+    double radius = opts.initial_trust_region_radius;
+    double decrease_factor = 2.0;
+    int num_consecutive_invalid = 0;
+    int iteration = 0;
+    while (true) {
+      if (iteration >= opts.max_num_iterations) { sm.termination_type = SFM_NO_CONVERGENCE; break; }
+      ++iteration;
+      sfm_ba_iteration itr;
+      std::memset(&itr, 0, sizeof(itr));
+      itr.iteration = iteration;
+      const double tls = now_s();
+      if ((rc = compute_step(h, radius))) return rc;
+      sm.linear_solver_time_s += now_s() - tls;
+      sm.num_linear_solves++;
+      int chol_fail = 0;
+      std::memcpy(&chol_fail, sc + kNumScalars, sizeof(int));
+      const bool solve_ok = chol_fail == 0 && !(sc[kBadStep] > 0.0) && !(sc[kBadCam] > 0.0) && !(sc[kBadBack] > 0.0);
+      const double model_cost_change = sc[kModelChange];
+      itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;
+      itr.step_is_successful = 0;
+      if (!itr.step_is_valid) {
+        ++num_consecutive_invalid;
+        sm.num_invalid_steps++;
+        if (num_consecutive_invalid >= opts.max_num_consecutive_invalid_steps) {
+          sm.termination_type = SFM_FAILURE;
+          itr.cost = cost; itr.gradient_max_norm = grad_max; itr.trust_region_radius = radius;
+          push(itr);
+          break;
+        }
+        itr.cost = cost;
+        itr.gradient_max_norm = grad_max;
+      } else {
+        num_consecutive_invalid = 0;
+        double new_cost = sc[kNewCost];
+        if (!std::isfinite(new_cost)) new_cost = std::numeric_limits<double>::max();
+        sm.num_residual_evaluations++;
+        itr.step_norm = std::sqrt(sc[kStep2Cam] + sc[kStep2Pt]);
+        const double step_size_tolerance = opts.parameter_tolerance * (x_norm + opts.parameter_tolerance);
+        if (itr.step_norm <= step_size_tolerance) {
+          sm.termination_type = SFM_CONVERGENCE;
+          itr.cost = cost; itr.gradient_max_norm = grad_max; itr.trust_region_radius = radius;
+          push(itr);
+          break;
+        }
+        itr.cost_change = cost - new_cost;
+        if (std::fabs(itr.cost_change) <= opts.function_tolerance * cost) {
+          sm.termination_type = SFM_CONVERGENCE;
+          itr.cost = cost; itr.gradient_max_norm = grad_max; itr.trust_region_radius = radius;
+          push(itr);
+          break;
+        }
+        itr.relative_decrease = itr.cost_change / model_cost_change;
+        itr.step_is_successful = itr.relative_decrease > opts.min_relative_decrease;
+      }
+      if (itr.step_is_successful) {
+        sm.num_successful_steps++;
+        radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * itr.relative_decrease - 1.0, 3));
+        radius = std::min(opts.max_trust_region_radius, radius);
+        decrease_factor = 2.0;
+        std::swap(d.cam, d.cam_new);
+        std::swap(d.X, d.X_new);
+        tj = now_s();
+        if ((rc = evaluate(h, false, opts.jacobi_scaling != 0))) return rc;
+        sm.jacobian_time_s += now_s() - tj;
+        sm.num_jacobian_evaluations++;
+        sm.num_residual_evaluations++;
+        cost = sc[kCost];
+        if (!std::isfinite(cost)) { sm.termination_type = SFM_FAILURE; break; }
+        grad_max = std::max(sc[kGradMaxCam], sc[kGradMaxPt]);
+        x_norm = std::sqrt(sc[kXNorm2Cam] + sc[kXNorm2Pt]);
+      } else {
+        sm.num_unsuccessful_steps++;
+        radius = radius / decrease_factor;
+        decrease_factor *= 2.0;
+      }
+      itr.gradient_max_norm = grad_max;
+      itr.cost = cost;
+      itr.trust_region_radius = radius;
+      push(itr);
+      if (itr.step_is_successful) {
+        if (grad_max <= opts.gradient_tolerance) { sm.termination_type = SFM_CONVERGENCE; break; }
+      } else {
+        if (radius < opts.min_trust_region_radius) { sm.termination_type = SFM_CONVERGENCE; break; }
+      }
+    }
+    sm.num_iterations = iteration;
+  }
+  sm.final_cost = cost;
+  sm.wall_time_s = now_s();
+  if (summary) *summary = sm;
+  return 0;
+}
+
+int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const double* obs_uv,
+                 const int32_t* cam_idx, const int32_t* pt_idx, int32_t n_cams, const double* K9, double* rot,
+                 double* t, int32_t n_pts, double* X, sfm_ba_summary* summary, sfm_ba_iteration* trace,
+                 int32_t trace_cap, int32_t* trace_len) {
+  if (mode < 0 || mode > 2 || n_obs == 0) {
+    if (summary) { std::memset(summary, 0, sizeof(*summary)); summary->termination_type = SFM_CONVERGENCE; }
+    if (trace_len) *trace_len = 0;
+    return 0;
+  }
+  int dev = 0;
+  hipGetDevice(&dev);
+  sfm_ba_handle* h = nullptr;
+  int rc = sfm_ba_create(dev, &h);
+  if (rc) return rc;
+  rc = sfm_ba_set_problem(h, n_obs, obs_uv, cam_idx, pt_idx, n_cams, K9, rot, t, n_pts, X);
+  if (!rc) rc = sfm_ba_solve_resident(h, opts, mode, summary, trace, trace_cap, trace_len);
+  if (!rc) rc = sfm_ba_get_parameters(h, rot, t, X);
+  std::string err = g_err;
+  sfm_ba_destroy(h);
+  g_err = err;
+  return rc;
+}
+
+int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
+  if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
+  HIPCHK(hipSetDevice(h->device));
+  DevProblem& d = h->d;
+  launch_cam_prep(d, d.cam, false, h->stream);
+  launch_jacobian(d, false, h->stream);
+  if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
+  launch_reduce(d, kPCost, std::max(1, blocks_for(d.N, 256)), 0, kCost, h->stream);
+  std::vector<double> rec(size_t(kJRec) * d.N);
+  if (d.N)
+    HIPCHK(hipMemcpyAsync(rec.data(), d.jrec, sizeof(double) * rec.size(), hipMemcpyDeviceToHost, h->stream));
+  double c = 0;
+  HIPCHK(hipMemcpyAsync(&c, d.scal + kCost, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (cost) *cost = c;
+  for (int64_t q = 0; q < d.N; ++q) {
+    const int64_t i = h->order[q];
+    const double* r = &rec[size_t(kJRec) * q];
+    if (res) { res[2 * i] = r[kRes]; res[2 * i + 1] = r[kRes + 1]; }
+    if (jac) {
+      double* J = jac + 18 * i;
+      for (int row = 0; row < 2; ++row) {
+        for (int k = 0; k < 6; ++k) J[9 * row + k] = r[kJC + 6 * row + k];
+        for (int k = 0; k < 3; ++k) J[9 * row + 6 + k] = r[kJX + 3 * row + k];
+      }
+    }
+  }
+  return 0;
+}
+
+int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
+  if (!h || !h->has_problem || reps < 1) return fail(SFM_EINVAL, "bad arguments");
+  HIPCHK(hipSetDevice(h->device));
+  DevProblem& d = h->d;
+  launch_cam_prep(d, d.cam, false, h->stream);
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  launch_jacobian(d, true, h->stream);  // warm
+  HIPCHK(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < reps; ++i) launch_jacobian(d, true, h->stream);
+  HIPCHK(hipEventRecord(e1, h->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (avg_ms) *avg_ms = double(ms) / reps;
+  return 0;
+}
+
+}  // extern "C"

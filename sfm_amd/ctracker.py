@@ -1,0 +1,106 @@
+"""Host-side mirror of the reference's CTracker call surface for the hot path.
+
+Mirrors /root/reference/CTracker.h:44-67 (same names, argument meaning and
+behaviour) over the C ABI; OpenCV types are replaced by their memory layout
+(Point2d -> float64 [n][2], Matx33d -> float64 [9] row-major, Mat of BRISK
+descriptors -> uint8 [n][64]).
+
+  bundleAdjustmentStructAndPose  CTracker.h:65,  CTracker.cpp:670-702
+  matchFeatures (6 overloads)    CTracker.h:50-58, CTracker.cpp:114-149,
+                                 211-250, 368-417, 419-477
+
+The reference passes parameter blocks as vector<double*> with one pointer
+per observation (duplicates across observations, identity by address,
+CSfM.cpp:321-340).  Python has no raw pointers; the mirror takes the
+deduplicated form (`pts3d` [P][3] + per-observation `pt_idx`) and writes
+results back in place, exactly as Ceres writes through the pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_int32
+
+import numpy as np
+
+from . import ba as _ba
+from ._ffi import check, lib, ptr
+
+STRUCT_ONLY, POSE_ONLY, STRUCT_AND_POSE = _ba.STRUCT_ONLY, _ba.POSE_ONLY, _ba.STRUCT_AND_POSE
+
+
+class CTracker:
+    """Hot-path subset of CTracker (constructor constants: CTracker.cpp:25-49)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._ratioTest = 0.8             # CTracker.cpp:27
+        self._maxMatchDistance = 40.0     # CTracker.cpp:30
+        self._minMatchDistance = 1.5      # CTracker.cpp:31
+        self._minFeatures = 5             # CTracker.cpp:32
+        self.last_summary = None
+        self.last_trace = None
+
+    # ---- bundle adjustment (CTracker.cpp:670-702) --------------------------
+    def bundleAdjustmentStructAndPose(self, observations, camIdx, K, R, t, pts3D, isStructOrPose, pt_idx=None,
+                                      options=None):
+        """observations [N][2]; camIdx [N]; K [C][9] (or [C][3][3]); R, t [C][3]
+        (updated in place); pts3D [P][3] (updated in place) with pt_idx [N], or
+        pts3D [N][3] one row per observation when pt_idx is None (then rows
+        that are equal objects are NOT merged — pass pt_idx for shared points).
+        Returns the Ceres-style summary the reference discards."""
+        K9 = np.ascontiguousarray(np.asarray(K, dtype=np.float64).reshape(-1, 9))
+        if pt_idx is None:
+            pt_idx = np.arange(len(observations), dtype=np.int32)
+        sm, tr = _ba.solve(observations, camIdx, pt_idx, K9, R, t, pts3D, options=options, mode=isStructOrPose)
+        self.last_summary, self.last_trace = sm, tr
+        return sm
+
+    # ---- matching --------------------------------------------------------
+    def _match(self, pts0, desc0, pts1, desc1, min_d, max_d):
+        pts0 = np.ascontiguousarray(pts0, dtype=np.float64).reshape(-1, 2)
+        pts1 = np.ascontiguousarray(pts1, dtype=np.float64).reshape(-1, 2)
+        desc0 = np.ascontiguousarray(desc0, dtype=np.uint8)
+        desc1 = np.ascontiguousarray(desc1, dtype=np.uint8)
+        n0, n1 = pts0.shape[0], pts1.shape[0]
+        nb = desc0.shape[1] if desc0.ndim == 2 and n0 else (desc1.shape[1] if desc1.ndim == 2 and n1 else 64)
+        cap = max(1, min(n0, n1))
+        i0 = np.zeros(cap, np.int32)
+        i1 = np.zeros(cap, np.int32)
+        nm = c_int32(0)
+        check(lib().sfm_match_features(self.device, ptr(pts0), ptr(desc0), n0, ptr(pts1), ptr(desc1), n1, nb,
+                                       self._ratioTest, float(min_d), float(max_d), ptr(i0), ptr(i1),
+                                       ctypes.byref(nm)), "sfm_match_features")
+        m = nm.value
+        return i0[:m].copy(), i1[:m].copy()
+
+    def matchFeatures(self, *args):
+        """Overloads of CTracker::matchFeatures:
+        (pts0, desc0, pts1, desc1)                         CTracker.cpp:114-149
+        (pts0, desc0, pts1, desc1, minDist, maxDist)       CTracker.cpp:211-250
+        (prevPts, prevDesc, currPts, currDesc, prevIdx, currIdx)   index-subset
+           form of CTracker.cpp:368-417 (frame data passed explicitly: the
+           mirror has no CFrame); returns frame-global indices.
+        Each returns (matchIdx0, matchIdx1)."""
+        if len(args) == 4:
+            return self._match(*args, self._minMatchDistance, self._maxMatchDistance)
+        if len(args) == 6 and np.isscalar(args[4]):
+            return self._match(*args)
+        if len(args) == 6:
+            prevPts, prevDesc, currPts, currDesc, prevIdx, currIdx = args
+            prevIdx = np.asarray(prevIdx, dtype=np.int64)
+            currIdx = np.asarray(currIdx, dtype=np.int64)
+            a, b = self._match(np.asarray(prevPts)[prevIdx], np.asarray(prevDesc)[prevIdx],
+                               np.asarray(currPts)[currIdx], np.asarray(currDesc)[currIdx],
+                               self._minMatchDistance, self._maxMatchDistance)
+            return prevIdx[a].astype(np.int32), currIdx[b].astype(np.int32)
+        raise TypeError("matchFeatures: unsupported overload")
+
+    def knnMatch2(self, desc0, desc1):
+        """The 2-NN Hamming search alone (brisk::BruteForceMatcher::knnMatch, k=2)."""
+        desc0 = np.ascontiguousarray(desc0, dtype=np.uint8)
+        desc1 = np.ascontiguousarray(desc1, dtype=np.uint8)
+        n0, n1 = desc0.shape[0], desc1.shape[0]
+        out = [np.zeros(n0, np.int32) for _ in range(4)]
+        check(lib().sfm_knn2_hamming(self.device, ptr(desc0), n0, ptr(desc1), n1, desc0.shape[1], *map(ptr, out)),
+              "sfm_knn2_hamming")
+        return tuple(out)
