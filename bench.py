@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark: landmark-sharded bundle adjustment on MI355X (BASELINE.json metric
+"BA iterations/sec + residual-evals/sec (cams x pts x obs); 1/2/4/8 GPU").
+
+A step is one complete BA solve -- CTracker::bundleAdjustmentStructAndPose
+(/root/reference/CTracker.cpp:670-702) with the reference's Ceres options --
+over a synthetic scene resident in HBM: parameters are reset on the device
+(inside the timed region), then the LM loop runs to Ceres' own termination.
+
+Workload per GPU: BASELINE config C3 (500 cameras, 200k points, 2M
+observations, fp64).  With N GPUs the scene has N x 200k points sharded by
+landmark (weak scaling; cameras replicated, RCCL all-reduce of the reduced
+camera system every LM iteration).  `value` = residual evaluations x
+observations (whole job) per second; LM iterations/s is reported beside it.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+   N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F64_MFMA_PEAK_TFS = 78.6   # MI355X fp64 matrix spec
+CAMS, PTS_PER_GPU, VIEWS = 500, 200_000, 10
+SEED = 0x5F3D2017 + 3      # config C3
+
+
+def jacobian_bytes(n_obs: int, n_cams: int, n_pts: int) -> int:
+    # uv 16 + cam/pt index 8 + r 16 + J 144 per observation,
+    # pose 48 + K 40 per camera, X 24 per point.
+    return 184 * n_obs + 88 * n_cams + 24 * n_pts
+
+
+def cholesky_flops(n: int) -> float:
+    return n ** 3 / 3.0
+
+
+def cpu_baseline(scene) -> dict:
+    """Oracle (single-threaded C++ restatement of the reference's Ceres path)
+    on a bounded sample: one complete C3 solve on the host."""
+    from oracle import ffi as O
+    r, t, X = scene.copy_params()
+    t0 = time.perf_counter()
+    sm, _ = O.solve(scene.uv, scene.cam_idx, scene.pt_idx, scene.K, r, t, X)
+    wall = time.perf_counter() - t0
+    evals = sm["num_residual_evaluations"]
+    return {
+        "value": scene.n_obs * evals / wall,
+        "unit": "residual-evals/s (obs x evaluations)",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"one complete C3 solve ({scene.n_cams} cams / {scene.n_pts} pts / {scene.n_obs} obs): "
+                   f"{sm['num_iterations']} LM iterations, {evals} residual evaluations, {wall:.1f} s "
+                   "(oracle/ba_oracle.cpp, Ceres-1.12-equivalent restatement, 1 thread)"),
+        "lm_iterations_per_s": sm["num_iterations"] / wall,
+        "solve_s": wall,
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pts-per-gpu", type=int, default=PTS_PER_GPU)
+    ap.add_argument("--cams", type=int, default=CAMS)
+    ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    import sfm_amd
+    from sfm_amd import scene as S
+
+    P = args.pts_per_gpu
+    sc = S.generate(args.cams, P * world, seed=SEED, p_begin=rank * P, p_end=(rank + 1) * P)
+    ba = sfm_amd.BundleAdjuster(device=local_rank)
+    if world > 1:
+        uid = [sfm_amd.BundleAdjuster.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ba.set_comm(world, rank, uid[0])
+    ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
+    opts = sfm_amd.default_options()
+
+    def barrier():
+        ba.sync()
+        torch.cuda.synchronize(local_rank)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ba.reset()
+        ba.solve(opts)
+    ba.set_profiling(True)
+    barrier()
+    t0 = time.perf_counter()
+    iters = evals = jevals = 0
+    last = None
+    for _ in range(args.steps):
+        ba.reset()
+        sm, _ = ba.solve(opts)
+        iters += sm.num_iterations
+        evals += sm.num_residual_evaluations
+        jevals += sm.num_jacobian_evaluations
+        last = sm
+    barrier()
+    elapsed = time.perf_counter() - t0
+    phases = ba.phase_times()
+    ba.set_profiling(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    n_obs_total = sc.n_obs * world
+    n_pts_total = P * world
+    value = n_obs_total * evals / elapsed
+    jac = phases["jacobian"]
+    jac_ms = jac["ms"] / max(1, jac["count"])
+    jac_bytes = jacobian_bytes(sc.n_obs, sc.n_cams, sc.n_pts)
+    jac_gbs = jac_bytes / (jac_ms * 1e-3) / 1e9
+    chol = phases["cholesky"]
+    chol_ms = chol["ms"] / max(1, chol["count"])
+    n_sys = 6 * sc.n_cams
+    chol_tfs = cholesky_flops(n_sys) / (chol_ms * 1e-3) / 1e12
+    total_phase = sum(p["ms"] for p in phases.values())
+    dominant = max(phases, key=lambda k: phases[k]["ms"])
+
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_jacobian.json")
+    if os.path.exists(prof):
+        try:
+            with open(prof) as f:
+                pm = json.load(f)
+            if pm.get("n_obs") == sc.n_obs:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass)", "bound": "hbm", "achieved": round(jac_gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5)}
+    roof_chol = {"kernel": "dense reduced-camera Cholesky (k_chol_diag/k_chol_gemm, f64 MFMA)", "bound": "mfma",
+                 "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                 "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": None,
+                 "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4)}
+    roofline = roof_chol if dominant == "cholesky" else roof_jac
+
+    out = {
+        "metric": "BA iterations/sec + residual-evals/sec (cams x pts x obs); 1/2/4/8 GPU",
+        "value": value,
+        "unit": "residual-evals/s (obs x evaluations)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded object-scanning scene, SURVEY.md §8d; K from main/main.cpp:47-50)",
+        "config": {
+            "workload": "C3 per GPU: full BA solve (LM + DENSE_SCHUR, Ceres default options)",
+            "cams": sc.n_cams, "points": n_pts_total, "observations": n_obs_total,
+            "points_per_gpu": sc.n_pts, "obs_per_gpu": sc.n_obs, "views_per_point": VIEWS,
+            "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
+        },
+        "lm_iterations_per_s": iters / elapsed,
+        "lm_iterations_per_solve": iters / args.steps,
+        "residual_evals_per_solve": evals / args.steps,
+        "jacobian_evals_per_solve": jevals / args.steps,
+        "final_cost": last.final_cost if last else None,
+        "roofline": roofline,
+        "roofline_jacobian": roof_jac,
+        "roofline_cholesky": roof_chol,
+        "phase_ms_per_solve": {k: round(v["ms"] / args.steps, 4) for k, v in phases.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(sc)
+        out["cpu_baseline"] = cpu
+        out["speedup_vs_cpu"] = value / cpu["value"]
+    else:
+        out["cpu_baseline"] = None
+    if args.phases and rank == 0:
+        print(json.dumps(phases, indent=1), file=sys.stderr)
+    if rank == 0:
+        print(json.dumps(out))
+    ba.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

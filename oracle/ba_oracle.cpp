@@ -799,3 +799,96 @@ write_back:
 int oracle_abi_version(void) { return 1; }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Test helper for the landmark-sharding decomposition:
+// the DENSE_SCHUR reduced camera system of a set of observations at given
+// parameters, Jacobi scale and LM diagonal D (all explicit, so a shard can
+// be assembled with the GLOBAL scale / D).  S [6C][6C] (full, row-major),
+// rhs [6C].  The camera diagonal D_c^2 is added iff add_cam_diag.
+// Also returns the unscaled squared column norms of the observations
+// (colnorm_c [C][6], colnorm_p [P][3]) when those pointers are non-NULL.
+extern "C" int oracle_ba_reduced_system(int64_t n_obs, const double* obs_uv, const int32_t* cam_idx,
+                                        const int32_t* pt_idx, int32_t n_cams, const double* K9, const double* rot,
+                                        const double* t, int32_t n_pts, const double* X, const double* scale_c,
+                                        const double* scale_p, const double* D_c, const double* D_p,
+                                        int32_t add_cam_diag, double* S, double* rhs, double* colnorm_c,
+                                        double* colnorm_p) {
+  const int C = n_cams, nf = 6 * C;
+  std::vector<std::vector<int64_t>> by_pt(n_pts);
+  for (int64_t i = 0; i < n_obs; ++i) by_pt[pt_idx[i]].push_back(i);
+  std::memset(S, 0, sizeof(double) * size_t(nf) * nf);
+  std::memset(rhs, 0, sizeof(double) * nf);
+  if (colnorm_c) std::memset(colnorm_c, 0, sizeof(double) * 6 * size_t(C));
+  if (colnorm_p) std::memset(colnorm_p, 0, sizeof(double) * 3 * size_t(n_pts));
+  if (add_cam_diag)
+    for (int i = 0; i < nf; ++i) S[size_t(i) * nf + i] += D_c[i] * D_c[i];
+  std::vector<double> Ebuf;
+  std::vector<int> fcams;
+  for (int p = 0; p < n_pts; ++p) {
+    if (by_pt[p].empty()) continue;
+    double ete[9] = {0};
+    for (int k = 0; k < 3; ++k) ete[4 * k] = D_p[3 * p + k] * D_p[3 * p + k];
+    double g[3] = {0, 0, 0};
+    fcams.clear();
+    Ebuf.clear();
+    std::vector<double> Es, Fs, bs;
+    for (int64_t i : by_pt[p]) {
+      const int c = cam_idx[i];
+      double res[2], J[18];
+      EvalJet(rot + 3 * size_t(c), t + 3 * size_t(c), X + 3 * size_t(p), K9 + 9 * size_t(c), obs_uv[2 * i],
+              obs_uv[2 * i + 1], res, J);
+      for (int row = 0; row < 2; ++row) {
+        for (int k = 0; k < 6; ++k) if (colnorm_c) colnorm_c[6 * c + k] += J[9 * row + k] * J[9 * row + k];
+        for (int k = 0; k < 3; ++k) if (colnorm_p) colnorm_p[3 * p + k] += J[9 * row + 6 + k] * J[9 * row + 6 + k];
+      }
+      int slot = -1;
+      for (size_t s2 = 0; s2 < fcams.size(); ++s2) if (fcams[s2] == c) { slot = int(s2); break; }
+      if (slot < 0) { slot = int(fcams.size()); fcams.push_back(c); Ebuf.resize(Ebuf.size() + 18, 0.0); }
+      double E[6], F[12];
+      for (int row = 0; row < 2; ++row) {
+        for (int k = 0; k < 3; ++k) E[3 * row + k] = J[9 * row + 6 + k] * scale_p[3 * p + k];
+        for (int k = 0; k < 6; ++k) F[6 * row + k] = J[9 * row + k] * scale_c[6 * c + k];
+      }
+      for (int a = 0; a < 3; ++a) {
+        for (int bb = 0; bb < 3; ++bb) ete[3 * a + bb] += E[a] * E[bb] + E[3 + a] * E[3 + bb];
+        g[a] += E[a] * res[0] + E[3 + a] * res[1];
+        for (int k = 0; k < 6; ++k) Ebuf[18 * slot + 6 * a + k] += E[a] * F[k] + E[3 + a] * F[6 + k];
+      }
+      for (int a = 0; a < 6; ++a)
+        for (int bb = 0; bb < 6; ++bb) S[size_t(6 * c + a) * nf + 6 * c + bb] += F[a] * F[bb] + F[6 + a] * F[6 + bb];
+      Es.insert(Es.end(), E, E + 6);
+      Fs.insert(Fs.end(), F, F + 12);
+      bs.push_back(res[0]); bs.push_back(res[1]);
+    }
+    double L[9], inv[9];
+    if (!Llt3(ete, L)) return -1;
+    for (int col = 0; col < 3; ++col) {
+      double e[3] = {0, 0, 0}; e[col] = 1.0;
+      Llt3Solve(L, e);
+      for (int a = 0; a < 3; ++a) inv[3 * a + col] = e[a];
+    }
+    double ig[3];
+    for (int a = 0; a < 3; ++a) ig[a] = inv[3 * a] * g[0] + inv[3 * a + 1] * g[1] + inv[3 * a + 2] * g[2];
+    for (size_t q = 0; q < by_pt[p].size(); ++q) {
+      const int c = cam_idx[by_pt[p][q]];
+      double sj[2];
+      for (int row = 0; row < 2; ++row) {
+        sj[row] = bs[2 * q + row];
+        for (int k = 0; k < 3; ++k) sj[row] -= Es[6 * q + 3 * row + k] * ig[k];
+      }
+      for (int k = 0; k < 6; ++k) rhs[6 * c + k] += Fs[12 * q + k] * sj[0] + Fs[12 * q + 6 + k] * sj[1];
+    }
+    const int m = int(fcams.size());
+    for (int j = 0; j < m; ++j)
+      for (int k = 0; k < m; ++k)
+        for (int a = 0; a < 6; ++a)
+          for (int bb = 0; bb < 6; ++bb) {
+            double s = 0;
+            for (int u = 0; u < 3; ++u)
+              for (int v = 0; v < 3; ++v) s += Ebuf[18 * j + 6 * u + a] * inv[3 * u + v] * Ebuf[18 * k + 6 * v + bb];
+            S[size_t(6 * fcams[j] + a) * nf + 6 * fcams[k] + bb] -= s;
+          }
+  }
+  return 0;
+}

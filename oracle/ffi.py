@@ -67,6 +67,10 @@ def lib():
         L.oracle_match_features.argtypes = [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                             c_double, c_double, c_double, c_void_p, c_void_p]
         L.oracle_match_features.restype = c_int
+        L.oracle_ba_reduced_system.argtypes = [c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                               c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+        L.oracle_ba_reduced_system.restype = c_int
         _L = L
     return _L
 
@@ -138,3 +142,24 @@ def match_features(pts0, desc0, pts1, desc1, ratio=0.8, min_distance=1.5, max_di
     m = lib().oracle_match_features(_p(pts0), _p(desc0), n0, _p(pts1), _p(desc1), n1, nb, ratio, min_distance,
                                     max_distance, _p(i0), _p(i1))
     return i0[:m].copy(), i1[:m].copy()
+
+
+def reduced_system(uv, cam_idx, pt_idx, K9, rot, t, X, scale_c, scale_p, D_c, D_p, add_cam_diag=True):
+    """DENSE_SCHUR reduced camera system (S [6C][6C], rhs [6C]) plus unscaled
+    squared column norms, for the sharding-decomposition tests."""
+    uv = np.ascontiguousarray(uv, np.float64)
+    cam_idx = np.ascontiguousarray(cam_idx, np.int32)
+    pt_idx = np.ascontiguousarray(pt_idx, np.int32)
+    K9 = np.ascontiguousarray(K9, np.float64).reshape(-1, 9)
+    arrs = [np.ascontiguousarray(a, np.float64) for a in (rot, t, X, scale_c, scale_p, D_c, D_p)]
+    C, P = arrs[0].shape[0], arrs[2].shape[0]
+    S = np.zeros((6 * C, 6 * C))
+    rhs = np.zeros(6 * C)
+    cc = np.zeros((C, 6))
+    cp = np.zeros((P, 3))
+    rc = lib().oracle_ba_reduced_system(uv.shape[0], _p(uv), _p(cam_idx), _p(pt_idx), C, _p(K9), _p(arrs[0]),
+                                        _p(arrs[1]), P, _p(arrs[2]), _p(arrs[3]), _p(arrs[4]), _p(arrs[5]),
+                                        _p(arrs[6]), 1 if add_cam_diag else 0, _p(S), _p(rhs), _p(cc), _p(cp))
+    if rc != 0:
+        raise RuntimeError("oracle_ba_reduced_system failed")
+    return S, rhs, cc, cp
