@@ -177,6 +177,14 @@ int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uin
                      int32_t desc_bytes, int32_t* best_idx, int32_t* best_dist, int32_t* second_idx,
                      int32_t* second_dist);
 
+/* Testing hook: solve the dense SPD system A y = b (A [n][n] row-major,
+ * both triangles given; only the upper triangle is read) with the device
+ * Cholesky + substitution kernels used for the reduced camera system.
+ * reps > 1 repeats the factorisation for timing; *ms = mean device time per
+ * factor+solve; *chol_fail = 1 if a pivot was not positive. */
+int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double* b, double* y, int32_t reps,
+                        double* ms, int32_t* chol_fail);
+
 /* Synthetic scenes, host-only.  Points [p_begin, p_end) of a
  * scene with n_pts_total points; every camera is returned.  Observations are
  * sorted by (point, camera); pt_idx is relative to p_begin.

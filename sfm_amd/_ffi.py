@@ -110,6 +110,8 @@ _SIGNATURES = {
                                    c_double, c_double, c_double, c_void_p, c_void_p, POINTER(c_int32)]),
     "sfm_knn2_hamming": (c_int, [c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
+    "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
+                                    POINTER(c_int32)]),
     "sfm_scene_default_intrinsics": (None, [c_void_p]),
     "sfm_scene_generate": (c_int, [c_int32, c_int32, c_int32, c_int32, c_int32, c_uint64, c_double, c_double,
                                    c_double, c_double] + [c_void_p] * 10),

@@ -137,3 +137,17 @@ def solve(uv, cam_idx, pt_idx, K9, rot, t, X, options: BAOptions | None = None, 
                              int(rot.shape[0]), ptr(K9), ptr(rot), ptr(t), int(X.shape[0]), ptr(X),
                              ctypes.byref(sm), tr, trace_cap, ctypes.byref(tl)), "sfm_ba_solve")
     return sm, [tr[i].as_dict() for i in range(tl.value)]
+
+
+def dense_spd_solve(A, b, device: int = 0, reps: int = 1):
+    """Testing hook: y = A^-1 b with the device Cholesky used for the reduced
+    camera system.  Returns (y, ms_per_solve, chol_fail)."""
+    A = _f64(A)
+    b = _f64(b)
+    n = int(A.shape[0])
+    y = np.zeros(n)
+    ms = c_double(0.0)
+    fl = c_int32(0)
+    check(lib().sfm_dense_spd_solve(device, n, ptr(A), ptr(b), ptr(y), reps, ctypes.byref(ms), ctypes.byref(fl)),
+          "sfm_dense_spd_solve")
+    return y, ms.value, fl.value

@@ -706,6 +706,61 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   return 0;
 }
 
+int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double* b, double* y, int32_t reps,
+                        double* ms, int32_t* chol_fail) {
+  if (n <= 0 || !A || !b || !y || reps < 1) return fail(SFM_EINVAL, "bad arguments");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return fail(SFM_ENODEV, "no device");
+  HIPCHK(hipSetDevice(device));
+  DevProblem d;
+  d.n = n;
+  d.ld = ((n + 1 + kNB - 1) / kNB) * kNB;
+  d.nblk = d.ld / kNB;
+  // augmented column-major-lower image: (i, j) at j*ld + i, i >= j
+  std::vector<double> img(size_t(d.ld) * d.ld, 0.0);
+  for (int j = 0; j < n; ++j)
+    for (int i = j; i < n; ++i) img[size_t(j) * d.ld + i] = A[size_t(j) * n + i];  // row-major upper (j, i)
+  for (int j = 0; j < n; ++j) img[size_t(j) * d.ld + n] = b[j];
+  for (int j = n; j < d.ld; ++j) img[size_t(j) * d.ld + j] = 1.0;
+  double *S = nullptr, *S0 = nullptr, *invd = nullptr, *z = nullptr, *ys = nullptr;
+  int* fl = nullptr;
+  const size_t bytes = sizeof(double) * img.size();
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreate(&s));
+  HIPCHK(hipMalloc(&S, bytes));
+  HIPCHK(hipMalloc(&S0, bytes));
+  HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
+  HIPCHK(hipMalloc(&z, sizeof(double) * d.ld));
+  HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
+  HIPCHK(hipMalloc(&fl, sizeof(int)));
+  HIPCHK(hipMemcpy(S0, img.data(), bytes, hipMemcpyHostToDevice));
+  d.S = S; d.invL = invd; d.zwork = z; d.ysol = ys; d.fail = fl;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  float total = 0.f;
+  for (int r = 0; r < reps; ++r) {
+    HIPCHK(hipMemcpyAsync(S, S0, bytes, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipEventRecord(e0, s));
+    launch_cholesky(d, s);
+    launch_backsolve(d, s);
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    float m = 0.f;
+    HIPCHK(hipEventElapsedTime(&m, e0, e1));
+    if (r > 0 || reps == 1) total += m;
+  }
+  int f = 0;
+  HIPCHK(hipMemcpy(&f, fl, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(y, ys, sizeof(double) * n, hipMemcpyDeviceToHost));
+  if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
+  if (chol_fail) *chol_fail = f;
+  hipEventDestroy(e0); hipEventDestroy(e1);
+  hipFree(S); hipFree(S0); hipFree(invd); hipFree(z); hipFree(ys); hipFree(fl);
+  hipStreamDestroy(s);
+  return 0;
+}
+
 int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
   if (!h || !h->has_problem || reps < 1) return fail(SFM_EINVAL, "bad arguments");
   HIPCHK(hipSetDevice(h->device));
