@@ -9,14 +9,13 @@
 // rows beyond n are identity padding up to a multiple of the 64-wide tile.
 //
 // Right-looking blocked algorithm, tile 64, three launches per step k:
-//   k_chol_potrf : factor tile (k,k) in registers (one workgroup), store
-//                  1/L_jj for the substitutions
-//   k_chol_trsm  : panel tiles (i,k) <- A_ik L_kk^-T by column substitution
-//                  (no barriers: rows are independent)
+//   k_chol_potrf : factor tile (k,k) in registers (one wavefront) and form
+//                  its inverse W_k = L_kk^-1 (stored for the next two)
+//   k_chol_trsm  : panel tiles (i,k) <- A_ik W_k^T on MFMA
 //   k_chol_syrk  : trailing tiles (i,j) -= L_ik L_jk^T on v_mfma_f64_16x16x4_f64,
 //                  operands loaded straight into registers
-// and the back substitution L^T y = z (one launch per tile row, each
-// workgroup solving the 64x64 diagonal block redundantly).
+// and the back substitution L^T y = z (one launch per tile row, y_k = W_k^T z_k
+// recomputed by each workgroup, then the update of the rows above).
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include "ba_device.h"
@@ -44,91 +43,130 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
-// POTRF of one 64x64 tile by ONE wavefront.  Lane r holds row r of the tile
-// (a[j] = A(r, j), upper part taken from the symmetric lower storage), so
-// for column j lane r's own a[j] = A(r, j) = A(j, r) and no column ever has
-// to be gathered:
+// POTRF of one 64x64 tile plus the tile inverse W = L^-1, two wavefronts.
+// Wave 0 factors: lane r holds row r of the tile (a[j] = A(r, j), upper part
+// taken from the symmetric lower storage), so for column j lane r's own
+// a[j] = A(j, r):
 //   pivot  d = a[j] of lane j           (readlane broadcast)
 //   l_r    = a[j] / sqrt(d)             (own register: L(r, j))
 //   update a[c] -= l_r * L(c, j), c > j (L(c, j) by LDS broadcast reads)
-// Fully unrolled (register indices are compile-time), one 64-lane LDS store
-// and no barrier per column: the pivot chain is readlane -> rsq -> mul.
-__global__ __launch_bounds__(64) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
-                                                   double* __restrict__ invd, int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double colb[NB];
-  const int r = threadIdx.x;
+// and leaves every column L(:, j) in LDS.  L = E_0 E_1 ... E_63 with E_j the
+// identity whose column j is L(:, j), so wave 1 forms W = E_63^-1 ... E_0^-1
+// from those columns, one block of 8 behind wave 0: lane m holds column m
+// of W (w[c] = W(c, m)) and applies w[j] *= 1/L(j, j); w[c] -= L(c, j) w[j].
+// W turns the panel solve and the back substitution into products
+// (k_chol_trsm, k_backsolve_step) with no per-column chain outside this
+// kernel.  Fully unrolled; the broadcast reads of a column are issued
+// together.  Pivots at or beyond n (augmented row, identity padding) are
+// taken as 1 so the padding stays finite; they are never read back.
+constexpr int kPotrfBlk = 8;
+__global__ __launch_bounds__(128) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
+                                                    double* __restrict__ Winv, int* __restrict__ fail) {
+  __shared__ __attribute__((aligned(16))) double Lcol[NB * NB];  // Lcol[j][c] = L(c, j)
+  __shared__ double invs[NB];
+  const int r = threadIdx.x & 63;
   const int k0 = k * NB;
-  double a[NB];
+  if (threadIdx.x < 64) {
+    double a[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j)
-    a[j] = (j <= r) ? A[size_t(k0 + j) * ld + k0 + r] : A[size_t(k0 + r) * ld + k0 + j];
-  bool bad = false;
-  double myinv = 0.0;
+    for (int j = 0; j < NB; ++j)
+      a[j] = (j <= r) ? A[size_t(k0 + j) * ld + k0 + r] : A[size_t(k0 + r) * ld + k0 + j];
+    bool bad = false;
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double d = bcast(a[j], j);
-    bad |= !(d > 0.0) && (k0 + j) < n;
-    const double inv = rsqrt_nr(d);
-    if (r == j) myinv = inv;
-    const double l = a[j] * inv;  // L(r, j) for r >= j (r == j: sqrt(d))
-    a[j] = l;
-    colb[r] = l;
-    if (j < NB - 1) {
+    for (int j = 0; j < NB; ++j) {
+      double d = bcast(a[j], j);
+      if ((k0 + j) < n) bad |= !(d > 0.0);
+      else d = 1.0;
+      const double inv = rsqrt_nr(d);
+      const double l = a[j] * inv;  // L(r, j) for r >= j (r == j: sqrt(d))
+      a[j] = l;
+      Lcol[j * NB + r] = l;
+      invs[j] = inv;
+      if (j < NB - 1) {
+        double lc[NB];
 #pragma unroll
-      for (int c = j + 1; c < NB; ++c) a[c] = fma(-l, colb[c], a[c]);
+        for (int c = (j + 1) & ~1; c < NB; c += 2) {
+          const double2 v2 = *reinterpret_cast<const double2*>(&Lcol[j * NB + c]);
+          lc[c] = v2.x;
+          lc[c + 1] = v2.y;
+        }
+#pragma unroll
+        for (int c = j + 1; c < NB; ++c) a[c] = fma(-l, lc[c], a[c]);
+      }
+      if (j % kPotrfBlk == kPotrfBlk - 1) __syncthreads();
     }
-  }
-  if (bad && r == 0) atomicOr(fail, 1);
-  invd[k0 + r] = myinv;
+    if (bad && r == 0) atomicOr(fail, 1);
 #pragma unroll
-  for (int j = 0; j < NB; ++j)
-    if (j <= r) A[size_t(k0 + j) * ld + k0 + r] = a[j];
+    for (int j = 0; j < NB; ++j)
+      if (j <= r) A[size_t(k0 + j) * ld + k0 + r] = a[j];
+  } else {
+    double w[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) w[c] = (c == r) ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (j % kPotrfBlk == 0) __syncthreads();
+      w[j] *= invs[j];
+      if (j < NB - 1) {
+        double lc[NB];
+#pragma unroll
+        for (int c = (j + 1) & ~1; c < NB; c += 2) {
+          const double2 v2 = *reinterpret_cast<const double2*>(&Lcol[j * NB + c]);
+          lc[c] = v2.x;
+          lc[c + 1] = v2.y;
+        }
+#pragma unroll
+        for (int c = j + 1; c < NB; ++c) w[c] = fma(-lc[c], w[j], w[c]);
+      }
+    }
+    // W column-major (Wc[m][c] = W(c, m)); lane m writes 64 contiguous doubles
+    double* Wk = Winv + size_t(k) * NB * NB + size_t(r) * NB;
+#pragma unroll
+    for (int c = 0; c < NB; c += 2) *reinterpret_cast<double2*>(Wk + c) = double2{w[c], w[c + 1]};
+  }
 }
 
 // ---------------------------------------------------------------------------
-// Panel tiles (i, k), i > k:  X L_kk^T = B.  One thread per tile row (row r
-// of B in registers), one wavefront per tile, four tiles per workgroup
-// sharing L_kk in LDS.  Column j: x_j *= 1/L_jj, then x_c -= x_j L(c, j)
-// for c > j with L(c, j) read as an LDS broadcast; no cross-lane traffic.
-__global__ __launch_bounds__(256) void k_chol_trsm(double* __restrict__ A, int ld, int k, int m,
-                                                   const double* __restrict__ invd) {
-  __shared__ __attribute__((aligned(16))) double Lc[NB][NB];  // Lc[j][c] = L_kk(c, j)
-  __shared__ double id[NB];
-  const int t = threadIdx.x, r = t & 63, w = t >> 6;
-  const int k0 = k * NB;
-  const int tile = 4 * blockIdx.x + w;  // panel tile index (0-based below the diagonal)
-  {
-    double v[16];
+// Panel tile (i, k), i > k:  X L_kk^T = B  ->  X = B W^T, one workgroup per
+// tile on v_mfma_f64_16x16x4_f64, computed transposed like k_chol_syrk:
+// D[c][r] = sum_m W(c, m) B(r, m).  X overwrites B in place, so every wave
+// finishes its MFMA chain (all operand loads consumed) before any store.
+__global__ __launch_bounds__(256) void k_chol_trsm(double* __restrict__ A, int ld, int k,
+                                                   const double* __restrict__ Winv) {
+  const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
+  const int lr = lane & 15, lk = lane >> 4;
+  const double* Wk = Winv + size_t(k) * NB * NB;
+  double xa[2][16], yb[2][16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, j = e >> 6, c = e & 63;
-      v[q] = A[size_t(k0 + j) * ld + k0 + c];
-    }
+  for (int ks = 0; ks < 16; ++ks) {
+    const int m = 4 * ks + lk;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, j = e >> 6, c = e & 63;
-      Lc[j][c] = v[q];
-    }
+    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = A[size_t(k0 + m) * ld + i0 + rb + 16 * bb + lr];
   }
-  if (t < NB) id[t] = invd[k0 + t];
-  const bool active = tile < m;
-  const int i0 = (k + 1 + (active ? tile : 0)) * NB;
-  double x[NB];
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int c = 0; c < NB; ++c) x[c] = active ? A[size_t(k0 + c) * ld + i0 + r] : 0.0;
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    x[j] *= id[j];
-    if (j < NB - 1) {
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int c = j + 1; c < NB; ++c) x[c] = fma(-x[j], Lc[j][c], x[c]);
-    }
-  }
-  if (active) {
+    for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-    for (int c = 0; c < NB; ++c) A[size_t(k0 + c) * ld + i0 + r] = x[c];
-  }
+      for (int reg = 0; reg < 4; ++reg)
+        A[size_t(k0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = acc[a][bb][reg];
 }
 
 // ---------------------------------------------------------------------------
@@ -203,66 +241,58 @@ __global__ void k_copy_z(const double* __restrict__ A, int ld, int n, double* __
   }
 }
 
-// One step of the blocked back substitution L^T y = z, tile k (descending).
-// Every workgroup loads L_kk (all loads in flight at once), wavefront 0
-// solves L_kk^T y_k = z_k (redundant across workgroups; workgroup 0 stores
-// y_k), then thread l of workgroup b updates z_j, j = 256b + l < k0:
+// One step of the blocked back substitution L^T y = z, tile k (descending):
+// y_k = W^T z_k (a 64x64 product, recomputed by every workgroup; workgroup 0
+// stores it), then thread l of workgroup b updates z_j, j = 256b + l < k0:
 //   z_j -= sum_r L(k0 + r, j) y_k[r]
-// from its column's 64 contiguous doubles, prefetched before the solve.
+// from its column's 64 contiguous doubles, prefetched first.
 __global__ __launch_bounds__(256) void k_backsolve_step(const double* __restrict__ A, int ld, int n, int k,
-                                                        const double* __restrict__ invd, double* __restrict__ z,
+                                                        const double* __restrict__ Winv, double* __restrict__ z,
                                                         double* __restrict__ y) {
-  __shared__ double Lt[NB][NB + 1];  // Lt[r][j] = L_kk(r, j)
+  __shared__ double zk[NB];
+  __shared__ double part[4][NB];
   __shared__ double yk[NB];
   const int k0 = k * NB;
   const int nreal = (n - k0) < NB ? (n - k0) : NB;
-  const int t = threadIdx.x, lane = t & 63;
+  const int t = threadIdx.x, r = t & 63, q = t >> 6;
   const int j = blockIdx.x * 256 + t;
   const bool upd = j < k0;
   double col[NB];
   if (upd) {
 #pragma unroll
-    for (int q = 0; q < NB / 2; ++q) {
-      const double2 v2 = *reinterpret_cast<const double2*>(A + size_t(j) * ld + k0 + 2 * q);
-      col[2 * q] = v2.x;
-      col[2 * q + 1] = v2.y;
+    for (int p = 0; p < NB / 2; ++p) {
+      const double2 v2 = *reinterpret_cast<const double2*>(A + size_t(j) * ld + k0 + 2 * p);
+      col[2 * p] = v2.x;
+      col[2 * p + 1] = v2.y;
     }
   }
-  {
-    double v[16];
+  // y_k[r] = sum_c W(c, r) z_k[c], W(c, r) = Wc[r][c]; quarter q sums c in [16q, 16q + 16)
+  const double* Wr = Winv + size_t(k) * NB * NB + size_t(r) * NB + 16 * q;
+  double wv[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, jj = e >> 6, r = e & 63;
-      v[q] = A[size_t(k0 + jj) * ld + k0 + r];
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, jj = e >> 6, r = e & 63;
-      Lt[r][jj] = (r >= jj) ? v[q] : 0.0;
-    }
+  for (int p = 0; p < 8; ++p) {
+    const double2 v2 = *reinterpret_cast<const double2*>(Wr + 2 * p);
+    wv[2 * p] = v2.x;
+    wv[2 * p + 1] = v2.y;
   }
+  if (t < NB) zk[t] = (t < nreal) ? z[k0 + t] : 0.0;
   __syncthreads();
-  if (t < 64) {
-    // lane r holds z_r; descending columns, y_j broadcast by readlane
-    double v = (lane < nreal) ? z[k0 + lane] * invd[k0 + lane] : 0.0;
-    const double idl = (lane < nreal) ? invd[k0 + lane] : 0.0;
+  double s = 0.0;
 #pragma unroll
-    for (int jj = NB - 1; jj >= 0; --jj) {
-      if (jj < nreal) {
-        const double yj = bcast(v, jj);
-        if (lane < jj) v = fma(-Lt[jj][lane] * idl, yj, v);
-      }
-    }
-    if (lane >= nreal) v = 0.0;
-    yk[lane] = v;
-    if (blockIdx.x == 0 && lane < nreal) y[k0 + lane] = v;
+  for (int p = 0; p < 16; ++p) s = fma(wv[p], zk[16 * q + p], s);
+  part[q][r] = s;
+  __syncthreads();
+  if (t < NB) {
+    const double v = (t < nreal) ? (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]) : 0.0;
+    yk[t] = v;
+    if (blockIdx.x == 0 && t < nreal) y[k0 + t] = v;
   }
   __syncthreads();
   if (upd) {
-    double s = 0.0;
+    double acc = 0.0;
 #pragma unroll
-    for (int r = 0; r < NB; ++r) s += col[r] * yk[r];
-    z[j] -= s;
+    for (int rr = 0; rr < NB; ++rr) acc = fma(col[rr], yk[rr], acc);
+    z[j] -= acc;
   }
 }
 
@@ -271,10 +301,10 @@ __global__ __launch_bounds__(256) void k_backsolve_step(const double* __restrict
 void launch_cholesky(const DevProblem& d, hipStream_t s) {
   (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   for (int k = 0; k < d.nblk; ++k) {
-    k_chol_potrf<<<1, 64, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
+    k_chol_potrf<<<1, 128, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
     const int m = d.nblk - k - 1;
     if (m == 0) break;
-    k_chol_trsm<<<(m + 3) / 4, 256, 0, s>>>(d.S, d.ld, k, m, d.invL);
+    k_chol_trsm<<<m, 256, 0, s>>>(d.S, d.ld, k, d.invL);
     k_chol_syrk<<<m * (m + 1) / 2, 256, 0, s>>>(d.S, d.ld, k);
   }
 }

@@ -1,5 +1,5 @@
 import sys, numpy as np
-sys.path.insert(0, '.')
+import os; sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sfm_amd.ba import dense_spd_solve
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
 rng = np.random.default_rng(0)
