@@ -36,9 +36,9 @@ SEED = 0x5F3D2017 + 3      # config C3
 
 
 def jacobian_bytes(n_obs: int, n_cams: int, n_pts: int) -> int:
-    # uv 16 + cam/pt index 8 + r 16 + J 144 per observation,
-    # pose 48 + K 40 per camera, X 24 per point.
-    return 184 * n_obs + 88 * n_cams + 24 * n_pts
+    # per observation: camera-major index record 16 + uv 16 + r 16 + J 144
+    # (k_jacobian); per camera: pose 48 + K 40; per point: X 24.
+    return 192 * n_obs + 88 * n_cams + 24 * n_pts
 
 
 def cholesky_flops(n: int) -> float:

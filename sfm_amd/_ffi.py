@@ -13,7 +13,7 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsfm_amd.so")
+LIB_PATH = os.environ.get("SFM_AMD_LIB") or os.path.join(_HERE, "libsfm_amd.so")
 
 
 class SfmError(RuntimeError):

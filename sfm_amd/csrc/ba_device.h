@@ -25,6 +25,9 @@ constexpr int kPtV = 10;
 constexpr int kPtL = 10;
 // Cholesky tile size.
 constexpr int kNB = 64;
+// Schur LDS strip: 6x6 block per column camera at an odd stride (37 doubles)
+// so the ds_add_f64 of lanes on different blocks spread over the 64 banks.
+constexpr int kBlkStride = 37;
 
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
@@ -54,6 +57,12 @@ struct DevProblem {
   int32_t* pt_off = nullptr;   // [P+1]
   int32_t* cam_obs = nullptr;  // [N] observation ids grouped by camera
   int32_t* cam_off = nullptr;  // [C+1]
+  int32_t* cm_p = nullptr;     // [N] point index at camera-major position i
+  int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
+  int32_t n_jchunks = 0;
+  int32_t jac_blocks = 1;      // persistent grid of k_jacobian (cost partials)
+  double* uv_cm = nullptr;     // [N][2] uv in camera-major order
+  int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q (jrec index)
   double* Kc = nullptr;        // [C][5] fx skew cx fy cy
   // parameters (current and candidate)
   double* cam = nullptr;      // [C][6] rot(3) t(3)
@@ -70,7 +79,7 @@ struct DevProblem {
   // per-iteration work arrays
   double* camR = nullptr;     // [C][36]
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
-  double* jrec = nullptr;     // [N][20]
+  double* jrec = nullptr;     // [N][20] at camera-major position (J_X 6 | r 2 | J_c 12)
   double* mrec = nullptr;     // [N][8]
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]

@@ -131,78 +131,141 @@ __global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __re
 }
 
 // ---------------------------------------------------------------------------
-// Residual + Jacobian, one lane per observation.  Per observation the pass
-// moves 184 B of algorithmic HBM traffic (uv 16, cam/pt index 8, record 160)
-// plus the per-camera (88 B) and per-point (24 B) parameter reads.  Records
-// are staged in LDS so the stores leave as fully coalesced 16-B lanes.
-constexpr int kStage = kJRec + 1;  // odd stride: conflict-light LDS staging
-__global__ __launch_bounds__(kThreads) void k_jacobian(int64_t N, const double* __restrict__ uv,
-                                                       const int32_t* __restrict__ obs_cam,
-                                                       const int32_t* __restrict__ obs_pt,
+// Residual + Jacobian in CAMERA-major order, the record stored at the
+// camera-major position i: every consumer that walks a camera's
+// observations (U_c, the Schur row) then streams, and the point-side
+// consumers reach a record through pos[q].
+// Work unit = one wavefront chunk: up to 64 consecutive observations of ONE
+// camera (host-built table, 63 chunks per camera at C3).  The camera is
+// wave-uniform, so its 44 doubles (R, dR/dw, t, K, Jacobi scale) are scalar
+// loads; per lane the pass moves the point index (4 B), uv (16 B), the point
+// X (24 B, a 4.8-MB L2/MALL-resident gather) and its 160-B record.  The
+// chunk's records are one contiguous run, written through a wave-local LDS
+// transpose as fully coalesced 1-KB rows (strided per-lane stores touch 80
+// cache lines per instruction and were store-issue bound).  The grid is
+// persistent (waves stride over the chunk table).  Algorithmic HBM traffic:
+// 180 B per observation (point index 4, uv 16, record 160) plus 88 B per
+// camera and 24 B per point.
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Store the wave's staged chunk (cnt records, contiguous from position ib)
+// as coalesced 1-KB rows.
+__device__ __forceinline__ void jac_flush(const double* wst, double* __restrict__ jrec, int64_t ib, int cnt, int l) {
+  double* dst = jrec + ib * kJRec;
+#pragma unroll
+  for (int kq = 0; kq < kJRec / 2; ++kq) {
+    const int e = 2 * (64 * kq + l);
+    if (e < cnt * kJRec) st2(dst + e, wst[e], wst[e + 1]);
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4* __restrict__ chunks,
+                                                       const int32_t* __restrict__ cm_p,
+                                                       const double* __restrict__ uv_cm,
                                                        const double* __restrict__ Kc, const double* __restrict__ cam,
                                                        const double* __restrict__ camR, const double* __restrict__ X,
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ scale_p, int scaled,
                                                        double* __restrict__ jrec, double* __restrict__ part_cost) {
-  __shared__ double stage[kThreads * kStage];
   __shared__ double sh[4];
-  const int64_t base = int64_t(blockIdx.x) * kThreads;
-  const int64_t o = base + threadIdx.x;
+  __shared__ __attribute__((aligned(16))) double stage[kThreads * kJRec];  // 10 KB per wave
+  const int l = threadIdx.x & 63;
+  const int wv = wave_uniform(threadIdx.x >> 6);
+  double* wst = stage + wv * 64 * kJRec;
+  const int stride = gridDim.x * (kThreads / 64);
   double cost = 0.0;
-  if (o < N) {
-    const int c = obs_cam[o], p = obs_pt[o];
+  int t = blockIdx.x * (kThreads / 64) + wv;
+  // software pipeline: the next chunk's point index and uv are in flight
+  // while the current chunk computes, and the previous chunk's records
+  // leave while the current chunk's loads are outstanding
+  int p_cur = 0;
+  double2 uv_cur = make_double2(0.0, 0.0);
+  if (t < n_chunks) {
+    const int4 ch = chunks[t];
+    if (l < ch.z) { p_cur = cm_p[ch.y + l]; uv_cur = ld2(uv_cm + 2 * (int64_t(ch.y) + l)); }
+  }
+  int64_t prev_ib = 0;
+  int prev_cnt = 0;
+  for (; t < n_chunks; t += stride) {
+    const int4 ch = chunks[t];
+    const int c = ch.x, cnt = ch.z;
+    const int64_t ib = ch.y;
+    const bool act = l < cnt;
+    const int p = p_cur;
+    const double2 uvo = uv_cur;
+    double Xp[3] = {0.0, 0.0, 1.0};
+    double sp[3] = {1.0, 1.0, 1.0};
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Xp[j] = X[3 * size_t(p) + j];
+      if (scaled)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) sp[j] = scale_p[3 * size_t(p) + j];
+    }
+    const int tn = t + stride;
+    if (tn < n_chunks) {
+      const int4 cn = chunks[tn];
+      if (l < cn.z) { p_cur = cm_p[cn.y + l]; uv_cur = ld2(uv_cm + 2 * (int64_t(cn.y) + l)); }
+    }
+    if (prev_cnt) {
+      jac_flush(wst, jrec, prev_ib, prev_cnt, l);
+      wave_lds_sync();
+    }
+    // camera data (wave-uniform -> scalar loads)
     const double* cr = camR + size_t(kCamR) * c;
-    const double2 uvo = ld2(uv + 2 * o);
-    const double Xp[3] = {X[3 * size_t(p)], X[3 * size_t(p) + 1], X[3 * size_t(p) + 2]};
     const double* k = Kc + 5 * size_t(c);
     const double fx = k[0], sk = k[1], cx = k[2], fy = k[3], cy = k[4];
-    double pc[3];
+    double sc[6];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      pc[i] = cr[3 * i] * Xp[0] + cr[3 * i + 1] * Xp[1] + cr[3 * i + 2] * Xp[2] + cam[6 * c + 3 + i];
-    const double xp = pc[0] / pc[2], yp = pc[1] / pc[2];
-    const double r0 = fx * xp + sk * yp + cx - uvo.x;
-    const double r1 = fy * yp + cy - uvo.y;
-    const double iz = 1.0 / pc[2];
-    // d r / d pc
-    const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
-    const double b1 = fy * iz, b2 = -fy * yp * iz;
-    double* st = stage + threadIdx.x * kStage;
-    // J_X = dr/dpc * R
+    for (int a = 0; a < 6; ++a) sc[a] = scaled ? scale_c[6 * size_t(c) + a] : 1.0;
+    if (act) {
+      const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + cam[6 * c + 3];
+      const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + cam[6 * c + 4];
+      const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + cam[6 * c + 5];
+      const double xp = pc0 / pc2, yp = pc1 / pc2;
+      const double r0 = fx * xp + sk * yp + cx - uvo.x;
+      const double r1 = fy * yp + cy - uvo.y;
+      const double iz = 1.0 / pc2;
+      // d r / d pc
+      const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+      const double b1 = fy * iz, b2 = -fy * yp * iz;
+      double rec[kJRec];
+      // J_X = dr/dpc * R
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double sj = scaled ? scale_p[3 * size_t(p) + j] : 1.0;
-      st[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sj;
-      st[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sj;
+      for (int j = 0; j < 3; ++j) {
+        rec[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
+        rec[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
+      }
+      rec[kRes] = r0;
+      rec[kRes + 1] = r1;
+      // J_w[:,k] = dr/dpc * (dR_k X);  J_t = dr/dpc
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) {
+        const double* D = cr + 9 + 9 * kk;
+        const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+        const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+        const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+        rec[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
+        rec[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
+      }
+      rec[kJC + 3] = a0 * sc[3]; rec[kJC + 4] = a1 * sc[4]; rec[kJC + 5] = a2 * sc[5];
+      rec[kJC + 9] = 0.0;        rec[kJC + 10] = b1 * sc[4]; rec[kJC + 11] = b2 * sc[5];
+      double* mine = wst + l * kJRec;
+#pragma unroll
+      for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
+      cost += 0.5 * (r0 * r0 + r1 * r1);
     }
-    st[kRes] = r0;
-    st[kRes + 1] = r1;
-    // J_w[:,k] = dr/dpc * (dR_k X);  J_t = dr/dpc
-#pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-      const double* D = cr + 9 + 9 * kk;
-      const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
-      const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
-      const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
-      const double sk_ = scaled ? scale_c[6 * size_t(c) + kk] : 1.0;
-      st[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sk_;
-      st[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sk_;
-    }
-    const double st0 = scaled ? scale_c[6 * size_t(c) + 3] : 1.0;
-    const double st1 = scaled ? scale_c[6 * size_t(c) + 4] : 1.0;
-    const double st2_ = scaled ? scale_c[6 * size_t(c) + 5] : 1.0;
-    st[kJC + 3] = a0 * st0; st[kJC + 4] = a1 * st1; st[kJC + 5] = a2 * st2_;
-    st[kJC + 9] = 0.0;      st[kJC + 10] = b1 * st1; st[kJC + 11] = b2 * st2_;
-    cost = 0.5 * (r0 * r0 + r1 * r1);
+    wave_lds_sync();
+    prev_ib = ib;
+    prev_cnt = cnt;
   }
-  __syncthreads();
-  const int64_t nrec = (N - base) < kThreads ? (N - base) : kThreads;
-  double* dst = jrec + base * kJRec;
-  const int npairs = int(nrec) * (kJRec / 2);
-  for (int e = threadIdx.x; e < npairs; e += kThreads) {
-    const int t = e / (kJRec / 2), f = 2 * (e - t * (kJRec / 2));
-    st2(dst + 2 * e, stage[t * kStage + f], stage[t * kStage + f + 1]);
-  }
+  if (prev_cnt) jac_flush(wst, jrec, prev_ib, prev_cnt, l);
   const double r = block_reduce(cost, sh, false);
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
 }
@@ -211,7 +274,6 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(int64_t N, const double* 
 // Per-camera normal-equation block U_c = sum J_c^T J_c and b_c = sum J_c^T r,
 // one workgroup per camera, fixed-order reduction.
 __global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_off,
-                                                         const int32_t* __restrict__ cam_obs,
                                                          const double* __restrict__ jrec, double* __restrict__ Ucam) {
   __shared__ double sh[4 * 27];
   const int c = blockIdx.x;
@@ -220,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restri
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   const int i0 = cam_off[c], i1 = cam_off[c + 1];
   for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
-    const double* J = jrec + size_t(cam_obs[i]) * kJRec;
+    const double* J = jrec + size_t(i) * kJRec;  // camera-major records: a contiguous stream
     const double2 rr = ld2(J + kRes);
     double j0[6], j1[6];
 #pragma unroll
@@ -279,6 +341,7 @@ __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* 
 // mode 0: Jacobi scale of the point columns; mode 1: V_p, b_p, LM diagonal,
 // gradient max-norm and |X|^2.
 __global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* __restrict__ pt_off,
+                                                         const int32_t* __restrict__ pos,
                                                          const double* __restrict__ jrec, const double* __restrict__ X,
                                                          double* __restrict__ scale_p, double* __restrict__ diag_p,
                                                          double* __restrict__ ptV, double min_diag, double max_diag,
@@ -291,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* _
     double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      const double* J = jrec + size_t(q) * kJRec;
+      const double* J = jrec + size_t(pos[q]) * kJRec;
       const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4), rr = ld2(J + kRes);
       const double u0 = e0.x, u1 = e0.y, u2 = e1.x, v0 = e1.y, v1 = e2.x, v2 = e2.y;
       V[0] += u0 * u0 + v0 * v0;
@@ -324,6 +387,7 @@ __global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* _
 // V_p + D_p^2 = L L^T, z = L^-1 b_p, and per observation M = J_X L^-T,
 // h = M z (the ingredients of W V^-1 W^T and W V^-1 b).
 __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* __restrict__ pt_off,
+                                                         const int32_t* __restrict__ pos,
                                                          const double* __restrict__ jrec, const double* __restrict__ ptV,
                                                          const double* __restrict__ diag_p, double radius,
                                                          double* __restrict__ mrec, double* __restrict__ ptL,
@@ -347,7 +411,7 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
     st2(L, l00, l10); st2(L + 2, l11, l20); st2(L + 4, l21, l22); st2(L + 6, z0, z1); st2(L + 8, z2, 0.0);
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      const double* J = jrec + size_t(q) * kJRec;
+      const double* J = jrec + size_t(pos[q]) * kJRec;
       const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
       const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
       const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
@@ -375,14 +439,15 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
 __global__ __launch_bounds__(kThreads) void k_schur(
     const int32_t* __restrict__ tasks, const int32_t* __restrict__ cam_off, const int32_t* __restrict__ cam_obs,
     const int32_t* __restrict__ obs_pt, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pt_off,
-    const double* __restrict__ jrec, const double* __restrict__ mrec, const double* __restrict__ Ucam,
+    const int32_t* __restrict__ pos, const double* __restrict__ jrec, const double* __restrict__ mrec,
+    const double* __restrict__ Ucam,
     const double* __restrict__ diag_c, double radius, int add_diag, double* __restrict__ S, int ld, int n) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int c1 = tasks[3 * blockIdx.x], a = tasks[3 * blockIdx.x + 1], b = tasks[3 * blockIdx.x + 2];
   const int ncol = b - a;
   double* acc = smem;
-  double* red = smem + ncol * 36;  // 4 waves x 6
-  for (int i = threadIdx.x; i < ncol * 36; i += kThreads) acc[i] = 0.0;
+  double* red = smem + ncol * kBlkStride;  // 4 waves x 6
+  for (int i = threadIdx.x; i < ncol * kBlkStride; i += kThreads) acc[i] = 0.0;
   __syncthreads();
   const int lo = a > c1 ? a : c1;
   const bool own = (a <= c1) && (c1 < b);
@@ -391,7 +456,7 @@ __global__ __launch_bounds__(kThreads) void k_schur(
   for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
     const int o1 = cam_obs[i];
     const int p = obs_pt[o1];
-    const double* J1p = jrec + size_t(o1) * kJRec;
+    const double* J1p = jrec + size_t(i) * kJRec;  // camera-major record: streamed
     const double* M1p = mrec + size_t(o1) * kMRec;
     double J1[12], M1[6];
 #pragma unroll
@@ -409,7 +474,7 @@ __global__ __launch_bounds__(kThreads) void k_schur(
       const int c2 = obs_cam[o2];
       if (c2 < lo) continue;
       if (c2 >= b) break;
-      const double* J2p = jrec + size_t(o2) * kJRec + kJC;
+      const double* J2p = jrec + size_t(pos[o2]) * kJRec + kJC;
       const double* M2p = mrec + size_t(o2) * kMRec;
       double J2[12], M2[6];
 #pragma unroll
@@ -420,7 +485,7 @@ __global__ __launch_bounds__(kThreads) void k_schur(
       const double G01 = M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5];
       const double G10 = M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2];
       const double G11 = M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5];
-      double* blk = acc + (c2 - a) * 36;
+      double* blk = acc + (c2 - a) * kBlkStride;
 #pragma unroll
       for (int u = 0; u < 6; ++u) {
         const double H0 = J1[u] * G00 + J1[6 + u] * G10;
@@ -436,7 +501,7 @@ __global__ __launch_bounds__(kThreads) void k_schur(
   for (int e = threadIdx.x; e < 6 * W; e += kThreads) {
     const int u = e / W, col = e - u * W;
     const int cb = col / 6, v = col - 6 * cb;
-    double val = -acc[cb * 36 + 6 * u + v];
+    double val = -acc[cb * kBlkStride + 6 * u + v];
     if (add_diag && a + cb == c1) {
       val += U[up6(u, v)];
       if (u == v) { const double d = sqrt(diag_c[6 * size_t(c1) + u] / radius); val += d * d; }
@@ -503,7 +568,8 @@ __global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __
 //   model cost change -= q . (r + q/2)   (ceres trust_region_minimizer),
 //   candidate residual at (cam_new, X + s*delta_p).
 __global__ __launch_bounds__(kThreads) void k_point_backsub(
-    int P, const int32_t* __restrict__ pt_off, const int32_t* __restrict__ obs_cam, const double* __restrict__ uv,
+    int P, const int32_t* __restrict__ pt_off, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pos,
+    const double* __restrict__ uv,
     const double* __restrict__ Kc, const double* __restrict__ jrec, const double* __restrict__ mrec,
     const double* __restrict__ ptL, const double* __restrict__ ysol, const double* __restrict__ scale_p,
     const double* __restrict__ X, double* __restrict__ X_new, const double* __restrict__ camRn,
@@ -519,7 +585,7 @@ __global__ __launch_bounds__(kThreads) void k_point_backsub(
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
       const int c = obs_cam[q];
-      const double* J = jrec + size_t(q) * kJRec + kJC;
+      const double* J = jrec + size_t(pos[q]) * kJRec + kJC;
       const double* M = mrec + size_t(q) * kMRec;
       const double* y = ysol + 6 * size_t(c);
       double e0 = 0.0, e1 = 0.0;
@@ -544,7 +610,7 @@ __global__ __launch_bounds__(kThreads) void k_point_backsub(
     }
     for (int q = q0; q < q1; ++q) {
       const int c = obs_cam[q];
-      const double* Jr = jrec + size_t(q) * kJRec;
+      const double* Jr = jrec + size_t(pos[q]) * kJRec;
       const double* y = ysol + 6 * size_t(c);
       double e0 = 0.0, e1 = 0.0;
 #pragma unroll
@@ -603,13 +669,11 @@ void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hi
   k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
-  if (d.N == 0) return;
-  k_jacobian<<<blocks_for(d.N, kThreads), kThreads, 0, s>>>(d.N, d.uv, d.obs_cam, d.obs_pt, d.Kc, d.cam, d.camR, d.X,
-                                                           d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
-                                                           slot(d, kPCost));
+  k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.n_jchunks, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
+                                                d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost));
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
-  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_off, d.cam_obs, d.jrec, d.Ucam);
+  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_off, d.jrec, d.Ucam);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, 1e-6, 1e32, mode,
@@ -618,18 +682,18 @@ void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool co
 }
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
   if (d.P == 0) return;
-  k_point_eval<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.jrec, d.X, d.scale_p, d.diag_p, d.ptV,
+  k_point_eval<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.X, d.scale_p, d.diag_p, d.ptV,
                                                              1e-6, 1e32, mode, reuse_diag ? 1 : 0,
                                                              slot(d, kPGradPt), slot(d, kPXNormPt));
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P == 0) return;
-  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.jrec, d.ptV, d.diag_p, radius, d.mrec,
+  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.ptV, d.diag_p, radius, d.mrec,
                                                              d.ptL, slot(d, kPBad));
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
-  const size_t lds = (size_t(d.tile_cams) * 36 + 32) * sizeof(double);
-  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_off, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.jrec,
+  const size_t lds = (size_t(d.tile_cams) * kBlkStride + 32) * sizeof(double);
+  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_off, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.pos, d.jrec,
                                            d.mrec, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld, d.n);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }
@@ -641,7 +705,7 @@ void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
 void launch_point_backsub(const DevProblem& d, hipStream_t s) {
   if (d.P == 0) return;
   k_point_backsub<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(
-      d.P, d.pt_off, d.obs_cam, d.uv, d.Kc, d.jrec, d.mrec, d.ptL, d.ysol, d.scale_p, d.X, d.X_new, d.camRn,
+      d.P, d.pt_off, d.obs_cam, d.pos, d.uv, d.Kc, d.jrec, d.mrec, d.ptL, d.ysol, d.scale_p, d.X, d.X_new, d.camRn,
       slot(d, kPModel), slot(d, kPNewCost), slot(d, kPStepPt), slot(d, kPBadBack));
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {

@@ -54,6 +54,7 @@ struct sfm_ba_handle {
   DevProblem d;
   // host copies needed for reordering / reset
   std::vector<int64_t> order;  // sorted position -> caller observation index
+  std::vector<int32_t> pos;      // point-major q -> camera-major record index
   std::vector<void*> allocs;
   bool has_problem = false;
   // multi-GPU
@@ -161,14 +162,14 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   mark_begin(h, kPhPtEval);
   launch_point_eval(d, 1, false, s);
   mark_end(h);
-  const int nbN = std::max(1, blocks_for(d.N, 256)), nbP = std::max(1, blocks_for(d.P, 256)),
+  const int nbP = std::max(1, blocks_for(d.P, 256)),
             nbC = std::max(1, blocks_for(d.C, 256));
   if (d.N == 0) hipMemsetAsync(d.partials + size_t(kPCost) * d.max_blocks, 0, sizeof(double), s);
   if (d.P == 0) {
     hipMemsetAsync(d.partials + size_t(kPGradPt) * d.max_blocks, 0, sizeof(double), s);
     hipMemsetAsync(d.partials + size_t(kPXNormPt) * d.max_blocks, 0, sizeof(double), s);
   }
-  launch_reduce(d, kPCost, nbN, 0, kCost, s);
+  launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, s);
   launch_reduce(d, kPGradCam, nbC, 1, kGradMaxCam, s);
   launch_reduce(d, kPGradPt, nbP, 1, kGradMaxPt, s);
   launch_reduce(d, kPXNormCam, nbC, 0, kXNorm2Cam, s);
@@ -358,6 +359,34 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     std::vector<int32_t> fill(cam_off.begin(), cam_off.end() - 1);
     for (int64_t q = 0; q < N; ++q) cam_obs[fill[cam_s[q]]++] = int32_t(q);
   }
+  // camera-major copies for the Jacobian pass (k_jacobian) and the record map
+  std::vector<int32_t> cm_p(N), pos(N);
+  // (camera, first position, count, 0) per wavefront chunk, issued
+  // piece-major: a camera's list is sorted by point, so piece k of every
+  // camera covers about the same slice of the points and the waves in
+  // flight gather X from a narrow, L2-resident range.
+  std::vector<int32_t> jchunks;
+  for (int32_t k = 0;; ++k) {
+    bool any = false;
+    for (int c = 0; c < C; ++c) {
+      const int32_t i = cam_off[c] + 64 * k;
+      if (i >= cam_off[c + 1]) continue;
+      any = true;
+      jchunks.insert(jchunks.end(), {c, i, std::min<int32_t>(64, cam_off[c + 1] - i), 0});
+    }
+    if (!any) break;
+  }
+  d.n_jchunks = int32_t(jchunks.size() / 4);
+  d.jac_blocks = std::max(1, std::min((d.n_jchunks + 3) / 4, 1024));
+  std::vector<double> uv_cm(2 * size_t(N));
+  for (int c = 0; c < C; ++c)
+    for (int32_t i = cam_off[c]; i < cam_off[c + 1]; ++i) {
+      const int32_t q = cam_obs[i];
+      cm_p[i] = pt_s[q];
+      pos[q] = i;
+      uv_cm[2 * size_t(i)] = uv_s[2 * size_t(q)];
+      uv_cm[2 * size_t(i) + 1] = uv_s[2 * size_t(q) + 1];
+    }
   std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
   for (int c = 0; c < C; ++c) {
     const double* k = K9 + 9 * size_t(c);
@@ -365,7 +394,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
   }
   // ---- Schur tasks: (row camera, column range) within the LDS budget ----
-  d.tile_cams = std::max(1, std::min(C, 220));  // (220*36+32)*8 B <= 64 KiB dynamic LDS
+  d.tile_cams = std::max(1, std::min(C, 200));  // (200*37+32)*8 B <= 64 KiB dynamic LDS
   std::vector<std::array<int32_t, 3>> tasks;
   std::vector<int64_t> work;
   for (int c1 = 0; c1 < C; ++c1)
@@ -385,7 +414,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n = 6 * C;
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
   d.nblk = d.ld / kNB;
-  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256)});
+  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks});
   // ---- device allocation ----
   int rc = 0;
 #define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) { free_problem(h); return rc; }
@@ -395,6 +424,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.pt_off, size_t(P) + 1);
   ALLOC(d.cam_obs, size_t(N));
   ALLOC(d.cam_off, size_t(C) + 1);
+  ALLOC(d.cm_p, size_t(N));
+  ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
+  ALLOC(d.uv_cm, 2 * size_t(N));
+  ALLOC(d.pos, size_t(N));
   ALLOC(d.Kc, 5 * size_t(C));
   ALLOC(d.cam, 6 * size_t(C));
   ALLOC(d.cam_new, 6 * size_t(C));
@@ -433,6 +466,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     H2D(d.obs_cam, cam_s.data(), size_t(N));
     H2D(d.obs_pt, pt_s.data(), size_t(N));
     H2D(d.cam_obs, cam_obs.data(), size_t(N));
+    H2D(d.cm_p, cm_p.data(), size_t(N));
+    HIPCHK(hipMemcpyAsync(d.jchunks, jchunks.data(), sizeof(int32_t) * jchunks.size(), hipMemcpyHostToDevice, s));
+    H2D(d.uv_cm, uv_cm.data(), 2 * size_t(N));
+    H2D(d.pos, pos.data(), size_t(N));
+    h->pos = pos;
   }
   H2D(d.pt_off, pt_off.data(), size_t(P) + 1);
   H2D(d.cam_off, cam_off.data(), size_t(C) + 1);
@@ -683,7 +721,7 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   launch_cam_prep(d, d.cam, false, h->stream);
   launch_jacobian(d, false, h->stream);
   if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
-  launch_reduce(d, kPCost, std::max(1, blocks_for(d.N, 256)), 0, kCost, h->stream);
+  launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, h->stream);
   std::vector<double> rec(size_t(kJRec) * d.N);
   if (d.N)
     HIPCHK(hipMemcpyAsync(rec.data(), d.jrec, sizeof(double) * rec.size(), hipMemcpyDeviceToHost, h->stream));
@@ -693,7 +731,7 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   if (cost) *cost = c;
   for (int64_t q = 0; q < d.N; ++q) {
     const int64_t i = h->order[q];
-    const double* r = &rec[size_t(kJRec) * q];
+    const double* r = &rec[size_t(kJRec) * h->pos[q]];
     if (res) { res[2 * i] = r[kRes]; res[2 * i + 1] = r[kRes + 1]; }
     if (jac) {
       double* J = jac + 18 * i;
