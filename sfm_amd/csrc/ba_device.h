@@ -55,13 +55,14 @@ struct DevProblem {
   int32_t* obs_cam = nullptr;  // [N]
   int32_t* obs_pt = nullptr;   // [N]
   int32_t* pt_off = nullptr;   // [P+1]
-  int32_t* cam_obs = nullptr;  // [N] observation ids grouped by camera
-  int32_t* cam_off = nullptr;  // [C+1]
-  int32_t* cm_p = nullptr;     // [N] point index at camera-major position i
+  int64_t N_pad = 0;           // camera-major positions incl. per-camera padding to 64
+  int32_t* cam_obs = nullptr;  // [N_pad] point-major observation id at camera-major position (-1: padding)
+  int32_t* cam_rng = nullptr;  // [C][2] camera c's records: positions [begin, end)
+  int32_t* cm_p = nullptr;     // [N_pad] point index at camera-major position i
   int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
   int32_t n_jchunks = 0;
   int32_t jac_blocks = 1;      // persistent grid of k_jacobian (cost partials)
-  double* uv_cm = nullptr;     // [N][2] uv in camera-major order
+  double* uv_cm = nullptr;     // [N_pad][2] uv in camera-major order
   int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q (jrec index)
   double* Kc = nullptr;        // [C][5] fx skew cx fy cy
   // parameters (current and candidate)
@@ -79,7 +80,7 @@ struct DevProblem {
   // per-iteration work arrays
   double* camR = nullptr;     // [C][36]
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
-  double* jrec = nullptr;     // [N][20] at camera-major position (J_X 6 | r 2 | J_c 12)
+  double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12)
   double* mrec = nullptr;     // [N][8]
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]

@@ -148,15 +148,15 @@ __global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __re
 // camera and 24 B per point.
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Store the wave's staged chunk (cnt records, contiguous from position ib)
-// as coalesced 1-KB rows.
-__device__ __forceinline__ void jac_flush(const double* wst, double* __restrict__ jrec, int64_t ib, int cnt, int l) {
+// Store the wave's staged chunk (64 records from position ib; a camera's
+// run is padded to whole chunks) as ten coalesced 1-KB rows.
+__device__ __forceinline__ void jac_flush(const double* wst, double* __restrict__ jrec, int64_t ib, int l) {
   double* dst = jrec + ib * kJRec;
+  double2 v[kJRec / 2];
 #pragma unroll
-  for (int kq = 0; kq < kJRec / 2; ++kq) {
-    const int e = 2 * (64 * kq + l);
-    if (e < cnt * kJRec) st2(dst + e, wst[e], wst[e + 1]);
-  }
+  for (int kq = 0; kq < kJRec / 2; ++kq) v[kq] = ld2(wst + 2 * (64 * kq + l));
+#pragma unroll
+  for (int kq = 0; kq < kJRec / 2; ++kq) *reinterpret_cast<double2*>(dst + 2 * (64 * kq + l)) = v[kq];
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -165,6 +165,47 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One observation's residual and 2x9 Jacobian record (layout kJX|kRes|kJC).
+__device__ __forceinline__ double jac_record(const double* cr, double tc0, double tc1, double tc2, double fx, double sk,
+                                             double cx, double fy, double cy, const double* sc, const double* sp,
+                                             const double Xp[3], double2 uvo, double rec[kJRec]) {
+  const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc0;
+  const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc1;
+  const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc2;
+  const double xp = pc0 / pc2, yp = pc1 / pc2;
+  const double r0 = fx * xp + sk * yp + cx - uvo.x;
+  const double r1 = fy * yp + cy - uvo.y;
+  const double iz = 1.0 / pc2;
+  // d r / d pc
+  const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+  const double b1 = fy * iz, b2 = -fy * yp * iz;
+  // J_X = dr/dpc * R
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    rec[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
+    rec[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
+  }
+  rec[kRes] = r0;
+  rec[kRes + 1] = r1;
+  // J_w[:,k] = dr/dpc * (dR_k X);  J_t = dr/dpc
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const double* D = cr + 9 + 9 * kk;
+    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+    rec[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
+    rec[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
+  }
+  rec[kJC + 3] = a0 * sc[3]; rec[kJC + 4] = a1 * sc[4]; rec[kJC + 5] = a2 * sc[5];
+  rec[kJC + 9] = 0.0;        rec[kJC + 10] = b1 * sc[4]; rec[kJC + 11] = b2 * sc[5];
+  return 0.5 * (r0 * r0 + r1 * r1);
+}
+
+// Pipeline per wave, chunk t (vmcnt is one in-order counter for loads AND
+// stores on CDNA, so a wait on a load also covers every older store):
+//   [X_t, uv_t in flight] issue p_{t+1}, uv_{t+1} -> wait X_t -> compute t
+//   -> stage t in LDS -> issue X_{t+1} -> store chunk t.
 __global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4* __restrict__ chunks,
                                                        const int32_t* __restrict__ cm_p,
                                                        const double* __restrict__ uv_cm,
@@ -181,91 +222,63 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4*
   const int stride = gridDim.x * (kThreads / 64);
   double cost = 0.0;
   int t = blockIdx.x * (kThreads / 64) + wv;
-  // software pipeline: the next chunk's point index and uv are in flight
-  // while the current chunk computes, and the previous chunk's records
-  // leave while the current chunk's loads are outstanding
+  // Lanes past the real observations of a camera's last chunk compute the
+  // padding slots (copies of its last observation): every load and store is
+  // unpredicated, so nothing forces an early wait; padding records are never
+  // read back and their cost is masked.
+  // prologue: p_t, uv_t, then X_t / scale_p_t in flight
   int p_cur = 0;
   double2 uv_cur = make_double2(0.0, 0.0);
+  double Xc[3] = {0.0, 0.0, 1.0}, spc[3] = {1.0, 1.0, 1.0};
   if (t < n_chunks) {
     const int4 ch = chunks[t];
-    if (l < ch.z) { p_cur = cm_p[ch.y + l]; uv_cur = ld2(uv_cm + 2 * (int64_t(ch.y) + l)); }
+    const int64_t i = int64_t(ch.y) + l;
+    p_cur = cm_p[i];
+    uv_cur = ld2(uv_cm + 2 * i);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p_cur) + j];
+    if (scaled)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) spc[j] = scale_p[3 * size_t(p_cur) + j];
   }
-  int64_t prev_ib = 0;
-  int prev_cnt = 0;
   for (; t < n_chunks; t += stride) {
     const int4 ch = chunks[t];
     const int c = ch.x, cnt = ch.z;
     const int64_t ib = ch.y;
-    const bool act = l < cnt;
-    const int p = p_cur;
-    const double2 uvo = uv_cur;
-    double Xp[3] = {0.0, 0.0, 1.0};
-    double sp[3] = {1.0, 1.0, 1.0};
-    if (act) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Xp[j] = X[3 * size_t(p) + j];
-      if (scaled)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) sp[j] = scale_p[3 * size_t(p) + j];
-    }
+    // next chunk's index + uv
     const int tn = t + stride;
-    if (tn < n_chunks) {
-      const int4 cn = chunks[tn];
-      if (l < cn.z) { p_cur = cm_p[cn.y + l]; uv_cur = ld2(uv_cm + 2 * (int64_t(cn.y) + l)); }
-    }
-    if (prev_cnt) {
-      jac_flush(wst, jrec, prev_ib, prev_cnt, l);
-      wave_lds_sync();
-    }
+    const bool has_next = tn < n_chunks;
+    const int4 cn = chunks[has_next ? tn : t];
+    const int64_t inx = int64_t(cn.y) + l;
+    const int p_nxt = cm_p[inx];
+    const double2 uv_nxt = ld2(uv_cm + 2 * inx);
     // camera data (wave-uniform -> scalar loads)
     const double* cr = camR + size_t(kCamR) * c;
     const double* k = Kc + 5 * size_t(c);
-    const double fx = k[0], sk = k[1], cx = k[2], fy = k[3], cy = k[4];
     double sc[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) sc[a] = scaled ? scale_c[6 * size_t(c) + a] : 1.0;
-    if (act) {
-      const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + cam[6 * c + 3];
-      const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + cam[6 * c + 4];
-      const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + cam[6 * c + 5];
-      const double xp = pc0 / pc2, yp = pc1 / pc2;
-      const double r0 = fx * xp + sk * yp + cx - uvo.x;
-      const double r1 = fy * yp + cy - uvo.y;
-      const double iz = 1.0 / pc2;
-      // d r / d pc
-      const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
-      const double b1 = fy * iz, b2 = -fy * yp * iz;
+    {
       double rec[kJRec];
-      // J_X = dr/dpc * R
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        rec[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
-        rec[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
-      }
-      rec[kRes] = r0;
-      rec[kRes + 1] = r1;
-      // J_w[:,k] = dr/dpc * (dR_k X);  J_t = dr/dpc
-#pragma unroll
-      for (int kk = 0; kk < 3; ++kk) {
-        const double* D = cr + 9 + 9 * kk;
-        const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
-        const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
-        const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
-        rec[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
-        rec[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
-      }
-      rec[kJC + 3] = a0 * sc[3]; rec[kJC + 4] = a1 * sc[4]; rec[kJC + 5] = a2 * sc[5];
-      rec[kJC + 9] = 0.0;        rec[kJC + 10] = b1 * sc[4]; rec[kJC + 11] = b2 * sc[5];
+      const double cl = jac_record(cr, cam[6 * c + 3], cam[6 * c + 4], cam[6 * c + 5], k[0], k[1], k[2], k[3], k[4],
+                                   sc, spc, Xc, uv_cur, rec);
+      cost += (l < cnt) ? cl : 0.0;
       double* mine = wst + l * kJRec;
 #pragma unroll
       for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
-      cost += 0.5 * (r0 * r0 + r1 * r1);
     }
     wave_lds_sync();
-    prev_ib = ib;
-    prev_cnt = cnt;
+    // next chunk's point data
+    p_cur = p_nxt;
+    uv_cur = uv_nxt;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p_cur) + j];
+    if (scaled)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) spc[j] = scale_p[3 * size_t(p_cur) + j];
+    jac_flush(wst, jrec, ib, l);
+    wave_lds_sync();
   }
-  if (prev_cnt) jac_flush(wst, jrec, prev_ib, prev_cnt, l);
   const double r = block_reduce(cost, sh, false);
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
 }
@@ -273,14 +286,14 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4*
 // ---------------------------------------------------------------------------
 // Per-camera normal-equation block U_c = sum J_c^T J_c and b_c = sum J_c^T r,
 // one workgroup per camera, fixed-order reduction.
-__global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_off,
+__global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_rng,
                                                          const double* __restrict__ jrec, double* __restrict__ Ucam) {
   __shared__ double sh[4 * 27];
   const int c = blockIdx.x;
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-  const int i0 = cam_off[c], i1 = cam_off[c + 1];
+  const int i0 = cam_rng[2 * c], i1 = cam_rng[2 * c + 1];
   for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
     const double* J = jrec + size_t(i) * kJRec;  // camera-major records: a contiguous stream
     const double2 rr = ld2(J + kRes);
@@ -437,7 +450,7 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
 //   rhs_c1 = sum_{o in c1} J_c^T (r_o - h_o)
 // into the augmented column n.
 __global__ __launch_bounds__(kThreads) void k_schur(
-    const int32_t* __restrict__ tasks, const int32_t* __restrict__ cam_off, const int32_t* __restrict__ cam_obs,
+    const int32_t* __restrict__ tasks, const int32_t* __restrict__ cam_rng, const int32_t* __restrict__ cam_obs,
     const int32_t* __restrict__ obs_pt, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pt_off,
     const int32_t* __restrict__ pos, const double* __restrict__ jrec, const double* __restrict__ mrec,
     const double* __restrict__ Ucam,
@@ -452,7 +465,7 @@ __global__ __launch_bounds__(kThreads) void k_schur(
   const int lo = a > c1 ? a : c1;
   const bool own = (a <= c1) && (c1 < b);
   double rhs[6] = {0, 0, 0, 0, 0, 0};
-  const int i0 = cam_off[c1], i1 = cam_off[c1 + 1];
+  const int i0 = cam_rng[2 * c1], i1 = cam_rng[2 * c1 + 1];
   for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
     const int o1 = cam_obs[i];
     const int p = obs_pt[o1];
@@ -673,7 +686,7 @@ void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
                                                 d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost));
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
-  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_off, d.jrec, d.Ucam);
+  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.jrec, d.Ucam);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, 1e-6, 1e32, mode,
@@ -693,7 +706,7 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   const size_t lds = (size_t(d.tile_cams) * kBlkStride + 32) * sizeof(double);
-  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_off, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.pos, d.jrec,
+  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_rng, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.pos, d.jrec,
                                            d.mrec, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld, d.n);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }

@@ -359,34 +359,54 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     std::vector<int32_t> fill(cam_off.begin(), cam_off.end() - 1);
     for (int64_t q = 0; q < N; ++q) cam_obs[fill[cam_s[q]]++] = int32_t(q);
   }
-  // camera-major copies for the Jacobian pass (k_jacobian) and the record map
-  std::vector<int32_t> cm_p(N), pos(N);
+  // ---- record layout: camera-major, each camera's run padded to a whole
+  // number of 64-record wavefront chunks (padding duplicates the camera's
+  // last observation and is never read back), so k_jacobian stores whole
+  // 10-KB chunks with no predication ----
+  std::vector<int32_t> cam_rng(2 * size_t(C));
+  int64_t npad = 0;
+  for (int c = 0; c < C; ++c) {
+    const int32_t n_c = cam_off[c + 1] - cam_off[c];
+    cam_rng[2 * c] = int32_t(npad);
+    cam_rng[2 * c + 1] = int32_t(npad + n_c);
+    npad += (n_c + 63) / 64 * 64;
+  }
+  d.N_pad = npad;
   // (camera, first position, count, 0) per wavefront chunk, issued
   // piece-major: a camera's list is sorted by point, so piece k of every
   // camera covers about the same slice of the points and the waves in
-  // flight gather X from a narrow, L2-resident range.
+  // flight gather X from a narrow range.
   std::vector<int32_t> jchunks;
   for (int32_t k = 0;; ++k) {
     bool any = false;
     for (int c = 0; c < C; ++c) {
-      const int32_t i = cam_off[c] + 64 * k;
-      if (i >= cam_off[c + 1]) continue;
+      const int32_t n_c = cam_off[c + 1] - cam_off[c];
+      if (64 * k >= n_c) continue;
       any = true;
-      jchunks.insert(jchunks.end(), {c, i, std::min<int32_t>(64, cam_off[c + 1] - i), 0});
+      jchunks.insert(jchunks.end(), {c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), 0});
     }
     if (!any) break;
   }
   d.n_jchunks = int32_t(jchunks.size() / 4);
   d.jac_blocks = std::max(1, std::min((d.n_jchunks + 3) / 4, 1024));
-  std::vector<double> uv_cm(2 * size_t(N));
-  for (int c = 0; c < C; ++c)
-    for (int32_t i = cam_off[c]; i < cam_off[c + 1]; ++i) {
-      const int32_t q = cam_obs[i];
+  // camera-major copies for the Jacobian pass and the record map
+  std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1);
+  std::vector<double> uv_cm(2 * size_t(npad), 0.0);
+  for (int c = 0; c < C; ++c) {
+    const int32_t n_c = cam_off[c + 1] - cam_off[c];
+    const int32_t padded = (n_c + 63) / 64 * 64;
+    for (int32_t j = 0; j < padded; ++j) {
+      const int32_t q = cam_obs[cam_off[c] + std::min(j, n_c - 1)];
+      const int64_t i = cam_rng[2 * c] + j;
       cm_p[i] = pt_s[q];
-      pos[q] = i;
-      uv_cm[2 * size_t(i)] = uv_s[2 * size_t(q)];
-      uv_cm[2 * size_t(i) + 1] = uv_s[2 * size_t(q) + 1];
+      uv_cm[2 * i] = uv_s[2 * size_t(q)];
+      uv_cm[2 * i + 1] = uv_s[2 * size_t(q) + 1];
+      if (j < n_c) {
+        pos[q] = int32_t(i);
+        cam_obs_pad[i] = q;
+      }
     }
+  }
   std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
   for (int c = 0; c < C; ++c) {
     const double* k = K9 + 9 * size_t(c);
@@ -422,11 +442,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.obs_cam, size_t(N));
   ALLOC(d.obs_pt, size_t(N));
   ALLOC(d.pt_off, size_t(P) + 1);
-  ALLOC(d.cam_obs, size_t(N));
-  ALLOC(d.cam_off, size_t(C) + 1);
-  ALLOC(d.cm_p, size_t(N));
+  ALLOC(d.cam_obs, size_t(npad));
+  ALLOC(d.cam_rng, 2 * size_t(C));
+  ALLOC(d.cm_p, size_t(npad));
   ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
-  ALLOC(d.uv_cm, 2 * size_t(N));
+  ALLOC(d.uv_cm, 2 * size_t(npad));
   ALLOC(d.pos, size_t(N));
   ALLOC(d.Kc, 5 * size_t(C));
   ALLOC(d.cam, 6 * size_t(C));
@@ -441,7 +461,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.diag_p, 3 * size_t(P));
   ALLOC(d.camR, size_t(kCamR) * C);
   ALLOC(d.camRn, 12 * size_t(C));
-  ALLOC(d.jrec, size_t(kJRec) * N);
+  ALLOC(d.jrec, size_t(kJRec) * npad);
   ALLOC(d.mrec, size_t(kMRec) * N);
   ALLOC(d.ptV, size_t(kPtV) * P);
   ALLOC(d.ptL, size_t(kPtL) * P);
@@ -465,15 +485,15 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     H2D(d.uv, uv_s.data(), 2 * size_t(N));
     H2D(d.obs_cam, cam_s.data(), size_t(N));
     H2D(d.obs_pt, pt_s.data(), size_t(N));
-    H2D(d.cam_obs, cam_obs.data(), size_t(N));
-    H2D(d.cm_p, cm_p.data(), size_t(N));
+    H2D(d.cam_obs, cam_obs_pad.data(), size_t(npad));
+    H2D(d.cm_p, cm_p.data(), size_t(npad));
     HIPCHK(hipMemcpyAsync(d.jchunks, jchunks.data(), sizeof(int32_t) * jchunks.size(), hipMemcpyHostToDevice, s));
-    H2D(d.uv_cm, uv_cm.data(), 2 * size_t(N));
+    H2D(d.uv_cm, uv_cm.data(), 2 * size_t(npad));
     H2D(d.pos, pos.data(), size_t(N));
     h->pos = pos;
   }
   H2D(d.pt_off, pt_off.data(), size_t(P) + 1);
-  H2D(d.cam_off, cam_off.data(), size_t(C) + 1);
+  if (C) H2D(d.cam_rng, cam_rng.data(), 2 * size_t(C));
   if (C) {
     H2D(d.Kc, Kc.data(), 5 * size_t(C));
     H2D(d.cam, cam.data(), 6 * size_t(C));
@@ -722,7 +742,7 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   launch_jacobian(d, false, h->stream);
   if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
   launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, h->stream);
-  std::vector<double> rec(size_t(kJRec) * d.N);
+  std::vector<double> rec(size_t(kJRec) * d.N_pad);
   if (d.N)
     HIPCHK(hipMemcpyAsync(rec.data(), d.jrec, sizeof(double) * rec.size(), hipMemcpyDeviceToHost, h->stream));
   double c = 0;

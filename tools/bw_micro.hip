@@ -24,7 +24,7 @@ __global__ void k_read(const double2* __restrict__ p, size_t n, double* out) {
 __global__ void k_copy(const double2* __restrict__ a, double2* __restrict__ b, size_t n) {
   for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) b[i] = a[i];
 }
-int main() {
+int main1() {
   const size_t bytes = 320ull << 20, n = bytes / 16;
   double2 *a, *b; double* o;
   hipMalloc(&a, bytes); hipMalloc(&b, bytes); hipMalloc(&o, 8);
@@ -47,3 +47,28 @@ int main() {
     }
   }
 }
+// (appended) write 10-KB runs: one wave per run, run order sequential or permuted
+__global__ void k_runs(double2* __restrict__ p, int nruns, int stride_perm, int per_wave) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, l = threadIdx.x & 63;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int r = wave; r < nruns; r += nw) {
+    const int run = stride_perm ? int((long long)r * stride_perm % nruns) : r;
+    double2* d = p + size_t(run) * 640;
+    for (int k = 0; k < 10; ++k) d[64 * k + l] = make_double2(double(r), double(k));
+  }
+}
+int main2() {
+  const int nruns = 31250;
+  double2* a; hipMalloc(&a, size_t(nruns) * 10240);
+  hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  for (int perm : {0, 7919, 12345}) for (int grid : {1024, 4096}) {
+    float best = 1e9, ms;
+    for (int r = 0; r < 5; ++r) {
+      hipEventRecord(e0); k_runs<<<grid, 256>>>(a, nruns, perm, 0); hipEventRecord(e1);
+      hipEventSynchronize(e1); hipEventElapsedTime(&ms, e0, e1); if (ms < best) best = ms;
+    }
+    printf("runs perm %5d grid %5d  %.1f us  %.1f GB/s\n", perm, grid, best * 1e3, nruns * 10240.0 / (best * 1e-3) / 1e9);
+  }
+  return 0;
+}
+int main() { main2(); return 0; }
