@@ -16,6 +16,7 @@ constexpr int kJX = 0, kRes = 6, kJC = 8;
 // Per-observation Schur record written every LM iteration:
 //   [0..5] M = J_X L_p^-T (2 x 3)   [6..7] h = M z_p
 constexpr int kMRec = 8;
+constexpr int kFRec = 18;  // F = J_c^T M per observation (6x3), point-major
 // Per-camera rotation data: R (9, row-major) and dR/dw_k (27, k-major).
 constexpr int kCamR = 36;
 // Per-camera reduction record: U (21, packed upper 6x6), b_c (6), pad.
@@ -25,9 +26,6 @@ constexpr int kPtV = 10;
 constexpr int kPtL = 10;
 // Cholesky tile size.
 constexpr int kNB = 64;
-// Schur LDS strip: 6x6 block per column camera at an odd stride (37 doubles)
-// so the ds_add_f64 of lanes on different blocks spread over the 64 banks.
-constexpr int kBlkStride = 37;
 
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
@@ -81,6 +79,7 @@ struct DevProblem {
   double* camR = nullptr;     // [C][36]
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
   double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12)
+  double* frec = nullptr;     // [N][18] F = J_c^T M (point-major): Schur pair blocks F_o1 F_o2^T
   double* mrec = nullptr;     // [N][8]
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]
@@ -93,10 +92,12 @@ struct DevProblem {
   double* zwork = nullptr;    // [ld]
   double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
   int32_t* fail = nullptr;    // [1] Cholesky failure flag
-  // Schur tasks: (row camera, first column camera, end column camera)
-  int32_t n_tasks = 0;
-  int32_t* tasks = nullptr;   // [n_tasks][3]
-  int32_t tile_cams = 0;      // max column cameras per task (LDS budget)
+  // Schur: upper-triangle blocks (c1, c2) in row-major order, CSR offsets
+  // of their (o1, o2) pair lists, and the pairs (point-major ids)
+  int64_t n_blk = 0, n_pairs = 0;
+  int2* blk = nullptr;        // [n_blk]
+  int32_t* seg = nullptr;     // [n_blk + 1]
+  int2* pairs = nullptr;      // [n_pairs]
   // reductions
   double* partials = nullptr; // scratch [kNumPartialSlots][max_blocks]
   int32_t max_blocks = 0;

@@ -403,7 +403,8 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
                                                          const int32_t* __restrict__ pos,
                                                          const double* __restrict__ jrec, const double* __restrict__ ptV,
                                                          const double* __restrict__ diag_p, double radius,
-                                                         double* __restrict__ mrec, double* __restrict__ ptL,
+                                                         double* __restrict__ mrec, double* __restrict__ frec,
+                                                         double* __restrict__ ptL,
                                                          double* __restrict__ part_bad) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,6 +432,20 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
       double* M = mrec + size_t(q) * kMRec;
       st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
       st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
+      // F = J_c^T M (6x3, row-major): the Schur pair block is F_o1 F_o2^T
+      double jc[12];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+      double F[kFRec];
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+        F[3 * u] = jc[u] * m0 + jc[6 + u] * n0;
+        F[3 * u + 1] = jc[u] * m1 + jc[6 + u] * n1;
+        F[3 * u + 2] = jc[u] * m2 + jc[6 + u] * n2;
+      }
+      double* Fo = frec + size_t(q) * kFRec;
+#pragma unroll
+      for (int f = 0; f < kFRec; f += 2) st2(Fo + f, F[f], F[f + 1]);
     }
   }
   const double r = block_reduce(bad, sh, true);
@@ -438,100 +453,139 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
 }
 
 // ---------------------------------------------------------------------------
-// Reduced camera matrix, one workgroup per task (row camera c1, column
-// cameras [a, b) with a >= c1).  The row's block strip lives in LDS; each
-// lane walks the row camera's observations and, for each, the observations
-// of the same point whose camera falls in [max(a,c1), b) (a contiguous run,
-// since a point's observations are sorted by camera), adding
-//   A_o1 A_o2^T = J_c1^T (M_o1 M_o2^T) J_c2
-// into block (c1, c2).  Written out as S[c1][c2] = [c1==c2](U + D^2) - acc
-// into the row-major upper triangle (== column-major lower) of S; the first
-// task of each row also writes the reduced right-hand side
-//   rhs_c1 = sum_{o in c1} J_c^T (r_o - h_o)
-// into the augmented column n.
-__global__ __launch_bounds__(kThreads) void k_schur(
-    const int32_t* __restrict__ tasks, const int32_t* __restrict__ cam_rng, const int32_t* __restrict__ cam_obs,
-    const int32_t* __restrict__ obs_pt, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pt_off,
-    const int32_t* __restrict__ pos, const double* __restrict__ jrec, const double* __restrict__ mrec,
-    const double* __restrict__ Ucam,
-    const double* __restrict__ diag_c, double radius, int add_diag, double* __restrict__ S, int ld, int n) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int c1 = tasks[3 * blockIdx.x], a = tasks[3 * blockIdx.x + 1], b = tasks[3 * blockIdx.x + 2];
-  const int ncol = b - a;
-  double* acc = smem;
-  double* red = smem + ncol * kBlkStride;  // 4 waves x 6
-  for (int i = threadIdx.x; i < ncol * kBlkStride; i += kThreads) acc[i] = 0.0;
-  __syncthreads();
-  const int lo = a > c1 ? a : c1;
-  const bool own = (a <= c1) && (c1 < b);
-  double rhs[6] = {0, 0, 0, 0, 0, 0};
-  const int i0 = cam_rng[2 * c1], i1 = cam_rng[2 * c1 + 1];
-  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
-    const int o1 = cam_obs[i];
-    const int p = obs_pt[o1];
-    const double* J1p = jrec + size_t(i) * kJRec;  // camera-major record: streamed
-    const double* M1p = mrec + size_t(o1) * kMRec;
-    double J1[12], M1[6];
+// Reduced camera matrix  S = U + D^2 - sum_p F_p F_p^T,  F_o = J_c^T M_o
+// (6x3 per observation, k_point_prep), row-major upper triangle (==
+// column-major lower) of the augmented matrix, plus the reduced right-hand
+// side rhs_c = sum_{o in c} J_c^T (r_o - h_o) in column n.
+//
+// k_schur: one THREAD per block (c1, c2), c1 <= c2, of the upper triangle
+// (row-major block order, so a wavefront covers one row camera and its
+// F_o1 records stay L2-hot).  The thread walks its block's pair list --
+// (o1, o2) observations of a common point, cameras c1 and c2, host-built --
+// and accumulates F_o1 F_o2^T in registers: no atomics, no barriers, a fixed
+// summation order (S is bitwise reproducible), and every iteration's two
+// 144-B gathers are independent of the previous one, two pairs in flight
+// per step.  (f64 LDS atomics retire about one lane per clock per CU: the
+// atomic strip formulation was bound at ~0.8 ms on C3.)  A diagonal block's
+// list holds only same-camera duplicate pairs (normally none);
+// k_schur_diag, launched after, adds the rest of that block and the rhs.
+__global__ __launch_bounds__(kThreads) void k_schur(int64_t n_blk, const int2* __restrict__ blk,
+                                                    const int32_t* __restrict__ seg, const int2* __restrict__ pairs,
+                                                    const double* __restrict__ frec, double* __restrict__ S, int ld) {
+  const int64_t b = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (b >= n_blk) return;
+  const int2 cc = blk[b];
+  const int kb = seg[b], ke = seg[b + 1];
+  double acc[36];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) { const double2 t = ld2(J1p + kJC + 2 * k); J1[2 * k] = t.x; J1[2 * k + 1] = t.y; }
+  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+  for (int k = kb; k < ke; k += 2) {
+    const bool two = k + 1 < ke;
+    const int2 pa = pairs[k], pb = pairs[two ? k + 1 : k];
+    const double wb = two ? 1.0 : 0.0;
+    const double* A1 = frec + size_t(pa.x) * kFRec;
+    const double* A2 = frec + size_t(pa.y) * kFRec;
+    const double* B1 = frec + size_t(pb.x) * kFRec;
+    const double* B2 = frec + size_t(pb.y) * kFRec;
+    double Ga[kFRec], Gb[kFRec];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { const double2 t = ld2(M1p + 2 * k); M1[2 * k] = t.x; M1[2 * k + 1] = t.y; }
-    if (own) {
-      const double2 rr = ld2(J1p + kRes), hh = ld2(M1p + 6);
-      const double e0 = rr.x - hh.x, e1 = rr.y - hh.y;
-#pragma unroll
-      for (int u = 0; u < 6; ++u) rhs[u] += J1[u] * e0 + J1[6 + u] * e1;
+    for (int f = 0; f < kFRec; f += 2) {
+      const double2 x = ld2(A2 + f), y = ld2(B2 + f);
+      Ga[f] = x.x; Ga[f + 1] = x.y; Gb[f] = y.x * wb; Gb[f + 1] = y.y * wb;
     }
-    const int q0 = pt_off[p], q1 = pt_off[p + 1];
-    for (int o2 = q0; o2 < q1; ++o2) {
-      const int c2 = obs_cam[o2];
-      if (c2 < lo) continue;
-      if (c2 >= b) break;
-      const double* J2p = jrec + size_t(pos[o2]) * kJRec + kJC;
-      const double* M2p = mrec + size_t(o2) * kMRec;
-      double J2[12], M2[6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) { const double2 t = ld2(J2p + 2 * k); J2[2 * k] = t.x; J2[2 * k + 1] = t.y; }
+    for (int u = 0; u < 6; ++u) {
+      const double2 a01 = ld2(A1 + 3 * u - (u & 1)), b01 = ld2(B1 + 3 * u - (u & 1));
+      // F_o1 row u = (x, y, z) at 3u; 16-B aligned loads straddle it
+      const double a0 = (u & 1) ? a01.y : a01.x, a1 = (u & 1) ? A1[3 * u + 1] : a01.y, a2 = A1[3 * u + 2];
+      const double b0 = (u & 1) ? b01.y : b01.x, b1 = (u & 1) ? B1[3 * u + 1] : b01.y, b2 = B1[3 * u + 2];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { const double2 t = ld2(M2p + 2 * k); M2[2 * k] = t.x; M2[2 * k + 1] = t.y; }
-      const double G00 = M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2];
-      const double G01 = M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5];
-      const double G10 = M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2];
-      const double G11 = M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5];
-      double* blk = acc + (c2 - a) * kBlkStride;
-#pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        const double H0 = J1[u] * G00 + J1[6 + u] * G10;
-        const double H1 = J1[u] * G01 + J1[6 + u] * G11;
-#pragma unroll
-        for (int v = 0; v < 6; ++v) atomicAdd(blk + 6 * u + v, H0 * J2[v] + H1 * J2[6 + v]);
+      for (int v = 0; v < 6; ++v) {
+        acc[6 * u + v] += a0 * Ga[3 * v] + a1 * Ga[3 * v + 1] + a2 * Ga[3 * v + 2];
+        acc[6 * u + v] += b0 * Gb[3 * v] + b1 * Gb[3 * v + 1] + b2 * Gb[3 * v + 2];
       }
     }
   }
-  __syncthreads();
-  const int W = 6 * ncol;
-  const double* U = Ucam + size_t(kUcam) * c1;
-  for (int e = threadIdx.x; e < 6 * W; e += kThreads) {
-    const int u = e / W, col = e - u * W;
-    const int cb = col / 6, v = col - 6 * cb;
-    double val = -acc[cb * kBlkStride + 6 * u + v];
-    if (add_diag && a + cb == c1) {
-      val += U[up6(u, v)];
-      if (u == v) { const double d = sqrt(diag_c[6 * size_t(c1) + u] / radius); val += d * d; }
-    }
-    S[size_t(6 * c1 + u) * ld + 6 * size_t(a) + col] = val;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
+#pragma unroll
+    for (int v = 0; v < 6; v += 2) st2(row + v, -acc[6 * u + v], -acc[6 * u + v + 1]);
   }
-  if (own) {
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+}
+
+// Diagonal blocks and right-hand side, one workgroup per camera c (after
+// k_schur, which left the block's same-camera duplicate pairs in S):
+//   S_cc += [rank 0] (U_c + D_c^2) - sum_{o in c} F_o F_o^T,
+//   S[c][n] = sum_{o in c} J_c^T (r_o - h_o); fixed-order reductions.
+__global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restrict__ cam_rng,
+                                                         const int32_t* __restrict__ cam_obs,
+                                                         const double* __restrict__ jrec,
+                                                         const double* __restrict__ mrec,
+                                                         const double* __restrict__ Ucam,
+                                                         const double* __restrict__ diag_c, double radius,
+                                                         int add_diag, double* __restrict__ S, int ld, int n) {
+  __shared__ double red[(kThreads / 64) * 28];
+  const int c = blockIdx.x;
+  const int i0 = cam_rng[2 * c], i1 = cam_rng[2 * c + 1];
+  double dacc[21], rhs[6];
+#pragma unroll
+  for (int e = 0; e < 21; ++e) dacc[e] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 6; ++e) rhs[e] = 0.0;
+  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
+    const double* J1p = jrec + size_t(i) * kJRec;
+    const double* M1p = mrec + size_t(cam_obs[i]) * kMRec;
+    double J1[12], M1[8];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { const double2 v = ld2(J1p + kJC + 2 * k); J1[2 * k] = v.x; J1[2 * k + 1] = v.y; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const double2 v = ld2(M1p + 2 * k); M1[2 * k] = v.x; M1[2 * k + 1] = v.y; }
+    double F[kFRec];
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
-      const double v = wave_sum(rhs[u]);
-      if (l == 0) red[w * 6 + u] = v;
+      F[3 * u] = J1[u] * M1[0] + J1[6 + u] * M1[3];
+      F[3 * u + 1] = J1[u] * M1[1] + J1[6 + u] * M1[4];
+      F[3 * u + 2] = J1[u] * M1[2] + J1[6 + u] * M1[5];
     }
-    __syncthreads();
-    if (threadIdx.x < 6)
-      S[size_t(6 * c1 + threadIdx.x) * ld + n] =
-          red[threadIdx.x] + red[6 + threadIdx.x] + red[12 + threadIdx.x] + red[18 + threadIdx.x];
+    const double2 rr = ld2(J1p + kRes);
+    const double e0 = rr.x - M1[6], e1 = rr.y - M1[7];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) rhs[u] += J1[u] * e0 + J1[6 + u] * e1;
+    int q = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int v = u; v < 6; ++v, ++q) dacc[q] += F[3 * u] * F[3 * v] + F[3 * u + 1] * F[3 * v + 1] + F[3 * u + 2] * F[3 * v + 2];
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int e = 0; e < 21; ++e) {
+    const double v = wave_sum(dacc[e]);
+    if (l == 0) red[w * 28 + e] = v;
+  }
+#pragma unroll
+  for (int e = 0; e < 6; ++e) {
+    const double v = wave_sum(rhs[e]);
+    if (l == 0) red[w * 28 + 21 + e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 36) {
+    const int u = threadIdx.x / 6, v = threadIdx.x % 6, q = up6(u, v);
+    double tot = red[q];
+    for (int w2 = 1; w2 < kThreads / 64; ++w2) tot += red[28 * w2 + q];
+    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + v;
+    double val = *sp - tot;
+    if (add_diag) {
+      val += Ucam[size_t(kUcam) * c + q];
+      if (u == v) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
+    }
+    *sp = val;
+  } else if (threadIdx.x < 42) {
+    const int u = threadIdx.x - 36;
+    double tot = red[21 + u];
+    for (int w2 = 1; w2 < kThreads / 64; ++w2) tot += red[28 * w2 + 21 + u];
+    S[size_t(6 * c + u) * ld + n] = tot;
   }
 }
 
@@ -701,13 +755,14 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P == 0) return;
-  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.ptV, d.diag_p, radius, d.mrec,
+  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.ptV, d.diag_p, radius, d.mrec, d.frec,
                                                              d.ptL, slot(d, kPBad));
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
-  const size_t lds = (size_t(d.tile_cams) * kBlkStride + 32) * sizeof(double);
-  k_schur<<<d.n_tasks, kThreads, lds, s>>>(d.tasks, d.cam_rng, d.cam_obs, d.obs_pt, d.obs_cam, d.pt_off, d.pos, d.jrec,
-                                           d.mrec, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld, d.n);
+  if (d.n_blk)
+    k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
+  k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
+                                        add_diag ? 1 : 0, d.S, d.ld, d.n);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {

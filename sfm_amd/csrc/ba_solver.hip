@@ -413,23 +413,33 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     Kc[5 * c] = k[0]; Kc[5 * c + 1] = k[1]; Kc[5 * c + 2] = k[2]; Kc[5 * c + 3] = k[4]; Kc[5 * c + 4] = k[5];
     for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
   }
-  // ---- Schur tasks: (row camera, column range) within the LDS budget ----
-  d.tile_cams = std::max(1, std::min(C, 200));  // (200*37+32)*8 B <= 64 KiB dynamic LDS
-  std::vector<std::array<int32_t, 3>> tasks;
-  std::vector<int64_t> work;
-  for (int c1 = 0; c1 < C; ++c1)
-    for (int a = c1; a < C; a += d.tile_cams) {
-      const int b = std::min(C, a + d.tile_cams);
-      tasks.push_back({c1, a, b});
-      work.push_back(int64_t(cam_off[c1 + 1] - cam_off[c1] + 1) * (b - a));
+  // ---- Schur blocks (k_schur): every upper-triangle block (c1, c2),
+  // c1 <= c2, in row-major order, with the CSR list of its (o1, o2) pairs:
+  // observations of a common point with cameras c1 and c2 (o2 != o1; on the
+  // diagonal only same-camera duplicates).  Pairs are point-major ids. ----
+  std::vector<int32_t> blk, seg, pairs;
+  {
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> cols(C);
+    for (int c1 = 0; c1 < C; ++c1) {
+      for (int c2 = c1; c2 < C; ++c2) cols[c2].clear();
+      for (int32_t i = cam_off[c1]; i < cam_off[c1 + 1]; ++i) {
+        const int32_t o1 = cam_obs[i];
+        const int p = pt_s[o1];
+        for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
+          if (cam_s[o2] >= c1 && o2 != o1) cols[cam_s[o2]].push_back({o1, o2});
+      }
+      for (int c2 = c1; c2 < C; ++c2) {
+        blk.push_back(c1);
+        blk.push_back(c2);
+        seg.push_back(int32_t(pairs.size() / 2));
+        for (auto& pr : cols[c2]) { pairs.push_back(pr.first); pairs.push_back(pr.second); }
+      }
     }
-  std::vector<int> tord(tasks.size());
-  for (size_t i = 0; i < tord.size(); ++i) tord[i] = int(i);
-  std::stable_sort(tord.begin(), tord.end(), [&](int x, int y) { return work[x] > work[y]; });
-  std::vector<int32_t> task_flat(3 * tasks.size());
-  for (size_t i = 0; i < tord.size(); ++i)
-    for (int k = 0; k < 3; ++k) task_flat[3 * i + k] = tasks[tord[i]][k];
-  d.n_tasks = int32_t(tasks.size());
+    seg.push_back(int32_t(pairs.size() / 2));
+  }
+  if (pairs.size() / 2 >= size_t(INT32_MAX)) return fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets");
+  d.n_blk = int64_t(blk.size() / 2);
+  d.n_pairs = int64_t(pairs.size() / 2);
   // ---- dense system geometry ----
   d.n = 6 * C;
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
@@ -463,6 +473,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.camRn, 12 * size_t(C));
   ALLOC(d.jrec, size_t(kJRec) * npad);
   ALLOC(d.mrec, size_t(kMRec) * N);
+  ALLOC(d.frec, size_t(kFRec) * N);
   ALLOC(d.ptV, size_t(kPtV) * P);
   ALLOC(d.ptL, size_t(kPtL) * P);
   ALLOC(d.Ucam, size_t(kUcam) * C);
@@ -471,7 +482,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.zwork, size_t(d.ld));
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
-  ALLOC(d.tasks, 3 * tasks.size());
+  ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
+  ALLOC(d.pairs, std::max<size_t>(1, size_t(d.n_pairs)));
+  ALLOC(d.seg, size_t(d.n_blk) + 1);
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars));
 #undef ALLOC
@@ -503,7 +516,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     H2D(d.X, X, 3 * size_t(P));
     H2D(d.X0, X, 3 * size_t(P));
   }
-  if (!tasks.empty()) H2D(d.tasks, task_flat.data(), task_flat.size());
+  if (d.n_blk)
+    HIPCHK(hipMemcpyAsync(d.blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice, s));
+  if (d.n_pairs)
+    HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
+  H2D(d.seg, seg.data(), seg.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
   HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
