@@ -36,9 +36,9 @@ SEED = 0x5F3D2017 + 3      # config C3
 
 
 def jacobian_bytes(n_obs: int, n_cams: int, n_pts: int) -> int:
-    # per observation: camera-major index record 16 + uv 16 + r 16 + J 144
-    # (k_jacobian, DESIGN.md); per camera: pose 48 + K 40; per point: X 24.
-    return 192 * n_obs + 88 * n_cams + 24 * n_pts
+    # per observation: point index 4 + uv 16 + record 160 (r 16 + J 144)
+    # (k_jacobian, DESIGN.md §5); per camera: pose 48 + K 40; per point: X 24.
+    return 180 * n_obs + 88 * n_cams + 24 * n_pts
 
 
 def cholesky_flops(n: int) -> float:
@@ -162,7 +162,7 @@ def main() -> int:
     roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass)", "bound": "hbm", "achieved": round(jac_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5)}
-    roof_chol = {"kernel": "dense reduced-camera Cholesky (k_chol_diag/k_chol_gemm, f64 MFMA)", "bound": "mfma",
+    roof_chol = {"kernel": "dense reduced-camera Cholesky phase (k_chol_potrf/trsm/syrk, f64 MFMA)", "bound": "mfma",
                  "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                  "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": None,
                  "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4)}

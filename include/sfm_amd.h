@@ -153,7 +153,8 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms);
 /* Per-phase device time of the last solve (ms): [jacobian, cam_reduce,
  * point_eval, point_prep, schur, cholesky, backsolve, backsub, other]. */
 int sfm_ba_phase_times(sfm_ba_handle* h, double* ms9);
-/* Enable per-phase HIP-event timing for subsequent solves (adds syncs). */
+/* Enable per-phase HIP-event timing for subsequent solves (events on the
+ * solver stream, read at the per-iteration scalar sync: no extra syncs). */
 int sfm_ba_set_profiling(sfm_ba_handle* h, int32_t on);
 /* Synchronise the handle's stream. */
 int sfm_ba_sync(sfm_ba_handle* h);

@@ -1,0 +1,144 @@
+// sfm_ctracker_compat.hpp -- header-only C++ shim that gives the reference's
+// CTracker hot-path signatures on top of the plain C ABI of sfm_amd.h.
+//
+// A maintainer swaps the Ceres body of
+//   void CTracker::bundleAdjustmentStructAndPose(const vector<Point2d>&,
+//       const vector<int>&, const vector<Matx33d>&, vector<double*>& R,
+//       vector<double*>& t, vector<double*>& pts3D, int isStructOrPose)
+//   (/root/reference/CTracker.h:65, CTracker.cpp:670-702)
+// for a call to sfm_compat::bundleAdjustmentStructAndPose(...) with the same
+// arguments.  The shim
+//   1. deduplicates the per-observation point pointers into pt_idx in
+//      first-seen order (the reference identifies Ceres parameter blocks by
+//      address, CSfM.cpp:321-340),
+//   2. packs the structure-of-arrays the ABI takes,
+//   3. calls sfm_ba_solve,
+//   4. scatters the solution back through the caller's pointers, exactly
+//      where Ceres would have written it.
+// Cameras are identified by camIdx (index into R / t / K), as in the
+// reference.  On an error nothing is written back and the ABI code is
+// returned (the reference has no error channel; callers may ignore it).
+//
+// Types are templates so the header does not depend on OpenCV: Point2 needs
+// .x/.y, Matx33 needs .val[9] (row-major, cv::Matx33d layout), the
+// descriptor matrix needs .rows / .cols / .data (cv::Mat of CV_8U).
+#ifndef SFM_CTRACKER_COMPAT_HPP_
+#define SFM_CTRACKER_COMPAT_HPP_
+
+#include <cstdint>
+#include <unordered_map>
+#include <vector>
+
+#include "sfm_amd.h"
+
+namespace sfm_compat {
+
+// Packed form of one BA problem (what sfm_ba_solve consumes).
+struct PackedProblem {
+  std::vector<double> uv, K9, rot, t, X;
+  std::vector<int32_t> cam_idx, pt_idx;
+  std::vector<double*> point_ptr;  // distinct point blocks, first-seen order
+};
+
+template <class Point2, class Matx33>
+inline int pack_problem(const std::vector<Point2>& observations, const std::vector<int>& camIdx,
+                        const std::vector<Matx33>& K, const std::vector<double*>& R, const std::vector<double*>& t,
+                        const std::vector<double*>& pts3D, PackedProblem* out) {
+  const size_t n = observations.size();
+  if (camIdx.size() != n || pts3D.size() != n || R.size() != t.size() || K.size() < R.size()) return SFM_EINVAL;
+  PackedProblem& p = *out;
+  p.uv.resize(2 * n);
+  p.cam_idx.resize(n);
+  p.pt_idx.resize(n);
+  p.point_ptr.clear();
+  std::unordered_map<const double*, int32_t> id;
+  id.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    p.uv[2 * i] = observations[i].x;
+    p.uv[2 * i + 1] = observations[i].y;
+    if (camIdx[i] < 0 || size_t(camIdx[i]) >= R.size()) return SFM_EINVAL;
+    p.cam_idx[i] = camIdx[i];
+    auto it = id.find(pts3D[i]);
+    if (it == id.end()) {
+      it = id.emplace(pts3D[i], int32_t(p.point_ptr.size())).first;
+      p.point_ptr.push_back(pts3D[i]);
+    }
+    p.pt_idx[i] = it->second;
+  }
+  const size_t C = R.size(), P = p.point_ptr.size();
+  p.K9.resize(9 * C);
+  p.rot.resize(3 * C);
+  p.t.resize(3 * C);
+  for (size_t c = 0; c < C; ++c) {
+    for (int k = 0; k < 9; ++k) p.K9[9 * c + k] = K[c].val[k];
+    for (int k = 0; k < 3; ++k) {
+      p.rot[3 * c + k] = R[c][k];
+      p.t[3 * c + k] = t[c][k];
+    }
+  }
+  p.X.resize(3 * P);
+  for (size_t q = 0; q < P; ++q)
+    for (int k = 0; k < 3; ++k) p.X[3 * q + k] = p.point_ptr[q][k];
+  return SFM_OK;
+}
+
+// Drop-in for CTracker::bundleAdjustmentStructAndPose (CTracker.cpp:670-702).
+// opts == nullptr: the reference's options (DENSE_SCHUR, Ceres defaults,
+// CTracker.cpp:571-577).  summary (optional) receives what Ceres' Summary
+// would have said; the reference discards it (CTracker.cpp:700-701).
+template <class Point2, class Matx33>
+inline int bundleAdjustmentStructAndPose(const std::vector<Point2>& observations, const std::vector<int>& camIdx,
+                                         const std::vector<Matx33>& K, std::vector<double*>& R,
+                                         std::vector<double*>& t, std::vector<double*>& pts3D, int isStructOrPose,
+                                         const sfm_ba_options* opts = nullptr, sfm_ba_summary* summary = nullptr) {
+  PackedProblem p;
+  int rc = pack_problem(observations, camIdx, K, R, t, pts3D, &p);
+  if (rc) return rc;
+  sfm_ba_options o;
+  if (opts) o = *opts; else sfm_ba_default_options(&o);
+  sfm_ba_summary sm;
+  rc = sfm_ba_solve(&o, isStructOrPose, int64_t(observations.size()), p.uv.data(), p.cam_idx.data(),
+                    p.pt_idx.data(), int32_t(R.size()), p.K9.data(), p.rot.data(), p.t.data(),
+                    int32_t(p.point_ptr.size()), p.X.data(), &sm, nullptr, 0, nullptr);
+  if (rc) return rc;
+  for (size_t c = 0; c < R.size(); ++c)
+    for (int k = 0; k < 3; ++k) {
+      R[c][k] = p.rot[3 * c + k];
+      t[c][k] = p.t[3 * c + k];
+    }
+  for (size_t q = 0; q < p.point_ptr.size(); ++q)
+    for (int k = 0; k < 3; ++k) p.point_ptr[q][k] = p.X[3 * q + k];
+  if (summary) *summary = sm;
+  return SFM_OK;
+}
+
+// Drop-in for CTracker::matchFeatures(pts0, desc0, pts1, desc1, idx0, idx1,
+// minDistance, maxDistance) (CTracker.h:55, CTracker.cpp:211-250); with
+// (1.5, 40) it is the member-window overload (CTracker.h:53,
+// CTracker.cpp:114-149).  Like the reference it APPENDS the matches to
+// matchIdx0 / matchIdx1 (push_back, CTracker.cpp:238-239) and returns
+// nothing useful: the int is the ABI code (0 on success).
+template <class Point2, class DescMat>
+inline int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, const std::vector<Point2>& pts1,
+                         const DescMat& desc1, std::vector<int>& matchIdx0, std::vector<int>& matchIdx1,
+                         double minDistance = 1.5, double maxDistance = 40.0, int32_t device = 0,
+                         double ratio = 0.8) {
+  const int32_t n0 = int32_t(pts0.size()), n1 = int32_t(pts1.size());
+  std::vector<double> p0(2 * size_t(n0)), p1(2 * size_t(n1));
+  for (int32_t i = 0; i < n0; ++i) { p0[2 * i] = pts0[i].x; p0[2 * i + 1] = pts0[i].y; }
+  for (int32_t i = 0; i < n1; ++i) { p1[2 * i] = pts1[i].x; p1[2 * i + 1] = pts1[i].y; }
+  const int32_t cap = n0 < n1 ? n0 : n1;
+  std::vector<int32_t> i0(size_t(cap > 0 ? cap : 0)), i1(size_t(cap > 0 ? cap : 0));
+  int32_t nm = 0;
+  const int rc = sfm_match_features(device, p0.data(), static_cast<const uint8_t*>(desc0.data), n0, p1.data(),
+                                    static_cast<const uint8_t*>(desc1.data), n1, int32_t(desc0.cols), ratio,
+                                    minDistance, maxDistance, i0.data(), i1.data(), &nm);
+  if (rc) return rc;
+  matchIdx0.insert(matchIdx0.end(), i0.begin(), i0.begin() + nm);
+  matchIdx1.insert(matchIdx1.end(), i1.begin(), i1.begin() + nm);
+  return SFM_OK;
+}
+
+}  // namespace sfm_compat
+
+#endif  // SFM_CTRACKER_COMPAT_HPP_
