@@ -30,10 +30,13 @@ constexpr int NB = kNB;  // 64
 // Pivot: 1/sqrt(d) by the hardware estimate + two Newton steps (full double
 // precision), sqrt(d) = d * (1/sqrt(d)).  Keeps the pivot chain short.
 __device__ __forceinline__ double rsqrt_nr(double d) {
-  double y = __builtin_amdgcn_rsq(d);
-  y = y * fma(-0.5 * d * y, y, 1.5);
-  y = y * fma(-0.5 * d * y, y, 1.5);
-  return y;
+  // v_rsq_f64 is good to ~5e-8; one third-order step
+  //   y1 = y0 (1 + e/2 + 3e^2/8),  e = 1 - d y0^2
+  // reaches full precision with four dependent operations (two Newton
+  // steps would take six).
+  const double y = __builtin_amdgcn_rsq(d);
+  const double e = fma(-d * y, y, 1.0);
+  return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
 // Uniform broadcast of lane `src`'s double (two v_readlane_b32 -> SGPRs).
@@ -43,86 +46,152 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
-// POTRF of one 64x64 tile plus the tile inverse W = L^-1, two wavefronts.
-// Wave 0 factors: lane r holds row r of the tile (a[j] = A(r, j), upper part
-// taken from the symmetric lower storage), so for column j lane r's own
-// a[j] = A(j, r):
-//   pivot  d = a[j] of lane j           (readlane broadcast)
-//   l_r    = a[j] / sqrt(d)             (own register: L(r, j))
-//   update a[c] -= l_r * L(c, j), c > j (L(c, j) by LDS broadcast reads)
-// and leaves every column L(:, j) in LDS.  L = E_0 E_1 ... E_63 with E_j the
-// identity whose column j is L(:, j), so wave 1 forms W = E_63^-1 ... E_0^-1
-// from those columns, one block of 8 behind wave 0: lane m holds column m
-// of W (w[c] = W(c, m)) and applies w[j] *= 1/L(j, j); w[c] -= L(c, j) w[j].
-// W turns the panel solve and the back substitution into products
-// (k_chol_trsm, k_backsolve_step) with no per-column chain outside this
-// kernel.  Fully unrolled; the broadcast reads of a column are issued
-// together.  Pivots at or beyond n (augmented row, identity padding) are
-// taken as 1 so the padding stays finite; they are never read back.
-constexpr int kPotrfBlk = 8;
-__global__ __launch_bounds__(128) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
+// POTRF of one 64x64 tile plus its inverse W = L^-1, four wavefronts,
+// blocked in 16-column panels so that the per-pivot work is small and the
+// bulk of the flops runs on MFMA.  For panel b = 0..3 (columns 16b..16b+15):
+//   wave 0     factors the panel column by column, lane r = row r holding
+//              its 16 panel entries in registers.  The pivot chain is
+//              readlane-only: the next pivot is lane g+1's own a - l*l and
+//              L(g+1, g) reaches every lane by readlane; the other columns'
+//              L(c, g) come from the column just written to LDS.  Lanes
+//              0..15 also carry the columns of W_bb = L_bb^-1 through the
+//              same eliminations (w_j *= 1/L_jj, w_c -= L_cj w_j).
+//   waves 1-3  meanwhile form row b-1 of W off the diagonal,
+//              W_{b-1,J} = -W_{b-1,b-1} sum_{K=J}^{b-2} L_{b-1,K} W_KJ (MFMA).
+//   all waves  then apply the trailing update C_IJ -= P_I P_J^T to the 16x16
+//              blocks right of and below the panel (v_mfma_f64_16x16x4_f64).
+// Row 3 of W closes the kernel.  Pivots at or beyond n (augmented row,
+// identity padding) are taken as 1 so the padding stays finite; they are
+// never read back.  The strictly upper part of the stored tile is a
+// don't-care (never read by any kernel).
+constexpr int TS = NB + 1;  // LDS column stride (doubles) of the tile images
+
+// D (16x16) += sum_{k<16} A(i, k) B(k, j) with A(i, k) = Ap[i*ai + k*ak],
+// B(k, j) = Bp[k*bk + j*bj] (LDS).  Lane l's reg r holds D(4r + (l>>4), l&15).
+__device__ __forceinline__ f64x4 mfma16(const double* Ap, int ai, int ak, const double* Bp, int bk, int bj, f64x4 acc,
+                                        int lane) {
+  const int i = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + kk;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ap[i * ai + k * ak], Bp[k * bk + i * bj], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// W_IJ = -W_II sum_{K=J}^{I-1} L_IK W_KJ, by one wavefront (scr: its 16x16 scratch).
+__device__ __forceinline__ void w_offdiag(const double* T, double* Wl, double* scr, int I, int J, int lane) {
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int K = J; K < I; ++K)  // A(i,k) = L(16I+i, 16K+k), B(k,j) = W(16K+k, 16J+j)
+    acc = mfma16(T + (16 * K) * TS + 16 * I, 1, TS, Wl + (16 * J) * TS + 16 * K, 1, TS, acc, lane);
+  const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) scr[(4 * rr + kk) * 16 + j] = acc[rr];  // row-major T1(i, j)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  f64x4 acc2 = {0.0, 0.0, 0.0, 0.0};  // A(i,k) = W(16I+i, 16I+k), B(k,j) = T1(k, j)
+  acc2 = mfma16(Wl + (16 * I) * TS + 16 * I, 1, TS, scr, 16, 1, acc2, lane);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) Wl[(16 * J + j) * TS + 16 * I + 4 * rr + kk] = -acc2[rr];
+}
+
+template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
+__global__ __launch_bounds__(256) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
                                                     double* __restrict__ Winv, int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double Lcol[NB * NB];  // Lcol[j][c] = L(c, j)
-  __shared__ double invs[NB];
-  const int r = threadIdx.x & 63;
+  __shared__ double T[NB * TS];    // T[c*TS + r] = A(r, c), becomes L
+  __shared__ double Wl[NB * TS];   // Wl[c*TS + r] = W(r, c)
+  __shared__ double scr[4][256];   // per-wave 16x16 scratch (row-major)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int k0 = k * NB;
-  if (threadIdx.x < 64) {
-    double a[NB];
+  // ---- load the tile (coalesced columns), clear W ----
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
-      a[j] = (j <= r) ? A[size_t(k0 + j) * ld + k0 + r] : A[size_t(k0 + r) * ld + k0 + j];
-    bool bad = false;
+  for (int q = 0; q < 16; ++q) {
+    const int e = t + 256 * q, c = e >> 6, r = e & 63;
+    T[c * TS + r] = A[size_t(k0 + c) * ld + k0 + r];
+    Wl[c * TS + r] = 0.0;
+  }
+  __syncthreads();
+  bool bad = false;
+  for (int b = 0; b < 4; ++b) {
+    const int g0 = 16 * b;
+    if (w == 0) {
+      // ---- panel factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
+      const int r = lane;
+      double p[16], wc[16];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      double d = bcast(a[j], j);
-      if ((k0 + j) < n) bad |= !(d > 0.0);
-      else d = 1.0;
-      const double inv = rsqrt_nr(d);
-      const double l = a[j] * inv;  // L(r, j) for r >= j (r == j: sqrt(d))
-      a[j] = l;
-      Lcol[j * NB + r] = l;
-      invs[j] = inv;
-      if (j < NB - 1) {
-        double lc[NB];
-#pragma unroll
-        for (int c = (j + 1) & ~1; c < NB; c += 2) {
-          const double2 v2 = *reinterpret_cast<const double2*>(&Lcol[j * NB + c]);
-          lc[c] = v2.x;
-          lc[c + 1] = v2.y;
-        }
-#pragma unroll
-        for (int c = j + 1; c < NB; ++c) a[c] = fma(-l, lc[c], a[c]);
+      for (int j = 0; j < 16; ++j) {
+        p[j] = T[(g0 + j) * TS + r];
+        wc[j] = (j == r) ? 1.0 : 0.0;
       }
-      if (j % kPotrfBlk == kPotrfBlk - 1) __syncthreads();
-    }
-    if (bad && r == 0) atomicOr(fail, 1);
+      double d = bcast(p[0], g0);
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
-      if (j <= r) A[size_t(k0 + j) * ld + k0 + r] = a[j];
-  } else {
-    double w[NB];
+      for (int j = 0; j < 16; ++j) {
+        const int g = g0 + j;
+        if (kFull || k0 + g < n) bad |= !(d > 0.0);
+        else d = 1.0;
+        const double inv = rsqrt_nr(d);
+        const double l = p[j] * inv;  // L(r, g) for r >= g (r == g: sqrt(d))
+        p[j] = l;
+        T[g * TS + r] = l;
+        wc[j] *= inv;
+        if (j < 15) {
+          // critical path by readlane only: the next pivot (lane g+1's own
+          // a - l*l) and the next column's L(g+1, g) for every lane
+          const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
+          const double l1 = bcast(l, g + 1);
+          p[j + 1] = fma(-l, l1, p[j + 1]);
+          wc[j + 1] = fma(-l1, wc[j], wc[j + 1]);
+          if (j < 14) {
+            double lc[16];
 #pragma unroll
-    for (int c = 0; c < NB; ++c) w[c] = (c == r) ? 1.0 : 0.0;
+            for (int c = j + 2; c < 16; ++c) lc[c] = T[g * TS + g0 + c];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      if (j % kPotrfBlk == 0) __syncthreads();
-      w[j] *= invs[j];
-      if (j < NB - 1) {
-        double lc[NB];
-#pragma unroll
-        for (int c = (j + 1) & ~1; c < NB; c += 2) {
-          const double2 v2 = *reinterpret_cast<const double2*>(&Lcol[j * NB + c]);
-          lc[c] = v2.x;
-          lc[c + 1] = v2.y;
+            for (int c = j + 2; c < 16; ++c) {
+              p[c] = fma(-l, lc[c], p[c]);
+              wc[c] = fma(-lc[c], wc[j], wc[c]);
+            }
+          }
+          d = dn;
         }
-#pragma unroll
-        for (int c = j + 1; c < NB; ++c) w[c] = fma(-lc[c], w[j], w[c]);
       }
-    }
-    // W column-major (Wc[m][c] = W(c, m)); lane m writes 64 contiguous doubles
-    double* Wk = Winv + size_t(k) * NB * NB + size_t(r) * NB;
+      if (r < 16)
 #pragma unroll
-    for (int c = 0; c < NB; c += 2) *reinterpret_cast<double2*>(Wk + c) = double2{w[c], w[c + 1]};
+        for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = wc[c];
+    } else if (b >= 2 && w - 1 < b - 1) {
+      w_offdiag(T, Wl, scr[w], b - 1, w - 1, lane);  // row b-1 of W (its diagonal block is done)
+    }
+    __syncthreads();
+    // ---- trailing update: blocks (I, J), b < J <= I <= 3 ----
+    if (b < 3) {
+      const int nJ = 3 - b, nq = nJ * (nJ + 1) / 2;
+      for (int q = w; q < nq; q += 4) {
+        // q -> (J, I) column-major over the trailing lower triangle
+        int J = b + 1, qq = q;
+        while (qq >= 4 - J) { qq -= 4 - J; ++J; }
+        const int I = J + qq;
+        const double* P = T + g0 * TS;  // P(row, kk) = L(row, g0 + kk) = P[kk*TS + row]
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        // A(i, k) = L(16I + i, g0 + k), B(k, j) = L(16J + j, g0 + k)
+        acc = mfma16(P + 16 * I, 1, TS, P + 16 * J, TS, 1, acc, lane);
+        const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) T[(16 * J + j) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
+      }
+      __syncthreads();
+    }
+  }
+  // ---- W row 3 off the diagonal ----
+  if (w < 3) w_offdiag(T, Wl, scr[w], 3, w, lane);
+  if (bad && t == 0) atomicOr(fail, 1);
+  __syncthreads();
+  // ---- store L (whole columns; the strict upper part is a don't-care) and W ----
+  double* Wk = Winv + size_t(k) * NB * NB;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = t + 256 * q, c = e >> 6, r = e & 63;
+    A[size_t(k0 + c) * ld + k0 + r] = T[c * TS + r];
+    Wk[c * NB + r] = Wl[c * TS + r];  // column-major: Wk[m][c] = W(c, m)
   }
 }
 
@@ -301,7 +370,10 @@ __global__ __launch_bounds__(256) void k_backsolve_step(const double* __restrict
 void launch_cholesky(const DevProblem& d, hipStream_t s) {
   (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   for (int k = 0; k < d.nblk; ++k) {
-    k_chol_potrf<<<1, 128, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
+    if ((k + 1) * NB <= d.n)
+      k_chol_potrf<true><<<1, 256, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
+    else
+      k_chol_potrf<false><<<1, 256, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
     const int m = d.nblk - k - 1;
     if (m == 0) break;
     k_chol_trsm<<<m, 256, 0, s>>>(d.S, d.ld, k, d.invL);
