@@ -89,9 +89,9 @@ struct DevProblem {
   int32_t n = 0, ld = 0, nblk = 0;
   double* S = nullptr;
   double* invL = nullptr;     // [nblk][64][64] inverses of the diagonal tiles
-  double* zwork = nullptr;    // [ld]
   double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
-  int32_t* fail = nullptr;    // [1] Cholesky failure flag
+  int32_t* fail = nullptr;    // [1] bit 0: Cholesky pivot not positive; bit 1: back-substitution hand-off timeout
+  int32_t* flags = nullptr;   // [nblk] back-substitution hand-off flags (epoch-stamped)
   // Schur: upper-triangle blocks (c1, c2) in row-major order, CSR offsets
   // of their (o1, o2) pair lists, and the pairs (point-major ids)
   int64_t n_blk = 0, n_pairs = 0;
@@ -131,6 +131,6 @@ int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
 void launch_cholesky(const DevProblem& d, hipStream_t s);
-void launch_backsolve(const DevProblem& d, hipStream_t s);
+void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
 
 }  // namespace sfm

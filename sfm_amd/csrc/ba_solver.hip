@@ -55,6 +55,7 @@ struct sfm_ba_handle {
   // host copies needed for reordering / reset
   std::vector<int64_t> order;  // sorted position -> caller observation index
   std::vector<int32_t> pos;      // point-major q -> camera-major record index
+  int32_t bs_epoch = 0;          // stamp of the last back-substitution launch (k_backsolve flags)
   std::vector<void*> allocs;
   bool has_problem = false;
   // multi-GPU
@@ -200,7 +201,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
   launch_cholesky(d, s);
   mark_end(h);
   mark_begin(h, kPhBack);
-  launch_backsolve(d, s);
+  launch_backsolve(d, ++h->bs_epoch, s);
   mark_end(h);
   launch_cam_update(d, h->rank == 0, s);
   mark_begin(h, kPhBacksub);
@@ -479,7 +480,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.Ucam, size_t(kUcam) * C);
   ALLOC(d.S, size_t(d.ld) * d.ld);
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
-  ALLOC(d.zwork, size_t(d.ld));
+  ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
@@ -523,6 +524,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   H2D(d.seg, seg.data(), seg.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
+  HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
+  h->bs_epoch = 0;
   HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
   HIPCHK(hipStreamSynchronize(s));
   h->has_problem = true;
@@ -651,6 +654,7 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
       sm.num_linear_solves++;
       int chol_fail = 0;
       std::memcpy(&chol_fail, sc + kNumScalars, sizeof(int));
+      if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out");
       const bool solve_ok = chol_fail == 0 && !(sc[kBadStep] > 0.0) && !(sc[kBadCam] > 0.0) && !(sc[kBadBack] > 0.0);
       const double model_cost_change = sc[kModelChange];
       itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;
@@ -797,19 +801,20 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
     for (int i = j; i < n; ++i) img[size_t(j) * d.ld + i] = A[size_t(j) * n + i];  // row-major upper (j, i)
   for (int j = 0; j < n; ++j) img[size_t(j) * d.ld + n] = b[j];
   for (int j = n; j < d.ld; ++j) img[size_t(j) * d.ld + j] = 1.0;
-  double *S = nullptr, *S0 = nullptr, *invd = nullptr, *z = nullptr, *ys = nullptr;
-  int* fl = nullptr;
+  double *S = nullptr, *S0 = nullptr, *invd = nullptr, *ys = nullptr;
+  int *fl = nullptr, *flags = nullptr;
   const size_t bytes = sizeof(double) * img.size();
   hipStream_t s = nullptr;
   HIPCHK(hipStreamCreate(&s));
   HIPCHK(hipMalloc(&S, bytes));
   HIPCHK(hipMalloc(&S0, bytes));
   HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
-  HIPCHK(hipMalloc(&z, sizeof(double) * d.ld));
+  HIPCHK(hipMalloc(&flags, sizeof(int) * d.nblk));
+  HIPCHK(hipMemset(flags, 0, sizeof(int) * d.nblk));
   HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
   HIPCHK(hipMalloc(&fl, sizeof(int)));
   HIPCHK(hipMemcpy(S0, img.data(), bytes, hipMemcpyHostToDevice));
-  d.S = S; d.invL = invd; d.zwork = z; d.ysol = ys; d.fail = fl;
+  d.S = S; d.invL = invd; d.ysol = ys; d.fail = fl; d.flags = flags;
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
@@ -818,7 +823,7 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
     HIPCHK(hipMemcpyAsync(S, S0, bytes, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(e0, s));
     launch_cholesky(d, s);
-    launch_backsolve(d, s);
+    launch_backsolve(d, r + 1, s);
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     float m = 0.f;
@@ -831,7 +836,7 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
   if (chol_fail) *chol_fail = f;
   hipEventDestroy(e0); hipEventDestroy(e1);
-  hipFree(S); hipFree(S0); hipFree(invd); hipFree(z); hipFree(ys); hipFree(fl);
+  hipFree(S); hipFree(S0); hipFree(invd); hipFree(flags); hipFree(ys); hipFree(fl);
   hipStreamDestroy(s);
   return 0;
 }

@@ -301,67 +301,86 @@ __global__ __launch_bounds__(256) void k_chol_syrk(double* __restrict__ A, int l
         A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
 }
 
-// z <- row n of the factor (z = L^-1 rhs), y <- 0
-__global__ void k_copy_z(const double* __restrict__ A, int ld, int n, double* __restrict__ z, double* __restrict__ y) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < ld) {
-    z[j] = (j < n) ? A[size_t(j) * ld + n] : 0.0;
-    y[j] = 0.0;
-  }
-}
+// Back substitution L^T y = z (z = row n of the augmented factor, i.e.
+// L^-1 rhs), ONE launch: workgroup b owns block row b (64 unknowns) and
+//   y_b = W_b^T (z_b - sum_{k>b} L_kb^T y_k).
+// y_k are published block by block (descending) through device-scope flags
+// (producer: stores, fence, release store of the flag; consumer: acquire
+// poll by one lane, barrier, plain loads).  Every L_kb tile is prefetched
+// before its y_k is awaited, so the chain costs one flag hand-off per block
+// instead of one kernel launch per block.  All nb workgroups are co-resident
+// (nb <= a few hundred, one CU each); every wait is bounded and a timeout
+// sets bit 1 of *fail (reported as an error, never a hang).
+constexpr long kSpinLimit = 1L << 24;
 
-// One step of the blocked back substitution L^T y = z, tile k (descending):
-// y_k = W^T z_k (a 64x64 product, recomputed by every workgroup; workgroup 0
-// stores it), then thread l of workgroup b updates z_j, j = 256b + l < k0:
-//   z_j -= sum_r L(k0 + r, j) y_k[r]
-// from its column's 64 contiguous doubles, prefetched first.
-__global__ __launch_bounds__(256) void k_backsolve_step(const double* __restrict__ A, int ld, int n, int k,
-                                                        const double* __restrict__ Winv, double* __restrict__ z,
-                                                        double* __restrict__ y) {
-  __shared__ double zk[NB];
-  __shared__ double part[4][NB];
-  __shared__ double yk[NB];
-  const int k0 = k * NB;
+__global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
+                                                   const double* __restrict__ Winv, double* __restrict__ y,
+                                                   int* __restrict__ flags, int epoch, int* __restrict__ fail) {
+  __shared__ double v[NB];
+  __shared__ int timed_out;
+  const int b = nb - 1 - blockIdx.x;  // the chain's first block is the first workgroup
+  const int k0 = b * NB;
   const int nreal = (n - k0) < NB ? (n - k0) : NB;
-  const int t = threadIdx.x, r = t & 63, q = t >> 6;
-  const int j = blockIdx.x * 256 + t;
-  const bool upd = j < k0;
-  double col[NB];
-  if (upd) {
+  const int t = threadIdx.x, col = t >> 2, seg = t & 3;
+  if (t == 0) timed_out = 0;
+  // off the chain: this block's z entry and W_b row (thread t < 64 -> y_b[t])
+  const double zc = (seg == 0 && col < nreal) ? A[size_t(k0 + col) * ld + n] : 0.0;
+  double wr[NB];
+  if (t < NB) {
+    const double* Wr = Winv + size_t(b) * NB * NB + size_t(t) * NB;  // W(c, t), c = 0..63
 #pragma unroll
-    for (int p = 0; p < NB / 2; ++p) {
-      const double2 v2 = *reinterpret_cast<const double2*>(A + size_t(j) * ld + k0 + 2 * p);
-      col[2 * p] = v2.x;
-      col[2 * p + 1] = v2.y;
+    for (int c = 0; c < NB; c += 2) {
+      const double2 q = *reinterpret_cast<const double2*>(Wr + c);
+      wr[c] = q.x;
+      wr[c + 1] = q.y;
     }
   }
-  // y_k[r] = sum_c W(c, r) z_k[c], W(c, r) = Wc[r][c]; quarter q sums c in [16q, 16q + 16)
-  const double* Wr = Winv + size_t(k) * NB * NB + size_t(r) * NB + 16 * q;
-  double wv[16];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const double2 v2 = *reinterpret_cast<const double2*>(Wr + 2 * p);
-    wv[2 * p] = v2.x;
-    wv[2 * p + 1] = v2.y;
-  }
-  if (t < NB) zk[t] = (t < nreal) ? z[k0 + t] : 0.0;
   __syncthreads();
-  double s = 0.0;
+  double acc = 0.0;
+  // column k0 + col, rows 64k + 16 seg .. +16 of tile (k, b)
+  const double* colp = A + size_t(k0 + col) * ld + 16 * seg;
+  for (int k = nb - 1; k > b; --k) {
+    double lv[16];
 #pragma unroll
-  for (int p = 0; p < 16; ++p) s = fma(wv[p], zk[16 * q + p], s);
-  part[q][r] = s;
+    for (int i = 0; i < 16; i += 2) {
+      const double2 q = *reinterpret_cast<const double2*>(colp + size_t(k) * NB + i);
+      lv[i] = q.x;
+      lv[i + 1] = q.y;
+    }
+    if (t == 0) {
+      long spins = 0;
+      while (__hip_atomic_load(flags + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        if (++spins > kSpinLimit) { timed_out = 1; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (timed_out) break;
+    const double* yk = y + size_t(k) * NB + 16 * seg;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      const double2 q = *reinterpret_cast<const double2*>(yk + i);
+      acc = fma(lv[i], q.x, acc);
+      acc = fma(lv[i + 1], q.y, acc);
+    }
+  }
+  // the four row segments of a column sit in adjacent lanes
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  if (seg == 0) v[col] = (col < nreal) ? zc - acc : 0.0;
   __syncthreads();
   if (t < NB) {
-    const double v = (t < nreal) ? (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]) : 0.0;
-    yk[t] = v;
-    if (blockIdx.x == 0 && t < nreal) y[k0 + t] = v;
-  }
-  __syncthreads();
-  if (upd) {
-    double acc = 0.0;
+    // y_b[t] = sum_c W(c, t) v[c]
+    double s = 0.0;
 #pragma unroll
-    for (int rr = 0; rr < NB; ++rr) acc = fma(col[rr], yk[rr], acc);
-    z[j] -= acc;
+    for (int c = 0; c < NB; ++c) s = fma(wr[c], v[c], s);
+    y[size_t(k0) + t] = (t < nreal) ? s : 0.0;
+  }
+  __threadfence();
+  __syncthreads();
+  if (t == 0) {
+    if (timed_out) atomicOr(fail, 2);
+    __hip_atomic_store(flags + b, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -381,11 +400,9 @@ void launch_cholesky(const DevProblem& d, hipStream_t s) {
   }
 }
 
-void launch_backsolve(const DevProblem& d, hipStream_t s) {
-  k_copy_z<<<(d.ld + 255) / 256, 256, 0, s>>>(d.S, d.ld, d.n, d.zwork, d.ysol);
+void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s) {
   const int nb_real = (d.n + NB - 1) / NB;
-  for (int k = nb_real - 1; k >= 0; --k)
-    k_backsolve_step<<<k > 0 ? (k + 3) / 4 : 1, 256, 0, s>>>(d.S, d.ld, d.n, k, d.invL, d.zwork, d.ysol);
+  if (nb_real > 0) k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.flags, epoch, d.fail);
 }
 
 }  // namespace sfm

@@ -1,7 +1,8 @@
 import csv, sys, glob
 f = sys.argv[1]
 if not f.endswith('.csv'):
-    f = glob.glob(f + '/**/*kernel_stats.csv', recursive=True)[0]
+    import os
+    f = max(glob.glob(f + '/**/*kernel_stats.csv', recursive=True), key=os.path.getmtime)
 rows = list(csv.DictReader(open(f)))
 for r in rows:
     n = r['Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('sfm::', '')
