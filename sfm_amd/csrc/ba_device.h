@@ -59,6 +59,7 @@ struct DevProblem {
   int32_t* cm_p = nullptr;     // [N_pad] point index at camera-major position i
   int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
   int32_t n_jchunks = 0;
+  int32_t* jgrp = nullptr;     // [9] chunk-table offsets of the 8 point slices (one per XCD)
   int32_t jac_blocks = 1;      // persistent grid of k_jacobian (cost partials)
   double* uv_cm = nullptr;     // [N_pad][2] uv in camera-major order
   int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q (jrec index)
@@ -88,6 +89,7 @@ struct DevProblem {
   // n = 6C unknowns, row n holds the reduced right-hand side (augmented).
   int32_t n = 0, ld = 0, nblk = 0;
   double* S = nullptr;
+  double* Spack = nullptr;    // [n(n+1)/2 + n] packed upper triangle + rhs (cross-rank all-reduce)
   double* invL = nullptr;     // [nblk][64][64] inverses of the diagonal tiles
   double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
   int32_t* fail = nullptr;    // [1] bit 0: Cholesky pivot not positive; bit 1: back-substitution hand-off timeout
@@ -123,6 +125,7 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s);
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
 void launch_pad_init(const DevProblem& d, hipStream_t s);
+void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
 void launch_point_backsub(const DevProblem& d, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]

@@ -55,6 +55,16 @@ __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_ca
 __device__ __forceinline__ void st2(double* p, double a, double b) {
   *reinterpret_cast<double2*>(p) = make_double2(a, b);
 }
+// Streaming (non-temporal) 16-B store for write-once outputs that the same
+// kernel never re-reads: on gfx950 the record stream of the Jacobian pass
+// runs at ~5.4 TB/s this way against ~3 TB/s with plain stores (measured:
+// plain write-allocating stores evict the L2-resident point data the
+// gathers need and stall the store path).
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st2_nt(double* p, double a, double b) {
+  const f64x2 v = {a, b};
+  __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
+}
 
 // Rotation matrix R(w) with the branch of ceres::AngleAxisRotatePoint:
 // theta^2 > DBL_EPSILON -> Rodrigues; otherwise the first-order map I + [w]x.
@@ -156,7 +166,7 @@ __device__ __forceinline__ void jac_flush(const double* wst, double* __restrict_
 #pragma unroll
   for (int kq = 0; kq < kJRec / 2; ++kq) v[kq] = ld2(wst + 2 * (64 * kq + l));
 #pragma unroll
-  for (int kq = 0; kq < kJRec / 2; ++kq) *reinterpret_cast<double2*>(dst + 2 * (64 * kq + l)) = v[kq];
+  for (int kq = 0; kq < kJRec / 2; ++kq) st2_nt(dst + 2 * (64 * kq + l), v[kq].x, v[kq].y);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -206,7 +216,8 @@ __device__ __forceinline__ double jac_record(const double* cr, double tc0, doubl
 // stores on CDNA, so a wait on a load also covers every older store):
 //   [X_t, uv_t in flight] issue p_{t+1}, uv_{t+1} -> wait X_t -> compute t
 //   -> stage t in LDS -> issue X_{t+1} -> store chunk t.
-__global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4* __restrict__ chunks,
+__global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict__ grp_off,
+                                                       const int4* __restrict__ chunks,
                                                        const int32_t* __restrict__ cm_p,
                                                        const double* __restrict__ uv_cm,
                                                        const double* __restrict__ Kc, const double* __restrict__ cam,
@@ -219,41 +230,62 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4*
   const int l = threadIdx.x & 63;
   const int wv = wave_uniform(threadIdx.x >> 6);
   double* wst = stage + wv * 64 * kJRec;
-  const int stride = gridDim.x * (kThreads / 64);
+  // XCD-aware split: the chunk table is grouped into 8 slices of the point
+  // range (a camera's list is sorted by point, so each chunk covers a narrow
+  // slice); workgroup b serves slice b % 8 -- the round-robin workgroup ->
+  // XCD dispatch puts each slice on one XCD, whose 4-MB L2 then holds that
+  // slice's X (0.6 MB at C3) instead of every XCD gathering all 4.8 MB.
+  // (Placement is a speed assumption only; any mapping is correct.)
+  const int grp = blockIdx.x & 7;
+  const int nbg = (int(gridDim.x) - 1 - grp) / 8 + 1;
+  const int n_chunks = grp_off[grp + 1];
+  const int stride = nbg * (kThreads / 64);
   double cost = 0.0;
-  int t = blockIdx.x * (kThreads / 64) + wv;
+  int t = grp_off[grp] + (blockIdx.x >> 3) * (kThreads / 64) + wv;
   // Lanes past the real observations of a camera's last chunk compute the
   // padding slots (copies of its last observation): every load and store is
   // unpredicated, so nothing forces an early wait; padding records are never
   // read back and their cost is masked.
-  // prologue: p_t, uv_t, then X_t / scale_p_t in flight
-  int p_cur = 0;
-  double2 uv_cur = make_double2(0.0, 0.0);
+  // Prefetch depths: point index 2 chunks ahead, uv and X one chunk ahead,
+  // so the only load a wave ever waits for right after issuing stores is
+  // one issued a whole chunk earlier (vmcnt counts loads and stores in issue
+  // order: waiting on a young load would also wait on the stores before it).
+  auto chunk_at = [&](int tt) { return chunks[tt < n_chunks ? tt : t]; };
+  int p_nxt = 0;                              // point index of chunk t + stride
+  double2 uv_cur = make_double2(0.0, 0.0);    // chunk t
   double Xc[3] = {0.0, 0.0, 1.0}, spc[3] = {1.0, 1.0, 1.0};
   if (t < n_chunks) {
-    const int4 ch = chunks[t];
-    const int64_t i = int64_t(ch.y) + l;
-    p_cur = cm_p[i];
+    const int64_t i = int64_t(chunks[t].y) + l;
+    const int p0 = cm_p[i];
     uv_cur = ld2(uv_cm + 2 * i);
+    p_nxt = cm_p[int64_t(chunk_at(t + stride).y) + l];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p_cur) + j];
+    for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p0) + j];
     if (scaled)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) spc[j] = scale_p[3 * size_t(p_cur) + j];
+      for (int j = 0; j < 3; ++j) spc[j] = scale_p[3 * size_t(p0) + j];
   }
+  // materialise the prologue loads here, so the loop entry carries no
+  // outstanding loads from this path (the compiler's wait counting merges
+  // the prologue and back-edge states conservatively)
+  asm volatile("" : "+v"(Xc[0]), "+v"(Xc[1]), "+v"(Xc[2]), "+v"(spc[0]), "+v"(spc[1]), "+v"(spc[2]), "+v"(uv_cur.x),
+               "+v"(uv_cur.y), "+v"(p_nxt));
   for (; t < n_chunks; t += stride) {
     const int4 ch = chunks[t];
     const int c = ch.x, cnt = ch.z;
     const int64_t ib = ch.y;
-    // next chunk's index + uv
-    const int tn = t + stride;
-    const bool has_next = tn < n_chunks;
-    const int4 cn = chunks[has_next ? tn : t];
-    const int64_t inx = int64_t(cn.y) + l;
-    const int p_nxt = cm_p[inx];
-    const double2 uv_nxt = ld2(uv_cm + 2 * inx);
-    // camera data (wave-uniform -> scalar loads)
-    const double* cr = camR + size_t(kCamR) * c;
+    // ---- issue: X / scale of chunk t+1 (its index is already here), uv of
+    // chunk t+1, index of chunk t+2 ----
+    double Xn[3], spn[3] = {1.0, 1.0, 1.0};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Xn[j] = X[3 * size_t(p_nxt) + j];
+    if (scaled)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) spn[j] = scale_p[3 * size_t(p_nxt) + j];
+    const double2 uv_nxt = ld2(uv_cm + 2 * (int64_t(chunk_at(t + stride).y) + l));
+    const int p_nn = cm_p[int64_t(chunk_at(t + 2 * stride).y) + l];
+    // ---- chunk t ----
+    const double* cr = camR + size_t(kCamR) * c;  // camera data: wave-uniform -> scalar loads
     const double* k = Kc + 5 * size_t(c);
     double sc[6];
 #pragma unroll
@@ -268,16 +300,12 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(int n_chunks, const int4*
       for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
     }
     wave_lds_sync();
-    // next chunk's point data
-    p_cur = p_nxt;
-    uv_cur = uv_nxt;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p_cur) + j];
-    if (scaled)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) spc[j] = scale_p[3 * size_t(p_cur) + j];
     jac_flush(wst, jrec, ib, l);
     wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { Xc[j] = Xn[j]; spc[j] = spn[j]; }
+    uv_cur = uv_nxt;
+    p_nxt = p_nn;
   }
   const double r = block_reduce(cost, sh, false);
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
@@ -589,6 +617,26 @@ __global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restri
   }
 }
 
+// Packed form of the reduced system for the cross-rank all-reduce: row i
+// of the row-major upper triangle, columns i..n (the rhs column n
+// included), at offset i(n+1) - i(i-1)/2.  Half the bytes of the full ld^2
+// image, and none of the stale factor entries outside the triangle.
+__device__ __forceinline__ size_t packed_row(int i, int n) { return size_t(i) * (n + 1) - size_t(i) * (i - 1) / 2; }
+
+__global__ void k_pack_upper(const double* __restrict__ S, int ld, int n, double* __restrict__ P) {
+  const int i = blockIdx.x;
+  const double* row = S + size_t(i) * ld;
+  double* dst = P + packed_row(i, n) - i;
+  for (int j = i + threadIdx.x; j <= n; j += blockDim.x) dst[j] = row[j];
+}
+
+__global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, double* __restrict__ S) {
+  const int i = blockIdx.x;
+  double* row = S + size_t(i) * ld;
+  const double* src = P + packed_row(i, n) - i;
+  for (int j = i + threadIdx.x; j <= n; j += blockDim.x) row[j] = src[j];
+}
+
 // Identity padding beyond the augmented row n (column-major lower view).
 __global__ void k_pad_init(double* __restrict__ S, int ld, int n) {
   const int j = blockIdx.x;
@@ -736,7 +784,7 @@ void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hi
   k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
-  k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.n_jchunks, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
+  k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
                                                 d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost));
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
@@ -763,6 +811,11 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
     k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
   k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
                                         add_diag ? 1 : 0, d.S, d.ld, d.n);
+}
+void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
+  if (d.n == 0) return;
+  if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S);
+  else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {

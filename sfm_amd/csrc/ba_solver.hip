@@ -14,6 +14,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -56,6 +57,7 @@ struct sfm_ba_handle {
   std::vector<int64_t> order;  // sorted position -> caller observation index
   std::vector<int32_t> pos;      // point-major q -> camera-major record index
   int32_t bs_epoch = 0;          // stamp of the last back-substitution launch (k_backsolve flags)
+  bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
   std::vector<void*> allocs;
   bool has_problem = false;
   // multi-GPU
@@ -119,6 +121,8 @@ void collect_marks(sfm_ba_handle* h) {
   h->ev_marks.clear();
   h->ev_used = 0;
 }
+
+size_t packed_size(int n) { return size_t(n) * (n + 1) / 2 + size_t(n); }
 
 int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
   if (h->nranks <= 1) return 0;
@@ -195,7 +199,12 @@ int compute_step(sfm_ba_handle* h, double radius) {
   mark_begin(h, kPhSchur);
   launch_schur(d, radius, h->rank == 0, s);
   mark_end(h);
-  if ((rc = allreduce(h, d.S, size_t(d.ld) * d.ld, ncclSum))) return rc;
+  if (h->nranks > 1 || h->force_pack) {
+    // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
+    launch_pack_upper(d, false, s);
+    if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
+    launch_pack_upper(d, true, s);
+  }
   launch_pad_init(d, s);
   mark_begin(h, kPhChol);
   launch_cholesky(d, s);
@@ -373,23 +382,32 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     npad += (n_c + 63) / 64 * 64;
   }
   d.N_pad = npad;
-  // (camera, first position, count, 0) per wavefront chunk, issued
-  // piece-major: a camera's list is sorted by point, so piece k of every
-  // camera covers about the same slice of the points and the waves in
-  // flight gather X from a narrow range.
-  std::vector<int32_t> jchunks;
-  for (int32_t k = 0;; ++k) {
-    bool any = false;
-    for (int c = 0; c < C; ++c) {
-      const int32_t n_c = cam_off[c + 1] - cam_off[c];
-      if (64 * k >= n_c) continue;
-      any = true;
-      jchunks.insert(jchunks.end(), {c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), 0});
+  // (camera, first position, count, 0) per wavefront chunk, in 8 groups by
+  // the point slice of the chunk's first observation (k_jacobian serves
+  // group b % 8 from workgroup b: one slice of X per XCD's L2); within a
+  // group, piece-major across cameras.
+  std::vector<int32_t> jchunks, jgrp(9, 0);
+  {
+    std::vector<std::vector<int32_t>> grp(8);
+    for (int32_t k = 0;; ++k) {
+      bool any = false;
+      for (int c = 0; c < C; ++c) {
+        const int32_t n_c = cam_off[c + 1] - cam_off[c];
+        if (64 * k >= n_c) continue;
+        any = true;
+        const int32_t p0 = pt_s[cam_obs[cam_off[c] + 64 * k]];
+        const int g = int(int64_t(p0) * 8 / std::max(1, P));
+        grp[g].insert(grp[g].end(), {c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), 0});
+      }
+      if (!any) break;
     }
-    if (!any) break;
+    for (int g = 0; g < 8; ++g) {
+      jchunks.insert(jchunks.end(), grp[g].begin(), grp[g].end());
+      jgrp[g + 1] = int32_t(jchunks.size() / 4);
+    }
   }
   d.n_jchunks = int32_t(jchunks.size() / 4);
-  d.jac_blocks = std::max(1, std::min((d.n_jchunks + 3) / 4, 1024));
+  d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
   // camera-major copies for the Jacobian pass and the record map
   std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1);
   std::vector<double> uv_cm(2 * size_t(npad), 0.0);
@@ -457,6 +475,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.cam_rng, 2 * size_t(C));
   ALLOC(d.cm_p, size_t(npad));
   ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
+  ALLOC(d.jgrp, size_t(9));
   ALLOC(d.uv_cm, 2 * size_t(npad));
   ALLOC(d.pos, size_t(N));
   ALLOC(d.Kc, 5 * size_t(C));
@@ -479,6 +498,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.ptL, size_t(kPtL) * P);
   ALLOC(d.Ucam, size_t(kUcam) * C);
   ALLOC(d.S, size_t(d.ld) * d.ld);
+  h->force_pack = std::getenv("SFM_FORCE_PACK") && std::getenv("SFM_FORCE_PACK")[0] == '1';
+  if (h->nranks > 1 || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.ysol, size_t(d.ld));
@@ -507,6 +528,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     h->pos = pos;
   }
   H2D(d.pt_off, pt_off.data(), size_t(P) + 1);
+  H2D(d.jgrp, jgrp.data(), size_t(9));
   if (C) H2D(d.cam_rng, cam_rng.data(), 2 * size_t(C));
   if (C) {
     H2D(d.Kc, Kc.data(), 5 * size_t(C));
