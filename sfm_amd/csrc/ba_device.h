@@ -80,8 +80,8 @@ struct DevProblem {
   double* camR = nullptr;     // [C][36]
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
   double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12)
-  double* frec = nullptr;     // [N][18] F = J_c^T M (point-major): Schur pair blocks F_o1 F_o2^T
-  double* mrec = nullptr;     // [N][8]
+  double* frec = nullptr;     // [N_pad][18] F = J_c^T M at the camera-major position: Schur pair blocks F_o1 F_o2^T
+  double* mrec = nullptr;     // [N_pad][8] M = J_X L^-T (2x3) and h = M z at the camera-major position
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]
   double* Ucam = nullptr;     // [C][28]

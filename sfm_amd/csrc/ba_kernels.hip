@@ -424,16 +424,11 @@ __global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* _
   }
 }
 
-// Per-iteration point factorisation (depends on the trust-region radius):
-// V_p + D_p^2 = L L^T, z = L^-1 b_p, and per observation M = J_X L^-T,
-// h = M z (the ingredients of W V^-1 W^T and W V^-1 b).
-__global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* __restrict__ pt_off,
-                                                         const int32_t* __restrict__ pos,
-                                                         const double* __restrict__ jrec, const double* __restrict__ ptV,
-                                                         const double* __restrict__ diag_p, double radius,
-                                                         double* __restrict__ mrec, double* __restrict__ frec,
-                                                         double* __restrict__ ptL,
-                                                         double* __restrict__ part_bad) {
+// Per-iteration point factorisation (depends on the trust-region radius),
+// one lane per point: V_p + D_p^2 = L L^T, z = L^-1 b_p -> ptL.
+__global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* __restrict__ ptV,
+                                                           const double* __restrict__ diag_p, double radius,
+                                                           double* __restrict__ ptL, double* __restrict__ part_bad) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double bad = 0.0;
@@ -451,33 +446,68 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int P, const int32_t* _
     const double z0 = v[6] / l00, z1 = (v[7] - l10 * z0) / l11, z2 = (v[8] - l20 * z0 - l21 * z1) / l22;
     double* L = ptL + size_t(kPtL) * p;
     st2(L, l00, l10); st2(L + 2, l11, l20); st2(L + 4, l21, l22); st2(L + 6, z0, z1); st2(L + 8, z2, 0.0);
-    const int q0 = pt_off[p], q1 = pt_off[p + 1];
-    for (int q = q0; q < q1; ++q) {
-      const double* J = jrec + size_t(pos[q]) * kJRec;
-      const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
-      const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
-      const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
-      double* M = mrec + size_t(q) * kMRec;
-      st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
-      st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
-      // F = J_c^T M (6x3, row-major): the Schur pair block is F_o1 F_o2^T
-      double jc[12];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
-      double F[kFRec];
-#pragma unroll
-      for (int u = 0; u < 6; ++u) {
-        F[3 * u] = jc[u] * m0 + jc[6 + u] * n0;
-        F[3 * u + 1] = jc[u] * m1 + jc[6 + u] * n1;
-        F[3 * u + 2] = jc[u] * m2 + jc[6 + u] * n2;
-      }
-      double* Fo = frec + size_t(q) * kFRec;
-#pragma unroll
-      for (int f = 0; f < kFRec; f += 2) st2(Fo + f, F[f], F[f + 1]);
-    }
   }
   const double r = block_reduce(bad, sh, true);
   if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
+}
+
+// Per observation, one lane per CAMERA-major position (the J records
+// stream; the point's factor is a 80-B gather):  M = J_X L^-T, h = M z
+// (the ingredients of W V^-1 W^T and W V^-1 b) -> mrec, and F = J_c^T M
+// (6x3, the Schur pair block is F_o1 F_o2^T) -> frec, both at the same
+// camera-major position, so the row camera's terms stream in k_schur_diag.
+// A wavefront's 64 records of each kind are one contiguous run (camera
+// runs are padded to whole wavefronts; padding lanes compute a copy of the
+// camera's last observation, never read): they are staged in LDS and
+// leave as full 1-KB rows with streaming stores, like the Jacobian records.
+__global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int32_t* __restrict__ cm_p,
+                                                       const double* __restrict__ jrec,
+                                                       const double* __restrict__ ptL, double* __restrict__ mrec,
+                                                       double* __restrict__ frec) {
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kMRec + kFRec)];  // 13 KB per wave
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t(blockIdx.x) * kThreads) + 64 * wv;  // first position of this wavefront
+  if (i0 >= N_pad) return;  // whole wavefronts (N_pad is a multiple of 64)
+  const int64_t i = i0 + l;
+  const double* L = ptL + size_t(kPtL) * cm_p[i];
+  const double2 a0 = ld2(L), a1 = ld2(L + 2), a2 = ld2(L + 4), a3 = ld2(L + 6), a4 = ld2(L + 8);
+  const double l00 = a0.x, l10 = a0.y, l11 = a1.x, l20 = a1.y, l21 = a2.x, l22 = a2.y;
+  const double z0 = a3.x, z1 = a3.y, z2 = a4.x;
+  const double* J = jrec + size_t(i) * kJRec;
+  const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
+  const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
+  const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
+  double* sm = stage[wv];                 // [64][8]  M records
+  double* sf = stage[wv] + 64 * kMRec;    // [64][18] F records
+  double* M = sm + l * kMRec;
+  st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
+  st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
+  double jc[12];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+  double* Fo = sf + l * kFRec;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const double f0 = jc[u] * m0 + jc[6 + u] * n0;
+    const double f1 = jc[u] * m1 + jc[6 + u] * n1;
+    const double f2 = jc[u] * m2 + jc[6 + u] * n2;
+    Fo[3 * u] = f0; Fo[3 * u + 1] = f1; Fo[3 * u + 2] = f2;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double* dm = mrec + i0 * kMRec;
+  double* df = frec + i0 * kFRec;
+#pragma unroll
+  for (int kq = 0; kq < kMRec / 2; ++kq) {
+    const double2 v = ld2(sm + 2 * (64 * kq + l));
+    st2_nt(dm + 2 * (64 * kq + l), v.x, v.y);
+  }
+#pragma unroll
+  for (int kq = 0; kq < kFRec / 2; ++kq) {
+    const double2 v = ld2(sf + 2 * (64 * kq + l));
+    st2_nt(df + 2 * (64 * kq + l), v.x, v.y);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -563,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restri
   for (int e = 0; e < 6; ++e) rhs[e] = 0.0;
   for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
     const double* J1p = jrec + size_t(i) * kJRec;
-    const double* M1p = mrec + size_t(cam_obs[i]) * kMRec;
+    const double* M1p = mrec + size_t(i) * kMRec;  // camera-major: streamed
     double J1[12], M1[8];
 #pragma unroll
     for (int k = 0; k < 6; ++k) { const double2 v = ld2(J1p + kJC + 2 * k); J1[2 * k] = v.x; J1[2 * k + 1] = v.y; }
@@ -701,7 +731,7 @@ __global__ __launch_bounds__(kThreads) void k_point_backsub(
     for (int q = q0; q < q1; ++q) {
       const int c = obs_cam[q];
       const double* J = jrec + size_t(pos[q]) * kJRec + kJC;
-      const double* M = mrec + size_t(q) * kMRec;
+      const double* M = mrec + size_t(pos[q]) * kMRec;
       const double* y = ysol + 6 * size_t(c);
       double e0 = 0.0, e1 = 0.0;
 #pragma unroll
@@ -802,9 +832,10 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
                                                              slot(d, kPGradPt), slot(d, kPXNormPt));
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
-  if (d.P == 0) return;
-  k_point_prep<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.ptV, d.diag_p, radius, d.mrec, d.frec,
-                                                             d.ptL, slot(d, kPBad));
+  if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
+                                                                         slot(d, kPBad));
+  if (d.N_pad)
+    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   if (d.n_blk)

@@ -435,7 +435,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // ---- Schur blocks (k_schur): every upper-triangle block (c1, c2),
   // c1 <= c2, in row-major order, with the CSR list of its (o1, o2) pairs:
   // observations of a common point with cameras c1 and c2 (o2 != o1; on the
-  // diagonal only same-camera duplicates).  Pairs are point-major ids. ----
+  // diagonal only same-camera duplicates), as camera-major record positions. ----
   std::vector<int32_t> blk, seg, pairs;
   {
     std::vector<std::vector<std::pair<int32_t, int32_t>>> cols(C);
@@ -445,7 +445,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
         const int32_t o1 = cam_obs[i];
         const int p = pt_s[o1];
         for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
-          if (cam_s[o2] >= c1 && o2 != o1) cols[cam_s[o2]].push_back({o1, o2});
+          if (cam_s[o2] >= c1 && o2 != o1) cols[cam_s[o2]].push_back({pos[o1], pos[o2]});
       }
       for (int c2 = c1; c2 < C; ++c2) {
         blk.push_back(c1);
@@ -492,8 +492,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.camR, size_t(kCamR) * C);
   ALLOC(d.camRn, 12 * size_t(C));
   ALLOC(d.jrec, size_t(kJRec) * npad);
-  ALLOC(d.mrec, size_t(kMRec) * N);
-  ALLOC(d.frec, size_t(kFRec) * N);
+  ALLOC(d.mrec, size_t(kMRec) * npad);
+  ALLOC(d.frec, size_t(kFRec) * npad);
   ALLOC(d.ptV, size_t(kPtV) * P);
   ALLOC(d.ptL, size_t(kPtL) * P);
   ALLOC(d.Ucam, size_t(kUcam) * C);
