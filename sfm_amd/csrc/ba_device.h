@@ -16,7 +16,8 @@ constexpr int kJX = 0, kRes = 6, kJC = 8;
 // Per-observation Schur record written every LM iteration:
 //   [0..5] M = J_X L_p^-T (2 x 3)   [6..7] h = M z_p
 constexpr int kMRec = 8;
-constexpr int kFRec = 18;  // F = J_c^T M per observation (6x3), point-major
+constexpr int kFRec = 18;
+constexpr int kEU = 6;     // back substitution: e = J_c y_c (2) | u = M^T e (3) | pad  // F = J_c^T M per observation (6x3), point-major
 // Per-camera rotation data: R (9, row-major) and dR/dw_k (27, k-major).
 constexpr int kCamR = 36;
 // Per-camera reduction record: U (21, packed upper 6x6), b_c (6), pad.
@@ -49,9 +50,6 @@ struct DevProblem {
   int32_t C = 0, P = 0;      // cameras (global), points (this shard)
   int64_t N = 0;             // observations (this shard)
   // structure (point-major observation order; within a point by camera)
-  double* uv = nullptr;        // [N][2]
-  int32_t* obs_cam = nullptr;  // [N]
-  int32_t* obs_pt = nullptr;   // [N]
   int32_t* pt_off = nullptr;   // [P+1]
   int64_t N_pad = 0;           // camera-major positions incl. per-camera padding to 64
   int32_t* cam_obs = nullptr;  // [N_pad] point-major observation id at camera-major position (-1: padding)
@@ -81,6 +79,9 @@ struct DevProblem {
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
   double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12)
   double* frec = nullptr;     // [N_pad][18] F = J_c^T M at the camera-major position: Schur pair blocks F_o1 F_o2^T
+  double* eu = nullptr;       // [N_pad][6] back substitution pass A output (camera-major)
+  double* ypt = nullptr;      // [P][3] point steps y_p (scaled space)
+  int32_t* wcam = nullptr;    // [N_pad / 64] camera of each camera-major wavefront (runs padded to 64)
   double* mrec = nullptr;     // [N_pad][8] M = J_X L^-T (2x3) and h = M z at the camera-major position
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]

@@ -707,84 +707,142 @@ __global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __
   if (threadIdx.x == 0) part_bad[blockIdx.x] = rb;
 }
 
-// Point back-substitution + model cost change + candidate cost, one lane per
-// point:  y_p = L^-T (z - sum_o M_o^T (J_c,o y_c)),  delta_p = -y_p,
-//   model residual q_o = J_s delta = -(J_c y_c + J_X y_p),
-//   model cost change -= q . (r + q/2)   (ceres trust_region_minimizer),
-//   candidate residual at (cam_new, X + s*delta_p).
-__global__ __launch_bounds__(kThreads) void k_point_backsub(
-    int P, const int32_t* __restrict__ pt_off, const int32_t* __restrict__ obs_cam, const int32_t* __restrict__ pos,
-    const double* __restrict__ uv,
-    const double* __restrict__ Kc, const double* __restrict__ jrec, const double* __restrict__ mrec,
-    const double* __restrict__ ptL, const double* __restrict__ ysol, const double* __restrict__ scale_p,
-    const double* __restrict__ X, double* __restrict__ X_new, const double* __restrict__ camRn,
-    double* __restrict__ part_model, double* __restrict__ part_cost, double* __restrict__ part_step,
-    double* __restrict__ part_bad) {
+// ---------------------------------------------------------------------------
+// Point back substitution, model cost change and candidate cost, in three
+// passes so that every per-observation array is streamed in camera-major
+// order and only per-point quantities are gathered:
+//   A (camera-major, one wavefront = 64 positions of one camera):
+//       e_o = J_c,o y_c,  u_o = M_o^T e_o               -> eu[i] (e 2 | u 3)
+//   B (one lane per point):  y_p = L^-T (z_p - sum_o u_o),  delta_p = -y_p,
+//       X_new = X + s_p delta_p, |dX|^2, finite check  -> ypt[p], X_new
+//   C (camera-major): model residual q_o = -(e_o + J_X,o y_p),
+//       model cost change -= q . (r + q/2)   (ceres trust_region_minimizer),
+//       candidate residual at (cam_new, X_new).
+// Camera runs are padded to whole wavefronts, so a wavefront never spans two
+// cameras (its camera comes from wcam) and padding lanes are masked.
+__global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                        const double* __restrict__ jrec,
+                                                        const double* __restrict__ mrec,
+                                                        const double* __restrict__ ysol, double* __restrict__ eu) {
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kEU];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
+  if (i0 >= N_pad) return;
+  const int64_t i = i0 + l;
+  const double* y = ysol + 6 * size_t(wcam[i0 >> 6]);  // wave-uniform
+  const double* J = jrec + size_t(i) * kJRec + kJC;
+  const double* M = mrec + size_t(i) * kMRec;
+  double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
+  const double2 m01 = ld2(M), m23 = ld2(M + 2), m45 = ld2(M + 4);
+  // M row-major 2x3 (m0 m1 m2 | n0 n1 n2) = M[0..5];  u = M^T e
+  double* o = stage[wv] + l * kEU;
+  st2(o, e0, e1);
+  st2(o + 2, m01.x * e0 + m23.y * e1, m01.y * e0 + m45.x * e1);
+  st2(o + 4, m23.x * e0 + m45.y * e1, 0.0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double* dst = eu + i0 * kEU;
+#pragma unroll
+  for (int kq = 0; kq < kEU / 2; ++kq) {
+    const double2 v = ld2(stage[wv] + 2 * (64 * kq + l));
+    st2_nt(dst + 2 * (64 * kq + l), v.x, v.y);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __restrict__ pt_off,
+                                                        const int32_t* __restrict__ pos,
+                                                        const double* __restrict__ eu,
+                                                        const double* __restrict__ ptL,
+                                                        const double* __restrict__ scale_p,
+                                                        const double* __restrict__ X, double* __restrict__ X_new,
+                                                        double* __restrict__ ypt, double* __restrict__ part_step,
+                                                        double* __restrict__ part_bad) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  double model = 0.0, ncost = 0.0, st = 0.0, bad = 0.0;
+  double st = 0.0, bad = 0.0;
   if (p < P) {
     const double* L = ptL + size_t(kPtL) * p;
     const double l00 = L[0], l10 = L[1], l11 = L[2], l20 = L[3], l21 = L[4], l22 = L[5];
     double w0 = L[6], w1 = L[7], w2 = L[8];
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      const int c = obs_cam[q];
-      const double* J = jrec + size_t(pos[q]) * kJRec + kJC;
-      const double* M = mrec + size_t(pos[q]) * kMRec;
-      const double* y = ysol + 6 * size_t(c);
-      double e0 = 0.0, e1 = 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
-      w0 -= M[0] * e0 + M[3] * e1;
-      w1 -= M[1] * e0 + M[4] * e1;
-      w2 -= M[2] * e0 + M[5] * e1;
+      const double* u = eu + size_t(pos[q]) * kEU + 2;
+      const double2 u01 = ld2(u);
+      w0 -= u01.x;
+      w1 -= u01.y;
+      w2 -= u[2];
     }
     const double y2 = w2 / l22;
     const double y1 = (w1 - l21 * y2) / l11;
     const double y0 = (w0 - l10 * y1 - l20 * y2) / l00;
     if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) bad = 1.0;
     const double yp[3] = {y0, y1, y2};
-    double Xn[3];
     for (int k = 0; k < 3; ++k) {
       const double x = X[3 * size_t(p) + k];
-      Xn[k] = x + scale_p[3 * size_t(p) + k] * (-yp[k]);
-      const double d = x - Xn[k];
+      const double xn = x + scale_p[3 * size_t(p) + k] * (-yp[k]);
+      const double d = x - xn;
       st += d * d;
-      X_new[3 * size_t(p) + k] = Xn[k];
+      X_new[3 * size_t(p) + k] = xn;
+      ypt[3 * size_t(p) + k] = yp[k];
     }
-    for (int q = q0; q < q1; ++q) {
-      const int c = obs_cam[q];
-      const double* Jr = jrec + size_t(pos[q]) * kJRec;
-      const double* y = ysol + 6 * size_t(c);
-      double e0 = 0.0, e1 = 0.0;
+  }
+  double r = block_reduce(st, sh, false);
+  if (threadIdx.x == 0) part_step[blockIdx.x] = r;
+  r = block_reduce(bad, sh, true);
+  if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                        const int32_t* __restrict__ cam_obs,
+                                                        const int32_t* __restrict__ cm_p,
+                                                        const double* __restrict__ uv_cm,
+                                                        const double* __restrict__ Kc,
+                                                        const double* __restrict__ jrec,
+                                                        const double* __restrict__ eu,
+                                                        const double* __restrict__ ypt,
+                                                        const double* __restrict__ X_new,
+                                                        const double* __restrict__ camRn,
+                                                        double* __restrict__ part_model,
+                                                        double* __restrict__ part_cost) {
+  __shared__ double sh[4];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
+  double model = 0.0, ncost = 0.0;
+  if (i0 < N_pad) {
+    const int64_t i = i0 + l;
+    const int c = wcam[i0 >> 6];  // wave-uniform
+    const bool real = cam_obs[i] >= 0;
+    const int p = cm_p[i];
+    const double* Jr = jrec + size_t(i) * kJRec;
+    const double2 e = ld2(eu + size_t(i) * kEU);
+    const double y0 = ypt[3 * size_t(p)], y1 = ypt[3 * size_t(p) + 1], y2 = ypt[3 * size_t(p) + 2];
+    const double m0 = -(e.x + Jr[0] * y0 + Jr[1] * y1 + Jr[2] * y2);
+    const double m1 = -(e.y + Jr[3] * y0 + Jr[4] * y1 + Jr[5] * y2);
+    const double r0 = Jr[kRes], r1 = Jr[kRes + 1];
+    const double mc = -(m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0));
+    // candidate residual
+    const double* Rn = camRn + 12 * size_t(c);
+    const double Xn0 = X_new[3 * size_t(p)], Xn1 = X_new[3 * size_t(p) + 1], Xn2 = X_new[3 * size_t(p) + 2];
+    double pc[3];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) { e0 += Jr[kJC + k] * y[k]; e1 += Jr[kJC + 6 + k] * y[k]; }
-      const double m0 = -(e0 + Jr[0] * y0 + Jr[1] * y1 + Jr[2] * y2);
-      const double m1 = -(e1 + Jr[3] * y0 + Jr[4] * y1 + Jr[5] * y2);
-      const double r0 = Jr[kRes], r1 = Jr[kRes + 1];
-      model -= m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
-      // candidate residual
-      const double* Rn = camRn + 12 * size_t(c);
-      double pc[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pc[i] = Rn[3 * i] * Xn[0] + Rn[3 * i + 1] * Xn[1] + Rn[3 * i + 2] * Xn[2] + Rn[9 + i];
-      const double xp = pc[0] / pc[2], ypj = pc[1] / pc[2];
-      const double* k = Kc + 5 * size_t(c);
-      const double2 uvo = ld2(uv + 2 * size_t(q));
-      const double rn0 = k[0] * xp + k[1] * ypj + k[2] - uvo.x;
-      const double rn1 = k[3] * ypj + k[4] - uvo.y;
-      ncost += 0.5 * (rn0 * rn0 + rn1 * rn1);
+    for (int k = 0; k < 3; ++k) pc[k] = Rn[3 * k] * Xn0 + Rn[3 * k + 1] * Xn1 + Rn[3 * k + 2] * Xn2 + Rn[9 + k];
+    const double xp = pc[0] / pc[2], ypj = pc[1] / pc[2];
+    const double* k5 = Kc + 5 * size_t(c);
+    const double2 uvo = ld2(uv_cm + 2 * i);
+    const double rn0 = k5[0] * xp + k5[1] * ypj + k5[2] - uvo.x;
+    const double rn1 = k5[3] * ypj + k5[4] - uvo.y;
+    if (real) {
+      model = mc;
+      ncost = 0.5 * (rn0 * rn0 + rn1 * rn1);
     }
   }
   double r = block_reduce(model, sh, false);
   if (threadIdx.x == 0) part_model[blockIdx.x] = r;
   r = block_reduce(ncost, sh, false);
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
-  r = block_reduce(st, sh, false);
-  if (threadIdx.x == 0) part_step[blockIdx.x] = r;
-  r = block_reduce(bad, sh, true);
-  if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
 }
 
 // Fixed-order final reduction of one partial slot.
@@ -855,10 +913,15 @@ void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
                                                              slot(d, kPBadCam));
 }
 void launch_point_backsub(const DevProblem& d, hipStream_t s) {
-  if (d.P == 0) return;
-  k_point_backsub<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(
-      d.P, d.pt_off, d.obs_cam, d.pos, d.uv, d.Kc, d.jrec, d.mrec, d.ptL, d.ysol, d.scale_p, d.X, d.X_new, d.camRn,
-      slot(d, kPModel), slot(d, kPNewCost), slot(d, kPStepPt), slot(d, kPBadBack));
+  if (d.N_pad)
+    k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.jrec, d.mrec, d.ysol, d.eu);
+  if (d.P)
+    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.scale_p, d.X,
+                                                               d.X_new, d.ypt, slot(d, kPStepPt), slot(d, kPBadBack));
+  if (d.N_pad)
+    k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
+                                                                   d.jrec, d.eu, d.ypt, d.X_new, d.camRn,
+                                                                   slot(d, kPModel), slot(d, kPNewCost));
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);

@@ -222,8 +222,9 @@ int compute_step(sfm_ba_handle* h, double radius) {
     for (int sl : slots) hipMemsetAsync(d.partials + size_t(sl) * d.max_blocks, 0, sizeof(double), s);
   }
   if (h->rank != 0) hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
-  launch_reduce(d, kPModel, nbP, 0, kModelChange, s);
-  launch_reduce(d, kPNewCost, nbP, 0, kNewCost, s);
+  const int nbI = std::max(1, blocks_for(d.N_pad, 256));  // k_backsub_c grid
+  launch_reduce(d, kPModel, nbI, 0, kModelChange, s);
+  launch_reduce(d, kPNewCost, nbI, 0, kNewCost, s);
   launch_reduce(d, kPStepPt, nbP, 0, kStep2Pt, s);
   launch_reduce(d, kPStepCam, nbC, 0, kStep2Cam, s);
   // bad-step flags: max over point_prep, cam_update and backsub partials
@@ -409,7 +410,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n_jchunks = int32_t(jchunks.size() / 4);
   d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
   // camera-major copies for the Jacobian pass and the record map
-  std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1);
+  std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1), wcam(size_t(npad / 64) + 1, 0);
+  for (int c = 0; c < C; ++c)
+    for (int64_t w = cam_rng[2 * c] / 64; w < (cam_rng[2 * c] + (cam_off[c + 1] - cam_off[c]) + 63) / 64; ++w) wcam[w] = c;
   std::vector<double> uv_cm(2 * size_t(npad), 0.0);
   for (int c = 0; c < C; ++c) {
     const int32_t n_c = cam_off[c + 1] - cam_off[c];
@@ -463,13 +466,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n = 6 * C;
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
   d.nblk = d.ld / kNB;
-  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks});
+  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks,
+                           blocks_for(npad, 256)});
   // ---- device allocation ----
   int rc = 0;
 #define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) { free_problem(h); return rc; }
-  ALLOC(d.uv, 2 * size_t(N));
-  ALLOC(d.obs_cam, size_t(N));
-  ALLOC(d.obs_pt, size_t(N));
   ALLOC(d.pt_off, size_t(P) + 1);
   ALLOC(d.cam_obs, size_t(npad));
   ALLOC(d.cam_rng, 2 * size_t(C));
@@ -494,6 +495,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.jrec, size_t(kJRec) * npad);
   ALLOC(d.mrec, size_t(kMRec) * npad);
   ALLOC(d.frec, size_t(kFRec) * npad);
+  ALLOC(d.eu, size_t(kEU) * npad);
+  ALLOC(d.ypt, 3 * size_t(P));
+  ALLOC(d.wcam, size_t(npad / 64) + 1);
   ALLOC(d.ptV, size_t(kPtV) * P);
   ALLOC(d.ptL, size_t(kPtL) * P);
   ALLOC(d.Ucam, size_t(kUcam) * C);
@@ -517,10 +521,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   hipStream_t s = h->stream;
 #define H2D(dst, src, cnt) HIPCHK(hipMemcpyAsync((dst), (src), sizeof(*(dst)) * (cnt), hipMemcpyHostToDevice, s))
   if (N) {
-    H2D(d.uv, uv_s.data(), 2 * size_t(N));
-    H2D(d.obs_cam, cam_s.data(), size_t(N));
-    H2D(d.obs_pt, pt_s.data(), size_t(N));
     H2D(d.cam_obs, cam_obs_pad.data(), size_t(npad));
+    H2D(d.wcam, wcam.data(), wcam.size());
     H2D(d.cm_p, cm_p.data(), size_t(npad));
     HIPCHK(hipMemcpyAsync(d.jchunks, jchunks.data(), sizeof(int32_t) * jchunks.size(), hipMemcpyHostToDevice, s));
     H2D(d.uv_cm, uv_cm.data(), 2 * size_t(npad));
