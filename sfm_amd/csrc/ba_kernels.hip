@@ -66,6 +66,28 @@ __device__ __forceinline__ void st2_nt(double* p, double a, double b) {
   __builtin_nontemporal_store(v, reinterpret_cast<f64x2*>(p));
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-cooperative load of the 64 consecutive R-double records that start at
+// g into the wave's LDS slice s, returning this lane's record.  A lane-per-
+// record load of an AoS array is a 16-B access at an R*8-B stride: every
+// instruction touches 64 cache lines (the vector-memory pipeline pays per
+// line); these R/2 coalesced 1-KB rows touch 8 each.
+template <int R>
+__device__ __forceinline__ const double* wave_records(double* s, const double* __restrict__ g, int l) {
+  double2 v[R / 2];
+#pragma unroll
+  for (int k = 0; k < R / 2; ++k) v[k] = ld2(g + 2 * (64 * k + l));
+#pragma unroll
+  for (int k = 0; k < R / 2; ++k) st2(s + 2 * (64 * k + l), v[k].x, v[k].y);
+  wave_sync_lds();
+  return s + l * R;
+}
+
 // Rotation matrix R(w) with the branch of ceres::AngleAxisRotatePoint:
 // theta^2 > DBL_EPSILON -> Rodrigues; otherwise the first-order map I + [w]x.
 // Optionally dR/dw_k (k-major, 3 x row-major 3x3), differentiated through
@@ -317,20 +339,27 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
 __global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_rng,
                                                          const double* __restrict__ jrec, double* __restrict__ Ucam) {
   __shared__ double sh[4 * 27];
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kJRec];
   const int c = blockIdx.x;
+  const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63;
   double acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.0;
   const int i0 = cam_rng[2 * c], i1 = cam_rng[2 * c + 1];
-  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
-    const double* J = jrec + size_t(i) * kJRec;  // camera-major records: a contiguous stream
-    const double2 rr = ld2(J + kRes);
+  // camera runs start on a wavefront boundary and are padded to one
+  for (int base = i0 + 64 * w0; base < i1; base += kThreads) {
+    const double* J = wave_records<kJRec>(stage[w0], jrec + size_t(base) * kJRec, l0);
+    const bool real = base + l0 < i1;
+    double2 rr = ld2(J + kRes);
+    if (!real) rr = make_double2(0.0, 0.0);
     double j0[6], j1[6];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const double2 a = ld2(J + kJC + 2 * k), b = ld2(J + kJC + 6 + 2 * k);
-      j0[2 * k] = a.x; j0[2 * k + 1] = a.y; j1[2 * k] = b.x; j1[2 * k + 1] = b.y;
+      j0[2 * k] = real ? a.x : 0.0; j0[2 * k + 1] = real ? a.y : 0.0;
+      j1[2 * k] = real ? b.x : 0.0; j1[2 * k + 1] = real ? b.y : 0.0;
     }
+    wave_sync_lds();
     int q = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
@@ -473,8 +502,13 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
   const double2 a0 = ld2(L), a1 = ld2(L + 2), a2 = ld2(L + 4), a3 = ld2(L + 6), a4 = ld2(L + 8);
   const double l00 = a0.x, l10 = a0.y, l11 = a1.x, l20 = a1.y, l21 = a2.x, l22 = a2.y;
   const double z0 = a3.x, z1 = a3.y, z2 = a4.x;
-  const double* J = jrec + size_t(i) * kJRec;
+  // the wave's 64 J records arrive through its LDS slice (coalesced rows)
+  const double* J = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l);
   const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
+  double jc[12];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+  wave_sync_lds();
   const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
   const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
   double* sm = stage[wv];                 // [64][8]  M records
@@ -482,9 +516,6 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
   double* M = sm + l * kMRec;
   st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
   st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
-  double jc[12];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
   double* Fo = sf + l * kFRec;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
@@ -591,14 +622,27 @@ __global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restri
   for (int e = 0; e < 21; ++e) dacc[e] = 0.0;
 #pragma unroll
   for (int e = 0; e < 6; ++e) rhs[e] = 0.0;
-  for (int i = i0 + threadIdx.x; i < i1; i += kThreads) {
-    const double* J1p = jrec + size_t(i) * kJRec;
-    const double* M1p = mrec + size_t(i) * kMRec;  // camera-major: streamed
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kJRec + kMRec)];
+  const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63;
+  for (int base = i0 + 64 * w0; base < i1; base += kThreads) {
+    // camera-major records, streamed through the wave's LDS slice
+    const double* J1p = wave_records<kJRec>(stage[w0], jrec + size_t(base) * kJRec, l0);
+    const double* M1p = wave_records<kMRec>(stage[w0] + 64 * kJRec, mrec + size_t(base) * kMRec, l0);
+    const bool real = base + l0 < i1;
     double J1[12], M1[8];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) { const double2 v = ld2(J1p + kJC + 2 * k); J1[2 * k] = v.x; J1[2 * k + 1] = v.y; }
+    for (int k = 0; k < 6; ++k) {
+      const double2 v = ld2(J1p + kJC + 2 * k);
+      J1[2 * k] = real ? v.x : 0.0; J1[2 * k + 1] = real ? v.y : 0.0;
+    }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { const double2 v = ld2(M1p + 2 * k); M1[2 * k] = v.x; M1[2 * k + 1] = v.y; }
+    for (int k = 0; k < 4; ++k) {
+      const double2 v = ld2(M1p + 2 * k);
+      M1[2 * k] = real ? v.x : 0.0; M1[2 * k + 1] = real ? v.y : 0.0;
+    }
+    double2 rr = ld2(J1p + kRes);
+    if (!real) rr = make_double2(0.0, 0.0);
+    wave_sync_lds();
     double F[kFRec];
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
@@ -606,7 +650,6 @@ __global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restri
       F[3 * u + 1] = J1[u] * M1[1] + J1[6 + u] * M1[4];
       F[3 * u + 2] = J1[u] * M1[2] + J1[6 + u] * M1[5];
     }
-    const double2 rr = ld2(J1p + kRes);
     const double e0 = rr.x - M1[6], e1 = rr.y - M1[7];
 #pragma unroll
     for (int u = 0; u < 6; ++u) rhs[u] += J1[u] * e0 + J1[6 + u] * e1;
@@ -724,18 +767,21 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int
                                                         const double* __restrict__ jrec,
                                                         const double* __restrict__ mrec,
                                                         const double* __restrict__ ysol, double* __restrict__ eu) {
-  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kEU];
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kJRec + kMRec)];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
   if (i0 >= N_pad) return;
-  const int64_t i = i0 + l;
   const double* y = ysol + 6 * size_t(wcam[i0 >> 6]);  // wave-uniform
-  const double* J = jrec + size_t(i) * kJRec + kJC;
-  const double* M = mrec + size_t(i) * kMRec;
+  double yc[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) yc[k] = y[k];
+  const double* J = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l) + kJC;
+  const double* M = wave_records<kMRec>(stage[wv] + 64 * kJRec, mrec + size_t(i0) * kMRec, l);
   double e0 = 0.0, e1 = 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
+  for (int k = 0; k < 6; ++k) { e0 += J[k] * yc[k]; e1 += J[6 + k] * yc[k]; }
   const double2 m01 = ld2(M), m23 = ld2(M + 2), m45 = ld2(M + 4);
+  wave_sync_lds();
   // M row-major 2x3 (m0 m1 m2 | n0 n1 n2) = M[0..5];  u = M^T e
   double* o = stage[wv] + l * kEU;
   st2(o, e0, e1);
@@ -808,6 +854,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
                                                         double* __restrict__ part_model,
                                                         double* __restrict__ part_cost) {
   __shared__ double sh[4];
+  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kJRec];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
   double model = 0.0, ncost = 0.0;
@@ -816,7 +863,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
     const int c = wcam[i0 >> 6];  // wave-uniform
     const bool real = cam_obs[i] >= 0;
     const int p = cm_p[i];
-    const double* Jr = jrec + size_t(i) * kJRec;
+    const double* Jr = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l);
     const double2 e = ld2(eu + size_t(i) * kEU);
     const double y0 = ypt[3 * size_t(p)], y1 = ypt[3 * size_t(p) + 1], y2 = ypt[3 * size_t(p) + 2];
     const double m0 = -(e.x + Jr[0] * y0 + Jr[1] * y1 + Jr[2] * y2);
