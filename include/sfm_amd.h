@@ -47,7 +47,7 @@ extern "C" {
 #define SFM_ENOMEM (-12)   /* device allocation failed */
 #define SFM_ENODEV (-19)   /* no usable HIP device */
 #define SFM_EIO (-5)       /* HIP / RCCL runtime error */
-#define SFM_ENOTSUP (-95)  /* mode not supported by the device path */
+#define SFM_ENOTSUP (-95)  /* reserved: operation not supported */
 
 /* BA_TYPE (CTracker.h:67). */
 #define SFM_BA_STRUCT_ONLY 0

@@ -124,11 +124,13 @@ void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool co
 // mode 0: unscaled pass -> scale_p; mode 1: V, b, diag (if !reuse), gradient, x-norm
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s);
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s);
+void launch_point_factor(const DevProblem& d, double radius, hipStream_t s);
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
 void launch_pad_init(const DevProblem& d, hipStream_t s);
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
-void launch_point_backsub(const DevProblem& d, hipStream_t s);
+void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = true, bool pts_var = true);
+void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
 int blocks_for(int64_t n, int threads);

@@ -750,6 +750,55 @@ __global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __
   if (threadIdx.x == 0) part_bad[blockIdx.x] = rb;
 }
 
+// Pose-only step (mode POSE_ONLY: BAPoseFunctor, CTracker.cpp:607-636,
+// 684-687).  With the points held constant no point block is eliminated and
+// the normal matrix is block diagonal: one 6x6 block U_c + D_c^2 per camera
+// (R_c and t_c are coupled through their shared residuals), right-hand side
+// J_c^T r.  One lane per camera, in-register Cholesky; a non-positive or
+// non-finite pivot sets fail bit 0, as a failed dense LLT does.
+__global__ __launch_bounds__(kThreads) void k_cam_solve(int C, const double* __restrict__ Ucam,
+                                                        const double* __restrict__ diag_c, double radius,
+                                                        double* __restrict__ ysol, int* __restrict__ fail) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double* U = Ucam + size_t(kUcam) * c;
+  double L[21], y[6];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double s = U[up6(j, j)] + diag_c[6 * c + j] / radius;
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= L[up6(k, j)] * L[up6(k, j)];
+    ok = ok && s > 0.0 && isfinite(s);
+    const double ljj = sqrt(s);
+    L[up6(j, j)] = ljj;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double a = U[up6(j, i)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) a -= L[up6(k, i)] * L[up6(k, j)];
+      L[up6(j, i)] = a / ljj;  // L(i, j) kept at the upper index (j, i)
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double s = U[21 + i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= L[up6(k, i)] * y[k];
+    y[i] = s / L[up6(i, i)];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double s = y[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) s -= L[up6(i, k)] * y[k];
+    y[i] = s / L[up6(i, i)];
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) ysol[6 * c + i] = y[i];
+  if (!ok) atomicOr(fail, 1);
+}
+
 // ---------------------------------------------------------------------------
 // Point back substitution, model cost change and candidate cost, in three
 // passes so that every per-observation array is streamed in camera-major
@@ -936,6 +985,10 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
                                                              1e-6, 1e32, mode, reuse_diag ? 1 : 0,
                                                              slot(d, kPGradPt), slot(d, kPXNormPt));
 }
+void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
+  if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
+                                                                         slot(d, kPBad));
+}
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
                                                                          slot(d, kPBad));
@@ -959,12 +1012,27 @@ void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
                                                              count_norm ? slot(d, kPStepCam) : nullptr,
                                                              slot(d, kPBadCam));
 }
-void launch_point_backsub(const DevProblem& d, hipStream_t s) {
-  if (d.N_pad)
+void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
+  (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
+  if (d.C) k_cam_solve<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.diag_c, radius, d.ysol, d.fail);
+}
+void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
+  // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
+  if (d.N_pad && cams_var)
     k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.jrec, d.mrec, d.ysol, d.eu);
-  if (d.P)
+  else if (d.N_pad)
+    (void)hipMemsetAsync(d.eu, 0, sizeof(double) * kEU * size_t(d.N_pad), s);
+  if (d.P && pts_var) {
     k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.scale_p, d.X,
                                                                d.X_new, d.ypt, slot(d, kPStepPt), slot(d, kPBadBack));
+  } else if (d.P) {
+    // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
+    const size_t nbP = size_t(blocks_for(d.P, kThreads));
+    (void)hipMemsetAsync(d.ypt, 0, sizeof(double) * 3 * size_t(d.P), s);
+    (void)hipMemcpyAsync(d.X_new, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToDevice, s);
+    (void)hipMemsetAsync(slot(d, kPStepPt), 0, sizeof(double) * nbP, s);
+    (void)hipMemsetAsync(slot(d, kPBadBack), 0, sizeof(double) * nbP, s);
+  }
   if (d.N_pad)
     k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
                                                                    d.jrec, d.eu, d.ypt, d.X_new, d.camRn,

@@ -56,6 +56,7 @@ struct sfm_ba_handle {
   // host copies needed for reordering / reset
   std::vector<int64_t> order;  // sorted position -> caller observation index
   std::vector<int32_t> pos;      // point-major q -> camera-major record index
+  int32_t mode = SFM_BA_STRUCT_AND_POSE;  // of the running solve (CTracker.h:67)
   int32_t bs_epoch = 0;          // stamp of the last back-substitution launch (k_backsolve flags)
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
   std::vector<void*> allocs;
@@ -144,31 +145,47 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
-  launch_cam_prep(d, d.cam, true, s);
+  // constant blocks (STRUCT_ONLY: cameras, POSE_ONLY: points) carry a zero
+  // Jacobi scale, so their scaled Jacobian columns vanish; their norms and
+  // gradients are left out like Ceres leaves out constant blocks
+  const bool cams_var = h->mode != SFM_BA_STRUCT_ONLY, pts_var = h->mode != SFM_BA_POSE_ONLY;
+  const int nbP = std::max(1, blocks_for(d.P, 256)),
+            nbC = std::max(1, blocks_for(d.C, 256));
+  launch_cam_prep(d, d.cam, cams_var, s);
   mark_begin(h, kPhJac);
   launch_jacobian(d, !first || !jacobi_scaling ? true : false, s);
   mark_end(h);
   if (first && jacobi_scaling) {
-    mark_begin(h, kPhCamRed);
-    launch_cam_reduce(d, s);
-    mark_end(h);
-    if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
-    launch_cam_finalize(d, 0, false, false, s);
-    launch_point_eval(d, 0, false, s);
+    if (cams_var) {
+      mark_begin(h, kPhCamRed);
+      launch_cam_reduce(d, s);
+      mark_end(h);
+      if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+      launch_cam_finalize(d, 0, false, false, s);
+    }
+    if (pts_var) launch_point_eval(d, 0, false, s);
     mark_begin(h, kPhJac);
     launch_jacobian(d, true, s);
     mark_end(h);
   }
-  mark_begin(h, kPhCamRed);
-  launch_cam_reduce(d, s);
-  mark_end(h);
-  if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
-  launch_cam_finalize(d, 1, false, true, s);
-  mark_begin(h, kPhPtEval);
-  launch_point_eval(d, 1, false, s);
-  mark_end(h);
-  const int nbP = std::max(1, blocks_for(d.P, 256)),
-            nbC = std::max(1, blocks_for(d.C, 256));
+  if (cams_var) {
+    mark_begin(h, kPhCamRed);
+    launch_cam_reduce(d, s);
+    mark_end(h);
+    if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+    launch_cam_finalize(d, 1, false, true, s);
+  } else {
+    hipMemsetAsync(d.partials + size_t(kPGradCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
+    hipMemsetAsync(d.partials + size_t(kPXNormCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
+  }
+  if (pts_var) {
+    mark_begin(h, kPhPtEval);
+    launch_point_eval(d, 1, false, s);
+    mark_end(h);
+  } else {
+    hipMemsetAsync(d.partials + size_t(kPGradPt) * d.max_blocks, 0, sizeof(double) * nbP, s);
+    hipMemsetAsync(d.partials + size_t(kPXNormPt) * d.max_blocks, 0, sizeof(double) * nbP, s);
+  }
   if (d.N == 0) hipMemsetAsync(d.partials + size_t(kPCost) * d.max_blocks, 0, sizeof(double), s);
   if (d.P == 0) {
     hipMemsetAsync(d.partials + size_t(kPGradPt) * d.max_blocks, 0, sizeof(double), s);
@@ -193,35 +210,51 @@ int compute_step(sfm_ba_handle* h, double radius) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
-  mark_begin(h, kPhPtPrep);
-  launch_point_prep(d, radius, s);
-  mark_end(h);
-  mark_begin(h, kPhSchur);
-  launch_schur(d, radius, h->rank == 0, s);
-  mark_end(h);
-  if (h->nranks > 1 || h->force_pack) {
-    // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
-    launch_pack_upper(d, false, s);
-    if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
-    launch_pack_upper(d, true, s);
-  }
-  launch_pad_init(d, s);
-  mark_begin(h, kPhChol);
-  launch_cholesky(d, s);
-  mark_end(h);
-  mark_begin(h, kPhBack);
-  launch_backsolve(d, ++h->bs_epoch, s);
-  mark_end(h);
-  launch_cam_update(d, h->rank == 0, s);
-  mark_begin(h, kPhBacksub);
-  launch_point_backsub(d, s);
-  mark_end(h);
   const int nbP = std::max(1, blocks_for(d.P, 256)), nbC = std::max(1, blocks_for(d.C, 256));
+  if (h->mode == SFM_BA_STRUCT_AND_POSE) {
+    mark_begin(h, kPhPtPrep);
+    launch_point_prep(d, radius, s);
+    mark_end(h);
+    mark_begin(h, kPhSchur);
+    launch_schur(d, radius, h->rank == 0, s);
+    mark_end(h);
+    if (h->nranks > 1 || h->force_pack) {
+      // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
+      launch_pack_upper(d, false, s);
+      if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
+      launch_pack_upper(d, true, s);
+    }
+    launch_pad_init(d, s);
+    mark_begin(h, kPhChol);
+    launch_cholesky(d, s);
+    mark_end(h);
+    mark_begin(h, kPhBack);
+    launch_backsolve(d, ++h->bs_epoch, s);
+    mark_end(h);
+  } else if (h->mode == SFM_BA_POSE_ONLY) {
+    // block-diagonal camera system from the all-reduced U_c (same on every rank)
+    launch_cam_solve(d, radius, s);
+    hipMemsetAsync(d.partials + size_t(kPBad) * d.max_blocks, 0, sizeof(double) * nbP, s);
+  } else {
+    // STRUCT_ONLY: per-point 3x3 systems only; y_c = 0
+    hipMemsetAsync(d.fail, 0, sizeof(int), s);
+    if (d.P) {
+      mark_begin(h, kPhPtPrep);
+      launch_point_factor(d, radius, s);
+      mark_end(h);
+    }
+    hipMemsetAsync(d.ysol, 0, sizeof(double) * 6 * size_t(d.C), s);
+  }
+  launch_cam_update(d, h->rank == 0 && h->mode != SFM_BA_STRUCT_ONLY, s);
+  mark_begin(h, kPhBacksub);
+  launch_point_backsub(d, s, h->mode != SFM_BA_STRUCT_ONLY, h->mode != SFM_BA_POSE_ONLY);
+  mark_end(h);
   if (d.P == 0) {
     const int slots[] = {kPModel, kPNewCost, kPStepPt, kPBadBack, kPBad};
     for (int sl : slots) hipMemsetAsync(d.partials + size_t(sl) * d.max_blocks, 0, sizeof(double), s);
   }
-  if (h->rank != 0) hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
+  if (h->rank != 0 || h->mode == SFM_BA_STRUCT_ONLY)
+    hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
   const int nbI = std::max(1, blocks_for(d.N_pad, 256));  // k_backsub_c grid
   launch_reduce(d, kPModel, nbI, 0, kModelChange, s);
   launch_reduce(d, kPNewCost, nbI, 0, kNewCost, s);
@@ -623,16 +656,19 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
     if (summary) *summary = sm;
     return 0;
   }
-  if (mode != SFM_BA_STRUCT_AND_POSE)
-    return fail(SFM_ENOTSUP, "STRUCT_ONLY / POSE_ONLY are not implemented on the device path yet");
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;
+  h->mode = mode;
   int rc;
   if (!opts.jacobi_scaling) {
     std::vector<double> ones(std::max(6 * size_t(d.C), 3 * size_t(d.P)), 1.0);
     HIPCHK(hipMemcpyAsync(d.scale_c, ones.data(), sizeof(double) * 6 * d.C, hipMemcpyHostToDevice, h->stream));
     if (d.P) HIPCHK(hipMemcpyAsync(d.scale_p, ones.data(), sizeof(double) * 3 * d.P, hipMemcpyHostToDevice, h->stream));
   }
+  // constant blocks (CTracker.cpp:679-687): zero scale, so the scaled
+  // Jacobian columns of the constant side vanish and its step is zero
+  if (mode == SFM_BA_STRUCT_ONLY && d.C) HIPCHK(hipMemsetAsync(d.scale_c, 0, sizeof(double) * 6 * d.C, h->stream));
+  if (mode == SFM_BA_POSE_ONLY && d.P) HIPCHK(hipMemsetAsync(d.scale_p, 0, sizeof(double) * 3 * d.P, h->stream));
   double* sc = d.scal_host;
   double tj = now_s();
   if ((rc = evaluate(h, true, opts.jacobi_scaling != 0))) return rc;

@@ -125,3 +125,42 @@ def test_edge_cases_duplicate_camera_empty_camera_single_view():
     o, g = _solve_both(s)
     _assert_parity(o, g)
     assert np.array_equal(g[2][11], s.rot[11]) and np.array_equal(g[3][11], s.t[11])
+
+
+def _solve_both_mode(s, mode):
+    r_o, t_o, X_o = s.copy_params()
+    sm_o, tr_o = O.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r_o, t_o, X_o, mode=mode)
+    r_g, t_g, X_g = s.copy_params()
+    sm_g, tr_g = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r_g, t_g, X_g, mode=mode)
+    return (sm_o, tr_o, r_o, t_o, X_o), (sm_g, tr_g, r_g, t_g, X_g)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+@pytest.mark.parametrize("mode", [sfm_amd.STRUCT_ONLY, sfm_amd.POSE_ONLY])
+def test_struct_only_and_pose_only_modes(cfg, mode):
+    """BAStructFunctor / BAPoseFunctor (CTracker.cpp:607-668, 679-687): the
+    constant side is bitwise unchanged, the variable side matches the oracle."""
+    s = scene.config(cfg)
+    o, g = _solve_both_mode(s, mode)
+    _assert_parity(o, g)
+    r0, t0, X0 = s.copy_params()
+    if mode == sfm_amd.STRUCT_ONLY:
+        assert np.array_equal(g[2], r0) and np.array_equal(g[3], t0)
+        assert not np.array_equal(g[4], X0)
+    else:
+        assert np.array_equal(g[4], X0)
+        assert not np.array_equal(g[3], t0)
+    costs = [t["cost"] for t in g[1]]
+    assert all(b <= a for a, b in zip(costs, costs[1:]))
+
+
+def test_pose_only_with_unobserved_camera_and_duplicates():
+    s = scene.generate(12, 400, views=4, seed=5)
+    q = int(np.nonzero(s.pt_idx == 7)[0][0])
+    _append_obs(s, [s.cam_idx[q]], [7], s.uv[q] - 0.4)
+    drop = s.cam_idx == 3
+    s.uv, s.cam_idx, s.pt_idx = s.uv[~drop], s.cam_idx[~drop], s.pt_idx[~drop]
+    for mode in (sfm_amd.STRUCT_ONLY, sfm_amd.POSE_ONLY):
+        o, g = _solve_both_mode(s, mode)
+        _assert_parity(o, g)
+        assert np.array_equal(g[2][3], s.rot[3]) and np.array_equal(g[3][3], s.t[3])
