@@ -95,6 +95,11 @@ struct DevProblem {
   double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
   int32_t* fail = nullptr;    // [1] bit 0: Cholesky pivot not positive; bit 1: back-substitution hand-off timeout
   int32_t* flags = nullptr;   // [nblk] back-substitution hand-off flags (epoch-stamped)
+  int32_t* cflags = nullptr;  // [2][nblk][nblk] fused Cholesky: final (F) and partial (P) tile flags
+  unsigned long long* cticket = nullptr;  // fused Cholesky tile ticket (monotone across launches)
+  int32_t n_cu = 0;           // compute units (co-residency bound of the persistent grids)
+  bool chol_stepwise = false; // SFM_CHOL_STEPWISE=1: three launches per tile column instead
+
   // Schur: upper-triangle blocks (c1, c2) in row-major order, CSR offsets
   // of their (o1, o2) pair lists, and the pairs (point-major ids)
   int64_t n_blk = 0, n_pairs = 0;
@@ -136,7 +141,7 @@ void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipSt
 int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
-void launch_cholesky(const DevProblem& d, hipStream_t s);
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s);
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
 
 }  // namespace sfm

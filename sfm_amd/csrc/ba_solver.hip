@@ -57,7 +57,8 @@ struct sfm_ba_handle {
   std::vector<int64_t> order;  // sorted position -> caller observation index
   std::vector<int32_t> pos;      // point-major q -> camera-major record index
   int32_t mode = SFM_BA_STRUCT_AND_POSE;  // of the running solve (CTracker.h:67)
-  int32_t bs_epoch = 0;          // stamp of the last back-substitution launch (k_backsolve flags)
+  int32_t bs_epoch = 0;
+  int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem          // stamp of the last back-substitution launch (k_backsolve flags)
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
   std::vector<void*> allocs;
   bool has_problem = false;
@@ -121,6 +122,19 @@ void collect_marks(sfm_ba_handle* h) {
   }
   h->ev_marks.clear();
   h->ev_used = 0;
+}
+
+bool env_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '1';
+}
+
+// Compute units of the device: the persistent grids (fused Cholesky) must
+// stay co-resident, one workgroup per CU.
+int device_cus(int device) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess || prop.multiProcessorCount < 2) return 2;
+  return prop.multiProcessorCount;
 }
 
 size_t packed_size(int n) { return size_t(n) * (n + 1) / 2 + size_t(n); }
@@ -226,7 +240,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     }
     launch_pad_init(d, s);
     mark_begin(h, kPhChol);
-    launch_cholesky(d, s);
+    launch_cholesky(d, ++h->chol_epoch, s);
     mark_end(h);
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s);
@@ -535,10 +549,12 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.ptL, size_t(kPtL) * P);
   ALLOC(d.Ucam, size_t(kUcam) * C);
   ALLOC(d.S, size_t(d.ld) * d.ld);
-  h->force_pack = std::getenv("SFM_FORCE_PACK") && std::getenv("SFM_FORCE_PACK")[0] == '1';
+  h->force_pack = env_flag("SFM_FORCE_PACK");
   if (h->nranks > 1 || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
+  ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);
+  ALLOC(d.cticket, 1);
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
@@ -582,6 +598,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
   HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
+  HIPCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
+  HIPCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
+  h->chol_epoch = 0;
+  d.n_cu = device_cus(h->device);
+  d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   h->bs_epoch = 0;
   HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -869,12 +890,17 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   HIPCHK(hipMalloc(&S, bytes));
   HIPCHK(hipMalloc(&S0, bytes));
   HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
-  HIPCHK(hipMalloc(&flags, sizeof(int) * d.nblk));
-  HIPCHK(hipMemset(flags, 0, sizeof(int) * d.nblk));
+  HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
+  HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
   HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
   HIPCHK(hipMalloc(&fl, sizeof(int)));
   HIPCHK(hipMemcpy(S0, img.data(), bytes, hipMemcpyHostToDevice));
   d.S = S; d.invL = invd; d.ysol = ys; d.fail = fl; d.flags = flags;
+  d.cflags = flags + d.nblk;
+  d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk);
+  if (reinterpret_cast<uintptr_t>(d.cticket) % 8) d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk + 1);
+  d.n_cu = device_cus(device);
+  d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
@@ -882,7 +908,7 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipMemcpyAsync(S, S0, bytes, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(e0, s));
-    launch_cholesky(d, s);
+    launch_cholesky(d, r + 1, s);
     launch_backsolve(d, r + 1, s);
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));

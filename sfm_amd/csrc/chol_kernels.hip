@@ -17,6 +17,7 @@
 // and the back substitution L^T y = z (one launch per tile row, y_k = W_k^T z_k
 // recomputed by each workgroup, then the update of the rows above).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include "ba_device.h"
 
@@ -96,19 +97,14 @@ __device__ __forceinline__ void w_offdiag(const double* T, double* Wl, double* s
   for (int rr = 0; rr < 4; ++rr) Wl[(16 * J + j) * TS + 16 * I + 4 * rr + kk] = -acc2[rr];
 }
 
+// The factorisation proper, on the tile image T in LDS (256 threads; Wl is
+// cleared here).  Returns this thread's bad-pivot flag; ends with a barrier.
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
-__global__ __launch_bounds__(256) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
-                                                    double* __restrict__ Winv, int* __restrict__ fail) {
-  __shared__ double T[NB * TS];    // T[c*TS + r] = A(r, c), becomes L
-  __shared__ double Wl[NB * TS];   // Wl[c*TS + r] = W(r, c)
-  __shared__ double scr[4][256];   // per-wave 16x16 scratch (row-major)
+__device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int k0 = k * NB;
-  // ---- load the tile (coalesced columns), clear W ----
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    T[c * TS + r] = A[size_t(k0 + c) * ld + k0 + r];
     Wl[c * TS + r] = 0.0;
   }
   __syncthreads();
@@ -183,8 +179,27 @@ __global__ __launch_bounds__(256) void k_chol_potrf(double* __restrict__ A, int 
   }
   // ---- W row 3 off the diagonal ----
   if (w < 3) w_offdiag(T, Wl, scr[w], 3, w, lane);
-  if (bad && t == 0) atomicOr(fail, 1);
   __syncthreads();
+  return bad;
+}
+
+template <bool kFull>
+__global__ __launch_bounds__(256) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
+                                                    double* __restrict__ Winv, int* __restrict__ fail) {
+  __shared__ double T[NB * TS];    // T[c*TS + r] = A(r, c), becomes L
+  __shared__ double Wl[NB * TS];   // Wl[c*TS + r] = W(r, c)
+  __shared__ double scr[4][256];   // per-wave 16x16 scratch (row-major)
+  const int t = threadIdx.x;
+  const int k0 = k * NB;
+  // ---- load the tile (coalesced columns) ----
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = t + 256 * q, c = e >> 6, r = e & 63;
+    T[c * TS + r] = A[size_t(k0 + c) * ld + k0 + r];
+  }
+  __syncthreads();
+  const bool bad = potrf_tile<kFull>(T, Wl, scr, k0, n);
+  if (bad && t == 0) atomicOr(fail, 1);
   // ---- store L (whole columns; the strict upper part is a don't-care) and W ----
   double* Wk = Winv + size_t(k) * NB * NB;
 #pragma unroll
@@ -301,6 +316,304 @@ __global__ __launch_bounds__(256) void k_chol_syrk(double* __restrict__ A, int l
         A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
 }
 
+// ---------------------------------------------------------------------------
+// The whole factorisation in ONE persistent launch (left-looking tiles,
+// device-scope flags instead of kernel boundaries).
+//
+// Workgroup 0 walks the diagonal -- the critical path -- and never waits for
+// a launch: for j = 0, 1, ...
+//   T_jj (updated by the helpers for k <= j-2)  -= L_j,j-1 L_j,j-1^T
+//   POTRF -> L_jj, W_j = L_jj^-1                 (publish F(j,j))
+//   L_j+1,j = T_j+1,j W_j^T                      (publish F(j+1,j); kept in
+//                                                 LDS for the next update)
+// Every other workgroup is a helper that takes tiles (i, j), column-major,
+// from an atomic ticket and accumulates T_ij = A_ij - sum_k L_ik L_jk^T in
+// MFMA registers as the L columns become final (flags F).  Tiles (j, j) and
+// (j+1, j) stop one update short and hand the partial tile to the walker
+// (flag P); every other tile finishes with its TRSM against W_j (F(j,j)).
+// Tickets are taken in an order in which every dependency was taken
+// earlier, all workgroups are co-resident (grid <= CU count, one per CU),
+// so the waits always drain; every wait is bounded anyway (fail bit 1).
+// Polls are relaxed agent-scope atomic loads (coherent across the XCDs'
+// L2s); the acquire fence comes once, after the flag is seen.  (An acquire
+// load per poll would invalidate the poller's L2 on every spin.)
+constexpr long kFlagSpins = 1L << 19;
+
+__device__ __forceinline__ bool spin_until(const int* f, int epoch) {
+  long spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    if (++spins > kFlagSpins) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// Branches around barriers are kept SCALAR: "this is wave 0" is tested on
+// readfirstlane(threadIdx.x) (an SGPR), and everything inside runs on all 64
+// lanes (same flag, same value).  A per-lane `if (threadIdx.x == 0)` inside a
+// loop that also holds barriers lets the compiler split the loop by lane
+// masks, so that lanes 1..63 of wave 0 pass the barrier without lane 0
+// (seen on gfx950: a hang on a stale ticket).
+__device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64; }
+
+// Wave 0 waits for one flag, then the block proceeds (acquire by wave 0; the
+// barrier orders the other waves' loads after it).
+__device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
+  if (wave0()) {
+    if (!spin_until(f, epoch)) atomicOr(fail, 2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// Stores of the whole block are made visible device-wide, then the flag.
+__device__ __forceinline__ void block_publish(int* f, int epoch) {
+  __threadfence();
+  __syncthreads();
+  if (wave0()) __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 finds how many of k = k_from.. (<= K) have both F(i,k) and F(j,k)
+// final (waiting until at least one has); the block gets the new bound.
+__device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, int k_from, int K, int epoch,
+                                           int* sh, int* fail) {
+  if (wave0()) {
+    const int lane = threadIdx.x;
+    long spins = 0;
+    int bound = k_from;
+    while (true) {
+      const int k = k_from + lane;
+      bool ok = true;
+      if (k <= K)
+        ok = __hip_atomic_load(F + i * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+             __hip_atomic_load(F + j * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      const unsigned long long miss = __ballot(!ok);
+      const int run = miss ? __builtin_ctzll(miss) : 64;
+      bound = k_from + run;
+      if (run > 0 || ++spins > kFlagSpins) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (bound == k_from) {  // timed out: proceed (garbage), reported as an error
+      atomicOr(fail, 2);
+      bound = k_from + 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *sh = bound > K + 1 ? K + 1 : bound;  // every lane: the same value
+  }
+  __syncthreads();
+  // readfirstlane: the bound steers a loop with barriers in it, so it must be
+  // a scalar (uniform) value, never an exec-mask (per-lane) loop exit
+  const int b = __builtin_amdgcn_readfirstlane(*sh);
+  __syncthreads();
+  return b;
+}
+
+// Helper: one tile (i, j).  Wave w owns the 32x32 quadrant (c in cb.., r in
+// rb..), accumulated transposed as in k_chol_syrk.
+__device__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
+                                  int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
+                                  int* sh, int* __restrict__ fail) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int i0 = i * NB, j0 = j * NB;
+  const bool diag = i == j;
+  const bool skipq = diag && cb > rb;        // strictly upper quadrant: never read
+  const int K = diag ? j - 2 : j - 1;        // updates k = 0..K by the helper
+  double cv[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        cv[a][bb][reg] = skipq ? 0.0 : A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr];
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+  int kr = 0;  // k < kr are known final
+  for (int k = 0; k <= K; ++k) {
+    if (k >= kr) kr = ready_bound(F, nb, i, j, k, K, epoch, sh, fail);
+    if (skipq) continue;  // wave-uniform; no barrier below in this iteration
+    const int k0 = k * NB;
+    double xa[2][16], yb[2][16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const size_t colbase = size_t(k0 + 4 * ks + lk) * ld;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) xa[a][ks] = A[colbase + j0 + cb + 16 * a + lr];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = A[colbase + i0 + rb + 16 * bb + lr];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+          acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
+  }
+  if (diag || i == j + 1) {
+    // partial tile for the diagonal walker
+    if (K >= 0 && !skipq) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
+    }
+    block_publish(Pf + i * nb + j, epoch);
+    return;
+  }
+  // final tile: T -> LDS, then X = T W_j^T on MFMA once W_j is out
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        T[(cb + 16 * a + lk + 4 * reg) * TS + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
+  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+  const double* Wk = Winv + size_t(j) * NB * NB;
+  double xa[2][16], yb[2][16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int m = 4 * ks + lk;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = T[m * TS + rb + 16 * bb + lr];
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = acc[a][bb][reg];
+  block_publish(F + i * nb + j, epoch);
+}
+
+__device__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
+                             int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
+                             double* Ls, double (*scr)[256], int* __restrict__ fail) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int li = lane & 15, kk = lane >> 4;
+  for (int j = 0; j < nb; ++j) {
+    const int j0 = j * NB;
+    block_wait(Pf + j * nb + j, epoch, fail);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      T[c * TS + r] = A[size_t(j0 + c) * ld + j0 + r];
+    }
+    __syncthreads();
+    if (j > 0) {
+      // T -= L_j,j-1 L_j,j-1^T on the ten lower 16x16 blocks
+      for (int q = w; q < 10; q += 4) {
+        int J = 0, qq = q;
+        while (qq >= 4 - J) { qq -= 4 - J; ++J; }
+        const int I = J + qq;
+        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int M = 0; M < 4; ++M)
+          acc = mfma16(Ls + 16 * M * TS + 16 * I, 1, TS, Ls + 16 * M * TS + 16 * J, TS, 1, acc, lane);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) T[(16 * J + li) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
+      }
+      __syncthreads();
+    }
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n) : potrf_tile<false>(T, Wl, scr, j0, n);
+    if (bad) atomicOr(fail, 1);
+    double* Wk = Winv + size_t(j) * NB * NB;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      A[size_t(j0 + c) * ld + j0 + r] = T[c * TS + r];
+      Wk[c * NB + r] = Wl[c * TS + r];
+    }
+    block_publish(F + j * nb + j, epoch);
+    if (j + 1 == nb) break;
+    // subdiagonal tile: X = T W^T (W lower triangular), kept in Ls
+    const int i0 = j0 + NB;
+    block_wait(Pf + (j + 1) * nb + j, epoch, fail);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      T[c * TS + r] = A[size_t(j0 + c) * ld + i0 + r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int Cb = 0; Cb < 4; ++Cb) {
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      for (int M = 0; M <= Cb; ++M)
+        acc = mfma16(T + 16 * M * TS + 16 * w, 1, TS, Wl + 16 * M * TS + 16 * Cb, TS, 1, acc, lane);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Ls[(16 * Cb + li) * TS + 16 * w + 4 * rr + kk] = acc[rr];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      A[size_t(j0 + c) * ld + i0 + r] = Ls[c * TS + r];
+    }
+    block_publish(F + (j + 1) * nb + j, epoch);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb,
+                                                    double* __restrict__ Winv, int* __restrict__ F,
+                                                    int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
+                                                    int epoch, int nhelp, int* __restrict__ fail) {
+  __shared__ double T[NB * TS];
+  __shared__ double Wl[NB * TS];
+  __shared__ double Ls[NB * TS];
+  __shared__ double scr[4][256];
+  __shared__ int sh[2];
+  if (blockIdx.x == 0) {
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, fail);
+    return;
+  }
+  const int ntask = nb * (nb + 1) / 2;
+  // every launch takes exactly ntask + nhelp tickets (one failing grab per helper)
+  const unsigned long long base = (unsigned long long)(epoch - 1) * (unsigned long long)(ntask + nhelp);
+  while (true) {
+    if (wave0()) {
+      // one increment per wave (lane 0 adds 1, the others 0); every lane
+      // writes lane 0's ticket
+      const unsigned long long v = atomicAdd(ticket, threadIdx.x == 0 ? 1ULL : 0ULL);
+      const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
+      const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
+      sh[1] = int(((unsigned long long)hi << 32 | lo) - base);
+    }
+    __syncthreads();
+    // uniform (scalar) loop exit: a per-lane exit lets the compiler split the
+    // loop by lane masks around the thread-0 ticket grab (observed: lanes
+    // 1..63 re-running the body on a stale ticket, i.e. a hang)
+    const int tk = __builtin_amdgcn_readfirstlane(sh[1]);
+    __syncthreads();
+    if (tk >= ntask) break;
+    int j = 0, r = tk;
+    while (r >= nb - j) { r -= nb - j; ++j; }
+    fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
+  }
+}
+
 // Back substitution L^T y = z (z = row n of the augmented factor, i.e.
 // L^-1 rhs), ONE launch: workgroup b owns block row b (64 unknowns) and
 //   y_b = W_b^T (z_b - sum_{k>b} L_kb^T y_k).
@@ -311,7 +624,6 @@ __global__ __launch_bounds__(256) void k_chol_syrk(double* __restrict__ A, int l
 // instead of one kernel launch per block.  All nb workgroups are co-resident
 // (nb <= a few hundred, one CU each); every wait is bounded and a timeout
 // sets bit 1 of *fail (reported as an error, never a hang).
-constexpr long kSpinLimit = 1L << 24;
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
@@ -347,15 +659,12 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
       lv[i] = q.x;
       lv[i + 1] = q.y;
     }
-    if (t == 0) {
-      long spins = 0;
-      while (__hip_atomic_load(flags + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-        if (++spins > kSpinLimit) { timed_out = 1; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
+    if (wave0()) {  // scalar branch (see block_wait)
+      if (!spin_until(flags + k, epoch)) timed_out = 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
-    if (timed_out) break;
+    if (__builtin_amdgcn_readfirstlane(timed_out)) break;
     const double* yk = y + size_t(k) * NB + 16 * seg;
 #pragma unroll
     for (int i = 0; i < 16; i += 2) {
@@ -378,7 +687,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
   }
   __threadfence();
   __syncthreads();
-  if (t == 0) {
+  if (wave0()) {
     if (timed_out) atomicOr(fail, 2);
     __hip_atomic_store(flags + b, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -386,8 +695,15 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 
 }  // namespace
 
-void launch_cholesky(const DevProblem& d, hipStream_t s) {
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s) {
   (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
+  if (d.cflags && !d.chol_stepwise) {
+    const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
+    const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+    k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
+                                           d.cticket, epoch, nhelp, d.fail);
+    return;
+  }
   for (int k = 0; k < d.nblk; ++k) {
     if ((k + 1) * NB <= d.n)
       k_chol_potrf<true><<<1, 256, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);

@@ -94,9 +94,14 @@ def test_matcher_bit_exact():
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("path", ["fused", "stepwise"])
 @pytest.mark.parametrize("n", [6, 63, 64, 65, 130, 600, 3000])
-def test_dense_cholesky_solve(n):
+def test_dense_cholesky_solve(n, path, monkeypatch):
+    """Both factorisations: the persistent single-launch one (default) and
+    the three-launches-per-column one (SFM_CHOL_STEPWISE=1)."""
     from sfm_amd.ba import dense_spd_solve
+    if path == "stepwise":
+        monkeypatch.setenv("SFM_CHOL_STEPWISE", "1")
     rng = np.random.default_rng(n)
     M = rng.standard_normal((n, n))
     A = M @ M.T + n * np.eye(n)
@@ -108,10 +113,13 @@ def test_dense_cholesky_solve(n):
     print(f"n={n}: {ms:.3f} ms per factor+solve")
 
 
-def test_dense_cholesky_reports_indefinite():
+@pytest.mark.parametrize("path", ["fused", "stepwise"])
+@pytest.mark.parametrize("n", [100, 700])
+def test_dense_cholesky_reports_indefinite(n, path, monkeypatch):
     from sfm_amd.ba import dense_spd_solve
-    n = 100
+    if path == "stepwise":
+        monkeypatch.setenv("SFM_CHOL_STEPWISE", "1")
     A = np.eye(n)
-    A[50, 50] = -1.0
+    A[n // 2, n // 2] = -1.0
     _, _, fl = dense_spd_solve(A, np.ones(n))
     assert fl == 1
