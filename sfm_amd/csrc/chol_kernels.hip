@@ -323,13 +323,12 @@ __global__ __launch_bounds__(256) void k_chol_syrk(double* __restrict__ A, int l
 // Workgroup 0 walks the diagonal -- the critical path -- and never waits for
 // a launch: for j = 0, 1, ...
 //   T_jj (updated by the helpers for k <= j-2)  -= L_j,j-1 L_j,j-1^T
-//   POTRF -> L_jj, W_j = L_jj^-1                 (publish F(j,j))
-//   L_j+1,j = T_j+1,j W_j^T                      (publish F(j+1,j); kept in
-//                                                 LDS for the next update)
+//   POTRF -> L_jj, W_j = L_jj^-1
+//   L_j+1,j = T_j+1,j W_j^T  (kept in LDS for the next update)
 // Every other workgroup is a helper that takes tiles (i, j), column-major,
 // from an atomic ticket and accumulates T_ij = A_ij - sum_k L_ik L_jk^T in
-// MFMA registers as the L columns become final (flags F).  Tiles (j, j) and
-// (j+1, j) stop one update short and hand the partial tile to the walker
+// MFMA registers as the L columns become final (flags F).  Tiles (j, j)
+// (one update short) and (j+1, j) hand the partial tile to the walker
 // (flag P); every other tile finishes with its TRSM against W_j (F(j,j)).
 // Tickets are taken in an order in which every dependency was taken
 // earlier, all workgroups are co-resident (grid <= CU count, one per CU),
@@ -455,8 +454,8 @@ __device__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const 
         for (int bb = 0; bb < 2; ++bb)
           acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
   }
-  if (diag || i == j + 1) {
-    // partial tile for the diagonal walker
+  if (i <= j + 1) {
+    // partial tile for the diagonal walker (its diagonal update / TRSM)
     if (K >= 0 && !skipq) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
@@ -509,18 +508,64 @@ __device__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const 
   block_publish(F + i * nb + j, epoch);
 }
 
+// X = T W^T for one 64x64 tile (T and W in LDS, W lower triangular): wave w
+// gets row block w, x[Cb] = block (w, Cb) in the mfma16 D layout.
+__device__ __forceinline__ void trsm_lds(const double* T, const double* Wl, f64x4 x[4], int lane) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int Cb = 0; Cb < 4; ++Cb) {
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int M = 0; M <= Cb; ++M)
+      acc = mfma16(T + 16 * M * TS + 16 * w, 1, TS, Wl + 16 * M * TS + 16 * Cb, TS, 1, acc, lane);
+    x[Cb] = acc;
+  }
+}
+__device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) {
+  const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int Cb = 0; Cb < 4; ++Cb)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) D[(16 * Cb + li) * TS + 16 * w + 4 * rr + kk] = x[Cb][rr];
+}
+__device__ __forceinline__ void load_tile(double* D, const double* __restrict__ A, int ld, int i0, int j0) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
+    D[c * TS + r] = A[size_t(j0 + c) * ld + i0 + r];
+  }
+}
+__device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i0, int j0, const double* D) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
+    A[size_t(j0 + c) * ld + i0 + r] = D[c * TS + r];
+  }
+}
+
+// The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
+// TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
+// (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
+// last update of T_j+2,j+2, measured no better: the extra TRSM costs what
+// the saved hand-off gains.)
 __device__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
                              double* Ls, double (*scr)[256], int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int li = lane & 15, kk = lane >> 4;
+  // the next diagonal tile travels in registers (prefetched one step ahead)
+  double nx[16];
+  block_wait(Pf, epoch, fail);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = t + 256 * q, c = e >> 6, r = e & 63;
+    nx[q] = A[size_t(c) * ld + r];
+  }
   for (int j = 0; j < nb; ++j) {
     const int j0 = j * NB;
-    block_wait(Pf + j * nb + j, epoch, fail);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      T[c * TS + r] = A[size_t(j0 + c) * ld + j0 + r];
+      T[c * TS + r] = nx[q];
     }
     __syncthreads();
     if (j > 0) {
@@ -547,31 +592,26 @@ __device__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, doub
       A[size_t(j0 + c) * ld + j0 + r] = T[c * TS + r];
       Wk[c * NB + r] = Wl[c * TS + r];
     }
+    // W_j out at once: the helpers' TRSMs of column j feed the last updates
+    // of the diagonal tiles two steps ahead (a chain as long as a step)
     block_publish(F + j * nb + j, epoch);
     if (j + 1 == nb) break;
-    // subdiagonal tile: X = T W^T (W lower triangular), kept in Ls
+    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
     const int i0 = j0 + NB;
     block_wait(Pf + (j + 1) * nb + j, epoch, fail);
+    load_tile(T, A, ld, i0, j0);
+    // prefetch the next diagonal tile (the loads overlap the TRSM)
+    block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      T[c * TS + r] = A[size_t(j0 + c) * ld + i0 + r];
+      nx[q] = A[size_t(i0 + c) * ld + i0 + r];
     }
+    f64x4 x[4];
+    trsm_lds(T, Wl, x, lane);
+    put_tile(Ls, x, lane);
     __syncthreads();
-#pragma unroll
-    for (int Cb = 0; Cb < 4; ++Cb) {
-      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int M = 0; M <= Cb; ++M)
-        acc = mfma16(T + 16 * M * TS + 16 * w, 1, TS, Wl + 16 * M * TS + 16 * Cb, TS, 1, acc, lane);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) Ls[(16 * Cb + li) * TS + 16 * w + 4 * rr + kk] = acc[rr];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      A[size_t(j0 + c) * ld + i0 + r] = Ls[c * TS + r];
-    }
+    store_tile(A, ld, i0, j0, Ls);
     block_publish(F + (j + 1) * nb + j, epoch);
   }
 }

@@ -13,8 +13,9 @@ buf = (ctypes.c_ulonglong * 2048)()
 lib.sfm_debug_stamps(buf, 2048)
 st = np.array(buf[:8 * 47], dtype=np.float64).reshape(47, 8) / 100.0  # 100 MHz -> us
 t0 = st[0, 0]
-for j in range(47):
-    r = st[j] - t0
-    d = np.diff(st[j])
-    print(f"j={j:2d} start {r[0]:8.1f} waitP {d[0]:5.2f} loadT {d[1]:5.2f} upd+potrf {d[2]:5.2f} store+pub {d[3]:5.2f} waitP2 {d[4]:5.2f} loadT+trsm {d[5]:5.2f} store+pub {d[6]:5.2f}")
-print('mean', np.mean(np.diff(st[:46], axis=1), axis=0))
+names = ["T+upd+potrf", "store L/W+waitP1", "ld T1+waitPd", "trsm1+st", "waitP2", "ld+trsm2+st", "fence+pub"]
+for j in range(44):
+    d = np.diff(st[j, :8])
+    print(f"j={j:2d} start {st[j,0]-t0:8.1f} " + " ".join(f"{nm} {v:5.2f}" for nm, v in zip(names, d)))
+print('mean', dict(zip(names, np.round(np.mean(np.diff(st[:44, :8], axis=1), axis=0), 2))))
+print('step mean', np.mean(np.diff(st[:46, 0])))
