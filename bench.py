@@ -148,23 +148,32 @@ def main() -> int:
     total_phase = sum(p["ms"] for p in phases.values())
     dominant = max(phases, key=lambda k: phases[k]["ms"])
 
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_jacobian.json")
+    # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.sh
+    # -> tools/pmc_json.py -> profiles/pmc_c3.json; FETCH_SIZE/WRITE_SIZE in
+    # separate passes, corrected per MI355X_MICROARCH.md "HBM").  Only valid
+    # for the workload they were collected on (C3).
+    pmc = {}
+    prof = os.path.join(ROOT, "profiles", "pmc_c3.json")
     if os.path.exists(prof):
         try:
             with open(prof) as f:
                 pm = json.load(f)
             if pm.get("n_obs") == sc.n_obs:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+                pmc = pm.get("kernels", {})
+        except (OSError, ValueError):
+            pmc = {}
+
+    def traffic(kernel):
+        e = pmc.get(kernel) or {}
+        v = e.get("hbm_bytes_per_launch")
+        return None if v is None else int(v)
 
     roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass)", "bound": "hbm", "achieved": round(jac_gbs, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian"),
                 "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5)}
-    roof_chol = {"kernel": "dense reduced-camera Cholesky phase (k_chol_potrf/trsm/syrk, f64 MFMA)", "bound": "mfma",
+    roof_chol = {"kernel": "k_chol_fused (dense reduced-camera Cholesky, one persistent launch, f64 MFMA)", "bound": "mfma",
                  "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                 "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": None,
+                 "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": traffic("k_chol_fused"),
                  "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4)}
     roofline = roof_chol if dominant == "cholesky" else roof_jac
 
