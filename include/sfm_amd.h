@@ -28,6 +28,16 @@
  *     (CTracker.h:56, CTracker.cpp:368-417) is the same call on gathered
  *     rows followed by an index map (sfm_amd/ctracker.py, the compat header).
  *
+ *   sfm_klt_compute_optical_flow
+ *     replaces bool CTracker::computeOpticalFlow()  (CTracker.h:60,
+ *     CTracker.cpp:480-562): pyramidal Lucas-Kanade from the previous to
+ *     the current frame (cv::calcOpticalFlowPyrLK, CTracker.cpp:513), the
+ *     nearest-detected-point association (CFrame::
+ *     findClosestPointIndexDistorted, CFrame.cpp:437-450) and the gate /
+ *     replacement loop (CTracker.cpp:515-545) producing _prevIdx/_currIdx.
+ *     The frames are CFrame::getFrameGrey() (8-bit grey), pushed once each
+ *     with sfm_klt_push_frame (the pyramid stays resident in HBM).
+ *
  * Every function is synchronous with respect to the caller's host buffers.
  */
 #ifndef SFM_AMD_H_
@@ -185,6 +195,56 @@ int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uin
  * factor+solve; *chol_fail = 1 if a pivot was not positive. */
 int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double* b, double* y, int32_t reps,
                         double* ms, int32_t* chol_fail);
+
+/* ---- Pyramidal Lucas-Kanade tracker -------------- */
+typedef struct sfm_klt_params {
+  int32_t win_size;          /* 21   (Size winSize(21,21), CTracker.cpp:484) */
+  int32_t max_level;         /* 3    (CTracker.cpp:487) */
+  int32_t max_count;         /* 20   (TermCriteria COUNT, CTracker.cpp:483) */
+  int32_t reserved;
+  double epsilon;            /* 0.03 (TermCriteria EPS; squared internally) */
+  double min_eig_threshold;  /* 0.001 (CTracker.cpp:513) */
+  double max_match_distance; /* 40  _maxMatchDistance  (CTracker.cpp:30) */
+  double min_match_distance; /* 1.5 _minMatchDistance  (CTracker.cpp:31) */
+  double max_org_feat_dist;  /* 1   _maxOrgFeatDist    (CTracker.cpp:33) */
+} sfm_klt_params;
+
+typedef struct sfm_klt_handle sfm_klt_handle;
+
+void sfm_klt_default_params(sfm_klt_params* p);
+/* One tracker per frame size; params NULL = defaults.  win_size odd, 3..31. */
+int sfm_klt_create(int32_t device, int32_t width, int32_t height, const sfm_klt_params* params,
+                   sfm_klt_handle** out);
+int sfm_klt_destroy(sfm_klt_handle* h);
+/* Pyramid levels actually built (buildOpticalFlowPyramid stops when a level
+ * would not exceed the window): max_level + 1 at most. */
+int32_t sfm_klt_num_levels(const sfm_klt_handle* h);
+/* Upload a new current frame (grey u8, row stride in bytes) and build its
+ * pyramid + Scharr derivatives; the old current frame becomes the previous
+ * one (CTracker's _prevFrame/_currFrame swap, CSfM.cpp:626-629). */
+int sfm_klt_push_frame(sfm_klt_handle* h, const uint8_t* grey, int32_t stride);
+/* Pyramid level `level` of the previous (which=0) or current (which=1)
+ * frame: img [h][w] u8 and dxy [h][w][2] int16 (either may be NULL). */
+int sfm_klt_get_level(sfm_klt_handle* h, int32_t which, int32_t level, uint8_t* img, int16_t* dxy, int32_t* w,
+                      int32_t* hh);
+/* cv::calcOpticalFlowPyrLK(prev, curr, prev_pts, next_pts, status, ...)
+ * between the two most recent frames; points [n][2] float. */
+int sfm_klt_calc_flow(sfm_klt_handle* h, const float* prev_pts, int32_t n, float* next_pts, uint8_t* status);
+/* CTracker::computeOpticalFlow: prev_pts_dist [n_prev][2] (previous frame's
+ * CFrame::getPointsDistorted), curr_pts_dist [n_curr][2] (current frame's
+ * detected points).  Writes *n_matches (prev_idx, curr_idx) pairs in the
+ * reference's slot order (capacity >= n_prev); flowed [n_prev][2] and
+ * status [n_prev] are optional outputs of the LK stage.  The reference's
+ * bool is (*n_matches >= _minFeatures). */
+int sfm_klt_compute_optical_flow(sfm_klt_handle* h, const double* prev_pts_dist, int32_t n_prev,
+                                 const double* curr_pts_dist, int32_t n_curr, int32_t* prev_idx, int32_t* curr_idx,
+                                 int32_t* n_matches, float* flowed, uint8_t* status);
+/* Device time (ms) of the last push (pyramid), LK and association stages. */
+int sfm_klt_phase_times(sfm_klt_handle* h, double* ms3);
+/* One-shot calcOpticalFlowPyrLK on two host frames (creates a temporary tracker). */
+int sfm_calc_optical_flow_pyr_lk(int32_t device, const uint8_t* prev, const uint8_t* next, int32_t width,
+                                 int32_t height, const float* prev_pts, int32_t n, float* next_pts, uint8_t* status,
+                                 const sfm_klt_params* params);
 
 /* Synthetic scenes, host-only.  Points [p_begin, p_end) of a
  * scene with n_pts_total points; every camera is returned.  Observations are

@@ -71,6 +71,17 @@ def lib():
                                                c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
         L.oracle_ba_reduced_system.restype = c_int
+        L.oracle_pyr_down.argtypes = [c_void_p, c_int32, c_int32, c_void_p]
+        L.oracle_pyr_down.restype = None
+        L.oracle_scharr.argtypes = [c_void_p, c_int32, c_int32, c_void_p]
+        L.oracle_scharr.restype = None
+        L.oracle_calc_optical_flow_pyr_lk.argtypes = [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int32,
+                                                      c_void_p, c_void_p, c_int32, c_int32, c_int32, c_double,
+                                                      c_double]
+        L.oracle_calc_optical_flow_pyr_lk.restype = c_int
+        L.oracle_klt_associate.argtypes = [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_double,
+                                           c_double, c_double, c_void_p, c_void_p]
+        L.oracle_klt_associate.restype = c_int32
         _L = L
     return _L
 
@@ -163,3 +174,51 @@ def reduced_system(uv, cam_idx, pt_idx, K9, rot, t, X, scale_c, scale_p, D_c, D_
     if rc != 0:
         raise RuntimeError("oracle_ba_reduced_system failed")
     return S, rhs, cc, cp
+
+
+# ---- optical-flow tracker (klt_oracle.cpp) --------------------------------
+def pyr_down(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros(((h + 1) // 2, (w + 1) // 2), np.uint8)
+    lib().oracle_pyr_down(_p(img), w, h, _p(out))
+    return out
+
+
+def scharr(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w, 2), np.int16)
+    lib().oracle_scharr(_p(img), w, h, _p(out))
+    return out
+
+
+def calc_optical_flow_pyr_lk(prev, nxt, prev_pts, win=21, max_level=3, max_count=20, eps=0.03, min_eig=1e-3):
+    """cv::calcOpticalFlowPyrLK restatement (CTracker.cpp:513 call)."""
+    prev = np.ascontiguousarray(prev, np.uint8)
+    nxt = np.ascontiguousarray(nxt, np.uint8)
+    pts = np.ascontiguousarray(prev_pts, np.float32).reshape(-1, 2)
+    h, w = prev.shape
+    n = pts.shape[0]
+    out = np.zeros((n, 2), np.float32)
+    st = np.zeros(n, np.uint8)
+    rc = lib().oracle_calc_optical_flow_pyr_lk(_p(prev), _p(nxt), w, h, _p(pts), n, _p(out), _p(st), win, max_level,
+                                               max_count, eps, min_eig)
+    if rc:
+        raise ValueError(f"oracle_calc_optical_flow_pyr_lk: {rc}")
+    return out, st
+
+
+def klt_associate(prev_pts, flowed, status, curr_pts, max_match_distance=40.0, min_match_distance=1.5,
+                  max_org_feat_dist=1.0):
+    """CTracker::computeOpticalFlow association + gates (CTracker.cpp:515-545)."""
+    prev_pts = np.ascontiguousarray(prev_pts, np.float32).reshape(-1, 2)
+    flowed = np.ascontiguousarray(flowed, np.float32).reshape(-1, 2)
+    status = np.ascontiguousarray(status, np.uint8)
+    curr = np.ascontiguousarray(curr_pts, np.float64).reshape(-1, 2)
+    n, m = prev_pts.shape[0], curr.shape[0]
+    pi = np.zeros(max(1, n), np.int32)
+    ci = np.zeros(max(1, n), np.int32)
+    k = lib().oracle_klt_associate(_p(prev_pts), _p(flowed), _p(status), n, _p(curr), m, max_match_distance,
+                                   min_match_distance, max_org_feat_dist, _p(pi), _p(ci))
+    return pi[:k].copy(), ci[:k].copy()

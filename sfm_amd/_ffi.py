@@ -82,6 +82,20 @@ class BAIteration(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
 
 
+class KLTParams(ctypes.Structure):
+    _fields_ = [
+        ("win_size", c_int32),
+        ("max_level", c_int32),
+        ("max_count", c_int32),
+        ("reserved", c_int32),
+        ("epsilon", c_double),
+        ("min_eig_threshold", c_double),
+        ("max_match_distance", c_double),
+        ("min_match_distance", c_double),
+        ("max_org_feat_dist", c_double),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "sfm_abi_version": (c_int32, []),
@@ -112,6 +126,19 @@ _SIGNATURES = {
                                  c_void_p, c_void_p]),
     "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
                                     POINTER(c_int32)]),
+    "sfm_klt_default_params": (None, [POINTER(KLTParams)]),
+    "sfm_klt_create": (c_int, [c_int32, c_int32, c_int32, POINTER(KLTParams), POINTER(c_void_p)]),
+    "sfm_klt_destroy": (c_int, [c_void_p]),
+    "sfm_klt_num_levels": (c_int32, [c_void_p]),
+    "sfm_klt_push_frame": (c_int, [c_void_p, c_void_p, c_int32]),
+    "sfm_klt_get_level": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, POINTER(c_int32),
+                                  POINTER(c_int32)]),
+    "sfm_klt_calc_flow": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "sfm_klt_compute_optical_flow": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
+                                             POINTER(c_int32), c_void_p, c_void_p]),
+    "sfm_klt_phase_times": (c_int, [c_void_p, c_void_p]),
+    "sfm_calc_optical_flow_pyr_lk": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int32,
+                                             c_void_p, c_void_p, POINTER(KLTParams)]),
     "sfm_scene_default_intrinsics": (None, [c_void_p]),
     "sfm_scene_generate": (c_int, [c_int32, c_int32, c_int32, c_int32, c_int32, c_uint64, c_double, c_double,
                                    c_double, c_double] + [c_void_p] * 10),
@@ -159,9 +186,16 @@ def default_options() -> BAOptions:
     return o
 
 
+def default_klt_params() -> KLTParams:
+    p = KLTParams()
+    lib().sfm_klt_default_params(ctypes.byref(p))
+    return p
+
+
 def device_count() -> int:
     return int(lib().sfm_device_count())
 
 
-__all__ = ["lib", "check", "ptr", "BAOptions", "BASummary", "BAIteration", "SfmError", "default_options",
+__all__ = ["lib", "check", "ptr", "BAOptions", "BASummary", "BAIteration", "KLTParams", "SfmError", "default_options",
+           "default_klt_params",
            "device_count", "exported_symbols", "LIB_PATH", "c_uint8"]

@@ -21,6 +21,7 @@
 #include <string>
 #include <vector>
 #include "../../include/sfm_amd.h"
+#include "ordered_compact.h"
 
 void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
 
@@ -81,45 +82,6 @@ __global__ void k_accept(const double* __restrict__ p0, const double* __restrict
     atomicMin(&key[j], (static_cast<unsigned long long>(unsigned(bd[i])) << 32) | unsigned(i));
     atomicMin(&first[j], i);
   }
-}
-
-// slot_train[i] = j + 1 if query i is the first accepted query of train j.
-__global__ void k_mark(int n1, const int* __restrict__ first, int* __restrict__ slot_train) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < n1 && first[j] != 0x7fffffff) slot_train[first[j]] = j + 1;
-}
-
-// Ordered compaction (single workgroup, prefix sum over the query order).
-__global__ __launch_bounds__(1024) void k_compact(int n0, const int* __restrict__ slot_train,
-                                                  const unsigned long long* __restrict__ key,
-                                                  int* __restrict__ idx0, int* __restrict__ idx1,
-                                                  int* __restrict__ count) {
-  __shared__ int sums[1024];
-  __shared__ int base;
-  if (threadIdx.x == 0) base = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < n0; c0 += 1024) {
-    const int i = c0 + threadIdx.x;
-    const int f = (i < n0 && slot_train[i] > 0) ? 1 : 0;
-    sums[threadIdx.x] = f;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const int v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0;
-      __syncthreads();
-      sums[threadIdx.x] += v;
-      __syncthreads();
-    }
-    if (f) {
-      const int pos = base + sums[threadIdx.x] - 1;
-      const int j = slot_train[i] - 1;
-      idx0[pos] = int(key[j] & 0xffffffffull);
-      idx1[pos] = j;
-    }
-    __syncthreads();
-    if (threadIdx.x == 1023) base += sums[1023];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *count = base;
 }
 
 struct DevBufs {
@@ -237,8 +199,8 @@ int sfm_match_features(int32_t device, const double* pts0, const uint8_t* desc0,
     if (rc) return rc;
     const double minSq = min_distance * min_distance, maxSq = max_distance * max_distance;
     k_accept<<<(n0 + 255) / 256, 256, 0, s>>>(p0, p1, n0, r, r + n0, r + 3 * n0, ratio_test, minSq, maxSq, key, first);
-    k_mark<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
-    k_compact<<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
+    sfm::k_mark_first<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
+    sfm::k_compact_slots<false><<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
     std::vector<int> host(2 * size_t(n0) + 1);
     if (hipMemcpy(host.data(), out, host.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
       return mfail(SFM_EIO, "kernel or copy failed");
