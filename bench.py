@@ -67,6 +67,58 @@ def cpu_baseline(scene) -> dict:
     }
 
 
+def tracker_leg(device: int, steps: int, cpu: bool) -> dict:
+    """Config C5 tracker leg: one step = push a
+    1280x720 grey frame (upload + pyramid + Scharr derivatives, resident in
+    HBM) + CTracker::computeOpticalFlow of 500 points against ~550 detections
+    (calcOpticalFlowPyrLK 21x21 / 4 levels / <= 20 iterations + nearest-
+    detection association).  Frames cycle over 3 rendered synthetic frames."""
+    from sfm_amd import klt
+    from sfm_amd.video import SyntheticVideo
+    v = SyntheticVideo()
+    frames = [v.frame(k) for k in range(3)]
+    rng = np.random.default_rng(0)
+    n_pts = 500
+    pts = [v.features(k, n_pts, rng) for k in range(3)]
+    dets = [v.detections(k, (k + 1) % 3, pts[k], rng) for k in range(3)]
+    tr = klt.KLTTracker(v.w, v.h, device=device)
+    tr.push_frame(frames[0])
+    ph = {"pyramid": 0.0, "lk": 0.0, "associate": 0.0}
+    warm = 5
+    matches = 0
+    for it in range(steps + warm):
+        if it == warm:
+            t0 = time.perf_counter()
+            ph = {k: 0.0 for k in ph}
+        k = (it + 1) % 3
+        tr.push_frame(frames[k])
+        pi, _ = tr.compute_optical_flow(pts[(k - 1) % 3], dets[(k - 1) % 3])
+        matches = len(pi)
+        for a, b in tr.phase_times().items():
+            ph[a] += b
+    wall = (time.perf_counter() - t0) / steps
+    out = {"workload": "C5 tracker: 1280x720 grey synthetic video, 500 points/frame, push_frame + "
+                       "computeOpticalFlow (calcOpticalFlowPyrLK 21x21, 4 levels, <=20 its, eps 0.03) + association",
+           "frames_per_s": 1.0 / wall, "ms_per_frame": wall * 1e3, "points_per_s": n_pts / wall,
+           "matches_per_frame": matches, "levels": tr.num_levels,
+           "device_ms_per_frame": {a: round(b / steps, 4) for a, b in ph.items()},
+           "cpu_baseline": None}
+    tr.close()
+    if cpu:
+        from oracle import ffi as O
+        reps = 20
+        t0 = time.perf_counter()
+        for r in range(reps):
+            k = (r + 1) % 3
+            nx, st = O.calc_optical_flow_pyr_lk(frames[(k - 1) % 3], frames[k], pts[(k - 1) % 3])
+            O.klt_associate(pts[(k - 1) % 3].astype(np.float32), nx, st, dets[(k - 1) % 3])
+        cw = (time.perf_counter() - t0) / reps
+        out["cpu_baseline"] = {"frames_per_s": 1.0 / cw, "ms_per_frame": cw * 1e3, "cores": 1, "kind": "port",
+                               "sample": f"{reps} frames of the same work (both pyramids + LK + association) "
+                                         "on oracle/klt_oracle.cpp, 1 thread"}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +128,7 @@ def main() -> int:
     ap.add_argument("--pts-per-gpu", type=int, default=PTS_PER_GPU)
     ap.add_argument("--cams", type=int, default=CAMS)
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
+    ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,6 +265,8 @@ def main() -> int:
         out["speedup_vs_cpu"] = value / cpu["value"]
     else:
         out["cpu_baseline"] = None
+    if rank == 0 and world == 1 and not args.no_tracker:
+        out["tracker"] = tracker_leg(local_rank, 50, not args.no_cpu_baseline)
     if args.phases and rank == 0:
         print(json.dumps(phases, indent=1), file=sys.stderr)
     if rank == 0:

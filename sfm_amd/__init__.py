@@ -9,8 +9,9 @@ from ._ffi import (BAIteration, BAOptions, BASummary, SfmError, LIB_PATH, defaul
                    exported_symbols, lib)
 from .ba import BundleAdjuster, make_options, solve, STRUCT_ONLY, POSE_ONLY, STRUCT_AND_POSE
 from .ctracker import CTracker
-from . import scene
+from . import scene, video
+from .klt import KLTTracker, calc_optical_flow_pyr_lk
 
-__all__ = ["BundleAdjuster", "CTracker", "BAOptions", "BASummary", "BAIteration", "SfmError", "make_options",
+__all__ = ["BundleAdjuster", "CTracker", "KLTTracker", "calc_optical_flow_pyr_lk", "video", "BAOptions", "BASummary", "BAIteration", "SfmError", "make_options",
            "solve", "default_options", "device_count", "exported_symbols", "lib", "scene", "LIB_PATH",
            "STRUCT_ONLY", "POSE_ONLY", "STRUCT_AND_POSE"]

@@ -8,6 +8,7 @@ descriptors -> uint8 [n][64]).
   bundleAdjustmentStructAndPose  CTracker.h:65,  CTracker.cpp:670-702
   matchFeatures (6 overloads)    CTracker.h:50-58, CTracker.cpp:114-149,
                                  211-250, 368-417, 419-477
+  computeOpticalFlow             CTracker.h:60,  CTracker.cpp:480-562
 
 The reference passes parameter blocks as vector<double*> with one pointer
 per observation (duplicates across observations, identity by address,
@@ -37,8 +38,12 @@ class CTracker:
         self._maxMatchDistance = 40.0     # CTracker.cpp:30
         self._minMatchDistance = 1.5      # CTracker.cpp:31
         self._minFeatures = 5             # CTracker.cpp:32
+        self._maxOrgFeatDist = 1.0        # CTracker.cpp:33
         self.last_summary = None
         self.last_trace = None
+        self._klt = None
+        self._prevIdx = np.zeros(0, np.int32)
+        self._currIdx = np.zeros(0, np.int32)
 
     # ---- bundle adjustment (CTracker.cpp:670-702) --------------------------
     def bundleAdjustmentStructAndPose(self, observations, camIdx, K, R, t, pts3D, isStructOrPose, pt_idx=None,
@@ -104,3 +109,29 @@ class CTracker:
         check(lib().sfm_knn2_hamming(self.device, ptr(desc0), n0, ptr(desc1), n1, desc0.shape[1], *map(ptr, out)),
               "sfm_knn2_hamming")
         return tuple(out)
+
+    # ---- optical flow (CTracker.cpp:480-562) -------------------------------
+    def pushFrame(self, grey) -> None:
+        """Make `grey` (CFrame::getFrameGrey(), u8 [h][w]) the current frame;
+        the previous current frame becomes _prevFrame (CSfM.cpp:626-629).
+        Its pyramid is built once on the device and kept resident."""
+        from .klt import KLTTracker, make_params
+        g = np.asarray(grey)
+        if self._klt is None or (self._klt.height, self._klt.width) != g.shape:
+            if self._klt is not None:
+                self._klt.close()
+            self._klt = KLTTracker(g.shape[1], g.shape[0], device=self.device,
+                                   params=make_params(max_match_distance=self._maxMatchDistance,
+                                                      min_match_distance=self._minMatchDistance,
+                                                      max_org_feat_dist=self._maxOrgFeatDist))
+        self._klt.push_frame(g)
+
+    def computeOpticalFlow(self, prevPtsDistorted, currPtsDistorted) -> bool:
+        """LK flow of the previous frame's (distorted) points into the current
+        frame, associated with the current frame's detected points; fills
+        _prevIdx/_currIdx (CTracker.cpp:520-545) and returns
+        matchCount >= _minFeatures (CTracker.cpp:558-561)."""
+        if self._klt is None:
+            raise RuntimeError("computeOpticalFlow: pushFrame() the previous and current frames first")
+        self._prevIdx, self._currIdx = self._klt.compute_optical_flow(prevPtsDistorted, currPtsDistorted)
+        return len(self._prevIdx) >= self._minFeatures

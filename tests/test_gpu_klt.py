@@ -124,3 +124,20 @@ def test_compute_optical_flow_edge_cases(video):
     opi, oci = O.klt_associate(prev2.astype(np.float32), fl, st, det)
     assert np.array_equal(pi, opi) and np.array_equal(ci, oci)
     tr.close()
+
+
+def test_ctracker_mirror_compute_optical_flow(video):
+    """The CTracker mirror's pushFrame / computeOpticalFlow members."""
+    import sfm_amd
+    v, frames = video
+    rng = np.random.default_rng(8)
+    prev = v.features(0, 200, rng)
+    det = v.detections(0, 1, prev, rng)
+    t = sfm_amd.CTracker()
+    t.pushFrame(frames[0])
+    t.pushFrame(frames[1])
+    ok = t.computeOpticalFlow(prev, det)
+    o, os_ = O.calc_optical_flow_pyr_lk(frames[0], frames[1], prev)
+    opi, oci = O.klt_associate(prev.astype(np.float32), o, os_, det)
+    assert ok == (len(opi) >= 5)
+    assert np.array_equal(t._prevIdx, opi) and np.array_equal(t._currIdx, oci)
