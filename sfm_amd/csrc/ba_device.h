@@ -105,6 +105,9 @@ struct DevProblem {
   int64_t n_blk = 0, n_pairs = 0;
   int2* blk = nullptr;        // [n_blk]
   int32_t* seg = nullptr;     // [n_blk + 1]
+  int32_t schur_row = 1;       // row-staged k_schur_row (SFM_SCHUR_ROW=0 disables)
+  int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
+  int32_t n_srow = 0;
   int2* pairs = nullptr;      // [n_pairs]
   // reductions
   double* partials = nullptr; // scratch [kNumPartialSlots][max_blocks]

@@ -558,6 +558,7 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
 // atomic strip formulation was bound at ~0.8 ms on C3.)  A diagonal block's
 // list holds only same-camera duplicate pairs (normally none);
 // k_schur_diag, launched after, adds the rest of that block and the rhs.
+// (Kept as the ablation baseline of k_schur_row: SFM_SCHUR_ROW=0.)
 __global__ __launch_bounds__(kThreads) void k_schur(int64_t n_blk, const int2* __restrict__ blk,
                                                     const int32_t* __restrict__ seg, const int2* __restrict__ pairs,
                                                     const double* __restrict__ frec, double* __restrict__ S, int ld) {
@@ -595,6 +596,92 @@ __global__ __launch_bounds__(kThreads) void k_schur(int64_t n_blk, const int2* _
       }
     }
   }
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
+#pragma unroll
+    for (int v = 0; v < 6; v += 2) st2(row + v, -acc[6 * u + v], -acc[6 * u + v + 1]);
+  }
+}
+
+// k_schur_row: the same owner-computes blocks, one workgroup per (row camera
+// c1, up to 256 consecutive blocks of its row).  Camera c1's F records (the
+// o1 side of every pair in the row, a contiguous camera-major run) are
+// streamed through LDS in chunks of kRowCh with coalesced loads, so only the
+// o2 side is gathered from the fabric: measured on C3, k_schur moves 4.8 GB
+// per launch (37.7M 128-B requests, 31% L2 hits, ~7 TB/s) for 2.6 GB of
+// pair records; the o1 half of those requests becomes one streamed pass
+// over each row camera's run.  Measured: 37.7M -> 22.1M requests, 670 ->
+// 632 us — the remaining o2 gathers (each 144-B record two fresh lines, no
+// reuse within a row) are L1-miss-latency bound (TCP pending stalls), which
+// neither cooperative coalesced gathers nor point-sliced launches (to keep
+// F resident in the Infinity Cache) improved: both measured slower.
+constexpr int kRowCh = 448;  // 63 KB of F records per chunk: two workgroups per CU
+__global__ __launch_bounds__(kThreads) void k_schur_row(const int4* __restrict__ work,
+                                                        const int32_t* __restrict__ seg,
+                                                        const int2* __restrict__ pairs,
+                                                        const double* __restrict__ frec,
+                                                        const int32_t* __restrict__ cam_rng,
+                                                        const int2* __restrict__ blk, double* __restrict__ S, int ld) {
+  __shared__ __attribute__((aligned(16))) double F1[kRowCh * kFRec];
+  const int4 wk = work[blockIdx.x];  // (c1, first block, block count, 0)
+  const int t = threadIdx.x;
+  const bool has = t < wk.z;
+  const int64_t b = int64_t(wk.y) + t;
+  int k = has ? seg[b] : 0;
+  const int ke = has ? seg[b + 1] : 0;
+  double acc[36];
+#pragma unroll
+  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+  constexpr int kNone = 0x7fffffff;
+  int2 pa = k < ke ? pairs[k] : make_int2(kNone, 0);
+  int2 pb = k + 1 < ke ? pairs[k + 1] : make_int2(kNone, 0);
+  const int r0 = cam_rng[2 * wk.x], r1 = cam_rng[2 * wk.x + 1];
+  for (int base = r0; base < r1; base += kRowCh) {
+    const int cnt = min(kRowCh, r1 - base), end = base + cnt;
+    __syncthreads();
+    {
+      const double2* src = reinterpret_cast<const double2*>(frec + size_t(base) * kFRec);
+      double2* dst = reinterpret_cast<double2*>(F1);
+      for (int e = t; e < cnt * (kFRec / 2); e += kThreads) dst[e] = src[e];
+    }
+    __syncthreads();
+    while (pa.x < end) {
+      const bool two = pb.x < end;
+      const int2 qb = two ? pb : pa;
+      const double wb = two ? 1.0 : 0.0;
+      const double* A2 = frec + size_t(pa.y) * kFRec;
+      const double* B2 = frec + size_t(qb.y) * kFRec;
+      double Ga[kFRec], Gb[kFRec];
+#pragma unroll
+      for (int f = 0; f < kFRec; f += 2) {
+        const double2 x = ld2(A2 + f), y = ld2(B2 + f);
+        Ga[f] = x.x; Ga[f + 1] = x.y; Gb[f] = y.x * wb; Gb[f + 1] = y.y * wb;
+      }
+      k += two ? 2 : 1;
+      const int2 na = k < ke ? pairs[k] : make_int2(kNone, 0);
+      const int2 nb = k + 1 < ke ? pairs[k + 1] : make_int2(kNone, 0);
+      const double* A1 = F1 + (pa.x - base) * kFRec;
+      const double* B1 = F1 + (qb.x - base) * kFRec;
+      double a1[kFRec], b1[kFRec];
+#pragma unroll
+      for (int f = 0; f < kFRec; f += 2) {
+        const double2 x = ld2(A1 + f), y = ld2(B1 + f);
+        a1[f] = x.x; a1[f + 1] = x.y; b1[f] = y.x; b1[f + 1] = y.y;
+      }
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+#pragma unroll
+        for (int v = 0; v < 6; ++v) {
+          acc[6 * u + v] += a1[3 * u] * Ga[3 * v] + a1[3 * u + 1] * Ga[3 * v + 1] + a1[3 * u + 2] * Ga[3 * v + 2];
+          acc[6 * u + v] += b1[3 * u] * Gb[3 * v] + b1[3 * u + 1] * Gb[3 * v + 1] + b1[3 * u + 2] * Gb[3 * v + 2];
+        }
+      pa = na;
+      pb = nb;
+    }
+  }
+  if (!has) return;
+  const int2 cc = blk[b];
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
@@ -996,7 +1083,9 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
     k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
-  if (d.n_blk)
+  if (d.n_blk && d.schur_row && d.n_srow)
+    k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
+  else if (d.n_blk)
     k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
   k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
                                         add_diag ? 1 : 0, d.S, d.ld, d.n);

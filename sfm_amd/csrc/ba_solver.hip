@@ -506,6 +506,21 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     }
     seg.push_back(int32_t(pairs.size() / 2));
   }
+  {
+    const char* rs = std::getenv("SFM_SCHUR_ROW");
+    d.schur_row = rs ? std::atoi(rs) : 1;
+  }
+  // k_schur_row work items: each row c1 (blocks (c1, c1..C-1), consecutive in
+  // the row-major block order) cut into segments of at most kThreads blocks.
+  std::vector<int4> srow;
+  {
+    int64_t bfirst = 0;
+    for (int c1 = 0; c1 < C; ++c1) {
+      const int nrow = C - c1;
+      for (int o = 0; o < nrow; o += 256) srow.push_back(make_int4(c1, int(bfirst + o), std::min(256, nrow - o), 0));
+      bfirst += nrow;
+    }
+  }
   if (pairs.size() / 2 >= size_t(INT32_MAX)) return fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets");
   d.n_blk = int64_t(blk.size() / 2);
   d.n_pairs = int64_t(pairs.size() / 2);
@@ -559,7 +574,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.fail, size_t(1));
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
   ALLOC(d.pairs, std::max<size_t>(1, size_t(d.n_pairs)));
-  ALLOC(d.seg, size_t(d.n_blk) + 1);
+  ALLOC(d.seg, seg.size());
+  d.n_srow = int32_t(srow.size());
+  ALLOC(d.srow, std::max<size_t>(1, srow.size()));
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars));
 #undef ALLOC
@@ -595,6 +612,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   if (d.n_pairs)
     HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
   H2D(d.seg, seg.data(), seg.size());
+  if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
   HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));

@@ -99,6 +99,23 @@ def test_packed_allreduce_path_is_exact(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
+    """k_schur_row (default) and k_schur (SFM_SCHUR_ROW=0) sum every block's
+    pairs in the same order: whole solves are bitwise identical."""
+    s = scene.config(cfg)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_SCHUR_ROW", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            out.append((sm.final_cost, tr, ba.parameters()))
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    for a, b in zip(out[0][2], out[1][2]):
+        assert np.array_equal(a, b)
+
+
 def _append_obs(s, cam, pt, uv):
     s.uv = np.vstack([s.uv, np.asarray(uv, dtype=np.float64).reshape(-1, 2)])
     s.cam_idx = np.concatenate([s.cam_idx, np.asarray(cam, dtype=np.int32)])
