@@ -46,6 +46,17 @@ enum Scalar {
   kNumScalars
 };
 
+// Batched scalar reductions (k_reduce_batch): job i reduces partial slot
+// `slot` over `nb` blocks (op 0 sum, 1 max) into scal[dst].
+struct ReduceJob {
+  int slot, nb, op, dst;
+};
+struct ReduceBatch {
+  ReduceJob job[8];
+  int n = 0;
+  void add(int slot, int nb, int op, int dst) { job[n++] = ReduceJob{slot, nb, op, dst}; }
+};
+
 struct DevProblem {
   int32_t C = 0, P = 0;      // cameras (global), points (this shard)
   int64_t N = 0;             // observations (this shard)
@@ -141,10 +152,11 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = tr
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
+void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fail, hipStream_t s);
 int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s);
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
 
 }  // namespace sfm

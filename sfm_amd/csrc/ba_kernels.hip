@@ -798,8 +798,11 @@ __global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, doub
 }
 
 // Identity padding beyond the augmented row n (column-major lower view).
-__global__ void k_pad_init(double* __restrict__ S, int ld, int n) {
+// Identity padding of the augmented system, and the Cholesky failure flag
+// cleared (saves the separate memset dispatch before k_chol_fused).
+__global__ void k_pad_init(double* __restrict__ S, int ld, int n, int* __restrict__ fail) {
   const int j = blockIdx.x;
+  if (j == 0 && threadIdx.x == 0) *fail = 0;
   for (int i = (j > n ? j : n + 1) + threadIdx.x; i < ld; i += blockDim.x) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
   if (j == n && threadIdx.x == 0) S[size_t(n) * ld + n] = 1.0;
 }
@@ -1029,6 +1032,30 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
 }
 
 // Fixed-order final reduction of one partial slot.
+// Several fixed-order reductions in one launch (workgroup i = job i), and
+// the Cholesky failure flag copied next to the scalars (an int in the slot
+// after them), so one launch and one copy end each LM phase instead of up
+// to seven launches and two copies (~5-6 us of dispatch each).
+__global__ __launch_bounds__(1024) void k_reduce_batch(const double* __restrict__ partials, int64_t max_blocks,
+                                                       ReduceBatch b, double* __restrict__ scal,
+                                                       const int* __restrict__ fail) {
+  __shared__ double sh[16];
+  const ReduceJob j = b.job[blockIdx.x];
+  const double* src = partials + size_t(j.slot) * max_blocks;
+  double v = 0.0;
+  for (int i = threadIdx.x; i < j.nb; i += 1024) v = j.op ? fmax(v, src[i]) : v + src[i];
+  v = j.op ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = sh[0];
+    for (int i = 1; i < 16; ++i) r = j.op ? fmax(r, sh[i]) : r + sh[i];
+    scal[j.dst] = r;
+    if (fail && blockIdx.x == 0) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ src, int nb, int op,
                                                  double* __restrict__ dst) {
   __shared__ double sh[16];
@@ -1095,7 +1122,7 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S);
   else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack);
 }
-void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n); }
+void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail); }
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
   k_cam_update<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.cam, d.ysol, d.scale_c, d.cam_new, d.camRn,
                                                              count_norm ? slot(d, kPStepCam) : nullptr,
@@ -1129,6 +1156,10 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);
+}
+void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fail, hipStream_t s) {
+  if (b.n > 0)
+    k_reduce_batch<<<b.n, 1024, 0, s>>>(d.partials, d.max_blocks, b, d.scal, copy_fail ? d.fail : nullptr);
 }
 
 }  // namespace sfm

@@ -147,7 +147,8 @@ int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
 
 // D2H of the scalar block + stream sync.
 int fetch_scalars(sfm_ba_handle* h) {
-  HIPCHK(hipMemcpyAsync(h->d.scal_host, h->d.scal, sizeof(double) * kNumScalars, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.scal_host, h->d.scal, sizeof(double) * (kNumScalars + 1), hipMemcpyDeviceToHost,
+                        h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   collect_marks(h);
   return 0;
@@ -205,11 +206,13 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
     hipMemsetAsync(d.partials + size_t(kPGradPt) * d.max_blocks, 0, sizeof(double), s);
     hipMemsetAsync(d.partials + size_t(kPXNormPt) * d.max_blocks, 0, sizeof(double), s);
   }
-  launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, s);
-  launch_reduce(d, kPGradCam, nbC, 1, kGradMaxCam, s);
-  launch_reduce(d, kPGradPt, nbP, 1, kGradMaxPt, s);
-  launch_reduce(d, kPXNormCam, nbC, 0, kXNorm2Cam, s);
-  launch_reduce(d, kPXNormPt, nbP, 0, kXNorm2Pt, s);
+  ReduceBatch rb;
+  rb.add(kPCost, d.jac_blocks, 0, kCost);
+  rb.add(kPGradCam, nbC, 1, kGradMaxCam);
+  rb.add(kPGradPt, nbP, 1, kGradMaxPt);
+  rb.add(kPXNormCam, nbC, 0, kXNorm2Cam);
+  rb.add(kPXNormPt, nbP, 0, kXNorm2Pt);
+  launch_reduce_batch(d, rb, false, s);
   if (h->nranks > 1) {
     if ((rc = allreduce(h, d.scal + kCost, 1, ncclSum))) return rc;
     if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
@@ -238,9 +241,9 @@ int compute_step(sfm_ba_handle* h, double radius) {
       if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
       launch_pack_upper(d, true, s);
     }
-    launch_pad_init(d, s);
+    launch_pad_init(d, s);  // also clears the failure flag
     mark_begin(h, kPhChol);
-    launch_cholesky(d, ++h->chol_epoch, s);
+    launch_cholesky(d, ++h->chol_epoch, s, false);
     mark_end(h);
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s);
@@ -270,20 +273,21 @@ int compute_step(sfm_ba_handle* h, double radius) {
   if (h->rank != 0 || h->mode == SFM_BA_STRUCT_ONLY)
     hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
   const int nbI = std::max(1, blocks_for(d.N_pad, 256));  // k_backsub_c grid
-  launch_reduce(d, kPModel, nbI, 0, kModelChange, s);
-  launch_reduce(d, kPNewCost, nbI, 0, kNewCost, s);
-  launch_reduce(d, kPStepPt, nbP, 0, kStep2Pt, s);
-  launch_reduce(d, kPStepCam, nbC, 0, kStep2Cam, s);
+  ReduceBatch rb;
+  rb.add(kPModel, nbI, 0, kModelChange);
+  rb.add(kPNewCost, nbI, 0, kNewCost);
+  rb.add(kPStepPt, nbP, 0, kStep2Pt);
+  rb.add(kPStepCam, nbC, 0, kStep2Cam);
   // bad-step flags: max over point_prep, cam_update and backsub partials
-  launch_reduce(d, kPBad, nbP, 1, kBadStep, s);
-  launch_reduce(d, kPBadCam, nbC, 1, kBadCam, s);
-  launch_reduce(d, kPBadBack, nbP, 1, kBadBack, s);
+  rb.add(kPBad, nbP, 1, kBadStep);
+  rb.add(kPBadCam, nbC, 1, kBadCam);
+  rb.add(kPBadBack, nbP, 1, kBadBack);
+  // ... and the Cholesky failure flag (an int) into the slot after the scalars
+  launch_reduce_batch(d, rb, true, s);
   if (h->nranks > 1) {
     if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
   }
-  // the Cholesky failure flag is an int on the device: fold it into the block
-  HIPCHK(hipMemcpyAsync(d.scal_host + kNumScalars, d.fail, sizeof(int), hipMemcpyDeviceToHost, s));
   return fetch_scalars(h);
 }
 
@@ -578,7 +582,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n_srow = int32_t(srow.size());
   ALLOC(d.srow, std::max<size_t>(1, srow.size()));
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
-  ALLOC(d.scal, size_t(kNumScalars));
+  ALLOC(d.scal, size_t(kNumScalars) + 1);  // + the Cholesky failure int (k_reduce_batch)
 #undef ALLOC
   if (hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
     free_problem(h);

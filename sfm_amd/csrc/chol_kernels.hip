@@ -735,8 +735,8 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 
 }  // namespace
 
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s) {
-  (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
+  if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   if (d.cflags && !d.chol_stepwise) {
     const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
     const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
