@@ -139,6 +139,69 @@ inline int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, 
   return SFM_OK;
 }
 
+// Drop-in for CTracker::computeOpticalFlow (CTracker.h:60,
+// CTracker.cpp:480-562).  The reference reads its member frames
+// (_prevFrame/_currFrame: getFrameGrey(), getPointsDistorted()) and fills
+// _prevIdx/_currIdx; the shim keeps the two frames' pyramids resident on
+// the device (one push per frame, the previous current frame becomes the
+// previous one, like the _prevFrame = _currFrame swap, CSfM.cpp:626-629).
+//   OpticalFlowTracker flow(width, height);       // once per frame size
+//   flow.pushFrame(_currFrame.getFrameGrey());    // every new frame
+//   bool ok = flow.computeOpticalFlow(_prevFrame.getPointsDistorted(),
+//                                     _currFrame.getPointsDistorted(),
+//                                     _prevIdx, _currIdx, _minFeatures);
+// GreyMat needs .data (uint8), .step (row bytes, cv::Mat's MatStep converts),
+// .cols, .rows; Point2 needs .x/.y.  Like the reference, the index vectors
+// are cleared first and the result is matchCount >= minFeatures.  The
+// _prevMatch/_currMatch point lists are the caller's getPointsAt gathers
+// (CTracker.cpp:548-549), unchanged.
+class OpticalFlowTracker {
+ public:
+  OpticalFlowTracker(int32_t width, int32_t height, int32_t device = 0, const sfm_klt_params* params = nullptr) {
+    rc_ = sfm_klt_create(device, width, height, params, &h_);
+  }
+  ~OpticalFlowTracker() {
+    if (h_) sfm_klt_destroy(h_);
+  }
+  OpticalFlowTracker(const OpticalFlowTracker&) = delete;
+  OpticalFlowTracker& operator=(const OpticalFlowTracker&) = delete;
+  int status() const { return rc_; }
+
+  template <class GreyMat>
+  int pushFrame(const GreyMat& grey) {
+    if (!h_) return rc_;
+    return sfm_klt_push_frame(h_, static_cast<const uint8_t*>(grey.data), int32_t(static_cast<size_t>(grey.step)));
+  }
+
+  template <class Point2>
+  bool computeOpticalFlow(const std::vector<Point2>& prevPtsDistorted, const std::vector<Point2>& currPtsDistorted,
+                          std::vector<int>& prevIdx, std::vector<int>& currIdx, int minFeatures = 5,
+                          int* rc_out = nullptr) {
+    prevIdx.clear();
+    currIdx.clear();
+    int rc = rc_;
+    if (h_) {
+      const int32_t n = int32_t(prevPtsDistorted.size()), m = int32_t(currPtsDistorted.size());
+      std::vector<double> p(2 * size_t(n)), c(2 * size_t(m));
+      for (int32_t i = 0; i < n; ++i) { p[2 * i] = prevPtsDistorted[i].x; p[2 * i + 1] = prevPtsDistorted[i].y; }
+      for (int32_t i = 0; i < m; ++i) { c[2 * i] = currPtsDistorted[i].x; c[2 * i + 1] = currPtsDistorted[i].y; }
+      std::vector<int32_t> pi(size_t(n > 0 ? n : 1)), ci(size_t(n > 0 ? n : 1));
+      int32_t nm = 0;
+      rc = sfm_klt_compute_optical_flow(h_, p.data(), n, c.data(), m, pi.data(), ci.data(), &nm, nullptr, nullptr);
+      if (rc == SFM_OK) {
+        prevIdx.assign(pi.begin(), pi.begin() + nm);
+        currIdx.assign(ci.begin(), ci.begin() + nm);
+      }
+    }
+    if (rc_out) *rc_out = rc;
+    return rc == SFM_OK && int(prevIdx.size()) >= minFeatures;
+  }
+
+ private:
+  sfm_klt_handle* h_ = nullptr;
+  int rc_ = SFM_OK;
+};
+
 }  // namespace sfm_compat
 
 #endif  // SFM_CTRACKER_COMPAT_HPP_

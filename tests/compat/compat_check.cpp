@@ -7,6 +7,7 @@
 
 struct Pt { double x, y; };          // cv::Point2d layout
 struct M33 { double val[9]; };       // cv::Matx33d layout
+struct Grey { const unsigned char* data; size_t step; int cols, rows; };  // cv::Mat (CV_8U) fields used
 
 int main() {
   double X[3][3] = {{1, 2, 3}, {4, 5, 6}, {7, 8, 9}};
@@ -32,6 +33,18 @@ int main() {
   if (sfm_device_count() == 0) {
     const int rc = sfm_compat::bundleAdjustmentStructAndPose(obs, cam, K, R, T, pts, SFM_BA_STRUCT_AND_POSE);
     if (rc != SFM_ENODEV || X[0][0] != 1 || r1[0] != 0.1) { std::printf("rc=%d\n", rc); return 6; }
+  }
+  // optical flow shim: without a GPU creation fails and nothing is matched
+  if (sfm_device_count() == 0) {
+    sfm_compat::OpticalFlowTracker flow(64, 48);
+    if (flow.status() != SFM_ENODEV) { std::printf("klt rc=%d\n", flow.status()); return 7; }
+    std::vector<unsigned char> img(64 * 48, 7);
+    Grey g{img.data(), 64, 64, 48};
+    if (flow.pushFrame(g) != SFM_ENODEV) return 8;
+    std::vector<int> pi = {1}, ci = {2};
+    int rc = 0;
+    std::vector<Pt> prev = {{10, 10}}, curr = {{11, 11}};
+    if (flow.computeOpticalFlow(prev, curr, pi, ci, 5, &rc) || rc != SFM_ENODEV || !pi.empty() || !ci.empty()) return 9;
   }
   std::printf("compat ok\n");
   return 0;
