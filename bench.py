@@ -129,6 +129,8 @@ def main() -> int:
     ap.add_argument("--cams", type=int, default=CAMS)
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
     ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker leg")
+    ap.add_argument("--comm", action="store_true",
+                    help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,6 +155,8 @@ def main() -> int:
         uid = [sfm_amd.BundleAdjuster.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ba.set_comm(world, rank, uid[0])
+    elif args.comm:
+        ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
     ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
     opts = sfm_amd.default_options()
 

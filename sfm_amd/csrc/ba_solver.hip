@@ -140,7 +140,7 @@ int device_cus(int device) {
 size_t packed_size(int n) { return size_t(n) * (n + 1) / 2 + size_t(n); }
 
 int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
-  if (h->nranks <= 1) return 0;
+  if (!h->comm) return 0;
   NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, op, h->comm, h->stream));
   return 0;
 }
@@ -213,7 +213,7 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   rb.add(kPXNormCam, nbC, 0, kXNorm2Cam);
   rb.add(kPXNormPt, nbP, 0, kXNorm2Pt);
   launch_reduce_batch(d, rb, false, s);
-  if (h->nranks > 1) {
+  if (h->comm) {
     if ((rc = allreduce(h, d.scal + kCost, 1, ncclSum))) return rc;
     if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
     if ((rc = allreduce(h, d.scal + kXNorm2Pt, 1, ncclSum))) return rc;
@@ -235,7 +235,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
-    if (h->nranks > 1 || h->force_pack) {
+    if (h->comm || h->force_pack) {
       // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
       launch_pack_upper(d, false, s);
       if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
@@ -284,7 +284,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
   rb.add(kPBadBack, nbP, 1, kBadBack);
   // ... and the Cholesky failure flag (an int) into the slot after the scalars
   launch_reduce_batch(d, rb, true, s);
-  if (h->nranks > 1) {
+  if (h->comm) {
     if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
   }
@@ -362,7 +362,8 @@ int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_
   if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
   h->nranks = nranks;
   h->rank = rank;
-  if (nranks == 1) return 0;
+  // a one-rank communicator is created too: it runs every collective of the
+  // sharded path (identities over one rank), which the one-GPU tests use
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
@@ -569,7 +570,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.Ucam, size_t(kUcam) * C);
   ALLOC(d.S, size_t(d.ld) * d.ld);
   h->force_pack = env_flag("SFM_FORCE_PACK");
-  if (h->nranks > 1 || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
+  if (h->comm || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);

@@ -5,7 +5,8 @@ problem shape, through the C ABI (tolerances as in test_gpu_parity.py).
 * the C3 residual + Jacobian pass against the oracle (1e-10 relative);
 * bitwise reproducibility of whole solves (atomics-free reductions);
 * the packed upper-triangle all-reduce path (SFM_FORCE_PACK) is an exact
-  copy on one rank;
+  copy on one rank, and so is the whole solve over a one-rank RCCL
+  communicator (every collective of the sharded path);
 * edge cases: a point seen twice by the same camera (Ceres adds two residual
   blocks over the same parameter blocks), cameras without observations,
   points with a single observation.
@@ -95,6 +96,32 @@ def test_packed_allreduce_path_is_exact(monkeypatch):
         sm2, _ = ba.solve()
         p2 = ba.parameters()
     assert sm1.final_cost == sm2.final_cost
+    for a, b in zip(p1, p2):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("mode", [sfm_amd.STRUCT_AND_POSE, sfm_amd.POSE_ONLY, sfm_amd.STRUCT_ONLY])
+def test_one_rank_rccl_communicator_is_exact(mode):
+    """The sharded path's collectives (RCCL all-reduce of U_c, the packed
+    reduced camera system, costs, norms and step flags -- SURVEY.md 8e) run
+    on a one-rank communicator: every one is an identity, so the solve must
+    equal the communicator-free one bitwise.  This is the multi-GPU code path
+    minus the cross-rank sums (those are covered on CPU by test_dist_gloo)."""
+    s = scene.generate(40, 6000, views=8, seed=0x5F3D2017 + 11)
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm1, tr1 = ba.solve(mode=mode)
+        p1 = ba.parameters()
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm2, tr2 = ba.solve(mode=mode)
+        p2 = ba.parameters()
+        ba.reset()
+        sm3, _ = ba.solve(mode=mode)
+    assert sm1.num_iterations == sm2.num_iterations == sm3.num_iterations
+    assert sm1.final_cost == sm2.final_cost == sm3.final_cost
+    assert [t["cost"] for t in tr1] == [t["cost"] for t in tr2]
     for a, b in zip(p1, p2):
         assert np.array_equal(a, b)
 
