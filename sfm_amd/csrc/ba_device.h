@@ -152,6 +152,7 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = tr
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
+void launch_read_touch(const double* p, size_t n, double* out, hipStream_t s);
 void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fail, hipStream_t s);
 int blocks_for(int64_t n, int threads);
 

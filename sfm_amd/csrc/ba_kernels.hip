@@ -1154,6 +1154,19 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
                                                                    d.jrec, d.eu, d.ypt, d.X_new, d.camRn,
                                                                    slot(d, kPModel), slot(d, kPNewCost));
 }
+// Diagnostic (bench_jacobian SFM_JAC_THRASH=2): stream-read n doubles, no
+// stores but one word -- evicts caches without leaving dirty lines.
+__global__ void k_read_touch(const double2* __restrict__ p, size_t n2, double* __restrict__ out) {
+  double acc = 0.0;
+  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x) {
+    const double2 v = p[i];
+    acc += v.x + v.y;
+  }
+  if (acc == 12345.678) out[0] = acc;
+}
+void launch_read_touch(const double* p, size_t n, double* out, hipStream_t s) {
+  k_read_touch<<<2048, 256, 0, s>>>(reinterpret_cast<const double2*>(p), n / 2, out);
+}
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);
 }

@@ -461,6 +461,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   }
   d.n_jchunks = int32_t(jchunks.size() / 4);
   d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
+  if (const char* jw = std::getenv("SFM_JAC_WG_PER_XCD")) {  // tuning knob (tools/sweep_jac.sh)
+    const int v = std::atoi(jw);
+    if (v > 0) d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, v));
+  }
   // camera-major copies for the Jacobian pass and the record map
   std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1), wcam(size_t(npad / 64) + 1, 0);
   for (int c = 0; c < C; ++c)
@@ -959,6 +963,27 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   launch_jacobian(d, true, h->stream);  // warm
+  if (const char* th = std::getenv("SFM_JAC_THRASH")) {
+    const int kind = std::atoi(th);  // 1: 288-MB write, 2: 288-MB read
+    // diagnostic: each pass timed alone behind a 288-MB write of another
+    // buffer (the cache/TLB state the pass meets inside an LM iteration)
+    float tot = 0.f;
+    for (int i = 0; i < reps; ++i) {
+      if (kind == 2) launch_read_touch(d.frec, size_t(kFRec) * size_t(d.N), d.scal + kNumScalars - 1, h->stream);
+      else HIPCHK(hipMemsetAsync(d.frec, 0, sizeof(double) * kFRec * size_t(d.N), h->stream));
+      HIPCHK(hipEventRecord(e0, h->stream));
+      launch_jacobian(d, true, h->stream);
+      HIPCHK(hipEventRecord(e1, h->stream));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms;
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (avg_ms) *avg_ms = double(tot) / reps;
+    return 0;
+  }
   HIPCHK(hipEventRecord(e0, h->stream));
   for (int i = 0; i < reps; ++i) launch_jacobian(d, true, h->stream);
   HIPCHK(hipEventRecord(e1, h->stream));
