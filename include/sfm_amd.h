@@ -246,6 +246,31 @@ int sfm_calc_optical_flow_pyr_lk(int32_t device, const uint8_t* prev, const uint
                                  int32_t height, const float* prev_pts, int32_t n, float* next_pts, uint8_t* status,
                                  const sfm_klt_params* params);
 
+/* ---- Corner detector of the optical-flow tracker ---
+ * CTracker::detectFeaturesOpticalFlow (CTracker.cpp:252-272):
+ * goodFeaturesToTrack(grey, pts, 500, 0.05, 10) + cornerSubPix(grey, pts,
+ * Size(5,5), Size(-1,-1), TermCriteria(COUNT|EPS, 20, 0.03)). */
+typedef struct sfm_gftt_params {
+  int32_t max_corners;     /* 500  maxFeats      (CTracker.cpp:253) */
+  int32_t subpix_win;      /* 5    subPixWinSize (CTracker.cpp:257), 1..7; 0 = no cornerSubPix */
+  int32_t subpix_max_iter; /* 20   TermCriteria COUNT (CTracker.cpp:256) */
+  int32_t min_features;    /* 5    _minFeatures  (CTracker.cpp:32): the reference's bool is n >= this */
+  double quality_level;    /* 0.05 qualityLvl    (CTracker.cpp:254) */
+  double min_distance;     /* 10   minDistance   (CTracker.cpp:255) */
+  double subpix_epsilon;   /* 0.03 TermCriteria EPS (CTracker.cpp:256) */
+} sfm_gftt_params;
+void sfm_gftt_default_params(sfm_gftt_params* p);
+/* Corners of the handle's current frame (after sfm_klt_push_frame), in the
+ * reference's order (response descending), refined to subpixel; pts
+ * [capacity][2] float, capacity >= max_corners (<= 4096). */
+int sfm_klt_detect_features(sfm_klt_handle* h, const sfm_gftt_params* params, float* pts, int32_t capacity,
+                            int32_t* n_pts);
+/* Device time (ms) of the last sfm_klt_detect_features. */
+int sfm_klt_detect_time(sfm_klt_handle* h, double* ms);
+/* One-shot form on a host frame (temporary handle). */
+int sfm_good_features_to_track(int32_t device, const uint8_t* grey, int32_t width, int32_t height, int32_t stride,
+                               const sfm_gftt_params* params, float* pts, int32_t capacity, int32_t* n_pts);
+
 /* Synthetic scenes, host-only.  Points [p_begin, p_end) of a
  * scene with n_pts_total points; every camera is returned.  Observations are
  * sorted by (point, camera); pt_idx is relative to p_begin.

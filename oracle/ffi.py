@@ -79,6 +79,15 @@ def lib():
                                                       c_void_p, c_void_p, c_int32, c_int32, c_int32, c_double,
                                                       c_double]
         L.oracle_calc_optical_flow_pyr_lk.restype = c_int
+        L.oracle_min_eigen.argtypes = [c_void_p, c_int32, c_int32, c_void_p]
+        L.oracle_min_eigen.restype = None
+        L.oracle_good_features.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_double, c_double, c_void_p]
+        L.oracle_good_features.restype = c_int32
+        L.oracle_corner_subpix.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int32, c_double]
+        L.oracle_corner_subpix.restype = None
+        L.oracle_detect_features_of.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_double, c_double, c_int32,
+                                                c_int32, c_double, c_void_p]
+        L.oracle_detect_features_of.restype = c_int32
         L.oracle_klt_associate.argtypes = [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_double,
                                            c_double, c_double, c_void_p, c_void_p]
         L.oracle_klt_associate.restype = c_int32
@@ -222,3 +231,40 @@ def klt_associate(prev_pts, flowed, status, curr_pts, max_match_distance=40.0, m
     k = lib().oracle_klt_associate(_p(prev_pts), _p(flowed), _p(status), n, _p(curr), m, max_match_distance,
                                    min_match_distance, max_org_feat_dist, _p(pi), _p(ci))
     return pi[:k].copy(), ci[:k].copy()
+
+
+def min_eigen(img):
+    """cornerMinEigenVal(blockSize 3, ksize 3) restatement (gftt_oracle.cpp)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((h, w), np.float32)
+    lib().oracle_min_eigen(_p(img), w, h, _p(out))
+    return out
+
+
+def good_features(img, max_corners=500, quality=0.05, min_distance=10.0):
+    """goodFeaturesToTrack restatement (CTracker.cpp:262 call): integer corners."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((max(1, max_corners), 2), np.float32)
+    n = lib().oracle_good_features(_p(img), w, h, max_corners, quality, min_distance, _p(out))
+    return out[:n].copy()
+
+
+def corner_subpix(img, pts, win=5, max_iter=20, eps=0.03):
+    """cornerSubPix restatement (CTracker.cpp:265 call)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 2).copy()
+    lib().oracle_corner_subpix(_p(img), w, h, _p(p), p.shape[0], win, max_iter, eps)
+    return p
+
+
+def detect_features_of(img, max_corners=500, quality=0.05, min_distance=10.0, win=5, max_iter=20, eps=0.03):
+    """CTracker::detectFeaturesOpticalFlow (CTracker.cpp:252-272) minus setPoints."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((max(1, max_corners), 2), np.float32)
+    n = lib().oracle_detect_features_of(_p(img), w, h, max_corners, quality, min_distance, win, max_iter, eps,
+                                        _p(out))
+    return out[:n].copy()

@@ -96,6 +96,18 @@ class KLTParams(ctypes.Structure):
     ]
 
 
+class GFTTParams(ctypes.Structure):
+    _fields_ = [
+        ("max_corners", c_int32),
+        ("subpix_win", c_int32),
+        ("subpix_max_iter", c_int32),
+        ("min_features", c_int32),
+        ("quality_level", c_double),
+        ("min_distance", c_double),
+        ("subpix_epsilon", c_double),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "sfm_abi_version": (c_int32, []),
@@ -139,6 +151,11 @@ _SIGNATURES = {
     "sfm_klt_phase_times": (c_int, [c_void_p, c_void_p]),
     "sfm_calc_optical_flow_pyr_lk": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_int32,
                                              c_void_p, c_void_p, POINTER(KLTParams)]),
+    "sfm_gftt_default_params": (None, [POINTER(GFTTParams)]),
+    "sfm_klt_detect_features": (c_int, [c_void_p, POINTER(GFTTParams), c_void_p, c_int32, POINTER(c_int32)]),
+    "sfm_klt_detect_time": (c_int, [c_void_p, POINTER(c_double)]),
+    "sfm_good_features_to_track": (c_int, [c_int32, c_void_p, c_int32, c_int32, c_int32, POINTER(GFTTParams),
+                                           c_void_p, c_int32, POINTER(c_int32)]),
     "sfm_scene_default_intrinsics": (None, [c_void_p]),
     "sfm_scene_generate": (c_int, [c_int32, c_int32, c_int32, c_int32, c_int32, c_uint64, c_double, c_double,
                                    c_double, c_double] + [c_void_p] * 10),
@@ -192,10 +209,16 @@ def default_klt_params() -> KLTParams:
     return p
 
 
+def default_gftt_params() -> GFTTParams:
+    p = GFTTParams()
+    lib().sfm_gftt_default_params(ctypes.byref(p))
+    return p
+
+
 def device_count() -> int:
     return int(lib().sfm_device_count())
 
 
-__all__ = ["lib", "check", "ptr", "BAOptions", "BASummary", "BAIteration", "KLTParams", "SfmError", "default_options",
-           "default_klt_params",
+__all__ = ["lib", "check", "ptr", "BAOptions", "BASummary", "BAIteration", "KLTParams", "GFTTParams", "SfmError",
+           "default_options", "default_klt_params", "default_gftt_params",
            "device_count", "exported_symbols", "LIB_PATH", "c_uint8"]

@@ -30,6 +30,7 @@
 #include <vector>
 #include "../../include/sfm_amd.h"
 #include "ordered_compact.h"
+#include "klt_internal.h"
 
 void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
 
@@ -349,6 +350,7 @@ struct sfm_klt_handle {
   // phase timing: [0,1] pyramid, [2,3] lk, [4,5] association
   hipEvent_t ev[6] = {};
   bool timed_push = false, timed_flow = false, timed_assoc = false;
+  void* gftt = nullptr;  // corner-detector state (gftt_kernels.hip)
 
   Pyr pyr(int slot) const {
     Pyr p{};
@@ -481,6 +483,7 @@ int sfm_klt_destroy(sfm_klt_handle* h) {
     if (b) hipFree(b);
   for (auto& e : h->ev)
     if (e) hipEventDestroy(e);
+  if (h->gftt) sfm_internal_gftt_free(h->gftt);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -635,3 +638,15 @@ int sfm_calc_optical_flow_pyr_lk(int32_t device, const uint8_t* prev, const uint
 }
 
 }  // extern "C"
+
+int sfm_internal_klt_frame(sfm_klt_handle* h, KltFrame* out) {
+  if (!h || !out) return kfail(SFM_EINVAL, "NULL argument");
+  if (h->n_frames == 0) return kfail(SFM_EINVAL, "no frame pushed");
+  hipSetDevice(h->device);
+  out->img = h->img[h->cur] + h->img_off[0];
+  out->w = h->lw[0];
+  out->h = h->lh[0];
+  out->stream = h->stream;
+  out->gftt_slot = &h->gftt;
+  return 0;
+}

@@ -9,6 +9,7 @@ descriptors -> uint8 [n][64]).
   matchFeatures (6 overloads)    CTracker.h:50-58, CTracker.cpp:114-149,
                                  211-250, 368-417, 419-477
   computeOpticalFlow             CTracker.h:60,  CTracker.cpp:480-562
+  detectFeaturesOpticalFlow      CTracker.h:48,  CTracker.cpp:252-272
 
 The reference passes parameter blocks as vector<double*> with one pointer
 per observation (duplicates across observations, identity by address,
@@ -135,3 +136,14 @@ class CTracker:
             raise RuntimeError("computeOpticalFlow: pushFrame() the previous and current frames first")
         self._prevIdx, self._currIdx = self._klt.compute_optical_flow(prevPtsDistorted, currPtsDistorted)
         return len(self._prevIdx) >= self._minFeatures
+
+    def detectFeaturesOpticalFlow(self) -> bool:
+        """goodFeaturesToTrack(500, 0.05, 10) + cornerSubPix(5x5, 20, 0.03) on
+        the current frame (CTracker.cpp:252-272); the corners (float32 [n][2],
+        what the reference hands to CFrame::setPoints) are kept in
+        self.currPoints; returns n >= _minFeatures (CTracker.cpp:267)."""
+        if self._klt is None:
+            raise RuntimeError("detectFeaturesOpticalFlow: pushFrame() a frame first")
+        from .klt import make_gftt_params
+        self.currPoints = self._klt.detect_features(make_gftt_params(min_features=self._minFeatures))
+        return len(self.currPoints) >= self._minFeatures

@@ -16,7 +16,7 @@ from ctypes import c_int32, c_void_p
 
 import numpy as np
 
-from ._ffi import KLTParams, check, default_klt_params, lib, ptr
+from ._ffi import GFTTParams, KLTParams, check, default_gftt_params, default_klt_params, lib, ptr
 
 
 def make_params(**kw) -> KLTParams:
@@ -24,6 +24,15 @@ def make_params(**kw) -> KLTParams:
     for k, v in kw.items():
         if not hasattr(p, k):
             raise AttributeError(f"KLTParams has no field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def make_gftt_params(**kw) -> GFTTParams:
+    p = default_gftt_params()
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise AttributeError(f"GFTTParams has no field {k!r}")
         setattr(p, k, v)
     return p
 
@@ -90,6 +99,23 @@ class KLTTracker:
             out = out + (flowed[:n].copy(), st[:n].copy())
         return out
 
+    def detect_features(self, params: GFTTParams | None = None, **kw) -> np.ndarray:
+        """CTracker::detectFeaturesOpticalFlow (CTracker.cpp:252-272) on the
+        current frame: goodFeaturesToTrack(500, 0.05, 10) + cornerSubPix(5x5,
+        20, 0.03) -> corners float32 [n][2] in response order (row T7)."""
+        p = params if params is not None else make_gftt_params(**kw)
+        cap = max(1, int(p.max_corners))
+        out = np.zeros((cap, 2), np.float32)
+        n = c_int32(0)
+        check(lib().sfm_klt_detect_features(self._h, ctypes.byref(p), ptr(out), cap, ctypes.byref(n)),
+              "sfm_klt_detect_features")
+        return out[:n.value].copy()
+
+    def detect_time_ms(self) -> float:
+        ms = ctypes.c_double(0.0)
+        check(lib().sfm_klt_detect_time(self._h, ctypes.byref(ms)), "sfm_klt_detect_time")
+        return ms.value
+
     def phase_times(self) -> dict:
         ms = np.zeros(3)
         check(lib().sfm_klt_phase_times(self._h, ptr(ms)), "sfm_klt_phase_times")
@@ -120,3 +146,16 @@ def calc_optical_flow_pyr_lk(prev, nxt, prev_pts, device: int = 0, **kw):
     check(lib().sfm_calc_optical_flow_pyr_lk(device, ptr(prev), ptr(nxt), w, h, ptr(pts), n, ptr(out), ptr(st),
                                              ctypes.byref(p)), "sfm_calc_optical_flow_pyr_lk")
     return out, st
+
+
+def good_features_to_track(grey, device: int = 0, **kw) -> np.ndarray:
+    """One-shot goodFeaturesToTrack + cornerSubPix (the row-T7 pair) on a host frame."""
+    g = np.ascontiguousarray(grey, np.uint8)
+    h, w = g.shape
+    p = make_gftt_params(**kw)
+    cap = max(1, int(p.max_corners))
+    out = np.zeros((cap, 2), np.float32)
+    n = c_int32(0)
+    check(lib().sfm_good_features_to_track(device, ptr(g), w, h, w, ctypes.byref(p), ptr(out), cap, ctypes.byref(n)),
+          "sfm_good_features_to_track")
+    return out[:n.value].copy()
