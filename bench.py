@@ -68,54 +68,91 @@ def cpu_baseline(scene) -> dict:
 
 
 def tracker_leg(device: int, steps: int, cpu: bool) -> dict:
-    """Config C5 tracker leg: one step = push a
-    1280x720 grey frame (upload + pyramid + Scharr derivatives, resident in
-    HBM) + CTracker::computeOpticalFlow of 500 points against ~550 detections
-    (calcOpticalFlowPyrLK 21x21 / 4 levels / <= 20 iterations + nearest-
-    detection association).  Frames cycle over 3 rendered synthetic frames."""
+    """Config C5 tracker leg (SURVEY.md §8a rows T7 + T6): one step = one
+    1280x720 grey frame through the reference's optical-flow loop:
+    push_frame (upload + pyramid + Scharr derivatives, resident in HBM),
+    CTracker::detectFeaturesOpticalFlow (goodFeaturesToTrack 500 / 0.05 / 10
+    + cornerSubPix 5x5 / 20 / 0.03) and CTracker::computeOpticalFlow of the
+    previous frame's corners into this frame's (calcOpticalFlowPyrLK 21x21 /
+    4 levels / <= 20 its + nearest-corner association).  Frames cycle over 3
+    rendered synthetic frames."""
     from sfm_amd import klt
     from sfm_amd.video import SyntheticVideo
     v = SyntheticVideo()
     frames = [v.frame(k) for k in range(3)]
-    rng = np.random.default_rng(0)
-    n_pts = 500
-    pts = [v.features(k, n_pts, rng) for k in range(3)]
-    dets = [v.detections(k, (k + 1) % 3, pts[k], rng) for k in range(3)]
     tr = klt.KLTTracker(v.w, v.h, device=device)
     tr.push_frame(frames[0])
-    ph = {"pyramid": 0.0, "lk": 0.0, "associate": 0.0}
+    prev = tr.detect_features()
+    ph = {"pyramid": 0.0, "detect": 0.0, "lk": 0.0, "associate": 0.0}
     warm = 5
-    matches = 0
+    matches = corners = 0
     for it in range(steps + warm):
         if it == warm:
             t0 = time.perf_counter()
             ph = {k: 0.0 for k in ph}
         k = (it + 1) % 3
         tr.push_frame(frames[k])
-        pi, _ = tr.compute_optical_flow(pts[(k - 1) % 3], dets[(k - 1) % 3])
-        matches = len(pi)
+        cur = tr.detect_features()
+        pi, _ = tr.compute_optical_flow(prev, cur)
+        prev = cur
+        matches, corners = len(pi), len(cur)
         for a, b in tr.phase_times().items():
             ph[a] += b
+        ph["detect"] += tr.detect_time_ms()
     wall = (time.perf_counter() - t0) / steps
-    out = {"workload": "C5 tracker: 1280x720 grey synthetic video, 500 points/frame, push_frame + "
-                       "computeOpticalFlow (calcOpticalFlowPyrLK 21x21, 4 levels, <=20 its, eps 0.03) + association",
-           "frames_per_s": 1.0 / wall, "ms_per_frame": wall * 1e3, "points_per_s": n_pts / wall,
+    out = {"workload": "C5 tracker: 1280x720 grey synthetic video, per frame push_frame + detectFeaturesOpticalFlow "
+                       "(GFTT 500/0.05/10 + cornerSubPix) + computeOpticalFlow (calcOpticalFlowPyrLK 21x21, 4 levels, "
+                       "<=20 its, eps 0.03) + association",
+           "frames_per_s": 1.0 / wall, "ms_per_frame": wall * 1e3, "corners_per_frame": corners,
            "matches_per_frame": matches, "levels": tr.num_levels,
            "device_ms_per_frame": {a: round(b / steps, 4) for a, b in ph.items()},
            "cpu_baseline": None}
     tr.close()
     if cpu:
         from oracle import ffi as O
-        reps = 20
+        reps = 10
         t0 = time.perf_counter()
+        c_prev = O.detect_features_of(frames[0])
         for r in range(reps):
             k = (r + 1) % 3
-            nx, st = O.calc_optical_flow_pyr_lk(frames[(k - 1) % 3], frames[k], pts[(k - 1) % 3])
-            O.klt_associate(pts[(k - 1) % 3].astype(np.float32), nx, st, dets[(k - 1) % 3])
+            c = O.detect_features_of(frames[k])
+            nx, st = O.calc_optical_flow_pyr_lk(frames[(k - 1) % 3], frames[k], c_prev)
+            O.klt_associate(c_prev, nx, st, c)
+            c_prev = c
         cw = (time.perf_counter() - t0) / reps
         out["cpu_baseline"] = {"frames_per_s": 1.0 / cw, "ms_per_frame": cw * 1e3, "cores": 1, "kind": "port",
-                               "sample": f"{reps} frames of the same work (both pyramids + LK + association) "
-                                         "on oracle/klt_oracle.cpp, 1 thread"}
+                               "sample": f"{reps} frames of the same work (detection + both pyramids + LK + "
+                                         "association) on oracle/gftt_oracle.cpp + klt_oracle.cpp, 1 thread"}
+    return out
+
+
+def incremental_ba_leg(device: int, cpu: bool) -> dict:
+    """Keyframe-sized solves (the incremental BA CSfM::bundleAdjustment runs
+    after each new keyframe, CSfM.cpp:259/970): BASELINE config C1 (20 cams /
+    2k points / 20k obs), a complete LM solve per call, problem upload
+    included (sfm_ba_solve one-shot, as the drop-in is called)."""
+    import sfm_amd
+    from sfm_amd import scene as S
+    sc = S.config("C1")
+    reps = 20
+    for it in range(reps + 3):
+        if it == 3:
+            t0 = time.perf_counter()
+        r, t, X = sc.copy_params()
+        sm, _ = sfm_amd.solve(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, r, t, X)
+    wall = (time.perf_counter() - t0) / reps
+    out = {"workload": "C1 keyframe BA: 20 cams / 2000 pts / 20000 obs, one-shot sfm_ba_solve (upload + LM + download)",
+           "ms_per_solve": wall * 1e3, "lm_iterations": sm.num_iterations,
+           "residual_evals_per_s": sc.n_obs * sm.num_residual_evaluations / wall, "cpu_baseline": None}
+    if cpu:
+        from oracle import ffi as O
+        t0 = time.perf_counter()
+        for _ in range(3):
+            r, t, X = sc.copy_params()
+            smo, _ = O.solve(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, r, t, X)
+        cw = (time.perf_counter() - t0) / 3
+        out["cpu_baseline"] = {"ms_per_solve": cw * 1e3, "cores": 1, "kind": "port",
+                               "sample": "3 C1 solves on oracle/ba_oracle.cpp, 1 thread"}
     return out
 
 
@@ -271,6 +308,7 @@ def main() -> int:
         out["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_tracker:
         out["tracker"] = tracker_leg(local_rank, 50, not args.no_cpu_baseline)
+        out["incremental_ba"] = incremental_ba_leg(local_rank, not args.no_cpu_baseline)
     if args.phases and rank == 0:
         print(json.dumps(phases, indent=1), file=sys.stderr)
     if rank == 0:
