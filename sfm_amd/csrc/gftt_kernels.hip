@@ -8,8 +8,9 @@
 // for op with contraction off, so results are bit-exact against it.
 //
 // Pipeline (one stream, one host sync for the candidate count):
-//   k_min_eig   32x8 output tile per workgroup: Sobel products of the
-//               (34x10) halo in LDS, direct 3x3 box sums, min eigenvalue;
+//   k_min_eig   64x16 output tile per workgroup: frame patch staged in LDS
+//               (interior tiles), Sobel products of the (66x18) halo,
+//               direct 3x3 box sums, min eigenvalue;
 //               frame maximum by an ordered-uint atomicMax.
 //   k_cand      threshold TOZERO + 3x3 dilate + local-max test per interior
 //               pixel; candidates append (value bits << 32 | raster index)
@@ -46,10 +47,11 @@ void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
 
 namespace {
 
-constexpr int kTX = 32, kTY = 8;       // k_min_eig output tile
+constexpr int kTX = 64, kTY = 16;      // k_min_eig output tile (256 threads, 4 pixels each)
+constexpr int kEigThreads = 256;
 constexpr int kBatch = 1024;           // k_select batch (= workgroup size)
 constexpr int kMaxCorners = 4096;      // LDS list of accepted corners
-constexpr int kNbr = 24;               // per-candidate in-batch conflict list
+constexpr int kMaxCells = 4096;        // k_select cell grids (LDS)
 constexpr int kMaxWin = 7;             // cornerSubPix half window
 constexpr int kMaxSub = (2 * kMaxWin + 3) * (2 * kMaxWin + 3);
 
@@ -76,95 +78,161 @@ __device__ __forceinline__ float float_of_ord(unsigned int o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-__global__ __launch_bounds__(kTX * kTY) void k_min_eig(const uint8_t* __restrict__ img, int w, int h,
-                                                       float* __restrict__ eig, unsigned int* __restrict__ max_ord) {
-  constexpr int HX = kTX + 2, HY = kTY + 2;
+__global__ __launch_bounds__(kEigThreads) void k_min_eig(const uint8_t* __restrict__ img, int w, int h,
+                                                        float* __restrict__ eig, unsigned int* __restrict__ max_ord) {
+  constexpr int HX = kTX + 2, HY = kTY + 2, IX = kTX + 4, IY = kTY + 4;
+  __shared__ int pix[IY][IX];
   __shared__ float cxx[HY][HX], cxy[HY][HX], cyy[HY][HX];
   __shared__ float rxx[HY][kTX], rxy[HY][kTX], ryy[HY][kTX];
-  __shared__ unsigned int red[kTX * kTY / 64];
+  __shared__ unsigned int red[kEigThreads / 64];
   const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY, t = threadIdx.x;
   const double scale = 1.0 / (4.0 * 3.0 * 255.0);
+  // interior tiles: the (kTX+4) x (kTY+4) frame patch staged in LDS, no
+  // reflection anywhere; border tiles read the frame through reflect-101
+  const bool inner = x0 >= 2 && y0 >= 2 && x0 + kTX + 2 <= w && y0 + kTY + 2 <= h;
+  if (inner) {
+    for (int q = t; q < IX * IY; q += kEigThreads) {
+      const int iy = q / IX, ix = q % IX;
+      pix[iy][ix] = img[size_t(y0 - 2 + iy) * w + (x0 - 2 + ix)];
+    }
+    __syncthreads();
+  }
   // Sobel products at the halo positions, each taken at its reflect-101
   // position (the box filter's border is in the products' coordinates)
-  for (int q = t; q < HX * HY; q += kTX * kTY) {
+  for (int q = t; q < HX * HY; q += kEigThreads) {
     const int hy = q / HX, hx = q % HX;
-    const int x = r101(x0 + hx - 1, w), y = r101(y0 + hy - 1, h);
-    const int xm = r101(x - 1, w), xp = r101(x + 1, w), ym = r101(y - 1, h), yp = r101(y + 1, h);
-    const uint8_t* rm = img + size_t(ym) * w;
-    const uint8_t* rc = img + size_t(y) * w;
-    const uint8_t* rp = img + size_t(yp) * w;
-    const int dx = (int(rm[xp]) - int(rm[xm])) + 2 * (int(rc[xp]) - int(rc[xm])) + (int(rp[xp]) - int(rp[xm]));
-    const int dy = (int(rp[xm]) - int(rm[xm])) + 2 * (int(rp[x]) - int(rm[x])) + (int(rp[xp]) - int(rm[xp]));
+    int dx, dy;
+    if (inner) {
+      const int* rm = pix[hy];
+      const int* rc = pix[hy + 1];
+      const int* rp = pix[hy + 2];
+      const int xm = hx, xc = hx + 1, xp = hx + 2;
+      dx = (rm[xp] - rm[xm]) + 2 * (rc[xp] - rc[xm]) + (rp[xp] - rp[xm]);
+      dy = (rp[xm] - rm[xm]) + 2 * (rp[xc] - rm[xc]) + (rp[xp] - rm[xp]);
+    } else {
+      const int x = r101(x0 + hx - 1, w), y = r101(y0 + hy - 1, h);
+      const int xm = r101(x - 1, w), xp = r101(x + 1, w), ym = r101(y - 1, h), yp = r101(y + 1, h);
+      const uint8_t* rm = img + size_t(ym) * w;
+      const uint8_t* rc = img + size_t(y) * w;
+      const uint8_t* rp = img + size_t(yp) * w;
+      dx = (int(rm[xp]) - int(rm[xm])) + 2 * (int(rc[xp]) - int(rc[xm])) + (int(rp[xp]) - int(rp[xm]));
+      dy = (int(rp[xm]) - int(rm[xm])) + 2 * (int(rp[x]) - int(rm[x])) + (int(rp[xp]) - int(rm[xp]));
+    }
     const float ix = float(double(dx) * scale), iy = float(double(dy) * scale);
     cxx[hy][hx] = ix * ix;
     cxy[hy][hx] = ix * iy;
     cyy[hy][hx] = iy * iy;
   }
   __syncthreads();
-  for (int q = t; q < HY * kTX; q += kTX * kTY) {
+  for (int q = t; q < HY * kTX; q += kEigThreads) {
     const int hy = q / kTX, ox = q % kTX;
     rxx[hy][ox] = (cxx[hy][ox] + cxx[hy][ox + 1]) + cxx[hy][ox + 2];
     rxy[hy][ox] = (cxy[hy][ox] + cxy[hy][ox + 1]) + cxy[hy][ox + 2];
     ryy[hy][ox] = (cyy[hy][ox] + cyy[hy][ox + 1]) + cyy[hy][ox + 2];
   }
   __syncthreads();
-  const int ox = t % kTX, oy = t / kTX, x = x0 + ox, y = y0 + oy;
   unsigned int mo = 0u;
-  if (x < w && y < h) {
-    const float sxx = (rxx[oy][ox] + rxx[oy + 1][ox]) + rxx[oy + 2][ox];
-    const float sxy = (rxy[oy][ox] + rxy[oy + 1][ox]) + rxy[oy + 2][ox];
-    const float syy = (ryy[oy][ox] + ryy[oy + 1][ox]) + ryy[oy + 2][ox];
-    const float A = sxx * 0.5f, B = sxy, C = syy * 0.5f;
-    const float e = (A + C) - __fsqrt_rn((A - C) * (A - C) + B * B);
-    eig[size_t(y) * w + x] = e;
-    mo = ord_of(e);
+  for (int q = t; q < kTX * kTY; q += kEigThreads) {
+    const int ox = q % kTX, oy = q / kTX, x = x0 + ox, y = y0 + oy;
+    if (x < w && y < h) {
+      const float sxx = (rxx[oy][ox] + rxx[oy + 1][ox]) + rxx[oy + 2][ox];
+      const float sxy = (rxy[oy][ox] + rxy[oy + 1][ox]) + rxy[oy + 2][ox];
+      const float syy = (ryy[oy][ox] + ryy[oy + 1][ox]) + ryy[oy + 2][ox];
+      const float A = sxx * 0.5f, B = sxy, C = syy * 0.5f;
+      const float e = (A + C) - __fsqrt_rn((A - C) * (A - C) + B * B);
+      eig[size_t(y) * w + x] = e;
+      mo = max(mo, ord_of(e));
+    }
   }
   for (int off = 32; off >= 1; off >>= 1) mo = max(mo, __shfl_xor(mo, off));
   if ((t & 63) == 0) red[t >> 6] = mo;
   __syncthreads();
   if (t == 0) {
     unsigned int m = red[0];
-    for (int i = 1; i < kTX * kTY / 64; ++i) m = max(m, red[i]);
+    for (int i = 1; i < kEigThreads / 64; ++i) m = max(m, red[i]);
     atomicMax(max_ord, m);
   }
 }
 
+// 64x64 pixels per 256-thread workgroup (16 per thread), one atomic per
+// workgroup: one counter hit once per wavefront still serialised ~14k
+// atomics (~12 ns each) on textured frames.
+constexpr int kCandT = 64;
 __global__ __launch_bounds__(256) void k_cand(const float* __restrict__ eig, int w, int h,
                                               const unsigned int* __restrict__ max_ord, double quality,
                                               unsigned long long* __restrict__ keys, int* __restrict__ count) {
-  const int x = blockIdx.x * 32 + (threadIdx.x & 31), y = blockIdx.y * 8 + (threadIdx.x >> 5);
-  if (x < 1 || y < 1 || x >= w - 1 || y >= h - 1) return;
+  __shared__ int wcnt[4];
+  __shared__ int s_base;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int x = blockIdx.x * kCandT + lane, yb = blockIdx.y * kCandT + wv;
   const float thr = float(double(float_of_ord(*max_ord)) * quality);
   auto T = [&](int xx, int yy) {
     const float v = eig[size_t(yy) * w + xx];
     return v > thr ? v : 0.0f;
   };
-  const float v = T(x, y);
-  if (v == 0.0f) return;
-  float d = v;
-  for (int yy = y - 1; yy <= y + 1; ++yy)
-    for (int xx = x - 1; xx <= x + 1; ++xx) d = fmaxf(d, T(xx, yy));
-  if (v != d) return;
-  const int slot = atomicAdd(count, 1);
-  keys[slot] = (static_cast<unsigned long long>(__float_as_uint(v)) << 32) | unsigned(y * w + x);
+  unsigned int mine = 0u;  // bit k: row yb + 4k holds a candidate
+  float val[kCandT / 4];
+#pragma unroll
+  for (int k = 0; k < kCandT / 4; ++k) {
+    const int y = yb + 4 * k;
+    val[k] = 0.0f;
+    if (x >= 1 && y >= 1 && x < w - 1 && y < h - 1) {
+      const float v = T(x, y);
+      if (v != 0.0f) {
+        float d = v;
+        for (int yy = y - 1; yy <= y + 1; ++yy)
+          for (int xx = x - 1; xx <= x + 1; ++xx) d = fmaxf(d, T(xx, yy));
+        if (v == d) {
+          mine |= 1u << k;
+          val[k] = v;
+        }
+      }
+    }
+  }
+  const int c = __popc(mine);
+  int incl = c;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off);
+    if (lane >= off) incl += v;
+  }
+  if (lane == 63) wcnt[wv] = incl;
+  __syncthreads();
+  if (t == 0) {
+    const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    s_base = tot ? atomicAdd(count, tot) : 0;
+  }
+  __syncthreads();
+  int slot = s_base + incl - c;
+  for (int k = 0; k < wv; ++k) slot += wcnt[k];
+#pragma unroll
+  for (int k = 0; k < kCandT / 4; ++k)
+    if (mine & (1u << k))
+      keys[slot++] = (static_cast<unsigned long long>(__float_as_uint(val[k])) << 32) |
+                     unsigned((yb + 4 * k) * w + x);
 }
 
 // Greedy min-distance selection over the sorted keys (see file header).
+// Conflicts are found through two cell grids in LDS (accepted corners and
+// the current batch): cells are at least min_distance wide, so every pair
+// closer than min_distance lies in the same or an adjacent cell.
 __global__ __launch_bounds__(kBatch) void k_select(const unsigned long long* __restrict__ keys, int n, int w,
-                                                  int max_corners, double md2, int use_dist,
-                                                  float2* __restrict__ out, int* __restrict__ n_out) {
-  __shared__ short ax[kMaxCorners], ay[kMaxCorners];
-  __shared__ short bx[kBatch], by[kBatch];
+                                                  int max_corners, double md2, int use_dist, int cs, int gw,
+                                                  int gh, float2* __restrict__ out, int* __restrict__ n_out) {
+  __shared__ short ax[kMaxCorners], ay[kMaxCorners], anext[kMaxCorners];
+  __shared__ short bx[kBatch], by[kBatch], bnext[kBatch];
+  __shared__ int ahead[kMaxCells], bhead[kMaxCells];
   __shared__ unsigned char st[kBatch];   // 0 undecided, 1 accepted, 2 rejected / absent
-  __shared__ short nb[kNbr][kBatch];
   __shared__ int wsum[kBatch / 64];
   __shared__ int s_flag, s_nacc;
   const int i = threadIdx.x, lane = i & 63, wv = i >> 6;
+  const int ncell = gw * gh;
+  for (int c = i; c < ncell; c += kBatch) ahead[c] = -1;
   if (i == 0) s_nacc = 0;
   __syncthreads();
   for (int base = 0; base < n; base += kBatch) {
     const int nacc = s_nacc;
     if (nacc >= max_corners) break;
+    for (int c = i; c < ncell; c += kBatch) bhead[c] = -1;
     const bool valid = base + i < n;
     int x = 0, y = 0;
     if (valid) {
@@ -172,47 +240,37 @@ __global__ __launch_bounds__(kBatch) void k_select(const unsigned long long* __r
       y = lin / w;
       x = lin - y * w;
     }
+    const int gx = x / cs, gy = y / cs;
     bx[i] = short(x);
     by[i] = short(y);
-    unsigned char s = valid ? 0 : 2;
     auto conflict = [&](int xx, int yy) {
       const int dx = x - xx, dy = y - yy;
       return double(dx * dx + dy * dy) < md2;
     };
+    unsigned char sv = valid ? 0 : 2;
     if (valid && use_dist)
-      for (int j = 0; j < nacc; ++j)
-        if (conflict(ax[j], ay[j])) { s = 2; break; }
-    st[i] = s;
-    __syncthreads();
-    // higher-priority conflicting candidates of this batch (overflow: rescan)
-    int nn = 0;
-    bool over = false;
-    if (s == 0 && use_dist)
-      for (int j = 0; j < i; ++j)
-        if (st[j] != 2 && conflict(bx[j], by[j])) {
-          if (nn < kNbr) nb[nn++][i] = short(j);
-          else over = true;
-        }
+      for (int cy = max(gy - 1, 0); cy <= min(gy + 1, gh - 1) && sv == 0; ++cy)
+        for (int cx = max(gx - 1, 0); cx <= min(gx + 1, gw - 1) && sv == 0; ++cx)
+          for (int j = ahead[cy * gw + cx]; j >= 0; j = anext[j])
+            if (conflict(ax[j], ay[j])) { sv = 2; break; }
+    st[i] = sv;
+    __syncthreads();  // bhead cleared, st / bx / by written
+    if (sv == 0 && use_dist) bnext[i] = short(atomicExch(&bhead[gy * gw + gx], i));
     __syncthreads();
     for (;;) {
       if (i == 0) s_flag = 0;
       __syncthreads();
       if (st[i] == 0) {
         bool any_acc = false, all_rej = true;
-        if (!over) {
-          for (int k = 0; k < nn; ++k) {
-            const unsigned char sj = st[nb[k][i]];
-            any_acc |= sj == 1;
-            all_rej &= sj == 2;
-          }
-        } else {
-          for (int j = 0; j < i; ++j)
-            if (conflict(bx[j], by[j])) {
-              const unsigned char sj = st[j];
-              any_acc |= sj == 1;
-              all_rej &= sj == 2;
-            }
-        }
+        if (use_dist)
+          for (int cy = max(gy - 1, 0); cy <= min(gy + 1, gh - 1); ++cy)
+            for (int cx = max(gx - 1, 0); cx <= min(gx + 1, gw - 1); ++cx)
+              for (int j = bhead[cy * gw + cx]; j >= 0; j = bnext[j])
+                if (j < i && conflict(bx[j], by[j])) {
+                  const unsigned char sj = st[j];
+                  any_acc |= sj == 1;
+                  all_rej &= sj == 2;
+                }
         if (any_acc) st[i] = 2;
         else if (all_rej) st[i] = 1;
         else s_flag = 1;  // still undecided
@@ -239,6 +297,7 @@ __global__ __launch_bounds__(kBatch) void k_select(const unsigned long long* __r
       ax[rank] = short(x);
       ay[rank] = short(y);
       out[rank] = make_float2(float(x), float(y));
+      if (use_dist) anext[rank] = short(atomicExch(&ahead[gy * gw + gx], rank));
     }
     __syncthreads();
     if (i == 0) s_nacc = min(max_corners, nacc + tot);
@@ -418,8 +477,8 @@ int sfm_klt_detect_features(sfm_klt_handle* kh, const sfm_gftt_params* params, f
   hipMemsetAsync(g->ints, 0, 4 * sizeof(int), s);
   hipMemcpyAsync(g->mask, mask.data(), mask.size() * sizeof(float), hipMemcpyHostToDevice, s);
   dim3 ge((f.w + kTX - 1) / kTX, (f.h + kTY - 1) / kTY);
-  k_min_eig<<<ge, kTX * kTY, 0, s>>>(f.img, f.w, f.h, g->eig, reinterpret_cast<unsigned int*>(g->ints));
-  dim3 gc((f.w + 31) / 32, (f.h + 7) / 8);
+  k_min_eig<<<ge, kEigThreads, 0, s>>>(f.img, f.w, f.h, g->eig, reinterpret_cast<unsigned int*>(g->ints));
+  dim3 gc((f.w + kCandT - 1) / kCandT, (f.h + kCandT - 1) / kCandT);
   k_cand<<<gc, 256, 0, s>>>(g->eig, f.w, f.h, reinterpret_cast<unsigned int*>(g->ints), prm.quality_level, g->keys,
                             g->ints + 1);
   int n_cand = 0;
@@ -431,9 +490,13 @@ int sfm_klt_detect_features(sfm_klt_handle* kh, const sfm_gftt_params* params, f
     if (hipcub::DeviceRadixSort::SortKeysDescending(g->sort_tmp, tmp, g->keys, g->keys_sorted, n_cand, 0, 64, s) !=
         hipSuccess)
       return gfail(SFM_EIO, "candidate sort failed");
+    // cells at least min_distance wide and few enough for LDS
+    int cs = std::max(1, int(std::ceil(prm.min_distance)));
+    while (size_t((f.w + cs - 1) / cs) * size_t((f.h + cs - 1) / cs) > size_t(kMaxCells)) ++cs;
+    const int gw = (f.w + cs - 1) / cs, gh = (f.h + cs - 1) / cs;
     k_select<<<1, kBatch, 0, s>>>(g->keys_sorted, n_cand, f.w, prm.max_corners,
-                                  prm.min_distance * prm.min_distance, prm.min_distance >= 1.0 ? 1 : 0, g->corners,
-                                  g->ints + 2);
+                                  prm.min_distance * prm.min_distance, prm.min_distance >= 1.0 ? 1 : 0, cs, gw, gh,
+                                  g->corners, g->ints + 2);
     const int max_iter = std::min(std::max(prm.subpix_max_iter, 1), 100);
     const double e = std::max(prm.subpix_epsilon, 0.0);
     if (prm.subpix_win > 0)
