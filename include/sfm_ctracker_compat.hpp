@@ -173,6 +173,41 @@ class OpticalFlowTracker {
     return sfm_klt_push_frame(h_, static_cast<const uint8_t*>(grey.data), int32_t(static_cast<size_t>(grey.step)));
   }
 
+  // Drop-in for CTracker::detectFeaturesOpticalFlow (CTracker.h:48,
+  // CTracker.cpp:252-272) on the frame pushed last: goodFeaturesToTrack
+  // (500, 0.05, 10) + cornerSubPix (5x5, 20, 0.03); `pts` receives the
+  // refined corners in the reference's order (what it hands to
+  // CFrame::setPoints); returns pts.size() >= minFeatures.
+  //   bool CTracker::detectFeaturesOpticalFlow() {
+  //     std::vector<cv::Point2f> pts;
+  //     if (!_flow.detectFeaturesOpticalFlow(pts, _minFeatures)) return false;
+  //     _currFrame.setPoints(pts);
+  //     return true;
+  //   }
+  template <class Point2f>
+  bool detectFeaturesOpticalFlow(std::vector<Point2f>& pts, int minFeatures = 5,
+                                 const sfm_gftt_params* params = nullptr, int* rc_out = nullptr) {
+    pts.clear();
+    int rc = rc_;
+    if (h_) {
+      sfm_gftt_params p;
+      if (params) p = *params;
+      else sfm_gftt_default_params(&p);
+      std::vector<float> buf(2 * size_t(p.max_corners > 0 ? p.max_corners : 1));
+      int32_t n = 0;
+      rc = sfm_klt_detect_features(h_, &p, buf.data(), p.max_corners, &n);
+      if (rc == SFM_OK) {
+        pts.resize(size_t(n));
+        for (int32_t i = 0; i < n; ++i) {
+          pts[i].x = buf[2 * i];
+          pts[i].y = buf[2 * i + 1];
+        }
+      }
+    }
+    if (rc_out) *rc_out = rc;
+    return rc == SFM_OK && int(pts.size()) >= minFeatures;
+  }
+
   template <class Point2>
   bool computeOpticalFlow(const std::vector<Point2>& prevPtsDistorted, const std::vector<Point2>& currPtsDistorted,
                           std::vector<int>& prevIdx, std::vector<int>& currIdx, int minFeatures = 5,

@@ -120,6 +120,15 @@ struct DevProblem {
   int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
   int32_t n_srow = 0;
   int2* pairs = nullptr;      // [n_pairs]
+  // fused Schur + Cholesky (one persistent launch; single rank only): task
+  // table (type, a, b, c): 0 = first row segment of camera a (holds block
+  // (a, a)), 3 = further row segment (a, first block b, count c),
+  // 1 = diagonal/rhs of camera a, 2 = Cholesky tile (a, b)
+  int4* stasks = nullptr;      // [n_stasks]
+  int32_t n_stasks = 0;
+  int32_t* scnt = nullptr;     // [nblk] Schur items done per tile column (monotone) | [nblk] per-launch targets | [C] S_cc stamps
+  unsigned long long* sticket = nullptr;
+  bool schur_fused = false;    // SFM_SCHUR_FUSED=1: one fused launch (experimental, slower: DESIGN.md §5)
   // reductions
   double* partials = nullptr; // scratch [kNumPartialSlots][max_blocks]
   int32_t max_blocks = 0;
@@ -159,5 +168,9 @@ int blocks_for(int64_t n, int threads);
 // ---- dense Cholesky (chol_kernels.hip) ----
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
+// Schur (row segments + diagonal/rhs) and Cholesky in ONE persistent launch
+// (single rank; the multi-rank path all-reduces S in between instead).
+void launch_schur_cholesky(const DevProblem& d, double radius, bool add_diag, int chol_epoch, int schur_epoch,
+                           hipStream_t s);
 
 }  // namespace sfm

@@ -58,6 +58,7 @@ struct sfm_ba_handle {
   std::vector<int32_t> pos;      // point-major q -> camera-major record index
   int32_t mode = SFM_BA_STRUCT_AND_POSE;  // of the running solve (CTracker.h:67)
   int32_t bs_epoch = 0;
+  int32_t schur_epoch = 0;       // launches of the fused Schur + Cholesky since the last set_problem
   int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem          // stamp of the last back-substitution launch (k_backsolve flags)
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
   std::vector<void*> allocs;
@@ -232,6 +233,19 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhPtPrep);
     launch_point_prep(d, radius, s);
     mark_end(h);
+    if (!h->comm && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags &&
+        !d.chol_stepwise) {
+      // single rank: Schur assembly and factorisation in one persistent
+      // launch (the padding rows are set first; they are no Schur output)
+      launch_pad_init(d, s);
+      mark_begin(h, kPhChol);
+      launch_schur_cholesky(d, radius, true, ++h->chol_epoch, ++h->schur_epoch, s);
+      mark_end(h);
+      mark_begin(h, kPhBack);
+      launch_backsolve(d, ++h->bs_epoch, s);
+      mark_end(h);
+      goto factored;
+    }
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
@@ -248,6 +262,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s);
     mark_end(h);
+  factored:;
   } else if (h->mode == SFM_BA_POSE_ONLY) {
     // block-diagonal camera system from the all-reduced U_c (same on every rank)
     launch_cam_solve(d, radius, s);
@@ -586,6 +601,55 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.seg, seg.size());
   d.n_srow = int32_t(srow.size());
   ALLOC(d.srow, std::max<size_t>(1, srow.size()));
+  // fused Schur + Cholesky task table (k_chol_schur_fused, chol_kernels.hip)
+  std::vector<int4> stasks;
+  std::vector<int32_t> scnt_init;
+  {
+    const int nb = d.nblk;
+    std::vector<int32_t> target(nb, 0);
+    std::vector<std::vector<int4>> items(nb);  // Schur items by the first tile column of their camera
+    size_t si = 0;
+    for (int c = 0; c < C; ++c) {
+      const int j0 = (6 * c) / kNB, j1 = (6 * c + 5) / kNB;
+      int nitem = 0;
+      bool first = true;
+      for (; si < srow.size() && srow[si].x == c; ++si, ++nitem, first = false)
+        items[j0].push_back(make_int4(first ? 0 : 3, c, srow[si].y, srow[si].z));
+      items[j0].push_back(make_int4(1, c, 0, 0));
+      ++nitem;
+      for (int j = j0; j <= j1; ++j) target[j] += nitem;
+    }
+    // Schur items run this many tile columns ahead of the tiles
+    int kLook = 16;  // best of 4 / 8 / 16 / 64 at C3
+    if (const char* lk = std::getenv("SFM_SCHUR_LOOKAHEAD")) kLook = std::max(1, std::atoi(lk));
+    int emitted = -1;
+    auto emit_upto = [&](int jmax) {
+      for (; emitted < std::min(jmax, nb - 1);) {
+        ++emitted;
+        stasks.insert(stasks.end(), items[emitted].begin(), items[emitted].end());
+      }
+    };
+    emit_upto(kLook - 1);
+    for (int j = 0; j < nb; ++j) {
+      for (int i = j; i < nb; ++i) stasks.push_back(make_int4(2, i, j, 0));
+      emit_upto(j + kLook);
+    }
+    scnt_init.assign(2 * size_t(nb) + size_t(C), 0);
+    for (int j = 0; j < nb; ++j) scnt_init[nb + j] = target[j];
+  }
+  d.n_stasks = int32_t(stasks.size());
+  {
+    // experimental, off by default: measured slower at C3 (2.15 ms per fused
+    // launch at the best lookahead vs 0.69 + 1.10 ms for the two launches):
+    // inside the Cholesky's footprint (421 VGPRs, 108 KB LDS: one workgroup
+    // of four waves per CU) the gather-bound Schur items lose the occupancy
+    // they need
+    const char* sf = std::getenv("SFM_SCHUR_FUSED");
+    d.schur_fused = sf ? std::atoi(sf) != 0 : false;
+  }
+  ALLOC(d.stasks, std::max<size_t>(1, stasks.size()));
+  ALLOC(d.scnt, std::max<size_t>(1, scnt_init.size()));
+  ALLOC(d.sticket, 1);
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars) + 1);  // + the Cholesky failure int (k_reduce_batch)
 #undef ALLOC
@@ -622,12 +686,16 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
   H2D(d.seg, seg.data(), seg.size());
   if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
+  if (!stasks.empty()) H2D(d.stasks, stasks.data(), stasks.size());
+  if (!scnt_init.empty()) H2D(d.scnt, scnt_init.data(), scnt_init.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
   HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
   HIPCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
   HIPCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
+  HIPCHK(hipMemsetAsync(d.sticket, 0, sizeof(unsigned long long), s));
   h->chol_epoch = 0;
+  h->schur_epoch = 0;
   d.n_cu = device_cus(h->device);
   d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   h->bs_epoch = 0;

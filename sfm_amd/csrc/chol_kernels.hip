@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include "ba_device.h"
+#include "schur_tasks.h"
 
 namespace sfm {
 namespace {
@@ -409,7 +410,7 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
 
 // Helper: one tile (i, j).  Wave w owns the 32x32 quadrant (c in cb.., r in
 // rb..), accumulated transposed as in k_chol_syrk.
-__device__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
+__device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
                                   int* sh, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -547,7 +548,7 @@ __device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
-__device__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
+__device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
                              double* Ls, double (*scr)[256], int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -654,6 +655,120 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Schur complement and Cholesky in ONE persistent launch (single rank).
+// The dense factorisation is a latency chain (the diagonal walker) that
+// leaves most CUs idle; the Schur assembly is a gather-bound pass over all
+// CUs.  Here the helper workgroups take, from one atomic ticket, a task
+// table built on the host in dependency order:
+//   Schur items of tile columns 0 and 1, then for j = 0, 1, ...:
+//   the Cholesky tiles (i, j) of column j, then the Schur items of column
+//   j + 2,
+// where a camera's items (its row segments, then its diagonal/rhs item)
+// belong to the first tile column its six columns touch.  A row segment or
+// diagonal item publishes (release) one count to every tile column the
+// camera touches; a tile (i, j) waits for column j's count before it reads
+// A_ij; a diagonal item waits for the S_cc stamp of its camera's first row
+// segment.  Every wait is on an item that sits earlier in the table or on
+// the walker, and all workgroups are co-resident, so the waits drain; they
+// are bounded anyway (fail bit 1).  The arithmetic is the separate
+// kernels' own (schur_tasks.h), so results are bitwise those of the
+// two-launch path.
+struct SchurArgs {
+  const int32_t* seg;
+  const int2* pairs;
+  const double* frec;
+  const int32_t* cam_rng;
+  const int32_t* cam_obs;
+  const double* jrec;
+  const double* mrec;
+  const double* Ucam;
+  const double* diag_c;
+  const int2* blk;
+  double radius;
+  int add_diag;
+  int C;
+};
+
+__device__ __forceinline__ void schur_publish(int* cnt, int c) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int j0 = (6 * c) / NB, j1 = (6 * c + 5) / NB;
+    for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(cnt + j, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Wave 0 waits until *f >= target, then the block proceeds.
+__device__ __forceinline__ void block_wait_count(const int* f, int target, int* fail) {
+  if (wave0()) {
+    long spins = 0;
+    bool ok = true;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > kFlagSpins) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) atomicOr(fail, 2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+constexpr int kPoolDoubles = 3 * NB * TS + 4 * 256;
+static_assert(kPoolDoubles >= kRowCh * kFRec, "row-segment chunk must fit the pool");
+static_assert(kPoolDoubles >= kDiagLds, "diagonal item must fit the pool");
+
+__global__ __launch_bounds__(256) void k_chol_schur_fused(double* __restrict__ A, int ld, int n, int nb,
+                                                          double* __restrict__ Winv, int* __restrict__ F,
+                                                          int* __restrict__ Pf,
+                                                          unsigned long long* __restrict__ ticket, int epoch,
+                                                          int sepoch, int ntask, const int4* __restrict__ tasks,
+                                                          int nhelp, int* __restrict__ scnt, SchurArgs sa,
+                                                          int* __restrict__ fail) {
+  __shared__ __attribute__((aligned(16))) double pool[kPoolDoubles];
+  __shared__ int sh[2];
+  double* T = pool;
+  double* Wl = pool + NB * TS;
+  double* Ls = pool + 2 * NB * TS;
+  double (*scr)[256] = reinterpret_cast<double (*)[256]>(pool + 3 * NB * TS);
+  if (blockIdx.x == 0) {
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, fail);
+    return;
+  }
+  int* colcnt = scnt;
+  const int* coltgt = scnt + nb;
+  int* camstamp = scnt + 2 * nb;
+  const unsigned long long base = (unsigned long long)(sepoch - 1) * (unsigned long long)(ntask + nhelp);
+  while (true) {
+    if (wave0()) {
+      const unsigned long long v = atomicAdd(ticket, threadIdx.x == 0 ? 1ULL : 0ULL);
+      const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
+      const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
+      sh[1] = int(((unsigned long long)hi << 32 | lo) - base);
+    }
+    __syncthreads();
+    const int tk = __builtin_amdgcn_readfirstlane(sh[1]);
+    __syncthreads();
+    if (tk >= ntask) break;
+    const int4 q = tasks[tk];
+    const int type = __builtin_amdgcn_readfirstlane(q.x), a = __builtin_amdgcn_readfirstlane(q.y),
+              b = __builtin_amdgcn_readfirstlane(q.z), c = __builtin_amdgcn_readfirstlane(q.w);
+    if (type == 2) {
+      block_wait_count(colcnt + b, sepoch * coltgt[b], fail);
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, a, b, T, sh, fail);
+    } else if (type == 1) {
+      block_wait(camstamp + a, sepoch, fail);
+      schur_diag_task<true>(a, sa.cam_rng, sa.cam_obs, sa.jrec, sa.mrec, sa.Ucam, sa.diag_c, sa.radius, sa.add_diag, A,
+                      ld, n, pool);
+      schur_publish(colcnt, a);
+    } else {
+      schur_row_task<4, true>(make_int4(a, b, c, 0), sa.seg, sa.pairs, sa.frec, sa.cam_rng, sa.blk, A, ld, pool);
+      if (type == 0) block_publish(camstamp + a, sepoch);  // S_cc written (its fence covers the rest)
+      schur_publish(colcnt, a);
+    }
+  }
+}
+
 // Back substitution L^T y = z (z = row n of the augmented factor, i.e.
 // L^-1 rhs), ONE launch: workgroup b owns block row b (64 unknowns) and
 //   y_b = W_b^T (z_b - sum_{k>b} L_kb^T y_k).
@@ -754,6 +869,16 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
     k_chol_trsm<<<m, 256, 0, s>>>(d.S, d.ld, k, d.invL);
     k_chol_syrk<<<m * (m + 1) / 2, 256, 0, s>>>(d.S, d.ld, k);
   }
+}
+
+void launch_schur_cholesky(const DevProblem& d, double radius, bool add_diag, int chol_epoch, int schur_epoch,
+                           hipStream_t s) {
+  const int nhelp = std::max(1, std::min(d.n_stasks, d.n_cu - 1));
+  SchurArgs sa{d.seg, d.pairs, d.frec, d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, d.blk, radius,
+               add_diag ? 1 : 0, d.C};
+  k_chol_schur_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.invL, d.cflags,
+                                               d.cflags + size_t(d.nblk) * d.nblk, d.sticket, chol_epoch,
+                                               schur_epoch, d.n_stasks, d.stasks, nhelp, d.scnt, sa, d.fail);
 }
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s) {

@@ -45,6 +45,9 @@ int main() {
     int rc = 0;
     std::vector<Pt> prev = {{10, 10}}, curr = {{11, 11}};
     if (flow.computeOpticalFlow(prev, curr, pi, ci, 5, &rc) || rc != SFM_ENODEV || !pi.empty() || !ci.empty()) return 9;
+    struct Pt2f { float x, y; };
+    std::vector<Pt2f> corners = {{1.f, 2.f}};
+    if (flow.detectFeaturesOpticalFlow(corners, 5, nullptr, &rc) || rc != SFM_ENODEV || !corners.empty()) return 10;
   }
   std::printf("compat ok\n");
   return 0;

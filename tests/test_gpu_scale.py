@@ -128,6 +128,30 @@ def test_one_rank_rccl_communicator_is_exact(mode):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
+def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
+    """The single-rank fused launch (Schur items + Cholesky tiles on one
+    ticket, k_chol_schur_fused) runs the separate kernels' arithmetic, so
+    whole solves are bitwise those of the two-launch path (the default;
+    the fused launch is the experimental SFM_SCHUR_FUSED=1)."""
+    s = scene.config(cfg)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SFM_SCHUR_FUSED", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+            ba.reset()
+            sm2, tr2 = ba.solve()  # a second launch sequence (epochs > 1)
+            p2 = ba.parameters()
+        out.append((sm.final_cost, tr, p, sm2.final_cost, p2))
+    (c0, t0, p0, d0, q0), (c1, t1, p1, d1, q1) = out
+    assert c0 == c1 == d0 == d1 and t0 == t1
+    for a, b, c in zip(p0, p1, q1):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
 def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
     """k_schur_row (default) and k_schur (SFM_SCHUR_ROW=0) sum every block's
