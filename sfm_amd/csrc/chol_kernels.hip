@@ -362,15 +362,26 @@ __device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
   if (wave0()) {
     if (!spin_until(f, epoch)) atomicOr(fail, 2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
   }
   __syncthreads();
 }
 
-// Stores of the whole block are made visible device-wide, then the flag.
+// Stores of the whole block are made visible device-wide, then the flag
+// (MI355X_MICROARCH.md, valid producer form): every wave drains its own
+// stores, a barrier, ONE agent-scope release by wave 0 (buffer_wbl2), a
+// drain (explicit: the compiler may drop the wait after buffer_wbl2 when it
+// believes the scoreboard empty), then a relaxed flag store.  The former
+// __threadfence() in every wave (write-back + invalidate, ~3.5 us) followed
+// by a release store paid the write-back twice on the walker's chain.
 __device__ __forceinline__ void block_publish(int* f, int epoch) {
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (wave0()) __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave0()) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Wave 0 finds how many of k = k_from.. (<= K) have both F(i,k) and F(j,k)
@@ -398,6 +409,7 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
       bound = k_from + 1;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
     *sh = bound > K + 1 ? K + 1 : bound;  // every lane: the same value
   }
   __syncthreads();
@@ -691,11 +703,15 @@ struct SchurArgs {
 };
 
 __device__ __forceinline__ void schur_publish(int* cnt, int c) {
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int j0 = (6 * c) / NB, j1 = (6 * c + 5) / NB;
-    for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(cnt + j, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave0()) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      const int j0 = (6 * c) / NB, j1 = (6 * c + 5) / NB;
+      for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(cnt + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -710,6 +726,7 @@ __device__ __forceinline__ void block_wait_count(const int* f, int target, int* 
     }
     if (!ok) atomicOr(fail, 2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
   }
   __syncthreads();
 }
@@ -817,6 +834,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
     if (wave0()) {  // scalar branch (see block_wait)
       if (!spin_until(flags + k, epoch)) timed_out = 1;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(timed_out)) break;
@@ -840,11 +858,13 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
     for (int c = 0; c < NB; ++c) s = fma(wr[c], v[c], s);
     y[size_t(k0) + t] = (t < nreal) ? s : 0.0;
   }
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (wave0()) {
     if (timed_out) atomicOr(fail, 2);
-    __hip_atomic_store(flags + b, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
