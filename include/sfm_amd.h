@@ -188,6 +188,15 @@ int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uin
                      int32_t desc_bytes, int32_t* best_idx, int32_t* best_dist, int32_t* second_idx,
                      int32_t* second_dist);
 
+/* CMap::getRepresentativeDescriptors (CMap.cpp:345-381),
+ * the map-point descriptors matched at CSfM.cpp:673 and :208-210.  Point i
+ * owns rows [row_off[i], row_off[i+1]) of desc [rows][desc_bytes] (one per
+ * observing keyframe; row_off[0] = 0, every point >= 1 row).  best[i] = row
+ * (within the point) minimising the sum of Hamming distances to the point's
+ * rows, the first on ties; out [n_pts][desc_bytes] (optional) = those rows. */
+int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const int32_t* row_off, int32_t n_pts,
+                                   int32_t desc_bytes, int32_t* best, uint8_t* out);
+
 /* Testing hook: solve the dense SPD system A y = b (A [n][n] row-major,
  * both triangles given; only the upper triangle is read) with the device
  * Cholesky + substitution kernels used for the reduced camera system.

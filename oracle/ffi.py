@@ -79,6 +79,8 @@ def lib():
                                                       c_void_p, c_void_p, c_int32, c_int32, c_int32, c_double,
                                                       c_double]
         L.oracle_calc_optical_flow_pyr_lk.restype = c_int
+        L.oracle_representative_descriptors.argtypes = [c_void_p, c_void_p, c_int32, c_int32, c_void_p]
+        L.oracle_representative_descriptors.restype = c_int
         L.oracle_min_eigen.argtypes = [c_void_p, c_int32, c_int32, c_void_p]
         L.oracle_min_eigen.restype = None
         L.oracle_good_features.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_double, c_double, c_void_p]
@@ -268,3 +270,15 @@ def detect_features_of(img, max_corners=500, quality=0.05, min_distance=10.0, wi
     n = lib().oracle_detect_features_of(_p(img), w, h, max_corners, quality, min_distance, win, max_iter, eps,
                                         _p(out))
     return out[:n].copy()
+
+
+def representative_descriptors(desc, row_off):
+    """CMap::getRepresentativeDescriptors restatement -> best row per point."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    row_off = np.ascontiguousarray(row_off, np.int32)
+    n = row_off.shape[0] - 1
+    best = np.zeros(max(1, n), np.int32)
+    rc = lib().oracle_representative_descriptors(_p(desc), _p(row_off), n, desc.shape[1], _p(best))
+    if rc:
+        raise ValueError("a point has no descriptor rows")
+    return best[:n].copy()

@@ -26,6 +26,8 @@
 // Reference UB: with fewer than 2 train rows
 // matches[i][1] is read out of range.  Restated as "no matches".
 //
+// Also CMap::getRepresentativeDescriptors (CMap.cpp:345-381), below.
+//
 // PARITY UNPINNED: no reference test or fixture covers the matcher.
 // ============================================================================
 #include <cstdint>
@@ -96,6 +98,38 @@ int oracle_match_features(const double* pts0, const uint8_t* desc0, int32_t n0, 
     }
   }
   return matchCount;
+}
+
+// CMap::getRepresentativeDescriptors (/root/reference/CMap.cpp:345-381),
+// restated: per point, the symmetric Hamming distance matrix of its rows
+// (NORM_HAMMING, float), column sums (reduce dim 0), then the first row with
+// the strictly smallest sum.  Returns -1 if a point has no rows (the
+// reference would read row -1).
+int oracle_representative_descriptors(const uint8_t* desc, const int32_t* row_off, int32_t n_pts, int32_t nbytes,
+                                      int32_t* best) {
+  for (int32_t i = 0; i < n_pts; ++i) {
+    const int32_t r0 = row_off[i], k = row_off[i + 1] - r0;
+    if (k <= 0) return -1;
+    std::vector<float> dist(size_t(k) * k, 0.0f);
+    for (int j = 0; j < k; ++j)
+      for (int q = j + 1; q < k; ++q) {
+        const float d = float(hamming(desc + size_t(r0 + j) * nbytes, desc + size_t(r0 + q) * nbytes, nbytes));
+        dist[size_t(j) * k + q] = d;
+        dist[size_t(q) * k + j] = d;
+      }
+    int min_idx = -1;
+    float min_d = 3.402823466e+38f;
+    for (int c = 0; c < k; ++c) {
+      float s = 0.0f;
+      for (int j = 0; j < k; ++j) s += dist[size_t(j) * k + c];
+      if (s < min_d) {
+        min_d = s;
+        min_idx = c;
+      }
+    }
+    best[i] = min_idx;
+  }
+  return 0;
 }
 
 }  // extern "C"

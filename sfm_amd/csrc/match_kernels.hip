@@ -129,6 +129,35 @@ int words_for(int nbytes) {
   return p;
 }
 
+// CMap::getRepresentativeDescriptors (CMap.cpp:345-381): one wavefront per
+// map point; lane r owns rows r, r+64, ... of the point's descriptor matrix
+// and sums its Hamming distances to every row (the reference's column sums
+// of the symmetric distance matrix: integers, exact in its float), then a
+// wave argmin keeps the lowest row on ties (the reference's strict `<` scan).
+// Row k's words are wave-uniform loads (one line per instruction).
+template <int W>
+__global__ __launch_bounds__(64) void k_repr(const uint64_t* __restrict__ d, const int* __restrict__ off, int n_pts,
+                                             int* __restrict__ best) {
+  const int p = blockIdx.x, l = threadIdx.x;
+  if (p >= n_pts) return;
+  const int r0 = off[p], k = off[p + 1] - r0;
+  const uint64_t* dp = d + size_t(r0) * W;
+  unsigned long long key = ~0ull;  // (sum << 32 | row): the min is the first minimal row
+  for (int r = l; r - l < k; r += 64) {
+    uint64_t x[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = r < k ? dp[size_t(r) * W + w] : 0ull;
+    unsigned int sum = 0;
+    for (int q = 0; q < k; ++q) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) sum += __popcll(x[w] ^ dp[size_t(q) * W + w]);
+    }
+    if (r < k) key = min(key, (static_cast<unsigned long long>(sum) << 32) | unsigned(r));
+  }
+  for (int o = 32; o >= 1; o >>= 1) key = min(key, static_cast<unsigned long long>(__shfl_xor(key, o)));
+  if (l == 0) best[p] = int(key & 0xffffffffu);
+}
+
 }  // namespace
 
 extern "C" {
@@ -209,6 +238,40 @@ int sfm_match_features(int32_t device, const double* pts0, const uint8_t* desc0,
     std::memcpy(idx1, host.data() + n0, m * sizeof(int));
     *n_matches = m;
   }
+  return 0;
+}
+
+int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const int32_t* row_off, int32_t n_pts,
+                                   int32_t desc_bytes, int32_t* best, uint8_t* out) {
+  if (n_pts < 0 || desc_bytes <= 0 || desc_bytes > 512) return mfail(SFM_EINVAL, "bad sizes");
+  if (n_pts == 0) return 0;
+  if (!desc || !row_off || !best) return mfail(SFM_EINVAL, "NULL argument");
+  if (row_off[0] != 0) return mfail(SFM_EINVAL, "row_off[0] must be 0");
+  for (int32_t i = 0; i < n_pts; ++i)
+    if (row_off[i + 1] <= row_off[i])
+      return mfail(SFM_EINVAL, "every point needs at least one descriptor (the reference reads row -1 otherwise)");
+  if (hipSetDevice(device) != hipSuccess) return mfail(SFM_ENODEV, "hipSetDevice failed");
+  const int W = words_for(desc_bytes);
+  const int rows = row_off[n_pts];
+  auto h = pack_words(desc, rows, desc_bytes, W);
+  DevBufs b;
+  auto* d = b.get<uint64_t>(h.size());
+  int* o = b.get<int>(size_t(n_pts) + 1);
+  int* r = b.get<int>(size_t(n_pts));
+  if (!d || !o || !r) return mfail(SFM_ENOMEM, "hipMalloc failed");
+  hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice);
+  hipMemcpy(o, row_off, (size_t(n_pts) + 1) * sizeof(int), hipMemcpyHostToDevice);
+  switch (W) {
+#define CASE(w) case w: k_repr<w><<<n_pts, 64>>>(d, o, n_pts, r); break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
+#undef CASE
+    default: return mfail(SFM_EINVAL, "descriptor width must be <= 512 bytes");
+  }
+  if (hipMemcpy(best, r, size_t(n_pts) * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return mfail(SFM_EIO, "kernel or copy failed");
+  if (out)
+    for (int32_t i = 0; i < n_pts; ++i)
+      std::memcpy(out + size_t(i) * desc_bytes, desc + (size_t(row_off[i]) + best[i]) * desc_bytes, desc_bytes);
   return 0;
 }
 
