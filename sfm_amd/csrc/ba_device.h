@@ -120,6 +120,12 @@ struct DevProblem {
   int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
   int32_t n_srow = 0;
   int2* pairs = nullptr;      // [n_pairs]
+  // small problems: pair-chunk items (block, first pair, end pair) with
+  // per-block item ranges and partial 6x6 sums (k_schur_split)
+  int4* sitems = nullptr;
+  int32_t n_sitems = 0;
+  int32_t* sboff = nullptr;    // [n_blk + 1]
+  double* spart = nullptr;     // [n_sitems][36]
   // fused Schur + Cholesky (one persistent launch; single rank only): task
   // table (type, a, b, c): 0 = first row segment of camera a (holds block
   // (a, a)), 3 = further row segment (a, first block b, count c),

@@ -569,6 +569,70 @@ __global__ __launch_bounds__(kThreads) void k_schur(int64_t n_blk, const int2* _
 // reuse within a row) are L1-miss-latency bound (TCP pending stalls), which
 // neither cooperative coalesced gathers nor point-sliced launches (to keep
 // F resident in the Infinity Cache) improved: both measured slower.
+// Small problems (few camera blocks, long pair lists: C1 has 210 blocks of
+// ~470 pairs): the owner-computes kernels would run one thread per block
+// through hundreds of dependent gathers.  k_schur_split gives every chunk of
+// kSplitPairs pairs of a block its own thread (partial 6x6 sums), and
+// k_schur_split_reduce adds a block's chunks in chunk order: deterministic,
+// atomics-free, fully parallel.
+__global__ __launch_bounds__(kThreads) void k_schur_split(int n_items, const int4* __restrict__ items,
+                                                          const int2* __restrict__ pairs,
+                                                          const double* __restrict__ frec,
+                                                          double* __restrict__ part) {
+  const int it = blockIdx.x * kThreads + threadIdx.x;
+  if (it >= n_items) return;
+  const int4 w = items[it];  // (block, first pair, end pair, -)
+  double acc[36];
+#pragma unroll
+  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+  for (int k = w.y; k < w.z; ++k) {
+    const int2 pr = pairs[k];
+    const double* A1 = frec + size_t(pr.x) * kFRec;
+    const double* A2 = frec + size_t(pr.y) * kFRec;
+    double a1[kFRec], g[kFRec];
+#pragma unroll
+    for (int f = 0; f < kFRec; f += 2) {
+      const double2 x = ld2(A1 + f), y = ld2(A2 + f);
+      a1[f] = x.x; a1[f + 1] = x.y; g[f] = y.x; g[f + 1] = y.y;
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int v = 0; v < 6; ++v)
+        acc[6 * u + v] += a1[3 * u] * g[3 * v] + a1[3 * u + 1] * g[3 * v + 1] + a1[3 * u + 2] * g[3 * v + 2];
+  }
+  double* dst = part + size_t(it) * 36;
+#pragma unroll
+  for (int e = 0; e < 36; e += 2) st2(dst + e, acc[e], acc[e + 1]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_schur_split_reduce(int64_t n_blk, const int2* __restrict__ blk,
+                                                                 const int32_t* __restrict__ boff,
+                                                                 const double* __restrict__ part,
+                                                                 double* __restrict__ S, int ld) {
+  const int64_t b = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (b >= n_blk) return;
+  double acc[36];
+#pragma unroll
+  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+  for (int it = boff[b]; it < boff[b + 1]; ++it) {
+    const double* src = part + size_t(it) * 36;
+#pragma unroll
+    for (int e = 0; e < 36; e += 2) {
+      const double2 x = ld2(src + e);
+      acc[e] += x.x;
+      acc[e + 1] += x.y;
+    }
+  }
+  const int2 cc = blk[b];
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
+#pragma unroll
+    for (int v = 0; v < 6; v += 2) st2(row + v, -acc[6 * u + v], -acc[6 * u + v + 1]);
+  }
+}
+
 constexpr int kRowChunkLds = kRowCh * kFRec;
 __global__ __launch_bounds__(kThreads) void k_schur_row(const int4* __restrict__ work,
                                                         const int32_t* __restrict__ seg,
@@ -928,7 +992,12 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
     k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
-  if (d.n_blk && d.schur_row && d.n_srow)
+  if (d.n_blk && d.n_sitems) {
+    k_schur_split<<<blocks_for(d.n_sitems, kThreads), kThreads, 0, s>>>(d.n_sitems, d.sitems, d.pairs, d.frec,
+                                                                         d.spart);
+    k_schur_split_reduce<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.sboff, d.spart, d.S,
+                                                                            d.ld);
+  } else if (d.n_blk && d.schur_row && d.n_srow)
     k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
   else if (d.n_blk)
     k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);

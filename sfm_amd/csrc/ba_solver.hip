@@ -8,6 +8,7 @@
 // chol_kernels.hip and only ~10 scalars cross PCIe per iteration.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <map>
 
 #include <algorithm>
 #include <array>
@@ -61,7 +62,8 @@ struct sfm_ba_handle {
   int32_t schur_epoch = 0;       // launches of the fused Schur + Cholesky since the last set_problem
   int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem          // stamp of the last back-substitution launch (k_backsolve flags)
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
-  std::vector<void*> allocs;
+  std::vector<std::pair<size_t, void*>> allocs;  // (bytes, buffer) of the resident problem
+  std::multimap<size_t, void*> pool;             // buffers of the previous problem, reused by size
   bool has_problem = false;
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -77,22 +79,43 @@ struct sfm_ba_handle {
 
 namespace {
 
+// Device buffers are taken from the handle's pool (the previous problem's
+// buffers, best fit within 2x) before hipMalloc: repeated keyframe-sized
+// solves (CSfM::bundleAdjustment after every keyframe) then allocate
+// nothing.  Contents are never assumed: set_problem initialises every
+// buffer it relies on.
 template <typename T>
 int dalloc(sfm_ba_handle* h, T** p, size_t count) {
-  void* q = nullptr;
   if (count == 0) count = 1;
-  hipError_t e = hipMalloc(&q, count * sizeof(T));
-  if (e != hipSuccess) return fail(SFM_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  h->allocs.push_back(q);
+  const size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+  auto it = h->pool.lower_bound(bytes);
+  void* q = nullptr;
+  size_t got = bytes;
+  if (it != h->pool.end() && it->first <= 2 * bytes) {
+    q = it->second;
+    got = it->first;
+    h->pool.erase(it);
+  } else {
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return fail(SFM_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  h->allocs.push_back({got, q});
   *p = static_cast<T*>(q);
   return 0;
 }
 
+void release_pool(sfm_ba_handle* h) {
+  for (auto& kv : h->pool) hipFree(kv.second);
+  h->pool.clear();
+}
+
+// Retires the problem's buffers into the pool (freed by release_pool).
 void free_problem(sfm_ba_handle* h) {
-  for (void* p : h->allocs) hipFree(p);
+  for (auto& a : h->allocs) h->pool.insert(a);
   h->allocs.clear();
-  if (h->d.scal_host) { hipHostFree(h->d.scal_host); h->d.scal_host = nullptr; }
+  double* keep = h->d.scal_host;  // pinned mirror: kept for the handle's life
   h->d = DevProblem();
+  h->d.scal_host = keep;
   h->has_problem = false;
 }
 
@@ -233,7 +256,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhPtPrep);
     launch_point_prep(d, radius, s);
     mark_end(h);
-    if (!h->comm && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags &&
+    if (!h->comm && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags && !d.n_sitems &&
         !d.chol_stepwise) {
       // single rank: Schur assembly and factorisation in one persistent
       // launch (the padding rows are set first; they are no Schur output)
@@ -356,6 +379,8 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   hipSetDevice(h->device);
   hipStreamSynchronize(h->stream);
   free_problem(h);
+  release_pool(h);
+  if (h->d.scal_host) hipHostFree(h->d.scal_host);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -601,6 +626,29 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.seg, seg.size());
   d.n_srow = int32_t(srow.size());
   ALLOC(d.srow, std::max<size_t>(1, srow.size()));
+  // small problems: split every block's pair list into chunks (k_schur_split)
+  std::vector<int4> sitems;
+  std::vector<int32_t> sboff;
+  {
+    int64_t kSplitMaxBlocks = 8192;  // C1: 210, C2: 5050, C3: 125250 blocks
+    // chunk length: enough items to fill the chip, few partials to reduce
+    // (measured best: 16 pairs at C1's 0.1M pairs, 64 at C2's 2.3M)
+    int kSplitPairs = int(std::min<int64_t>(64, std::max<int64_t>(16, d.n_pairs / 32768)));
+    if (const char* e = std::getenv("SFM_SCHUR_SPLIT_MAXBLK")) kSplitMaxBlocks = std::atoll(e);
+    if (const char* e = std::getenv("SFM_SCHUR_SPLIT_PAIRS")) kSplitPairs = std::max(1, std::atoi(e));
+    const char* sp = std::getenv("SFM_SCHUR_SPLIT");
+    const bool split = (sp ? std::atoi(sp) != 0 : true) && d.n_blk > 0 && d.n_blk <= kSplitMaxBlocks;
+    if (split) {
+      sboff.push_back(0);
+      for (int64_t b = 0; b < d.n_blk; ++b) {
+        const int k0 = seg[b], k1 = seg[b + 1];
+        if (k1 == k0) sitems.push_back(make_int4(int(b), k0, k1, 0));
+        for (int k = k0; k < k1; k += kSplitPairs) sitems.push_back(make_int4(int(b), k, std::min(k1, k + kSplitPairs), 0));
+        sboff.push_back(int32_t(sitems.size()));
+      }
+    }
+  }
+  d.n_sitems = int32_t(sitems.size());
   // fused Schur + Cholesky task table (k_chol_schur_fused, chol_kernels.hip)
   std::vector<int4> stasks;
   std::vector<int32_t> scnt_init;
@@ -647,13 +695,18 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     const char* sf = std::getenv("SFM_SCHUR_FUSED");
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
+  ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
+  ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
+  ALLOC(d.spart, 36 * std::max<size_t>(1, sitems.size()));
   ALLOC(d.stasks, std::max<size_t>(1, stasks.size()));
   ALLOC(d.scnt, std::max<size_t>(1, scnt_init.size()));
   ALLOC(d.sticket, 1);
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars) + 1);  // + the Cholesky failure int (k_reduce_batch)
 #undef ALLOC
-  if (hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
+  release_pool(h);  // what the new problem did not reuse
+  if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
+    d.scal_host = nullptr;
     free_problem(h);
     return fail(SFM_ENOMEM, "hipHostMalloc failed");
   }
@@ -687,6 +740,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   H2D(d.seg, seg.data(), seg.size());
   if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
   if (!stasks.empty()) H2D(d.stasks, stasks.data(), stasks.size());
+  if (!sitems.empty()) H2D(d.sitems, sitems.data(), sitems.size());
+  if (!sboff.empty()) H2D(d.sboff, sboff.data(), sboff.size());
   if (!scnt_init.empty()) H2D(d.scnt, scnt_init.data(), scnt_init.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
@@ -919,15 +974,20 @@ int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const 
   }
   int dev = 0;
   hipGetDevice(&dev);
-  sfm_ba_handle* h = nullptr;
-  int rc = sfm_ba_create(dev, &h);
-  if (rc) return rc;
+  // One cached handle per device and calling thread: the drop-in is called
+  // once per keyframe (CSfM.cpp:259, 970), so the stream, the pinned mirror
+  // and (through the pool) the device buffers are created once, not per call
+  // (measured at C1: create 1.7 ms + destroy 2.2 ms against a 1.9-ms solve).
+  static thread_local std::map<int, sfm_ba_handle*> cache;
+  sfm_ba_handle*& h = cache[dev];
+  int rc = 0;
+  if (!h && (rc = sfm_ba_create(dev, &h))) {
+    h = nullptr;
+    return rc;
+  }
   rc = sfm_ba_set_problem(h, n_obs, obs_uv, cam_idx, pt_idx, n_cams, K9, rot, t, n_pts, X);
   if (!rc) rc = sfm_ba_solve_resident(h, opts, mode, summary, trace, trace_cap, trace_len);
   if (!rc) rc = sfm_ba_get_parameters(h, rot, t, X);
-  std::string err = g_err;
-  sfm_ba_destroy(h);
-  g_err = err;
   return rc;
 }
 

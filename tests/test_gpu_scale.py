@@ -135,6 +135,7 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
     whole solves are bitwise those of the two-launch path (the default;
     the fused launch is the experimental SFM_SCHUR_FUSED=1)."""
     s = scene.config(cfg)
+    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
     out = []
     for flag in ("0", "1"):
         monkeypatch.setenv("SFM_SCHUR_FUSED", flag)
@@ -155,8 +156,10 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
 def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
     """k_schur_row (default) and k_schur (SFM_SCHUR_ROW=0) sum every block's
-    pairs in the same order: whole solves are bitwise identical."""
+    pairs in the same order: whole solves are bitwise identical (the
+    small-problem split path, which sums pair chunks, is switched off)."""
     s = scene.config(cfg)
+    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("SFM_SCHUR_ROW", flag)
@@ -167,6 +170,51 @@ def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
     assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
     for a, b in zip(out[0][2], out[1][2]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_split_schur_small_problems(monkeypatch, cfg):
+    """Keyframe-sized problems sum each block's pairs in chunks
+    (k_schur_split, default up to 8192 blocks): deterministic run to run,
+    and the same solve as the one-thread-per-block order to rounding."""
+    s = scene.config(cfg)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_SCHUR_SPLIT", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+            ba.reset()
+            sm2, _ = ba.solve()
+            p2 = ba.parameters()
+        assert sm.final_cost == sm2.final_cost
+        for a, b in zip(p, p2):
+            assert np.array_equal(a, b)
+        res[flag] = (sm, tr, p)
+    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
+    assert s1.num_iterations == s0.num_iterations
+    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
+    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
+    for a, b in zip(p1, p0):
+        assert _rel(a, b) < 1e-6
+
+
+def test_one_shot_solves_reuse_the_cached_handle():
+    """sfm_ba_solve keeps one handle per device and thread (buffers pooled):
+    back-to-back one-shot solves of different sizes give the resident
+    API's results."""
+    for cfg in ("C1", "C2", "C1"):
+        s = scene.config(cfg)
+        r, t, X = s.copy_params()
+        sm, _ = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm2, _ = ba.solve()
+            p2 = ba.parameters()
+        assert sm.final_cost == sm2.final_cost
+        for a, b in zip((r, t, X), p2):
+            assert np.array_equal(a, b)
 
 
 def _append_obs(s, cam, pt, uv):
