@@ -367,6 +367,19 @@ __device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
   __syncthreads();
 }
 
+// Write-through publication (MI355X_MICROARCH.md: a producer that stores
+// every handed-off byte sc1 and drains every wave before the flag needs no
+// agent release; the consumers keep their acquire): the diagonal walker's
+// L / W tiles, so its chain pays no L2 write-back per publication.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void block_publish_wt(int* f, int epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave0()) __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Stores of the whole block are made visible device-wide, then the flag
 // (MI355X_MICROARCH.md, valid producer form): every wave drains its own
 // stores, a barrier, ONE agent-scope release by wave 0 (buffer_wbl2), a
@@ -602,12 +615,12 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      A[size_t(j0 + c) * ld + j0 + r] = T[c * TS + r];
-      Wk[c * NB + r] = Wl[c * TS + r];
+      st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+      st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
-    block_publish(F + j * nb + j, epoch);
+    block_publish_wt(F + j * nb + j, epoch);
     if (j + 1 == nb) break;
     // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
     const int i0 = j0 + NB;
@@ -624,8 +637,12 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     trsm_lds(T, Wl, x, lane);
     put_tile(Ls, x, lane);
     __syncthreads();
-    store_tile(A, ld, i0, j0, Ls);
-    block_publish(F + (j + 1) * nb + j, epoch);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+    }
+    block_publish_wt(F + (j + 1) * nb + j, epoch);
   }
 }
 
