@@ -174,6 +174,12 @@ int sfm_ba_sync(sfm_ba_handle* h);
  * calls sfm_ba_set_comm before sfm_ba_set_problem. */
 int sfm_comm_unique_id(uint8_t out[128]);
 int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* Test hook: the same sharded path with the all-reduce done by a host
+ * callback (in place on `count` doubles; op 0 = sum, 1 = max; return 0 on
+ * success), e.g. over gloo: several ranks can then share ONE GPU, which
+ * RCCL does not allow.  Replaces any RCCL communicator. */
+typedef int (*sfm_allreduce_fn)(double* buf, int64_t count, int32_t op, void* user);
+int sfm_ba_set_host_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_allreduce_fn fn, void* user);
 
 /* Hamming 2-NN matcher + the reference's sequential acceptance rule.
  *   pts0/pts1 [n][2] double positions, desc0/desc1 [n][desc_bytes] (BRISK: 64)

@@ -68,6 +68,23 @@ class BundleAdjuster:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().sfm_ba_set_comm(self._h, nranks, rank, buf), "sfm_ba_set_comm")
 
+    # test hook: the sharded path with a host all-reduce (several ranks on ONE GPU)
+    ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(c_double), ctypes.c_int64, ctypes.c_int32,
+                                    c_void_p)
+
+    def set_host_comm(self, nranks: int, rank: int, allreduce) -> None:
+        """allreduce(array float64 view, op) with op 0 = sum, 1 = max, in place
+        (e.g. torch.distributed over gloo); see sfm_ba_set_host_comm."""
+        def _cb(buf, count, op, user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, (int(count),)), int(op))
+                return 0
+            except Exception:
+                return 1
+        self._host_cb = BundleAdjuster.ALLREDUCE_FN(_cb)  # kept alive with the handle
+        check(lib().sfm_ba_set_host_comm(self._h, nranks, rank, ctypes.cast(self._host_cb, c_void_p), None),
+              "sfm_ba_set_host_comm")
+
     # ---- problem ---------------------------------------------------------
     def set_problem(self, uv, cam_idx, pt_idx, K9, rot, t, X) -> None:
         uv, K9, rot, t, X = _f64(uv), _f64(K9), _f64(rot), _f64(t), _f64(X)

@@ -68,6 +68,11 @@ struct sfm_ba_handle {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // host-callback collective (sfm_ba_set_host_comm: tests run the sharded
+  // path with several ranks on one GPU, where RCCL allows one rank per GPU)
+  sfm_allreduce_fn host_fn = nullptr;
+  void* host_user = nullptr;
+  std::vector<double> host_buf;
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -161,9 +166,21 @@ int device_cus(int device) {
   return prop.multiProcessorCount;
 }
 
+bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
+
 size_t packed_size(int n) { return size_t(n) * (n + 1) / 2 + size_t(n); }
 
 int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
+  if (h->host_fn) {
+    h->host_buf.resize(count);
+    HIPCHK(hipMemcpyAsync(h->host_buf.data(), buf, count * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->host_fn(h->host_buf.data(), int64_t(count), op == ncclMax ? 1 : 0, h->host_user) != 0)
+      return fail(SFM_EIO, "host all-reduce callback failed");
+    HIPCHK(hipMemcpyAsync(buf, h->host_buf.data(), count * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+  }
   if (!h->comm) return 0;
   NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, op, h->comm, h->stream));
   return 0;
@@ -237,7 +254,7 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   rb.add(kPXNormCam, nbC, 0, kXNorm2Cam);
   rb.add(kPXNormPt, nbP, 0, kXNorm2Pt);
   launch_reduce_batch(d, rb, false, s);
-  if (h->comm) {
+  if (sharded(h)) {
     if ((rc = allreduce(h, d.scal + kCost, 1, ncclSum))) return rc;
     if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
     if ((rc = allreduce(h, d.scal + kXNorm2Pt, 1, ncclSum))) return rc;
@@ -256,7 +273,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhPtPrep);
     launch_point_prep(d, radius, s);
     mark_end(h);
-    if (!h->comm && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags && !d.n_sitems &&
+    if (!sharded(h) && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags && !d.n_sitems &&
         !d.chol_stepwise) {
       // single rank: Schur assembly and factorisation in one persistent
       // launch (the padding rows are set first; they are no Schur output)
@@ -272,7 +289,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
-    if (h->comm || h->force_pack) {
+    if (sharded(h) || h->force_pack) {
       // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
       launch_pack_upper(d, false, s);
       if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
@@ -322,7 +339,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
   rb.add(kPBadBack, nbP, 1, kBadBack);
   // ... and the Cholesky failure flag (an int) into the slot after the scalars
   launch_reduce_batch(d, rb, true, s);
-  if (h->comm) {
+  if (sharded(h)) {
     if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
   }
@@ -400,6 +417,7 @@ int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_
   if (!h || nranks < 1 || rank < 0 || rank >= nranks) return fail(SFM_EINVAL, "bad communicator arguments");
   HIPCHK(hipSetDevice(h->device));
   if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
+  h->host_fn = nullptr;
   h->nranks = nranks;
   h->rank = rank;
   // a one-rank communicator is created too: it runs every collective of the
@@ -407,6 +425,16 @@ int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
+  return 0;
+}
+
+int sfm_ba_set_host_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_allreduce_fn fn, void* user) {
+  if (!h || nranks < 1 || rank < 0 || rank >= nranks || !fn) return fail(SFM_EINVAL, "bad communicator arguments");
+  if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
+  h->nranks = nranks;
+  h->rank = rank;
+  h->host_fn = fn;
+  h->host_user = user;
   return 0;
 }
 
@@ -614,7 +642,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.Ucam, size_t(kUcam) * C);
   ALLOC(d.S, size_t(d.ld) * d.ld);
   h->force_pack = env_flag("SFM_FORCE_PACK");
-  if (h->comm || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
+  if (sharded(h) || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);
