@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <map>
+#include <atomic>
+#include <thread>
 
 #include <algorithm>
 #include <array>
@@ -164,6 +166,39 @@ int device_cus(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess || prop.multiProcessorCount < 2) return 2;
   return prop.multiProcessorCount;
+}
+
+// SFM_TIMING=1: host phase times of sfm_ba_set_problem on stderr.
+struct HostTimer {
+  bool on = env_flag("SFM_TIMING");
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[set_problem] %-22s %8.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+
+// Dynamic parallel-for over [0, n) on up to 16 host threads (problem setup:
+// the per-camera copies and the Schur pair lists are independent per
+// camera / per row camera and dominated host time at C2-C4).
+template <class F>
+void parallel_for(int n, F f) {
+  const int nth = int(std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
+  if (n < 64 || nth == 1) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<int> next(0);
+  auto body = [&]() {
+    for (int i; (i = next.fetch_add(1)) < n;) f(i);
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < nth; ++k) th.emplace_back(body);
+  body();
+  for (auto& x : th) x.join();
 }
 
 bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
@@ -453,6 +488,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     if (!std::isfinite(obs_uv[2 * i]) || !std::isfinite(obs_uv[2 * i + 1]))
       return fail(SFM_EINVAL, "non-finite observation at " + std::to_string(i));
   }
+  HostTimer timer;
+  timer.mark("validate");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
   free_problem(h);
@@ -474,6 +511,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
       std::stable_sort(b, e, [&](int64_t x, int64_t y) { return cam_idx[x] < cam_idx[y]; });
     }
   }
+  timer.mark("point-major order");
   std::vector<double> uv_s(2 * size_t(N));
   std::vector<int32_t> cam_s(N), pt_s(N);
   for (int64_t q = 0; q < N; ++q) {
@@ -533,12 +571,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     const int v = std::atoi(jw);
     if (v > 0) d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, v));
   }
+  timer.mark("camera-major + chunks");
   // camera-major copies for the Jacobian pass and the record map
   std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1), wcam(size_t(npad / 64) + 1, 0);
   for (int c = 0; c < C; ++c)
     for (int64_t w = cam_rng[2 * c] / 64; w < (cam_rng[2 * c] + (cam_off[c + 1] - cam_off[c]) + 63) / 64; ++w) wcam[w] = c;
   std::vector<double> uv_cm(2 * size_t(npad), 0.0);
-  for (int c = 0; c < C; ++c) {
+  parallel_for(C, [&](int c) {
     const int32_t n_c = cam_off[c + 1] - cam_off[c];
     const int32_t padded = (n_c + 63) / 64 * 64;
     for (int32_t j = 0; j < padded; ++j) {
@@ -552,7 +591,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
         cam_obs_pad[i] = q;
       }
     }
-  }
+  });
   std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
   for (int c = 0; c < C; ++c) {
     const double* k = K9 + 9 * size_t(c);
@@ -563,26 +602,50 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // c1 <= c2, in row-major order, with the CSR list of its (o1, o2) pairs:
   // observations of a common point with cameras c1 and c2 (o2 != o1; on the
   // diagonal only same-camera duplicates), as camera-major record positions. ----
+  timer.mark("camera-major copies");
   std::vector<int32_t> blk, seg, pairs;
   {
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> cols(C);
-    for (int c1 = 0; c1 < C; ++c1) {
-      for (int c2 = c1; c2 < C; ++c2) cols[c2].clear();
+    // two parallel passes over the row cameras c1: pair counts per block,
+    // then the pairs at their CSR offsets, in the order of the sequential
+    // definition (o1 in c1's camera-major order, o2 ascending in its point)
+    std::vector<int64_t> rowstart(size_t(C) + 1, 0);
+    for (int c1 = 0; c1 < C; ++c1) rowstart[c1 + 1] = rowstart[c1] + (C - c1);
+    const int64_t nblk = rowstart[C];
+    std::vector<int32_t> cnt(size_t(nblk) + 1, 0);
+    parallel_for(C, [&](int c1) {
+      int32_t* row = cnt.data() + rowstart[c1] - c1;  // row[c2], c2 >= c1
       for (int32_t i = cam_off[c1]; i < cam_off[c1 + 1]; ++i) {
         const int32_t o1 = cam_obs[i];
         const int p = pt_s[o1];
         for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
-          if (cam_s[o2] >= c1 && o2 != o1) cols[cam_s[o2]].push_back({pos[o1], pos[o2]});
+          if (cam_s[o2] >= c1 && o2 != o1) ++row[cam_s[o2]];
       }
+    });
+    seg.assign(size_t(nblk) + 1, 0);
+    for (int64_t b = 0; b < nblk; ++b) seg[b + 1] = seg[b] + cnt[b];
+    pairs.assign(2 * size_t(seg[nblk]), 0);
+    blk.resize(2 * size_t(nblk));
+    for (int c1 = 0; c1 < C; ++c1)
       for (int c2 = c1; c2 < C; ++c2) {
-        blk.push_back(c1);
-        blk.push_back(c2);
-        seg.push_back(int32_t(pairs.size() / 2));
-        for (auto& pr : cols[c2]) { pairs.push_back(pr.first); pairs.push_back(pr.second); }
+        const int64_t b = rowstart[c1] + (c2 - c1);
+        blk[2 * b] = c1;
+        blk[2 * b + 1] = c2;
       }
-    }
-    seg.push_back(int32_t(pairs.size() / 2));
+    parallel_for(C, [&](int c1) {
+      std::vector<int32_t> cur(seg.begin() + rowstart[c1], seg.begin() + rowstart[c1 + 1]);  // cursor per c2 - c1
+      for (int32_t i = cam_off[c1]; i < cam_off[c1 + 1]; ++i) {
+        const int32_t o1 = cam_obs[i];
+        const int p = pt_s[o1];
+        for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
+          if (cam_s[o2] >= c1 && o2 != o1) {
+            const int32_t k = cur[cam_s[o2] - c1]++;
+            pairs[2 * size_t(k)] = pos[o1];
+            pairs[2 * size_t(k) + 1] = pos[o2];
+          }
+      }
+    });
   }
+  timer.mark("schur pair lists");
   {
     const char* rs = std::getenv("SFM_SCHUR_ROW");
     d.schur_row = rs ? std::atoi(rs) : 1;
@@ -732,6 +795,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars) + 1);  // + the Cholesky failure int (k_reduce_batch)
 #undef ALLOC
+  timer.mark("task tables + alloc");
   release_pool(h);  // what the new problem did not reuse
   if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
     d.scal_host = nullptr;
@@ -784,6 +848,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   h->bs_epoch = 0;
   HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
   HIPCHK(hipStreamSynchronize(s));
+  timer.mark("uploads");
   h->has_problem = true;
   return 0;
 }
