@@ -257,6 +257,15 @@ def main() -> int:
         except (OSError, ValueError):
             pmc = {}
 
+    mfma = {}
+    prof2 = os.path.join(ROOT, "profiles", "pmc_mfma_c3.json")
+    if os.path.exists(prof2) and pmc:
+        try:
+            with open(prof2) as f:
+                mfma = json.load(f).get("kernels", {})
+        except (OSError, ValueError):
+            mfma = {}
+
     def traffic(kernel):
         e = pmc.get(kernel) or {}
         v = e.get("hbm_bytes_per_launch")
@@ -268,7 +277,8 @@ def main() -> int:
     roof_chol = {"kernel": "k_chol_fused (dense reduced-camera Cholesky, one persistent launch, f64 MFMA)", "bound": "mfma",
                  "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                  "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": traffic("k_chol_fused"),
-                 "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4)}
+                 "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4),
+                 "mfma_busy_frac_pmc": (mfma.get("k_chol_fused") or {}).get("mfma_busy_frac")}
     roofline = roof_chol if dominant == "cholesky" else roof_jac
 
     out = {
