@@ -112,8 +112,47 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   bool bad = false;
   for (int b = 0; b < 4; ++b) {
     const int g0 = 16 * b;
-    if (w == 0) {
-      // ---- panel factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
+    if (w == 0 && b > 0) {
+      // ---- panels 1..3: rows r < g0 are above the diagonal (don't-care), so
+      // lanes 0..15 carry W_bb column r in p itself: the elimination applies
+      // the same operations to [A_panel | I] rows (p[j] *= inv, p[c] -= p[j]
+      // L(g0+c, g)), so one FMA stream updates both -- half the pivot work of
+      // the separate wc[] registers.  Their T writes land in the tile's
+      // strictly upper part, which nothing reads.
+      const int r = lane;
+      const bool wl = r < 16;
+      double p[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) p[j] = wl ? ((j == r) ? 1.0 : 0.0) : T[(g0 + j) * TS + r];
+      double d = bcast(p[0], g0);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int g = g0 + j;
+        if (kFull || k0 + g < n) bad |= !(d > 0.0);
+        else d = 1.0;
+        const double inv = rsqrt_nr(d);
+        const double l = p[j] * inv;
+        p[j] = l;
+        T[g * TS + r] = l;
+        if (j < 15) {
+          const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
+          const double l1 = bcast(l, g + 1);
+          p[j + 1] = fma(-l, l1, p[j + 1]);
+          if (j < 14) {
+            double lc[16];
+#pragma unroll
+            for (int c = j + 2; c < 16; ++c) lc[c] = T[g * TS + g0 + c];
+#pragma unroll
+            for (int c = j + 2; c < 16; ++c) p[c] = fma(-l, lc[c], p[c]);
+          }
+          d = dn;
+        }
+      }
+      if (wl)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = p[c];
+    } else if (w == 0) {
+      // ---- panel 0 factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
       const int r = lane;
       double p[16], wc[16];
 #pragma unroll
