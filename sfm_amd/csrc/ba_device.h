@@ -120,6 +120,9 @@ struct DevProblem {
   int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
   int32_t n_srow = 0;
   int2* pairs = nullptr;      // [n_pairs]
+  // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
+  // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
+  double* dpart = nullptr;
   // small problems: pair-chunk items (block, first pair, end pair) with
   // per-block item ranges and partial 6x6 sums (k_schur_split)
   int4* sitems = nullptr;

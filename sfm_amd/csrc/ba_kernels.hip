@@ -442,10 +442,17 @@ __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* 
 // runs are padded to whole wavefronts; padding lanes compute a copy of the
 // camera's last observation, never read): they are staged in LDS and
 // leave as full 1-KB rows with streaming stores, like the Jacobian records.
+// With dpart != nullptr the wave (64 positions of ONE camera: runs are
+// padded to whole wavefronts) also reduces the camera's diagonal-block and
+// rhs terms of the Schur complement, sum F F^T (21) and J_c^T (r - h) (6),
+// over its real observations into dpart[wave][27] (fixed tree order), so
+// k_schur_diag_sum reads 27 doubles per wave instead of every J and M record.
 __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int32_t* __restrict__ cm_p,
                                                        const double* __restrict__ jrec,
                                                        const double* __restrict__ ptL, double* __restrict__ mrec,
-                                                       double* __restrict__ frec) {
+                                                       double* __restrict__ frec,
+                                                       const int32_t* __restrict__ cam_obs,
+                                                       double* __restrict__ dpart) {
   __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kMRec + kFRec)];  // 13 KB per wave
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = (int64_t(blockIdx.x) * kThreads) + 64 * wv;  // first position of this wavefront
@@ -461,6 +468,7 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
   double jc[12];
 #pragma unroll
   for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+  const double2 rr = ld2(J + kRes);
   wave_sync_lds();
   const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
   const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
@@ -470,12 +478,31 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
   st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
   st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
   double* Fo = sf + l * kFRec;
+  double F[kFRec];
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
-    const double f0 = jc[u] * m0 + jc[6 + u] * n0;
-    const double f1 = jc[u] * m1 + jc[6 + u] * n1;
-    const double f2 = jc[u] * m2 + jc[6 + u] * n2;
-    Fo[3 * u] = f0; Fo[3 * u + 1] = f1; Fo[3 * u + 2] = f2;
+    F[3 * u] = jc[u] * m0 + jc[6 + u] * n0;
+    F[3 * u + 1] = jc[u] * m1 + jc[6 + u] * n1;
+    F[3 * u + 2] = jc[u] * m2 + jc[6 + u] * n2;
+    Fo[3 * u] = F[3 * u]; Fo[3 * u + 1] = F[3 * u + 1]; Fo[3 * u + 2] = F[3 * u + 2];
+  }
+  if (dpart) {
+    const bool real = cam_obs[i] >= 0;  // padding positions carry -1
+    const double h0 = m0 * z0 + m1 * z1 + m2 * z2, h1 = n0 * z0 + n1 * z1 + n2 * z2;
+    const double r0 = real ? rr.x - h0 : 0.0, r1 = real ? rr.y - h1 : 0.0;
+    double v[32];
+    int q = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int w = u; w < 6; ++w, ++q)
+        v[q] = real ? F[3 * u] * F[3 * w] + F[3 * u + 1] * F[3 * w + 1] + F[3 * u + 2] * F[3 * w + 2] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) v[21 + u] = jc[u] * r0 + jc[6 + u] * r1;
+#pragma unroll
+    for (int e = 27; e < 32; ++e) v[e] = 0.0;
+    const double tot = wave_sum32(v, l);  // lane l: entry l >> 1
+    if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -657,6 +684,35 @@ __global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restri
                                                          int add_diag, double* __restrict__ S, int ld, int n) {
   __shared__ __attribute__((aligned(16))) double lds[kDiagLds];
   schur_diag_task(blockIdx.x, cam_rng, cam_obs, jrec, mrec, Ucam, diag_c, radius, add_diag, S, ld, n, lds);
+}
+
+// Diagonal blocks and rhs from k_obs_prep's per-wave partials: camera c's
+// waves are positions cam_rng[2c]/64 .. (run end)/64, summed in order.
+//   S_cc += [rank 0] (U_c + D_c^2) - sum F F^T,   S[c][n] = sum J_c^T (r - h)
+__global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict__ cam_rng,
+                                                       const double* __restrict__ dpart,
+                                                       const double* __restrict__ Ucam,
+                                                       const double* __restrict__ diag_c, double radius,
+                                                       int add_diag, double* __restrict__ S, int ld, int n) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+  if (t < 36) {
+    const int u = t / 6, v = t % 6, q = up6(u, v);
+    double tot = 0.0;
+    for (int w = w0; w < w1; ++w) tot += dpart[size_t(w) * 27 + q];
+    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + v;
+    double val = *sp - tot;
+    if (add_diag) {
+      val += Ucam[size_t(kUcam) * c + q];
+      if (u == v) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
+    }
+    *sp = val;
+  } else if (t < 42) {
+    const int u = t - 36;
+    double tot = 0.0;
+    for (int w = w0; w < w1; ++w) tot += dpart[size_t(w) * 27 + 21 + u];
+    S[size_t(6 * c + u) * ld + n] = tot;
+  }
 }
 
 // Packed form of the reduced system for the cross-rank all-reduce: row i
@@ -989,7 +1045,8 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
                                                                          slot(d, kPBad));
   if (d.N_pad)
-    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec);
+    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec,
+                                                                 d.cam_obs, d.dpart);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   if (d.n_blk && d.n_sitems) {
@@ -1001,8 +1058,12 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
     k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
   else if (d.n_blk)
     k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
-  k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
-                                        add_diag ? 1 : 0, d.S, d.ld, d.n);
+  if (d.dpart)
+    k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
+                                        d.n);
+  else
+    k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
+                                          add_diag ? 1 : 0, d.S, d.ld, d.n);
 }
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (d.n == 0) return;

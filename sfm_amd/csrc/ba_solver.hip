@@ -786,6 +786,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     const char* sf = std::getenv("SFM_SCHUR_FUSED");
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
+  {
+    const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
+    if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
+  }
   ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
   ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
   ALLOC(d.spart, 36 * std::max<size_t>(1, sitems.size()));

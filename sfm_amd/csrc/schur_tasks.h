@@ -17,6 +17,27 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
+// Wave sums of 32 values at once by recursive halving (reduce-scatter): at
+// each of the 5 exchange distances 32..2 a lane keeps half of its values and
+// trades the other half with its partner, then the two lanes of a pair add
+// once more.  32 shuffles instead of 32 x 6; lane l returns the sum of
+// value l >> 1 over the wave (fixed order: deterministic).
+// (The halves are picked with bit masks: a select between two array
+// elements becomes a select of addresses and pushes the array to scratch.)
+__device__ __forceinline__ double wave_sum32(double (&v)[32], int l) {
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const uint64_t m = (l & (2 * h)) ? ~0ull : 0ull;  // exchange distance 2h
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+      const uint64_t a = __builtin_bit_cast(uint64_t, v[j]), b = __builtin_bit_cast(uint64_t, v[h + j]);
+      const double keep = __builtin_bit_cast(double, (b & m) | (a & ~m));
+      const double send = __builtin_bit_cast(double, (a & m) | (b & ~m));
+      v[j] = keep + __shfl_xor(send, 2 * h);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ __forceinline__ void st2(double* p, double a, double b) {
   *reinterpret_cast<double2*>(p) = make_double2(a, b);

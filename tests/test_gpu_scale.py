@@ -136,6 +136,9 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
     the fused launch is the experimental SFM_SCHUR_FUSED=1)."""
     s = scene.config(cfg)
     monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
+    # the fused launch sums the diagonal blocks per camera (schur_diag_task);
+    # the two-launch default sums k_obs_prep's per-wave partials instead
+    monkeypatch.setenv("SFM_SCHUR_DIAG_FUSED", "0")
     out = []
     for flag in ("0", "1"):
         monkeypatch.setenv("SFM_SCHUR_FUSED", flag)
@@ -151,6 +154,35 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
     assert c0 == c1 == d0 == d1 and t0 == t1
     for a, b, c in zip(p0, p1, q1):
         assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
+def test_diag_partials_from_obs_prep(monkeypatch, cfg):
+    """The diagonal blocks / rhs summed from k_obs_prep's per-wave partials
+    (default) and re-read per camera by k_schur_diag (SFM_SCHUR_DIAG_FUSED=0)
+    are the same sums in a different order: deterministic, same LM path,
+    same solve to rounding."""
+    s = scene.config(cfg)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_SCHUR_DIAG_FUSED", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+            ba.reset()
+            sm2, _ = ba.solve()
+            p2 = ba.parameters()
+        assert sm.final_cost == sm2.final_cost
+        for a, b in zip(p, p2):
+            assert np.array_equal(a, b)
+        res[flag] = (sm, tr, p)
+    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
+    assert s1.num_iterations == s0.num_iterations
+    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
+    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
+    for a, b in zip(p1, p0):
+        assert _rel(a, b) < 1e-6
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
