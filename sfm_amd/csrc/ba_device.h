@@ -25,6 +25,8 @@ constexpr int kUcam = 28;
 // Per-point record: V (6 packed lower), b_p (3), pad | L (6), z (3), pad.
 constexpr int kPtV = 10;
 constexpr int kPtL = 10;
+// Per-point Schur record (k_schur_pts): X (3), Jacobi scale (3), L (6), 1/l_ii (3), pad: 128 B.
+constexpr int kPtS = 16;
 // Cholesky tile size.
 constexpr int kNB = 64;
 
@@ -120,6 +122,13 @@ struct DevProblem {
   int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
   int32_t n_srow = 0;
   int2* pairs = nullptr;      // [n_pairs]
+  // k_schur_pts (default for large problems): the pair lists as the common
+  // point of each pair, and the per-point records; F is recomputed per pair
+  // from the point and the two wave-uniform cameras instead of gathered
+  int32_t* bpts = nullptr;    // [n_pairs]
+  double* ptS = nullptr;      // [P][kPtS]
+  bool schur_pts = false;
+  int32_t schur_pts_sub = 32;  // lanes per block (32 or 64)
   // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
   // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
   double* dpart = nullptr;

@@ -408,9 +408,14 @@ __global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* _
 
 // Per-iteration point factorisation (depends on the trust-region radius),
 // one lane per point: V_p + D_p^2 = L L^T, z = L^-1 b_p -> ptL.
+// With ptS != nullptr it also writes the point's 128-B Schur record
+// (X 3 | Jacobi scale 3 | L 6 | 1/l_ii 3 | pad) for k_schur_pts.
 __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* __restrict__ ptV,
                                                            const double* __restrict__ diag_p, double radius,
-                                                           double* __restrict__ ptL, double* __restrict__ part_bad) {
+                                                           double* __restrict__ ptL, double* __restrict__ part_bad,
+                                                           const double* __restrict__ X,
+                                                           const double* __restrict__ scale_p,
+                                                           double* __restrict__ ptS) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double bad = 0.0;
@@ -428,6 +433,14 @@ __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* 
     const double z0 = v[6] / l00, z1 = (v[7] - l10 * z0) / l11, z2 = (v[8] - l20 * z0 - l21 * z1) / l22;
     double* L = ptL + size_t(kPtL) * p;
     st2(L, l00, l10); st2(L + 2, l11, l20); st2(L + 4, l21, l22); st2(L + 6, z0, z1); st2(L + 8, z2, 0.0);
+    if (ptS) {
+      double* o = ptS + size_t(kPtS) * p;
+      const double* x = X + 3 * size_t(p);
+      const double* sp = scale_p + 3 * size_t(p);
+      st2(o, x[0], x[1]); st2(o + 2, x[2], sp[0]); st2(o + 4, sp[1], sp[2]);
+      st2(o + 6, l00, l10); st2(o + 8, l11, l20); st2(o + 10, l21, l22);
+      st2(o + 12, 1.0 / l00, 1.0 / l11); st2(o + 14, 1.0 / l22, 0.0);
+    }
   }
   const double r = block_reduce(bad, sh, true);
   if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
@@ -514,11 +527,12 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
     const double2 v = ld2(sm + 2 * (64 * kq + l));
     st2_nt(dm + 2 * (64 * kq + l), v.x, v.y);
   }
+  if (frec)  // (k_schur_pts recomputes F from the point records instead)
 #pragma unroll
-  for (int kq = 0; kq < kFRec / 2; ++kq) {
-    const double2 v = ld2(sf + 2 * (64 * kq + l));
-    st2_nt(df + 2 * (64 * kq + l), v.x, v.y);
-  }
+    for (int kq = 0; kq < kFRec / 2; ++kq) {
+      const double2 v = ld2(sf + 2 * (64 * kq + l));
+      st2_nt(df + 2 * (64 * kq + l), v.x, v.y);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -669,6 +683,154 @@ __global__ __launch_bounds__(kThreads) void k_schur_row(const int4* __restrict__
                                                         const int2* __restrict__ blk, double* __restrict__ S, int ld) {
   __shared__ __attribute__((aligned(16))) double F1[kRowChunkLds];
   schur_row_task(work[blockIdx.x], seg, pairs, frec, cam_rng, blk, S, ld, F1);
+}
+
+// ---------------------------------------------------------------------------
+// k_schur_pts: the off-diagonal Schur blocks WITHOUT the F gathers.  A pair
+// (o1, o2) of block (c1, c2) shares its point p, and
+//   F_o1 F_o2^T = J_c1^T M_1 M_2^T J_c2,   M_i = J_X,i L_p^-T,
+// where J_X,i and J_c,i are functions of (camera c_i, X_p) alone.  So kSub
+// lanes own one block: the two cameras' constants (R, dR/dw, t, K, Jacobi
+// scale: 50 doubles each) sit in LDS as wave-uniform broadcasts, and each
+// lane takes one pair per step, gathering only its point's 128-B record
+// (X, scale, L_p, 1/l_ii: one line, 25.6 MB in all at C3, so L2/MALL
+// resident) and recomputing both scaled Jacobians with the Jacobian pass's
+// own arithmetic (jac_record).  The k_schur_row formulation gathers a fresh
+// 144-B F record per pair from a 293-MB array (~2.9 GB of HBM traffic per
+// launch at C3); this one trades that for ~400 fp64 ops per pair.  The
+// block's lanes end with a fixed-order recursive-halving reduction, so S is
+// bitwise reproducible run to run.  (Same sums as k_schur_row to rounding:
+// M uses the reciprocals 1/l_ii and F is re-associated as J^T (M M^T) J.)
+constexpr int kCamS = 50;  // R 9 | dR/dw 27 | t 3 | K 5 | scale 6
+
+__device__ __forceinline__ void stage_cam(double* cs, int c, const double* __restrict__ camR,
+                                          const double* __restrict__ cam, const double* __restrict__ Kc,
+                                          const double* __restrict__ scale_c, int l) {
+  if (l < 36) cs[l] = camR[size_t(kCamR) * c + l];
+  else if (l < 39) cs[l] = cam[6 * size_t(c) + 3 + (l - 36)];
+  else if (l < 44) cs[l] = Kc[5 * size_t(c) + (l - 39)];
+  else if (l < 50) cs[l] = scale_c[6 * size_t(c) + (l - 44)];
+}
+
+// One side of a pair: scaled J_c (2x6) and M = J_X L^-T (2x3, rows m | n).
+__device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], const double sp[3], const double Lp[9],
+                                          double M[6], double jc[12]) {
+  double rec[kJRec];
+  jac_record(cs, cs[36], cs[37], cs[38], cs[39], cs[40], cs[41], cs[42], cs[43], cs + 44, sp, Xp,
+             make_double2(0.0, 0.0), rec);
+#pragma unroll
+  for (int k = 0; k < 12; ++k) jc[k] = rec[kJC + k];
+  const double *e = rec + kJX, l10 = Lp[1], l20 = Lp[3], l21 = Lp[4], i00 = Lp[6], i11 = Lp[7], i22 = Lp[8];
+  M[0] = e[0] * i00; M[1] = (e[1] - l10 * M[0]) * i11; M[2] = (e[2] - l20 * M[0] - l21 * M[1]) * i22;
+  M[3] = e[3] * i00; M[4] = (e[4] - l10 * M[3]) * i11; M[5] = (e[5] - l20 * M[3] - l21 * M[4]) * i22;
+}
+
+// Sums of 32 values over the kSub lanes of a segment by recursive halving
+// (see wave_sum32): lane l returns the sum of value (l & 31) (kSub = 32) or
+// (l >> 1) (kSub = 64).
+template <int kSub>
+__device__ __forceinline__ double seg_sum32(double (&v)[32], int l) {
+  if (kSub == 64) return wave_sum32(v, l);
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const uint64_t m = (l & h) ? ~0ull : 0ull;
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+      const uint64_t a = __builtin_bit_cast(uint64_t, v[j]), b = __builtin_bit_cast(uint64_t, v[h + j]);
+      const double keep = __builtin_bit_cast(double, (b & m) | (a & ~m));
+      const double send = __builtin_bit_cast(double, (a & m) | (b & ~m));
+      v[j] = keep + __shfl_xor(send, h);
+    }
+  }
+  return v[0];
+}
+template <int kSub>
+__device__ __forceinline__ double seg_sum(double v) {
+#pragma unroll
+  for (int off = kSub / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+template <int kSub>
+__global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int2* __restrict__ blk,
+                                                        const int32_t* __restrict__ seg,
+                                                        const int32_t* __restrict__ bpts,
+                                                        const double* __restrict__ ptS,
+                                                        const double* __restrict__ camR,
+                                                        const double* __restrict__ cam, const double* __restrict__ Kc,
+                                                        const double* __restrict__ scale_c, double* __restrict__ S,
+                                                        int ld) {
+  constexpr int kPer = 64 / kSub;  // blocks per wave
+  __shared__ double cst[kThreads / 64][kPer][2 * kCamS];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
+  const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
+  if (wb >= n_blk) return;  // wave-uniform
+  const int64_t b = min(wb + g, n_blk - 1);
+  const bool own = wb + g < n_blk;
+  const int2 cc = blk[b];
+  double* cs1 = cst[wv][g];
+  double* cs2 = cs1 + kCamS;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int2 cq = blk[min(wb + q, n_blk - 1)];
+    stage_cam(cst[wv][q], cq.x, camR, cam, Kc, scale_c, l);
+    stage_cam(cst[wv][q] + kCamS, cq.y, camR, cam, Kc, scale_c, l);
+  }
+  wave_lds_sync();
+  const int kb = seg[b], ke = own ? seg[b + 1] : kb;
+  double acc[36];
+#pragma unroll
+  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
+  // the segments of a wave run as many steps as the longest list
+  int len = ke - kb;
+#pragma unroll
+  for (int off = kSub; off < 64; off <<= 1) len = max(len, __shfl_xor(len, off));
+  for (int k0 = 0; k0 < len; k0 += kSub) {
+    // the camera constants are re-read from LDS each step (hoisted, they
+    // would hold 200 VGPRs)
+    asm volatile("" ::: "memory");
+    const int k = kb + k0 + sl;
+    const bool valid = k < ke;
+    const int p = valid ? bpts[k] : 0;
+    const double* r = ptS + size_t(kPtS) * p;
+    double q[16];
+#pragma unroll
+    for (int f = 0; f < 16; f += 2) {
+      const double2 x = ld2(r + f);
+      q[f] = x.x; q[f + 1] = x.y;
+    }
+    const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
+    const double Lp[9] = {q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14]};
+    double M1[6], J1[12], M2[6], J2[12];
+    pair_side(cs1, Xp, sp, Lp, M1, J1);
+    pair_side(cs2, Xp, sp, Lp, M2, J2);
+    const double w = valid ? 1.0 : 0.0;
+    const double g00 = (M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2]) * w;
+    const double g01 = (M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5]) * w;
+    const double g10 = (M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2]) * w;
+    const double g11 = (M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5]) * w;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const double h0 = J1[u] * g00 + J1[6 + u] * g10, h1 = J1[u] * g01 + J1[6 + u] * g11;
+#pragma unroll
+      for (int v = 0; v < 6; ++v) acc[6 * u + v] += h0 * J2[v] + h1 * J2[6 + v];
+    }
+  }
+  double v32[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v32[e] = acc[e];
+  const double t = seg_sum32<kSub>(v32, l);
+  const double t32 = seg_sum<kSub>(acc[32]), t33 = seg_sum<kSub>(acc[33]), t34 = seg_sum<kSub>(acc[34]),
+               t35 = seg_sum<kSub>(acc[35]);
+  if (!own) return;
+  double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
+  const int e = kSub == 64 ? (sl >> 1) : sl;
+  if (kSub == 32 || !(sl & 1)) Sb[size_t(e / 6) * ld + e % 6] = -t;
+  if (sl < 4) {
+    const double x = sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35;
+    const int e2 = 32 + sl;
+    Sb[size_t(e2 / 6) * ld + e2 % 6] = -x;
+  }
 }
 
 // Diagonal blocks and right-hand side, one workgroup per camera c (after
@@ -1039,14 +1201,16 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad));
+                                                                         slot(d, kPBad), d.X, d.scale_p, nullptr);
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad));
+                                                                         slot(d, kPBad), d.X, d.scale_p,
+                                                                         d.schur_pts ? d.ptS : nullptr);
   if (d.N_pad)
-    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec, d.frec,
-                                                                 d.cam_obs, d.dpart);
+    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec,
+                                                                 d.schur_pts ? nullptr : d.frec, d.cam_obs,
+                                                                 d.dpart);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   if (d.n_blk && d.n_sitems) {
@@ -1054,6 +1218,13 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
                                                                          d.spart);
     k_schur_split_reduce<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.sboff, d.spart, d.S,
                                                                             d.ld);
+  } else if (d.n_blk && d.schur_pts) {
+    if (d.schur_pts_sub == 32)
+      k_schur_pts<32><<<int((d.n_blk + 7) / 8), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam,
+                                                                 d.Kc, d.scale_c, d.S, d.ld);
+    else
+      k_schur_pts<64><<<int((d.n_blk + 3) / 4), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam,
+                                                                 d.Kc, d.scale_c, d.S, d.ld);
   } else if (d.n_blk && d.schur_row && d.n_srow)
     k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
   else if (d.n_blk)

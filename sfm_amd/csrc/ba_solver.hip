@@ -603,7 +603,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // observations of a common point with cameras c1 and c2 (o2 != o1; on the
   // diagonal only same-camera duplicates), as camera-major record positions. ----
   timer.mark("camera-major copies");
-  std::vector<int32_t> blk, seg, pairs;
+  std::vector<int32_t> blk, seg, pairs, bpts;
   {
     // two parallel passes over the row cameras c1: pair counts per block,
     // then the pairs at their CSR offsets, in the order of the sequential
@@ -624,6 +624,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     seg.assign(size_t(nblk) + 1, 0);
     for (int64_t b = 0; b < nblk; ++b) seg[b + 1] = seg[b] + cnt[b];
     pairs.assign(2 * size_t(seg[nblk]), 0);
+    bpts.assign(size_t(seg[nblk]), 0);
     blk.resize(2 * size_t(nblk));
     for (int c1 = 0; c1 < C; ++c1)
       for (int c2 = c1; c2 < C; ++c2) {
@@ -641,6 +642,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
             const int32_t k = cur[cam_s[o2] - c1]++;
             pairs[2 * size_t(k)] = pos[o1];
             pairs[2 * size_t(k) + 1] = pos[o2];
+            bpts[size_t(k)] = p;
           }
       }
     });
@@ -787,6 +789,17 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
   {
+    // k_schur_pts (recomputed F, point-record gathers) wherever the row /
+    // thread-per-block kernels would run; SFM_SCHUR_PTS=0 restores those
+    const char* sp = std::getenv("SFM_SCHUR_PTS");
+    d.schur_pts = (sp ? std::atoi(sp) != 0 : true) && d.n_blk > 0 && sitems.empty() && !d.schur_fused;
+    if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) d.schur_pts_sub = std::atoi(ss) == 64 ? 64 : 32;
+    if (d.schur_pts) {
+      ALLOC(d.bpts, std::max<size_t>(1, bpts.size()));
+      ALLOC(d.ptS, size_t(kPtS) * std::max(1, P));
+    }
+  }
+  {
     const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
     if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
   }
@@ -834,6 +847,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   if (d.n_pairs)
     HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
   H2D(d.seg, seg.data(), seg.size());
+  if (d.schur_pts && !bpts.empty()) H2D(d.bpts, bpts.data(), bpts.size());
   if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
   if (!stasks.empty()) H2D(d.stasks, stasks.data(), stasks.size());
   if (!sitems.empty()) H2D(d.sitems, sitems.data(), sitems.size());

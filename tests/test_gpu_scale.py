@@ -139,6 +139,7 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
     # the fused launch sums the diagonal blocks per camera (schur_diag_task);
     # the two-launch default sums k_obs_prep's per-wave partials instead
     monkeypatch.setenv("SFM_SCHUR_DIAG_FUSED", "0")
+    monkeypatch.setenv("SFM_SCHUR_PTS", "0")  # the fused launch gathers F records
     out = []
     for flag in ("0", "1"):
         monkeypatch.setenv("SFM_SCHUR_FUSED", flag)
@@ -192,6 +193,7 @@ def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
     small-problem split path, which sums pair chunks, is switched off)."""
     s = scene.config(cfg)
     monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
+    monkeypatch.setenv("SFM_SCHUR_PTS", "0")
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("SFM_SCHUR_ROW", flag)
@@ -202,6 +204,37 @@ def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
     assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
     for a, b in zip(out[0][2], out[1][2]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg,sub", [("C1", "32"), ("C2", "32"), ("C2", "64"), ("C3", "32")])
+def test_recomputed_schur_matches_gathered(monkeypatch, cfg, sub):
+    """k_schur_pts (F recomputed per pair from the point record and the two
+    cameras; the default once the split path is off) against k_schur_row
+    (gathered F records): deterministic, same LM path, same solve to
+    rounding."""
+    s = scene.config(cfg)
+    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
+    monkeypatch.setenv("SFM_SCHUR_PTS_SUB", sub)
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_SCHUR_PTS", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+            ba.reset()
+            sm2, _ = ba.solve()
+            p2 = ba.parameters()
+        assert sm.final_cost == sm2.final_cost
+        for a, b in zip(p, p2):
+            assert np.array_equal(a, b)
+        res[flag] = (sm, tr, p)
+    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
+    assert s1.num_iterations == s0.num_iterations
+    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
+    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
+    for a, b in zip(p1, p0):
+        assert _rel(a, b) < 1e-6
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
@@ -255,7 +288,13 @@ def _append_obs(s, cam, pt, uv):
     s.pt_idx = np.concatenate([s.pt_idx, np.asarray(pt, dtype=np.int32)])
 
 
-def test_edge_cases_duplicate_camera_empty_camera_single_view():
+@pytest.mark.parametrize("schur", ["split", "pts", "row"])
+def test_edge_cases_duplicate_camera_empty_camera_single_view(monkeypatch, schur):
+    # every Schur formulation (the small-problem split, the recomputed-F
+    # blocks, the gathered-F rows) meets the same edge cases
+    if schur != "split":
+        monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
+        monkeypatch.setenv("SFM_SCHUR_PTS", "1" if schur == "pts" else "0")
     s = scene.generate(12, 400, views=4, seed=11)
     # point 3 seen a second time by one of its cameras (two residual blocks,
     # same parameter blocks): the Schur diagonal gets the cross term
