@@ -128,7 +128,7 @@ struct DevProblem {
   int32_t* bpts = nullptr;    // [n_pairs]
   double* ptS = nullptr;      // [P][kPtS]
   bool schur_pts = false;
-  int32_t schur_pts_sub = 32;  // lanes per block (32 or 64)
+  int32_t schur_pts_sub = 8;   // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
   // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
   // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
   double* dpart = nullptr;

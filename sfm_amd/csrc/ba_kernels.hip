@@ -715,34 +715,58 @@ __device__ __forceinline__ void stage_cam(double* cs, int c, const double* __res
 // One side of a pair: scaled J_c (2x6) and M = J_X L^-T (2x3, rows m | n).
 __device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], const double sp[3], const double Lp[9],
                                           double M[6], double jc[12]) {
-  double rec[kJRec];
-  jac_record(cs, cs[36], cs[37], cs[38], cs[39], cs[40], cs[41], cs[42], cs[43], cs + 44, sp, Xp,
-             make_double2(0.0, 0.0), rec);
+  // jac_record's Jacobian columns, with one reciprocal for the projection
+  // (1/z) instead of three divisions
+  const double* cr = cs;
+  const double fx = cs[39], sk = cs[40], fy = cs[42];
+  const double* sc = cs + 44;
+  const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + cs[36];
+  const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + cs[37];
+  const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + cs[38];
+  const double iz = 1.0 / pc2, xp = pc0 * iz, yp = pc1 * iz;
+  const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+  const double b1 = fy * iz, b2 = -fy * yp * iz;
+  double e[6];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) jc[k] = rec[kJC + k];
-  const double *e = rec + kJX, l10 = Lp[1], l20 = Lp[3], l21 = Lp[4], i00 = Lp[6], i11 = Lp[7], i22 = Lp[8];
+  for (int j = 0; j < 3; ++j) {
+    e[j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
+    e[3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
+  }
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const double* D = cr + 9 + 9 * kk;
+    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+    jc[kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
+    jc[6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
+  }
+  jc[3] = a0 * sc[3]; jc[4] = a1 * sc[4]; jc[5] = a2 * sc[5];
+  jc[9] = 0.0;        jc[10] = b1 * sc[4]; jc[11] = b2 * sc[5];
+  const double l10 = Lp[1], l20 = Lp[3], l21 = Lp[4], i00 = Lp[6], i11 = Lp[7], i22 = Lp[8];
   M[0] = e[0] * i00; M[1] = (e[1] - l10 * M[0]) * i11; M[2] = (e[2] - l20 * M[0] - l21 * M[1]) * i22;
   M[3] = e[3] * i00; M[4] = (e[4] - l10 * M[3]) * i11; M[5] = (e[5] - l20 * M[3] - l21 * M[4]) * i22;
 }
 
 // Sums of 32 values over the kSub lanes of a segment by recursive halving
-// (see wave_sum32): lane l returns the sum of value (l & 31) (kSub = 32) or
-// (l >> 1) (kSub = 64).
+// (see wave_sum32): afterwards lane l holds in v[0 .. kR) the sums of values
+// kR * (l % kSub) + r (kSub <= 32, kR = 32 / kSub), or of value l >> 1
+// (kSub = 64, kR = 1).
 template <int kSub>
-__device__ __forceinline__ double seg_sum32(double (&v)[32], int l) {
-  if (kSub == 64) return wave_sum32(v, l);
+__device__ __forceinline__ void seg_reduce32(double (&v)[32], int l) {
 #pragma unroll
-  for (int h = 16; h >= 1; h >>= 1) {
-    const uint64_t m = (l & h) ? ~0ull : 0ull;
+  for (int d = (kSub >= 64 ? 32 : kSub / 2), n = 32; d >= 1 && n > 1; d >>= 1, n >>= 1) {
+    const int h = n / 2;
+    const uint64_t m = (l & d) ? ~0ull : 0ull;
 #pragma unroll
     for (int j = 0; j < h; ++j) {
       const uint64_t a = __builtin_bit_cast(uint64_t, v[j]), b = __builtin_bit_cast(uint64_t, v[h + j]);
       const double keep = __builtin_bit_cast(double, (b & m) | (a & ~m));
       const double send = __builtin_bit_cast(double, (a & m) | (b & ~m));
-      v[j] = keep + __shfl_xor(send, h);
+      v[j] = keep + __shfl_xor(send, d);
     }
   }
-  return v[0];
+  if (kSub == 64) v[0] += __shfl_xor(v[0], 1);
 }
 template <int kSub>
 __device__ __forceinline__ double seg_sum(double v) {
@@ -761,7 +785,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int ld) {
   constexpr int kPer = 64 / kSub;  // blocks per wave
-  __shared__ double cst[kThreads / 64][kPer][2 * kCamS];
+  __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
   const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
   if (wb >= n_blk) return;  // wave-uniform
@@ -819,13 +843,22 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
   double v32[32];
 #pragma unroll
   for (int e = 0; e < 32; ++e) v32[e] = acc[e];
-  const double t = seg_sum32<kSub>(v32, l);
+  seg_reduce32<kSub>(v32, l);
   const double t32 = seg_sum<kSub>(acc[32]), t33 = seg_sum<kSub>(acc[33]), t34 = seg_sum<kSub>(acc[34]),
                t35 = seg_sum<kSub>(acc[35]);
   if (!own) return;
   double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
-  const int e = kSub == 64 ? (sl >> 1) : sl;
-  if (kSub == 32 || !(sl & 1)) Sb[size_t(e / 6) * ld + e % 6] = -t;
+  constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
+  if (kSub == 64) {
+    const int e = sl >> 1;
+    if (!(sl & 1)) Sb[size_t(e / 6) * ld + e % 6] = -v32[0];
+  } else {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int e = kR * sl + r;
+      Sb[size_t(e / 6) * ld + e % 6] = -v32[r];
+    }
+  }
   if (sl < 4) {
     const double x = sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35;
     const int e2 = 32 + sl;
@@ -1219,12 +1252,16 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
     k_schur_split_reduce<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.sboff, d.spart, d.S,
                                                                             d.ld);
   } else if (d.n_blk && d.schur_pts) {
-    if (d.schur_pts_sub == 32)
-      k_schur_pts<32><<<int((d.n_blk + 7) / 8), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam,
-                                                                 d.Kc, d.scale_c, d.S, d.ld);
-    else
-      k_schur_pts<64><<<int((d.n_blk + 3) / 4), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam,
-                                                                 d.Kc, d.scale_c, d.S, d.ld);
+    const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
+    const int nb = int((d.n_blk + per - 1) / per);
+#define SFM_PTS(S_)                                                                                     \
+  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
+                                             d.S, d.ld)
+    if (sub == 8) SFM_PTS(8);
+    else if (sub == 16) SFM_PTS(16);
+    else if (sub == 32) SFM_PTS(32);
+    else SFM_PTS(64);
+#undef SFM_PTS
   } else if (d.n_blk && d.schur_row && d.n_srow)
     k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
   else if (d.n_blk)

@@ -793,7 +793,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     // thread-per-block kernels would run; SFM_SCHUR_PTS=0 restores those
     const char* sp = std::getenv("SFM_SCHUR_PTS");
     d.schur_pts = (sp ? std::atoi(sp) != 0 : true) && d.n_blk > 0 && sitems.empty() && !d.schur_fused;
-    if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) d.schur_pts_sub = std::atoi(ss) == 64 ? 64 : 32;
+    if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
+      const int v = std::atoi(ss);
+      d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
+    }
     if (d.schur_pts) {
       ALLOC(d.bpts, std::max<size_t>(1, bpts.size()));
       ALLOC(d.ptS, size_t(kPtS) * std::max(1, P));

@@ -206,7 +206,7 @@ def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("cfg,sub", [("C1", "32"), ("C2", "32"), ("C2", "64"), ("C3", "32")])
+@pytest.mark.parametrize("cfg,sub", [("C1", "8"), ("C2", "16"), ("C2", "64"), ("C3", "8")])
 def test_recomputed_schur_matches_gathered(monkeypatch, cfg, sub):
     """k_schur_pts (F recomputed per pair from the point record and the two
     cameras; the default once the split path is off) against k_schur_row
