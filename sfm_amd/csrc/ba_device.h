@@ -128,6 +128,12 @@ struct DevProblem {
   int32_t* bpts = nullptr;    // [n_pairs]
   double* ptS = nullptr;      // [P][kPtS]
   bool schur_pts = false;
+  // concurrent Schur + Cholesky (single rank, pts mode): [nblk] monotone
+  // per-tile-column counts of finished k_schur_pts workgroups | [nblk]
+  // workgroups per column and launch
+  int32_t* pcnt = nullptr;
+  bool schur_overlap = false;
+  int32_t chol_helpers = 0;    // SFM_CHOL_HELPERS: cap on the Cholesky helper workgroups (0: CU count - 1)
   int32_t schur_pts_sub = 8;   // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
   // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
   // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
@@ -184,7 +190,12 @@ void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fa
 int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
+// sepoch > 0: gated on the concurrent k_schur_pts launch of that epoch (pcnt)
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true, int sepoch = 0);
+// k_schur_pts only (publishing per-column counts when sepoch > 0), after
+// launch_schur_diag_first: the overlapped Schur of the single-rank pts mode
+void launch_schur_diag_first(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
+void launch_schur_pts(const DevProblem& d, int sepoch, hipStream_t s);
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
 // Schur (row segments + diagonal/rhs) and Cholesky in ONE persistent launch
 // (single rank; the multi-rank path all-reduces S in between instead).

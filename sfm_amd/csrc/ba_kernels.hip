@@ -783,12 +783,13 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
                                                         const double* __restrict__ camR,
                                                         const double* __restrict__ cam, const double* __restrict__ Kc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
-                                                        int ld) {
+                                                        int ld, int diag_add, int* __restrict__ colcnt) {
   constexpr int kPer = 64 / kSub;  // blocks per wave
   __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
   const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
-  if (wb >= n_blk) return;  // wave-uniform
+  // (no early exit: a wave past the end runs empty lists, so every wave
+  // reaches the publishing barrier)
   const int64_t b = min(wb + g, n_blk - 1);
   const bool own = wb + g < n_blk;
   const int2 cc = blk[b];
@@ -846,23 +847,40 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
   seg_reduce32<kSub>(v32, l);
   const double t32 = seg_sum<kSub>(acc[32]), t33 = seg_sum<kSub>(acc[33]), t34 = seg_sum<kSub>(acc[34]),
                t35 = seg_sum<kSub>(acc[35]);
-  if (!own) return;
-  double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
-  constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
-  if (kSub == 64) {
-    const int e = sl >> 1;
-    if (!(sl & 1)) Sb[size_t(e / 6) * ld + e % 6] = -v32[0];
-  } else {
+  if (own) {
+    // a diagonal block (same-camera duplicate pairs only) is added to what
+    // k_schur_diag_sum wrote before this launch (diag_add), else stored
+    double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
+    const bool add = diag_add && cc.x == cc.y;
+    auto put = [&](int e, double v) {
+      double* q = Sb + size_t(e / 6) * ld + e % 6;
+      *q = add ? *q - v : -v;
+    };
+    constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
+    if (kSub == 64) {
+      if (!(sl & 1)) put(sl >> 1, v32[0]);
+    } else {
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      const int e = kR * sl + r;
-      Sb[size_t(e / 6) * ld + e % 6] = -v32[r];
+      for (int r = 0; r < kR; ++r) put(kR * sl + r, v32[r]);
     }
+    if (sl < 4) put(32 + sl, sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35);
   }
-  if (sl < 4) {
-    const double x = sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35;
-    const int e2 = 32 + sl;
-    Sb[size_t(e2 / 6) * ld + e2 % 6] = -x;
+  if (colcnt) {
+    // publish (guide form: every wave drains its stores, one agent release,
+    // relaxed counter adds): one count to each tile column whose S rows
+    // this workgroup's blocks wrote (their row cameras c1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) {
+        const int64_t b0 = int64_t(blockIdx.x) * (kThreads / 64) * kPer;
+        const int64_t b1 = min(b0 + (kThreads / 64) * kPer, n_blk) - 1;
+        const int j0 = (6 * blk[b0].x) / kNB, j1 = (6 * blk[b1].x + 5) / kNB;
+        for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(colcnt + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -888,25 +906,37 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        const double* __restrict__ dpart,
                                                        const double* __restrict__ Ucam,
                                                        const double* __restrict__ diag_c, double radius,
-                                                       int add_diag, double* __restrict__ S, int ld, int n) {
+                                                       int add_diag, double* __restrict__ S, int ld, int n,
+                                                       int init) {
   const int c = blockIdx.x, t = threadIdx.x;
   const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+  // lane t sums waves w0 + t, w0 + t + 64, ... (coalesced 216-B rows), then
+  // one reduce-scatter over the wave: lane 2e ends with entry e
+  double v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v[e] = 0.0;
+  for (int w = w0 + t; w < w1; w += 64) {
+    const double* src = dpart + size_t(w) * 27;
+#pragma unroll
+    for (int e = 0; e < 27; ++e) v[e] += src[e];
+  }
+  const double sum = wave_sum32(v, t);
+  // every lane takes part in the shuffle (a source lane must be active):
+  // lanes < 36 fetch their S_cc entry, lanes 36..41 the rhs entries
+  const int tu = t < 36 ? t / 6 : 0, tv = t < 36 ? t % 6 : 0;
+  const int src = t < 36 ? up6(tu, tv) : (t < 42 ? 21 + (t - 36) : 0);
+  const double tot = __shfl(sum, 2 * src);
   if (t < 36) {
-    const int u = t / 6, v = t % 6, q = up6(u, v);
-    double tot = 0.0;
-    for (int w = w0; w < w1; ++w) tot += dpart[size_t(w) * 27 + q];
-    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + v;
-    double val = *sp - tot;
+    const int u = tu, vv = tv, q = src;
+    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + vv;
+    double val = (init ? 0.0 : *sp) - tot;  // init: before the off-diagonal launch (k_schur_pts adds its part)
     if (add_diag) {
       val += Ucam[size_t(kUcam) * c + q];
-      if (u == v) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
+      if (u == vv) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
     }
     *sp = val;
   } else if (t < 42) {
-    const int u = t - 36;
-    double tot = 0.0;
-    for (int w = w0; w < w1; ++w) tot += dpart[size_t(w) * 27 + 21 + u];
-    S[size_t(6 * c + u) * ld + n] = tot;
+    S[size_t(6 * c + (t - 36)) * ld + n] = tot;
   }
 }
 
@@ -1252,26 +1282,42 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
     k_schur_split_reduce<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.sboff, d.spart, d.S,
                                                                             d.ld);
   } else if (d.n_blk && d.schur_pts) {
-    const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
-    const int nb = int((d.n_blk + per - 1) / per);
-#define SFM_PTS(S_)                                                                                     \
-  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                             d.S, d.ld)
-    if (sub == 8) SFM_PTS(8);
-    else if (sub == 16) SFM_PTS(16);
-    else if (sub == 32) SFM_PTS(32);
-    else SFM_PTS(64);
-#undef SFM_PTS
+    if (d.dpart) {
+      launch_schur_diag_first(d, radius, add_diag, s);
+      launch_schur_pts(d, 0, s);
+      return;
+    }
+    launch_schur_pts(d, 0, s);
   } else if (d.n_blk && d.schur_row && d.n_srow)
     k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
   else if (d.n_blk)
     k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
   if (d.dpart)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
-                                        d.n);
+                                        d.n, 0);
   else
     k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
                                           add_diag ? 1 : 0, d.S, d.ld, d.n);
+}
+void launch_schur_diag_first(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
+  if (d.C)
+    k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
+                                        d.n, 1);
+}
+void launch_schur_pts(const DevProblem& d, int sepoch, hipStream_t s) {
+  if (!d.n_blk) return;
+  const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
+  const int nb = int((d.n_blk + per - 1) / per);
+  const int diag_add = d.dpart ? 1 : 0;
+  int* cnt = sepoch > 0 ? d.pcnt : nullptr;
+#define SFM_PTS(S_)                                                                                           \
+  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
+                                          d.S, d.ld, diag_add, cnt)
+  if (sub == 8) SFM_PTS(8);
+  else if (sub == 16) SFM_PTS(16);
+  else if (sub == 32) SFM_PTS(32);
+  else SFM_PTS(64);
+#undef SFM_PTS
 }
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (d.n == 0) return;

@@ -64,6 +64,11 @@ struct sfm_ba_handle {
   int32_t schur_epoch = 0;       // launches of the fused Schur + Cholesky since the last set_problem
   int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem          // stamp of the last back-substitution launch (k_backsolve flags)
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
+  // concurrent Schur + Cholesky: the Cholesky runs on stream2, ordered by
+  // two events (created with the first overlapped step)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int32_t pts_epoch = 0;         // overlapped k_schur_pts launches since the last set_problem
   std::vector<std::pair<size_t, void*>> allocs;  // (bytes, buffer) of the resident problem
   std::multimap<size_t, void*> pool;             // buffers of the previous problem, reused by size
   bool has_problem = false;
@@ -321,6 +326,34 @@ int compute_step(sfm_ba_handle* h, double radius) {
       mark_end(h);
       goto factored;
     }
+    if (!sharded(h) && !h->force_pack && d.schur_overlap && d.cflags && !d.chol_stepwise) {
+      // single rank: the Cholesky runs CONCURRENTLY with the off-diagonal
+      // Schur blocks, its helpers gated per tile column on k_schur_pts'
+      // counts (rows are assembled in camera order, so the first columns
+      // are ready within a few percent of the Schur pass)
+      if (!h->stream2) {
+        HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+      }
+      launch_pad_init(d, s);  // also clears the failure flag
+      mark_begin(h, kPhSchur);
+      launch_schur_diag_first(d, radius, true, s);
+      mark_end(h);
+      mark_begin(h, kPhChol);
+      HIPCHK(hipEventRecord(h->ev_fork, s));
+      HIPCHK(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+      const int sep = ++h->pts_epoch;
+      launch_cholesky(d, ++h->chol_epoch, h->stream2, false, sep);
+      launch_schur_pts(d, sep, s);
+      HIPCHK(hipEventRecord(h->ev_join, h->stream2));
+      HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
+      mark_end(h);
+      mark_begin(h, kPhBack);
+      launch_backsolve(d, ++h->bs_epoch, s);
+      mark_end(h);
+      goto factored;
+    }
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
@@ -435,6 +468,12 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->d.scal_host) hipHostFree(h->d.scal_host);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
+  if (h->stream2) {
+    hipStreamSynchronize(h->stream2);
+    hipStreamDestroy(h->stream2);
+  }
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
   hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -744,7 +783,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n_sitems = int32_t(sitems.size());
   // fused Schur + Cholesky task table (k_chol_schur_fused, chol_kernels.hip)
   std::vector<int4> stasks;
-  std::vector<int32_t> scnt_init;
+  std::vector<int32_t> scnt_init, pcnt_init;
   {
     const int nb = d.nblk;
     std::vector<int32_t> target(nb, 0);
@@ -789,6 +828,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
   {
+    const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
+    if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
+  }
+  {
     // k_schur_pts (recomputed F, point-record gathers) wherever the row /
     // thread-per-block kernels would run; SFM_SCHUR_PTS=0 restores those
     const char* sp = std::getenv("SFM_SCHUR_PTS");
@@ -800,11 +843,24 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     if (d.schur_pts) {
       ALLOC(d.bpts, std::max<size_t>(1, bpts.size()));
       ALLOC(d.ptS, size_t(kPtS) * std::max(1, P));
+      // k_schur_pts workgroups per tile column (the columns of their blocks'
+      // row cameras), for the Cholesky launched concurrently
+      const int64_t per = int64_t(64 / d.schur_pts_sub) * 4;
+      pcnt_init.assign(2 * size_t(d.nblk), 0);
+      for (int64_t b0 = 0; b0 < d.n_blk; b0 += per) {
+        const int64_t b1 = std::min(b0 + per, d.n_blk) - 1;
+        const int j0 = (6 * blk[2 * b0]) / kNB, j1 = (6 * blk[2 * b1] + 5) / kNB;
+        for (int j = j0; j <= j1; ++j) ++pcnt_init[size_t(d.nblk) + j];
+      }
+      ALLOC(d.pcnt, pcnt_init.size());
     }
-  }
-  {
-    const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
-    if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
+    // experimental, off by default: measured slower at C3 (3.90 ms per solve
+    // for the overlapped pair vs 1.07 + 2.62 ms serial; the Cholesky alone
+    // is as fast with 127 helpers as with 255, so the loss is the walker's
+    // chain slowed by the concurrent Schur traffic and the late columns)
+    const char* so = std::getenv("SFM_SCHUR_OVERLAP");
+    d.schur_overlap = (so ? std::atoi(so) != 0 : false) && d.schur_pts && d.dpart != nullptr;
+    if (const char* ch = std::getenv("SFM_CHOL_HELPERS")) d.chol_helpers = std::max(0, std::atoi(ch));
   }
   ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
   ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
@@ -856,6 +912,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   if (!sitems.empty()) H2D(d.sitems, sitems.data(), sitems.size());
   if (!sboff.empty()) H2D(d.sboff, sboff.data(), sboff.size());
   if (!scnt_init.empty()) H2D(d.scnt, scnt_init.data(), scnt_init.size());
+  if (!pcnt_init.empty()) H2D(d.pcnt, pcnt_init.data(), pcnt_init.size());
 #undef H2D
   HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
   HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
@@ -864,6 +921,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   HIPCHK(hipMemsetAsync(d.sticket, 0, sizeof(unsigned long long), s));
   h->chol_epoch = 0;
   h->schur_epoch = 0;
+  h->pts_epoch = 0;
   d.n_cu = device_cus(h->device);
   d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   h->bs_epoch = 0;

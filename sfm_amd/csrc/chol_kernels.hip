@@ -685,10 +685,34 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
   }
 }
 
+// Wave 0 waits until *f >= target, then the block proceeds.
+__device__ __forceinline__ void block_wait_count(const int* f, int target, int* fail) {
+  if (wave0()) {
+    long spins = 0;
+    bool ok = true;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > kFlagSpins) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) atomicOr(fail, 2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
+  }
+  __syncthreads();
+}
+
+// colcnt != nullptr: the Schur assembly runs concurrently (k_schur_pts on
+// another stream publishes, per tile column j, a monotone count of finished
+// workgroups that wrote S rows of column j); a helper waits for
+// colcnt[j] >= sepoch * coltgt[j] before it reads any tile (i, j).  The
+// walker reads only tiles a helper handed over (flag P), so it needs no
+// wait of its own.
 __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb,
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
-                                                    int epoch, int nhelp, int* __restrict__ fail) {
+                                                    int epoch, int nhelp, int* __restrict__ fail,
+                                                    const int* __restrict__ colcnt, const int* __restrict__ coltgt,
+                                                    int sepoch) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
@@ -719,6 +743,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     if (tk >= ntask) break;
     int j = 0, r = tk;
     while (r >= nb - j) { r -= nb - j; ++j; }
+    if (colcnt) block_wait_count(colcnt + j, sepoch * coltgt[j], fail);
     fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
   }
 }
@@ -769,22 +794,6 @@ __device__ __forceinline__ void schur_publish(int* cnt, int c) {
       for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(cnt + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-}
-
-// Wave 0 waits until *f >= target, then the block proceeds.
-__device__ __forceinline__ void block_wait_count(const int* f, int target, int* fail) {
-  if (wave0()) {
-    long spins = 0;
-    bool ok = true;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > kFlagSpins) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) atomicOr(fail, 2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
-  }
-  __syncthreads();
 }
 
 constexpr int kPoolDoubles = 3 * NB * TS + 4 * 256;
@@ -926,13 +935,21 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 
 }  // namespace
 
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int sepoch) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   if (d.cflags && !d.chol_stepwise) {
     const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
-    const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+    // gated (concurrent Schur): at most half the CUs, so that the Schur
+    // workgroups always have CUs a Cholesky workgroup (108 KB of LDS, one
+    // per CU) does not hold -- the helpers' waits then always drain
+    // (fixed per problem: the ticket base assumes every launch of a problem
+    // takes ntask + nhelp tickets)
+    int cap = d.schur_overlap ? d.n_cu / 2 - 1 : d.n_cu - 1;
+    if (d.chol_helpers > 0) cap = std::min(cap, d.chol_helpers);
+    const int nhelp = std::max(1, std::min(ntask, cap));
     k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
-                                           d.cticket, epoch, nhelp, d.fail);
+                                           d.cticket, epoch, nhelp, d.fail, sepoch > 0 ? d.pcnt : nullptr,
+                                           d.pcnt + nb, sepoch);
     return;
   }
   for (int k = 0; k < d.nblk; ++k) {

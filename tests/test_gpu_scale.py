@@ -237,6 +237,33 @@ def test_recomputed_schur_matches_gathered(monkeypatch, cfg, sub):
         assert _rel(a, b) < 1e-6
 
 
+@pytest.mark.parametrize("cfg,helpers", [("C2", "0"), ("C3", "0"), ("C3", "3")])
+def test_overlapped_schur_cholesky_is_exact(monkeypatch, cfg, helpers):
+    """Single rank, recomputed-F Schur: the Cholesky runs concurrently on a
+    second stream, its helpers gated per tile column on k_schur_pts' counts
+    (experimental SFM_SCHUR_OVERLAP=1).  The arithmetic is that of the serial launches, so whole
+    solves are bitwise equal -- also with only 3 helper workgroups (every
+    gate waited on)."""
+    s = scene.config(cfg)
+    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
+    monkeypatch.setenv("SFM_CHOL_HELPERS", helpers)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SFM_SCHUR_OVERLAP", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+            ba.reset()
+            sm2, _ = ba.solve()
+            p2 = ba.parameters()
+        out.append((sm.final_cost, tr, p, sm2.final_cost, p2))
+    (c0, t0, p0, d0, q0), (c1, t1, p1, d1, q1) = out
+    assert c0 == c1 == d0 == d1 and t0 == t1
+    for a, b, c in zip(p0, p1, q1):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
 def test_split_schur_small_problems(monkeypatch, cfg):
     """Keyframe-sized problems sum each block's pairs in chunks
