@@ -45,6 +45,7 @@ enum Scalar {
   kCholFail,        // reserved (the Cholesky flag is an int, fetched separately)
   kBadCam,          // > 0 if the camera step is non-finite
   kBadBack,         // > 0 if the point step is non-finite
+  kModelChangePt,   // point share of the model cost change (k_backsub_b; kModelChange holds the observations')
   kNumScalars
 };
 
@@ -163,7 +164,7 @@ struct DevProblem {
 // Partial-sum slots (each max_blocks doubles).
 enum PartialSlot {
   kPCost = 0, kPXNormCam, kPXNormPt, kPGradCam, kPGradPt, kPModel, kPNewCost, kPStepPt, kPStepCam, kPBad,
-  kPBadCam, kPBadBack,
+  kPBadCam, kPBadBack, kPModelPt,
   kNumPartialSlots
 };
 

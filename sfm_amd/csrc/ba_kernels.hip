@@ -1066,13 +1066,17 @@ __global__ __launch_bounds__(kThreads) void k_cam_solve(int C, const double* __r
 // Camera runs are padded to whole wavefronts, so a wavefront never spans two
 // cameras (its camera comes from wcam) and padding lanes are masked.
 __global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                        const int32_t* __restrict__ cam_obs,
                                                         const double* __restrict__ jrec,
                                                         const double* __restrict__ mrec,
-                                                        const double* __restrict__ ysol, double* __restrict__ eu) {
+                                                        const double* __restrict__ ysol, double* __restrict__ eu,
+                                                        double* __restrict__ part_model) {
   __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kJRec + kMRec)];
+  __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
-  if (i0 >= N_pad) return;
+  double model = 0.0;
+  if (i0 < N_pad) {
   const double* y = ysol + 6 * size_t(wcam[i0 >> 6]);  // wave-uniform
   double yc[6];
 #pragma unroll
@@ -1083,7 +1087,10 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int
 #pragma unroll
   for (int k = 0; k < 6; ++k) { e0 += J[k] * yc[k]; e1 += J[6 + k] * yc[k]; }
   const double2 m01 = ld2(M), m23 = ld2(M + 2), m45 = ld2(M + 4);
+  const double2 rr = ld2(J - kJC + kRes);
   wave_sync_lds();
+  // the observation's share of the model cost change (see k_backsub_b)
+  if (cam_obs[i0 + l] >= 0) model = e0 * rr.x + e1 * rr.y - 0.5 * (e0 * e0 + e1 * e1);
   // M row-major 2x3 (m0 m1 m2 | n0 n1 n2) = M[0..5];  u = M^T e
   double* o = stage[wv] + l * kEU;
   st2(o, e0, e1);
@@ -1098,35 +1105,57 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int
     const double2 v = ld2(stage[wv] + 2 * (64 * kq + l));
     st2_nt(dst + 2 * (64 * kq + l), v.x, v.y);
   }
+  }
+  const double r = block_reduce(model, sh, false);
+  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
 }
 
 __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __restrict__ pt_off,
                                                         const int32_t* __restrict__ pos,
                                                         const double* __restrict__ eu,
                                                         const double* __restrict__ ptL,
+                                                        const double* __restrict__ ptV,
                                                         const double* __restrict__ scale_p,
                                                         const double* __restrict__ X, double* __restrict__ X_new,
                                                         double* __restrict__ ypt, double* __restrict__ part_step,
-                                                        double* __restrict__ part_bad) {
+                                                        double* __restrict__ part_bad,
+                                                        double* __restrict__ part_model) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  double st = 0.0, bad = 0.0;
+  double st = 0.0, bad = 0.0, model = 0.0;
   if (p < P) {
     const double* L = ptL + size_t(kPtL) * p;
     const double l00 = L[0], l10 = L[1], l11 = L[2], l20 = L[3], l21 = L[4], l22 = L[5];
     double w0 = L[6], w1 = L[7], w2 = L[8];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;  // sum of u = L^-1 J_X^T e
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
       const double* u = eu + size_t(pos[q]) * kEU + 2;
       const double2 u01 = ld2(u);
+      const double u2 = u[2];
       w0 -= u01.x;
       w1 -= u01.y;
-      w2 -= u[2];
+      w2 -= u2;
+      s0 += u01.x; s1 += u01.y; s2 += u2;
     }
     const double y2 = w2 / l22;
     const double y1 = (w1 - l21 * y2) / l11;
     const double y0 = (w0 - l10 * y1 - l20 * y2) / l00;
     if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) bad = 1.0;
+    // Model cost change, ceres' -sum_o m_o.(r_o + m_o/2) with m_o = -(e_o +
+    // J_X,o y_p), split by observation and point:
+    //   sum_o (e.r - |e|^2/2)                      (k_backsub_a)
+    //   + y.g_p - y.h_p - y^T V0_p y / 2           (here, per point)
+    // with g_p = sum J_X^T r and V0_p = sum J_X^T J_X (ptV, k_point_eval)
+    // and h_p = sum J_X^T e = L_p sum u.  The candidate pass then reads no
+    // Jacobian record at all.
+    {
+      const double* v = ptV + size_t(kPtV) * p;
+      const double h0 = l00 * s0, h1 = l10 * s0 + l11 * s1, h2 = l20 * s0 + l21 * s1 + l22 * s2;
+      const double yVy = v[0] * y0 * y0 + v[2] * y1 * y1 + v[5] * y2 * y2 +
+                         2.0 * (v[1] * y0 * y1 + v[3] * y0 * y2 + v[4] * y1 * y2);
+      model = y0 * (v[6] - h0) + y1 * (v[7] - h1) + y2 * (v[8] - h2) - 0.5 * yVy;
+    }
     const double yp[3] = {y0, y1, y2};
     for (int k = 0; k < 3; ++k) {
       const double x = X[3 * size_t(p) + k];
@@ -1141,6 +1170,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
   if (threadIdx.x == 0) part_step[blockIdx.x] = r;
   r = block_reduce(bad, sh, true);
   if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
+  r = block_reduce(model, sh, false);
+  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
 }
 
 __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int32_t* __restrict__ wcam,
@@ -1148,31 +1179,19 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
                                                         const int32_t* __restrict__ cm_p,
                                                         const double* __restrict__ uv_cm,
                                                         const double* __restrict__ Kc,
-                                                        const double* __restrict__ jrec,
-                                                        const double* __restrict__ eu,
-                                                        const double* __restrict__ ypt,
                                                         const double* __restrict__ X_new,
                                                         const double* __restrict__ camRn,
-                                                        double* __restrict__ part_model,
                                                         double* __restrict__ part_cost) {
   __shared__ double sh[4];
-  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kJRec];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
-  double model = 0.0, ncost = 0.0;
+  double ncost = 0.0;
   if (i0 < N_pad) {
     const int64_t i = i0 + l;
     const int c = wcam[i0 >> 6];  // wave-uniform
     const bool real = cam_obs[i] >= 0;
     const int p = cm_p[i];
-    const double* Jr = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l);
-    const double2 e = ld2(eu + size_t(i) * kEU);
-    const double y0 = ypt[3 * size_t(p)], y1 = ypt[3 * size_t(p) + 1], y2 = ypt[3 * size_t(p) + 2];
-    const double m0 = -(e.x + Jr[0] * y0 + Jr[1] * y1 + Jr[2] * y2);
-    const double m1 = -(e.y + Jr[3] * y0 + Jr[4] * y1 + Jr[5] * y2);
-    const double r0 = Jr[kRes], r1 = Jr[kRes + 1];
-    const double mc = -(m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0));
-    // candidate residual
+    // candidate residual at (cam_new, X_new)
     const double* Rn = camRn + 12 * size_t(c);
     const double Xn0 = X_new[3 * size_t(p)], Xn1 = X_new[3 * size_t(p) + 1], Xn2 = X_new[3 * size_t(p) + 2];
     double pc[3];
@@ -1183,14 +1202,9 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
     const double2 uvo = ld2(uv_cm + 2 * i);
     const double rn0 = k5[0] * xp + k5[1] * ypj + k5[2] - uvo.x;
     const double rn1 = k5[3] * ypj + k5[4] - uvo.y;
-    if (real) {
-      model = mc;
-      ncost = 0.5 * (rn0 * rn0 + rn1 * rn1);
-    }
+    if (real) ncost = 0.5 * (rn0 * rn0 + rn1 * rn1);
   }
-  double r = block_reduce(model, sh, false);
-  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
-  r = block_reduce(ncost, sh, false);
+  const double r = block_reduce(ncost, sh, false);
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
 }
 
@@ -1337,12 +1351,16 @@ void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
   if (d.N_pad && cams_var)
-    k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.jrec, d.mrec, d.ysol, d.eu);
-  else if (d.N_pad)
+    k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.jrec, d.mrec, d.ysol,
+                                                                   d.eu, slot(d, kPModel));
+  else if (d.N_pad) {
     (void)hipMemsetAsync(d.eu, 0, sizeof(double) * kEU * size_t(d.N_pad), s);
+    (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
+  }
   if (d.P && pts_var) {
-    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.scale_p, d.X,
-                                                               d.X_new, d.ypt, slot(d, kPStepPt), slot(d, kPBadBack));
+    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.ptV, d.scale_p,
+                                                               d.X, d.X_new, d.ypt, slot(d, kPStepPt),
+                                                               slot(d, kPBadBack), slot(d, kPModelPt));
   } else if (d.P) {
     // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
     const size_t nbP = size_t(blocks_for(d.P, kThreads));
@@ -1350,11 +1368,11 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
     (void)hipMemcpyAsync(d.X_new, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToDevice, s);
     (void)hipMemsetAsync(slot(d, kPStepPt), 0, sizeof(double) * nbP, s);
     (void)hipMemsetAsync(slot(d, kPBadBack), 0, sizeof(double) * nbP, s);
+    (void)hipMemsetAsync(slot(d, kPModelPt), 0, sizeof(double) * nbP, s);
   }
   if (d.N_pad)
     k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
-                                                                   d.jrec, d.eu, d.ypt, d.X_new, d.camRn,
-                                                                   slot(d, kPModel), slot(d, kPNewCost));
+                                                                   d.X_new, d.camRn, slot(d, kPNewCost));
 }
 // Diagnostic (bench_jacobian SFM_JAC_THRASH=2): stream-read n doubles, no
 // stores but one word -- evicts caches without leaving dirty lines.

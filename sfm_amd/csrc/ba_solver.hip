@@ -390,7 +390,7 @@ int compute_step(sfm_ba_handle* h, double radius) {
   launch_point_backsub(d, s, h->mode != SFM_BA_STRUCT_ONLY, h->mode != SFM_BA_POSE_ONLY);
   mark_end(h);
   if (d.P == 0) {
-    const int slots[] = {kPModel, kPNewCost, kPStepPt, kPBadBack, kPBad};
+    const int slots[] = {kPModel, kPModelPt, kPNewCost, kPStepPt, kPBadBack, kPBad};
     for (int sl : slots) hipMemsetAsync(d.partials + size_t(sl) * d.max_blocks, 0, sizeof(double), s);
   }
   if (h->rank != 0 || h->mode == SFM_BA_STRUCT_ONLY)
@@ -405,11 +405,13 @@ int compute_step(sfm_ba_handle* h, double radius) {
   rb.add(kPBad, nbP, 1, kBadStep);
   rb.add(kPBadCam, nbC, 1, kBadCam);
   rb.add(kPBadBack, nbP, 1, kBadBack);
+  rb.add(kPModelPt, nbP, 0, kModelChangePt);
   // ... and the Cholesky failure flag (an int) into the slot after the scalars
   launch_reduce_batch(d, rb, true, s);
   if (sharded(h)) {
     if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
+    if ((rc = allreduce(h, d.scal + kModelChangePt, 1, ncclSum))) return rc;
   }
   return fetch_scalars(h);
 }
@@ -1059,7 +1061,7 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
       std::memcpy(&chol_fail, sc + kNumScalars, sizeof(int));
       if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out");
       const bool solve_ok = chol_fail == 0 && !(sc[kBadStep] > 0.0) && !(sc[kBadCam] > 0.0) && !(sc[kBadBack] > 0.0);
-      const double model_cost_change = sc[kModelChange];
+      const double model_cost_change = sc[kModelChange] + sc[kModelChangePt];
       itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;
       itr.step_is_successful = 0;
       if (!itr.step_is_valid) {
