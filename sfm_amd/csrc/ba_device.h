@@ -139,6 +139,9 @@ struct DevProblem {
   // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
   // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
   double* dpart = nullptr;
+  // per-chunk U_c / b_c partials from k_jacobian ([N_pad/64][27]); nullptr
+  // (SFM_CAM_FUSED=0): k_cam_reduce re-reads the records
+  double* jpart = nullptr;
   // small problems: pair-chunk items (block, first pair, end pair) with
   // per-block item ranges and partial 6x6 sums (k_schur_split)
   int4* sitems = nullptr;

@@ -199,7 +199,8 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
                                                        const double* __restrict__ camR, const double* __restrict__ X,
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ scale_p, int scaled,
-                                                       double* __restrict__ jrec, double* __restrict__ part_cost) {
+                                                       double* __restrict__ jrec, double* __restrict__ part_cost,
+                                                       double* __restrict__ jpart) {
   __shared__ double sh[4];
   __shared__ __attribute__((aligned(16))) double stage[kThreads * kJRec];  // 10 KB per wave
   const int l = threadIdx.x & 63;
@@ -273,6 +274,27 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
       double* mine = wst + l * kJRec;
 #pragma unroll
       for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
+      if (jpart) {
+        // the chunk's share of U_c = sum J_c^T J_c (21, packed upper) and
+        // b_c = sum J_c^T r (6): one reduce-scatter over the wave, lane 2e
+        // stores entry e of the chunk's partial (k_cam_sum adds a camera's
+        // chunks in order) -- no second pass over the records
+        const bool real = l < cnt;
+        const double* j0 = rec + kJC;
+        const double* j1 = rec + kJC + 6;
+        double v[32];
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int b = a; b < 6; ++b, ++q) v[q] = real ? j0[a] * j0[b] + j1[a] * j1[b] : 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) v[21 + a] = real ? j0[a] * rec[kRes] + j1[a] * rec[kRes + 1] : 0.0;
+#pragma unroll
+        for (int e = 27; e < 32; ++e) v[e] = 0.0;
+        const double tot = wave_sum32(v, l);
+        if (!(l & 1) && (l >> 1) < 27) jpart[size_t(ib / 64) * 27 + (l >> 1)] = tot;
+      }
     }
     wave_lds_sync();
     jac_flush(wst, jrec, ib, l);
@@ -336,6 +358,24 @@ __global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restri
 
 // mode 0: Jacobi scale from the unscaled column norms (diagonal of U).
 // mode 1: LM diagonal (unless reused) and camera gradient max-norm.
+// U_c and b_c from k_jacobian's per-chunk partials (jpart): lane t sums
+// chunks w0 + t, w0 + t + 64, ..., then one reduce-scatter over the wave.
+__global__ __launch_bounds__(64) void k_cam_sum(const int32_t* __restrict__ cam_rng,
+                                                const double* __restrict__ jpart, double* __restrict__ Ucam) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+  double v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v[e] = 0.0;
+  for (int w = w0 + t; w < w1; w += 64) {
+    const double* src = jpart + size_t(w) * 27;
+#pragma unroll
+    for (int e = 0; e < 27; ++e) v[e] += src[e];
+  }
+  const double sum = wave_sum32(v, t);
+  if (!(t & 1) && (t >> 1) < 27) Ucam[size_t(kUcam) * c + (t >> 1)] = sum;
+}
+
 __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* __restrict__ Ucam,
                                                            double* __restrict__ scale_c, double* __restrict__ diag_c,
                                                            double min_diag, double max_diag, int mode, int reuse,
@@ -1260,10 +1300,12 @@ void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hi
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
   k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
-                                                d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost));
+                                                d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost),
+                                                d.jpart);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
-  k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.jrec, d.Ucam);
+  if (d.jpart) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);
+  else k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.jrec, d.Ucam);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, 1e-6, 1e32, mode,

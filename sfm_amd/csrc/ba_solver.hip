@@ -830,6 +830,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
   {
+    const char* cf = std::getenv("SFM_CAM_FUSED");
+    if (!cf || std::atoi(cf) != 0) ALLOC(d.jpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
+  }
+  {
     const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
     if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
   }

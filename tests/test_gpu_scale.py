@@ -157,16 +157,18 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
         assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
+@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED"])
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
-def test_diag_partials_from_obs_prep(monkeypatch, cfg):
-    """The diagonal blocks / rhs summed from k_obs_prep's per-wave partials
-    (default) and re-read per camera by k_schur_diag (SFM_SCHUR_DIAG_FUSED=0)
-    are the same sums in a different order: deterministic, same LM path,
-    same solve to rounding."""
+def test_fused_partials_match_rereads(monkeypatch, cfg, knob):
+    """Sums taken from per-wavefront partials of the producing pass (default)
+    against a second pass over the records (knob=0): the Schur diagonal
+    blocks / rhs from k_obs_prep vs k_schur_diag, and U_c / b_c from
+    k_jacobian vs k_cam_reduce.  Same sums in a different order:
+    deterministic, same LM path, same solve to rounding."""
     s = scene.config(cfg)
     res = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SFM_SCHUR_DIAG_FUSED", flag)
+        monkeypatch.setenv(knob, flag)
         with sfm_amd.BundleAdjuster() as ba:
             ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
             sm, tr = ba.solve()
