@@ -770,8 +770,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     int kSplitPairs = int(std::min<int64_t>(64, std::max<int64_t>(16, d.n_pairs / 32768)));
     if (const char* e = std::getenv("SFM_SCHUR_SPLIT_MAXBLK")) kSplitMaxBlocks = std::atoll(e);
     if (const char* e = std::getenv("SFM_SCHUR_SPLIT_PAIRS")) kSplitPairs = std::max(1, std::atoi(e));
+    // (default off: the recomputed-F k_schur_pts at 64 lanes per block is
+    // faster on the keyframe sizes too -- C1 Schur 0.35 -> 0.07 ms per solve;
+    // SFM_SCHUR_SPLIT=1, or SFM_SCHUR_PTS=0, brings the split back)
     const char* sp = std::getenv("SFM_SCHUR_SPLIT");
-    const bool split = (sp ? std::atoi(sp) != 0 : true) && d.n_blk > 0 && d.n_blk <= kSplitMaxBlocks;
+    const char* pe = std::getenv("SFM_SCHUR_PTS");
+    const bool pts_on = pe ? std::atoi(pe) != 0 : true;
+    const bool split = (sp ? std::atoi(sp) != 0 : !pts_on) && d.n_blk > 0 && d.n_blk <= kSplitMaxBlocks;
     if (split) {
       sboff.push_back(0);
       for (int64_t b = 0; b < d.n_blk; ++b) {
@@ -845,6 +850,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
       const int v = std::atoi(ss);
       d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
+    } else {
+      // lanes per block ~ a tenth of the mean pair count, 8..64 (measured
+      // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
+      const double avg = d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0;
+      int sub = 8;
+      while (sub < 64 && sub < avg / 10.0) sub *= 2;
+      d.schur_pts_sub = sub;
     }
     if (d.schur_pts) {
       ALLOC(d.bpts, std::max<size_t>(1, bpts.size()));

@@ -271,6 +271,7 @@ def test_split_schur_small_problems(monkeypatch, cfg):
     """Keyframe-sized problems sum each block's pairs in chunks
     (k_schur_split, default up to 8192 blocks): deterministic run to run,
     and the same solve as the one-thread-per-block order to rounding."""
+    monkeypatch.setenv("SFM_SCHUR_PTS", "0")  # split vs the gathered-F blocks
     s = scene.config(cfg)
     res = {}
     for flag in ("1", "0"):
@@ -321,8 +322,8 @@ def _append_obs(s, cam, pt, uv):
 def test_edge_cases_duplicate_camera_empty_camera_single_view(monkeypatch, schur):
     # every Schur formulation (the small-problem split, the recomputed-F
     # blocks, the gathered-F rows) meets the same edge cases
+    monkeypatch.setenv("SFM_SCHUR_SPLIT", "1" if schur == "split" else "0")
     if schur != "split":
-        monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
         monkeypatch.setenv("SFM_SCHUR_PTS", "1" if schur == "pts" else "0")
     s = scene.generate(12, 400, views=4, seed=11)
     # point 3 seen a second time by one of its cameras (two residual blocks,
