@@ -654,12 +654,18 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
       st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
     block_publish_wt(F + j * nb + j, epoch);
+    // L_jj after the flag: no helper reads it (their TRSMs use W_j); the
+    // next publish's drain covers these stores
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+    }
     if (j + 1 == nb) break;
     // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
     const int i0 = j0 + NB;
@@ -917,20 +923,18 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
   if (seg == 0) v[col] = (col < nreal) ? zc - acc : 0.0;
   __syncthreads();
   if (t < NB) {
-    // y_b[t] = sum_c W(c, t) v[c]
-    double s = 0.0;
+    // y_b[t] = sum_c W(c, t) v[c]: four interleaved chains (the step is on
+    // the hand-off chain; one 64-deep FMA chain cost ~0.25 us)
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int c = 0; c < NB; ++c) s = fma(wr[c], v[c], s);
-    y[size_t(k0) + t] = (t < nreal) ? s : 0.0;
+    for (int c = 0; c < NB; ++c) s4[c & 3] = fma(wr[c], v[c], s4[c & 3]);
+    const double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    // write-through (sc1): the flag then needs no L2 write-back (the
+    // walker's producer form, block_publish_wt)
+    st_wt(y + size_t(k0) + t, (t < nreal) ? s : 0.0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave0()) {
-    if (timed_out) atomicOr(fail, 2);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (wave0() && timed_out) atomicOr(fail, 2);
+  block_publish_wt(flags + b, epoch);
 }
 
 }  // namespace
