@@ -142,6 +142,10 @@ struct DevProblem {
   // per-chunk U_c / b_c partials from k_jacobian ([N_pad/64][27]); nullptr
   // (SFM_CAM_FUSED=0): k_cam_reduce re-reads the records
   double* jpart = nullptr;
+  // point-major uv and camera index (k_point_eval_rc recomputes J_X and r;
+  // nullptr with SFM_PTEVAL_RC=0: k_point_eval gathers the records)
+  double* uv_pm = nullptr;     // [N][2]
+  int32_t* cam_pm = nullptr;   // [N]
   // small problems: pair-chunk items (block, first pair, end pair) with
   // per-block item ranges and partial 6x6 sums (k_schur_split)
   int4* sitems = nullptr;

@@ -835,6 +835,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     d.schur_fused = sf ? std::atoi(sf) != 0 : false;
   }
   {
+    const char* pr = std::getenv("SFM_PTEVAL_RC");
+    if (!pr || std::atoi(pr) != 0) {
+      ALLOC(d.uv_pm, 2 * std::max<size_t>(1, size_t(N)));
+      ALLOC(d.cam_pm, std::max<size_t>(1, size_t(N)));
+    }
+  }
+  {
     const char* cf = std::getenv("SFM_CAM_FUSED");
     if (!cf || std::atoi(cf) != 0) ALLOC(d.jpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
   }
@@ -905,6 +912,10 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HIPCHK(hipMemcpyAsync(d.jchunks, jchunks.data(), sizeof(int32_t) * jchunks.size(), hipMemcpyHostToDevice, s));
     H2D(d.uv_cm, uv_cm.data(), 2 * size_t(npad));
     H2D(d.pos, pos.data(), size_t(N));
+    if (d.uv_pm) {
+      H2D(d.uv_pm, uv_s.data(), 2 * size_t(N));
+      H2D(d.cam_pm, cam_s.data(), size_t(N));
+    }
     h->pos = pos;
   }
   H2D(d.pt_off, pt_off.data(), size_t(P) + 1);

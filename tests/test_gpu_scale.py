@@ -157,13 +157,14 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
         assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
-@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED"])
+@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED", "SFM_PTEVAL_RC"])
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
 def test_fused_partials_match_rereads(monkeypatch, cfg, knob):
     """Sums taken from per-wavefront partials of the producing pass (default)
     against a second pass over the records (knob=0): the Schur diagonal
     blocks / rhs from k_obs_prep vs k_schur_diag, and U_c / b_c from
-    k_jacobian vs k_cam_reduce.  Same sums in a different order:
+    k_jacobian vs k_cam_reduce, V_p / b_p from recomputed J_X (uv streamed
+    point-major) vs the gathered records.  Same sums in a different order:
     deterministic, same LM path, same solve to rounding."""
     s = scene.config(cfg)
     res = {}
