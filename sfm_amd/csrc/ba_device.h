@@ -145,6 +145,10 @@ struct DevProblem {
   // point-major uv and camera index (k_point_eval_rc recomputes J_X and r;
   // nullptr with SFM_PTEVAL_RC=0: k_point_eval gathers the records)
   double* uv_pm = nullptr;     // [N][2]
+  // record-free observation passes (k_obs_prep_rc, k_backsub_a_rc; SFM_OBS_RC=0
+  // restores the record readers); need_jrec: some consumer still reads jrec
+  bool obs_rc = false;
+  bool need_jrec = true;
   int32_t* cam_pm = nullptr;   // [N]
   // small problems: pair-chunk items (block, first pair, end pair) with
   // per-block item ranges and partial 6x6 sums (k_schur_split)
@@ -177,7 +181,8 @@ enum PartialSlot {
 
 // ---- launchers (ba_kernels.hip) ----
 void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s);
-void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s);
+// force_records: write the 160-B records even in the record-free path (evaluate API, tools)
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool force_records = false);
 void launch_cam_reduce(const DevProblem& d, hipStream_t s);
 // mode 0: unscaled pass -> compute scale_c from colnorms; mode 1: diag (if !reuse) + gradient
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s);

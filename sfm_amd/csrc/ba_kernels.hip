@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ scale_p, int scaled,
                                                        double* __restrict__ jrec, double* __restrict__ part_cost,
-                                                       double* __restrict__ jpart) {
+                                                       double* __restrict__ jpart, int write_rec) {
   __shared__ double sh[4];
   __shared__ __attribute__((aligned(16))) double stage[kThreads * kJRec];  // 10 KB per wave
   const int l = threadIdx.x & 63;
@@ -296,9 +296,11 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
         if (!(l & 1) && (l >> 1) < 27) jpart[size_t(ib / 64) * 27 + (l >> 1)] = tot;
       }
     }
-    wave_lds_sync();
-    jac_flush(wst, jrec, ib, l);
-    wave_lds_sync();
+    if (write_rec) {  // wave-uniform: no record consumer left in the record-free solve path
+      wave_lds_sync();
+      jac_flush(wst, jrec, ib, l);
+      wave_lds_sync();
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) { Xc[j] = Xn[j]; spc[j] = spn[j]; }
     uv_cur = uv_nxt;
@@ -647,6 +649,157 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int3
       const double2 v = ld2(sf + 2 * (64 * kq + l));
       st2_nt(df + 2 * (64 * kq + l), v.x, v.y);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Record-free observation kernels (default): the camera-major passes after
+// the Jacobian recompute an observation's residual and scaled 2x9 Jacobian
+// with jac_record itself (bitwise the k_jacobian record) from the camera
+// (wave-uniform: R, dR/dw, t, K, scale are scalar loads), the point (X,
+// scale, L_p, z_p: L2/MALL-resident gathers) and the streamed uv, instead of
+// reading the 160-B record (325 MB) and the 64-B M record (130 MB) back from
+// HBM.  With every consumer recomputing, k_jacobian stops writing records.
+struct ObsRC {
+  double rec[kJRec];   // J_X 6 | r 2 | J_c 12 (scaled)
+  double M[6];         // J_X L^-T, rows m | n
+  double h0, h1;       // M z
+};
+__device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const double* __restrict__ camR,
+                                              const double* __restrict__ cam, const double* __restrict__ Kc,
+                                              const double* __restrict__ scale_c, const double* __restrict__ ptS,
+                                              const double* __restrict__ ptL, ObsRC& o) {
+  // camera (wave-uniform: scalar loads)
+  const double* cr = camR + size_t(kCamR) * c;
+  const double* k = Kc + 5 * size_t(c);
+  const double* tc = cam + 6 * size_t(c) + 3;
+  const double* sc = scale_c + 6 * size_t(c);
+  const double fx = k[0], sk = k[1], cx = k[2], fy = k[3], cy = k[4];
+  // point: one 128-B Schur record (X, scale, L, 1/l_ii) and z from ptL
+  const double* rp = ptS + size_t(kPtS) * p;
+  double q[16];
+#pragma unroll
+  for (int f = 0; f < 16; f += 2) {
+    const double2 x = ld2(rp + f);
+    q[f] = x.x; q[f + 1] = x.y;
+  }
+  const double2 z01 = ld2(ptL + size_t(kPtL) * p + 6);
+  const double z2 = ptL[size_t(kPtL) * p + 8];
+  const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
+  // jac_record's formulas with one reciprocal (1/z) for the projection
+  const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
+  const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc[1];
+  const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc[2];
+  const double iz = 1.0 / pc2, xp = pc0 * iz, yp = pc1 * iz;
+  double* rec = o.rec;
+  rec[kRes] = fx * xp + sk * yp + cx - uvo.x;
+  rec[kRes + 1] = fy * yp + cy - uvo.y;
+  const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+  const double b1 = fy * iz, b2 = -fy * yp * iz;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    rec[kJX + j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
+    rec[kJX + 3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
+  }
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk) {
+    const double* D = cr + 9 + 9 * kk;
+    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+    rec[kJC + kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
+    rec[kJC + 6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
+  }
+  rec[kJC + 3] = a0 * sc[3]; rec[kJC + 4] = a1 * sc[4]; rec[kJC + 5] = a2 * sc[5];
+  rec[kJC + 9] = 0.0;        rec[kJC + 10] = b1 * sc[4]; rec[kJC + 11] = b2 * sc[5];
+  const double l10 = q[7], l20 = q[9], l21 = q[10], i00 = q[12], i11 = q[13], i22 = q[14];
+  const double* e = rec + kJX;
+  o.M[0] = e[0] * i00; o.M[1] = (e[1] - l10 * o.M[0]) * i11; o.M[2] = (e[2] - l20 * o.M[0] - l21 * o.M[1]) * i22;
+  o.M[3] = e[3] * i00; o.M[4] = (e[4] - l10 * o.M[3]) * i11; o.M[5] = (e[5] - l20 * o.M[3] - l21 * o.M[4]) * i22;
+  o.h0 = o.M[0] * z01.x + o.M[1] * z01.y + o.M[2] * z2;
+  o.h1 = o.M[3] * z01.x + o.M[4] * z01.y + o.M[5] * z2;
+}
+
+// The Schur diagonal-block / rhs partials of k_obs_prep (dpart), recomputed
+// (ptS is written by k_point_factor in the same launch sequence).
+__global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                          const int32_t* __restrict__ cm_p,
+                                                          const double* __restrict__ uv_cm,
+                                                          const int32_t* __restrict__ cam_obs,
+                                                          const double* __restrict__ camR,
+                                                          const double* __restrict__ cam,
+                                                          const double* __restrict__ Kc,
+                                                          const double* __restrict__ scale_c,
+                                                          const double* __restrict__ ptS,
+                                                          const double* __restrict__ ptL, double* __restrict__ dpart) {
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
+  if (i0 >= N_pad) return;  // wave-uniform, no barriers below
+  const int64_t i = i0 + l;
+  const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
+  ObsRC o;
+  obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, ptL, o);
+  const double* jc = o.rec + kJC;
+  double F[kFRec];
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    F[3 * u] = jc[u] * o.M[0] + jc[6 + u] * o.M[3];
+    F[3 * u + 1] = jc[u] * o.M[1] + jc[6 + u] * o.M[4];
+    F[3 * u + 2] = jc[u] * o.M[2] + jc[6 + u] * o.M[5];
+  }
+  const bool real = cam_obs[i] >= 0;
+  const double r0 = real ? o.rec[kRes] - o.h0 : 0.0, r1 = real ? o.rec[kRes + 1] - o.h1 : 0.0;
+  double v[32];
+  int q = 0;
+#pragma unroll
+  for (int u = 0; u < 6; ++u)
+#pragma unroll
+    for (int w = u; w < 6; ++w, ++q)
+      v[q] = real ? F[3 * u] * F[3 * w] + F[3 * u + 1] * F[3 * w + 1] + F[3 * u + 2] * F[3 * w + 2] : 0.0;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) v[21 + u] = jc[u] * r0 + jc[6 + u] * r1;
+#pragma unroll
+  for (int e = 27; e < 32; ++e) v[e] = 0.0;
+  const double tot = wave_sum32(v, l);
+  if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
+}
+
+// Back substitution pass A (see k_backsub_a), recomputed: e = J_c y_c,
+// u = M^T e, and the observation's share of the model cost change.
+__global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                           const int32_t* __restrict__ cm_p,
+                                                           const double* __restrict__ uv_cm,
+                                                           const int32_t* __restrict__ cam_obs,
+                                                           const double* __restrict__ camR,
+                                                           const double* __restrict__ cam,
+                                                           const double* __restrict__ Kc,
+                                                           const double* __restrict__ scale_c,
+                                                           const double* __restrict__ ptS,
+                                                           const double* __restrict__ ptL,
+                                                           const double* __restrict__ ysol, double* __restrict__ eu,
+                                                           double* __restrict__ part_model) {
+  __shared__ double sh[4];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
+  double model = 0.0;
+  if (i0 < N_pad) {
+    const int64_t i = i0 + l;
+    const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
+    ObsRC o;
+    obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, ptL, o);
+    const double* y = ysol + 6 * size_t(c);
+    const double* J = o.rec + kJC;
+    double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
+    if (cam_obs[i] >= 0) model = e0 * o.rec[kRes] + e1 * o.rec[kRes + 1] - 0.5 * (e0 * e0 + e1 * e1);
+    const double* M = o.M;
+    double* dst = eu + size_t(i) * kEU;
+    st2(dst, e0, e1);
+    st2(dst + 2, M[0] * e0 + M[3] * e1, M[1] * e0 + M[4] * e1);
+    st2(dst + 4, M[2] * e0 + M[5] * e1, 0.0);
+  }
+  const double r = block_reduce(model, sh, false);
+  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -1372,10 +1525,10 @@ static inline double* slot(const DevProblem& d, int s) { return d.partials + siz
 void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s) {
   k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
 }
-void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s) {
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool force_records) {
   k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
                                                 d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost),
-                                                d.jpart);
+                                                d.jpart, (d.need_jrec || force_records) ? 1 : 0);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   if (d.jpart) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);
@@ -1401,12 +1554,18 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad), d.X, d.scale_p, nullptr);
+                                                                         slot(d, kPBad), d.X, d.scale_p,
+                                                                         d.schur_pts ? d.ptS : nullptr);
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
                                                                          slot(d, kPBad), d.X, d.scale_p,
                                                                          d.schur_pts ? d.ptS : nullptr);
+  if (d.N_pad && d.obs_rc && d.dpart) {
+    k_obs_prep_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
+                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.ptL, d.dpart);
+    return;
+  }
   if (d.N_pad)
     k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec,
                                                                  d.schur_pts ? nullptr : d.frec, d.cam_obs,
@@ -1473,7 +1632,11 @@ void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
 }
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
-  if (d.N_pad && cams_var)
+  if (d.N_pad && cams_var && d.obs_rc)
+    k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
+                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ptL,
+                                                                     d.ysol, d.eu, slot(d, kPModel));
+  else if (d.N_pad && cams_var)
     k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.jrec, d.mrec, d.ysol,
                                                                    d.eu, slot(d, kPModel));
   else if (d.N_pad) {

@@ -374,6 +374,9 @@ int compute_step(sfm_ba_handle* h, double radius) {
   } else if (h->mode == SFM_BA_POSE_ONLY) {
     // block-diagonal camera system from the all-reduced U_c (same on every rank)
     launch_cam_solve(d, radius, s);
+    // the record-free back substitution reads X from the point records
+    // (their factor is unused here: y_p = 0); its bad flags are cleared below
+    if (d.obs_rc && d.P) launch_point_factor(d, radius, s);
     hipMemsetAsync(d.partials + size_t(kPBad) * d.max_blocks, 0, sizeof(double) * nbP, s);
   } else {
     // STRUCT_ONLY: per-point 3x3 systems only; y_c = 0
@@ -887,6 +890,14 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     d.schur_overlap = (so ? std::atoi(so) != 0 : false) && d.schur_pts && d.dpart != nullptr;
     if (const char* ch = std::getenv("SFM_CHOL_HELPERS")) d.chol_helpers = std::max(0, std::atoi(ch));
   }
+  {
+    // record-free observation passes: they need the diagonal partials and
+    // the recomputed-F Schur (every gathered-F path reads F records);
+    // k_jacobian then writes no records unless another reader is selected
+    const char* orc = std::getenv("SFM_OBS_RC");
+    d.obs_rc = (orc ? std::atoi(orc) != 0 : true) && d.dpart != nullptr && d.schur_pts;
+    d.need_jrec = !(d.obs_rc && d.jpart != nullptr && d.uv_pm != nullptr);
+  }
   ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
   ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
   ALLOC(d.spart, 36 * std::max<size_t>(1, sitems.size()));
@@ -1197,7 +1208,7 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;
   launch_cam_prep(d, d.cam, false, h->stream);
-  launch_jacobian(d, false, h->stream);
+  launch_jacobian(d, false, h->stream, true);  // the records are the output
   if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
   launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, h->stream);
   std::vector<double> rec(size_t(kJRec) * d.N_pad);
@@ -1291,7 +1302,7 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
-  launch_jacobian(d, true, h->stream);  // warm
+  launch_jacobian(d, true, h->stream, true);  // warm (the record-writing pass is what is measured)
   if (const char* th = std::getenv("SFM_JAC_THRASH")) {
     const int kind = std::atoi(th);  // 1: 288-MB write, 2: 288-MB read
     // diagnostic: each pass timed alone behind a 288-MB write of another
@@ -1301,7 +1312,7 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
       if (kind == 2) launch_read_touch(d.frec, size_t(kFRec) * size_t(d.N), d.scal + kNumScalars - 1, h->stream);
       else HIPCHK(hipMemsetAsync(d.frec, 0, sizeof(double) * kFRec * size_t(d.N), h->stream));
       HIPCHK(hipEventRecord(e0, h->stream));
-      launch_jacobian(d, true, h->stream);
+      launch_jacobian(d, true, h->stream, true);
       HIPCHK(hipEventRecord(e1, h->stream));
       HIPCHK(hipEventSynchronize(e1));
       float ms = 0.f;
@@ -1314,7 +1325,7 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
     return 0;
   }
   HIPCHK(hipEventRecord(e0, h->stream));
-  for (int i = 0; i < reps; ++i) launch_jacobian(d, true, h->stream);
+  for (int i = 0; i < reps; ++i) launch_jacobian(d, true, h->stream, true);
   HIPCHK(hipEventRecord(e1, h->stream));
   HIPCHK(hipEventSynchronize(e1));
   float ms = 0.f;

@@ -157,7 +157,7 @@ def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
         assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
-@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED", "SFM_PTEVAL_RC"])
+@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED", "SFM_PTEVAL_RC", "SFM_OBS_RC"])
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
 def test_fused_partials_match_rereads(monkeypatch, cfg, knob):
     """Sums taken from per-wavefront partials of the producing pass (default)
