@@ -73,6 +73,7 @@ struct DevProblem {
   int32_t n_jchunks = 0;
   int32_t* jgrp = nullptr;     // [9] chunk-table offsets of the 8 point slices (one per XCD)
   int32_t jac_blocks = 1;      // persistent grid of k_jacobian (cost partials)
+  int32_t jac_blocks_rec = 1;  // ... of the record-writing variant (evaluate API, bench roofline)
   double* uv_cm = nullptr;     // [N_pad][2] uv in camera-major order
   int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q (jrec index)
   double* Kc = nullptr;        // [C][5] fx skew cx fy cy

@@ -1526,9 +1526,10 @@ void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hi
   k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool force_records) {
-  k_jacobian<<<d.jac_blocks, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
-                                                d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost),
-                                                d.jpart, (d.need_jrec || force_records) ? 1 : 0);
+  const bool rec = d.need_jrec || force_records;
+  k_jacobian<<<rec ? d.jac_blocks_rec : d.jac_blocks, kThreads, 0, s>>>(
+      d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X, d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
+      slot(d, kPCost), d.jpart, rec ? 1 : 0);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   if (d.jpart) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);

@@ -897,6 +897,12 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     const char* orc = std::getenv("SFM_OBS_RC");
     d.obs_rc = (orc ? std::atoi(orc) != 0 : true) && d.dpart != nullptr && d.schur_pts;
     d.need_jrec = !(d.obs_rc && d.jpart != nullptr && d.uv_pm != nullptr);
+    // the record-free Jacobian pass (no 160-B stores) prefers a larger grid:
+    // 256 workgroups per XCD, 0.256 -> 0.223 ms per C3 solve
+    d.jac_blocks_rec = d.jac_blocks;
+    if (!d.need_jrec && !std::getenv("SFM_JAC_WG_PER_XCD"))
+      d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 256));
+    d.max_blocks = std::max(d.max_blocks, d.jac_blocks);  // cost partials (allocated below)
   }
   ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
   ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
