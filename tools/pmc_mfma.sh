@@ -6,8 +6,8 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_mfma
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-RX='k_jacobian|k_chol_fused|k_schur_row|k_obs_prep'
-timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$RX" --output-format csv -d $OUT -- python3 $R/tools/pmc_c3.py > $OUT/run.log 2>&1 || exit 1
+RX='k_chol_fused|k_schur_pts|k_obs_prep'
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$RX" --output-format csv -d $OUT -- python3 $R/tools/pmc_c3.py solve > $OUT/run.log 2>&1 || exit 1
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
