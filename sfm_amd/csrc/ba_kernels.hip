@@ -791,12 +791,16 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
     double e0 = 0.0, e1 = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
-    if (cam_obs[i] >= 0) model = e0 * o.rec[kRes] + e1 * o.rec[kRes + 1] - 0.5 * (e0 * e0 + e1 * e1);
-    const double* M = o.M;
-    double* dst = eu + size_t(i) * kEU;
-    st2(dst, e0, e1);
-    st2(dst + 2, M[0] * e0 + M[3] * e1, M[1] * e0 + M[4] * e1);
-    st2(dst + 4, M[2] * e0 + M[5] * e1, 0.0);
+    const int qo = cam_obs[i];
+    if (qo >= 0) {
+      model = e0 * o.rec[kRes] + e1 * o.rec[kRes + 1] - 0.5 * (e0 * e0 + e1 * e1);
+      // u goes to the observation's POINT-major slot (32 B): pass B then
+      // streams a point's u contiguously instead of gathering 48-B records
+      const double* M = o.M;
+      double* dst = eu + 4 * size_t(qo);
+      st2(dst, M[0] * e0 + M[3] * e1, M[1] * e0 + M[4] * e1);
+      dst[2] = M[2] * e0 + M[5] * e1;
+    }
   }
   const double r = block_reduce(model, sh, false);
   if (threadIdx.x == 0) part_model[blockIdx.x] = r;
@@ -1386,7 +1390,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
                                                         const double* __restrict__ X, double* __restrict__ X_new,
                                                         double* __restrict__ ypt, double* __restrict__ part_step,
                                                         double* __restrict__ part_bad,
-                                                        double* __restrict__ part_model) {
+                                                        double* __restrict__ part_model, int upm) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0, model = 0.0;
@@ -1397,7 +1401,9 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;  // sum of u = L^-1 J_X^T e
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      const double* u = eu + size_t(pos[q]) * kEU + 2;
+      // upm: u at the point-major slot (k_backsub_a_rc), else in the
+      // camera-major e|u record (k_backsub_a)
+      const double* u = upm ? eu + 4 * size_t(q) : eu + size_t(pos[q]) * kEU + 2;
       const double2 u01 = ld2(u);
       const double u2 = u[2];
       w0 -= u01.x;
@@ -1647,7 +1653,8 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   if (d.P && pts_var) {
     k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.ptV, d.scale_p,
                                                                d.X, d.X_new, d.ypt, slot(d, kPStepPt),
-                                                               slot(d, kPBadBack), slot(d, kPModelPt));
+                                                               slot(d, kPBadBack), slot(d, kPModelPt),
+                                                               d.obs_rc ? 1 : 0);
   } else if (d.P) {
     // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
     const size_t nbP = size_t(blocks_for(d.P, kThreads));
