@@ -128,6 +128,7 @@ struct DevProblem {
   // point of each pair, and the per-point records; F is recomputed per pair
   // from the point and the two wave-uniform cameras instead of gathered
   int32_t* bpts = nullptr;    // [n_pairs]
+  int32_t* bperm = nullptr;   // [n_blk] blocks by descending pair count (k_schur_pts wave balance)
   double* ptS = nullptr;      // [P][kPtS]
   bool schur_pts = false;
   // concurrent Schur + Cholesky (single rank, pts mode): [nblk] monotone

@@ -1054,21 +1054,25 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
                                                         const double* __restrict__ camR,
                                                         const double* __restrict__ cam, const double* __restrict__ Kc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
-                                                        int ld, int diag_add, int* __restrict__ colcnt) {
+                                                        int ld, int diag_add, int* __restrict__ colcnt,
+                                                        const int32_t* __restrict__ bperm) {
   constexpr int kPer = 64 / kSub;  // blocks per wave
   __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
   const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
   // (no early exit: a wave past the end runs empty lists, so every wave
   // reaches the publishing barrier)
-  const int64_t b = min(wb + g, n_blk - 1);
+  // bperm: blocks taken in descending pair count, so the kPer segments of a
+  // wave run lists of nearly equal length (the wave steps to the longest)
+  auto blk_at = [&](int64_t k) -> int64_t { return bperm ? int64_t(bperm[k]) : k; };
+  const int64_t b = blk_at(min(wb + g, n_blk - 1));
   const bool own = wb + g < n_blk;
   const int2 cc = blk[b];
   double* cs1 = cst[wv][g];
   double* cs2 = cs1 + kCamS;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    const int2 cq = blk[min(wb + q, n_blk - 1)];
+    const int2 cq = blk[blk_at(min(wb + q, n_blk - 1))];
     stage_cam(cst[wv][q], cq.x, camR, cam, Kc, scale_c, l);
     stage_cam(cst[wv][q] + kCamS, cq.y, camR, cam, Kc, scale_c, l);
   }
@@ -1615,7 +1619,7 @@ void launch_schur_pts(const DevProblem& d, int sepoch, hipStream_t s) {
   int* cnt = sepoch > 0 ? d.pcnt : nullptr;
 #define SFM_PTS(S_)                                                                                           \
   k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                          d.S, d.ld, diag_add, cnt)
+                                          d.S, d.ld, diag_add, cnt, cnt ? nullptr : d.bperm)
   if (sub == 8) SFM_PTS(8);
   else if (sub == 16) SFM_PTS(16);
   else if (sub == 32) SFM_PTS(32);

@@ -793,7 +793,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n_sitems = int32_t(sitems.size());
   // fused Schur + Cholesky task table (k_chol_schur_fused, chol_kernels.hip)
   std::vector<int4> stasks;
-  std::vector<int32_t> scnt_init, pcnt_init;
+  std::vector<int32_t> scnt_init, pcnt_init, bperm;
   {
     const int nb = d.nblk;
     std::vector<int32_t> target(nb, 0);
@@ -881,6 +881,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
         for (int j = j0; j <= j1; ++j) ++pcnt_init[size_t(d.nblk) + j];
       }
       ALLOC(d.pcnt, pcnt_init.size());
+      if (!env_flag("SFM_SCHUR_PTS_NOPERM")) {
+        bperm.resize(size_t(d.n_blk));
+        for (int64_t b = 0; b < d.n_blk; ++b) bperm[b] = int32_t(b);
+        std::stable_sort(bperm.begin(), bperm.end(),
+                         [&](int32_t a, int32_t b) { return seg[a + 1] - seg[a] > seg[b + 1] - seg[b]; });
+        ALLOC(d.bperm, bperm.size());
+      }
     }
     // experimental, off by default: measured slower at C3 (3.90 ms per solve
     // for the overlapped pair vs 1.07 + 2.62 ms serial; the Cholesky alone
@@ -953,6 +960,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
   H2D(d.seg, seg.data(), seg.size());
   if (d.schur_pts && !bpts.empty()) H2D(d.bpts, bpts.data(), bpts.size());
+  if (d.bperm) H2D(d.bperm, bperm.data(), bperm.size());
   if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
   if (!stasks.empty()) H2D(d.stasks, stasks.data(), stasks.size());
   if (!sitems.empty()) H2D(d.sitems, sitems.data(), sitems.size());
