@@ -1465,7 +1465,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
   double ncost = 0.0;
   if (i0 < N_pad) {
     const int64_t i = i0 + l;
-    const int c = wcam[i0 >> 6];  // wave-uniform
+    const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);  // wave-uniform: scalar camera loads
     const bool real = cam_obs[i] >= 0;
     const int p = cm_p[i];
     // candidate residual at (cam_new, X_new)
