@@ -369,6 +369,20 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
 
   for (int64_t i = 0; i < n_obs; ++i)
     if (cam_idx[i] < 0 || cam_idx[i] >= n_cams || pt_idx[i] < 0 || pt_idx[i] >= n_pts) return -22;
+  // Ceres 1.12 Solver::Options::IsValid (CommonOptionsAreValid +
+  // TrustRegionOptionsAreValid): ceres::Solve refuses to run otherwise
+  {
+    const Options& o = *opts;
+    const bool ok = o.max_num_iterations >= 0 && o.function_tolerance >= 0 && o.gradient_tolerance >= 0 &&
+                    o.parameter_tolerance >= 0 && o.initial_trust_region_radius > 0 &&
+                    o.min_trust_region_radius > 0 && o.max_trust_region_radius > 0 &&
+                    o.min_trust_region_radius <= o.max_trust_region_radius &&
+                    o.min_trust_region_radius <= o.initial_trust_region_radius &&
+                    o.initial_trust_region_radius <= o.max_trust_region_radius && o.min_relative_decrease >= 0 &&
+                    o.min_lm_diagonal >= 0 && o.max_lm_diagonal >= 0 && o.min_lm_diagonal <= o.max_lm_diagonal &&
+                    o.max_num_consecutive_invalid_steps >= 0;
+    if (!ok) return -22;
+  }
 
   Problem pb;
   pb.mode = mode; pb.n_obs = (mode >= 0 && mode <= 2) ? n_obs : 0;

@@ -21,6 +21,23 @@ def _i32(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
+def _check_shapes(uv, cam_idx, pt_idx, K9, rot, t, X) -> None:
+    """Shapes the C ABI reads (it trusts n_obs / n_cams / n_pts): a short
+    array would be an out-of-bounds host read, so refuse it here."""
+    n = uv.shape[0] if uv.ndim == 2 else -1
+    if uv.ndim != 2 or uv.shape[1] != 2:
+        raise ValueError(f"uv must be (n, 2), got {uv.shape}")
+    if cam_idx.shape != (n,) or pt_idx.shape != (n,):
+        raise ValueError(f"cam_idx / pt_idx must be ({n},), got {cam_idx.shape} / {pt_idx.shape}")
+    if rot.ndim != 2 or rot.shape[1] != 3 or t.shape != rot.shape:
+        raise ValueError(f"rot and t must be (C, 3), got {rot.shape} / {t.shape}")
+    C = rot.shape[0]
+    if K9.size != 9 * C or not (K9.shape in ((C, 9), (C, 3, 3)) or (C == 1 and K9.shape in ((9,), (3, 3)))):
+        raise ValueError(f"K must be (C, 9) or (C, 3, 3) with C = {C}, got {K9.shape}")
+    if X.ndim != 2 or X.shape[1] != 3:
+        raise ValueError(f"X must be (P, 3), got {X.shape}")
+
+
 def make_options(**overrides) -> BAOptions:
     o = default_options()
     for k, v in overrides.items():
@@ -89,6 +106,7 @@ class BundleAdjuster:
     def set_problem(self, uv, cam_idx, pt_idx, K9, rot, t, X) -> None:
         uv, K9, rot, t, X = _f64(uv), _f64(K9), _f64(rot), _f64(t), _f64(X)
         cam_idx, pt_idx = _i32(cam_idx), _i32(pt_idx)
+        _check_shapes(uv, cam_idx, pt_idx, K9, rot, t, X)
         n = int(uv.shape[0])
         C, P = int(rot.shape[0]), int(X.shape[0])
         check(lib().sfm_ba_set_problem(self._h, n, ptr(uv), ptr(cam_idx), ptr(pt_idx), C, ptr(K9), ptr(rot),
@@ -146,6 +164,7 @@ def solve(uv, cam_idx, pt_idx, K9, rot, t, X, options: BAOptions | None = None, 
             raise TypeError(f"{name} must be a C-contiguous float64 array (updated in place)")
     uv, K9 = _f64(uv), _f64(K9)
     cam_idx, pt_idx = _i32(cam_idx), _i32(pt_idx)
+    _check_shapes(uv, cam_idx, pt_idx, K9, rot, t, X)
     opts = options if options is not None else default_options()
     sm = BASummary()
     tr = (BAIteration * trace_cap)()

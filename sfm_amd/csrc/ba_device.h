@@ -113,6 +113,8 @@ struct DevProblem {
   int32_t* cflags = nullptr;  // [2][nblk][nblk] fused Cholesky: final (F) and partial (P) tile flags
   unsigned long long* cticket = nullptr;  // fused Cholesky tile ticket (monotone across launches)
   int32_t n_cu = 0;           // compute units (co-residency bound of the persistent grids)
+  // LM diagonal clamp of the running solve (sfm_ba_options min/max_lm_diagonal)
+  double min_diag = 1e-6, max_diag = 1e32;
   bool chol_stepwise = false; // SFM_CHOL_STEPWISE=1: three launches per tile column instead
 
   // Schur: upper-triangle blocks (c1, c2) in row-major order, CSR offsets

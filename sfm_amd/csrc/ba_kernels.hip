@@ -1546,7 +1546,7 @@ void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   else k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.jrec, d.Ucam);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
-  k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, 1e-6, 1e32, mode,
+  k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
                                                                reuse_diag ? 1 : 0,
                                                                count_grad ? slot(d, kPGradCam) : nullptr);
 }
@@ -1554,13 +1554,13 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
   if (d.P == 0) return;
   if (d.uv_pm) {
     k_point_eval_rc<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam,
-                                                                   d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, 1e-6, 1e32,
+                                                                   d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag,
                                                                    mode, reuse_diag ? 1 : 0, slot(d, kPGradPt),
                                                                    slot(d, kPXNormPt));
     return;
   }
   k_point_eval<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.X, d.scale_p, d.diag_p, d.ptV,
-                                                             1e-6, 1e32, mode, reuse_diag ? 1 : 0,
+                                                             d.min_diag, d.max_diag, mode, reuse_diag ? 1 : 0,
                                                              slot(d, kPGradPt), slot(d, kPXNormPt));
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {

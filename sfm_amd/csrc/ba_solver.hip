@@ -419,6 +419,29 @@ int compute_step(sfm_ba_handle* h, double radius) {
   return fetch_scalars(h);
 }
 
+// Ceres 1.12 Solver::Options::IsValid (CommonOptionsAreValid +
+// TrustRegionOptionsAreValid): ceres::Solve refuses options that fail these
+// (the reference only sets linear_solver_type, CTracker.cpp:571-577).
+// Returns the offending rule, or nullptr.
+const char* invalid_option(const sfm_ba_options& o) {
+  if (!(o.max_num_iterations >= 0)) return "max_num_iterations >= 0";
+  if (!(o.max_num_consecutive_invalid_steps >= 0)) return "max_num_consecutive_invalid_steps >= 0";
+  if (!(o.function_tolerance >= 0)) return "function_tolerance >= 0";
+  if (!(o.gradient_tolerance >= 0)) return "gradient_tolerance >= 0";
+  if (!(o.parameter_tolerance >= 0)) return "parameter_tolerance >= 0";
+  if (!(o.initial_trust_region_radius > 0)) return "initial_trust_region_radius > 0";
+  if (!(o.min_trust_region_radius > 0)) return "min_trust_region_radius > 0";
+  if (!(o.max_trust_region_radius > 0)) return "max_trust_region_radius > 0";
+  if (!(o.min_trust_region_radius <= o.max_trust_region_radius)) return "min_trust_region_radius <= max";
+  if (!(o.min_trust_region_radius <= o.initial_trust_region_radius)) return "min_trust_region_radius <= initial";
+  if (!(o.initial_trust_region_radius <= o.max_trust_region_radius)) return "initial_trust_region_radius <= max";
+  if (!(o.min_relative_decrease >= 0)) return "min_relative_decrease >= 0";
+  if (!(o.min_lm_diagonal >= 0)) return "min_lm_diagonal >= 0";
+  if (!(o.max_lm_diagonal >= 0)) return "max_lm_diagonal >= 0";
+  if (!(o.min_lm_diagonal <= o.max_lm_diagonal)) return "min_lm_diagonal <= max_lm_diagonal";
+  return nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -665,6 +688,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
           if (cam_s[o2] >= c1 && o2 != o1) ++row[cam_s[o2]];
       }
     });
+    int64_t total = 0;
+    for (int64_t b = 0; b < nblk; ++b) total += cnt[b];
+    if (total >= int64_t(INT32_MAX)) return fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets");
     seg.assign(size_t(nblk) + 1, 0);
     for (int64_t b = 0; b < nblk; ++b) seg[b + 1] = seg[b] + cnt[b];
     pairs.assign(2 * size_t(seg[nblk]), 0);
@@ -707,7 +733,6 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
       bfirst += nrow;
     }
   }
-  if (pairs.size() / 2 >= size_t(INT32_MAX)) return fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets");
   d.n_blk = int64_t(blk.size() / 2);
   d.n_pairs = int64_t(pairs.size() / 2);
   // ---- dense system geometry ----
@@ -1038,6 +1063,7 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
   sfm_ba_options opts;
   if (opts_in) opts = *opts_in; else sfm_ba_default_options(&opts);
+  if (const char* why = invalid_option(opts)) return fail(SFM_EINVAL, std::string("invalid option: ") + why);
   sfm_ba_summary sm;
   std::memset(&sm, 0, sizeof(sm));
   int tl = 0;
@@ -1056,6 +1082,8 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;
   h->mode = mode;
+  d.min_diag = opts.min_lm_diagonal;
+  d.max_diag = opts.max_lm_diagonal;
   int rc;
   if (!opts.jacobi_scaling) {
     std::vector<double> ones(std::max(6 * size_t(d.C), 3 * size_t(d.P)), 1.0);
@@ -1204,8 +1232,17 @@ int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const 
   // once per keyframe (CSfM.cpp:259, 970), so the stream, the pinned mirror
   // and (through the pool) the device buffers are created once, not per call
   // (measured at C1: create 1.7 ms + destroy 2.2 ms against a 1.9-ms solve).
-  static thread_local std::map<int, sfm_ba_handle*> cache;
-  sfm_ba_handle*& h = cache[dev];
+  // The cache owns its handles: they are destroyed (stream, pinned mirror,
+  // pooled device buffers) when the calling thread exits.
+  struct HandleCache {
+    std::map<int, sfm_ba_handle*> by_dev;
+    ~HandleCache() {
+      for (auto& kv : by_dev)
+        if (kv.second) sfm_ba_destroy(kv.second);
+    }
+  };
+  static thread_local HandleCache cache;
+  sfm_ba_handle*& h = cache.by_dev[dev];
   int rc = 0;
   if (!h && (rc = sfm_ba_create(dev, &h))) {
     h = nullptr;
@@ -1224,7 +1261,9 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   launch_cam_prep(d, d.cam, false, h->stream);
   launch_jacobian(d, false, h->stream, true);  // the records are the output
   if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
-  launch_reduce(d, kPCost, d.jac_blocks, 0, kCost, h->stream);
+  // the record-writing grid (jac_blocks_rec) wrote the cost partials: the
+  // record-free grid's extra slots still hold the last solve's partials
+  launch_reduce(d, kPCost, d.jac_blocks_rec, 0, kCost, h->stream);
   std::vector<double> rec(size_t(kJRec) * d.N_pad);
   if (d.N)
     HIPCHK(hipMemcpyAsync(rec.data(), d.jrec, sizeof(double) * rec.size(), hipMemcpyDeviceToHost, h->stream));

@@ -1,0 +1,162 @@
+"""GPU: the HIP solver's Levenberg-Marquardt bookkeeping against the oracle
+on trajectories that force every branch of Ceres-1.12's trust-region loop
+(tests/lm_cases.py; fixtures tests/golden/lm_branches.{json,npz}; SURVEY.md
+Appendix A items 4-6; /root/reference/CTracker.cpp:571-577, 670-702).
+
+Per case, through the C ABI (sfm_ba_solve, the one-shot drop-in):
+  * the identical accept / reject / invalid sequence, termination type,
+    iteration count and summary counters;
+  * per-iteration cost and trust-region radius, and the final parameters,
+    within max(north-star floor, 20 x the disagreement of the oracle with
+    the independent dense numpy restatement on the same trajectory) -- the
+    rejecting scenes start 1e9..1e13 above the optimum, where two correct
+    fp64 implementations already differ by up to 2e-5 mid-trajectory;
+  * gauge-invariant checks next to the raw ones: per-observation residuals
+    and Sim(3)-aligned camera centres + points (SURVEY.md §7 hard part 2).
+The gauge_* cases (every tolerance 0, radius up to the 1e16 clamp) compare
+the decisive prefix of the trajectory plus the gauge-invariant end state:
+after it the accept / reject decisions are rounding noise.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import lm_cases as L
+import sfm_amd
+from oracle import ffi as O
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIX = json.load(open(os.path.join(G, "lm_branches.json")))
+TERM = {"CONVERGENCE": 0, "NO_CONVERGENCE": 1, "FAILURE": 2}
+
+
+def seq_of(trace):
+    return "".join("I" if not it["step_is_valid"] else ("A" if it["step_is_successful"] else "R") for it in trace[1:])
+
+
+def _residuals(uv, cam_idx, pt_idx, K, rot, t, X):
+    return O.residuals_jacobians(uv, cam_idx, pt_idx, K, rot, t, X, jacobian=False)[0]
+
+
+def _solve_both(name):
+    c = FIX[name]
+    build, _, mode = L.cases()[name]
+    s = build()
+    ro, to, Xo = s.copy_params()
+    sm_o, tr_o = O.solve(s.uv, s.cam_idx, s.pt_idx, s.K, ro, to, Xo, mode=mode,
+                         options=O.default_options(**c["options"]))
+    rg, tg, Xg = s.copy_params()
+    sm_g, tr_g = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, rg, tg, Xg, mode=mode,
+                               options=sfm_amd.make_options(**c["options"]))
+    return c, s, (sm_o, tr_o, (ro, to, Xo)), (sm_g, tr_g, (rg, tg, Xg))
+
+
+def _rel(a, b, floor=1e-3):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b)) / np.maximum(np.abs(np.asarray(b)), floor)))
+
+
+@pytest.mark.parametrize("name", sorted(n for n in FIX if not n.startswith("gauge")))
+def test_branch_trajectory_matches_oracle(name):
+    c, s, (sm_o, tr_o, sol_o), (sm_g, tr_g, sol_g) = _solve_both(name)
+    # the live oracle is the fixture's (pinned on CPU by test_lm_branches_oracle)
+    assert seq_of(tr_o) == seq_of(c["trace"])
+    assert seq_of(tr_g) == seq_of(tr_o), (seq_of(tr_g), seq_of(tr_o))
+    assert sm_g.termination_type == sm_o["termination_type"]
+    assert sm_g.num_iterations == sm_o["num_iterations"]
+    assert sm_g.num_successful_steps == sm_o["num_successful_steps"]
+    assert sm_g.num_unsuccessful_steps == sm_o["num_unsuccessful_steps"]
+    assert sm_g.num_invalid_steps == sm_o["num_invalid_steps"]
+    d_np, r_np = c["numpy_cost_rel_diff"], c["numpy_radius_rel_diff"]
+    for i, (a, b) in enumerate(zip(tr_g, tr_o)):
+        tol = max(1e-9, 20 * d_np[i])
+        assert abs(a["cost"] - b["cost"]) <= tol * b["cost"], (i, a["cost"], b["cost"], tol)
+        # the radius follows rho = cost change / model change, whose relative
+        # rounding grows as the cost change shrinks: 1e-6 floor
+        tol = max(1e-6, 20 * r_np[i])
+        assert abs(a["trust_region_radius"] - b["trust_region_radius"]) <= tol * b["trust_region_radius"], \
+            (i, a["trust_region_radius"], b["trust_region_radius"])
+    assert abs(sm_g.final_cost - sm_o["final_cost"]) <= max(1e-9, 20 * d_np[-1]) * sm_o["final_cost"]
+    # raw parameters (north star: 1e-6 relative) ...
+    tol_p = max(1e-6, 20 * c["numpy_param_max_rel"])
+    for a, b in zip(sol_g, sol_o):
+        assert _rel(a, b) < tol_p
+    # ... and gauge-invariant: residuals (px) and Sim(3)-aligned structure
+    res, al = L.gauge_invariant_diff(_residuals, s, sol_g, sol_o)
+    assert res <= max(1e-6, 20 * c["numpy_residual_max_abs"]), res
+    assert al <= max(1e-6, 20 * c["numpy_aligned_max_rel"]), al
+    if sm_o["termination_type"] == TERM["FAILURE"] or seq_of(tr_o) == "":
+        # no accepted step: the parameters are the input, bit for bit
+        for a, b in zip(sol_g, s.copy_params()):
+            assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["gauge_1e15", "gauge_1e16"])
+def test_gauge_runs_agree_on_gauge_invariants(name):
+    c, s, (sm_o, tr_o, sol_o), (sm_g, tr_g, sol_g) = _solve_both(name)
+    k = L.decisive_prefix(tr_o)
+    assert seq_of(tr_g)[:k] == seq_of(tr_o)[:k]
+    # (the prefix steps are taken with D^2 = diag / 3e15: their gauge
+    # components are rounding amplified by ~1e15, so the costs after them
+    # agree only loosely; the optimum below is rounding-tight)
+    for a, b in zip(tr_g[:k + 1], tr_o[:k + 1]):
+        assert abs(a["cost"] - b["cost"]) <= 1e-3 * b["cost"]
+    # both reach the same optimum (rounding-level final costs) ...
+    assert abs(sm_g.final_cost - sm_o["final_cost"]) <= 1e-10 * sm_o["final_cost"]
+    # ... and the radius clamp where the oracle does
+    if any(it["trust_region_radius"] == 1e16 for it in tr_o):
+        assert any(it["trust_region_radius"] == 1e16 for it in tr_g)
+    res, al = L.gauge_invariant_diff(_residuals, s, sol_g, sol_o)
+    assert res <= 1e-6, res
+    assert al <= 1e-6, al
+    raw = max(_rel(a, b) for a, b in zip(sol_g, sol_o))
+    print(f"{name}: GPU {seq_of(tr_g)} / oracle {seq_of(tr_o)}; raw parameter drift {raw:.2e} "
+          f"(gauge), residuals {res:.1e} px, Sim(3)-aligned {al:.1e}")
+
+
+def test_resident_api_takes_the_same_branches():
+    """The resident handle (sfm_ba_solve_resident) on the rejecting scene and
+    on the LLT-failure scene, twice each (reset in between): same sequence as
+    the oracle, bitwise-identical repeats."""
+    for name in ("reject_a", "llt_invalid"):
+        c = FIX[name]
+        build, _, mode = L.cases()[name]
+        s = build()
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm1, tr1 = ba.solve(sfm_amd.make_options(**c["options"]), mode=mode)
+            p1 = ba.parameters()
+            ba.reset()
+            sm2, tr2 = ba.solve(sfm_amd.make_options(**c["options"]), mode=mode)
+            p2 = ba.parameters()
+        assert seq_of(tr1) == seq_of(c["trace"]) and tr1 == tr2
+        for a, b in zip(p1, p2):
+            assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("bad", [dict(min_lm_diagonal=-1.0), dict(max_lm_diagonal=1e-9),
+                                 dict(min_trust_region_radius=2e4), dict(initial_trust_region_radius=0.0),
+                                 dict(function_tolerance=-1.0), dict(max_num_iterations=-1)])
+def test_device_refuses_invalid_options(bad):
+    s = L.reject_scene("reject_a")
+    r, t, X = s.copy_params()
+    with pytest.raises(sfm_amd.SfmError, match="invalid option"):
+        sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X, options=sfm_amd.make_options(**bad))
+
+
+def test_evaluate_after_solve_reports_the_current_cost():
+    """evaluate() after a solve must reduce only the partials its
+    own (record-writing) grid wrote."""
+    from sfm_amd import scene
+    s = scene.config("C2")
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        ba.solve()
+        cost, res, _ = ba.evaluate(want_jacobian=False)
+        rot, t, X = ba.parameters()
+    assert abs(cost - 0.5 * np.sum(res ** 2)) <= 1e-10 * cost
+    r_o = _residuals(s.uv, s.cam_idx, s.pt_idx, s.K, rot, t, X)
+    assert abs(cost - 0.5 * np.sum(r_o ** 2)) <= 1e-10 * cost
