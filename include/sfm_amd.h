@@ -194,6 +194,52 @@ int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uin
                      int32_t desc_bytes, int32_t* best_idx, int32_t* best_dist, int32_t* second_idx,
                      int32_t* second_dist);
 
+/* ---- Frame-resident descriptor matcher --------
+ * The per-frame hot loop of CSfM::tracking matches the previous frame's
+ * keypoint subset against the current frame's (CTracker::matchFeatures(
+ * prevIdx, currIdx, prevMatchIdx, currMatchIdx), CTracker.h:57,
+ * CTracker.cpp:368-417, called at CSfM.cpp:518).  A matcher keeps the last
+ * two frames' keypoints + descriptors resident in HBM (one upload per
+ * frame), pools its buffers, and runs each call as one stream of launches
+ * with one host sync.  Rules of every overload: 2-NN Hamming (ties to the
+ * lower train index), accept iff d^2 > min^2 && d^2 < max^2 &&
+ * float(d0)/float(d1) < ratio && (train unmatched || d0 < its best), a
+ * better query replaces the slot's query; fewer than 2 train rows -> no
+ * matches (the reference reads matches[i][1] out of range). */
+typedef struct sfm_matcher sfm_matcher;
+int sfm_matcher_create(int32_t device, int32_t desc_bytes, sfm_matcher** out);
+int sfm_matcher_destroy(sfm_matcher* h);
+/* New current frame: pts [n][2] undistorted (CFrame::_pts, what getPointsAt
+ * returns), pts_distorted [n][2] (CFrame::getPointsDistorted; NULL = pts),
+ * desc [n][desc_bytes]; the old current frame becomes the previous one
+ * (_prevFrame = _currFrame, CSfM.cpp:626-629). */
+int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_distorted, const uint8_t* desc,
+                           int32_t n);
+/* CTracker::matchFeatures(prevFrameIdx, currFrameIdx, prevMatchIdx,
+ * currMatchIdx) (CTracker.cpp:368-417): the keypoint subsets prev_idx of
+ * the previous and curr_idx of the current frame, undistorted positions,
+ * frame-global indices out (capacity >= min(n_prev, n_curr)).  The
+ * reference uses (ratio, min, max) = (0.8, 1.5, 40) (CTracker.cpp:27-31). */
+int sfm_matcher_match_subset(sfm_matcher* h, const int32_t* prev_idx, int32_t n_prev, const int32_t* curr_idx,
+                             int32_t n_curr, double ratio_test, double min_distance, double max_distance,
+                             int32_t* prev_match, int32_t* curr_match, int32_t* n_matches);
+/* bool CTracker::matchFeatures() (CTracker.cpp:419-477): the two whole
+ * frames, DISTORTED positions when distorted != 0 (CTracker.cpp:429-430);
+ * fills _prevIdx/_currIdx; the reference's bool is n >= _minFeatures. */
+int sfm_matcher_match_frames(sfm_matcher* h, int32_t distorted, double ratio_test, double min_distance,
+                             double max_distance, int32_t* prev_idx, int32_t* curr_idx, int32_t* n_matches);
+/* The (pts0, desc0, pts1, desc1, idx0, idx1[, min, max]) overloads
+ * (CTracker.cpp:114-149, 211-250) on host arrays through the handle's pooled
+ * buffers (map-point re-finding, CSfM.cpp:208-210, 673). */
+int sfm_matcher_match(sfm_matcher* h, const double* pts0, const uint8_t* desc0, int32_t n0, const double* pts1,
+                      const uint8_t* desc1, int32_t n1, double ratio_test, double min_distance, double max_distance,
+                      int32_t* idx0, int32_t* idx1, int32_t* n_matches);
+/* The 2-NN search alone on host arrays. */
+int sfm_matcher_knn2(sfm_matcher* h, const uint8_t* desc0, int32_t n0, const uint8_t* desc1, int32_t n1,
+                     int32_t* best_idx, int32_t* best_dist, int32_t* second_idx, int32_t* second_dist);
+/* Device time (ms, HIP events) of the last match: [2-NN search, whole call on the device]. */
+int sfm_matcher_last_time(sfm_matcher* h, double* ms2);
+
 /* CMap::getRepresentativeDescriptors (CMap.cpp:345-381),
  * the map-point descriptors matched at CSfM.cpp:673 and :208-210.  Point i
  * owns rows [row_off[i], row_off[i+1]) of desc [rows][desc_bytes] (one per

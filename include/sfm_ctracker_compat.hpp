@@ -25,6 +25,7 @@
 #ifndef SFM_CTRACKER_COMPAT_HPP_
 #define SFM_CTRACKER_COMPAT_HPP_
 
+#include <algorithm>
 #include <cstdint>
 #include <unordered_map>
 #include <vector>
@@ -138,6 +139,125 @@ inline int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, 
   matchIdx1.insert(matchIdx1.end(), i1.begin(), i1.begin() + nm);
   return SFM_OK;
 }
+
+// Frame-resident matcher: drop-ins for the per-frame matchFeatures
+// overloads.  CTracker keeps _prevFrame / _currFrame (CTracker.h:80-81); the
+// shim keeps the same two frames' keypoints + descriptors resident on the
+// device.  After CFrame::setKeyPoints of a new frame (CTracker.cpp:275-287):
+//   matcher.pushFrame(frame.getPoints(), frame.getPointsDistorted(), frame.getDescriptors());
+// then, in place of the reference's bodies,
+//   _tracker.matchFeatures(prev2DIdx, curr2DIdx, prevMatch2DIdx, currMatch2DIdx);   (CSfM.cpp:518)
+//     -> matcher.matchFeatures(prev2DIdx, curr2DIdx, prevMatch2DIdx, currMatch2DIdx);
+//   bool ok = _tracker.matchFeatures();                                                (CSfM.cpp:823)
+//     -> bool ok = matcher.matchFeatures(_prevIdx, _currIdx, _minFeatures);
+// (the _prevMatch/_currMatch point lists stay the caller's getPointsAt
+// gathers, CTracker.cpp:470-471).  Point2 needs .x/.y; DescMat .rows /
+// .cols / .data (cv::Mat of CV_8U, continuous).
+class FeatureMatcher {
+ public:
+  explicit FeatureMatcher(int32_t descBytes = 64, int32_t device = 0, double ratioTest = 0.8,
+                          double minMatchDistance = 1.5, double maxMatchDistance = 40.0)
+      : ratio_(ratioTest), min_(minMatchDistance), max_(maxMatchDistance) {
+    rc_ = sfm_matcher_create(device, descBytes, &h_);
+  }
+  ~FeatureMatcher() {
+    if (h_) sfm_matcher_destroy(h_);
+  }
+  FeatureMatcher(const FeatureMatcher&) = delete;
+  FeatureMatcher& operator=(const FeatureMatcher&) = delete;
+  int status() const { return rc_; }
+
+  // The new current frame (the previous current frame becomes the previous one).
+  template <class Point2, class DescMat>
+  int pushFrame(const std::vector<Point2>& pts, const std::vector<Point2>& ptsDistorted, const DescMat& desc) {
+    if (!h_) return rc_;
+    const int32_t n = int32_t(pts.size());
+    if (int32_t(ptsDistorted.size()) != n || int32_t(desc.rows) != n) return SFM_EINVAL;
+    std::vector<double> p(2 * size_t(n)), d(2 * size_t(n));
+    for (int32_t i = 0; i < n; ++i) {
+      p[2 * i] = pts[i].x; p[2 * i + 1] = pts[i].y;
+      d[2 * i] = ptsDistorted[i].x; d[2 * i + 1] = ptsDistorted[i].y;
+    }
+    n_[0] = n_[1];
+    n_[1] = n;
+    return sfm_matcher_push_frame(h_, p.data(), d.data(), static_cast<const uint8_t*>(desc.data), n);
+  }
+
+  // void CTracker::matchFeatures(const vector<int>& prevFrameIdx, const
+  // vector<int>& currFrameIdx, vector<int>& prevMatchIdx, vector<int>&
+  // currMatchIdx) (CTracker.h:57, CTracker.cpp:368-417): appends
+  // frame-global indices (push_back, :406-407).  Returns the ABI code.
+  int matchFeatures(const std::vector<int>& prevFrameIdx, const std::vector<int>& currFrameIdx,
+                    std::vector<int>& prevMatchIdx, std::vector<int>& currMatchIdx) {
+    if (!h_) return rc_;
+    const size_t cap = std::max<size_t>(1, std::min(prevFrameIdx.size(), currFrameIdx.size()));
+    std::vector<int32_t> a(cap), b(cap);
+    int32_t nm = 0;
+    const int rc = sfm_matcher_match_subset(h_, prevFrameIdx.data(), int32_t(prevFrameIdx.size()),
+                                            currFrameIdx.data(), int32_t(currFrameIdx.size()), ratio_, min_, max_,
+                                            a.data(), b.data(), &nm);
+    if (rc) return rc;
+    prevMatchIdx.insert(prevMatchIdx.end(), a.begin(), a.begin() + nm);
+    currMatchIdx.insert(currMatchIdx.end(), b.begin(), b.begin() + nm);
+    return SFM_OK;
+  }
+
+  // bool CTracker::matchFeatures() (CTracker.h:59, CTracker.cpp:419-477):
+  // clears and fills _prevIdx / _currIdx from the two whole frames on their
+  // distorted positions; returns matchCount >= minFeatures.
+  bool matchFeatures(std::vector<int>& prevIdx, std::vector<int>& currIdx, int minFeatures = 5,
+                     int* rc_out = nullptr) {
+    prevIdx.clear();
+    currIdx.clear();
+    int rc = rc_;
+    if (h_) {
+      const size_t cap = std::max<size_t>(1, size_t(std::min(n_[0], n_[1])));
+      std::vector<int32_t> a(cap), b(cap);
+      int32_t nm = 0;
+      rc = sfm_matcher_match_frames(h_, 1, ratio_, min_, max_, a.data(), b.data(), &nm);
+      if (rc == SFM_OK) {
+        prevIdx.assign(a.begin(), a.begin() + nm);
+        currIdx.assign(b.begin(), b.begin() + nm);
+      }
+    }
+    if (rc_out) *rc_out = rc;
+    return rc == SFM_OK && int(prevIdx.size()) >= minFeatures;
+  }
+
+  // The (pts0, desc0, pts1, desc1, idx0, idx1[, minDistance, maxDistance])
+  // overloads (CTracker.cpp:114-149, 211-250) through the pooled handle.
+  template <class Point2, class DescMat>
+  int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, const std::vector<Point2>& pts1,
+                    const DescMat& desc1, std::vector<int>& matchIdx0, std::vector<int>& matchIdx1,
+                    double minDistance, double maxDistance) {
+    if (!h_) return rc_;
+    const int32_t n0 = int32_t(pts0.size()), n1 = int32_t(pts1.size());
+    std::vector<double> p0(2 * size_t(n0)), p1(2 * size_t(n1));
+    for (int32_t i = 0; i < n0; ++i) { p0[2 * i] = pts0[i].x; p0[2 * i + 1] = pts0[i].y; }
+    for (int32_t i = 0; i < n1; ++i) { p1[2 * i] = pts1[i].x; p1[2 * i + 1] = pts1[i].y; }
+    const size_t cap = std::max<size_t>(1, size_t(std::min(n0, n1)));
+    std::vector<int32_t> a(cap), b(cap);
+    int32_t nm = 0;
+    const int rc = sfm_matcher_match(h_, p0.data(), static_cast<const uint8_t*>(desc0.data), n0, p1.data(),
+                                     static_cast<const uint8_t*>(desc1.data), n1, ratio_, minDistance, maxDistance,
+                                     a.data(), b.data(), &nm);
+    if (rc) return rc;
+    matchIdx0.insert(matchIdx0.end(), a.begin(), a.begin() + nm);
+    matchIdx1.insert(matchIdx1.end(), b.begin(), b.begin() + nm);
+    return SFM_OK;
+  }
+  template <class Point2, class DescMat>
+  int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, const std::vector<Point2>& pts1,
+                    const DescMat& desc1, std::vector<int>& matchIdx0, std::vector<int>& matchIdx1) {
+    return matchFeatures(pts0, desc0, pts1, desc1, matchIdx0, matchIdx1, min_, max_);
+  }
+
+ private:
+  sfm_matcher* h_ = nullptr;
+  int rc_ = SFM_OK;
+  double ratio_, min_, max_;
+  int32_t n_[2] = {0, 0};
+};
 
 // Drop-in for CTracker::computeOpticalFlow (CTracker.h:60,
 // CTracker.cpp:480-562).  The reference reads its member frames

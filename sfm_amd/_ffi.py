@@ -137,6 +137,18 @@ _SIGNATURES = {
                                    c_double, c_double, c_double, c_void_p, c_void_p, POINTER(c_int32)]),
     "sfm_knn2_hamming": (c_int, [c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
+    "sfm_matcher_create": (c_int, [c_int32, c_int32, POINTER(c_void_p)]),
+    "sfm_matcher_destroy": (c_int, [c_void_p]),
+    "sfm_matcher_push_frame": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
+    "sfm_matcher_match_subset": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_double, c_double, c_double,
+                                         c_void_p, c_void_p, POINTER(c_int32)]),
+    "sfm_matcher_match_frames": (c_int, [c_void_p, c_int32, c_double, c_double, c_double, c_void_p, c_void_p,
+                                         POINTER(c_int32)]),
+    "sfm_matcher_match": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_double,
+                                  c_double, c_double, c_void_p, c_void_p, POINTER(c_int32)]),
+    "sfm_matcher_knn2": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
+    "sfm_matcher_last_time": (c_int, [c_void_p, c_void_p]),
     "sfm_representative_descriptors": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
                                     POINTER(c_int32)]),

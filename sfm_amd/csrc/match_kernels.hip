@@ -1,23 +1,38 @@
-// Per-frame descriptor matcher for gfx950: brute-force Hamming 2-NN
-// (replaces the external brisk::BruteForceMatcher::knnMatch, k = 2, called
-// at /root/reference/CTracker.cpp:117, 214, 381, 433) and a parallel
-// restatement of the reference's sequential acceptance loop
-// (CTracker.cpp:221-249, identical at :122-148, :390-416, :441-467):
+// Per-frame descriptor matcher for gfx950.
+//
+// Replaces brisk::BruteForceMatcher::knnMatch(k = 2) (called at
+// /root/reference/CTracker.cpp:117, 214, 381, 433) and the reference's
+// sequential acceptance loop, identical in all four matchFeatures overloads
+// (CTracker.cpp:122-148, 221-249, 390-416, 441-467):
 //
 //   for i in queries (in order):
 //     accept if d^2 > min^2 && d^2 < max^2 && float(d0)/float(d1) < ratio
 //            && (train j0 unmatched || d0 < bestDist[j0])
 //     new j0 -> append (i, j0); better -> overwrite the query at j0's slot
 //
-// Equivalent order-free form (proved in DESIGN.md §5): for each train j the
-// surviving query is the FIRST accepted query with the minimum distance, and
-// the output slots are ordered by the first accepted query of each j.  Both
-// are integer min-reductions (atomicMin on packed keys), so the result is
-// bit-exact and independent of scheduling.  Ties inside the 2-NN search go
-// to the lower train index (the oracle's restated knnMatch convention).
+// Order-free form: for each train j the surviving query is the
+// FIRST accepted query with the minimum distance, and the output slots are
+// ordered by the first accepted query of each j -- integer min-reductions
+// (atomicMin on packed keys), bit-exact and independent of scheduling.  2-NN
+// ties go to the lower train index (the restated knnMatch convention): the
+// search keeps the two smallest (distance << 32 | train) keys, so the scan
+// order of the train rows does not matter and the rows can be split across
+// workgroups and waves.
+//
+// Hot-path layout: an sfm_matcher handle keeps the last two frames'
+// keypoints and descriptors resident in HBM (one upload per frame, the
+// _prevFrame = _currFrame swap of CSfM.cpp:626-629), pools every device and
+// pinned buffer (no allocation per call) and runs a call as one stream of
+// launches with one host sync.  The 2-NN search is a 2-D grid (64 queries x
+// a train slice per workgroup, four waves each scanning a quarter of the
+// slice), so a 2k x 2k frame pair fills the chip; train rows are
+// wave-uniform 64-B scalar loads, the query lives in VGPRs.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <cmath>
+#include <map>
 #include <string>
 #include <vector>
 #include "../../include/sfm_amd.h"
@@ -27,106 +42,162 @@ void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
 
 namespace {
 
-thread_local std::string g_merr;
-
-constexpr int kQ = 64;        // queries per workgroup (one per lane)
-constexpr int kTrainTile = 256;
-
-// One lane per query; train descriptors streamed through LDS in tiles.
-// Descriptors are handled as 64-bit words; desc_bytes must be a multiple of 8
-// (BRISK: 64 bytes) — other widths are zero-padded on the host.
-template <int W>
-__global__ __launch_bounds__(kQ) void k_knn2(const uint64_t* __restrict__ d0, int n0, const uint64_t* __restrict__ d1,
-                                             int n1, int* __restrict__ bi, int* __restrict__ bd,
-                                             int* __restrict__ si, int* __restrict__ sd) {
-  __shared__ uint64_t tile[kTrainTile * W];
-  const int i = blockIdx.x * kQ + threadIdx.x;
-  uint64_t q[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) q[w] = (i < n0) ? d0[size_t(i) * W + w] : 0ull;
-  int b0 = 1 << 30, j0 = -1, b1 = 1 << 30, j1 = -1;
-  for (int t0 = 0; t0 < n1; t0 += kTrainTile) {
-    const int nt = min(kTrainTile, n1 - t0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < nt * W; e += kQ) tile[e] = d1[size_t(t0) * W + e];
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      int d = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) d += __popcll(q[w] ^ tile[t * W + w]);
-      const int j = t0 + t;
-      if (d < b0) { b1 = b0; j1 = j0; b0 = d; j0 = j; }
-      else if (d < b1) { b1 = d; j1 = j; }
-    }
-  }
-  if (i < n0) { bi[i] = j0; bd[i] = b0; si[i] = j1; sd[i] = b1; }
-}
-
-// Acceptance test per query + per-train min-reductions:
-//   key[j]   = min over accepted queries of (d0 << 32 | i)  -> surviving query
-//   first[j] = min over accepted queries of i               -> slot order
-__global__ void k_accept(const double* __restrict__ p0, const double* __restrict__ p1, int n0,
-                         const int* __restrict__ bi, const int* __restrict__ bd, const int* __restrict__ sd,
-                         double ratio_test, double minSq, double maxSq, unsigned long long* __restrict__ key,
-                         int* __restrict__ first) {
-#pragma clang fp contract(off)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n0) return;
-  const int j = bi[i];
-  if (j < 0) return;
-  const float f0 = float(bd[i]), f1 = float(sd[i]);
-  const double ratio = double(f0 / f1);
-  const double dx = p0[2 * i] - p1[2 * j], dy = p0[2 * i + 1] - p1[2 * j + 1];
-  const double d = dx * dx + dy * dy;
-  if (d > minSq && d < maxSq && ratio < ratio_test) {
-    atomicMin(&key[j], (static_cast<unsigned long long>(unsigned(bd[i])) << 32) | unsigned(i));
-    atomicMin(&first[j], i);
-  }
-}
-
-struct DevBufs {
-  std::vector<void*> ptrs;
-  ~DevBufs() { for (void* p : ptrs) hipFree(p); }
-  template <typename T>
-  T* get(size_t n) {
-    void* p = nullptr;
-    if (hipMalloc(&p, (n ? n : 1) * sizeof(T)) != hipSuccess) return nullptr;
-    ptrs.push_back(p);
-    return static_cast<T*>(p);
-  }
-};
-
 int mfail(int code, const std::string& m) {
-  g_merr = m;
   sfm_internal_set_error(m);
   return code;
 }
 
-// Pads descriptors to whole 64-bit words.
-std::vector<uint64_t> pack_words(const uint8_t* d, int n, int nbytes, int W) {
-  std::vector<uint64_t> out(size_t(n) * W, 0ull);
-  for (int i = 0; i < n; ++i) std::memcpy(&out[size_t(i) * W], d + size_t(i) * nbytes, nbytes);
-  return out;
+constexpr int kQ = 64;       // queries per workgroup (one per lane)
+constexpr int kWaves = 4;    // waves per workgroup, each a quarter of the train slice
+constexpr unsigned long long kNoKey = ~0ull;
+
+// branch-free: two compares and three selects per candidate
+__device__ __forceinline__ void top2_insert(unsigned long long k, unsigned long long& k0, unsigned long long& k1) {
+  const bool lt0 = k < k0, lt1 = k < k1;
+  k1 = lt0 ? k0 : (lt1 ? k : k1);
+  k0 = lt0 ? k : k0;
 }
 
-int run_knn(hipStream_t s, int W, const uint64_t* d0, int n0, const uint64_t* d1, int n1, int* bi, int* bd, int* si,
-            int* sd) {
-  const int grid = (n0 + kQ - 1) / kQ;
-  if (grid == 0) return 0;
-  switch (W) {
-#define CASE(w) case w: k_knn2<w><<<grid, kQ, 0, s>>>(d0, n0, d1, n1, bi, bd, si, sd); break;
-    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
-#undef CASE
-    default: return mfail(SFM_EINVAL, "descriptor width must be <= 512 bytes");
+// Partial 2-NN of query block blockIdx.x against train slice blockIdx.y.
+// Query i is row qidx[i] of q (qidx == nullptr: row i), train t is row
+// tidx[t] of tr; part[(y * n0 + i) * 2 + {0,1}] = the two smallest keys.
+template <int W, bool kIdx>
+__global__ __launch_bounds__(kQ * kWaves) void k_knn2_part(const uint64_t* __restrict__ q, const int* __restrict__ qidx,
+                                                           int n0, const uint64_t* __restrict__ tr,
+                                                           const int* __restrict__ tidx, int n1, int slice,
+                                                           unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long red[kWaves][kQ][2];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: the train loop is scalar
+  const int i = blockIdx.x * kQ + lane;
+  uint64_t x[W];
+  if (i < n0) {
+    const size_t row = qidx ? size_t(qidx[i]) : size_t(i);
+#pragma unroll
+    for (int k = 0; k < W; ++k) x[k] = q[row * W + k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < W; ++k) x[k] = 0ull;
   }
-  return 0;
+  unsigned long long k0 = kNoKey, k1 = kNoKey;
+  const int t0 = blockIdx.y * slice, t1 = min(n1, t0 + slice);
+  const int per = (t1 - t0 + kWaves - 1) / kWaves;
+  const int a = t0 + w * per, b = min(t1, a + per);
+  // four rows in flight per step (four 64-B scalar loads, then the
+  // popcounts), then the remainder
+  int t = a;
+  for (; t + 4 <= b; t += 4) {
+    const uint64_t* r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = tr + (kIdx ? size_t(tidx[t + u]) : size_t(t + u)) * W;
+    uint64_t y[4][W];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < W; ++k) y[u][k] = r[u][k];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      unsigned d = 0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) d += unsigned(__popcll(x[k] ^ y[u][k]));
+      top2_insert((static_cast<unsigned long long>(d) << 32) | unsigned(t + u), k0, k1);
+    }
+  }
+  for (; t < b; ++t) {
+    const uint64_t* r = tr + (kIdx ? size_t(tidx[t]) : size_t(t)) * W;   // wave-uniform: scalar loads
+    unsigned d = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) d += unsigned(__popcll(x[k] ^ r[k]));
+    top2_insert((static_cast<unsigned long long>(d) << 32) | unsigned(t), k0, k1);
+  }
+  red[w][lane][0] = k0;
+  red[w][lane][1] = k1;
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int v = 1; v < kWaves; ++v) {
+      top2_insert(red[v][lane][0], k0, k1);
+      top2_insert(red[v][lane][1], k0, k1);
+    }
+    if (i < n0) {
+      part[(size_t(blockIdx.y) * n0 + i) * 2] = k0;
+      part[(size_t(blockIdx.y) * n0 + i) * 2 + 1] = k1;
+    }
+  }
 }
 
+__device__ __forceinline__ void merge_parts(const unsigned long long* __restrict__ part, int n0, int nslice, int i,
+                                            unsigned long long& k0, unsigned long long& k1) {
+  k0 = kNoKey;
+  k1 = kNoKey;
+  for (int s = 0; s < nslice; ++s) {
+    top2_insert(part[(size_t(s) * n0 + i) * 2], k0, k1);
+    top2_insert(part[(size_t(s) * n0 + i) * 2 + 1], k0, k1);
+  }
+}
+
+// The 2-NN result alone (sfm_knn2_hamming): best / second train + distance.
+__global__ void k_knn2_merge(const unsigned long long* __restrict__ part, int n0, int nslice, int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n0) return;
+  unsigned long long k0, k1;
+  merge_parts(part, n0, nslice, i, k0, k1);
+  out[i] = k0 == kNoKey ? -1 : int(k0 & 0xffffffffu);
+  out[n0 + i] = k0 == kNoKey ? (1 << 30) : int(k0 >> 32);
+  out[2 * n0 + i] = k1 == kNoKey ? -1 : int(k1 & 0xffffffffu);
+  out[3 * n0 + i] = k1 == kNoKey ? (1 << 30) : int(k1 >> 32);
+}
+
+// Merge + the acceptance test of query i + the per-train min-reductions:
+//   key[j]   = min over accepted queries of (d0 << 32 | i)  -> surviving query
+//   first[j] = min over accepted queries of i               -> slot order
+// Positions are those of rows qidx[i] / tidx[j] (nullptr: i / j).
+__global__ void k_accept(const unsigned long long* __restrict__ part, int n0, int nslice,
+                         const double* __restrict__ p0, const int* __restrict__ qidx, const double* __restrict__ p1,
+                         const int* __restrict__ tidx, double ratio_test, double minSq, double maxSq,
+                         unsigned long long* __restrict__ key, int* __restrict__ first) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n0) return;
+  unsigned long long k0, k1;
+  merge_parts(part, n0, nslice, i, k0, k1);
+  if (k0 == kNoKey || k1 == kNoKey) return;  // < 2 train rows: the reference reads past matches[i] (UB)
+  const int j = int(k0 & 0xffffffffu);
+  const unsigned d0 = unsigned(k0 >> 32), d1 = unsigned(k1 >> 32);
+  // DMatch::distance is a float; the ratio is a float division stored in a double
+  const float f0 = float(d0), f1 = float(d1);
+  const double ratio = double(f0 / f1);
+  const size_t a = qidx ? size_t(qidx[i]) : size_t(i), b = tidx ? size_t(tidx[j]) : size_t(j);
+  const double dx = p0[2 * a] - p1[2 * b], dy = p0[2 * a + 1] - p1[2 * b + 1];
+  const double d = dx * dx + dy * dy;
+  if (d > minSq && d < maxSq && ratio < ratio_test) {
+    atomicMin(&key[j], (static_cast<unsigned long long>(d0) << 32) | unsigned(i));
+    atomicMin(&first[j], i);
+  }
+}
+
+__global__ void k_reset(int n1, unsigned long long* __restrict__ key, int* __restrict__ first, int n0,
+                        int* __restrict__ slot) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n1) { key[t] = kNoKey; first[t] = 0x7fffffff; }
+  if (t < n0) slot[t] = 0;
+}
+
+// Pads descriptors to whole 64-bit words (W a power of two).
 int words_for(int nbytes) {
   int W = (nbytes + 7) / 8;
   int p = 1;
   while (p < W) p <<= 1;
   return p;
+}
+
+void pack_words(const uint8_t* d, int n, int nbytes, int W, uint64_t* out) {
+  if (nbytes == 8 * W) {
+    std::memcpy(out, d, size_t(n) * nbytes);
+    return;
+  }
+  std::memset(out, 0, size_t(n) * W * 8);
+  for (int i = 0; i < n; ++i) std::memcpy(out + size_t(i) * W, d + size_t(i) * nbytes, nbytes);
 }
 
 // CMap::getRepresentativeDescriptors (CMap.cpp:345-381): one wavefront per
@@ -160,35 +231,373 @@ __global__ __launch_bounds__(64) void k_repr(const uint64_t* __restrict__ d, con
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// the handle
+
+struct MatchFrame {
+  int n = 0;
+  uint64_t* desc = nullptr;   // [n][W]
+  double* pts = nullptr;      // [n][2] undistorted (CFrame::getPointsAt)
+  double* ptsd = nullptr;     // [n][2] distorted (CFrame::getPointsDistorted)
+  size_t cap = 0;
+};
+
+struct sfm_matcher {
+  int device = 0;
+  int desc_bytes = 64, W = 8;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  MatchFrame frame[2];        // [prev, curr] after the swap
+  int cur = 1;                // index of the current frame in frame[]
+  int frames_pushed = 0;
+  // pooled scratch (grow-only)
+  std::map<std::string, std::pair<void*, size_t>> dev;
+  std::map<std::string, std::pair<void*, size_t>> pin;
+  float last_knn_ms = 0.f, last_total_ms = 0.f;
+};
+
+namespace {
+
+template <typename T>
+T* dbuf(sfm_matcher* h, const char* name, size_t count, int* rc) {
+  auto& e = h->dev[name];
+  const size_t bytes = std::max<size_t>(1, count) * sizeof(T);
+  if (e.second < bytes) {
+    if (e.first) hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    const size_t cap = std::max(bytes, size_t(4096)) * 3 / 2;
+    if (hipMalloc(&e.first, cap) != hipSuccess) {
+      *rc = mfail(SFM_ENOMEM, "hipMalloc failed (matcher scratch)");
+      return nullptr;
+    }
+    e.second = cap;
+  }
+  return static_cast<T*>(e.first);
+}
+
+template <typename T>
+T* pbuf(sfm_matcher* h, const char* name, size_t count, int* rc) {
+  auto& e = h->pin[name];
+  const size_t bytes = std::max<size_t>(1, count) * sizeof(T);
+  if (e.second < bytes) {
+    if (e.first) hipHostFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    const size_t cap = std::max(bytes, size_t(4096)) * 3 / 2;
+    if (hipHostMalloc(&e.first, cap) != hipSuccess) {
+      *rc = mfail(SFM_ENOMEM, "hipHostMalloc failed (matcher staging)");
+      return nullptr;
+    }
+    e.second = cap;
+  }
+  return static_cast<T*>(e.first);
+}
+
+// Train slices: enough workgroups to put ~8 waves on every CU, each slice
+// at least 64 rows (one row per lane-step of every wave is not worth less).
+int slices_for(const sfm_matcher* h, int n0, int n1) {
+  const int qb = (n0 + kQ - 1) / kQ;
+  const int want = std::max(1, (2 * h->n_cu + qb - 1) / qb);
+  const int most = std::max(1, n1 / 64);
+  return std::min(want, most);
+}
+
+int launch_knn(sfm_matcher* h, const uint64_t* q, const int* qidx, int n0, const uint64_t* tr, const int* tidx,
+               int n1, unsigned long long* part, int nslice) {
+  const int slice = (n1 + nslice - 1) / nslice;
+  dim3 grid((n0 + kQ - 1) / kQ, nslice);
+  switch (h->W) {
+#define CASE(w)                                                                                       \
+  case w:                                                                                             \
+    if (tidx) k_knn2_part<w, true><<<grid, kQ * kWaves, 0, h->stream>>>(q, qidx, n0, tr, tidx, n1, slice, part); \
+    else k_knn2_part<w, false><<<grid, kQ * kWaves, 0, h->stream>>>(q, qidx, n0, tr, tidx, n1, slice, part);     \
+    break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
+#undef CASE
+    default: return mfail(SFM_EINVAL, "descriptor width must be <= 512 bytes");
+  }
+  return 0;
+}
+
+// One match: queries (q, qidx, p0) against trains (tr, tidx, p1) already on
+// the device; results (query, train) in subset-local indices into the pinned
+// buffer `res` ([2 * n0 + 1]: idx0 | idx1 | count) after the stream sync.
+int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
+              const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** res_out) {
+  int rc = 0;
+  const int nslice = slices_for(h, n0, n1);
+  auto* part = dbuf<unsigned long long>(h, "part", 2 * size_t(n0) * nslice, &rc);
+  auto* key = dbuf<unsigned long long>(h, "key", size_t(n1), &rc);
+  int* first = dbuf<int>(h, "first", size_t(n1), &rc);
+  int* slot = dbuf<int>(h, "slot", size_t(n0), &rc);
+  int* out = dbuf<int>(h, "out", 2 * size_t(n0) + 1, &rc);
+  int* res = pbuf<int>(h, "res", 2 * size_t(n0) + 1, &rc);
+  if (rc) return rc;
+  hipStream_t s = h->stream;
+  hipEventRecord(h->ev[0], s);
+  k_reset<<<(std::max(n0, n1) + 255) / 256, 256, 0, s>>>(n1, key, first, n0, slot);
+  if ((rc = launch_knn(h, q, qidx, n0, tr, tidx, n1, part, nslice))) return rc;
+  hipEventRecord(h->ev[1], s);
+  k_accept<<<(n0 + 255) / 256, 256, 0, s>>>(part, n0, nslice, p0, qidx, p1, tidx, ratio, mn * mn, mx * mx, key, first);
+  sfm::k_mark_first<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
+  sfm::k_compact_slots<false><<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
+  hipEventRecord(h->ev[2], s);
+  hipMemcpyAsync(res, out, (2 * size_t(n0) + 1) * sizeof(int), hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return mfail(SFM_EIO, "matcher kernels failed");
+  hipEventElapsedTime(&h->last_knn_ms, h->ev[0], h->ev[1]);
+  hipEventElapsedTime(&h->last_total_ms, h->ev[0], h->ev[2]);
+  *res_out = res;
+  return 0;
+}
+
+bool ok_ratio_window(double ratio, double mn, double mx) {
+  return std::isfinite(ratio) && std::isfinite(mn) && std::isfinite(mx);
+}
+
+}  // namespace
+
 extern "C" {
 
-const char* sfm_match_last_error(void) { return g_merr.c_str(); }
+int sfm_matcher_create(int32_t device, int32_t desc_bytes, sfm_matcher** out) {
+  if (!out) return mfail(SFM_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (desc_bytes <= 0 || desc_bytes > 512) return mfail(SFM_EINVAL, "desc_bytes must be in 1..512");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return mfail(SFM_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n) return mfail(SFM_EINVAL, "device ordinal out of range");
+  if (hipSetDevice(device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  auto* h = new sfm_matcher();
+  h->device = device;
+  h->desc_bytes = desc_bytes;
+  h->W = words_for(desc_bytes);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    h->n_cu = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return mfail(SFM_EIO, "hipStreamCreate failed");
+  }
+  for (auto& e : h->ev) hipEventCreate(&e);
+  *out = h;
+  return 0;
+}
+
+int sfm_matcher_destroy(sfm_matcher* h) {
+  if (!h) return 0;
+  hipSetDevice(h->device);
+  hipStreamSynchronize(h->stream);
+  for (auto& f : h->frame) {
+    hipFree(f.desc);
+    hipFree(f.pts);
+    hipFree(f.ptsd);
+  }
+  for (auto& kv : h->dev) hipFree(kv.second.first);
+  for (auto& kv : h->pin) hipHostFree(kv.second.first);
+  for (auto e : h->ev) hipEventDestroy(e);
+  hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_distorted, const uint8_t* desc,
+                           int32_t n) {
+  if (!h) return mfail(SFM_EINVAL, "handle is NULL");
+  if (n < 0 || (n > 0 && (!pts || !desc))) return mfail(SFM_EINVAL, "bad frame arguments");
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  // the current frame becomes the previous one (CSfM.cpp:626-629)
+  h->cur ^= 1;
+  MatchFrame& f = h->frame[h->cur];
+  int rc = 0;
+  if (f.cap < size_t(std::max(n, 1))) {
+    hipStreamSynchronize(h->stream);
+    hipFree(f.desc); hipFree(f.pts); hipFree(f.ptsd);
+    f.desc = nullptr; f.pts = f.ptsd = nullptr;
+    f.cap = size_t(std::max(n, 1024)) * 3 / 2;
+    if (hipMalloc(&f.desc, f.cap * h->W * 8) != hipSuccess || hipMalloc(&f.pts, f.cap * 16) != hipSuccess ||
+        hipMalloc(&f.ptsd, f.cap * 16) != hipSuccess) {
+      f.cap = 0;
+      return mfail(SFM_ENOMEM, "hipMalloc failed (matcher frame)");
+    }
+  }
+  f.n = n;
+  if (n) {
+    // staging: one pinned block per frame slot (the previous upload from it
+    // may still be in flight only for the other slot)
+    const char* nm = h->cur ? "stage1" : "stage0";
+    const size_t words = size_t(n) * h->W;
+    auto* st = pbuf<uint64_t>(h, nm, words + 4 * size_t(n), &rc);
+    if (rc) return rc;
+    hipStreamSynchronize(h->stream);   // the stage may feed an earlier copy
+    pack_words(desc, n, h->desc_bytes, h->W, st);
+    double* sp = reinterpret_cast<double*>(st + words);
+    std::memcpy(sp, pts, 16 * size_t(n));
+    std::memcpy(sp + 2 * size_t(n), pts_distorted ? pts_distorted : pts, 16 * size_t(n));
+    hipMemcpyAsync(f.desc, st, words * 8, hipMemcpyHostToDevice, h->stream);
+    hipMemcpyAsync(f.pts, sp, 16 * size_t(n), hipMemcpyHostToDevice, h->stream);
+    hipMemcpyAsync(f.ptsd, sp + 2 * size_t(n), 16 * size_t(n), hipMemcpyHostToDevice, h->stream);
+  }
+  ++h->frames_pushed;
+  return 0;
+}
+
+int sfm_matcher_match_subset(sfm_matcher* h, const int32_t* prev_idx, int32_t n_prev, const int32_t* curr_idx,
+                             int32_t n_curr, double ratio_test, double min_distance, double max_distance,
+                             int32_t* prev_match, int32_t* curr_match, int32_t* n_matches) {
+  if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
+  *n_matches = 0;
+  if (h->frames_pushed < 2) return mfail(SFM_EINVAL, "push the previous and the current frame first");
+  if (n_prev < 0 || n_curr < 0 || (n_prev && !prev_idx) || (n_curr && !curr_idx))
+    return mfail(SFM_EINVAL, "bad index lists");
+  if (!ok_ratio_window(ratio_test, min_distance, max_distance)) return mfail(SFM_EINVAL, "non-finite threshold");
+  const MatchFrame& fp = h->frame[h->cur ^ 1];
+  const MatchFrame& fc = h->frame[h->cur];
+  for (int32_t i = 0; i < n_prev; ++i)
+    if (prev_idx[i] < 0 || prev_idx[i] >= fp.n) return mfail(SFM_EINVAL, "prev index out of range");
+  for (int32_t i = 0; i < n_curr; ++i)
+    if (curr_idx[i] < 0 || curr_idx[i] >= fc.n) return mfail(SFM_EINVAL, "curr index out of range");
+  if (n_prev == 0 || n_curr < 2) return 0;  // reference UB with < 2 train rows: no matches
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int rc = 0;
+  int* ix = pbuf<int>(h, "idx", size_t(n_prev) + n_curr, &rc);
+  int* dix = dbuf<int>(h, "didx", size_t(n_prev) + n_curr, &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);
+  std::memcpy(ix, prev_idx, sizeof(int) * size_t(n_prev));
+  std::memcpy(ix + n_prev, curr_idx, sizeof(int) * size_t(n_curr));
+  hipMemcpyAsync(dix, ix, sizeof(int) * (size_t(n_prev) + n_curr), hipMemcpyHostToDevice, h->stream);
+  int* res = nullptr;
+  // undistorted positions (CFrame::getPointsAt, CTracker.cpp:375-376)
+  if ((rc = run_match(h, fp.desc, dix, fp.pts, n_prev, fc.desc, dix + n_prev, fc.pts, n_curr, ratio_test,
+                      min_distance, max_distance, &res)))
+    return rc;
+  const int m = res[2 * n_prev];
+  // frame-global indices (CTracker.cpp:406-407, 412)
+  for (int k = 0; k < m; ++k) {
+    prev_match[k] = prev_idx[res[k]];
+    curr_match[k] = curr_idx[res[n_prev + k]];
+  }
+  *n_matches = m;
+  return 0;
+}
+
+int sfm_matcher_match_frames(sfm_matcher* h, int32_t distorted, double ratio_test, double min_distance,
+                             double max_distance, int32_t* prev_idx, int32_t* curr_idx, int32_t* n_matches) {
+  if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
+  *n_matches = 0;
+  if (h->frames_pushed < 2) return mfail(SFM_EINVAL, "push the previous and the current frame first");
+  if (!ok_ratio_window(ratio_test, min_distance, max_distance)) return mfail(SFM_EINVAL, "non-finite threshold");
+  const MatchFrame& fp = h->frame[h->cur ^ 1];
+  const MatchFrame& fc = h->frame[h->cur];
+  if (fp.n == 0 || fc.n < 2) return 0;
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int* res = nullptr;
+  int rc = run_match(h, fp.desc, nullptr, distorted ? fp.ptsd : fp.pts, fp.n, fc.desc, nullptr,
+                     distorted ? fc.ptsd : fc.pts, fc.n, ratio_test, min_distance, max_distance, &res);
+  if (rc) return rc;
+  const int m = res[2 * fp.n];
+  std::memcpy(prev_idx, res, sizeof(int) * size_t(m));
+  std::memcpy(curr_idx, res + fp.n, sizeof(int) * size_t(m));
+  *n_matches = m;
+  return 0;
+}
+
+int sfm_matcher_match(sfm_matcher* h, const double* pts0, const uint8_t* desc0, int32_t n0, const double* pts1,
+                      const uint8_t* desc1, int32_t n1, double ratio_test, double min_distance, double max_distance,
+                      int32_t* idx0, int32_t* idx1, int32_t* n_matches) {
+  if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
+  *n_matches = 0;
+  if (n0 < 0 || n1 < 0) return mfail(SFM_EINVAL, "negative size");
+  if ((n0 && (!pts0 || !desc0)) || (n1 && (!pts1 || !desc1))) return mfail(SFM_EINVAL, "NULL array");
+  if (!ok_ratio_window(ratio_test, min_distance, max_distance)) return mfail(SFM_EINVAL, "non-finite threshold");
+  if (n0 == 0 || n1 < 2) return 0;  // reference UB with < 2 train rows: no matches
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int rc = 0;
+  const size_t w0 = size_t(n0) * h->W, w1 = size_t(n1) * h->W;
+  auto* st = pbuf<uint64_t>(h, "in", w0 + w1 + 2 * (size_t(n0) + n1), &rc);
+  auto* d = dbuf<uint64_t>(h, "din", w0 + w1 + 2 * (size_t(n0) + n1), &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);
+  pack_words(desc0, n0, h->desc_bytes, h->W, st);
+  pack_words(desc1, n1, h->desc_bytes, h->W, st + w0);
+  double* sp = reinterpret_cast<double*>(st + w0 + w1);
+  std::memcpy(sp, pts0, 16 * size_t(n0));
+  std::memcpy(sp + 2 * size_t(n0), pts1, 16 * size_t(n1));
+  hipMemcpyAsync(d, st, (w0 + w1 + 2 * (size_t(n0) + n1)) * 8, hipMemcpyHostToDevice, h->stream);
+  const double* dp = reinterpret_cast<const double*>(d + w0 + w1);
+  int* res = nullptr;
+  if ((rc = run_match(h, d, nullptr, dp, n0, d + w0, nullptr, dp + 2 * size_t(n0), n1, ratio_test, min_distance,
+                      max_distance, &res)))
+    return rc;
+  const int m = res[2 * n0];
+  std::memcpy(idx0, res, sizeof(int) * size_t(m));
+  std::memcpy(idx1, res + n0, sizeof(int) * size_t(m));
+  *n_matches = m;
+  return 0;
+}
+
+int sfm_matcher_knn2(sfm_matcher* h, const uint8_t* desc0, int32_t n0, const uint8_t* desc1, int32_t n1,
+                     int32_t* best_idx, int32_t* best_dist, int32_t* second_idx, int32_t* second_dist) {
+  if (!h) return mfail(SFM_EINVAL, "handle is NULL");
+  if (n0 < 0 || n1 < 0 || (n0 && !desc0) || (n1 && !desc1)) return mfail(SFM_EINVAL, "bad arguments");
+  if (n0 == 0) return 0;
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int rc = 0;
+  const size_t w0 = size_t(n0) * h->W, w1 = size_t(n1) * h->W;
+  auto* st = pbuf<uint64_t>(h, "in", w0 + w1, &rc);
+  auto* d = dbuf<uint64_t>(h, "din", w0 + w1, &rc);
+  const int nslice = n1 > 0 ? slices_for(h, n0, n1) : 1;
+  auto* part = dbuf<unsigned long long>(h, "part", 2 * size_t(n0) * nslice, &rc);
+  int* out = dbuf<int>(h, "kout", 4 * size_t(n0), &rc);
+  int* res = pbuf<int>(h, "kres", 4 * size_t(n0), &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);
+  pack_words(desc0, n0, h->desc_bytes, h->W, st);
+  if (n1) pack_words(desc1, n1, h->desc_bytes, h->W, st + w0);
+  hipMemcpyAsync(d, st, (w0 + w1) * 8, hipMemcpyHostToDevice, h->stream);
+  if ((rc = launch_knn(h, d, nullptr, n0, d + w0, nullptr, n1, part, nslice))) return rc;
+  k_knn2_merge<<<(n0 + 255) / 256, 256, 0, h->stream>>>(part, n0, nslice, out);
+  hipMemcpyAsync(res, out, 4 * size_t(n0) * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return mfail(SFM_EIO, "matcher kernels failed");
+  std::memcpy(best_idx, res, n0 * sizeof(int));
+  std::memcpy(best_dist, res + n0, n0 * sizeof(int));
+  std::memcpy(second_idx, res + 2 * size_t(n0), n0 * sizeof(int));
+  std::memcpy(second_dist, res + 3 * size_t(n0), n0 * sizeof(int));
+  return 0;
+}
+
+int sfm_matcher_last_time(sfm_matcher* h, double* ms2) {
+  if (!h || !ms2) return mfail(SFM_EINVAL, "NULL argument");
+  ms2[0] = h->last_knn_ms;
+  ms2[1] = h->last_total_ms;
+  return 0;
+}
+
+// One-shot forms: a cached matcher per (device, calling thread), destroyed
+// at thread exit, so repeated calls allocate nothing.
+static sfm_matcher* cached_matcher(int32_t device, int32_t desc_bytes, int* rc) {
+  struct Cache {
+    std::map<std::pair<int, int>, sfm_matcher*> m;
+    ~Cache() {
+      for (auto& kv : m) sfm_matcher_destroy(kv.second);
+    }
+  };
+  static thread_local Cache cache;
+  sfm_matcher*& h = cache.m[{device, desc_bytes}];
+  if (!h && (*rc = sfm_matcher_create(device, desc_bytes, &h))) h = nullptr;
+  return h;
+}
 
 int sfm_knn2_hamming(int32_t device, const uint8_t* desc0, int32_t n0, const uint8_t* desc1, int32_t n1,
                      int32_t desc_bytes, int32_t* best_idx, int32_t* best_dist, int32_t* second_idx,
                      int32_t* second_dist) {
   if (n0 < 0 || n1 < 0 || desc_bytes <= 0 || desc_bytes > 512) return mfail(SFM_EINVAL, "bad sizes");
   if (n0 == 0) return 0;
-  if (hipSetDevice(device) != hipSuccess) return mfail(SFM_ENODEV, "hipSetDevice failed");
-  const int W = words_for(desc_bytes);
-  auto h0 = pack_words(desc0, n0, desc_bytes, W), h1 = pack_words(desc1, n1, desc_bytes, W);
-  DevBufs b;
-  auto* d0 = b.get<uint64_t>(h0.size());
-  auto* d1 = b.get<uint64_t>(h1.size());
-  int* r = b.get<int>(4 * size_t(n0));
-  if (!d0 || !d1 || !r) return mfail(SFM_ENOMEM, "hipMalloc failed");
-  hipMemcpy(d0, h0.data(), h0.size() * 8, hipMemcpyHostToDevice);
-  if (n1) hipMemcpy(d1, h1.data(), h1.size() * 8, hipMemcpyHostToDevice);
-  int rc = run_knn(0, W, d0, n0, d1, n1, r, r + n0, r + 2 * n0, r + 3 * n0);
-  if (rc) return rc;
-  std::vector<int> out(4 * size_t(n0));
-  if (hipMemcpy(out.data(), r, out.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-    return mfail(SFM_EIO, "kernel or copy failed");
-  std::memcpy(best_idx, out.data(), n0 * sizeof(int));
-  std::memcpy(best_dist, out.data() + n0, n0 * sizeof(int));
-  std::memcpy(second_idx, out.data() + 2 * n0, n0 * sizeof(int));
-  std::memcpy(second_dist, out.data() + 3 * n0, n0 * sizeof(int));
-  return 0;
+  int rc = 0;
+  sfm_matcher* h = cached_matcher(device, desc_bytes, &rc);
+  if (!h) return rc;
+  return sfm_matcher_knn2(h, desc0, n0, desc1, n1, best_idx, best_dist, second_idx, second_dist);
 }
 
 int sfm_match_features(int32_t device, const double* pts0, const uint8_t* desc0, int32_t n0, const double* pts1,
@@ -198,47 +607,11 @@ int sfm_match_features(int32_t device, const double* pts0, const uint8_t* desc0,
   *n_matches = 0;
   if (n0 < 0 || n1 < 0 || desc_bytes <= 0 || desc_bytes > 512) return mfail(SFM_EINVAL, "bad sizes");
   if (n0 == 0 || n1 < 2) return 0;  // reference UB with < 2 train rows: no matches
-  if (hipSetDevice(device) != hipSuccess) return mfail(SFM_ENODEV, "hipSetDevice failed");
-  const int W = words_for(desc_bytes);
-  auto h0 = pack_words(desc0, n0, desc_bytes, W), h1 = pack_words(desc1, n1, desc_bytes, W);
-  DevBufs b;
-  auto* d0 = b.get<uint64_t>(h0.size());
-  auto* d1 = b.get<uint64_t>(h1.size());
-  auto* p0 = b.get<double>(2 * size_t(n0));
-  auto* p1 = b.get<double>(2 * size_t(n1));
-  int* r = b.get<int>(4 * size_t(n0));
-  auto* key = b.get<unsigned long long>(n1);
-  int* first = b.get<int>(n1);
-  int* slot = b.get<int>(n0);
-  int* out = b.get<int>(2 * size_t(n0) + 1);
-  if (!d0 || !d1 || !p0 || !p1 || !r || !key || !first || !slot || !out) return mfail(SFM_ENOMEM, "hipMalloc failed");
-  hipStream_t s = 0;
-  hipMemcpyAsync(d0, h0.data(), h0.size() * 8, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d1, h1.data(), h1.size() * 8, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(p0, pts0, 16 * size_t(n0), hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(p1, pts1, 16 * size_t(n1), hipMemcpyHostToDevice, s);
-  hipMemsetAsync(key, 0xff, 8 * size_t(n1), s);
-  hipMemsetAsync(first, 0x7f, 4 * size_t(n1), s);  // 0x7f7f7f7f: overwritten below
-  hipMemsetAsync(slot, 0, 4 * size_t(n0), s);
-  {
-    // first[] must start at INT_MAX exactly
-    std::vector<int> inf(n1, 0x7fffffff);
-    hipMemcpyAsync(first, inf.data(), 4 * size_t(n1), hipMemcpyHostToDevice, s);
-    int rc = run_knn(s, W, d0, n0, d1, n1, r, r + n0, r + 2 * n0, r + 3 * n0);
-    if (rc) return rc;
-    const double minSq = min_distance * min_distance, maxSq = max_distance * max_distance;
-    k_accept<<<(n0 + 255) / 256, 256, 0, s>>>(p0, p1, n0, r, r + n0, r + 3 * n0, ratio_test, minSq, maxSq, key, first);
-    sfm::k_mark_first<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
-    sfm::k_compact_slots<false><<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
-    std::vector<int> host(2 * size_t(n0) + 1);
-    if (hipMemcpy(host.data(), out, host.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-      return mfail(SFM_EIO, "kernel or copy failed");
-    const int m = host[2 * n0];
-    std::memcpy(idx0, host.data(), m * sizeof(int));
-    std::memcpy(idx1, host.data() + n0, m * sizeof(int));
-    *n_matches = m;
-  }
-  return 0;
+  int rc = 0;
+  sfm_matcher* h = cached_matcher(device, desc_bytes, &rc);
+  if (!h) return rc;
+  return sfm_matcher_match(h, pts0, desc0, n0, pts1, desc1, n1, ratio_test, min_distance, max_distance, idx0, idx1,
+                           n_matches);
 }
 
 int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const int32_t* row_off, int32_t n_pts,
@@ -250,25 +623,32 @@ int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const in
   for (int32_t i = 0; i < n_pts; ++i)
     if (row_off[i + 1] <= row_off[i])
       return mfail(SFM_EINVAL, "every point needs at least one descriptor (the reference reads row -1 otherwise)");
+  int rc = 0;
+  sfm_matcher* h = cached_matcher(device, desc_bytes, &rc);
+  if (!h) return rc;
   if (hipSetDevice(device) != hipSuccess) return mfail(SFM_ENODEV, "hipSetDevice failed");
-  const int W = words_for(desc_bytes);
+  const int W = h->W;
   const int rows = row_off[n_pts];
-  auto h = pack_words(desc, rows, desc_bytes, W);
-  DevBufs b;
-  auto* d = b.get<uint64_t>(h.size());
-  int* o = b.get<int>(size_t(n_pts) + 1);
-  int* r = b.get<int>(size_t(n_pts));
-  if (!d || !o || !r) return mfail(SFM_ENOMEM, "hipMalloc failed");
-  hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice);
-  hipMemcpy(o, row_off, (size_t(n_pts) + 1) * sizeof(int), hipMemcpyHostToDevice);
+  auto* st = pbuf<uint64_t>(h, "in", size_t(rows) * W + size_t(n_pts) + 1, &rc);
+  auto* d = dbuf<uint64_t>(h, "din", size_t(rows) * W + size_t(n_pts) + 1, &rc);
+  int* r = dbuf<int>(h, "rbest", size_t(n_pts), &rc);
+  int* res = pbuf<int>(h, "rres", size_t(n_pts), &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);
+  pack_words(desc, rows, desc_bytes, W, st);
+  int* so = reinterpret_cast<int*>(st + size_t(rows) * W);
+  std::memcpy(so, row_off, (size_t(n_pts) + 1) * sizeof(int));
+  hipMemcpyAsync(d, st, (size_t(rows) * W + size_t(n_pts) + 1) * 8, hipMemcpyHostToDevice, h->stream);
+  const int* o = reinterpret_cast<const int*>(d + size_t(rows) * W);
   switch (W) {
-#define CASE(w) case w: k_repr<w><<<n_pts, 64>>>(d, o, n_pts, r); break;
+#define CASE(w) case w: k_repr<w><<<n_pts, 64, 0, h->stream>>>(d, o, n_pts, r); break;
     CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
 #undef CASE
     default: return mfail(SFM_EINVAL, "descriptor width must be <= 512 bytes");
   }
-  if (hipMemcpy(best, r, size_t(n_pts) * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-    return mfail(SFM_EIO, "kernel or copy failed");
+  hipMemcpyAsync(res, r, size_t(n_pts) * sizeof(int), hipMemcpyDeviceToHost, h->stream);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return mfail(SFM_EIO, "kernel or copy failed");
+  std::memcpy(best, res, size_t(n_pts) * sizeof(int));
   if (out)
     for (int32_t i = 0; i < n_pts; ++i)
       std::memcpy(out + size_t(i) * desc_bytes, desc + (size_t(row_off[i]) + best[i]) * desc_bytes, desc_bytes);

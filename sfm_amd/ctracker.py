@@ -6,8 +6,9 @@ behaviour) over the C ABI; OpenCV types are replaced by their memory layout
 descriptors -> uint8 [n][64]).
 
   bundleAdjustmentStructAndPose  CTracker.h:65,  CTracker.cpp:670-702
-  matchFeatures (6 overloads)    CTracker.h:50-58, CTracker.cpp:114-149,
-                                 211-250, 368-417, 419-477
+  matchFeatures (all overloads)  CTracker.h:53-58, CTracker.cpp:114-149,
+                                 211-250, 368-417, 419-477 (frame-resident
+                                 device matcher, sfm_amd/matcher.py)
   computeOpticalFlow             CTracker.h:60,  CTracker.cpp:480-562
   detectFeaturesOpticalFlow      CTracker.h:48,  CTracker.cpp:252-272
 
@@ -45,6 +46,7 @@ class CTracker:
         self._klt = None
         self._prevIdx = np.zeros(0, np.int32)
         self._currIdx = np.zeros(0, np.int32)
+        self._matcher = None
 
     # ---- bundle adjustment (CTracker.cpp:670-702) --------------------------
     def bundleAdjustmentStructAndPose(self, observations, camIdx, K, R, t, pts3D, isStructOrPose, pt_idx=None,
@@ -62,31 +64,53 @@ class CTracker:
         return sm
 
     # ---- matching --------------------------------------------------------
+    def _m(self, nbytes: int = 64):
+        from .matcher import FeatureMatcher
+        if self._matcher is None or self._matcher.desc_bytes != nbytes:
+            if self._matcher is not None:
+                self._matcher.close()
+            self._matcher = FeatureMatcher(nbytes, device=self.device)
+        return self._matcher
+
+    @staticmethod
+    def _nbytes(desc0, desc1) -> int:
+        for d in (desc0, desc1):
+            d = np.asarray(d)
+            if d.ndim == 2 and d.shape[0]:
+                return int(d.shape[1])
+        return 64
+
     def _match(self, pts0, desc0, pts1, desc1, min_d, max_d):
-        pts0 = np.ascontiguousarray(pts0, dtype=np.float64).reshape(-1, 2)
-        pts1 = np.ascontiguousarray(pts1, dtype=np.float64).reshape(-1, 2)
-        desc0 = np.ascontiguousarray(desc0, dtype=np.uint8)
-        desc1 = np.ascontiguousarray(desc1, dtype=np.uint8)
-        n0, n1 = pts0.shape[0], pts1.shape[0]
-        nb = desc0.shape[1] if desc0.ndim == 2 and n0 else (desc1.shape[1] if desc1.ndim == 2 and n1 else 64)
-        cap = max(1, min(n0, n1))
-        i0 = np.zeros(cap, np.int32)
-        i1 = np.zeros(cap, np.int32)
-        nm = c_int32(0)
-        check(lib().sfm_match_features(self.device, ptr(pts0), ptr(desc0), n0, ptr(pts1), ptr(desc1), n1, nb,
-                                       self._ratioTest, float(min_d), float(max_d), ptr(i0), ptr(i1),
-                                       ctypes.byref(nm)), "sfm_match_features")
-        m = nm.value
-        return i0[:m].copy(), i1[:m].copy()
+        return self._m(self._nbytes(desc0, desc1)).match(pts0, desc0, pts1, desc1, self._ratioTest, float(min_d),
+                                                         float(max_d))
+
+    def setKeyPoints(self, pts, desc, pts_distorted=None) -> None:
+        """The new current frame's keypoints (CFrame::setKeyPoints after
+        detectFeatures, CTracker.cpp:275-287): undistorted positions,
+        descriptors, distorted positions.  They stay resident on the device;
+        the previous current frame becomes _prevFrame (CSfM.cpp:626-629)."""
+        d = np.asarray(desc)
+        self._m(int(d.shape[1]) if d.ndim == 2 and d.shape[1] else 64).push_frame(pts, desc, pts_distorted)
 
     def matchFeatures(self, *args):
         """Overloads of CTracker::matchFeatures:
+        ()                                                 CTracker.cpp:419-477
+           the two resident frames (setKeyPoints), distorted positions;
+           fills _prevIdx/_currIdx, returns matchCount >= _minFeatures
+        (prevFrameIdx, currFrameIdx)                       CTracker.cpp:368-417
+           index subsets of the resident frames, undistorted positions;
+           returns frame-global (prevMatchIdx, currMatchIdx)
         (pts0, desc0, pts1, desc1)                         CTracker.cpp:114-149
         (pts0, desc0, pts1, desc1, minDist, maxDist)       CTracker.cpp:211-250
-        (prevPts, prevDesc, currPts, currDesc, prevIdx, currIdx)   index-subset
-           form of CTracker.cpp:368-417 (frame data passed explicitly: the
-           mirror has no CFrame); returns frame-global indices.
-        Each returns (matchIdx0, matchIdx1)."""
+        (prevPts, prevDesc, currPts, currDesc, prevIdx, currIdx)   the
+           index-subset rule on explicit frame data (no resident frames)."""
+        if len(args) == 0:
+            self._prevIdx, self._currIdx = self._m().match_frames(True, self._ratioTest, self._minMatchDistance,
+                                                                  self._maxMatchDistance)
+            return len(self._prevIdx) >= self._minFeatures
+        if len(args) == 2:
+            return self._m().match_subset(args[0], args[1], self._ratioTest, self._minMatchDistance,
+                                          self._maxMatchDistance)
         if len(args) == 4:
             return self._match(*args, self._minMatchDistance, self._maxMatchDistance)
         if len(args) == 6 and np.isscalar(args[4]):
@@ -103,13 +127,7 @@ class CTracker:
 
     def knnMatch2(self, desc0, desc1):
         """The 2-NN Hamming search alone (brisk::BruteForceMatcher::knnMatch, k=2)."""
-        desc0 = np.ascontiguousarray(desc0, dtype=np.uint8)
-        desc1 = np.ascontiguousarray(desc1, dtype=np.uint8)
-        n0, n1 = desc0.shape[0], desc1.shape[0]
-        out = [np.zeros(n0, np.int32) for _ in range(4)]
-        check(lib().sfm_knn2_hamming(self.device, ptr(desc0), n0, ptr(desc1), n1, desc0.shape[1], *map(ptr, out)),
-              "sfm_knn2_hamming")
-        return tuple(out)
+        return self._m(self._nbytes(desc0, desc1)).knn2(desc0, desc1)
 
     # ---- optical flow (CTracker.cpp:480-562) -------------------------------
     def pushFrame(self, grey) -> None:
