@@ -10,8 +10,16 @@ over a synthetic scene resident in HBM: parameters are reset on the device
 Workload per GPU: BASELINE config C3 (500 cameras, 200k points, 2M
 observations, fp64).  With N GPUs the scene has N x 200k points sharded by
 landmark (weak scaling; cameras replicated, RCCL all-reduce of the reduced
-camera system every LM iteration).  `value` = residual evaluations x
-observations (whole job) per second; LM iterations/s is reported beside it.
+camera system every LM iteration).  `value` = residual-only evaluations x
+observations (whole job) per second (the Jacobian evaluations,
+which also evaluate the residual vector, are counted separately and reported
+beside it as `jacobian_evals_per_s`); LM iterations/s is reported beside it.
+
+Also reported: the one-shot C3 wall-clock (host arrays in, problem setup +
+solve + download, sfm_ba_solve -- the reference rebuilds its ceres::Problem
+per call, CTracker.cpp:672), a measured STREAM-copy bandwidth next to the
+8 TB/s peak, the frame-resident matcher (CTracker::matchFeatures, 2k x 2k
+64-B descriptors), the C5 tracker and the keyframe-sized solve.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
    N>1:  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -36,34 +44,103 @@ SEED = 0x5F3D2017 + 3      # config C3
 
 
 def jacobian_bytes(n_obs: int, n_cams: int, n_pts: int) -> int:
-    # per observation: point index 4 + uv 16 + record 160 (r 16 + J 144)
-    # (k_jacobian); per camera: pose 48 + K 40; per point: X 24.
+    # record-writing variant (evaluate API): per observation point index 4 +
+    # uv 16 + record 160 (r 16 + J 144) (k_jacobian); per
+    # camera: pose 48 + K 40; per point: X 24.
     return 180 * n_obs + 88 * n_cams + 24 * n_pts
+
+
+def jacobian_bytes_solve(n_obs_pad: int, n_cams: int, n_pts: int) -> int:
+    # the solve's record-free pass: per (padded) observation slot point index
+    # 4 + uv 16 streamed; X read once per point (24 B); per camera pose 48 +
+    # K 40; out: 27 U_c / b_c partial sums (216 B) per 64-observation chunk.
+    return 20 * n_obs_pad + 24 * n_pts + 88 * n_cams + 216 * (n_obs_pad // 64)
+
+
+def jacobian_flops_solve(n_obs: int) -> float:
+    # per observation: rotation applied (R from the per-camera
+    # constants: 15), projection + residual (~12), the 2x9 Jacobian from the
+    # rotated point (~60), Jacobi scaling (18), U_c (21 entries x 2 rows x 2)
+    # + b_c (6 x 2 x 2) partial products (108), cost (4): ~217 fp64 flops.
+    return 217.0 * n_obs
+
+
+F64_VALU_PEAK_TFS = 78.6   # MI355X fp64 vector (MI355X_MICROARCH.md)
 
 
 def cholesky_flops(n: int) -> float:
     return n ** 3 / 3.0
 
 
-def cpu_baseline(scene) -> dict:
-    """Oracle (single-threaded C++ restatement of the reference's Ceres path)
-    on a bounded sample: one complete C3 solve on the host."""
+def host_info() -> dict:
+    """nproc / CPU model of the machine running the CPU legs (BASELINE.md
+    timing protocol)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"nproc": avail, "cpu_count": os.cpu_count(), "model": model}
+
+
+def cpu_threads() -> int:
+    """Threads for the all-cores CPU figure: the cores this process may use,
+    capped at the box's CPU share (16 per GPU on the MI355X pool)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def cpu_baseline(scene, reps: int = 3) -> dict:
+    """Oracle (the C++ restatement of the reference's Ceres path) on the same
+    C3 scene: BASELINE.md protocol -- one warm-up, then the median of `reps`
+    complete solves (problem setup included, as the reference rebuilds its
+    ceres::Problem per call), single-threaded (the reference's Ceres default
+    num_threads = 1); the all-cores OpenMP figure is timed beside it."""
     from oracle import ffi as O
-    r, t, X = scene.copy_params()
-    t0 = time.perf_counter()
-    sm, _ = O.solve(scene.uv, scene.cam_idx, scene.pt_idx, scene.K, r, t, X)
-    wall = time.perf_counter() - t0
-    evals = sm["num_residual_evaluations"]
+
+    def run(threads):
+        walls = []
+        sm = None
+        for k in range(reps + 1):
+            r, t, X = scene.copy_params()
+            t0 = time.perf_counter()
+            sm, _ = O.solve(scene.uv, scene.cam_idx, scene.pt_idx, scene.K, r, t, X, threads=threads)
+            if k > 0:
+                walls.append(time.perf_counter() - t0)
+        return float(np.median(walls)), walls, sm
+
+    wall, walls, sm = run(1)
+    res_only = sm["num_residual_evaluations"] - sm["num_jacobian_evaluations"]
+    nthr = cpu_threads()
+    wall_mt, walls_mt, _ = run(nthr)
     return {
-        "value": scene.n_obs * evals / wall,
-        "unit": "residual-evals/s (obs x evaluations)",
+        "value": scene.n_obs * res_only / wall,
+        "unit": "residual-evals/s (obs x residual-only evaluations)",
         "cores": 1,
         "kind": "port",
-        "sample": (f"one complete C3 solve ({scene.n_cams} cams / {scene.n_pts} pts / {scene.n_obs} obs): "
-                   f"{sm['num_iterations']} LM iterations, {evals} residual evaluations, {wall:.1f} s "
-                   "(oracle/ba_oracle.cpp, Ceres-1.12-equivalent restatement, 1 thread)"),
+        "sample": (f"complete C3 solves ({scene.n_cams} cams / {scene.n_pts} pts / {scene.n_obs} obs, setup "
+                   f"included): {sm['num_iterations']} LM iterations, {res_only} residual-only + "
+                   f"{sm['num_jacobian_evaluations']} Jacobian evaluations; median of {reps} after 1 warm-up: "
+                   f"{wall:.2f} s (oracle/ba_oracle.cpp, Ceres-1.12-equivalent restatement, 1 thread)"),
         "lm_iterations_per_s": sm["num_iterations"] / wall,
         "solve_s": wall,
+        "solve_s_runs": walls,
+        "all_cores": {"threads": nthr, "solve_s": wall_mt, "solve_s_runs": walls_mt,
+                      "value": scene.n_obs * res_only / wall_mt,
+                      "lm_iterations_per_s": sm["num_iterations"] / wall_mt,
+                      "note": "OpenMP oracle (Jacobian pass, Schur elimination, dense LLT in parallel)"},
+        "host": host_info(),
     }
 
 
@@ -156,6 +233,109 @@ def incremental_ba_leg(device: int, cpu: bool) -> dict:
     return out
 
 
+def oneshot_leg(sc, reps: int = 3) -> dict:
+    """One-shot C3 solve as the drop-in is called: host arrays in,
+    sfm_ba_solve (problem setup + upload + LM + download) -- the reference
+    rebuilds its ceres::Problem on every call (CTracker.cpp:672).  One
+    warm-up, then the median of `reps` (BASELINE.md timing protocol)."""
+    import sfm_amd
+    walls = []
+    sm = None
+    for k in range(reps + 1):
+        r, t, X = sc.copy_params()
+        t0 = time.perf_counter()
+        sm, _ = sfm_amd.solve(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, r, t, X)
+        if k > 0:
+            walls.append(time.perf_counter() - t0)
+    wall = float(np.median(walls))
+    return {"workload": f"C3 one-shot sfm_ba_solve ({sc.n_cams} cams / {sc.n_pts} pts / {sc.n_obs} obs): host "
+                        "arrays in, setup + upload + LM + download", "ms_per_solve": wall * 1e3,
+            "ms_runs": [w * 1e3 for w in walls], "lm_iterations": sm.num_iterations,
+            "lm_iterations_per_s": sm.num_iterations / wall}
+
+
+def stream_copy_gbs(device: int) -> float:
+    """Measured device-to-device copy bandwidth (STREAM copy: read + write
+    bytes / time) of a 4 GiB buffer, best of 5, beside the 8 TB/s spec."""
+    import torch
+    n = 1 << 29  # doubles: 4 GiB per buffer
+    a = torch.ones(n, dtype=torch.float64, device=f"cuda:{device}")
+    b = torch.empty_like(a)
+    best = 0.0
+    for _ in range(6):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = max(best, 2 * 8 * n / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del a, b
+    torch.cuda.empty_cache()
+    return best
+
+
+def matcher_leg(device: int, steps: int, cpu: bool) -> dict:
+    """The per-frame matcher of CSfM::tracking (CSfM.cpp:518 ->
+    CTracker::matchFeatures(prevIdx, currIdx, ...), CTracker.cpp:368-417):
+    2000 keypoints per frame with 64-B (512-bit) descriptors; one step =
+    push_frame (upload of the new frame's keypoints + descriptors, the
+    _prevFrame = _currFrame swap) + the 2-NN Hamming search + the ratio /
+    window / better-match-replaces rules over all keypoints of both frames.
+    Frames cycle over 3 synthetic frames (descriptors re-observed with bit
+    noise, keypoints moved a few pixels)."""
+    from sfm_amd.matcher import FeatureMatcher
+    rng = np.random.default_rng(11)
+    n = 2000
+    base_d = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    base_p = rng.uniform(0, [1280, 720], (n, 2))
+    frames = []
+    for k in range(3):
+        d = base_d.copy()
+        flips = rng.integers(0, 512, (n, 24))
+        for j in range(24):
+            d[np.arange(n), flips[:, j] // 8] ^= (1 << (flips[:, j] % 8)).astype(np.uint8)
+        p = base_p + rng.normal(0, 4, (n, 2)) + 3 * k
+        perm = rng.permutation(n)
+        frames.append((p[perm].copy(), d[perm].copy()))
+    idx = np.arange(n, dtype=np.int32)
+    m = FeatureMatcher(64, device=device)
+    m.push_frame(*frames[0])
+    warm = 5
+    knn_ms = call_ms = 0.0
+    nmatch = 0
+    for it in range(steps + warm):
+        if it == warm:
+            t0 = time.perf_counter()
+            knn_ms = call_ms = 0.0
+        m.push_frame(*frames[(it + 1) % 3])
+        a, b = m.match_subset(idx, idx)
+        nmatch = len(a)
+        k_ms, c_ms = m.last_time_ms()
+        knn_ms += k_ms
+        call_ms += c_ms
+    wall = (time.perf_counter() - t0) / steps
+    m.close()
+    pairs = n * n
+    out = {"workload": "C5 matcher: CTracker::matchFeatures(prevIdx, currIdx, ...) per frame, 2000 x 2000 keypoints, "
+                       "64-B descriptors (push_frame + 2-NN Hamming + ratio 0.8 / window (1.5, 40) / replacement)",
+           "frames_per_s": 1.0 / wall, "ms_per_frame": wall * 1e3, "matches_per_frame": nmatch,
+           "device_ms_per_frame": {"knn2": round(knn_ms / steps, 4), "match_call": round(call_ms / steps, 4)},
+           "hamming_pairs_per_s": pairs / (knn_ms / steps * 1e-3) if knn_ms > 0 else None,
+           "cpu_baseline": None}
+    if cpu:
+        from oracle import ffi as O
+        reps = 5
+        t0 = time.perf_counter()
+        for r in range(reps):
+            (p0, d0), (p1, d1) = frames[r % 3], frames[(r + 1) % 3]
+            O.match_features(p0, d0, p1, d1)
+        cw = (time.perf_counter() - t0) / reps
+        out["cpu_baseline"] = {"frames_per_s": 1.0 / cw, "ms_per_frame": cw * 1e3, "cores": 1, "kind": "port",
+                               "sample": f"{reps} frame pairs of the same match on oracle/match_oracle.cpp, 1 thread"}
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,7 +345,8 @@ def main() -> int:
     ap.add_argument("--pts-per-gpu", type=int, default=PTS_PER_GPU)
     ap.add_argument("--cams", type=int, default=CAMS)
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
-    ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker leg")
+    ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
+    ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
     ap.add_argument("--comm", action="store_true",
                     help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
     args = ap.parse_args()
@@ -236,7 +417,8 @@ def main() -> int:
 
     n_obs_total = sc.n_obs * world
     n_pts_total = P * world
-    value = n_obs_total * evals / elapsed
+    res_only = evals - jevals   # residual-only (candidate) evaluations
+    value = n_obs_total * res_only / elapsed
     jac = phases["jacobian"]
     # The solve's Jacobian pass is record-free (cost + U_c/b_c partials only;
     # the later passes recompute residuals and Jacobians), so the HBM
@@ -244,6 +426,11 @@ def main() -> int:
     # algorithmic traffic (point index, uv, 160-B record per observation) the
     # PMC traffic was collected on: timed with HIP events by bench_jacobian.
     jac_solve_ms = jac["ms"] / max(1, jac["count"])
+    cnt = np.bincount(sc.cam_idx, minlength=sc.n_cams)
+    n_pad = int(((cnt + 63) // 64 * 64).sum())   # camera-major slots, runs padded to 64
+    jac_bytes_s = jacobian_bytes_solve(n_pad, sc.n_cams, sc.n_pts)
+    jac_gbs_s = jac_bytes_s / (jac_solve_ms * 1e-3) / 1e9
+    jac_tfs_s = jacobian_flops_solve(sc.n_obs) / (jac_solve_ms * 1e-3) / 1e12
     jac_ms = ba.bench_jacobian(10)
     jac_bytes = jacobian_bytes(sc.n_obs, sc.n_cams, sc.n_pts)
     jac_gbs = jac_bytes / (jac_ms * 1e-3) / 1e9
@@ -283,12 +470,22 @@ def main() -> int:
         v = e.get("hbm_bytes_per_launch")
         return None if v is None else int(v)
 
-    roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass)", "bound": "hbm", "achieved": round(jac_gbs, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian"),
-                "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5),
-                "variant": "record-writing pass (evaluate API) timed back to back by sfm_ba_bench_jacobian "
-                           "(warm caches); the solve's record-free pass takes "
-                           f"{jac_solve_ms:.4f} ms"}
+    # the production pass of the solve (record-free): HIP events on the
+    # solver stream over the profiled pass of the same solves
+    roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass, record-free, as run inside the solve)",
+                "bound": "hbm", "achieved": round(jac_gbs_s, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(jac_gbs_s / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes": jac_bytes_s, "avg_launch_ms": round(jac_solve_ms, 5),
+                "valu": {"achieved_tflops": round(jac_tfs_s, 3), "peak_tflops": F64_VALU_PEAK_TFS,
+                         "frac": round(jac_tfs_s / F64_VALU_PEAK_TFS, 4),
+                         "algorithmic_flops": jacobian_flops_solve(sc.n_obs)},
+                "note": "neither HBM nor fp64-VALU bound: latency (wave reductions of the 27 U_c/b_c partials, "
+                        "X gathers); PMC traffic was collected on the record-writing variant only"}
+    roof_jac_rec = {"kernel": "k_jacobian (record-writing variant, evaluate API)", "bound": "hbm",
+                    "achieved": round(jac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian"),
+                    "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5),
+                    "variant": "timed back to back by sfm_ba_bench_jacobian (warm caches)"}
     roof_chol = {"kernel": "k_chol_fused (dense reduced-camera Cholesky, one persistent launch, f64 MFMA)", "bound": "mfma",
                  "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                  "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": traffic("k_chol_fused"),
@@ -316,23 +513,34 @@ def main() -> int:
             "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
         },
         "lm_iterations_per_s": iters / elapsed,
+        "jacobian_evals_per_s": n_obs_total * jevals / elapsed,
         "lm_iterations_per_solve": iters / args.steps,
-        "residual_evals_per_solve": evals / args.steps,
+        "residual_only_evals_per_solve": res_only / args.steps,
         "jacobian_evals_per_solve": jevals / args.steps,
         "final_cost": last.final_cost if last else None,
         "roofline": roofline,
         "roofline_jacobian": roof_jac,
+        "roofline_jacobian_records": roof_jac_rec,
         "roofline_cholesky": roof_chol,
         "phase_ms_per_solve": {k: round(v["ms"] / args.steps, 4) for k, v in phases.items()},
     }
+    if rank == 0 and world == 1:
+        out["stream_copy_gbs"] = round(stream_copy_gbs(local_rank), 1)
+    if rank == 0 and world == 1 and not args.no_oneshot:
+        ba.close()  # the one-shot path keeps its own cached handle
+        out["oneshot"] = oneshot_leg(sc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc)
         out["cpu_baseline"] = cpu
         out["speedup_vs_cpu"] = value / cpu["value"]
+        if "oneshot" in out:
+            out["speedup_vs_cpu_oneshot"] = cpu["solve_s"] * 1e3 / out["oneshot"]["ms_per_solve"]
+            out["speedup_vs_cpu_oneshot_all_cores"] = cpu["all_cores"]["solve_s"] * 1e3 / out["oneshot"]["ms_per_solve"]
     else:
         out["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_tracker:
         out["tracker"] = tracker_leg(local_rank, 50, not args.no_cpu_baseline)
+        out["matcher"] = matcher_leg(local_rank, 50, not args.no_cpu_baseline)
         out["incremental_ba"] = incremental_ba_leg(local_rank, not args.no_cpu_baseline)
     if args.phases and rank == 0:
         print(json.dumps(phases, indent=1), file=sys.stderr)

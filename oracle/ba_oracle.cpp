@@ -4,7 +4,7 @@
 // bench.py's cpu_baseline leg may load liboracle.so, and only as the checker
 // or the timed CPU baseline.
 //
-// What this is: a single-threaded C++ restatement of the reference's bundle
+// What this is: a C++ restatement of the reference's bundle
 // adjustment hot path, CTracker::bundleAdjustmentStructAndPose
 // (/root/reference/CTracker.cpp:670-702), including the third-party solver it
 // calls.  The reference cannot be built in this pipeline (OpenCV, Eigen,
@@ -31,6 +31,13 @@
 //     (BAStructFunctor, :638-668), 1 POSE_ONLY (BAPoseFunctor, :607-636),
 //     2 STRUCT_AND_POSE; any other value adds no residual blocks.
 //
+// Threads (oracle_set_threads, default 1 = Ceres' default num_threads, the
+// reference's setting): the per-observation / per-point / per-row work runs
+// in OpenMP loops, but every sum keeps the serial order (partitions own
+// whole output rows; reductions are serial passes over per-item results),
+// so any thread count gives bitwise the 1-thread result.  Only the timed
+// all-cores CPU figure of bench.py uses more than one.
+//
 // PARITY UNPINNED: the reference has no tests, fixtures or golden data for
 // this path and cannot be executed here, so this
 // restatement is checked only against independent restatements
@@ -47,6 +54,8 @@
 #include <vector>
 
 namespace oracle {
+
+static int g_threads = 1;
 
 // ---------------------------------------------------------------------------
 // Jet<double, N>: restates the arithmetic of ceres/jet.h (value part `a`,
@@ -205,6 +214,7 @@ static bool Cholesky(double* A, int n) {
       }
     }
     // panel: rows below, columns k0..k1 : solve X L_kk^T = A_ik
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1 && n - k1 > 256)
     for (int i = k1; i < n; ++i) {
       double* Ai = A + size_t(i) * n;
       for (int j = k0; j < k1; ++j) {
@@ -216,6 +226,7 @@ static bool Cholesky(double* A, int n) {
     }
     // trailing update A_ij -= L_ik L_jk^T (i >= j >= k1), blocked for cache
     const int w = k1 - k0;
+#pragma omp parallel for num_threads(g_threads) schedule(dynamic, 1) if (g_threads > 1 && n - k1 > 256)
     for (int ib = k1; ib < n; ib += nb) {
       const int ie = std::min(n, ib + nb);
       for (int jb = k1; jb <= ib; jb += nb) {
@@ -433,31 +444,36 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
     double s = 0; for (int i = 0; i < n; ++i) if (active[i]) s += v[i] * v[i]; return std::sqrt(s); };
 
   // ---- evaluation -------------------------------------------------------
-  std::vector<double> r(2 * N), J(18 * N), grad(n);
+  std::vector<double> r(2 * N), J(18 * N), grad(n), rtmp(2 * N);
   auto evaluate = [&](const std::vector<double>& xx, bool with_jac, double* cost_out,
                       std::vector<double>* rr) -> bool {
-    double cost = 0.0;
-    if (with_jac) std::fill(grad.begin(), grad.end(), 0.0);
+    // per-observation arithmetic (parallel when g_threads > 1), then the
+    // cost / gradient sums in the serial observation order
+    double* rb = rr ? rr->data() : rtmp.data();
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
     for (int64_t q = 0; q < N; ++q) {
       const int64_t i = pb.order[q];
       const int c = cam_idx[i], p = pt_idx[i];
       const double *Rp, *tp, *Xp;
       GetParams(pb, xx.data(), rot0.data(), t0.data(), X0.data(), c, p, Rp, tp, Xp);
-      double res[2];
+      if (with_jac)  // rows stored as [row][dR dt dX]
+        EvalJet(Rp, tp, Xp, K9 + 9 * size_t(c), obs_uv[2 * i], obs_uv[2 * i + 1], rb + 2 * q, &J[18 * q]);
+      else
+        EvalPlain(Rp, tp, Xp, K9 + 9 * size_t(c), obs_uv[2 * i], obs_uv[2 * i + 1], rb + 2 * q);
+    }
+    double cost = 0.0;
+    if (with_jac) std::fill(grad.begin(), grad.end(), 0.0);
+    for (int64_t q = 0; q < N; ++q) {
+      const double res[2] = {rb[2 * q], rb[2 * q + 1]};
       if (with_jac) {
-        double* Jq = &J[18 * q];
-        double Jrow[18];
-        EvalJet(Rp, tp, Xp, K9 + 9 * size_t(c), obs_uv[2 * i], obs_uv[2 * i + 1], res, Jrow);
-        // store rows as [row][dR dt dX]
-        std::memcpy(Jq, Jrow, sizeof(Jrow));
+        const int64_t i = pb.order[q];
+        const int c = cam_idx[i], p = pt_idx[i];
+        const double* Jrow = &J[18 * q];
         if (pb.cams_var)
           for (int k = 0; k < 6; ++k) grad[pb.np + 6 * c + k] += Jrow[k] * res[0] + Jrow[9 + k] * res[1];
         if (pb.pts_var)
           for (int k = 0; k < 3; ++k) grad[3 * p + k] += Jrow[6 + k] * res[0] + Jrow[15 + k] * res[1];
-      } else {
-        EvalPlain(Rp, tp, Xp, K9 + 9 * size_t(c), obs_uv[2 * i], obs_uv[2 * i + 1], res);
       }
-      if (rr) { (*rr)[2 * q] = res[0]; (*rr)[2 * q + 1] = res[1]; }
       cost += 0.5 * (res[0] * res[0] + res[1] * res[1]);
     }
     *cost_out = cost;
@@ -555,22 +571,28 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
         S.assign(size_t(nf) * nf, 0.0);
         rhs.assign(nf, 0.0);
         for (int i = 0; i < nf; ++i) S[size_t(i) * nf + i] += lm_D[pb.np + i] * lm_D[pb.np + i];
-        std::vector<double> Ebuf;  // per chunk E'F blocks
-        std::vector<int> fcams;
+        // Phase 1, per point (independent): ete = D_e^2 + sum E^T E,
+        // g = sum E^T b, buffer_f = sum E^T F per distinct camera (slot order
+        // = first appearance), inverse_ete.  Slots live at the point's
+        // observation offsets.
+        std::vector<double> ebuf(18 * size_t(N)), pinv(9 * size_t(n_pts)), pig(3 * size_t(n_pts));
+        std::vector<int> fc(N), nslot(n_pts, 0);
+        int any_bad = 0;
+#pragma omp parallel for num_threads(g_threads) schedule(static) reduction(| : any_bad) if (g_threads > 1)
         for (int p = 0; p < n_pts; ++p) {
           const int64_t q0 = pb.pt_off[p], q1 = pb.pt_off[p + 1];
           if (q0 == q1) continue;
-          // ete = D_e^2 + sum E^T E ; g = sum E^T b ; buffer_f = sum E^T F ; S(f,f) += F^T F
           double ete[9] = {0};
           for (int k = 0; k < 3; ++k) ete[4 * k] = lm_D[3 * p + k] * lm_D[3 * p + k];
           double g[3] = {0, 0, 0};
-          fcams.clear();
-          Ebuf.clear();
+          int* fcams = &fc[q0];
+          double* Ebuf = &ebuf[18 * size_t(q0)];
+          int m = 0;
           for (int64_t q = q0; q < q1; ++q) {
             const int c = cam_idx[pb.order[q]];
             int slot = -1;
-            for (size_t s = 0; s < fcams.size(); ++s) if (fcams[s] == c) { slot = int(s); break; }
-            if (slot < 0) { slot = int(fcams.size()); fcams.push_back(c); Ebuf.resize(Ebuf.size() + 18, 0.0); }
+            for (int s2 = 0; s2 < m; ++s2) if (fcams[s2] == c) { slot = s2; break; }
+            if (slot < 0) { slot = m++; fcams[slot] = c; std::fill(Ebuf + 18 * slot, Ebuf + 18 * slot + 18, 0.0); }
             double E[6], F[12];
             for (int row = 0; row < 2; ++row) {
               for (int k = 0; k < 3; ++k) E[3 * row + k] = Js(q, row, 6 + k);
@@ -582,49 +604,81 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
               g[a] += E[a] * b0 + E[3 + a] * b1;
               for (int k = 0; k < 6; ++k) Ebuf[18 * slot + 6 * a + k] += E[a] * F[k] + E[3 + a] * F[6 + k];
             }
-            // F^T F into S (both 3-blocks of the camera and their coupling)
-            const int base = 6 * c;
-            for (int a = 0; a < 6; ++a)
-              for (int bb = 0; bb < 6; ++bb)
-                S[size_t(base + a) * nf + base + bb] += F[a] * F[bb] + F[6 + a] * F[6 + bb];
           }
+          nslot[p] = m;
           double L[9];
-          if (!Llt3(ete, L)) { solve_ok = false; break; }
+          if (!Llt3(ete, L)) { any_bad = 1; continue; }
           // inverse_ete = llt.solve(I)
-          double inv[9];
+          double* inv = &pinv[9 * size_t(p)];
           for (int col = 0; col < 3; ++col) {
             double e[3] = {0, 0, 0}; e[col] = 1.0;
             Llt3Solve(L, e);
             for (int a = 0; a < 3; ++a) inv[3 * a + col] = e[a];
           }
-          double ig[3];
-          for (int a = 0; a < 3; ++a) ig[a] = inv[3 * a] * g[0] + inv[3 * a + 1] * g[1] + inv[3 * a + 2] * g[2];
-          // UpdateRhs: rhs_f += F^T (b - E * inverse_ete_g)
-          for (int64_t q = q0; q < q1; ++q) {
-            const int c = cam_idx[pb.order[q]];
-            double sj[2];
-            for (int row = 0; row < 2; ++row) {
-              sj[row] = r[2 * q + row];
-              for (int k = 0; k < 3; ++k) sj[row] -= Js(q, row, 6 + k) * ig[k];
-            }
-            for (int k = 0; k < 6; ++k) rhs[6 * c + k] += Js(q, 0, k) * sj[0] + Js(q, 1, k) * sj[1];
-          }
-          // ChunkOuterProduct: S(j,k) -= buffer_j^T inverse_ete buffer_k  (k >= j)
-          const int m = int(fcams.size());
-          for (int j = 0; j < m; ++j) {
-            double bt_inv[18];  // (6x3) = buffer_j^T * inv
-            for (int a = 0; a < 6; ++a)
-              for (int bb = 0; bb < 3; ++bb)
-                bt_inv[3 * a + bb] = Ebuf[18 * j + 0 * 6 + a] * inv[0 * 3 + bb] + Ebuf[18 * j + 1 * 6 + a] * inv[1 * 3 + bb] +
-                                     Ebuf[18 * j + 2 * 6 + a] * inv[2 * 3 + bb];
-            for (int k = 0; k < m; ++k) {
-              const int cj = fcams[j], ck = fcams[k];
-              for (int a = 0; a < 6; ++a)
-                for (int bb = 0; bb < 6; ++bb) {
-                  double s = bt_inv[3 * a] * Ebuf[18 * k + 0 * 6 + bb] + bt_inv[3 * a + 1] * Ebuf[18 * k + 1 * 6 + bb] +
-                             bt_inv[3 * a + 2] * Ebuf[18 * k + 2 * 6 + bb];
-                  S[size_t(6 * cj + a) * nf + 6 * ck + bb] -= s;
+          for (int a = 0; a < 3; ++a)
+            pig[3 * size_t(p) + a] = inv[3 * a] * g[0] + inv[3 * a + 1] * g[1] + inv[3 * a + 2] * g[2];
+        }
+        if (any_bad) solve_ok = false;
+        // Phase 2, per camera row range (each S / rhs row has one owner; the
+        // points are visited in order, so every entry sees the serial
+        // sequence: F^T F, then UpdateRhs, then ChunkOuterProduct, point by
+        // point).
+        if (solve_ok) {
+          const int T = std::max(1, std::min(g_threads, C));
+#pragma omp parallel for num_threads(T) schedule(static, 1) if (T > 1)
+          for (int th = 0; th < T; ++th) {
+            const int clo = int(int64_t(C) * th / T), chi = int(int64_t(C) * (th + 1) / T);
+            for (int p = 0; p < n_pts; ++p) {
+              const int64_t q0 = pb.pt_off[p], q1 = pb.pt_off[p + 1];
+              if (q0 == q1) continue;
+              // F^T F into S (both 3-blocks of the camera and their coupling)
+              for (int64_t q = q0; q < q1; ++q) {
+                const int c = cam_idx[pb.order[q]];
+                if (c < clo || c >= chi) continue;
+                double F[12];
+                for (int row = 0; row < 2; ++row)
+                  for (int k = 0; k < 6; ++k) F[6 * row + k] = Js(q, row, k);
+                const int base = 6 * c;
+                for (int a = 0; a < 6; ++a)
+                  for (int bb = 0; bb < 6; ++bb)
+                    S[size_t(base + a) * nf + base + bb] += F[a] * F[bb] + F[6 + a] * F[6 + bb];
+              }
+              const double* inv = &pinv[9 * size_t(p)];
+              const double* ig = &pig[3 * size_t(p)];
+              // UpdateRhs: rhs_f += F^T (b - E * inverse_ete_g)
+              for (int64_t q = q0; q < q1; ++q) {
+                const int c = cam_idx[pb.order[q]];
+                if (c < clo || c >= chi) continue;
+                double sj[2];
+                for (int row = 0; row < 2; ++row) {
+                  sj[row] = r[2 * q + row];
+                  for (int k = 0; k < 3; ++k) sj[row] -= Js(q, row, 6 + k) * ig[k];
                 }
+                for (int k = 0; k < 6; ++k) rhs[6 * c + k] += Js(q, 0, k) * sj[0] + Js(q, 1, k) * sj[1];
+              }
+              // ChunkOuterProduct: S(j,k) -= buffer_j^T inverse_ete buffer_k
+              const int m = nslot[p];
+              const int* fcams = &fc[q0];
+              const double* Ebuf = &ebuf[18 * size_t(q0)];
+              for (int j = 0; j < m; ++j) {
+                const int cj = fcams[j];
+                if (cj < clo || cj >= chi) continue;
+                double bt_inv[18];  // (6x3) = buffer_j^T * inv
+                for (int a = 0; a < 6; ++a)
+                  for (int bb = 0; bb < 3; ++bb)
+                    bt_inv[3 * a + bb] = Ebuf[18 * j + 0 * 6 + a] * inv[0 * 3 + bb] +
+                                         Ebuf[18 * j + 1 * 6 + a] * inv[1 * 3 + bb] +
+                                         Ebuf[18 * j + 2 * 6 + a] * inv[2 * 3 + bb];
+                for (int k = 0; k < m; ++k) {
+                  const int ck = fcams[k];
+                  for (int a = 0; a < 6; ++a)
+                    for (int bb = 0; bb < 6; ++bb) {
+                      double s = bt_inv[3 * a] * Ebuf[18 * k + 0 * 6 + bb] + bt_inv[3 * a + 1] * Ebuf[18 * k + 1 * 6 + bb] +
+                                 bt_inv[3 * a + 2] * Ebuf[18 * k + 2 * 6 + bb];
+                      S[size_t(6 * cj + a) * nf + 6 * ck + bb] -= s;
+                    }
+                }
+              }
             }
           }
         }
@@ -635,6 +689,8 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
             CholSolve(S.data(), nf, y.data());
             for (int i = 0; i < nf; ++i) step[pb.np + i] = y[i];
             // BackSubstitute: y_e = (E^T E + D_e^2)^-1 E^T (b - F y_f)
+            int bs_bad = 0;
+#pragma omp parallel for num_threads(g_threads) schedule(static) reduction(| : bs_bad) if (g_threads > 1)
             for (int p = 0; p < n_pts; ++p) {
               const int64_t q0 = pb.pt_off[p], q1 = pb.pt_off[p + 1];
               if (q0 == q1) continue;
@@ -655,10 +711,11 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
                 }
               }
               double L[9];
-              if (!Llt3(ete, L)) { solve_ok = false; break; }
+              if (!Llt3(ete, L)) { bs_bad = 1; continue; }
               Llt3Solve(L, ye);
               for (int k = 0; k < 3; ++k) step[3 * p + k] = ye[k];
             }
+            if (bs_bad) solve_ok = false;
           }
         }
       } else {
@@ -702,13 +759,15 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
       itr.step_is_successful = 0;
       if (solve_ok) {
         double mc = 0.0;
-        for (int64_t q = 0; q < N; ++q) {
-          double mr[2];
+#pragma omp parallel for num_threads(g_threads) schedule(static) if (g_threads > 1)
+        for (int64_t q = 0; q < N; ++q)
           for (int row = 0; row < 2; ++row) {
             double s = 0.0;
             for (int k = 0; k < 9; ++k) { const int col = col_of(q, k); if (col >= 0) s += Js(q, row, k) * step[col]; }
-            mr[row] = s;
+            model_res[2 * q + row] = s;
           }
+        for (int64_t q = 0; q < N; ++q) {
+          const double mr[2] = {model_res[2 * q], model_res[2 * q + 1]};
           mc += mr[0] * (r[2 * q] + mr[0] / 2.0) + mr[1] * (r[2 * q + 1] + mr[1] / 2.0);
         }
         model_cost_change = -mc;
@@ -811,6 +870,14 @@ write_back:
 }
 
 int oracle_abi_version(void) { return 1; }
+
+// Threads of the OpenMP loops of oracle_ba_solve (default 1; any value gives
+// bitwise the same result).  Returns the previous value.
+int oracle_set_threads(int threads) {
+  const int prev = g_threads;
+  g_threads = threads < 1 ? 1 : threads;
+  return prev;
+}
 
 }  // extern "C"
 
