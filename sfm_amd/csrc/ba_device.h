@@ -13,11 +13,9 @@ namespace sfm {
 //   [8..19] J_c  (2 x 6, row-major)   d r / d (rot, t)   (scaled)
 constexpr int kJRec = 20;
 constexpr int kJX = 0, kRes = 6, kJC = 8;
-// Per-observation Schur record written every LM iteration:
-//   [0..5] M = J_X L_p^-T (2 x 3)   [6..7] h = M z_p
-constexpr int kMRec = 8;
-constexpr int kFRec = 18;
-constexpr int kEU = 6;     // back substitution: e = J_c y_c (2) | u = M^T e (3) | pad  // F = J_c^T M per observation (6x3), point-major
+// Back-substitution pass A output per observation, at its point-major slot:
+// u = M^T e (3) | pad.
+constexpr int kEU = 4;
 // Per-camera rotation data: R (9, row-major) and dR/dw_k (27, k-major).
 constexpr int kCamR = 36;
 // Per-camera reduction record: U (21, packed upper 6x6), b_c (6), pad.
@@ -63,8 +61,10 @@ struct ReduceBatch {
 struct DevProblem {
   int32_t C = 0, P = 0;      // cameras (global), points (this shard)
   int64_t N = 0;             // observations (this shard)
-  // structure (point-major observation order; within a point by camera)
+  // structure (point-major observation order; within a point by camera,
+  // then by the caller's order) -- built on the device by set_problem
   int32_t* pt_off = nullptr;   // [P+1]
+  int32_t* order = nullptr;    // [N] caller's observation index of point-major q
   int64_t N_pad = 0;           // camera-major positions incl. per-camera padding to 64
   int32_t* cam_obs = nullptr;  // [N_pad] point-major observation id at camera-major position (-1: padding)
   int32_t* cam_rng = nullptr;  // [C][2] camera c's records: positions [begin, end)
@@ -72,10 +72,10 @@ struct DevProblem {
   int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
   int32_t n_jchunks = 0;
   int32_t* jgrp = nullptr;     // [9] chunk-table offsets of the 8 point slices (one per XCD)
-  int32_t jac_blocks = 1;      // persistent grid of k_jacobian (cost partials)
+  int32_t jac_blocks = 1;      // persistent grid of k_jacobian in the solve (cost partials)
   int32_t jac_blocks_rec = 1;  // ... of the record-writing variant (evaluate API, bench roofline)
   double* uv_cm = nullptr;     // [N_pad][2] uv in camera-major order
-  int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q (jrec index)
+  int32_t* pos = nullptr;      // [N] camera-major position of point-major observation q
   double* Kc = nullptr;        // [C][5] fx skew cx fy cy
   // parameters (current and candidate)
   double* cam = nullptr;      // [C][6] rot(3) t(3)
@@ -92,12 +92,11 @@ struct DevProblem {
   // per-iteration work arrays
   double* camR = nullptr;     // [C][36]
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
-  double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12)
-  double* frec = nullptr;     // [N_pad][18] F = J_c^T M at the camera-major position: Schur pair blocks F_o1 F_o2^T
-  double* eu = nullptr;       // [N_pad][6] back substitution pass A output (camera-major)
+  double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12): evaluate API only,
+                              // allocated on first use (the solve writes no records)
+  double* eu = nullptr;       // [N][kEU] back substitution pass A output (point-major)
   double* ypt = nullptr;      // [P][3] point steps y_p (scaled space)
   int32_t* wcam = nullptr;    // [N_pad / 64] camera of each camera-major wavefront (runs padded to 64)
-  double* mrec = nullptr;     // [N_pad][8] M = J_X L^-T (2x3) and h = M z at the camera-major position
   double* ptV = nullptr;      // [P][10]
   double* ptL = nullptr;      // [P][10]
   double* Ucam = nullptr;     // [C][28]
@@ -115,60 +114,25 @@ struct DevProblem {
   int32_t n_cu = 0;           // compute units (co-residency bound of the persistent grids)
   // LM diagonal clamp of the running solve (sfm_ba_options min/max_lm_diagonal)
   double min_diag = 1e-6, max_diag = 1e32;
-  bool chol_stepwise = false; // SFM_CHOL_STEPWISE=1: three launches per tile column instead
 
-  // Schur: upper-triangle blocks (c1, c2) in row-major order, CSR offsets
-  // of their (o1, o2) pair lists, and the pairs (point-major ids)
+  // Schur (k_schur_pts): every upper-triangle camera block (c1, c2), c1 <=
+  // c2, in row-major order, the CSR offsets of its pair list and, per pair
+  // (o1, o2) of a common point, that point; F is recomputed per pair from the
+  // point and the two wave-uniform cameras
   int64_t n_blk = 0, n_pairs = 0;
   int2* blk = nullptr;        // [n_blk]
   int32_t* seg = nullptr;     // [n_blk + 1]
-  int32_t schur_row = 1;       // row-staged k_schur_row (SFM_SCHUR_ROW=0 disables)
-  int4* srow = nullptr;        // [n_srow] k_schur_row work items (c1, first block, block count, 0)
-  int32_t n_srow = 0;
-  int2* pairs = nullptr;      // [n_pairs]
-  // k_schur_pts (default for large problems): the pair lists as the common
-  // point of each pair, and the per-point records; F is recomputed per pair
-  // from the point and the two wave-uniform cameras instead of gathered
   int32_t* bpts = nullptr;    // [n_pairs]
   int32_t* bperm = nullptr;   // [n_blk] blocks by descending pair count (k_schur_pts wave balance)
   double* ptS = nullptr;      // [P][kPtS]
-  bool schur_pts = false;
-  // concurrent Schur + Cholesky (single rank, pts mode): [nblk] monotone
-  // per-tile-column counts of finished k_schur_pts workgroups | [nblk]
-  // workgroups per column and launch
-  int32_t* pcnt = nullptr;
-  bool schur_overlap = false;
-  int32_t chol_helpers = 0;    // SFM_CHOL_HELPERS: cap on the Cholesky helper workgroups (0: CU count - 1)
-  int32_t schur_pts_sub = 8;   // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
-  // per-wave diagonal-block / rhs partials from k_obs_prep ([N_pad/64][27]);
-  // nullptr (SFM_SCHUR_DIAG_FUSED=0): k_schur_diag re-reads the records
+  int32_t schur_pts_sub = 8;  // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
+  // per-wave diagonal-block / rhs partials from k_obs_prep_rc ([N_pad/64][27])
   double* dpart = nullptr;
-  // per-chunk U_c / b_c partials from k_jacobian ([N_pad/64][27]); nullptr
-  // (SFM_CAM_FUSED=0): k_cam_reduce re-reads the records
+  // per-chunk U_c / b_c partials from k_jacobian ([N_pad/64][27])
   double* jpart = nullptr;
-  // point-major uv and camera index (k_point_eval_rc recomputes J_X and r;
-  // nullptr with SFM_PTEVAL_RC=0: k_point_eval gathers the records)
+  // point-major uv and camera index (k_point_eval_rc)
   double* uv_pm = nullptr;     // [N][2]
-  // record-free observation passes (k_obs_prep_rc, k_backsub_a_rc; SFM_OBS_RC=0
-  // restores the record readers); need_jrec: some consumer still reads jrec
-  bool obs_rc = false;
-  bool need_jrec = true;
   int32_t* cam_pm = nullptr;   // [N]
-  // small problems: pair-chunk items (block, first pair, end pair) with
-  // per-block item ranges and partial 6x6 sums (k_schur_split)
-  int4* sitems = nullptr;
-  int32_t n_sitems = 0;
-  int32_t* sboff = nullptr;    // [n_blk + 1]
-  double* spart = nullptr;     // [n_sitems][36]
-  // fused Schur + Cholesky (one persistent launch; single rank only): task
-  // table (type, a, b, c): 0 = first row segment of camera a (holds block
-  // (a, a)), 3 = further row segment (a, first block b, count c),
-  // 1 = diagonal/rhs of camera a, 2 = Cholesky tile (a, b)
-  int4* stasks = nullptr;      // [n_stasks]
-  int32_t n_stasks = 0;
-  int32_t* scnt = nullptr;     // [nblk] Schur items done per tile column (monotone) | [nblk] per-launch targets | [C] S_cc stamps
-  unsigned long long* sticket = nullptr;
-  bool schur_fused = false;    // SFM_SCHUR_FUSED=1: one fused launch (experimental, slower: DESIGN.md §5)
   // reductions
   double* partials = nullptr; // scratch [kNumPartialSlots][max_blocks]
   int32_t max_blocks = 0;
@@ -185,8 +149,8 @@ enum PartialSlot {
 
 // ---- launchers (ba_kernels.hip) ----
 void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s);
-// force_records: write the 160-B records even in the record-free path (evaluate API, tools)
-void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool force_records = false);
+// write_records: also store the 160-B records (evaluate API, bench roofline)
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records = false);
 void launch_cam_reduce(const DevProblem& d, hipStream_t s);
 // mode 0: unscaled pass -> compute scale_c from colnorms; mode 1: diag (if !reuse) + gradient
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s);
@@ -202,21 +166,11 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = tr
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
-void launch_read_touch(const double* p, size_t n, double* out, hipStream_t s);
 void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fail, hipStream_t s);
 int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
-// sepoch > 0: gated on the concurrent k_schur_pts launch of that epoch (pcnt)
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true, int sepoch = 0);
-// k_schur_pts only (publishing per-column counts when sepoch > 0), after
-// launch_schur_diag_first: the overlapped Schur of the single-rank pts mode
-void launch_schur_diag_first(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
-void launch_schur_pts(const DevProblem& d, int sepoch, hipStream_t s);
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
-// Schur (row segments + diagonal/rhs) and Cholesky in ONE persistent launch
-// (single rank; the multi-rank path all-reduces S in between instead).
-void launch_schur_cholesky(const DevProblem& d, double radius, bool add_diag, int chol_epoch, int schur_epoch,
-                           hipStream_t s);
 
 }  // namespace sfm

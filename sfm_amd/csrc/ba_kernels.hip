@@ -12,12 +12,12 @@
 //     residual evaluation.
 // Every reduction is a fixed-order tree (per-block partials, then one
 // ordered pass), so cost / gradient / step norms are bitwise reproducible.
-// The only order-dependent sum is the LDS accumulation of S (ds_add_f64).
+// (No atomics in any sum: whole solves are bitwise reproducible.)
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cmath>
 #include "ba_device.h"
-#include "schur_tasks.h"
+#include "ba_common.h"
 
 namespace sfm {
 
@@ -116,21 +116,18 @@ __global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __re
 }
 
 // ---------------------------------------------------------------------------
-// Residual + Jacobian in CAMERA-major order, the record stored at the
-// camera-major position i: every consumer that walks a camera's
-// observations (U_c, the Schur row) then streams, and the point-side
-// consumers reach a record through pos[q].
+// Residual + Jacobian in CAMERA-major order.
 // Work unit = one wavefront chunk: up to 64 consecutive observations of ONE
-// camera (host-built table, 63 chunks per camera at C3).  The camera is
+// camera (device-built table, 63 chunks per camera at C3).  The camera is
 // wave-uniform, so its 44 doubles (R, dR/dw, t, K, Jacobi scale) are scalar
-// loads; per lane the pass moves the point index (4 B), uv (16 B), the point
-// X (24 B, a 4.8-MB L2/MALL-resident gather) and its 160-B record.  The
-// chunk's records are one contiguous run, written through a wave-local LDS
-// transpose as fully coalesced 1-KB rows (strided per-lane stores touch 80
-// cache lines per instruction and were store-issue bound).  The grid is
-// persistent (waves stride over the chunk table).  Algorithmic HBM traffic:
-// 180 B per observation (point index 4, uv 16, record 160) plus 88 B per
-// camera and 24 B per point.
+// loads; per lane the pass moves the point index (4 B), uv (16 B) and the
+// point X (24 B, a 4.8-MB L2/MALL-resident gather).  In the solve the pass
+// writes no per-observation record: the cost and the chunk's 27 U_c / b_c
+// partial sums (jpart) are its only outputs, and every later observation
+// pass recomputes what it needs.  The evaluate API (write_rec) also stores
+// the 160-B record at the camera-major position, through a wave-local LDS
+// transpose as fully coalesced 1-KB rows.  The grid is persistent (waves
+// stride over the chunk table).
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Store the wave's staged chunk (64 records from position ib; a camera's
@@ -310,54 +307,6 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
   if (threadIdx.x == 0) part_cost[blockIdx.x] = r;
 }
 
-// ---------------------------------------------------------------------------
-// Per-camera normal-equation block U_c = sum J_c^T J_c and b_c = sum J_c^T r,
-// one workgroup per camera, fixed-order reduction.
-__global__ __launch_bounds__(kThreads) void k_cam_reduce(const int32_t* __restrict__ cam_rng,
-                                                         const double* __restrict__ jrec, double* __restrict__ Ucam) {
-  __shared__ double sh[4 * 27];
-  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * kJRec];
-  const int c = blockIdx.x;
-  const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63;
-  double acc[27];
-#pragma unroll
-  for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-  const int i0 = cam_rng[2 * c], i1 = cam_rng[2 * c + 1];
-  // camera runs start on a wavefront boundary and are padded to one
-  for (int base = i0 + 64 * w0; base < i1; base += kThreads) {
-    const double* J = wave_records<kJRec>(stage[w0], jrec + size_t(base) * kJRec, l0);
-    const bool real = base + l0 < i1;
-    double2 rr = ld2(J + kRes);
-    if (!real) rr = make_double2(0.0, 0.0);
-    double j0[6], j1[6];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double2 a = ld2(J + kJC + 2 * k), b = ld2(J + kJC + 6 + 2 * k);
-      j0[2 * k] = real ? a.x : 0.0; j0[2 * k + 1] = real ? a.y : 0.0;
-      j1[2 * k] = real ? b.x : 0.0; j1[2 * k + 1] = real ? b.y : 0.0;
-    }
-    wave_sync_lds();
-    int q = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = a; b < 6; ++b) acc[q++] += j0[a] * j0[b] + j1[a] * j1[b];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += j0[a] * rr.x + j1[a] * rr.y;
-  }
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-#pragma unroll
-  for (int i = 0; i < 27; ++i) {
-    const double v = wave_sum(acc[i]);
-    if (l == 0) sh[w * 27 + i] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 27) {
-    const double v = sh[threadIdx.x] + sh[27 + threadIdx.x] + sh[54 + threadIdx.x] + sh[81 + threadIdx.x];
-    Ucam[size_t(kUcam) * c + threadIdx.x] = v;
-  }
-}
-
 // mode 0: Jacobi scale from the unscaled column norms (diagonal of U).
 // mode 1: LM diagonal (unless reused) and camera gradient max-norm.
 // U_c and b_c from k_jacobian's per-chunk partials (jpart): lane t sums
@@ -401,58 +350,12 @@ __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* 
   if (threadIdx.x == 0 && part_grad) part_grad[blockIdx.x] = r;
 }
 
-// ---------------------------------------------------------------------------
-// Point pass after a Jacobian evaluation (one lane per point):
+// Point pass after a Jacobian evaluation (one lane per point), with the
+// point's residuals and J_X recomputed (jac_record's arithmetic) from
+// point-major uv (16 B per observation, streamed per lane), the camera index
+// and the camera's R, t, K (L2-resident):
 // mode 0: Jacobi scale of the point columns; mode 1: V_p, b_p, LM diagonal,
 // gradient max-norm and |X|^2.
-__global__ __launch_bounds__(kThreads) void k_point_eval(int P, const int32_t* __restrict__ pt_off,
-                                                         const int32_t* __restrict__ pos,
-                                                         const double* __restrict__ jrec, const double* __restrict__ X,
-                                                         double* __restrict__ scale_p, double* __restrict__ diag_p,
-                                                         double* __restrict__ ptV, double min_diag, double max_diag,
-                                                         int mode, int reuse, double* __restrict__ part_grad,
-                                                         double* __restrict__ part_xn) {
-  __shared__ double sh[4];
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  double g = 0.0, xn = 0.0;
-  if (p < P) {
-    double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    const int q0 = pt_off[p], q1 = pt_off[p + 1];
-    for (int q = q0; q < q1; ++q) {
-      const double* J = jrec + size_t(pos[q]) * kJRec;
-      const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4), rr = ld2(J + kRes);
-      const double u0 = e0.x, u1 = e0.y, u2 = e1.x, v0 = e1.y, v1 = e2.x, v2 = e2.y;
-      V[0] += u0 * u0 + v0 * v0;
-      V[1] += u1 * u0 + v1 * v0; V[2] += u1 * u1 + v1 * v1;
-      V[3] += u2 * u0 + v2 * v0; V[4] += u2 * u1 + v2 * v1; V[5] += u2 * u2 + v2 * v2;
-      b[0] += u0 * rr.x + v0 * rr.y; b[1] += u1 * rr.x + v1 * rr.y; b[2] += u2 * rr.x + v2 * rr.y;
-    }
-    const double cn[3] = {V[0], V[2], V[5]};
-    if (mode == 0) {
-      for (int k = 0; k < 3; ++k) scale_p[3 * size_t(p) + k] = 1.0 / (1.0 + sqrt(cn[k]));
-    } else {
-      for (int k = 0; k < 3; ++k) {
-        if (!reuse) diag_p[3 * size_t(p) + k] = fmin(fmax(cn[k], min_diag), max_diag);
-        g = fmax(g, fabs(b[k] / scale_p[3 * size_t(p) + k]));
-        xn += X[3 * size_t(p) + k] * X[3 * size_t(p) + k];
-      }
-      double* o = ptV + size_t(kPtV) * p;
-      st2(o, V[0], V[1]); st2(o + 2, V[2], V[3]); st2(o + 4, V[4], V[5]); st2(o + 6, b[0], b[1]); st2(o + 8, b[2], 0.0);
-    }
-  }
-  if (mode == 1) {
-    const double rg = block_reduce(g, sh, true);
-    if (threadIdx.x == 0) part_grad[blockIdx.x] = rg;
-    const double rx = block_reduce(xn, sh, false);
-    if (threadIdx.x == 0) part_xn[blockIdx.x] = rx;
-  }
-}
-
-// k_point_eval with the point's residuals and J_X recomputed instead of
-// gathered: the same sums as k_point_eval (jac_record's arithmetic), fed by
-// point-major uv (16 B per observation, streamed per lane), the camera index
-// and the camera's R, t, K (L2-resident) -- no 160-B Jacobian record, whose
-// 64-B J_X | r head touched ~1.5 lines per observation of a 325-MB array.
 __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t* __restrict__ pt_off,
                                                             const int32_t* __restrict__ cam_pm,
                                                             const double* __restrict__ uv_pm,
@@ -562,95 +465,6 @@ __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* 
   if (threadIdx.x == 0) part_bad[blockIdx.x] = r;
 }
 
-// Per observation, one lane per CAMERA-major position (the J records
-// stream; the point's factor is a 80-B gather):  M = J_X L^-T, h = M z
-// (the ingredients of W V^-1 W^T and W V^-1 b) -> mrec, and F = J_c^T M
-// (6x3, the Schur pair block is F_o1 F_o2^T) -> frec, both at the same
-// camera-major position, so the row camera's terms stream in k_schur_diag.
-// A wavefront's 64 records of each kind are one contiguous run (camera
-// runs are padded to whole wavefronts; padding lanes compute a copy of the
-// camera's last observation, never read): they are staged in LDS and
-// leave as full 1-KB rows with streaming stores, like the Jacobian records.
-// With dpart != nullptr the wave (64 positions of ONE camera: runs are
-// padded to whole wavefronts) also reduces the camera's diagonal-block and
-// rhs terms of the Schur complement, sum F F^T (21) and J_c^T (r - h) (6),
-// over its real observations into dpart[wave][27] (fixed tree order), so
-// k_schur_diag_sum reads 27 doubles per wave instead of every J and M record.
-__global__ __launch_bounds__(kThreads) void k_obs_prep(int64_t N_pad, const int32_t* __restrict__ cm_p,
-                                                       const double* __restrict__ jrec,
-                                                       const double* __restrict__ ptL, double* __restrict__ mrec,
-                                                       double* __restrict__ frec,
-                                                       const int32_t* __restrict__ cam_obs,
-                                                       double* __restrict__ dpart) {
-  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kMRec + kFRec)];  // 13 KB per wave
-  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i0 = (int64_t(blockIdx.x) * kThreads) + 64 * wv;  // first position of this wavefront
-  if (i0 >= N_pad) return;  // whole wavefronts (N_pad is a multiple of 64)
-  const int64_t i = i0 + l;
-  const double* L = ptL + size_t(kPtL) * cm_p[i];
-  const double2 a0 = ld2(L), a1 = ld2(L + 2), a2 = ld2(L + 4), a3 = ld2(L + 6), a4 = ld2(L + 8);
-  const double l00 = a0.x, l10 = a0.y, l11 = a1.x, l20 = a1.y, l21 = a2.x, l22 = a2.y;
-  const double z0 = a3.x, z1 = a3.y, z2 = a4.x;
-  // the wave's 64 J records arrive through its LDS slice (coalesced rows)
-  const double* J = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l);
-  const double2 e0 = ld2(J), e1 = ld2(J + 2), e2 = ld2(J + 4);
-  double jc[12];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { const double2 t = ld2(J + kJC + 2 * k); jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
-  const double2 rr = ld2(J + kRes);
-  wave_sync_lds();
-  const double m0 = e0.x / l00, m1 = (e0.y - l10 * m0) / l11, m2 = (e1.x - l20 * m0 - l21 * m1) / l22;
-  const double n0 = e1.y / l00, n1 = (e2.x - l10 * n0) / l11, n2 = (e2.y - l20 * n0 - l21 * n1) / l22;
-  double* sm = stage[wv];                 // [64][8]  M records
-  double* sf = stage[wv] + 64 * kMRec;    // [64][18] F records
-  double* M = sm + l * kMRec;
-  st2(M, m0, m1); st2(M + 2, m2, n0); st2(M + 4, n1, n2);
-  st2(M + 6, m0 * z0 + m1 * z1 + m2 * z2, n0 * z0 + n1 * z1 + n2 * z2);
-  double* Fo = sf + l * kFRec;
-  double F[kFRec];
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    F[3 * u] = jc[u] * m0 + jc[6 + u] * n0;
-    F[3 * u + 1] = jc[u] * m1 + jc[6 + u] * n1;
-    F[3 * u + 2] = jc[u] * m2 + jc[6 + u] * n2;
-    Fo[3 * u] = F[3 * u]; Fo[3 * u + 1] = F[3 * u + 1]; Fo[3 * u + 2] = F[3 * u + 2];
-  }
-  if (dpart) {
-    const bool real = cam_obs[i] >= 0;  // padding positions carry -1
-    const double h0 = m0 * z0 + m1 * z1 + m2 * z2, h1 = n0 * z0 + n1 * z1 + n2 * z2;
-    const double r0 = real ? rr.x - h0 : 0.0, r1 = real ? rr.y - h1 : 0.0;
-    double v[32];
-    int q = 0;
-#pragma unroll
-    for (int u = 0; u < 6; ++u)
-#pragma unroll
-      for (int w = u; w < 6; ++w, ++q)
-        v[q] = real ? F[3 * u] * F[3 * w] + F[3 * u + 1] * F[3 * w + 1] + F[3 * u + 2] * F[3 * w + 2] : 0.0;
-#pragma unroll
-    for (int u = 0; u < 6; ++u) v[21 + u] = jc[u] * r0 + jc[6 + u] * r1;
-#pragma unroll
-    for (int e = 27; e < 32; ++e) v[e] = 0.0;
-    const double tot = wave_sum32(v, l);  // lane l: entry l >> 1
-    if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double* dm = mrec + i0 * kMRec;
-  double* df = frec + i0 * kFRec;
-#pragma unroll
-  for (int kq = 0; kq < kMRec / 2; ++kq) {
-    const double2 v = ld2(sm + 2 * (64 * kq + l));
-    st2_nt(dm + 2 * (64 * kq + l), v.x, v.y);
-  }
-  if (frec)  // (k_schur_pts recomputes F from the point records instead)
-#pragma unroll
-    for (int kq = 0; kq < kFRec / 2; ++kq) {
-      const double2 v = ld2(sf + 2 * (64 * kq + l));
-      st2_nt(df + 2 * (64 * kq + l), v.x, v.y);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Record-free observation kernels (default): the camera-major passes after
 // the Jacobian recompute an observation's residual and scaled 2x9 Jacobian
@@ -719,8 +533,11 @@ __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const d
   o.h1 = o.M[3] * z01.x + o.M[4] * z01.y + o.M[5] * z2;
 }
 
-// The Schur diagonal-block / rhs partials of k_obs_prep (dpart), recomputed
-// (ptS is written by k_point_factor in the same launch sequence).
+// Per observation (camera-major, one wavefront = 64 positions of ONE camera):
+// F = J_c^T M (M = J_X L_p^-T) and the wave's share of the camera's Schur
+// diagonal block sum F F^T (21) and rhs sum J_c^T (r - h) (6), reduced over
+// its real observations into dpart[wave][27] (fixed tree order).  J, M, h
+// are recomputed (ptS is written by k_point_factor just before).
 __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
                                                           const int32_t* __restrict__ cm_p,
                                                           const double* __restrict__ uv_cm,
@@ -739,7 +556,7 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
   ObsRC o;
   obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, ptL, o);
   const double* jc = o.rec + kJC;
-  double F[kFRec];
+  double F[18];  // 6 x 3
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     F[3 * u] = jc[u] * o.M[0] + jc[6 + u] * o.M[3];
@@ -763,8 +580,8 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
   if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
 }
 
-// Back substitution pass A (see k_backsub_a), recomputed: e = J_c y_c,
-// u = M^T e, and the observation's share of the model cost change.
+// Back substitution pass A (see k_backsub_b): e = J_c y_c, u = M^T e, and
+// the observation's share of the model cost change (J, M recomputed).
 __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
                                                            const int32_t* __restrict__ cm_p,
                                                            const double* __restrict__ uv_cm,
@@ -807,156 +624,6 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
 }
 
 // ---------------------------------------------------------------------------
-// Reduced camera matrix  S = U + D^2 - sum_p F_p F_p^T,  F_o = J_c^T M_o
-// (6x3 per observation, k_point_prep), row-major upper triangle (==
-// column-major lower) of the augmented matrix, plus the reduced right-hand
-// side rhs_c = sum_{o in c} J_c^T (r_o - h_o) in column n.
-//
-// k_schur: one THREAD per block (c1, c2), c1 <= c2, of the upper triangle
-// (row-major block order, so a wavefront covers one row camera and its
-// F_o1 records stay L2-hot).  The thread walks its block's pair list --
-// (o1, o2) observations of a common point, cameras c1 and c2, host-built --
-// and accumulates F_o1 F_o2^T in registers: no atomics, no barriers, a fixed
-// summation order (S is bitwise reproducible), and every iteration's two
-// 144-B gathers are independent of the previous one, two pairs in flight
-// per step.  (f64 LDS atomics retire about one lane per clock per CU: the
-// atomic strip formulation was bound at ~0.8 ms on C3.)  A diagonal block's
-// list holds only same-camera duplicate pairs (normally none);
-// k_schur_diag, launched after, adds the rest of that block and the rhs.
-// (Kept as the ablation baseline of k_schur_row: SFM_SCHUR_ROW=0.)
-__global__ __launch_bounds__(kThreads) void k_schur(int64_t n_blk, const int2* __restrict__ blk,
-                                                    const int32_t* __restrict__ seg, const int2* __restrict__ pairs,
-                                                    const double* __restrict__ frec, double* __restrict__ S, int ld) {
-  const int64_t b = int64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (b >= n_blk) return;
-  const int2 cc = blk[b];
-  const int kb = seg[b], ke = seg[b + 1];
-  double acc[36];
-#pragma unroll
-  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
-  for (int k = kb; k < ke; k += 2) {
-    const bool two = k + 1 < ke;
-    const int2 pa = pairs[k], pb = pairs[two ? k + 1 : k];
-    const double wb = two ? 1.0 : 0.0;
-    const double* A1 = frec + size_t(pa.x) * kFRec;
-    const double* A2 = frec + size_t(pa.y) * kFRec;
-    const double* B1 = frec + size_t(pb.x) * kFRec;
-    const double* B2 = frec + size_t(pb.y) * kFRec;
-    double Ga[kFRec], Gb[kFRec];
-#pragma unroll
-    for (int f = 0; f < kFRec; f += 2) {
-      const double2 x = ld2(A2 + f), y = ld2(B2 + f);
-      Ga[f] = x.x; Ga[f + 1] = x.y; Gb[f] = y.x * wb; Gb[f + 1] = y.y * wb;
-    }
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const double2 a01 = ld2(A1 + 3 * u - (u & 1)), b01 = ld2(B1 + 3 * u - (u & 1));
-      // F_o1 row u = (x, y, z) at 3u; 16-B aligned loads straddle it
-      const double a0 = (u & 1) ? a01.y : a01.x, a1 = (u & 1) ? A1[3 * u + 1] : a01.y, a2 = A1[3 * u + 2];
-      const double b0 = (u & 1) ? b01.y : b01.x, b1 = (u & 1) ? B1[3 * u + 1] : b01.y, b2 = B1[3 * u + 2];
-#pragma unroll
-      for (int v = 0; v < 6; ++v) {
-        acc[6 * u + v] += a0 * Ga[3 * v] + a1 * Ga[3 * v + 1] + a2 * Ga[3 * v + 2];
-        acc[6 * u + v] += b0 * Gb[3 * v] + b1 * Gb[3 * v + 1] + b2 * Gb[3 * v + 2];
-      }
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
-#pragma unroll
-    for (int v = 0; v < 6; v += 2) st2(row + v, -acc[6 * u + v], -acc[6 * u + v + 1]);
-  }
-}
-
-// k_schur_row: the same owner-computes blocks, one workgroup per (row camera
-// c1, up to 256 consecutive blocks of its row).  Camera c1's F records (the
-// o1 side of every pair in the row, a contiguous camera-major run) are
-// streamed through LDS in chunks of kRowCh with coalesced loads, so only the
-// o2 side is gathered from the fabric: measured on C3, k_schur moves 4.8 GB
-// per launch (37.7M 128-B requests, 31% L2 hits, ~7 TB/s) for 2.6 GB of
-// pair records; the o1 half of those requests becomes one streamed pass
-// over each row camera's run.  Measured: 37.7M -> 22.1M requests, 670 ->
-// 632 us — the remaining o2 gathers (each 144-B record two fresh lines, no
-// reuse within a row) are L1-miss-latency bound (TCP pending stalls), which
-// neither cooperative coalesced gathers nor point-sliced launches (to keep
-// F resident in the Infinity Cache) improved: both measured slower.
-// Small problems (few camera blocks, long pair lists: C1 has 210 blocks of
-// ~470 pairs): the owner-computes kernels would run one thread per block
-// through hundreds of dependent gathers.  k_schur_split gives every chunk of
-// kSplitPairs pairs of a block its own thread (partial 6x6 sums), and
-// k_schur_split_reduce adds a block's chunks in chunk order: deterministic,
-// atomics-free, fully parallel.
-__global__ __launch_bounds__(kThreads) void k_schur_split(int n_items, const int4* __restrict__ items,
-                                                          const int2* __restrict__ pairs,
-                                                          const double* __restrict__ frec,
-                                                          double* __restrict__ part) {
-  const int it = blockIdx.x * kThreads + threadIdx.x;
-  if (it >= n_items) return;
-  const int4 w = items[it];  // (block, first pair, end pair, -)
-  double acc[36];
-#pragma unroll
-  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
-  for (int k = w.y; k < w.z; ++k) {
-    const int2 pr = pairs[k];
-    const double* A1 = frec + size_t(pr.x) * kFRec;
-    const double* A2 = frec + size_t(pr.y) * kFRec;
-    double a1[kFRec], g[kFRec];
-#pragma unroll
-    for (int f = 0; f < kFRec; f += 2) {
-      const double2 x = ld2(A1 + f), y = ld2(A2 + f);
-      a1[f] = x.x; a1[f + 1] = x.y; g[f] = y.x; g[f + 1] = y.y;
-    }
-#pragma unroll
-    for (int u = 0; u < 6; ++u)
-#pragma unroll
-      for (int v = 0; v < 6; ++v)
-        acc[6 * u + v] += a1[3 * u] * g[3 * v] + a1[3 * u + 1] * g[3 * v + 1] + a1[3 * u + 2] * g[3 * v + 2];
-  }
-  double* dst = part + size_t(it) * 36;
-#pragma unroll
-  for (int e = 0; e < 36; e += 2) st2(dst + e, acc[e], acc[e + 1]);
-}
-
-__global__ __launch_bounds__(kThreads) void k_schur_split_reduce(int64_t n_blk, const int2* __restrict__ blk,
-                                                                 const int32_t* __restrict__ boff,
-                                                                 const double* __restrict__ part,
-                                                                 double* __restrict__ S, int ld) {
-  const int64_t b = int64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (b >= n_blk) return;
-  double acc[36];
-#pragma unroll
-  for (int e = 0; e < 36; ++e) acc[e] = 0.0;
-  for (int it = boff[b]; it < boff[b + 1]; ++it) {
-    const double* src = part + size_t(it) * 36;
-#pragma unroll
-    for (int e = 0; e < 36; e += 2) {
-      const double2 x = ld2(src + e);
-      acc[e] += x.x;
-      acc[e + 1] += x.y;
-    }
-  }
-  const int2 cc = blk[b];
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    double* row = S + size_t(6 * cc.x + u) * ld + 6 * size_t(cc.y);
-#pragma unroll
-    for (int v = 0; v < 6; v += 2) st2(row + v, -acc[6 * u + v], -acc[6 * u + v + 1]);
-  }
-}
-
-constexpr int kRowChunkLds = kRowCh * kFRec;
-__global__ __launch_bounds__(kThreads) void k_schur_row(const int4* __restrict__ work,
-                                                        const int32_t* __restrict__ seg,
-                                                        const int2* __restrict__ pairs,
-                                                        const double* __restrict__ frec,
-                                                        const int32_t* __restrict__ cam_rng,
-                                                        const int2* __restrict__ blk, double* __restrict__ S, int ld) {
-  __shared__ __attribute__((aligned(16))) double F1[kRowChunkLds];
-  schur_row_task(work[blockIdx.x], seg, pairs, frec, cam_rng, blk, S, ld, F1);
-}
-
-// ---------------------------------------------------------------------------
 // k_schur_pts: the off-diagonal Schur blocks WITHOUT the F gathers.  A pair
 // (o1, o2) of block (c1, c2) shares its point p, and
 //   F_o1 F_o2^T = J_c1^T M_1 M_2^T J_c2,   M_i = J_X,i L_p^-T,
@@ -966,12 +633,11 @@ __global__ __launch_bounds__(kThreads) void k_schur_row(const int4* __restrict__
 // lane takes one pair per step, gathering only its point's 128-B record
 // (X, scale, L_p, 1/l_ii: one line, 25.6 MB in all at C3, so L2/MALL
 // resident) and recomputing both scaled Jacobians with the Jacobian pass's
-// own arithmetic (jac_record).  The k_schur_row formulation gathers a fresh
+// own arithmetic (jac_record).  A gathered-F formulation fetched a fresh
 // 144-B F record per pair from a 293-MB array (~2.9 GB of HBM traffic per
 // launch at C3); this one trades that for ~400 fp64 ops per pair.  The
 // block's lanes end with a fixed-order recursive-halving reduction, so S is
-// bitwise reproducible run to run.  (Same sums as k_schur_row to rounding:
-// M uses the reciprocals 1/l_ii and F is re-associated as J^T (M M^T) J.)
+// bitwise reproducible run to run.
 constexpr int kCamS = 50;  // R 9 | dR/dw 27 | t 3 | K 5 | scale 6
 
 __device__ __forceinline__ void stage_cam(double* cs, int c, const double* __restrict__ camR,
@@ -1054,7 +720,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
                                                         const double* __restrict__ camR,
                                                         const double* __restrict__ cam, const double* __restrict__ Kc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
-                                                        int ld, int diag_add, int* __restrict__ colcnt,
+                                                        int ld,
                                                         const int32_t* __restrict__ bperm) {
   constexpr int kPer = 64 / kSub;  // blocks per wave
   __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
@@ -1124,9 +790,9 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
                t35 = seg_sum<kSub>(acc[35]);
   if (own) {
     // a diagonal block (same-camera duplicate pairs only) is added to what
-    // k_schur_diag_sum wrote before this launch (diag_add), else stored
+    // k_schur_diag_sum wrote before this launch, else stored
     double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
-    const bool add = diag_add && cc.x == cc.y;
+    const bool add = cc.x == cc.y;
     auto put = [&](int e, double v) {
       double* q = Sb + size_t(e / 6) * ld + e % 6;
       *q = add ? *q - v : -v;
@@ -1140,41 +806,9 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
     }
     if (sl < 4) put(32 + sl, sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35);
   }
-  if (colcnt) {
-    // publish (guide form: every wave drains its stores, one agent release,
-    // relaxed counter adds): one count to each tile column whose S rows
-    // this workgroup's blocks wrote (their row cameras c1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) {
-        const int64_t b0 = int64_t(blockIdx.x) * (kThreads / 64) * kPer;
-        const int64_t b1 = min(b0 + (kThreads / 64) * kPer, n_blk) - 1;
-        const int j0 = (6 * blk[b0].x) / kNB, j1 = (6 * blk[b1].x + 5) / kNB;
-        for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(colcnt + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
 }
 
-// Diagonal blocks and right-hand side, one workgroup per camera c (after
-// k_schur, which left the block's same-camera duplicate pairs in S):
-//   S_cc += [rank 0] (U_c + D_c^2) - sum_{o in c} F_o F_o^T,
-//   S[c][n] = sum_{o in c} J_c^T (r_o - h_o); fixed-order reductions.
-__global__ __launch_bounds__(kThreads) void k_schur_diag(const int32_t* __restrict__ cam_rng,
-                                                         const int32_t* __restrict__ cam_obs,
-                                                         const double* __restrict__ jrec,
-                                                         const double* __restrict__ mrec,
-                                                         const double* __restrict__ Ucam,
-                                                         const double* __restrict__ diag_c, double radius,
-                                                         int add_diag, double* __restrict__ S, int ld, int n) {
-  __shared__ __attribute__((aligned(16))) double lds[kDiagLds];
-  schur_diag_task(blockIdx.x, cam_rng, cam_obs, jrec, mrec, Ucam, diag_c, radius, add_diag, S, ld, n, lds);
-}
-
-// Diagonal blocks and rhs from k_obs_prep's per-wave partials: camera c's
+// Diagonal blocks and rhs from k_obs_prep_rc's per-wave partials: camera c's
 // waves are positions cam_rng[2c]/64 .. (run end)/64, summed in order.
 //   S_cc += [rank 0] (U_c + D_c^2) - sum F F^T,   S[c][n] = sum J_c^T (r - h)
 __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict__ cam_rng,
@@ -1329,64 +963,19 @@ __global__ __launch_bounds__(kThreads) void k_cam_solve(int C, const double* __r
 
 // ---------------------------------------------------------------------------
 // Point back substitution, model cost change and candidate cost, in three
-// passes so that every per-observation array is streamed in camera-major
-// order and only per-point quantities are gathered:
-//   A (camera-major, one wavefront = 64 positions of one camera):
-//       e_o = J_c,o y_c,  u_o = M_o^T e_o               -> eu[i] (e 2 | u 3)
+// passes so that only per-point quantities are gathered:
+//   A (k_backsub_a_rc, camera-major, one wavefront = 64 positions of one
+//       camera): e_o = J_c,o y_c,  u_o = M_o^T e_o  -> eu at the
+//       observation's point-major slot (J and M recomputed)
 //   B (one lane per point):  y_p = L^-T (z_p - sum_o u_o),  delta_p = -y_p,
 //       X_new = X + s_p delta_p, |dX|^2, finite check  -> ypt[p], X_new
-//   C (camera-major): model residual q_o = -(e_o + J_X,o y_p),
-//       model cost change -= q . (r + q/2)   (ceres trust_region_minimizer),
-//       candidate residual at (cam_new, X_new).
+//   C (camera-major): candidate residual at (cam_new, X_new).
+// The model cost change (ceres trust_region_minimizer's -q.(r + q/2) with
+// q_o = -(e_o + J_X,o y_p)) is split between A and B (see below).
 // Camera runs are padded to whole wavefronts, so a wavefront never spans two
 // cameras (its camera comes from wcam) and padding lanes are masked.
-__global__ __launch_bounds__(kThreads) void k_backsub_a(int64_t N_pad, const int32_t* __restrict__ wcam,
-                                                        const int32_t* __restrict__ cam_obs,
-                                                        const double* __restrict__ jrec,
-                                                        const double* __restrict__ mrec,
-                                                        const double* __restrict__ ysol, double* __restrict__ eu,
-                                                        double* __restrict__ part_model) {
-  __shared__ __attribute__((aligned(16))) double stage[kThreads / 64][64 * (kJRec + kMRec)];
-  __shared__ double sh[4];
-  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
-  double model = 0.0;
-  if (i0 < N_pad) {
-  const double* y = ysol + 6 * size_t(wcam[i0 >> 6]);  // wave-uniform
-  double yc[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) yc[k] = y[k];
-  const double* J = wave_records<kJRec>(stage[wv], jrec + size_t(i0) * kJRec, l) + kJC;
-  const double* M = wave_records<kMRec>(stage[wv] + 64 * kJRec, mrec + size_t(i0) * kMRec, l);
-  double e0 = 0.0, e1 = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { e0 += J[k] * yc[k]; e1 += J[6 + k] * yc[k]; }
-  const double2 m01 = ld2(M), m23 = ld2(M + 2), m45 = ld2(M + 4);
-  const double2 rr = ld2(J - kJC + kRes);
-  wave_sync_lds();
-  // the observation's share of the model cost change (see k_backsub_b)
-  if (cam_obs[i0 + l] >= 0) model = e0 * rr.x + e1 * rr.y - 0.5 * (e0 * e0 + e1 * e1);
-  // M row-major 2x3 (m0 m1 m2 | n0 n1 n2) = M[0..5];  u = M^T e
-  double* o = stage[wv] + l * kEU;
-  st2(o, e0, e1);
-  st2(o + 2, m01.x * e0 + m23.y * e1, m01.y * e0 + m45.x * e1);
-  st2(o + 4, m23.x * e0 + m45.y * e1, 0.0);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double* dst = eu + i0 * kEU;
-#pragma unroll
-  for (int kq = 0; kq < kEU / 2; ++kq) {
-    const double2 v = ld2(stage[wv] + 2 * (64 * kq + l));
-    st2_nt(dst + 2 * (64 * kq + l), v.x, v.y);
-  }
-  }
-  const double r = block_reduce(model, sh, false);
-  if (threadIdx.x == 0) part_model[blockIdx.x] = r;
-}
 
 __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __restrict__ pt_off,
-                                                        const int32_t* __restrict__ pos,
                                                         const double* __restrict__ eu,
                                                         const double* __restrict__ ptL,
                                                         const double* __restrict__ ptV,
@@ -1394,7 +983,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
                                                         const double* __restrict__ X, double* __restrict__ X_new,
                                                         double* __restrict__ ypt, double* __restrict__ part_step,
                                                         double* __restrict__ part_bad,
-                                                        double* __restrict__ part_model, int upm) {
+                                                        double* __restrict__ part_model) {
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0, model = 0.0;
@@ -1405,9 +994,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;  // sum of u = L^-1 J_X^T e
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      // upm: u at the point-major slot (k_backsub_a_rc), else in the
-      // camera-major e|u record (k_backsub_a)
-      const double* u = upm ? eu + 4 * size_t(q) : eu + size_t(pos[q]) * kEU + 2;
+      const double* u = eu + 4 * size_t(q);  // point-major slot (pass A)
       const double2 u01 = ld2(u);
       const double u2 = u[2];
       w0 -= u01.x;
@@ -1421,9 +1008,9 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
     if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) bad = 1.0;
     // Model cost change, ceres' -sum_o m_o.(r_o + m_o/2) with m_o = -(e_o +
     // J_X,o y_p), split by observation and point:
-    //   sum_o (e.r - |e|^2/2)                      (k_backsub_a)
+    //   sum_o (e.r - |e|^2/2)                      (k_backsub_a_rc)
     //   + y.g_p - y.h_p - y^T V0_p y / 2           (here, per point)
-    // with g_p = sum J_X^T r and V0_p = sum J_X^T J_X (ptV, k_point_eval)
+    // with g_p = sum J_X^T r and V0_p = sum J_X^T J_X (ptV, k_point_eval_rc)
     // and h_p = sum J_X^T e = L_p sum u.  The candidate pass then reads no
     // Jacobian record at all.
     {
@@ -1535,15 +1122,14 @@ static inline double* slot(const DevProblem& d, int s) { return d.partials + siz
 void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s) {
   k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
 }
-void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool force_records) {
-  const bool rec = d.need_jrec || force_records;
-  k_jacobian<<<rec ? d.jac_blocks_rec : d.jac_blocks, kThreads, 0, s>>>(
+void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records) {
+  // the record-writing variant (evaluate API) runs on its own, smaller grid
+  k_jacobian<<<write_records ? d.jac_blocks_rec : d.jac_blocks, kThreads, 0, s>>>(
       d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X, d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
-      slot(d, kPCost), d.jpart, rec ? 1 : 0);
+      slot(d, kPCost), d.jpart, write_records ? 1 : 0);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
-  if (d.jpart) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);
-  else k_cam_reduce<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.jrec, d.Ucam);
+  if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
@@ -1552,74 +1138,33 @@ void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool co
 }
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
   if (d.P == 0) return;
-  if (d.uv_pm) {
-    k_point_eval_rc<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam,
-                                                                   d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag,
-                                                                   mode, reuse_diag ? 1 : 0, slot(d, kPGradPt),
-                                                                   slot(d, kPXNormPt));
-    return;
-  }
-  k_point_eval<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.jrec, d.X, d.scale_p, d.diag_p, d.ptV,
-                                                             d.min_diag, d.max_diag, mode, reuse_diag ? 1 : 0,
-                                                             slot(d, kPGradPt), slot(d, kPXNormPt));
+  k_point_eval_rc<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam,
+                                                                 d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag,
+                                                                 mode, reuse_diag ? 1 : 0, slot(d, kPGradPt),
+                                                                 slot(d, kPXNormPt));
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad), d.X, d.scale_p,
-                                                                         d.schur_pts ? d.ptS : nullptr);
+                                                                         slot(d, kPBad), d.X, d.scale_p, d.ptS);
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
-  if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad), d.X, d.scale_p,
-                                                                         d.schur_pts ? d.ptS : nullptr);
-  if (d.N_pad && d.obs_rc && d.dpart) {
+  launch_point_factor(d, radius, s);
+  if (d.N_pad)
     k_obs_prep_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
                                                                     d.cam, d.Kc, d.scale_c, d.ptS, d.ptL, d.dpart);
-    return;
-  }
-  if (d.N_pad)
-    k_obs_prep<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.cm_p, d.jrec, d.ptL, d.mrec,
-                                                                 d.schur_pts ? nullptr : d.frec, d.cam_obs,
-                                                                 d.dpart);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
-  if (d.n_blk && d.n_sitems) {
-    k_schur_split<<<blocks_for(d.n_sitems, kThreads), kThreads, 0, s>>>(d.n_sitems, d.sitems, d.pairs, d.frec,
-                                                                         d.spart);
-    k_schur_split_reduce<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.sboff, d.spart, d.S,
-                                                                            d.ld);
-  } else if (d.n_blk && d.schur_pts) {
-    if (d.dpart) {
-      launch_schur_diag_first(d, radius, add_diag, s);
-      launch_schur_pts(d, 0, s);
-      return;
-    }
-    launch_schur_pts(d, 0, s);
-  } else if (d.n_blk && d.schur_row && d.n_srow)
-    k_schur_row<<<d.n_srow, kThreads, 0, s>>>(d.srow, d.seg, d.pairs, d.frec, d.cam_rng, d.blk, d.S, d.ld);
-  else if (d.n_blk)
-    k_schur<<<blocks_for(d.n_blk, kThreads), kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.pairs, d.frec, d.S, d.ld);
-  if (d.dpart)
-    k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
-                                        d.n, 0);
-  else
-    k_schur_diag<<<d.C, kThreads, 0, s>>>(d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, radius,
-                                          add_diag ? 1 : 0, d.S, d.ld, d.n);
-}
-void launch_schur_diag_first(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
+  // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
+  // the off-diagonal blocks, which add a block's same-camera duplicate pairs
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
                                         d.n, 1);
-}
-void launch_schur_pts(const DevProblem& d, int sepoch, hipStream_t s) {
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
   const int nb = int((d.n_blk + per - 1) / per);
-  const int diag_add = d.dpart ? 1 : 0;
-  int* cnt = sepoch > 0 ? d.pcnt : nullptr;
 #define SFM_PTS(S_)                                                                                           \
   k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                          d.S, d.ld, diag_add, cnt, cnt ? nullptr : d.bperm)
+                                          d.S, d.ld, d.bperm)
   if (sub == 8) SFM_PTS(8);
   else if (sub == 16) SFM_PTS(16);
   else if (sub == 32) SFM_PTS(32);
@@ -1643,22 +1188,18 @@ void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
 }
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
-  if (d.N_pad && cams_var && d.obs_rc)
+  if (d.N_pad && cams_var)
     k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
                                                                      d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ptL,
                                                                      d.ysol, d.eu, slot(d, kPModel));
-  else if (d.N_pad && cams_var)
-    k_backsub_a<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.jrec, d.mrec, d.ysol,
-                                                                   d.eu, slot(d, kPModel));
   else if (d.N_pad) {
-    (void)hipMemsetAsync(d.eu, 0, sizeof(double) * kEU * size_t(d.N_pad), s);
+    (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.N), s);
     (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
   }
   if (d.P && pts_var) {
-    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.pos, d.eu, d.ptL, d.ptV, d.scale_p,
+    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.ptL, d.ptV, d.scale_p,
                                                                d.X, d.X_new, d.ypt, slot(d, kPStepPt),
-                                                               slot(d, kPBadBack), slot(d, kPModelPt),
-                                                               d.obs_rc ? 1 : 0);
+                                                               slot(d, kPBadBack), slot(d, kPModelPt));
   } else if (d.P) {
     // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
     const size_t nbP = size_t(blocks_for(d.P, kThreads));
@@ -1671,19 +1212,6 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   if (d.N_pad)
     k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
                                                                    d.X_new, d.camRn, slot(d, kPNewCost));
-}
-// Diagnostic (bench_jacobian SFM_JAC_THRASH=2): stream-read n doubles, no
-// stores but one word -- evicts caches without leaving dirty lines.
-__global__ void k_read_touch(const double2* __restrict__ p, size_t n2, double* __restrict__ out) {
-  double acc = 0.0;
-  for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x) {
-    const double2 v = p[i];
-    acc += v.x + v.y;
-  }
-  if (acc == 12345.678) out[0] = acc;
-}
-void launch_read_touch(const double* p, size_t n, double* out, hipStream_t s) {
-  k_read_touch<<<2048, 256, 0, s>>>(reinterpret_cast<const double2*>(p), n / 2, out);
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);

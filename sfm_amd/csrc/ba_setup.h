@@ -1,0 +1,46 @@
+// Launchers of the device-side problem setup (ba_setup.hip), driven by
+// sfm_ba_set_problem (ba_solver.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace sfm {
+
+// Temporary-storage bytes of the hipcub primitives for n items: which = 64 /
+// 32 (radix sort of uint64 / uint32 keys with int32 values), 1 / 2
+// (exclusive sum of int32 / int64).
+size_t setup_sort_bytes(int64_t n, int which);
+hipError_t sort_pairs64(void* tmp, size_t bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+                        int32_t* vout, int64_t n, uint64_t max_key, hipStream_t s);
+hipError_t sort_pairs32(void* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                        int32_t* vout, int64_t n, uint64_t max_key, hipStream_t s);
+hipError_t exclusive_sum32(void* tmp, size_t bytes, const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
+hipError_t exclusive_sum64(void* tmp, size_t bytes, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
+
+// err[0..2] = first observation with a bad camera index / point index /
+// non-finite uv (INT32_MAX: none); per-camera and per-point counts of the
+// observations with valid indices.
+void launch_validate(int64_t N, const double* uv, const int32_t* cam, const int32_t* pt, int C, int P, int32_t* err,
+                     int32_t* cam_cnt, int32_t* pt_cnt, hipStream_t s);
+void launch_pm_keys(int64_t N, const int32_t* cam, const int32_t* pt, int C, uint64_t* keys, int32_t* iota,
+                    hipStream_t s);
+void launch_gather_pm(int64_t N, const int32_t* order, const double* uv, const int32_t* cam, const int32_t* pt,
+                      double* uv_pm, int32_t* cam_pm, int32_t* pt_s, uint32_t* cam_key, int32_t* iota, hipStream_t s);
+void launch_fill_cm(int64_t N_pad, const int32_t* wcam, const int32_t* cam_rng, const int32_t* cam_off,
+                    const int32_t* cm_order, const int32_t* pt_s, const double* uv_pm, int32_t* cm_p, double* uv_cm,
+                    int32_t* cam_obs, int32_t* pos, hipStream_t s);
+void launch_chunk_keys(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, uint32_t* key,
+                       int32_t* iota, hipStream_t s);
+void launch_chunk_gather(int n, const int32_t* perm, const int4* ch, const uint32_t* key, int4* out, int32_t* grp,
+                         hipStream_t s);
+// cnt[i] (i < N) = pairs of camera-major list entry i; cnt[N] = 0
+void launch_pair_count(int64_t N, const int32_t* cm_order, const int32_t* cam_pm, const int32_t* pt_s,
+                       const int32_t* pt_off, int64_t* cnt, hipStream_t s);
+void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm, const int32_t* pt_s,
+                      const int32_t* pt_off, const int64_t* off, int C, uint32_t* key, int32_t* val, hipStream_t s);
+void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s);
+void launch_blk(int C, int2* blk, hipStream_t s);
+void launch_bperm_keys(int64_t n_blk, const int32_t* seg, uint32_t* key, int32_t* iota, hipStream_t s);
+
+}  // namespace sfm

@@ -1,0 +1,306 @@
+// Device-side problem setup for sfm_ba_set_problem (gfx950).
+//
+// The reference rebuilds its ceres::Problem on every call
+// (/root/reference/CTracker.cpp:672-691: one residual block per observation,
+// parameter blocks deduplicated by address), so the drop-in's per-call setup
+// is on the critical path of every keyframe BA.  Everything O(N) here runs on
+// the GPU from the caller's three observation arrays:
+//   * validation (index ranges, finite uv) and the per-camera / per-point
+//     observation counts;
+//   * point-major order: a stable radix sort on (point, camera) -- ties keep
+//     the caller's order, as the host definition did -- and the gathers of
+//     uv / camera / point into it; pt_off by an exclusive scan;
+//   * camera-major order: a stable radix sort of the point-major ids by
+//     camera (points ascending within a camera), padded per camera to whole
+//     64-wide wavefront chunks, with the chunk table grouped into 8 point
+//     slices (one per XCD, k_jacobian);
+//   * the Schur pair lists: for every observation o1 (camera-major), the
+//     observations o2 of its point with camera >= c1, o2 != o1, emitted as
+//     (block key, point) in (o1 camera-major, o2 ascending) order and stably
+//     radix-sorted by block: each block's list is exactly the sequential
+//     definition's; CSR offsets by binary search; the blocks by descending
+//     pair count for k_schur_pts' wave balance (stable).
+// Integer work only; every output is deterministic (no atomics decide an
+// order: the counters are commutative integer adds).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <climits>
+#include <cmath>
+#include "ba_setup.h"
+
+namespace sfm {
+namespace {
+
+constexpr int kT = 256;
+inline int nblocks(int64_t n) { return int(std::max<int64_t>(1, (n + kT - 1) / kT)); }
+
+// Camera counts go through a per-workgroup LDS histogram (a few hundred
+// cameras: one global counter per camera would serialise ~N/C atomics on
+// each); point counts are spread over P counters and go straight to memory.
+constexpr int kLdsCams = 8192;
+__global__ __launch_bounds__(kT) void k_validate(int64_t N, const double* __restrict__ uv,
+                                                 const int32_t* __restrict__ cam, const int32_t* __restrict__ pt, int C,
+                                                 int P, int32_t* __restrict__ err, int32_t* __restrict__ cam_cnt,
+                                                 int32_t* __restrict__ pt_cnt) {
+  __shared__ int32_t hist[kLdsCams];
+  const bool lds = C <= kLdsCams;
+  if (lds)
+    for (int c = threadIdx.x; c < C; c += kT) hist[c] = 0;
+  __syncthreads();
+  for (int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x; i < N; i += int64_t(gridDim.x) * kT) {
+    const int c = cam[i], p = pt[i];
+    const bool cok = c >= 0 && c < C, pok = p >= 0 && p < P;
+    const double2 u = reinterpret_cast<const double2*>(uv)[i];
+    const bool uok = isfinite(u.x) && isfinite(u.y);
+    if (!cok) atomicMin(err + 0, int32_t(i));
+    if (!pok) atomicMin(err + 1, int32_t(i));
+    if (!uok) atomicMin(err + 2, int32_t(i));
+    if (cok && pok) {
+      if (lds) atomicAdd(hist + c, 1);
+      else atomicAdd(cam_cnt + c, 1);
+      atomicAdd(pt_cnt + p, 1);
+    }
+  }
+  __syncthreads();
+  if (lds)
+    for (int c = threadIdx.x; c < C; c += kT)
+      if (hist[c]) atomicAdd(cam_cnt + c, hist[c]);
+}
+
+__global__ __launch_bounds__(kT) void k_pm_keys(int64_t N, const int32_t* __restrict__ cam,
+                                                const int32_t* __restrict__ pt, int C, uint64_t* __restrict__ keys,
+                                                int32_t* __restrict__ iota) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i >= N) return;
+  keys[i] = uint64_t(pt[i]) * uint64_t(C) + uint64_t(cam[i]);
+  iota[i] = int32_t(i);
+}
+
+__global__ __launch_bounds__(kT) void k_gather_pm(int64_t N, const int32_t* __restrict__ order,
+                                                  const double* __restrict__ uv, const int32_t* __restrict__ cam,
+                                                  const int32_t* __restrict__ pt, double* __restrict__ uv_pm,
+                                                  int32_t* __restrict__ cam_pm, int32_t* __restrict__ pt_s,
+                                                  uint32_t* __restrict__ cam_key, int32_t* __restrict__ iota) {
+  const int64_t q = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (q >= N) return;
+  const int64_t i = order[q];
+  reinterpret_cast<double2*>(uv_pm)[q] = reinterpret_cast<const double2*>(uv)[i];
+  const int c = cam[i];
+  cam_pm[q] = c;
+  pt_s[q] = pt[i];
+  cam_key[q] = uint32_t(c);
+  iota[q] = int32_t(q);
+}
+
+// Camera-major slot i (runs padded to 64): its point-major observation, the
+// point, uv, and the inverse map pos[q] = i.  Padding slots copy the
+// camera's last observation (never read back; cam_obs = -1 marks them).
+__global__ __launch_bounds__(kT) void k_fill_cm(int64_t N_pad, const int32_t* __restrict__ wcam,
+                                                const int32_t* __restrict__ cam_rng,
+                                                const int32_t* __restrict__ cam_off,
+                                                const int32_t* __restrict__ cm_order,
+                                                const int32_t* __restrict__ pt_s, const double* __restrict__ uv_pm,
+                                                int32_t* __restrict__ cm_p, double* __restrict__ uv_cm,
+                                                int32_t* __restrict__ cam_obs, int32_t* __restrict__ pos) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i >= N_pad) return;
+  const int c = wcam[i >> 6];
+  const int32_t j = int32_t(i - cam_rng[2 * c]);
+  const int32_t n_c = cam_off[c + 1] - cam_off[c];
+  const int32_t q = cm_order[cam_off[c] + min(j, n_c - 1)];
+  cm_p[i] = pt_s[q];
+  reinterpret_cast<double2*>(uv_cm)[i] = reinterpret_cast<const double2*>(uv_pm)[q];
+  cam_obs[i] = j < n_c ? q : -1;
+  if (j < n_c) pos[q] = int32_t(i);
+}
+
+// Chunk t of the (piece-major, camera-minor) chunk list: its XCD group is
+// the point slice of its first observation (.w holds that observation's
+// camera-major index until the gather clears it).
+__global__ __launch_bounds__(kT) void k_chunk_keys(int n, const int4* __restrict__ ch,
+                                                   const int32_t* __restrict__ cm_order,
+                                                   const int32_t* __restrict__ pt_s, int P, uint32_t* __restrict__ key,
+                                                   int32_t* __restrict__ iota) {
+  const int t = blockIdx.x * kT + threadIdx.x;
+  if (t >= n) return;
+  const int p0 = pt_s[cm_order[ch[t].w]];
+  key[t] = uint32_t(int64_t(p0) * 8 / max(1, P));
+  iota[t] = t;
+}
+
+__global__ __launch_bounds__(kT) void k_chunk_gather(int n, const int32_t* __restrict__ perm,
+                                                     const int4* __restrict__ ch, const uint32_t* __restrict__ key,
+                                                     int4* __restrict__ out, int32_t* __restrict__ grp) {
+  const int t = blockIdx.x * kT + threadIdx.x;
+  if (t < n) {
+    const int4 v = ch[perm[t]];
+    out[t] = make_int4(v.x, v.y, v.z, 0);
+  }
+  if (t <= 8) {  // grp[g] = first chunk of group g (lower bound in the sorted keys)
+    int lo = 0, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (int(key[mid]) < t) lo = mid + 1; else hi = mid;
+    }
+    grp[t] = lo;
+  }
+}
+
+// Pairs of the camera-major observation list entry i (unpadded): o2 in the
+// point's segment with camera >= c1, o2 != o1.
+__global__ __launch_bounds__(kT) void k_pair_count(int64_t N, const int32_t* __restrict__ cm_order,
+                                                   const int32_t* __restrict__ cam_pm,
+                                                   const int32_t* __restrict__ pt_s,
+                                                   const int32_t* __restrict__ pt_off, int64_t* __restrict__ cnt) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i > N) return;
+  if (i == N) { cnt[N] = 0; return; }
+  const int32_t o1 = cm_order[i];
+  const int c1 = cam_pm[o1], p = pt_s[o1];
+  int64_t k = 0;
+  for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2) k += (cam_pm[o2] >= c1 && o2 != o1) ? 1 : 0;
+  cnt[i] = k;
+}
+
+__device__ __forceinline__ int64_t row_start(int c1, int C) { return int64_t(c1) * C - int64_t(c1) * (c1 - 1) / 2; }
+
+__global__ __launch_bounds__(kT) void k_pair_fill(int64_t N, const int32_t* __restrict__ cm_order,
+                                                  const int32_t* __restrict__ cam_pm, const int32_t* __restrict__ pt_s,
+                                                  const int32_t* __restrict__ pt_off, const int64_t* __restrict__ off,
+                                                  int C, uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i >= N) return;
+  const int32_t o1 = cm_order[i];
+  const int c1 = cam_pm[o1], p = pt_s[o1];
+  const int64_t rs = row_start(c1, C) - c1;
+  int64_t k = off[i];
+  for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2) {
+    const int c2 = cam_pm[o2];
+    if (c2 >= c1 && o2 != o1) {
+      key[k] = uint32_t(rs + c2);
+      val[k] = p;
+      ++k;
+    }
+  }
+}
+
+// seg[b] = first pair of block b (lower bound of b in the sorted keys).
+__global__ __launch_bounds__(kT) void k_seg(int64_t n_blk, const uint32_t* __restrict__ key, int64_t n_pairs,
+                                            int32_t* __restrict__ seg) {
+  const int64_t b = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (b > n_blk) return;
+  int64_t lo = 0, hi = n_pairs;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (int64_t(key[mid]) < b) lo = mid + 1; else hi = mid;
+  }
+  seg[b] = int32_t(lo);
+}
+
+__global__ __launch_bounds__(kT) void k_blk(int C, int2* __restrict__ blk) {
+  const int c1 = blockIdx.y;
+  const int64_t rs = row_start(c1, C) - c1;
+  for (int c2 = c1 + int(blockIdx.x) * kT + int(threadIdx.x); c2 < C; c2 += int(gridDim.x) * kT)
+    blk[rs + c2] = make_int2(c1, c2);
+}
+
+// Blocks by descending pair count: ascending key INT32_MAX - count, stable.
+__global__ __launch_bounds__(kT) void k_bperm_keys(int64_t n_blk, const int32_t* __restrict__ seg,
+                                                   uint32_t* __restrict__ key, int32_t* __restrict__ iota) {
+  const int64_t b = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (b >= n_blk) return;
+  key[b] = uint32_t(INT32_MAX - (seg[b + 1] - seg[b]));
+  iota[b] = int32_t(b);
+}
+
+int bits_for(uint64_t max_key) {
+  int b = 1;
+  while (b < 64 && (max_key >> b) != 0) ++b;
+  return b;
+}
+
+}  // namespace
+
+size_t setup_sort_bytes(int64_t n, int which) {
+  size_t bytes = 0;
+  if (n <= 0) return 0;
+  if (which == 64)
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, int(n));
+  else if (which == 32)
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, int(n));
+  else if (which == 1)
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, int(n));
+  else
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr, int(n));
+  return bytes;
+}
+
+hipError_t sort_pairs64(void* tmp, size_t bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+                        int32_t* vout, int64_t n, uint64_t max_key, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, int(n), 0, bits_for(max_key), s);
+}
+hipError_t sort_pairs32(void* tmp, size_t bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                        int32_t* vout, int64_t n, uint64_t max_key, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, int(n), 0, bits_for(max_key), s);
+}
+hipError_t exclusive_sum32(void* tmp, size_t bytes, const int32_t* in, int32_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s);
+}
+hipError_t exclusive_sum64(void* tmp, size_t bytes, const int64_t* in, int64_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, int(n), s);
+}
+
+void launch_validate(int64_t N, const double* uv, const int32_t* cam, const int32_t* pt, int C, int P, int32_t* err,
+                     int32_t* cam_cnt, int32_t* pt_cnt, hipStream_t s) {
+  if (N <= 0) return;
+  k_validate<<<std::min(nblocks(N), 1024), kT, 0, s>>>(N, uv, cam, pt, C, P, err, cam_cnt, pt_cnt);
+}
+void launch_pm_keys(int64_t N, const int32_t* cam, const int32_t* pt, int C, uint64_t* keys, int32_t* iota,
+                    hipStream_t s) {
+  if (N > 0) k_pm_keys<<<nblocks(N), kT, 0, s>>>(N, cam, pt, C, keys, iota);
+}
+void launch_gather_pm(int64_t N, const int32_t* order, const double* uv, const int32_t* cam, const int32_t* pt,
+                      double* uv_pm, int32_t* cam_pm, int32_t* pt_s, uint32_t* cam_key, int32_t* iota,
+                      hipStream_t s) {
+  if (N > 0) k_gather_pm<<<nblocks(N), kT, 0, s>>>(N, order, uv, cam, pt, uv_pm, cam_pm, pt_s, cam_key, iota);
+}
+void launch_fill_cm(int64_t N_pad, const int32_t* wcam, const int32_t* cam_rng, const int32_t* cam_off,
+                    const int32_t* cm_order, const int32_t* pt_s, const double* uv_pm, int32_t* cm_p, double* uv_cm,
+                    int32_t* cam_obs, int32_t* pos, hipStream_t s) {
+  if (N_pad > 0)
+    k_fill_cm<<<nblocks(N_pad), kT, 0, s>>>(N_pad, wcam, cam_rng, cam_off, cm_order, pt_s, uv_pm, cm_p, uv_cm, cam_obs,
+                                            pos);
+}
+void launch_chunk_keys(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, uint32_t* key,
+                       int32_t* iota, hipStream_t s) {
+  if (n > 0) k_chunk_keys<<<nblocks(n), kT, 0, s>>>(n, ch, cm_order, pt_s, P, key, iota);
+}
+void launch_chunk_gather(int n, const int32_t* perm, const int4* ch, const uint32_t* key, int4* out, int32_t* grp,
+                         hipStream_t s) {
+  k_chunk_gather<<<nblocks(std::max(n, 9)), kT, 0, s>>>(n, perm, ch, key, out, grp);
+}
+void launch_pair_count(int64_t N, const int32_t* cm_order, const int32_t* cam_pm, const int32_t* pt_s,
+                       const int32_t* pt_off, int64_t* cnt, hipStream_t s) {
+  k_pair_count<<<nblocks(N + 1), kT, 0, s>>>(N, cm_order, cam_pm, pt_s, pt_off, cnt);
+}
+void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm, const int32_t* pt_s,
+                      const int32_t* pt_off, const int64_t* off, int C, uint32_t* key, int32_t* val, hipStream_t s) {
+  if (N > 0) k_pair_fill<<<nblocks(N), kT, 0, s>>>(N, cm_order, cam_pm, pt_s, pt_off, off, C, key, val);
+}
+void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s) {
+  k_seg<<<nblocks(n_blk + 1), kT, 0, s>>>(n_blk, key, n_pairs, seg);
+}
+void launch_blk(int C, int2* blk, hipStream_t s) {
+  if (C > 0) k_blk<<<dim3(unsigned((C + kT - 1) / kT), unsigned(C)), kT, 0, s>>>(C, blk);
+}
+void launch_bperm_keys(int64_t n_blk, const int32_t* seg, uint32_t* key, int32_t* iota, hipStream_t s) {
+  if (n_blk > 0) k_bperm_keys<<<nblocks(n_blk), kT, 0, s>>>(n_blk, seg, key, iota);
+}
+
+}  // namespace sfm

@@ -25,6 +25,7 @@
 #include <chrono>
 
 #include "ba_device.h"
+#include "ba_setup.h"
 #include "../../include/sfm_amd.h"
 
 namespace {
@@ -56,21 +57,13 @@ struct sfm_ba_handle {
   int device = 0;
   hipStream_t stream = nullptr;
   DevProblem d;
-  // host copies needed for reordering / reset
-  std::vector<int64_t> order;  // sorted position -> caller observation index
-  std::vector<int32_t> pos;      // point-major q -> camera-major record index
   int32_t mode = SFM_BA_STRUCT_AND_POSE;  // of the running solve (CTracker.h:67)
-  int32_t bs_epoch = 0;
-  int32_t schur_epoch = 0;       // launches of the fused Schur + Cholesky since the last set_problem
-  int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem          // stamp of the last back-substitution launch (k_backsolve flags)
+  int32_t bs_epoch = 0;          // stamp of the last back-substitution launch (k_backsolve flags)
+  int32_t chol_epoch = 0;        // launches of the fused Cholesky since the last set_problem
   bool force_pack = false;       // SFM_FORCE_PACK=1: exercise the packed all-reduce path on one rank (tests)
-  // concurrent Schur + Cholesky: the Cholesky runs on stream2, ordered by
-  // two events (created with the first overlapped step)
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int32_t pts_epoch = 0;         // overlapped k_schur_pts launches since the last set_problem
   std::vector<std::pair<size_t, void*>> allocs;  // (bytes, buffer) of the resident problem
-  std::multimap<size_t, void*> pool;             // buffers of the previous problem, reused by size
+  std::vector<std::pair<size_t, void*>> tmps;    // set_problem's scratch (back to the pool when it returns)
+  std::multimap<size_t, void*> pool;             // buffers of earlier problems, reused by size
   bool has_problem = false;
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -115,6 +108,19 @@ int dalloc(sfm_ba_handle* h, T** p, size_t count) {
   *p = static_cast<T*>(q);
   return 0;
 }
+// set_problem scratch: retired into the pool when set_problem returns
+template <typename T>
+int dalloc_tmp(sfm_ba_handle* h, T** p, size_t count) {
+  const int rc = dalloc(h, p, count);
+  if (rc) return rc;
+  h->tmps.push_back(h->allocs.back());
+  h->allocs.pop_back();
+  return 0;
+}
+void retire_tmps(sfm_ba_handle* h) {
+  for (auto& a : h->tmps) h->pool.insert(a);
+  h->tmps.clear();
+}
 
 void release_pool(sfm_ba_handle* h) {
   for (auto& kv : h->pool) hipFree(kv.second);
@@ -125,6 +131,7 @@ void release_pool(sfm_ba_handle* h) {
 void free_problem(sfm_ba_handle* h) {
   for (auto& a : h->allocs) h->pool.insert(a);
   h->allocs.clear();
+  retire_tmps(h);
   double* keep = h->d.scal_host;  // pinned mirror: kept for the handle's life
   h->d = DevProblem();
   h->d.scal_host = keep;
@@ -185,26 +192,6 @@ struct HostTimer {
     t0 = t1;
   }
 };
-
-// Dynamic parallel-for over [0, n) on up to 16 host threads (problem setup:
-// the per-camera copies and the Schur pair lists are independent per
-// camera / per row camera and dominated host time at C2-C4).
-template <class F>
-void parallel_for(int n, F f) {
-  const int nth = int(std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
-  if (n < 64 || nth == 1) {
-    for (int i = 0; i < n; ++i) f(i);
-    return;
-  }
-  std::atomic<int> next(0);
-  auto body = [&]() {
-    for (int i; (i = next.fetch_add(1)) < n;) f(i);
-  };
-  std::vector<std::thread> th;
-  for (int k = 1; k < nth; ++k) th.emplace_back(body);
-  body();
-  for (auto& x : th) x.join();
-}
 
 bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
 
@@ -313,47 +300,6 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhPtPrep);
     launch_point_prep(d, radius, s);
     mark_end(h);
-    if (!sharded(h) && !h->force_pack && d.schur_fused && d.schur_row && d.n_stasks && d.cflags && !d.n_sitems &&
-        !d.chol_stepwise) {
-      // single rank: Schur assembly and factorisation in one persistent
-      // launch (the padding rows are set first; they are no Schur output)
-      launch_pad_init(d, s);
-      mark_begin(h, kPhChol);
-      launch_schur_cholesky(d, radius, true, ++h->chol_epoch, ++h->schur_epoch, s);
-      mark_end(h);
-      mark_begin(h, kPhBack);
-      launch_backsolve(d, ++h->bs_epoch, s);
-      mark_end(h);
-      goto factored;
-    }
-    if (!sharded(h) && !h->force_pack && d.schur_overlap && d.cflags && !d.chol_stepwise) {
-      // single rank: the Cholesky runs CONCURRENTLY with the off-diagonal
-      // Schur blocks, its helpers gated per tile column on k_schur_pts'
-      // counts (rows are assembled in camera order, so the first columns
-      // are ready within a few percent of the Schur pass)
-      if (!h->stream2) {
-        HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
-      }
-      launch_pad_init(d, s);  // also clears the failure flag
-      mark_begin(h, kPhSchur);
-      launch_schur_diag_first(d, radius, true, s);
-      mark_end(h);
-      mark_begin(h, kPhChol);
-      HIPCHK(hipEventRecord(h->ev_fork, s));
-      HIPCHK(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-      const int sep = ++h->pts_epoch;
-      launch_cholesky(d, ++h->chol_epoch, h->stream2, false, sep);
-      launch_schur_pts(d, sep, s);
-      HIPCHK(hipEventRecord(h->ev_join, h->stream2));
-      HIPCHK(hipStreamWaitEvent(s, h->ev_join, 0));
-      mark_end(h);
-      mark_begin(h, kPhBack);
-      launch_backsolve(d, ++h->bs_epoch, s);
-      mark_end(h);
-      goto factored;
-    }
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
@@ -370,13 +316,12 @@ int compute_step(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s);
     mark_end(h);
-  factored:;
   } else if (h->mode == SFM_BA_POSE_ONLY) {
     // block-diagonal camera system from the all-reduced U_c (same on every rank)
     launch_cam_solve(d, radius, s);
-    // the record-free back substitution reads X from the point records
-    // (their factor is unused here: y_p = 0); its bad flags are cleared below
-    if (d.obs_rc && d.P) launch_point_factor(d, radius, s);
+    // the back substitution reads X from the point records (their factor
+    // is unused here: y_p = 0); its bad flags are cleared below
+    if (d.P) launch_point_factor(d, radius, s);
     hipMemsetAsync(d.partials + size_t(kPBad) * d.max_blocks, 0, sizeof(double) * nbP, s);
   } else {
     // STRUCT_ONLY: per-point 3x3 systems only; y_c = 0
@@ -496,12 +441,6 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->d.scal_host) hipHostFree(h->d.scal_host);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
-  if (h->stream2) {
-    hipStreamSynchronize(h->stream2);
-    hipStreamDestroy(h->stream2);
-  }
-  if (h->ev_fork) hipEventDestroy(h->ev_fork);
-  if (h->ev_join) hipEventDestroy(h->ev_join);
   hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -548,15 +487,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   if (n_obs > 0 && (!obs_uv || !cam_idx || !pt_idx)) return fail(SFM_EINVAL, "observation arrays are NULL");
   if (n_cams > 0 && (!K9 || !rot || !t)) return fail(SFM_EINVAL, "camera arrays are NULL");
   if (n_pts > 0 && !X) return fail(SFM_EINVAL, "point array is NULL");
-  if (n_obs > int64_t(INT32_MAX)) return fail(SFM_EINVAL, "more than 2^31-1 observations per shard");
-  for (int64_t i = 0; i < n_obs; ++i) {
-    if (cam_idx[i] < 0 || cam_idx[i] >= n_cams) return fail(SFM_EINVAL, "cam_idx out of range at " + std::to_string(i));
-    if (pt_idx[i] < 0 || pt_idx[i] >= n_pts) return fail(SFM_EINVAL, "pt_idx out of range at " + std::to_string(i));
-    if (!std::isfinite(obs_uv[2 * i]) || !std::isfinite(obs_uv[2 * i + 1]))
-      return fail(SFM_EINVAL, "non-finite observation at " + std::to_string(i));
-  }
+  if (n_obs > int64_t(INT32_MAX) - 64 * int64_t(n_cams))
+    return fail(SFM_EINVAL, "more than 2^31-1 observations per shard");
   HostTimer timer;
-  timer.mark("validate");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
   free_problem(h);
@@ -564,187 +497,104 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   const int64_t N = n_obs;
   const int C = n_cams, P = n_pts;
   d.C = C; d.P = P; d.N = N;
-  // ---- point-major order, cameras ascending within a point (stable) ----
-  std::vector<int32_t> pt_off(size_t(P) + 1, 0);
-  for (int64_t i = 0; i < N; ++i) pt_off[pt_idx[i] + 1]++;
-  for (int p = 0; p < P; ++p) pt_off[p + 1] += pt_off[p];
-  h->order.assign(N, 0);
+  hipStream_t s = h->stream;
+  int rc = 0;
+  // Any failure returns through here: the buffers go back to the pool.
+  auto bail = [&](int code) {
+    free_problem(h);
+    return code;
+  };
+#define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) return bail(rc)
+#define TMP(ptr, cnt) if ((rc = dalloc_tmp(h, &(ptr), (cnt)))) return bail(rc)
+#define HCHK(expr)                                                                                \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return bail(fail(SFM_EIO, std::string(#expr) + ": " + hipGetErrorString(e_))); \
+  } while (0)
+  // ---- the caller's observation arrays go up as they are; the O(N) layout
+  // work runs on the device (ba_setup.hip) ----
+  double* in_uv = nullptr;
+  int32_t *in_cam = nullptr, *in_pt = nullptr, *err = nullptr, *cnt_c = nullptr, *cnt_p = nullptr;
+  TMP(in_uv, 2 * size_t(N));
+  TMP(in_cam, size_t(N));
+  TMP(in_pt, size_t(N));
+  TMP(err, 4);
+  TMP(cnt_c, size_t(C) + 1);
+  TMP(cnt_p, size_t(P) + 1);
+  if (N) {
+    HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
+    HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
+    HCHK(hipMemcpyAsync(in_pt, pt_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
+  }
+  HCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), INT32_MAX, 4, s));
+  HCHK(hipMemsetAsync(cnt_c, 0, sizeof(int32_t) * (size_t(C) + 1), s));
+  HCHK(hipMemsetAsync(cnt_p, 0, sizeof(int32_t) * (size_t(P) + 1), s));
+  launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+  // one round trip: the first bad observation and the per-camera counts
+  // (the host lays out the C camera runs and the wavefront chunk table)
+  std::vector<int32_t> cam_cnt(size_t(C) + 4);
+  HCHK(hipMemcpyAsync(cam_cnt.data(), err, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, s));
+  if (C) HCHK(hipMemcpyAsync(cam_cnt.data() + 4, cnt_c, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost, s));
+  HCHK(hipStreamSynchronize(s));
+  timer.mark("upload + validate");
   {
-    std::vector<int32_t> fill(pt_off.begin(), pt_off.end() - 1);
-    for (int64_t i = 0; i < N; ++i) h->order[fill[pt_idx[i]]++] = i;
-    for (int p = 0; p < P; ++p) {
-      int64_t* b = h->order.data() + pt_off[p];
-      int64_t* e = h->order.data() + pt_off[p + 1];
-      std::stable_sort(b, e, [&](int64_t x, int64_t y) { return cam_idx[x] < cam_idx[y]; });
+    const int32_t e0 = cam_cnt[0], e1 = cam_cnt[1], e2 = cam_cnt[2];
+    const int32_t first = std::min({e0, e1, e2});
+    if (first != INT32_MAX) {
+      const char* what = first == e0 ? "cam_idx out of range at " : first == e1 ? "pt_idx out of range at "
+                                                                                   : "non-finite observation at ";
+      return bail(fail(SFM_EINVAL, what + std::to_string(first)));
     }
   }
-  timer.mark("point-major order");
-  std::vector<double> uv_s(2 * size_t(N));
-  std::vector<int32_t> cam_s(N), pt_s(N);
-  for (int64_t q = 0; q < N; ++q) {
-    const int64_t i = h->order[q];
-    uv_s[2 * q] = obs_uv[2 * i];
-    uv_s[2 * q + 1] = obs_uv[2 * i + 1];
-    cam_s[q] = cam_idx[i];
-    pt_s[q] = pt_idx[i];
-  }
-  std::vector<int32_t> cam_off(size_t(C) + 1, 0), cam_obs(N);
-  for (int64_t q = 0; q < N; ++q) cam_off[cam_s[q] + 1]++;
-  for (int c = 0; c < C; ++c) cam_off[c + 1] += cam_off[c];
-  {
-    std::vector<int32_t> fill(cam_off.begin(), cam_off.end() - 1);
-    for (int64_t q = 0; q < N; ++q) cam_obs[fill[cam_s[q]]++] = int32_t(q);
-  }
-  // ---- record layout: camera-major, each camera's run padded to a whole
-  // number of 64-record wavefront chunks (padding duplicates the camera's
-  // last observation and is never read back), so k_jacobian stores whole
-  // 10-KB chunks with no predication ----
-  std::vector<int32_t> cam_rng(2 * size_t(C));
+  // ---- camera runs: camera-major, each camera's run padded to a whole
+  // number of 64-wide wavefront chunks; the chunk table piece-major across
+  // cameras (grouped into 8 point slices on the device, one per XCD) ----
+  std::vector<int32_t> cam_off(size_t(C) + 1, 0), cam_rng(2 * size_t(C));
   int64_t npad = 0;
   for (int c = 0; c < C; ++c) {
-    const int32_t n_c = cam_off[c + 1] - cam_off[c];
+    const int32_t n_c = cam_cnt[4 + c];
+    cam_off[c + 1] = cam_off[c] + n_c;
     cam_rng[2 * c] = int32_t(npad);
     cam_rng[2 * c + 1] = int32_t(npad + n_c);
     npad += (n_c + 63) / 64 * 64;
   }
   d.N_pad = npad;
-  // (camera, first position, count, 0) per wavefront chunk, in 8 groups by
-  // the point slice of the chunk's first observation (k_jacobian serves
-  // group b % 8 from workgroup b: one slice of X per XCD's L2); within a
-  // group, piece-major across cameras.
-  std::vector<int32_t> jchunks, jgrp(9, 0);
-  {
-    std::vector<std::vector<int32_t>> grp(8);
-    for (int32_t k = 0;; ++k) {
-      bool any = false;
-      for (int c = 0; c < C; ++c) {
-        const int32_t n_c = cam_off[c + 1] - cam_off[c];
-        if (64 * k >= n_c) continue;
-        any = true;
-        const int32_t p0 = pt_s[cam_obs[cam_off[c] + 64 * k]];
-        const int g = int(int64_t(p0) * 8 / std::max(1, P));
-        grp[g].insert(grp[g].end(), {c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), 0});
-      }
-      if (!any) break;
+  std::vector<int32_t> wcam(size_t(npad / 64) + 1, 0);
+  for (int c = 0; c < C; ++c)
+    for (int64_t w = cam_rng[2 * c] / 64; w < (int64_t(cam_rng[2 * c]) + cam_off[c + 1] - cam_off[c] + 63) / 64; ++w)
+      wcam[w] = c;
+  std::vector<int4> chunks;  // (camera, first position, count, first observation's camera-major index)
+  for (int32_t k = 0;; ++k) {
+    bool any = false;
+    for (int c = 0; c < C; ++c) {
+      const int32_t n_c = cam_off[c + 1] - cam_off[c];
+      if (64 * k >= n_c) continue;
+      any = true;
+      chunks.push_back(make_int4(c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), cam_off[c] + 64 * k));
     }
-    for (int g = 0; g < 8; ++g) {
-      jchunks.insert(jchunks.end(), grp[g].begin(), grp[g].end());
-      jgrp[g + 1] = int32_t(jchunks.size() / 4);
-    }
+    if (!any) break;
   }
-  d.n_jchunks = int32_t(jchunks.size() / 4);
-  d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
+  d.n_jchunks = int32_t(chunks.size());
+  d.jac_blocks_rec = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
+  // the record-free pass of the solve (no 160-B stores) prefers a larger
+  // grid: 256 workgroups per XCD, 0.256 -> 0.223 ms per C3 solve
+  d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 256));
   if (const char* jw = std::getenv("SFM_JAC_WG_PER_XCD")) {  // tuning knob (tools/sweep_jac.sh)
     const int v = std::atoi(jw);
     if (v > 0) d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, v));
   }
-  timer.mark("camera-major + chunks");
-  // camera-major copies for the Jacobian pass and the record map
-  std::vector<int32_t> cm_p(npad, 0), pos(N), cam_obs_pad(npad, -1), wcam(size_t(npad / 64) + 1, 0);
-  for (int c = 0; c < C; ++c)
-    for (int64_t w = cam_rng[2 * c] / 64; w < (cam_rng[2 * c] + (cam_off[c + 1] - cam_off[c]) + 63) / 64; ++w) wcam[w] = c;
-  std::vector<double> uv_cm(2 * size_t(npad), 0.0);
-  parallel_for(C, [&](int c) {
-    const int32_t n_c = cam_off[c + 1] - cam_off[c];
-    const int32_t padded = (n_c + 63) / 64 * 64;
-    for (int32_t j = 0; j < padded; ++j) {
-      const int32_t q = cam_obs[cam_off[c] + std::min(j, n_c - 1)];
-      const int64_t i = cam_rng[2 * c] + j;
-      cm_p[i] = pt_s[q];
-      uv_cm[2 * i] = uv_s[2 * size_t(q)];
-      uv_cm[2 * i + 1] = uv_s[2 * size_t(q) + 1];
-      if (j < n_c) {
-        pos[q] = int32_t(i);
-        cam_obs_pad[i] = q;
-      }
-    }
-  });
   std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
   for (int c = 0; c < C; ++c) {
     const double* k = K9 + 9 * size_t(c);
     Kc[5 * c] = k[0]; Kc[5 * c + 1] = k[1]; Kc[5 * c + 2] = k[2]; Kc[5 * c + 3] = k[4]; Kc[5 * c + 4] = k[5];
     for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
   }
-  // ---- Schur blocks (k_schur): every upper-triangle block (c1, c2),
-  // c1 <= c2, in row-major order, with the CSR list of its (o1, o2) pairs:
-  // observations of a common point with cameras c1 and c2 (o2 != o1; on the
-  // diagonal only same-camera duplicates), as camera-major record positions. ----
-  timer.mark("camera-major copies");
-  std::vector<int32_t> blk, seg, pairs, bpts;
-  {
-    // two parallel passes over the row cameras c1: pair counts per block,
-    // then the pairs at their CSR offsets, in the order of the sequential
-    // definition (o1 in c1's camera-major order, o2 ascending in its point)
-    std::vector<int64_t> rowstart(size_t(C) + 1, 0);
-    for (int c1 = 0; c1 < C; ++c1) rowstart[c1 + 1] = rowstart[c1] + (C - c1);
-    const int64_t nblk = rowstart[C];
-    std::vector<int32_t> cnt(size_t(nblk) + 1, 0);
-    parallel_for(C, [&](int c1) {
-      int32_t* row = cnt.data() + rowstart[c1] - c1;  // row[c2], c2 >= c1
-      for (int32_t i = cam_off[c1]; i < cam_off[c1 + 1]; ++i) {
-        const int32_t o1 = cam_obs[i];
-        const int p = pt_s[o1];
-        for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
-          if (cam_s[o2] >= c1 && o2 != o1) ++row[cam_s[o2]];
-      }
-    });
-    int64_t total = 0;
-    for (int64_t b = 0; b < nblk; ++b) total += cnt[b];
-    if (total >= int64_t(INT32_MAX)) return fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets");
-    seg.assign(size_t(nblk) + 1, 0);
-    for (int64_t b = 0; b < nblk; ++b) seg[b + 1] = seg[b] + cnt[b];
-    pairs.assign(2 * size_t(seg[nblk]), 0);
-    bpts.assign(size_t(seg[nblk]), 0);
-    blk.resize(2 * size_t(nblk));
-    for (int c1 = 0; c1 < C; ++c1)
-      for (int c2 = c1; c2 < C; ++c2) {
-        const int64_t b = rowstart[c1] + (c2 - c1);
-        blk[2 * b] = c1;
-        blk[2 * b + 1] = c2;
-      }
-    parallel_for(C, [&](int c1) {
-      std::vector<int32_t> cur(seg.begin() + rowstart[c1], seg.begin() + rowstart[c1 + 1]);  // cursor per c2 - c1
-      for (int32_t i = cam_off[c1]; i < cam_off[c1 + 1]; ++i) {
-        const int32_t o1 = cam_obs[i];
-        const int p = pt_s[o1];
-        for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
-          if (cam_s[o2] >= c1 && o2 != o1) {
-            const int32_t k = cur[cam_s[o2] - c1]++;
-            pairs[2 * size_t(k)] = pos[o1];
-            pairs[2 * size_t(k) + 1] = pos[o2];
-            bpts[size_t(k)] = p;
-          }
-      }
-    });
-  }
-  timer.mark("schur pair lists");
-  {
-    const char* rs = std::getenv("SFM_SCHUR_ROW");
-    d.schur_row = rs ? std::atoi(rs) : 1;
-  }
-  // k_schur_row work items: each row c1 (blocks (c1, c1..C-1), consecutive in
-  // the row-major block order) cut into segments of at most kThreads blocks.
-  std::vector<int4> srow;
-  {
-    int64_t bfirst = 0;
-    for (int c1 = 0; c1 < C; ++c1) {
-      const int nrow = C - c1;
-      for (int o = 0; o < nrow; o += 256) srow.push_back(make_int4(c1, int(bfirst + o), std::min(256, nrow - o), 0));
-      bfirst += nrow;
-    }
-  }
-  d.n_blk = int64_t(blk.size() / 2);
-  d.n_pairs = int64_t(pairs.size() / 2);
-  // ---- dense system geometry ----
-  d.n = 6 * C;
-  d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
-  d.nblk = d.ld / kNB;
-  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks,
-                           blocks_for(npad, 256)});
-  // ---- device allocation ----
-  int rc = 0;
-#define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) { free_problem(h); return rc; }
+  timer.mark("camera runs (host)");
+  // ---- resident arrays of the point-major and camera-major layouts ----
   ALLOC(d.pt_off, size_t(P) + 1);
+  ALLOC(d.order, size_t(N));
+  ALLOC(d.uv_pm, 2 * size_t(N));
+  ALLOC(d.cam_pm, size_t(N));
   ALLOC(d.cam_obs, size_t(npad));
   ALLOC(d.cam_rng, 2 * size_t(C));
   ALLOC(d.cm_p, size_t(npad));
@@ -752,6 +602,106 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.jgrp, size_t(9));
   ALLOC(d.uv_cm, 2 * size_t(npad));
   ALLOC(d.pos, size_t(N));
+  ALLOC(d.wcam, wcam.size());
+  // scratch of the sorts
+  uint64_t *k64a = nullptr, *k64b = nullptr;
+  uint32_t *k32a = nullptr, *k32b = nullptr;
+  int32_t *iota = nullptr, *pt_s = nullptr, *cm_order = nullptr, *d_cam_off = nullptr, *perm = nullptr;
+  int4* ch_in = nullptr;
+  void* sort_tmp = nullptr;
+  const int64_t nch = d.n_jchunks;
+  const int64_t nmax = std::max<int64_t>({N, nch, 1});
+  TMP(k64a, size_t(N));
+  TMP(k64b, size_t(N));
+  TMP(k32a, size_t(nmax));
+  TMP(k32b, size_t(nmax));
+  TMP(iota, size_t(nmax));
+  TMP(pt_s, size_t(N));
+  TMP(cm_order, size_t(N));
+  TMP(d_cam_off, size_t(C) + 1);
+  TMP(perm, size_t(std::max<int64_t>(1, nch)));
+  TMP(ch_in, size_t(std::max<int64_t>(1, nch)));
+  size_t sort_bytes = std::max({setup_sort_bytes(N, 64), setup_sort_bytes(nmax, 32), setup_sort_bytes(P + 1, 1),
+                                setup_sort_bytes(N + 1, 2), size_t(256)});
+  {
+    uint8_t* tb = nullptr;
+    TMP(tb, sort_bytes);
+    sort_tmp = tb;
+  }
+  HCHK(hipMemcpyAsync(d.cam_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size(), hipMemcpyHostToDevice, s));
+  HCHK(hipMemcpyAsync(d_cam_off, cam_off.data(), sizeof(int32_t) * cam_off.size(), hipMemcpyHostToDevice, s));
+  HCHK(hipMemcpyAsync(d.wcam, wcam.data(), sizeof(int32_t) * wcam.size(), hipMemcpyHostToDevice, s));
+  if (nch) HCHK(hipMemcpyAsync(ch_in, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice, s));
+  // point-major order: stable sort by (point, camera)
+  launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
+  HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
+                    uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
+  launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
+  HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
+  // camera-major order of the point-major ids: stable sort by camera
+  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
+  launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
+  // chunk table grouped by point slice (stable: piece-major order kept)
+  launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
+  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
+  launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
+  // Schur pair counts: the second (and last) round trip
+  int64_t* pcnt = nullptr;
+  int64_t* poff = nullptr;
+  TMP(pcnt, size_t(N) + 1);
+  TMP(poff, size_t(N) + 1);
+  launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
+  HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
+  int64_t n_pairs = 0;
+  HCHK(hipMemcpyAsync(&n_pairs, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HCHK(hipStreamSynchronize(s));
+  timer.mark("layouts (device)");
+  if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
+  d.n_blk = int64_t(C) * (C + 1) / 2;
+  d.n_pairs = n_pairs;
+  ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
+  ALLOC(d.seg, size_t(d.n_blk) + 1);
+  ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
+  ALLOC(d.bperm, std::max<size_t>(1, size_t(d.n_blk)));
+  {
+    uint32_t *bk_a = nullptr, *bk_b = nullptr;
+    int32_t* bv = nullptr;
+    const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});
+    TMP(bk_a, size_t(nk));
+    TMP(bk_b, size_t(nk));
+    TMP(bv, size_t(nk));
+    const size_t need = std::max(setup_sort_bytes(n_pairs, 32), setup_sort_bytes(d.n_blk, 32));
+    if (need > sort_bytes) {
+      uint8_t* tb = nullptr;
+      TMP(tb, need);
+      sort_tmp = tb;
+      sort_bytes = need;
+    }
+    launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
+    HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
+                      s));
+    launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
+    launch_blk(C, d.blk, s);
+    launch_bperm_keys(d.n_blk, d.seg, bk_a, iota, s);
+    HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, iota, d.bperm, d.n_blk, uint64_t(INT32_MAX), s));
+  }
+  // lanes per Schur block ~ a tenth of the mean pair count, 8..64 (measured
+  // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
+  if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
+    const int v = std::atoi(ss);
+    d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
+  } else {
+    const double avg = d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0;
+    int sub = 8;
+    while (sub < 64 && sub < avg / 10.0) sub *= 2;
+    d.schur_pts_sub = sub;
+  }
+  // ---- parameters, per-iteration arrays, dense system ----
+  d.n = 6 * C;
+  d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
+  d.nblk = d.ld / kNB;
+  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks,
+                           d.jac_blocks_rec, blocks_for(npad, 256)});
   ALLOC(d.Kc, 5 * size_t(C));
   ALLOC(d.cam, 6 * size_t(C));
   ALLOC(d.cam_new, 6 * size_t(C));
@@ -765,15 +715,14 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.diag_p, 3 * size_t(P));
   ALLOC(d.camR, size_t(kCamR) * C);
   ALLOC(d.camRn, 12 * size_t(C));
-  ALLOC(d.jrec, size_t(kJRec) * npad);
-  ALLOC(d.mrec, size_t(kMRec) * npad);
-  ALLOC(d.frec, size_t(kFRec) * npad);
-  ALLOC(d.eu, size_t(kEU) * npad);
+  ALLOC(d.eu, size_t(kEU) * N);
   ALLOC(d.ypt, 3 * size_t(P));
-  ALLOC(d.wcam, size_t(npad / 64) + 1);
   ALLOC(d.ptV, size_t(kPtV) * P);
   ALLOC(d.ptL, size_t(kPtL) * P);
+  ALLOC(d.ptS, size_t(kPtS) * std::max(1, P));
   ALLOC(d.Ucam, size_t(kUcam) * C);
+  ALLOC(d.jpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
+  ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
   ALLOC(d.S, size_t(d.ld) * d.ld);
   h->force_pack = env_flag("SFM_FORCE_PACK");
   if (sharded(h) || h->force_pack) ALLOC(d.Spack, packed_size(d.n));
@@ -783,230 +732,36 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.cticket, 1);
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
-  ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
-  ALLOC(d.pairs, std::max<size_t>(1, size_t(d.n_pairs)));
-  ALLOC(d.seg, seg.size());
-  d.n_srow = int32_t(srow.size());
-  ALLOC(d.srow, std::max<size_t>(1, srow.size()));
-  // small problems: split every block's pair list into chunks (k_schur_split)
-  std::vector<int4> sitems;
-  std::vector<int32_t> sboff;
-  {
-    int64_t kSplitMaxBlocks = 8192;  // C1: 210, C2: 5050, C3: 125250 blocks
-    // chunk length: enough items to fill the chip, few partials to reduce
-    // (measured best: 16 pairs at C1's 0.1M pairs, 64 at C2's 2.3M)
-    int kSplitPairs = int(std::min<int64_t>(64, std::max<int64_t>(16, d.n_pairs / 32768)));
-    if (const char* e = std::getenv("SFM_SCHUR_SPLIT_MAXBLK")) kSplitMaxBlocks = std::atoll(e);
-    if (const char* e = std::getenv("SFM_SCHUR_SPLIT_PAIRS")) kSplitPairs = std::max(1, std::atoi(e));
-    // (default off: the recomputed-F k_schur_pts at 64 lanes per block is
-    // faster on the keyframe sizes too -- C1 Schur 0.35 -> 0.07 ms per solve;
-    // SFM_SCHUR_SPLIT=1, or SFM_SCHUR_PTS=0, brings the split back)
-    const char* sp = std::getenv("SFM_SCHUR_SPLIT");
-    const char* pe = std::getenv("SFM_SCHUR_PTS");
-    const bool pts_on = pe ? std::atoi(pe) != 0 : true;
-    const bool split = (sp ? std::atoi(sp) != 0 : !pts_on) && d.n_blk > 0 && d.n_blk <= kSplitMaxBlocks;
-    if (split) {
-      sboff.push_back(0);
-      for (int64_t b = 0; b < d.n_blk; ++b) {
-        const int k0 = seg[b], k1 = seg[b + 1];
-        if (k1 == k0) sitems.push_back(make_int4(int(b), k0, k1, 0));
-        for (int k = k0; k < k1; k += kSplitPairs) sitems.push_back(make_int4(int(b), k, std::min(k1, k + kSplitPairs), 0));
-        sboff.push_back(int32_t(sitems.size()));
-      }
-    }
-  }
-  d.n_sitems = int32_t(sitems.size());
-  // fused Schur + Cholesky task table (k_chol_schur_fused, chol_kernels.hip)
-  std::vector<int4> stasks;
-  std::vector<int32_t> scnt_init, pcnt_init, bperm;
-  {
-    const int nb = d.nblk;
-    std::vector<int32_t> target(nb, 0);
-    std::vector<std::vector<int4>> items(nb);  // Schur items by the first tile column of their camera
-    size_t si = 0;
-    for (int c = 0; c < C; ++c) {
-      const int j0 = (6 * c) / kNB, j1 = (6 * c + 5) / kNB;
-      int nitem = 0;
-      bool first = true;
-      for (; si < srow.size() && srow[si].x == c; ++si, ++nitem, first = false)
-        items[j0].push_back(make_int4(first ? 0 : 3, c, srow[si].y, srow[si].z));
-      items[j0].push_back(make_int4(1, c, 0, 0));
-      ++nitem;
-      for (int j = j0; j <= j1; ++j) target[j] += nitem;
-    }
-    // Schur items run this many tile columns ahead of the tiles
-    int kLook = 16;  // best of 4 / 8 / 16 / 64 at C3
-    if (const char* lk = std::getenv("SFM_SCHUR_LOOKAHEAD")) kLook = std::max(1, std::atoi(lk));
-    int emitted = -1;
-    auto emit_upto = [&](int jmax) {
-      for (; emitted < std::min(jmax, nb - 1);) {
-        ++emitted;
-        stasks.insert(stasks.end(), items[emitted].begin(), items[emitted].end());
-      }
-    };
-    emit_upto(kLook - 1);
-    for (int j = 0; j < nb; ++j) {
-      for (int i = j; i < nb; ++i) stasks.push_back(make_int4(2, i, j, 0));
-      emit_upto(j + kLook);
-    }
-    scnt_init.assign(2 * size_t(nb) + size_t(C), 0);
-    for (int j = 0; j < nb; ++j) scnt_init[nb + j] = target[j];
-  }
-  d.n_stasks = int32_t(stasks.size());
-  {
-    // experimental, off by default: measured slower at C3 (2.15 ms per fused
-    // launch at the best lookahead vs 0.69 + 1.10 ms for the two launches):
-    // inside the Cholesky's footprint (421 VGPRs, 108 KB LDS: one workgroup
-    // of four waves per CU) the gather-bound Schur items lose the occupancy
-    // they need
-    const char* sf = std::getenv("SFM_SCHUR_FUSED");
-    d.schur_fused = sf ? std::atoi(sf) != 0 : false;
-  }
-  {
-    const char* pr = std::getenv("SFM_PTEVAL_RC");
-    if (!pr || std::atoi(pr) != 0) {
-      ALLOC(d.uv_pm, 2 * std::max<size_t>(1, size_t(N)));
-      ALLOC(d.cam_pm, std::max<size_t>(1, size_t(N)));
-    }
-  }
-  {
-    const char* cf = std::getenv("SFM_CAM_FUSED");
-    if (!cf || std::atoi(cf) != 0) ALLOC(d.jpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
-  }
-  {
-    const char* df = std::getenv("SFM_SCHUR_DIAG_FUSED");
-    if (!df || std::atoi(df) != 0) ALLOC(d.dpart, 27 * std::max<size_t>(1, size_t(npad / 64)));
-  }
-  {
-    // k_schur_pts (recomputed F, point-record gathers) wherever the row /
-    // thread-per-block kernels would run; SFM_SCHUR_PTS=0 restores those
-    const char* sp = std::getenv("SFM_SCHUR_PTS");
-    d.schur_pts = (sp ? std::atoi(sp) != 0 : true) && d.n_blk > 0 && sitems.empty() && !d.schur_fused;
-    if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
-      const int v = std::atoi(ss);
-      d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
-    } else {
-      // lanes per block ~ a tenth of the mean pair count, 8..64 (measured
-      // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
-      const double avg = d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0;
-      int sub = 8;
-      while (sub < 64 && sub < avg / 10.0) sub *= 2;
-      d.schur_pts_sub = sub;
-    }
-    if (d.schur_pts) {
-      ALLOC(d.bpts, std::max<size_t>(1, bpts.size()));
-      ALLOC(d.ptS, size_t(kPtS) * std::max(1, P));
-      // k_schur_pts workgroups per tile column (the columns of their blocks'
-      // row cameras), for the Cholesky launched concurrently
-      const int64_t per = int64_t(64 / d.schur_pts_sub) * 4;
-      pcnt_init.assign(2 * size_t(d.nblk), 0);
-      for (int64_t b0 = 0; b0 < d.n_blk; b0 += per) {
-        const int64_t b1 = std::min(b0 + per, d.n_blk) - 1;
-        const int j0 = (6 * blk[2 * b0]) / kNB, j1 = (6 * blk[2 * b1] + 5) / kNB;
-        for (int j = j0; j <= j1; ++j) ++pcnt_init[size_t(d.nblk) + j];
-      }
-      ALLOC(d.pcnt, pcnt_init.size());
-      if (!env_flag("SFM_SCHUR_PTS_NOPERM")) {
-        bperm.resize(size_t(d.n_blk));
-        for (int64_t b = 0; b < d.n_blk; ++b) bperm[b] = int32_t(b);
-        std::stable_sort(bperm.begin(), bperm.end(),
-                         [&](int32_t a, int32_t b) { return seg[a + 1] - seg[a] > seg[b + 1] - seg[b]; });
-        ALLOC(d.bperm, bperm.size());
-      }
-    }
-    // experimental, off by default: measured slower at C3 (3.90 ms per solve
-    // for the overlapped pair vs 1.07 + 2.62 ms serial; the Cholesky alone
-    // is as fast with 127 helpers as with 255, so the loss is the walker's
-    // chain slowed by the concurrent Schur traffic and the late columns)
-    const char* so = std::getenv("SFM_SCHUR_OVERLAP");
-    d.schur_overlap = (so ? std::atoi(so) != 0 : false) && d.schur_pts && d.dpart != nullptr;
-    if (const char* ch = std::getenv("SFM_CHOL_HELPERS")) d.chol_helpers = std::max(0, std::atoi(ch));
-  }
-  {
-    // record-free observation passes: they need the diagonal partials and
-    // the recomputed-F Schur (every gathered-F path reads F records);
-    // k_jacobian then writes no records unless another reader is selected
-    const char* orc = std::getenv("SFM_OBS_RC");
-    d.obs_rc = (orc ? std::atoi(orc) != 0 : true) && d.dpart != nullptr && d.schur_pts;
-    d.need_jrec = !(d.obs_rc && d.jpart != nullptr && d.uv_pm != nullptr);
-    // the record-free Jacobian pass (no 160-B stores) prefers a larger grid:
-    // 256 workgroups per XCD, 0.256 -> 0.223 ms per C3 solve
-    d.jac_blocks_rec = d.jac_blocks;
-    if (!d.need_jrec && !std::getenv("SFM_JAC_WG_PER_XCD"))
-      d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 256));
-    d.max_blocks = std::max(d.max_blocks, d.jac_blocks);  // cost partials (allocated below)
-  }
-  ALLOC(d.sitems, std::max<size_t>(1, sitems.size()));
-  ALLOC(d.sboff, std::max<size_t>(1, sboff.size()));
-  ALLOC(d.spart, 36 * std::max<size_t>(1, sitems.size()));
-  ALLOC(d.stasks, std::max<size_t>(1, stasks.size()));
-  ALLOC(d.scnt, std::max<size_t>(1, scnt_init.size()));
-  ALLOC(d.sticket, 1);
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
   ALLOC(d.scal, size_t(kNumScalars) + 1);  // + the Cholesky failure int (k_reduce_batch)
 #undef ALLOC
-  timer.mark("task tables + alloc");
-  release_pool(h);  // what the new problem did not reuse
+#undef TMP
+  release_pool(h);  // earlier problems' buffers this one did not reuse
   if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
     d.scal_host = nullptr;
-    free_problem(h);
-    return fail(SFM_ENOMEM, "hipHostMalloc failed");
+    return bail(fail(SFM_ENOMEM, "hipHostMalloc failed"));
   }
-  hipStream_t s = h->stream;
-#define H2D(dst, src, cnt) HIPCHK(hipMemcpyAsync((dst), (src), sizeof(*(dst)) * (cnt), hipMemcpyHostToDevice, s))
-  if (N) {
-    H2D(d.cam_obs, cam_obs_pad.data(), size_t(npad));
-    H2D(d.wcam, wcam.data(), wcam.size());
-    H2D(d.cm_p, cm_p.data(), size_t(npad));
-    HIPCHK(hipMemcpyAsync(d.jchunks, jchunks.data(), sizeof(int32_t) * jchunks.size(), hipMemcpyHostToDevice, s));
-    H2D(d.uv_cm, uv_cm.data(), 2 * size_t(npad));
-    H2D(d.pos, pos.data(), size_t(N));
-    if (d.uv_pm) {
-      H2D(d.uv_pm, uv_s.data(), 2 * size_t(N));
-      H2D(d.cam_pm, cam_s.data(), size_t(N));
-    }
-    h->pos = pos;
-  }
-  H2D(d.pt_off, pt_off.data(), size_t(P) + 1);
-  H2D(d.jgrp, jgrp.data(), size_t(9));
-  if (C) H2D(d.cam_rng, cam_rng.data(), 2 * size_t(C));
   if (C) {
-    H2D(d.Kc, Kc.data(), 5 * size_t(C));
-    H2D(d.cam, cam.data(), 6 * size_t(C));
-    H2D(d.cam0, cam.data(), 6 * size_t(C));
+    HCHK(hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, s));
+    HCHK(hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, s));
+    HCHK(hipMemcpyAsync(d.cam0, d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToDevice, s));
   }
   if (P) {
-    H2D(d.X, X, 3 * size_t(P));
-    H2D(d.X0, X, 3 * size_t(P));
+    HCHK(hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, s));
+    HCHK(hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, s));
   }
-  if (d.n_blk)
-    HIPCHK(hipMemcpyAsync(d.blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice, s));
-  if (d.n_pairs)
-    HIPCHK(hipMemcpyAsync(d.pairs, pairs.data(), sizeof(int32_t) * pairs.size(), hipMemcpyHostToDevice, s));
-  H2D(d.seg, seg.data(), seg.size());
-  if (d.schur_pts && !bpts.empty()) H2D(d.bpts, bpts.data(), bpts.size());
-  if (d.bperm) H2D(d.bperm, bperm.data(), bperm.size());
-  if (!srow.empty()) H2D(d.srow, srow.data(), srow.size());
-  if (!stasks.empty()) H2D(d.stasks, stasks.data(), stasks.size());
-  if (!sitems.empty()) H2D(d.sitems, sitems.data(), sitems.size());
-  if (!sboff.empty()) H2D(d.sboff, sboff.data(), sboff.size());
-  if (!scnt_init.empty()) H2D(d.scnt, scnt_init.data(), scnt_init.size());
-  if (!pcnt_init.empty()) H2D(d.pcnt, pcnt_init.data(), pcnt_init.size());
-#undef H2D
-  HIPCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
-  HIPCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
-  HIPCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
-  HIPCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
-  HIPCHK(hipMemsetAsync(d.sticket, 0, sizeof(unsigned long long), s));
+  HCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
+  HCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
+  HCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
+  HCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
+  HCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
   h->chol_epoch = 0;
-  h->schur_epoch = 0;
-  h->pts_epoch = 0;
-  d.n_cu = device_cus(h->device);
-  d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   h->bs_epoch = 0;
-  HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
-  HIPCHK(hipStreamSynchronize(s));
-  timer.mark("uploads");
+  d.n_cu = device_cus(h->device);
+  HCHK(hipStreamSynchronize(s));
+#undef HCHK
+  retire_tmps(h);
+  timer.mark("pair lists + uploads (device)");
   h->has_problem = true;
   return 0;
 }
@@ -1254,26 +1009,40 @@ int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const 
   return rc;
 }
 
+// The record array of the evaluate API (the solve writes no records):
+// allocated on first use, kept with the problem.
+static int ensure_records(sfm_ba_handle* h) {
+  DevProblem& d = h->d;
+  if (d.jrec || d.N_pad == 0) return 0;
+  return dalloc(h, &d.jrec, size_t(kJRec) * size_t(d.N_pad));
+}
+
 int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;
+  int rc;
+  if ((rc = ensure_records(h))) return rc;
   launch_cam_prep(d, d.cam, false, h->stream);
   launch_jacobian(d, false, h->stream, true);  // the records are the output
   if (d.N == 0) HIPCHK(hipMemsetAsync(d.partials, 0, sizeof(double), h->stream));
   // the record-writing grid (jac_blocks_rec) wrote the cost partials: the
-  // record-free grid's extra slots still hold the last solve's partials
+  // solve's larger grid's extra slots still hold the last solve's partials
   launch_reduce(d, kPCost, d.jac_blocks_rec, 0, kCost, h->stream);
   std::vector<double> rec(size_t(kJRec) * d.N_pad);
-  if (d.N)
+  std::vector<int32_t> order(size_t(d.N)), pos(size_t(d.N));
+  if (d.N) {
     HIPCHK(hipMemcpyAsync(rec.data(), d.jrec, sizeof(double) * rec.size(), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(order.data(), d.order, sizeof(int32_t) * order.size(), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(pos.data(), d.pos, sizeof(int32_t) * pos.size(), hipMemcpyDeviceToHost, h->stream));
+  }
   double c = 0;
   HIPCHK(hipMemcpyAsync(&c, d.scal + kCost, sizeof(double), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (cost) *cost = c;
   for (int64_t q = 0; q < d.N; ++q) {
-    const int64_t i = h->order[q];
-    const double* r = &rec[size_t(kJRec) * h->pos[q]];
+    const int64_t i = order[q];
+    const double* r = &rec[size_t(kJRec) * pos[q]];
     if (res) { res[2 * i] = r[kRes]; res[2 * i + 1] = r[kRes + 1]; }
     if (jac) {
       double* J = jac + 18 * i;
@@ -1320,7 +1089,6 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk);
   if (reinterpret_cast<uintptr_t>(d.cticket) % 8) d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk + 1);
   d.n_cu = device_cus(device);
-  d.chol_stepwise = env_flag("SFM_CHOL_STEPWISE");
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
@@ -1351,32 +1119,13 @@ int sfm_ba_bench_jacobian(sfm_ba_handle* h, int32_t reps, double* avg_ms) {
   if (!h || !h->has_problem || reps < 1) return fail(SFM_EINVAL, "bad arguments");
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;
+  int rc;
+  if ((rc = ensure_records(h))) return rc;
   launch_cam_prep(d, d.cam, false, h->stream);
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   launch_jacobian(d, true, h->stream, true);  // warm (the record-writing pass is what is measured)
-  if (const char* th = std::getenv("SFM_JAC_THRASH")) {
-    const int kind = std::atoi(th);  // 1: 288-MB write, 2: 288-MB read
-    // diagnostic: each pass timed alone behind a 288-MB write of another
-    // buffer (the cache/TLB state the pass meets inside an LM iteration)
-    float tot = 0.f;
-    for (int i = 0; i < reps; ++i) {
-      if (kind == 2) launch_read_touch(d.frec, size_t(kFRec) * size_t(d.N), d.scal + kNumScalars - 1, h->stream);
-      else HIPCHK(hipMemsetAsync(d.frec, 0, sizeof(double) * kFRec * size_t(d.N), h->stream));
-      HIPCHK(hipEventRecord(e0, h->stream));
-      launch_jacobian(d, true, h->stream, true);
-      HIPCHK(hipEventRecord(e1, h->stream));
-      HIPCHK(hipEventSynchronize(e1));
-      float ms = 0.f;
-      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-      tot += ms;
-    }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    if (avg_ms) *avg_ms = double(tot) / reps;
-    return 0;
-  }
   HIPCHK(hipEventRecord(e0, h->stream));
   for (int i = 0; i < reps; ++i) launch_jacobian(d, true, h->stream, true);
   HIPCHK(hipEventRecord(e1, h->stream));

@@ -8,19 +8,17 @@
 // augmented matrix performs the forward substitution z = L^-1 rhs for free;
 // rows beyond n are identity padding up to a multiple of the 64-wide tile.
 //
-// Right-looking blocked algorithm, tile 64, three launches per step k:
-//   k_chol_potrf : factor tile (k,k) in registers (one wavefront) and form
-//                  its inverse W_k = L_kk^-1 (stored for the next two)
-//   k_chol_trsm  : panel tiles (i,k) <- A_ik W_k^T on MFMA
-//   k_chol_syrk  : trailing tiles (i,j) -= L_ik L_jk^T on v_mfma_f64_16x16x4_f64,
-//                  operands loaded straight into registers
-// and the back substitution L^T y = z (one launch per tile row, y_k = W_k^T z_k
-// recomputed by each workgroup, then the update of the rows above).
+// Blocked algorithm, tile 64, in ONE persistent launch (k_chol_fused): a
+// diagonal walker factors tile (k,k) (POTRF on v_mfma_f64_16x16x4_f64 with a
+// register pivot chain) and forms W_k = L_kk^-1; helper workgroups
+// accumulate the off-diagonal tiles' updates on MFMA and finish them with
+// X = T W_k^T.  Then the back substitution L^T y = z in one launch with
+// flag-chained block rows (k_backsolve).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cmath>
 #include "ba_device.h"
-#include "schur_tasks.h"
+#include "ba_common.h"
 
 namespace sfm {
 namespace {
@@ -223,139 +221,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   return bad;
 }
 
-template <bool kFull>
-__global__ __launch_bounds__(256) void k_chol_potrf(double* __restrict__ A, int ld, int k, int n,
-                                                    double* __restrict__ Winv, int* __restrict__ fail) {
-  __shared__ double T[NB * TS];    // T[c*TS + r] = A(r, c), becomes L
-  __shared__ double Wl[NB * TS];   // Wl[c*TS + r] = W(r, c)
-  __shared__ double scr[4][256];   // per-wave 16x16 scratch (row-major)
-  const int t = threadIdx.x;
-  const int k0 = k * NB;
-  // ---- load the tile (coalesced columns) ----
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    T[c * TS + r] = A[size_t(k0 + c) * ld + k0 + r];
-  }
-  __syncthreads();
-  const bool bad = potrf_tile<kFull>(T, Wl, scr, k0, n);
-  if (bad && t == 0) atomicOr(fail, 1);
-  // ---- store L (whole columns; the strict upper part is a don't-care) and W ----
-  double* Wk = Winv + size_t(k) * NB * NB;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    A[size_t(k0 + c) * ld + k0 + r] = T[c * TS + r];
-    Wk[c * NB + r] = Wl[c * TS + r];  // column-major: Wk[m][c] = W(c, m)
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Panel tile (i, k), i > k:  X L_kk^T = B  ->  X = B W^T, one workgroup per
-// tile on v_mfma_f64_16x16x4_f64, computed transposed like k_chol_syrk:
-// D[c][r] = sum_m W(c, m) B(r, m).  X overwrites B in place, so every wave
-// finishes its MFMA chain (all operand loads consumed) before any store.
-__global__ __launch_bounds__(256) void k_chol_trsm(double* __restrict__ A, int ld, int k,
-                                                   const double* __restrict__ Winv) {
-  const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
-  const int lr = lane & 15, lk = lane >> 4;
-  const double* Wk = Winv + size_t(k) * NB * NB;
-  double xa[2][16], yb[2][16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const int m = 4 * ks + lk;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = A[size_t(k0 + m) * ld + i0 + rb + 16 * bb + lr];
-  }
-  f64x4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb)
-        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
-  __syncthreads();
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        A[size_t(k0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = acc[a][bb][reg];
-}
-
-// ---------------------------------------------------------------------------
-// Trailing update of tile (i, j), k < j <= i:  A_ij -= L_ik L_jk^T.
-// Computed transposed, D[c][r] = sum_l L_jk[c][l] L_ik[r][l], so the MFMA's
-// D column (lane & 15) walks the tile's rows: each register of the
-// accumulator maps to 16 consecutive doubles of one column of A (128 B).
-// v_mfma_f64_16x16x4_f64 lane maps (cdna_hip_programming.md §3):
-//   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], D col = l&15, row = (l>>4) + 4*reg.
-// Operands go straight from L2 into registers (no LDS): wave w owns the
-// 32x32 quadrant (c in 32*(w>>1).., r in 32*(w&1)..) and loads all 64 k
-// of its 2+2 fragments before the MFMA chain.
-__global__ __launch_bounds__(256) void k_chol_syrk(double* __restrict__ A, int ld, int k) {
-  int i, j;
-  {
-    const int b = blockIdx.x;
-    int ii = int((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
-    while ((ii + 1) * (ii + 2) / 2 <= b) ++ii;
-    while (ii * (ii + 1) / 2 > b) --ii;
-    i = k + 1 + ii;
-    j = k + 1 + (b - ii * (ii + 1) / 2);
-  }
-  const int k0 = k * NB, i0 = i * NB, j0 = j * NB;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
-  const int lr = lane & 15, lk = lane >> 4;
-  if (i == j && cb > rb) return;  // strictly-upper quadrant of a diagonal tile: never read
-  double xa[2][16], yb[2][16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const size_t colbase = size_t(k0 + 4 * ks + lk) * ld;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) xa[a][ks] = A[colbase + j0 + cb + 16 * a + lr];
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = A[colbase + i0 + rb + 16 * bb + lr];
-  }
-  double cv[2][2][4];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        cv[a][bb][reg] = A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr];
-  f64x4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb)
-        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
-}
-
 // ---------------------------------------------------------------------------
 // The whole factorisation in ONE persistent launch (left-looking tiles,
 // device-scope flags instead of kernel boundaries).
@@ -473,7 +338,8 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
 }
 
 // Helper: one tile (i, j).  Wave w owns the 32x32 quadrant (c in cb.., r in
-// rb..), accumulated transposed as in k_chol_syrk.
+// rb..), accumulated transposed: D[c][r] = sum_l L_jk[c][l] L_ik[r][l], so the MFMA's D
+// column (lane & 15) walks the tile's rows (128-B column runs of A).
 __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
                                   int* sh, int* __restrict__ fail) {
@@ -691,34 +557,10 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
   }
 }
 
-// Wave 0 waits until *f >= target, then the block proceeds.
-__device__ __forceinline__ void block_wait_count(const int* f, int target, int* fail) {
-  if (wave0()) {
-    long spins = 0;
-    bool ok = true;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > kFlagSpins) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) atomicOr(fail, 2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
-  }
-  __syncthreads();
-}
-
-// colcnt != nullptr: the Schur assembly runs concurrently (k_schur_pts on
-// another stream publishes, per tile column j, a monotone count of finished
-// workgroups that wrote S rows of column j); a helper waits for
-// colcnt[j] >= sepoch * coltgt[j] before it reads any tile (i, j).  The
-// walker reads only tiles a helper handed over (flag P), so it needs no
-// wait of its own.
 __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb,
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
-                                                    int epoch, int nhelp, int* __restrict__ fail,
-                                                    const int* __restrict__ colcnt, const int* __restrict__ coltgt,
-                                                    int sepoch) {
+                                                    int epoch, int nhelp, int* __restrict__ fail) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
@@ -749,111 +591,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     if (tk >= ntask) break;
     int j = 0, r = tk;
     while (r >= nb - j) { r -= nb - j; ++j; }
-    if (colcnt) block_wait_count(colcnt + j, sepoch * coltgt[j], fail);
     fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Schur complement and Cholesky in ONE persistent launch (single rank).
-// The dense factorisation is a latency chain (the diagonal walker) that
-// leaves most CUs idle; the Schur assembly is a gather-bound pass over all
-// CUs.  Here the helper workgroups take, from one atomic ticket, a task
-// table built on the host in dependency order:
-//   Schur items of tile columns 0 and 1, then for j = 0, 1, ...:
-//   the Cholesky tiles (i, j) of column j, then the Schur items of column
-//   j + 2,
-// where a camera's items (its row segments, then its diagonal/rhs item)
-// belong to the first tile column its six columns touch.  A row segment or
-// diagonal item publishes (release) one count to every tile column the
-// camera touches; a tile (i, j) waits for column j's count before it reads
-// A_ij; a diagonal item waits for the S_cc stamp of its camera's first row
-// segment.  Every wait is on an item that sits earlier in the table or on
-// the walker, and all workgroups are co-resident, so the waits drain; they
-// are bounded anyway (fail bit 1).  The arithmetic is the separate
-// kernels' own (schur_tasks.h), so results are bitwise those of the
-// two-launch path.
-struct SchurArgs {
-  const int32_t* seg;
-  const int2* pairs;
-  const double* frec;
-  const int32_t* cam_rng;
-  const int32_t* cam_obs;
-  const double* jrec;
-  const double* mrec;
-  const double* Ucam;
-  const double* diag_c;
-  const int2* blk;
-  double radius;
-  int add_diag;
-  int C;
-};
-
-__device__ __forceinline__ void schur_publish(int* cnt, int c) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave0()) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) {
-      const int j0 = (6 * c) / NB, j1 = (6 * c + 5) / NB;
-      for (int j = j0; j <= j1; ++j) __hip_atomic_fetch_add(cnt + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-constexpr int kPoolDoubles = 3 * NB * TS + 4 * 256;
-static_assert(kPoolDoubles >= kRowCh * kFRec, "row-segment chunk must fit the pool");
-static_assert(kPoolDoubles >= kDiagLds, "diagonal item must fit the pool");
-
-__global__ __launch_bounds__(256) void k_chol_schur_fused(double* __restrict__ A, int ld, int n, int nb,
-                                                          double* __restrict__ Winv, int* __restrict__ F,
-                                                          int* __restrict__ Pf,
-                                                          unsigned long long* __restrict__ ticket, int epoch,
-                                                          int sepoch, int ntask, const int4* __restrict__ tasks,
-                                                          int nhelp, int* __restrict__ scnt, SchurArgs sa,
-                                                          int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double pool[kPoolDoubles];
-  __shared__ int sh[2];
-  double* T = pool;
-  double* Wl = pool + NB * TS;
-  double* Ls = pool + 2 * NB * TS;
-  double (*scr)[256] = reinterpret_cast<double (*)[256]>(pool + 3 * NB * TS);
-  if (blockIdx.x == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, fail);
-    return;
-  }
-  int* colcnt = scnt;
-  const int* coltgt = scnt + nb;
-  int* camstamp = scnt + 2 * nb;
-  const unsigned long long base = (unsigned long long)(sepoch - 1) * (unsigned long long)(ntask + nhelp);
-  while (true) {
-    if (wave0()) {
-      const unsigned long long v = atomicAdd(ticket, threadIdx.x == 0 ? 1ULL : 0ULL);
-      const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
-      const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
-      sh[1] = int(((unsigned long long)hi << 32 | lo) - base);
-    }
-    __syncthreads();
-    const int tk = __builtin_amdgcn_readfirstlane(sh[1]);
-    __syncthreads();
-    if (tk >= ntask) break;
-    const int4 q = tasks[tk];
-    const int type = __builtin_amdgcn_readfirstlane(q.x), a = __builtin_amdgcn_readfirstlane(q.y),
-              b = __builtin_amdgcn_readfirstlane(q.z), c = __builtin_amdgcn_readfirstlane(q.w);
-    if (type == 2) {
-      block_wait_count(colcnt + b, sepoch * coltgt[b], fail);
-      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, a, b, T, sh, fail);
-    } else if (type == 1) {
-      block_wait(camstamp + a, sepoch, fail);
-      schur_diag_task<true>(a, sa.cam_rng, sa.cam_obs, sa.jrec, sa.mrec, sa.Ucam, sa.diag_c, sa.radius, sa.add_diag, A,
-                      ld, n, pool);
-      schur_publish(colcnt, a);
-    } else {
-      schur_row_task<4, true>(make_int4(a, b, c, 0), sa.seg, sa.pairs, sa.frec, sa.cam_rng, sa.blk, A, ld, pool);
-      if (type == 0) block_publish(camstamp + a, sepoch);  // S_cc written (its fence covers the rest)
-      schur_publish(colcnt, a);
-    }
   }
 }
 
@@ -939,43 +677,13 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 
 }  // namespace
 
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int sepoch) {
+void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
-  if (d.cflags && !d.chol_stepwise) {
-    const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
-    // gated (concurrent Schur): at most half the CUs, so that the Schur
-    // workgroups always have CUs a Cholesky workgroup (108 KB of LDS, one
-    // per CU) does not hold -- the helpers' waits then always drain
-    // (fixed per problem: the ticket base assumes every launch of a problem
-    // takes ntask + nhelp tickets)
-    int cap = d.schur_overlap ? d.n_cu / 2 - 1 : d.n_cu - 1;
-    if (d.chol_helpers > 0) cap = std::min(cap, d.chol_helpers);
-    const int nhelp = std::max(1, std::min(ntask, cap));
-    k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
-                                           d.cticket, epoch, nhelp, d.fail, sepoch > 0 ? d.pcnt : nullptr,
-                                           d.pcnt + nb, sepoch);
-    return;
-  }
-  for (int k = 0; k < d.nblk; ++k) {
-    if ((k + 1) * NB <= d.n)
-      k_chol_potrf<true><<<1, 256, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
-    else
-      k_chol_potrf<false><<<1, 256, 0, s>>>(d.S, d.ld, k, d.n, d.invL, d.fail);
-    const int m = d.nblk - k - 1;
-    if (m == 0) break;
-    k_chol_trsm<<<m, 256, 0, s>>>(d.S, d.ld, k, d.invL);
-    k_chol_syrk<<<m * (m + 1) / 2, 256, 0, s>>>(d.S, d.ld, k);
-  }
-}
-
-void launch_schur_cholesky(const DevProblem& d, double radius, bool add_diag, int chol_epoch, int schur_epoch,
-                           hipStream_t s) {
-  const int nhelp = std::max(1, std::min(d.n_stasks, d.n_cu - 1));
-  SchurArgs sa{d.seg, d.pairs, d.frec, d.cam_rng, d.cam_obs, d.jrec, d.mrec, d.Ucam, d.diag_c, d.blk, radius,
-               add_diag ? 1 : 0, d.C};
-  k_chol_schur_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.invL, d.cflags,
-                                               d.cflags + size_t(d.nblk) * d.nblk, d.sticket, chol_epoch,
-                                               schur_epoch, d.n_stasks, d.stasks, nhelp, d.scnt, sa, d.fail);
+  const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
+  // one persistent workgroup per CU (the walker + helpers must be co-resident)
+  const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
+                                         epoch, nhelp, d.fail);
 }
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s) {

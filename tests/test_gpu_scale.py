@@ -9,6 +9,8 @@ problem shape, through the C ABI (tolerances as in test_gpu_parity.py).
 * the packed upper-triangle all-reduce path (SFM_FORCE_PACK) is an exact
   copy on one rank, and so is the whole solve over a one-rank RCCL
   communicator (every collective of the sharded path);
+* the device-side problem setup: validation errors name the first bad
+  observation; duplicates keep the caller's order;
 * edge cases: a point seen twice by the same camera (Ceres adds two residual
   blocks over the same parameter blocks), cameras without observations,
   points with a single observation.
@@ -128,172 +130,51 @@ def test_one_rank_rccl_communicator_is_exact(mode):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
-def test_fused_schur_cholesky_matches_two_launch_path(monkeypatch, cfg):
-    """The single-rank fused launch (Schur items + Cholesky tiles on one
-    ticket, k_chol_schur_fused) runs the separate kernels' arithmetic, so
-    whole solves are bitwise those of the two-launch path (the default;
-    the fused launch is the experimental SFM_SCHUR_FUSED=1)."""
-    s = scene.config(cfg)
-    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
-    # the fused launch sums the diagonal blocks per camera (schur_diag_task);
-    # the two-launch default sums k_obs_prep's per-wave partials instead
-    monkeypatch.setenv("SFM_SCHUR_DIAG_FUSED", "0")
-    monkeypatch.setenv("SFM_SCHUR_PTS", "0")  # the fused launch gathers F records
-    out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("SFM_SCHUR_FUSED", flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            p = ba.parameters()
-            ba.reset()
-            sm2, tr2 = ba.solve()  # a second launch sequence (epochs > 1)
-            p2 = ba.parameters()
-        out.append((sm.final_cost, tr, p, sm2.final_cost, p2))
-    (c0, t0, p0, d0, q0), (c1, t1, p1, d1, q1) = out
-    assert c0 == c1 == d0 == d1 and t0 == t1
-    for a, b, c in zip(p0, p1, q1):
-        assert np.array_equal(a, b) and np.array_equal(a, c)
+@pytest.mark.parametrize("kind", ["cam", "pt", "uv"])
+def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
+    """The device-side validation of sfm_ba_set_problem (ba_setup.hip
+    k_validate) reports the FIRST offending observation, as a host loop in
+    the caller's order would, and leaves no problem behind."""
+    s = scene.config("C1")
+    uv, cam, pt = s.uv.copy(), s.cam_idx.copy(), s.pt_idx.copy()
+    bad = [1234, 77, 15000]
+    for i in bad:
+        if kind == "cam":
+            cam[i] = s.n_cams + i % 3
+        elif kind == "pt":
+            pt[i] = -1 - i % 5
+        else:
+            uv[i, i % 2] = np.nan if i % 2 else np.inf
+    with sfm_amd.BundleAdjuster() as ba:
+        with pytest.raises(sfm_amd.SfmError) as ei:
+            ba.set_problem(uv, cam, pt, s.K, s.rot, s.t, s.X)
+        assert f"at {min(bad)}" in str(ei.value)
+        # the handle stays usable
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm, _ = ba.solve()
+        assert sm.num_iterations > 0
 
 
-@pytest.mark.parametrize("knob", ["SFM_SCHUR_DIAG_FUSED", "SFM_CAM_FUSED", "SFM_PTEVAL_RC", "SFM_OBS_RC"])
-@pytest.mark.parametrize("cfg", ["C1", "C2", "C3"])
-def test_fused_partials_match_rereads(monkeypatch, cfg, knob):
-    """Sums taken from per-wavefront partials of the producing pass (default)
-    against a second pass over the records (knob=0): the Schur diagonal
-    blocks / rhs from k_obs_prep vs k_schur_diag, and U_c / b_c from
-    k_jacobian vs k_cam_reduce, V_p / b_p from recomputed J_X (uv streamed
-    point-major) vs the gathered records.  Same sums in a different order:
-    deterministic, same LM path, same solve to rounding."""
-    s = scene.config(cfg)
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv(knob, flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            p = ba.parameters()
-            ba.reset()
-            sm2, _ = ba.solve()
-            p2 = ba.parameters()
-        assert sm.final_cost == sm2.final_cost
-        for a, b in zip(p, p2):
-            assert np.array_equal(a, b)
-        res[flag] = (sm, tr, p)
-    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
-    assert s1.num_iterations == s0.num_iterations
-    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
-    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
-    for a, b in zip(p1, p0):
-        assert _rel(a, b) < 1e-6
-
-
-@pytest.mark.parametrize("cfg", ["C1", "C2"])
-def test_row_staged_schur_matches_thread_per_block(monkeypatch, cfg):
-    """k_schur_row (default) and k_schur (SFM_SCHUR_ROW=0) sum every block's
-    pairs in the same order: whole solves are bitwise identical (the
-    small-problem split path, which sums pair chunks, is switched off)."""
-    s = scene.config(cfg)
-    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
-    monkeypatch.setenv("SFM_SCHUR_PTS", "0")
-    out = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SFM_SCHUR_ROW", flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            out.append((sm.final_cost, tr, ba.parameters()))
-    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
-    for a, b in zip(out[0][2], out[1][2]):
-        assert np.array_equal(a, b)
-
-
-@pytest.mark.parametrize("cfg,sub", [("C1", "8"), ("C2", "16"), ("C2", "64"), ("C3", "8")])
-def test_recomputed_schur_matches_gathered(monkeypatch, cfg, sub):
-    """k_schur_pts (F recomputed per pair from the point record and the two
-    cameras; the default once the split path is off) against k_schur_row
-    (gathered F records): deterministic, same LM path, same solve to
-    rounding."""
-    s = scene.config(cfg)
-    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
-    monkeypatch.setenv("SFM_SCHUR_PTS_SUB", sub)
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SFM_SCHUR_PTS", flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            p = ba.parameters()
-            ba.reset()
-            sm2, _ = ba.solve()
-            p2 = ba.parameters()
-        assert sm.final_cost == sm2.final_cost
-        for a, b in zip(p, p2):
-            assert np.array_equal(a, b)
-        res[flag] = (sm, tr, p)
-    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
-    assert s1.num_iterations == s0.num_iterations
-    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
-    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
-    for a, b in zip(p1, p0):
-        assert _rel(a, b) < 1e-6
-
-
-@pytest.mark.parametrize("cfg,helpers", [("C2", "0"), ("C3", "0"), ("C3", "3")])
-def test_overlapped_schur_cholesky_is_exact(monkeypatch, cfg, helpers):
-    """Single rank, recomputed-F Schur: the Cholesky runs concurrently on a
-    second stream, its helpers gated per tile column on k_schur_pts' counts
-    (experimental SFM_SCHUR_OVERLAP=1).  The arithmetic is that of the serial launches, so whole
-    solves are bitwise equal -- also with only 3 helper workgroups (every
-    gate waited on)."""
-    s = scene.config(cfg)
-    monkeypatch.setenv("SFM_SCHUR_SPLIT", "0")
-    monkeypatch.setenv("SFM_CHOL_HELPERS", helpers)
-    out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("SFM_SCHUR_OVERLAP", flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            p = ba.parameters()
-            ba.reset()
-            sm2, _ = ba.solve()
-            p2 = ba.parameters()
-        out.append((sm.final_cost, tr, p, sm2.final_cost, p2))
-    (c0, t0, p0, d0, q0), (c1, t1, p1, d1, q1) = out
-    assert c0 == c1 == d0 == d1 and t0 == t1
-    for a, b, c in zip(p0, p1, q1):
-        assert np.array_equal(a, b) and np.array_equal(a, c)
-
-
-@pytest.mark.parametrize("cfg", ["C1", "C2"])
-def test_split_schur_small_problems(monkeypatch, cfg):
-    """Keyframe-sized problems sum each block's pairs in chunks
-    (k_schur_split, default up to 8192 blocks): deterministic run to run,
-    and the same solve as the one-thread-per-block order to rounding."""
-    monkeypatch.setenv("SFM_SCHUR_PTS", "0")  # split vs the gathered-F blocks
-    s = scene.config(cfg)
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SFM_SCHUR_SPLIT", flag)
-        with sfm_amd.BundleAdjuster() as ba:
-            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-            sm, tr = ba.solve()
-            p = ba.parameters()
-            ba.reset()
-            sm2, _ = ba.solve()
-            p2 = ba.parameters()
-        assert sm.final_cost == sm2.final_cost
-        for a, b in zip(p, p2):
-            assert np.array_equal(a, b)
-        res[flag] = (sm, tr, p)
-    (s1, t1, p1), (s0, t0, p0) = res["1"], res["0"]
-    assert s1.num_iterations == s0.num_iterations
-    assert [t["step_is_successful"] for t in t1] == [t["step_is_successful"] for t in t0]
-    assert abs(s1.final_cost - s0.final_cost) <= 1e-10 * s0.final_cost
-    for a, b in zip(p1, p0):
-        assert _rel(a, b) < 1e-6
+def test_device_layout_keeps_caller_order_of_duplicates():
+    """Observations of one (point, camera) pair keep the caller's order in
+    the device-built point-major layout (stable radix sort), so the
+    per-observation outputs of evaluate() come back in the caller's order
+    even for shuffled input with duplicates."""
+    s = scene.generate(12, 400, views=4, seed=23)
+    rng = np.random.default_rng(5)
+    dup = rng.choice(len(s.pt_idx), 40, replace=False)
+    _append_obs(s, s.cam_idx[dup], s.pt_idx[dup], s.uv[dup] + rng.normal(0, 0.3, (40, 2)))
+    perm = rng.permutation(len(s.pt_idx))
+    s.uv, s.cam_idx, s.pt_idx = s.uv[perm], s.cam_idx[perm], s.pt_idx[perm]
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        cost, res, jac = ba.evaluate()
+    r_o, j_o = O.residuals_jacobians(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+    assert np.max(np.abs(res - r_o)) < 1e-9
+    scale = np.maximum(np.abs(j_o).max(axis=(1, 2), keepdims=True), 1e-300)
+    assert np.max(np.abs(jac - j_o) / scale) < 1e-10
+    o, g = _solve_both(s)
+    _assert_parity(o, g)
 
 
 def test_one_shot_solves_reuse_the_cached_handle():
@@ -319,13 +200,7 @@ def _append_obs(s, cam, pt, uv):
     s.pt_idx = np.concatenate([s.pt_idx, np.asarray(pt, dtype=np.int32)])
 
 
-@pytest.mark.parametrize("schur", ["split", "pts", "row"])
-def test_edge_cases_duplicate_camera_empty_camera_single_view(monkeypatch, schur):
-    # every Schur formulation (the small-problem split, the recomputed-F
-    # blocks, the gathered-F rows) meets the same edge cases
-    monkeypatch.setenv("SFM_SCHUR_SPLIT", "1" if schur == "split" else "0")
-    if schur != "split":
-        monkeypatch.setenv("SFM_SCHUR_PTS", "1" if schur == "pts" else "0")
+def test_edge_cases_duplicate_camera_empty_camera_single_view():
     s = scene.generate(12, 400, views=4, seed=11)
     # point 3 seen a second time by one of its cameras (two residual blocks,
     # same parameter blocks): the Schur diagonal gets the cross term
