@@ -751,6 +751,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HCHK(hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, s));
   }
   HCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
+  // the walker stores only the lower 16x16 blocks of each W_k (k_chol_fused)
+  HCHK(hipMemsetAsync(d.invL, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB, s));
   HCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
   HCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
   HCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
@@ -1079,6 +1081,7 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   HIPCHK(hipMalloc(&S, bytes));
   HIPCHK(hipMalloc(&S0, bytes));
   HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
+  HIPCHK(hipMemset(invd, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB));
   HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
   HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
   HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));

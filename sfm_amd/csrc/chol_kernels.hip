@@ -520,17 +520,23 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      st_wt(Wk + c * NB + r, Wl[c * TS + r]);
+      // lower 16x16 blocks only: the upper blocks of every W_k stay zero
+      // from set_problem (one memset), 37% fewer bytes on the chain
+      if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
     block_publish_wt(F + j * nb + j, epoch);
-    // L_jj after the flag: no helper reads it (their TRSMs use W_j); the
-    // next publish's drain covers these stores
+    // L_jj is read by nobody (the helpers' TRSMs and the back substitution
+    // use W_j; the next Schur pass rewrites the lower triangle) except in the
+    // tile that holds the augmented row n: its z entries feed k_backsolve.
+    // The next publish's drain covers these stores.
+    if (j0 <= n && n < j0 + NB) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+      }
     }
     if (j + 1 == nb) break;
     // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
