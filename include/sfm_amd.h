@@ -249,6 +249,21 @@ int sfm_matcher_last_time(sfm_matcher* h, double* ms2);
 int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const int32_t* row_off, int32_t n_pts,
                                    int32_t desc_bytes, int32_t* best, uint8_t* out);
 
+/* Per-frame pose: cv::solvePnPRansac(objectPoints, imagePoints, K, dist = 0,
+ * rvec, tvec, false, iterations, reproj_err, confidence, inliers,
+ * SOLVEPNP_ITERATIVE) as CSfM::tracking calls it (CSfM.cpp:553-565:
+ * iterations 20, reproj_err _maxReprErr = 7, confidence 0.99), OpenCV 3.0
+ * semantics (oracle/pnp_oracle.py: RANSAC over 5-point EPnP hypotheses with
+ * cv::RNG(-1), float32 point data, the best hypothesis's pose and inlier
+ * mask returned).  obj [n][3], img [n][2] (undistorted pixels, Kopt), K9
+ * row-major (fx, fy, cx, cy read).  Outputs: rvec/tvec (Rodrigues vector,
+ * translation), inliers (ascending indices, capacity n; may be NULL),
+ * *n_inliers, *found = 0 when no model exists (n < 5, or no hypothesis with
+ * more than 4 inliers) -- the reference's `false` return. */
+int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, const double* img, const double* K9,
+                   int32_t iterations, double reproj_err, double confidence, double* rvec, double* tvec,
+                   int32_t* inliers, int32_t* n_inliers, int32_t* found);
+
 /* Testing hook: solve the dense SPD system A y = b (A [n][n] row-major,
  * both triangles given; only the upper triangle is read) with the device
  * Cholesky + substitution kernels used for the reduced camera system.

@@ -140,6 +140,42 @@ inline int matchFeatures(const std::vector<Point2>& pts0, const DescMat& desc0, 
   return SFM_OK;
 }
 
+// Per-frame pose, the cv::solvePnPRansac call of CSfM::tracking
+// (/root/reference/CSfM.cpp:553-565):
+//   solvePnPRansac(currMatch3D, currMatch2D, K, Mat::zeros(4,1,CV_64FC1), rvec, tvec,
+//                  false, iter = 20, _maxReprErr = 7, 0.99, inlierIdx, SOLVEPNP_ITERATIVE)
+// becomes
+//   sfm_compat::solvePnPRansac(currMatch3D, currMatch2D, K, rvec3, tvec3, inlierIdx, 20, 7.0, 0.99)
+// with Point3 = anything with .val[3] (cv::Matx31d) or .x/.y/.z via the
+// overload below, Point2 .x/.y, Matx33 .val[9]; rvec3 / tvec3 are double[3]
+// (cv::Mat(3,1,CV_64F, ptr) wraps them).  Returns true when a model was
+// found (the reference's bool), false otherwise (inliers cleared); ABI
+// errors also return false, with sfm_last_error() set.
+template <class Point3, class Point2, class Matx33>
+inline bool solvePnPRansac(const std::vector<Point3>& objectPoints, const std::vector<Point2>& imagePoints,
+                           const Matx33& K, double rvec[3], double tvec[3], std::vector<int>& inliers,
+                           int iterationsCount = 20, double reprojectionError = 7.0, double confidence = 0.99,
+                           int device = 0) {
+  inliers.clear();
+  const size_t n = objectPoints.size();
+  if (imagePoints.size() != n) return false;
+  std::vector<double> obj(3 * n), img(2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    for (int m = 0; m < 3; ++m) obj[3 * i + m] = objectPoints[i].val[m];
+    img[2 * i] = imagePoints[i].x;
+    img[2 * i + 1] = imagePoints[i].y;
+  }
+  double K9[9];
+  for (int m = 0; m < 9; ++m) K9[m] = K.val[m];
+  std::vector<int32_t> inl(std::max<size_t>(1, n));
+  int32_t n_inl = 0, found = 0;
+  if (sfm_pnp_ransac(device, int32_t(n), obj.data(), img.data(), K9, iterationsCount, reprojectionError, confidence,
+                     rvec, tvec, inl.data(), &n_inl, &found) != 0)
+    return false;
+  inliers.assign(inl.begin(), inl.begin() + n_inl);
+  return found != 0;
+}
+
 // Frame-resident matcher: drop-ins for the per-frame matchFeatures
 // overloads.  CTracker keeps _prevFrame / _currFrame (CTracker.h:80-81); the
 // shim keeps the same two frames' keypoints + descriptors resident on the

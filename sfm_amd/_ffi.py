@@ -150,6 +150,8 @@ _SIGNATURES = {
                                  c_void_p]),
     "sfm_matcher_last_time": (c_int, [c_void_p, c_void_p]),
     "sfm_representative_descriptors": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "sfm_pnp_ransac": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_double, c_double,
+                               c_void_p, c_void_p, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
                                     POINTER(c_int32)]),
     "sfm_klt_default_params": (None, [POINTER(KLTParams)]),

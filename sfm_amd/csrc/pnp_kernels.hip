@@ -1,0 +1,785 @@
+// Per-frame pose: cv::solvePnPRansac as CSfM::tracking calls it
+// (/root/reference/CSfM.cpp:553-565: iterationsCount 20, reprojectionError
+// _maxReprErr = 7 (CSfM.cpp:35), confidence 0.99, SOLVEPNP_ITERATIVE), on
+// gfx950.  The semantics are OpenCV 3.0's (README.md:28), restated in
+// oracle/pnp_oracle.py (parity unpinned: OpenCV is absent):
+//   * RANSAC over 5-point subsets drawn by cv::RNG(uint64(-1)), kernel =
+//     EPnP on the subset, inlier when the float reprojection DISTANCE is
+//     <= reprErr^2 (3.0's findInliers squares the threshold), model kept
+//     when its inlier count beats max(best, 4), iteration bound shrunk by
+//     RANSACUpdateNumIters;
+//   * the returned pose is the best RANSAC model (3.0 discards the pose of
+//     its final refinement), the inliers are its mask.
+//
+// Device mapping.  RANSAC's hypotheses are independent once the subsets are
+// drawn, so: one thread draws every subset of the iteration bound (the RNG
+// sequence is inherently sequential, ~100 draws); one WAVE per hypothesis
+// solves its EPnP (the 12x12 M^T M eigen-decomposition by one-sided Jacobi
+// with lane i holding row i, everything else wave-uniform in registers);
+// one workgroup per hypothesis scores all n points (fixed-order count);
+// one wave replays the sequential acceptance rule over the counts (the
+// bound only shrinks, so evaluating the full bound and replaying gives the
+// sequential result exactly) and compacts the winner's inliers in order.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+#include "../../include/sfm_amd.h"
+
+void sfm_internal_set_error(const std::string& msg);
+
+namespace sfm {
+namespace {
+
+constexpr int kModel = 5;      // RANSAC subset size (EPnP kernel)
+constexpr int kMaxIters = 1024;
+
+struct PnPCam {
+  double fu, fv, uc, vc;
+};
+
+// ---- OpenCV's small dense linear algebra, wave-uniform (every lane computes
+// the same values; the whole file is compiled with -ffp-contract=off so the
+// products and sums round as OpenCV's SSE2 build and oracle/pnp_oracle.py)
+
+constexpr double kDblEps = DBL_EPSILON, kDblMin = DBL_MIN;
+
+__host__ __device__ __forceinline__ unsigned cv_rng_next(uint64_t& state) {
+  state = uint64_t(unsigned(state)) * 4164903690ull + (state >> 32);
+  return unsigned(state);
+}
+
+// cv::SVD of A (M x N, M >= N) as JacobiSVDImpl_ computes it: one-sided
+// Jacobi on the rows of At = A^T (eps 10 DBL_EPSILON, max(M, 30) sweeps),
+// singular values sorted descending, rows of At normalised to the left
+// singular vectors (zero singular values completed from cv::RNG(0x12345678)
+// vectors).  On return U[i] = i-th left singular vector (At row i), w
+// descending, Vt rows = right singular vectors.
+template <int M, int N>
+__host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
+  double W[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sd = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) { U[i][k] = A[k][i]; sd += U[i][k] * U[i][k]; }
+    W[i] = sd;
+#pragma unroll
+    for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
+  }
+  const double eps = kDblEps * 10;
+  for (int iter = 0; iter < (M > 30 ? M : 30); ++iter) {
+    bool changed = false;
+#pragma unroll
+    for (int i = 0; i < N - 1; ++i)
+#pragma unroll
+      for (int j = i + 1; j < N; ++j) {
+        double a = W[i], b = W[j], p = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) p += U[i][k] * U[j][k];
+        if (fabs(p) <= eps * sqrt(a * b)) continue;
+        p *= 2;
+        // hypot as sqrt(p^2 + beta^2): one formula on every side (std::hypot /
+        // CPython / ocml disagree in the last ulp, which rotates the 2-D
+        // near-null space of the 5-point M^T M arbitrarily)
+        const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+        double c, s;
+        if (beta < 0) {
+          const double delta = (gamma - beta) * 0.5;
+          s = sqrt(delta / gamma);
+          c = p / (gamma * s * 2);
+        } else {
+          c = sqrt((gamma + beta) / (gamma * 2));
+          s = p / (gamma * c * 2);
+        }
+        a = b = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          const double t0 = c * U[i][k] + s * U[j][k], t1 = -s * U[i][k] + c * U[j][k];
+          U[i][k] = t0; U[j][k] = t1;
+          a += t0 * t0; b += t1 * t1;
+        }
+        W[i] = a; W[j] = b;
+        changed = true;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          const double t0 = c * Vt[i][k] + s * Vt[j][k], t1 = -s * Vt[i][k] + c * Vt[j][k];
+          Vt[i][k] = t0; Vt[j][k] = t1;
+        }
+      }
+    if (!changed) break;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sd = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) sd += U[i][k] * U[i][k];
+    W[i] = sqrt(sd);
+  }
+#pragma unroll
+  for (int i = 0; i < N - 1; ++i) {
+    int j = i;
+#pragma unroll
+    for (int k = i + 1; k < N; ++k)
+      if (W[j] < W[k]) j = k;
+    // swap rows i and j (j is data-dependent: a select over the candidates)
+#pragma unroll
+    for (int k = i + 1; k < N; ++k)
+      if (j == k) {
+        const double tw = W[i]; W[i] = W[k]; W[k] = tw;
+#pragma unroll
+        for (int e = 0; e < M; ++e) { const double x = U[i][e]; U[i][e] = U[k][e]; U[k][e] = x; }
+#pragma unroll
+        for (int e = 0; e < N; ++e) { const double x = Vt[i][e]; Vt[i][e] = Vt[k][e]; Vt[k][e] = x; }
+      }
+  }
+  uint64_t rng = 0x12345678ull;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sd = W[i];
+    for (int ii = 0; ii < 100 && sd <= kDblMin; ++ii) {
+      const double val0 = 1.0 / M;
+#pragma unroll
+      for (int k = 0; k < M; ++k) U[i][k] = (cv_rng_next(rng) & 256) != 0 ? val0 : -val0;
+      for (int it2 = 0; it2 < 2; ++it2)
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+          sd = 0.0;
+#pragma unroll
+          for (int k = 0; k < M; ++k) sd += U[i][k] * U[j][k];
+          double asum = 0.0;
+#pragma unroll
+          for (int k = 0; k < M; ++k) {
+            const double t = U[i][k] - sd * U[j][k];
+            U[i][k] = t;
+            asum += fabs(t);
+          }
+          asum = asum > eps * 100 ? 1.0 / asum : 0.0;
+#pragma unroll
+          for (int k = 0; k < M; ++k) U[i][k] *= asum;
+        }
+      sd = 0.0;
+#pragma unroll
+      for (int k = 0; k < M; ++k) sd += U[i][k] * U[i][k];
+      sd = sqrt(sd);
+    }
+    const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) U[i][k] *= sc;
+    w[i] = W[i];
+  }
+}
+
+// cv::solve(A, b, x, DECOMP_SVD) = SVBkSb: x = sum over w_i > 2 DBL_EPSILON
+// sum(w) of (u_i . b / w_i) v_i, in descending-w order.
+template <int M, int N>
+__host__ __device__ void cv_lstsq(const double (&A)[M][N], const double (&b)[M], double (&x)[N]) {
+  double U[N][M], w[N], Vt[N][N];
+  cv_svd<M, N>(A, U, w, Vt);
+  double thr = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) thr += w[i];
+  thr *= kDblEps * 2;
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double wi = w[i];
+    if (fabs(wi) <= thr) continue;
+    wi = 1.0 / wi;
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) s += U[i][j] * b[j];
+    s *= wi;
+#pragma unroll
+    for (int j = 0; j < N; ++j) x[j] = x[j] + s * Vt[i][j];
+  }
+}
+
+// epnp::qr_solve (Householder, Lepetit's code) for the 6 x 4 Gauss-Newton
+// system; false when A is singular (the caller's betas stay unchanged).
+__host__ __device__ bool qr_solve(double (&A)[6][4], double (&b)[6], double (&x)[4]) {
+  double A1[4], A2[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double eta = fabs(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      const double elt = fabs(A[i][k]);
+      if (eta < elt) eta = elt;
+    }
+    if (eta == 0) return false;
+    const double inv_eta = 1. / eta;
+    double sum1 = 0.0;
+#pragma unroll
+    for (int i = k; i < 6; ++i) { A[i][k] *= inv_eta; sum1 += A[i][k] * A[i][k]; }
+    double sigma = sqrt(sum1);
+    if (A[k][k] < 0) sigma = -sigma;
+    A[k][k] += sigma;
+    A1[k] = sigma * A[k][k];
+    A2[k] = -eta * sigma;
+#pragma unroll
+    for (int j = k + 1; j < 4; ++j) {
+      double sum = 0.0;
+#pragma unroll
+      for (int i = k; i < 6; ++i) sum += A[i][k] * A[i][j];
+      const double tau = sum / A1[k];
+#pragma unroll
+      for (int i = k; i < 6; ++i) A[i][j] -= tau * A[i][k];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double tau = 0.0;
+#pragma unroll
+    for (int i = j; i < 6; ++i) tau += A[i][j] * b[i];
+    tau /= A1[j];
+#pragma unroll
+    for (int i = j; i < 6; ++i) b[i] -= tau * A[i][j];
+  }
+  x[3] = b[3] / A2[3];
+#pragma unroll
+  for (int i = 2; i >= 0; --i) {
+    double sum = 0.0;
+#pragma unroll
+    for (int j = i + 1; j < 4; ++j) sum += A[i][j] * x[j];
+    x[i] = (b[i] - sum) / A2[i];
+  }
+  return true;
+}
+
+__host__ __device__ void rodrigues_v2m(const double r[3], double R[9]) {
+  const double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (th < DBL_EPSILON) {
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  const double c = cos(th), s = sin(th), c1 = 1.0 - c, it = 1.0 / th;
+  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  // c I + c1 r r^T + s [r]x, summed as cv::Matx33d does (elementwise, in order)
+  R[0] = c + c1 * (x * x);     R[1] = c1 * (x * y) + s * -z; R[2] = c1 * (x * z) + s * y;
+  R[3] = c1 * (x * y) + s * z; R[4] = c + c1 * (y * y);       R[5] = c1 * (y * z) + s * -x;
+  R[6] = c1 * (x * z) + s * -y; R[7] = c1 * (y * z) + s * x;  R[8] = c + c1 * (z * z);
+}
+
+__host__ __device__ void rodrigues_m2v(const double R[9], double r[3]) {
+  double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+  const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+  double c = (R[0] + R[4] + R[8] - 1.0) * 0.5;
+  c = c > 1.0 ? 1.0 : (c < -1.0 ? -1.0 : c);
+  const double th = acos(c);
+  if (s < 1e-5) {
+    if (c > 0) {
+      r[0] = r[1] = r[2] = 0.0;
+      return;
+    }
+    double t = (R[0] + 1) * 0.5;
+    rx = sqrt(fmax(t, 0.0));
+    t = (R[4] + 1) * 0.5;
+    ry = sqrt(fmax(t, 0.0)) * (R[1] < 0 ? -1.0 : 1.0);
+    t = (R[8] + 1) * 0.5;
+    rz = sqrt(fmax(t, 0.0)) * (R[2] < 0 ? -1.0 : 1.0);
+    if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+    const double k = th / sqrt(rx * rx + ry * ry + rz * rz);
+    r[0] = rx * k; r[1] = ry * k; r[2] = rz * k;
+    return;
+  }
+  const double k = th / (2.0 * s);
+  r[0] = rx * k; r[1] = ry * k; r[2] = rz * k;
+}
+
+// ---- EPnP (epnp::compute_pose) on 5 correspondences, one wave ----------
+struct EpnpIn {
+  double pw[kModel][3];
+  double us[kModel][2];
+};
+
+__host__ __device__ __forceinline__ double dot3(const double* x, const double* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; }
+
+__host__ __device__ double r_and_t(const EpnpIn& in, const double (&alpha)[kModel][4], const double (&ut)[4][12],
+                          const double betas[4], const PnPCam& k, double R[9], double t[3]) {
+  double ccs[4][3] = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) ccs[j][m] += betas[i] * ut[i][3 * j + m];
+  double pcs[kModel][3];
+#pragma unroll
+  for (int p = 0; p < kModel; ++p)
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      pcs[p][m] = alpha[p][0] * ccs[0][m] + alpha[p][1] * ccs[1][m] + alpha[p][2] * ccs[2][m] + alpha[p][3] * ccs[3][m];
+  if (pcs[0][2] < 0.0) {
+#pragma unroll
+    for (int p = 0; p < kModel; ++p)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) pcs[p][m] = -pcs[p][m];
+  }
+  double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < kModel; ++p)
+#pragma unroll
+    for (int m = 0; m < 3; ++m) { pc0[m] += pcs[p][m]; pw0[m] += in.pw[p][m]; }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) { pc0[m] /= kModel; pw0[m] /= kModel; }
+  double abt[3][3] = {};
+#pragma unroll
+  for (int p = 0; p < kModel; ++p)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) abt[j][m] += (pcs[p][j] - pc0[j]) * (in.pw[p][m] - pw0[m]);
+  double U3[3][3], w3[3], Vt3[3][3];
+  cv_svd<3, 3>(abt, U3, w3, Vt3);
+  // R = U V^T: R(i, j) = sum_k U(i, k) V(j, k), U(i, k) = U3[k][i], V(j, k) = Vt3[k][j]
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = U3[0][i] * Vt3[0][j] + U3[1][i] * Vt3[1][j] + U3[2][i] * Vt3[2][j];
+  const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
+                     R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+  if (det < 0) { R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8]; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = pc0[i] - dot3(R + 3 * i, pw0);
+  double sum = 0.0;
+#pragma unroll
+  for (int p = 0; p < kModel; ++p) {
+    const double* x = in.pw[p];
+    const double Xc = dot3(R, x) + t[0];
+    const double Yc = dot3(R + 3, x) + t[1];
+    const double iz = 1.0 / (dot3(R + 6, x) + t[2]);
+    const double ue = k.uc + k.fu * Xc * iz, ve = k.vc + k.fv * Yc * iz;
+    const double du = in.us[p][0] - ue, dv = in.us[p][1] - ve;
+    sum += sqrt(du * du + dv * dv);
+  }
+  return sum / kModel;
+}
+
+__host__ __device__ void gauss_newton(const double (&L)[6][10], const double (&rho)[6], double b[4]) {
+  for (int it = 0; it < 5; ++it) {
+    double A[6][4], r[6], x[4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double* l = L[i];
+      A[i][0] = 2 * l[0] * b[0] + l[1] * b[1] + l[3] * b[2] + l[6] * b[3];
+      A[i][1] = l[1] * b[0] + 2 * l[2] * b[1] + l[4] * b[2] + l[7] * b[3];
+      A[i][2] = l[3] * b[0] + l[4] * b[1] + 2 * l[5] * b[2] + l[8] * b[3];
+      A[i][3] = l[6] * b[0] + l[7] * b[1] + l[8] * b[2] + 2 * l[9] * b[3];
+      r[i] = rho[i] - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] + l[3] * b[0] * b[2] +
+                       l[4] * b[1] * b[2] + l[5] * b[2] * b[2] + l[6] * b[0] * b[3] + l[7] * b[1] * b[3] +
+                       l[8] * b[2] * b[3] + l[9] * b[3] * b[3]);
+    }
+    if (!qr_solve(A, r, x)) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] += x[i];
+  }
+}
+
+// (every lane of the wave computes the same: wave-uniform control flow)
+__host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double R[9], double t[3]) {
+  // choose_control_points: centroid + PCA (cv::SVD of PW0^T PW0)
+  double cws[4][3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    double s = 0.0;
+#pragma unroll
+    for (int p = 0; p < kModel; ++p) s += in.pw[p][m];
+    cws[0][m] = s / kModel;
+  }
+  double pw0[kModel][3];
+#pragma unroll
+  for (int p = 0; p < kModel; ++p)
+#pragma unroll
+    for (int m = 0; m < 3; ++m) pw0[p][m] = in.pw[p][m] - cws[0][m];
+  double ptp[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      double s = 0.0;
+#pragma unroll
+      for (int p = 0; p < kModel; ++p) s += pw0[p][a] * pw0[p][b];
+      ptp[a][b] = s;
+    }
+  {
+    double Uc[3][3], dc[3], Vtc[3][3];
+    cv_svd<3, 3>(ptp, Uc, dc, Vtc);
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      const double kk = sqrt(dc[i - 1] / kModel);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) cws[i][m] = cws[0][m] + kk * Uc[i - 1][m];
+    }
+  }
+  // compute_barycentric_coordinates: cvInvert(CC, CV_SVD) = SVBkSb pinv
+  double ci[3][3];
+  {
+    double cc[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 1; j < 4; ++j) cc[i][j - 1] = cws[j][i] - cws[0][i];
+    double Uc[3][3], wc[3], Vtc[3][3];
+    cv_svd<3, 3>(cc, Uc, wc, Vtc);
+    double thr = (wc[0] + wc[1] + wc[2]) * (kDblEps * 2);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) ci[j][q] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      double wi = wc[i];
+      if (fabs(wi) <= thr) continue;
+      wi = 1.0 / wi;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double vw = Vtc[i][j] * wi;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) ci[j][q] = ci[j][q] + vw * Uc[i][q];
+      }
+    }
+  }
+  double alpha[kModel][4];
+#pragma unroll
+  for (int p = 0; p < kModel; ++p) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      alpha[p][1 + j] = ci[j][0] * (in.pw[p][0] - cws[0][0]) + ci[j][1] * (in.pw[p][1] - cws[0][1]) +
+                        ci[j][2] * (in.pw[p][2] - cws[0][2]);
+    alpha[p][0] = 1.0 - alpha[p][1] - alpha[p][2] - alpha[p][3];
+  }
+  // M^T M (cvMulTransposed: the rows of M summed in order), then cv::SVD of
+  // it with OpenCV's sequential sums -- the 5-point problem leaves a 2-D
+  // (near-)null space whose basis any reordering of the sums would rotate
+  double ut[4][12];  // ut[q] = OpenCV's ut row 11 - q
+  {
+    double MtM[12][12];
+#pragma unroll
+    for (int x = 0; x < 12; ++x)
+#pragma unroll
+      for (int y = 0; y < 12; ++y) MtM[x][y] = 0.0;
+#pragma unroll
+    for (int p = 0; p < kModel; ++p) {
+      double M1[12], M2[12];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        M1[3 * jj] = alpha[p][jj] * k.fu; M1[3 * jj + 1] = 0.0; M1[3 * jj + 2] = alpha[p][jj] * (k.uc - in.us[p][0]);
+        M2[3 * jj] = 0.0; M2[3 * jj + 1] = alpha[p][jj] * k.fv; M2[3 * jj + 2] = alpha[p][jj] * (k.vc - in.us[p][1]);
+      }
+#pragma unroll
+      for (int x = 0; x < 12; ++x)
+#pragma unroll
+        for (int y = 0; y < 12; ++y) MtM[x][y] = MtM[x][y] + M1[x] * M1[y];
+#pragma unroll
+      for (int x = 0; x < 12; ++x)
+#pragma unroll
+        for (int y = 0; y < 12; ++y) MtM[x][y] = MtM[x][y] + M2[x] * M2[y];
+    }
+    double U[12][12], w[12], Vt[12][12];
+    cv_svd<12, 12>(MtM, U, w, Vt);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < 12; ++m) ut[q][m] = U[11 - q][m];
+  }
+  double L[6][10], rho[6];
+  {
+    const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double dv[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) dv[q][m] = ut[q][3 * pa[i] + m] - ut[q][3 * pb[i] + m];
+      L[i][0] = dot3(dv[0], dv[0]); L[i][1] = 2.0 * dot3(dv[0], dv[1]); L[i][2] = dot3(dv[1], dv[1]);
+      L[i][3] = 2.0 * dot3(dv[0], dv[2]); L[i][4] = 2.0 * dot3(dv[1], dv[2]); L[i][5] = dot3(dv[2], dv[2]);
+      L[i][6] = 2.0 * dot3(dv[0], dv[3]); L[i][7] = 2.0 * dot3(dv[1], dv[3]); L[i][8] = 2.0 * dot3(dv[2], dv[3]);
+      L[i][9] = dot3(dv[3], dv[3]);
+      const double d0 = cws[pa[i]][0] - cws[pb[i]][0], d1 = cws[pa[i]][1] - cws[pb[i]][1],
+                   d2 = cws[pa[i]][2] - cws[pb[i]][2];
+      rho[i] = d0 * d0 + d1 * d1 + d2 * d2;
+    }
+  }
+  double Rs[3][9], ts[3][3], err[3];
+  {
+    double A4[6][4], b4[4];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { A4[i][0] = L[i][0]; A4[i][1] = L[i][1]; A4[i][2] = L[i][3]; A4[i][3] = L[i][6]; }
+    cv_lstsq<6, 4>(A4, rho, b4);
+    double be[4];
+    if (b4[0] < 0) {
+      be[0] = sqrt(-b4[0]); be[1] = -b4[1] / be[0]; be[2] = -b4[2] / be[0]; be[3] = -b4[3] / be[0];
+    } else {
+      be[0] = sqrt(b4[0]); be[1] = b4[1] / be[0]; be[2] = b4[2] / be[0]; be[3] = b4[3] / be[0];
+    }
+    gauss_newton(L, rho, be);
+    err[0] = r_and_t(in, alpha, ut, be, k, Rs[0], ts[0]);
+  }
+  {
+    double A3[6][3], b3[3];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { A3[i][0] = L[i][0]; A3[i][1] = L[i][1]; A3[i][2] = L[i][2]; }
+    cv_lstsq<6, 3>(A3, rho, b3);
+    double be[4];
+    if (b3[0] < 0) { be[0] = sqrt(-b3[0]); be[1] = b3[2] < 0 ? sqrt(-b3[2]) : 0.0; }
+    else { be[0] = sqrt(b3[0]); be[1] = b3[2] > 0 ? sqrt(b3[2]) : 0.0; }
+    if (b3[1] < 0) be[0] = -be[0];
+    be[2] = 0.0; be[3] = 0.0;
+    gauss_newton(L, rho, be);
+    err[1] = r_and_t(in, alpha, ut, be, k, Rs[1], ts[1]);
+  }
+  {
+    double A5[6][5], b5[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) A5[i][j] = L[i][j];
+    cv_lstsq<6, 5>(A5, rho, b5);
+    double be[4];
+    if (b5[0] < 0) { be[0] = sqrt(-b5[0]); be[1] = b5[2] < 0 ? sqrt(-b5[2]) : 0.0; }
+    else { be[0] = sqrt(b5[0]); be[1] = b5[2] > 0 ? sqrt(b5[2]) : 0.0; }
+    if (b5[1] < 0) be[0] = -be[0];
+    be[2] = b5[3] / be[0];
+    be[3] = 0.0;
+    gauss_newton(L, rho, be);
+    err[2] = r_and_t(in, alpha, ut, be, k, Rs[2], ts[2]);
+  }
+  int N = 0;
+  if (err[1] < err[0]) N = 1;
+  if (err[2] < err[N]) N = 2;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = N == 0 ? Rs[0][i] : N == 1 ? Rs[1][i] : Rs[2][i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = N == 0 ? ts[0][i] : N == 1 ? ts[1][i] : ts[2][i];
+}
+
+// cv::RNG(uint64(-1)) subsets of the whole iteration bound (one thread).
+__global__ void k_pnp_subsets(int n, int iters, int* __restrict__ sub) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t state = ~0ull;
+  auto next = [&]() -> unsigned { return cv_rng_next(state); };
+  for (int it = 0; it < iters; ++it) {
+    int idx[kModel];
+    if (n == kModel) {
+      for (int i = 0; i < kModel; ++i) idx[i] = i;
+    } else {
+      for (int i = 0; i < kModel; ++i) {
+        int v;
+        while (true) {
+          v = int(next() % unsigned(n));
+          int j = 0;
+          for (; j < i; ++j)
+            if (idx[j] == v) break;
+          if (j == i) break;
+        }
+        idx[i] = v;
+      }
+    }
+    for (int i = 0; i < kModel; ++i) sub[it * kModel + i] = idx[i];
+  }
+}
+
+// One wave per hypothesis: EPnP on its subset -> model (rvec 3 | tvec 3).
+__global__ __launch_bounds__(64) void k_pnp_epnp(const double* __restrict__ obj, const double* __restrict__ img,
+                                                 const int* __restrict__ sub, PnPCam k, double* __restrict__ model) {
+  const int it = blockIdx.x;
+  EpnpIn in;
+#pragma unroll
+  for (int p = 0; p < kModel; ++p) {
+    const int q = sub[it * kModel + p];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) in.pw[p][m] = double(float(obj[3 * q + m]));
+    // undistortPoints (normalised, stored as float), mapped back by epnp
+    const float xn = float((double(float(img[2 * q])) - k.uc) * (1.0 / k.fu));
+    const float yn = float((double(float(img[2 * q + 1])) - k.vc) * (1.0 / k.fv));
+    in.us[p][0] = double(xn) * k.fu + k.uc;
+    in.us[p][1] = double(yn) * k.fv + k.vc;
+  }
+  double R[9], t[3], r[3];
+  epnp5(in, k, R, t);
+  rodrigues_m2v(R, r);
+  if (threadIdx.x == 0) {
+    double* o = model + 6 * it;
+    o[0] = r[0]; o[1] = r[1]; o[2] = r[2]; o[3] = t[0]; o[4] = t[1]; o[5] = t[2];
+  }
+}
+
+// PnPRansacCallback::computeError + findInliers for object point q.
+__device__ __forceinline__ bool pnp_inlier(const double* __restrict__ obj, const double* __restrict__ img, int q,
+                                           const double R[9], const double t[3], const PnPCam& k, float thr) {
+  const double x = double(float(obj[3 * q])), y = double(float(obj[3 * q + 1])), z = double(float(obj[3 * q + 2]));
+  const double X = R[0] * x + R[1] * y + R[2] * z + t[0];
+  const double Y = R[3] * x + R[4] * y + R[5] * z + t[1];
+  const double Z = R[6] * x + R[7] * y + R[8] * z + t[2];
+  const double iz = Z != 0.0 ? 1.0 / Z : 1.0;
+  const float pu = float(X * iz * k.fu + k.uc), pv = float(Y * iz * k.fv + k.vc);
+  const float du = float(img[2 * q]) - pu, dv = float(img[2 * q + 1]) - pv;
+  const float e = float(sqrt(double(du) * du + double(dv) * dv));
+  return e <= thr;
+}
+
+__global__ __launch_bounds__(256) void k_pnp_count(int n, const double* __restrict__ obj,
+                                                   const double* __restrict__ img, const double* __restrict__ model,
+                                                   PnPCam k, float thr, int* __restrict__ cnt) {
+  __shared__ int sh[4];
+  const int it = blockIdx.x;
+  double R[9], t[3];
+  rodrigues_v2m(model + 6 * it, R);
+  t[0] = model[6 * it + 3]; t[1] = model[6 * it + 4]; t[2] = model[6 * it + 5];
+  int c = 0;
+  for (int q = threadIdx.x; q < n; q += 256) c += pnp_inlier(obj, img, q, R, t, k, thr) ? 1 : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[it] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// Replay of RANSACPointSetRegistrator::run's acceptance over the counts, then
+// the winner's inliers in index order.  One wave.  res: [0] found, [1] best
+// iteration, [2] inlier count.
+__global__ __launch_bounds__(64) void k_pnp_select(int n, int iters, double confidence,
+                                                   const double* __restrict__ obj, const double* __restrict__ img,
+                                                   const double* __restrict__ model, const int* __restrict__ cnt,
+                                                   PnPCam k, float thr, int* __restrict__ res, int* __restrict__ inl) {
+  const int lane = threadIdx.x;
+  int best = -1, max_good = 0;
+  int niters = iters > 1 ? iters : 1;
+  for (int it = 0; it < niters && it < iters; ++it) {
+    const int good = cnt[it];
+    if (n == kModel) { best = it; max_good = n; break; }
+    if (good > (max_good > kModel - 1 ? max_good : kModel - 1)) {
+      best = it;
+      max_good = good;
+      // RANSACUpdateNumIters(confidence, outlier ratio, 5, niters)
+      double p = fmin(fmax(confidence, 0.0), 1.0), ep = fmin(fmax(double(n - good) / n, 0.0), 1.0);
+      double num = fmax(1.0 - p, DBL_MIN);
+      double denom = 1.0 - pow(1.0 - ep, double(kModel));
+      if (denom < DBL_MIN) {
+        niters = 0;
+      } else {
+        num = log(num);
+        denom = log(denom);
+        niters = (denom >= 0 || -num >= niters * (-denom)) ? niters : int(rint(num / denom));
+      }
+    }
+  }
+  if (lane == 0) { res[0] = best >= 0 ? 1 : 0; res[1] = best; res[2] = best >= 0 ? max_good : 0; }
+  if (best < 0) return;
+  if (n == kModel) {  // run() with count == modelPoints: the mask is all ones
+    if (lane < kModel) inl[lane] = lane;
+    return;
+  }
+  double R[9], t[3];
+  rodrigues_v2m(model + 6 * best, R);
+  t[0] = model[6 * best + 3]; t[1] = model[6 * best + 4]; t[2] = model[6 * best + 5];
+  int base = 0;
+  for (int q0 = 0; q0 < n; q0 += 64) {
+    const int q = q0 + lane;
+    const bool in = q < n && pnp_inlier(obj, img, q, R, t, k, thr);
+    const unsigned long long m = __ballot(in);
+    if (in) inl[base + __popcll(m & ((1ull << lane) - 1ull))] = q;
+    base += __popcll(m);
+  }
+}
+
+struct PnPCtx {
+  hipStream_t stream = nullptr;
+  size_t cap = 0;
+  double* obj = nullptr;
+  double* img = nullptr;
+  int* inl = nullptr;
+  int* sub = nullptr;
+  double* model = nullptr;
+  int* cnt = nullptr;
+  int* res = nullptr;
+  ~PnPCtx() {
+    if (stream) hipStreamSynchronize(stream);
+    hipFree(obj); hipFree(img); hipFree(inl); hipFree(sub); hipFree(model); hipFree(cnt); hipFree(res);
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+int pfail(int code, const char* msg) {
+  sfm_internal_set_error(msg);
+  return code;
+}
+
+}  // namespace
+}  // namespace sfm
+
+using namespace sfm;
+
+extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, const double* img, const double* K9,
+                              int32_t iterations, double reproj_err, double confidence, double* rvec, double* tvec,
+                              int32_t* inliers, int32_t* n_inliers, int32_t* found) {
+  if (!found || !n_inliers || !rvec || !tvec || !K9) return pfail(SFM_EINVAL, "NULL argument");
+  *found = 0;
+  *n_inliers = 0;
+  if (n < 0 || iterations < 0 || iterations > kMaxIters) return pfail(SFM_EINVAL, "bad n or iterations");
+  if (!(confidence > 0.0 && confidence < 1.0)) return pfail(SFM_EINVAL, "confidence must lie in (0, 1)");
+  if (n > 0 && (!obj || !img)) return pfail(SFM_EINVAL, "NULL point arrays");
+  if (n < kModel) return 0;  // RANSAC needs a full subset: no model (as cv::solvePnPRansac's false)
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return pfail(SFM_ENODEV, "no device");
+  if (hipSetDevice(device) != hipSuccess) return pfail(SFM_ENODEV, "hipSetDevice failed");
+  struct Cache {
+    std::map<int, PnPCtx*> m;
+    ~Cache() {
+      for (auto& kv : m) delete kv.second;
+    }
+  };
+  static thread_local Cache cache;
+  PnPCtx*& c = cache.m[device];
+  if (!c) {
+    c = new PnPCtx();
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      c = nullptr;
+      return pfail(SFM_EIO, "hipStreamCreate failed");
+    }
+    if (hipMalloc(&c->sub, sizeof(int) * kModel * kMaxIters) != hipSuccess ||
+        hipMalloc(&c->model, sizeof(double) * 6 * kMaxIters) != hipSuccess ||
+        hipMalloc(&c->cnt, sizeof(int) * kMaxIters) != hipSuccess || hipMalloc(&c->res, sizeof(int) * 4) != hipSuccess)
+      return pfail(SFM_ENOMEM, "hipMalloc failed");
+  }
+  if (size_t(n) > c->cap) {
+    hipFree(c->obj); hipFree(c->img); hipFree(c->inl);
+    c->obj = nullptr; c->img = nullptr; c->inl = nullptr; c->cap = 0;
+    const size_t cap = std::max<size_t>(size_t(n), 1024);
+    if (hipMalloc(&c->obj, sizeof(double) * 3 * cap) != hipSuccess ||
+        hipMalloc(&c->img, sizeof(double) * 2 * cap) != hipSuccess || hipMalloc(&c->inl, sizeof(int) * cap) != hipSuccess)
+      return pfail(SFM_ENOMEM, "hipMalloc failed");
+    c->cap = cap;
+  }
+  const PnPCam k{K9[0], K9[4], K9[2], K9[5]};
+  const int iters = iterations > 0 ? iterations : 1;
+  const float thr = float(reproj_err * reproj_err);
+  hipStream_t s = c->stream;
+  if (hipMemcpyAsync(c->obj, obj, sizeof(double) * 3 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(c->img, img, sizeof(double) * 2 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess)
+    return pfail(SFM_EIO, "upload failed");
+  k_pnp_subsets<<<1, 64, 0, s>>>(n, iters, c->sub);
+  k_pnp_epnp<<<iters, 64, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
+  k_pnp_count<<<iters, 256, 0, s>>>(n, c->obj, c->img, c->model, k, thr, c->cnt);
+  k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->res, c->inl);
+  int res[4] = {0, -1, 0, 0};
+  double mdl[6];
+  hipMemcpyAsync(res, c->res, sizeof(int) * 4, hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return pfail(SFM_EIO, "PnP kernels failed");
+  if (!res[0]) return 0;
+  hipMemcpyAsync(mdl, c->model + 6 * res[1], sizeof(double) * 6, hipMemcpyDeviceToHost, s);
+  if (inliers && res[2] > 0) hipMemcpyAsync(inliers, c->inl, sizeof(int) * res[2], hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return pfail(SFM_EIO, "PnP download failed");
+  for (int i = 0; i < 3; ++i) { rvec[i] = mdl[i]; tvec[i] = mdl[3 + i]; }
+  *n_inliers = res[2];
+  *found = 1;
+  return 0;
+}

@@ -1,0 +1,42 @@
+"""GPU: the device solvePnPRansac (sfm_pnp_ransac, pnp_kernels.hip) against
+the oracle (oracle/pnp_oracle.py) on seeded scenes: the same found flag,
+the SAME inlier index list (integer parity), and the pose within 1e-6 (the
+device's Jacobi SVDs and the oracle's LAPACK agree to rounding; the pose
+is invariant to the eigenvector signs).  Covers n = 5 (no sampling), n = 6,
+planar points, 90 % outliers (adaptive bound never shrinks) and n < 5."""
+import numpy as np
+import pytest
+
+import sfm_amd
+from oracle import pnp_oracle as P
+from tests.pnp_cases import CASES, K, scene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,seed,noise,outl,planar", CASES)
+def test_pnp_ransac_matches_oracle(n, seed, noise, outl, planar):
+    X, uv, rv, tv = scene(n, seed, noise=noise, outliers=outl, planar=planar)
+    ok_o, r_o, t_o, inl_o = P.solve_pnp_ransac(X, uv, K)
+    ok_g, r_g, t_g, inl_g = sfm_amd.solvePnPRansac(X, uv, K)
+    assert ok_g == ok_o
+    assert np.array_equal(inl_g, inl_o), (len(inl_g), len(inl_o))
+    if ok_o:
+        assert np.max(np.abs(r_g - r_o)) <= 1e-6 * max(1.0, np.max(np.abs(r_o)))
+        assert np.max(np.abs(t_g - t_o)) <= 1e-6 * max(1.0, np.max(np.abs(t_o)))
+
+
+@pytest.mark.parametrize("iters,thr", [(1, 7.0), (100, 2.0), (20, 0.5)])
+def test_pnp_ransac_parameters(iters, thr):
+    X, uv, _, _ = scene(400, 21, noise=0.7, outliers=0.3)
+    ok_o, r_o, t_o, inl_o = P.solve_pnp_ransac(X, uv, K, iterations=iters, reproj_err=thr)
+    ok_g, r_g, t_g, inl_g = sfm_amd.solvePnPRansac(X, uv, K, iterationsCount=iters, reprojectionError=thr)
+    assert ok_g == ok_o and np.array_equal(inl_g, inl_o)
+    if ok_o:
+        assert np.allclose(r_g, r_o, atol=1e-6) and np.allclose(t_g, t_o, atol=1e-6)
+
+
+def test_pnp_too_few_points():
+    X, uv, _, _ = scene(4, 1, noise=0.0, outliers=0.0)
+    ok, r, t, inl = sfm_amd.solvePnPRansac(X, uv, K)
+    assert not ok and len(inl) == 0
