@@ -264,6 +264,13 @@ int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, const double* i
                    int32_t iterations, double reproj_err, double confidence, double* rvec, double* tvec,
                    int32_t* inliers, int32_t* n_inliers, int32_t* found);
 
+/* Two-view triangulation of new map points (GeometryUtils::triangulatePoints
+ * at CSfM.cpp:156 / :918), as cv::triangulatePoints on P = K [R|t]: point i
+ * seen at uv0[i] by camera cam0[i] and at uv1[i] by camera cam1[i]; P
+ * [n_cams][12] row-major 3x4 projection matrices; X [n][3] out. */
+int sfm_triangulate_points(int32_t device, int32_t n, const int32_t* cam0, const int32_t* cam1, const double* uv0,
+                           const double* uv1, int32_t n_cams, const double* P, double* X);
+
 /* Testing hook: solve the dense SPD system A y = b (A [n][n] row-major,
  * both triangles given; only the upper triangle is read) with the device
  * Cholesky + substitution kernels used for the reduced camera system.

@@ -552,3 +552,24 @@ def solve_pnp_ransac(opts, ipts, K, iterations: int = 20, reproj_err: float = 7.
     if best is None:
         return False, np.zeros(3), np.zeros(3), np.zeros(0, np.int32)
     return True, best[0], best[1], np.nonzero(best_mask)[0].astype(np.int32)
+
+
+def triangulate_points(cam0, cam1, uv0, uv1, P):
+    """cv::triangulatePoints (cvTriangulatePoints) per point on P = K [R|t]
+    (P [C][3][4]): the 4x4 DLT system of both views, the right singular
+    vector of its smallest singular value (cv_svd), homogeneous division
+    (the CSfM.cpp:156 / :918 call; GeometryUtils is absent: parity
+    unpinned).  -> X [n][3]."""
+    P = np.asarray(P, np.float64).reshape(-1, 3, 4)
+    n = len(cam0)
+    X = np.zeros((n, 3))
+    for i in range(n):
+        Pa, Pb = P[cam0[i]], P[cam1[i]]
+        xa, ya = float(uv0[i][0]), float(uv0[i][1])
+        xb, yb = float(uv1[i][0]), float(uv1[i][1])
+        A = [[xa * Pa[2, k] - Pa[0, k] for k in range(4)], [ya * Pa[2, k] - Pa[1, k] for k in range(4)],
+             [xb * Pb[2, k] - Pb[0, k] for k in range(4)], [yb * Pb[2, k] - Pb[1, k] for k in range(4)]]
+        _, _, Vt = cv_svd(A)
+        h = Vt[3][3]
+        X[i] = [Vt[3][0] / h, Vt[3][1] / h, Vt[3][2] / h]
+    return X

@@ -152,6 +152,8 @@ _SIGNATURES = {
     "sfm_representative_descriptors": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "sfm_pnp_ransac": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_double, c_double,
                                c_void_p, c_void_p, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    "sfm_triangulate_points": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                       c_void_p]),
     "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
                                     POINTER(c_int32)]),
     "sfm_klt_default_params": (None, [POINTER(KLTParams)]),
