@@ -134,19 +134,37 @@ DBL_EPS = np.finfo(float).eps
 DBL_MIN = np.finfo(float).tiny
 
 
-def cv_svd(A):
-    """A (m x n), m >= n -> (w [n] descending, U [m x n] columns, Vt [n x n])."""
+def tree16(v):
+    """The 16-lane butterfly sum of pnp_kernels.hip (shfl_xor 8, 4, 2, 1 within
+    16 lanes; entries past len(v) are zeros): ((v_k + v_k^8) + ...)."""
+    a = list(map(float, v)) + [0.0] * (16 - len(v))
+    for off in (8, 4, 2, 1):
+        a = [a[k] + a[k ^ off] for k in range(16)]
+    return a[0]
+
+
+def cv_svd(A, tree=False):
+    """A (m x n), m >= n -> (w [n] descending, U [m x n] columns, Vt [n x n]).
+    tree=True: every sum over the m entries of a row is the 16-lane butterfly
+    (tree16) -- the order in which the kernel's lane-parallel 12x12 SVD of
+    EPnP's M^T M adds (m <= 16); otherwise OpenCV's sequential order."""
     A = np.asarray(A, np.float64)
     m, n = A.shape
-    assert m >= n
+    assert m >= n and (not tree or m <= 16)
+
+    def ssum(vals):
+        if tree:
+            return tree16(vals)
+        acc = 0.0
+        for x in vals:
+            acc += x
+        return acc
+
     At = [list(map(float, A[:, i])) for i in range(n)]
     Vt = [[1.0 if i == j else 0.0 for j in range(n)] for i in range(n)]
     W = [0.0] * n
     for i in range(n):
-        sd = 0.0
-        for k in range(m):
-            sd += At[i][k] * At[i][k]
-        W[i] = sd
+        W[i] = ssum([At[i][k] * At[i][k] for k in range(m)])
     eps = DBL_EPS * 10
     for _ in range(max(m, 30)):
         changed = False
@@ -154,9 +172,7 @@ def cv_svd(A):
             for j in range(i + 1, n):
                 Ai, Aj = At[i], At[j]
                 a, b = W[i], W[j]
-                p = 0.0
-                for k in range(m):
-                    p += Ai[k] * Aj[k]
+                p = ssum([Ai[k] * Aj[k] for k in range(m)])
                 if abs(p) <= eps * math.sqrt(a * b):
                     continue
                 p *= 2
@@ -169,15 +185,13 @@ def cv_svd(A):
                 else:
                     c = math.sqrt((gamma + beta) / (gamma * 2))
                     s = p / (gamma * c * 2)
-                a = b = 0.0
                 for k in range(m):
                     t0 = c * Ai[k] + s * Aj[k]
                     t1 = -s * Ai[k] + c * Aj[k]
                     Ai[k] = t0
                     Aj[k] = t1
-                    a += t0 * t0
-                    b += t1 * t1
-                W[i], W[j] = a, b
+                W[i] = ssum([x * x for x in Ai])
+                W[j] = ssum([x * x for x in Aj])
                 changed = True
                 Vi, Vj = Vt[i], Vt[j]
                 for k in range(n):
@@ -188,10 +202,7 @@ def cv_svd(A):
         if not changed:
             break
     for i in range(n):
-        sd = 0.0
-        for k in range(m):
-            sd += At[i][k] * At[i][k]
-        W[i] = math.sqrt(sd)
+        W[i] = math.sqrt(ssum([At[i][k] * At[i][k] for k in range(m)]))
     for i in range(n - 1):
         j = i
         for k in range(i + 1, n):
@@ -211,21 +222,14 @@ def cv_svd(A):
                 At[i][k] = val0 if (rng.next() & 256) != 0 else -val0
             for _ in range(2):
                 for j in range(i):
-                    sd = 0.0
+                    sd = ssum([At[i][k] * At[j][k] for k in range(m)])
                     for k in range(m):
-                        sd += At[i][k] * At[j][k]
-                    asum = 0.0
-                    for k in range(m):
-                        t = At[i][k] - sd * At[j][k]
-                        At[i][k] = t
-                        asum += abs(t)
+                        At[i][k] = At[i][k] - sd * At[j][k]
+                    asum = ssum([abs(At[i][k]) for k in range(m)])
                     asum = 1.0 / asum if asum > eps * 100 else 0.0
                     for k in range(m):
                         At[i][k] *= asum
-            sd = 0.0
-            for k in range(m):
-                sd += At[i][k] * At[i][k]
-            sd = math.sqrt(sd)
+            sd = math.sqrt(ssum([At[i][k] * At[i][k] for k in range(m)]))
             ii += 1
         s = 1.0 / sd if sd > DBL_MIN else 0.0
         for k in range(m):
@@ -378,7 +382,7 @@ def epnp(K, opts, ipts):
             for r in range(2 * n):
                 s += M[r][a] * M[r][b]
             MtM[a][b] = s
-    _, Um, _ = cv_svd(MtM)
+    _, Um, _ = cv_svd(MtM, tree=True)
     ut = Um.T  # rows: left singular vectors, descending singular values
     v = [ut[11], ut[10], ut[9], ut[8]]
     pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]

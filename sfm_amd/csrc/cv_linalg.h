@@ -26,17 +26,21 @@ __host__ __device__ __forceinline__ unsigned cv_rng_next(uint64_t& state) {
 // singular vectors (zero singular values completed from cv::RNG(0x12345678)
 // vectors).  On return U[i] = i-th left singular vector (At row i), w
 // descending, Vt rows = right singular vectors.
-template <int M, int N>
-__host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
+// In place on At (= A^T, N rows of length M); kV = false skips the right
+// singular vectors (Vt is then not touched): EPnP needs only U of M^T M,
+// and without the second 12x12 array the kernel stays in registers.
+template <int M, int N, bool kV>
+__host__ __device__ void cv_svd_at(double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
   double W[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double sd = 0.0;
 #pragma unroll
-    for (int k = 0; k < M; ++k) { U[i][k] = A[k][i]; sd += U[i][k] * U[i][k]; }
+    for (int k = 0; k < M; ++k) sd += U[i][k] * U[i][k];
     W[i] = sd;
+    if (kV)
 #pragma unroll
-    for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
+      for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
   }
   const double eps = kDblEps * 10;
   for (int iter = 0; iter < (M > 30 ? M : 30); ++iter) {
@@ -72,11 +76,12 @@ __host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], doub
         }
         W[i] = a; W[j] = b;
         changed = true;
+        if (kV)
 #pragma unroll
-        for (int k = 0; k < N; ++k) {
-          const double t0 = c * Vt[i][k] + s * Vt[j][k], t1 = -s * Vt[i][k] + c * Vt[j][k];
-          Vt[i][k] = t0; Vt[j][k] = t1;
-        }
+          for (int k = 0; k < N; ++k) {
+            const double t0 = c * Vt[i][k] + s * Vt[j][k], t1 = -s * Vt[i][k] + c * Vt[j][k];
+            Vt[i][k] = t0; Vt[j][k] = t1;
+          }
       }
     if (!changed) break;
   }
@@ -100,8 +105,9 @@ __host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], doub
         const double tw = W[i]; W[i] = W[k]; W[k] = tw;
 #pragma unroll
         for (int e = 0; e < M; ++e) { const double x = U[i][e]; U[i][e] = U[k][e]; U[k][e] = x; }
+        if (kV)
 #pragma unroll
-        for (int e = 0; e < N; ++e) { const double x = Vt[i][e]; Vt[i][e] = Vt[k][e]; Vt[k][e] = x; }
+          for (int e = 0; e < N; ++e) { const double x = Vt[i][e]; Vt[i][e] = Vt[k][e]; Vt[k][e] = x; }
       }
   }
   uint64_t rng = 0x12345678ull;
@@ -139,6 +145,16 @@ __host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], doub
     for (int k = 0; k < M; ++k) U[i][k] *= sc;
     w[i] = W[i];
   }
+}
+
+// cv::SVD of A itself (A is copied transposed into U first).
+template <int M, int N>
+__host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int k = 0; k < M; ++k) U[i][k] = A[k][i];
+  cv_svd_at<M, N, true>(U, w, Vt);
 }
 
 // cv::solve(A, b, x, DECOMP_SVD) = SVBkSb: x = sum over w_i > 2 DBL_EPSILON

@@ -83,6 +83,212 @@ __host__ __device__ void rodrigues_m2v(const double R[9], double r[3]) {
   r[0] = rx * k; r[1] = ry * k; r[2] = rz * k;
 }
 
+// ---- cv::SVD of EPnP's 12x12 M^T M with the 12 columns over lanes --------
+// Lane k (mod 16) holds entry k of every row of At (lanes 12..15 of each
+// 16-lane segment hold zeros); the row sums are the 16-lane butterfly
+// (shfl_xor 8, 4, 2, 1 -- every lane ends with the same value, floating
+// addition being commutative), which oracle/pnp_oracle.py cv_svd(tree=True)
+// reproduces.  Otherwise JacobiSVDImpl_ step for step (no V).
+__device__ __forceinline__ double tree16(double v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+  return v;
+}
+
+// u[i] = At[i][lane & 15] on entry (M^T M is symmetric); on return the
+// four left singular vectors of the smallest singular values are in
+// ut[q] = OpenCV's ut row 11 - q, every lane holding all 12 entries.
+__device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]) {
+  const int k = threadIdx.x & 15;
+  double W[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) W[i] = tree16(u[i] * u[i]);
+  const double eps = kDblEps * 10;
+  for (int iter = 0; iter < 30; ++iter) {
+    bool changed = false;
+#pragma unroll
+    for (int i = 0; i < 11; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 12; ++j) {
+        const double a = W[i], b = W[j];
+        double p = tree16(u[i] * u[j]);
+        if (fabs(p) <= eps * sqrt(a * b)) continue;
+        p *= 2;
+        const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+        double c, sn;
+        if (beta < 0) {
+          const double delta = (gamma - beta) * 0.5;
+          sn = sqrt(delta / gamma);
+          c = p / (gamma * sn * 2);
+        } else {
+          c = sqrt((gamma + beta) / (gamma * 2));
+          sn = p / (gamma * c * 2);
+        }
+        const double t0 = c * u[i] + sn * u[j], t1 = -sn * u[i] + c * u[j];
+        u[i] = t0;
+        u[j] = t1;
+        W[i] = tree16(t0 * t0);
+        W[j] = tree16(t1 * t1);
+        changed = true;
+      }
+    if (!changed) break;
+  }
+  int ord[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { W[i] = sqrt(tree16(u[i] * u[i])); ord[i] = i; }
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    int j = i;
+#pragma unroll
+    for (int q = i + 1; q < 12; ++q)
+      if (W[j] < W[q]) j = q;
+#pragma unroll
+    for (int q = i + 1; q < 12; ++q)
+      if (j == q) {
+        const double tw = W[i]; W[i] = W[q]; W[q] = tw;
+        const int to = ord[i]; ord[i] = ord[q]; ord[q] = to;
+      }
+  }
+  // rows in sorted order (row r = u[ord[r]]), zero singular values completed
+  // from cv::RNG(0x12345678), then normalised; only rows 8..11 are kept
+  double row[12];
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    double x = 0.0;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) x = ord[r] == c ? u[c] : x;
+    row[r] = x;
+  }
+  uint64_t rng = 0x12345678ull;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    double sd = W[i];
+    for (int ii = 0; ii < 100 && sd <= kDblMin; ++ii) {
+      const double val0 = 1.0 / 12;
+      for (int e = 0; e < 12; ++e) {
+        const double v = (cv_rng_next(rng) & 256) != 0 ? val0 : -val0;
+        if (e == k) row[i] = v;
+      }
+      for (int it2 = 0; it2 < 2; ++it2)
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+          sd = tree16(row[i] * row[j]);
+          row[i] = row[i] - sd * row[j];
+          double asum = tree16(fabs(row[i]));
+          asum = asum > eps * 100 ? 1.0 / asum : 0.0;
+          row[i] *= asum;
+        }
+      sd = sqrt(tree16(row[i] * row[i]));
+    }
+    const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
+    row[i] *= sc;
+  }
+  if (k < 12 && threadIdx.x < 16)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lds[q * 12 + k] = row[11 - q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < 12; ++m) ut[q][m] = lds[q * 12 + m];
+}
+
+// Host build of the same 12x12 SVD (tools/pnp_host_check): the butterfly
+// order computed serially.
+__host__ inline double host_tree16(const double (&v)[12]) {
+  double a[16];
+  for (int q = 0; q < 16; ++q) a[q] = q < 12 ? v[q] : 0.0;
+  for (int off = 8; off > 0; off >>= 1) {
+    double b[16];
+    for (int q = 0; q < 16; ++q) b[q] = a[q] + a[q ^ off];
+    for (int q = 0; q < 16; ++q) a[q] = b[q];
+  }
+  return a[0];
+}
+__host__ inline void host_svd12_tree(double (&U)[12][12], double (&ut)[4][12]) {
+  double W[12], tmp[12];
+  for (int i = 0; i < 12; ++i) {
+    for (int q = 0; q < 12; ++q) tmp[q] = U[i][q] * U[i][q];
+    W[i] = host_tree16(tmp);
+  }
+  const double eps = kDblEps * 10;
+  for (int iter = 0; iter < 30; ++iter) {
+    bool changed = false;
+    for (int i = 0; i < 11; ++i)
+      for (int j = i + 1; j < 12; ++j) {
+        const double a = W[i], b = W[j];
+        for (int q = 0; q < 12; ++q) tmp[q] = U[i][q] * U[j][q];
+        double p = host_tree16(tmp);
+        if (fabs(p) <= eps * sqrt(a * b)) continue;
+        p *= 2;
+        const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+        double c, sn;
+        if (beta < 0) {
+          const double delta = (gamma - beta) * 0.5;
+          sn = sqrt(delta / gamma);
+          c = p / (gamma * sn * 2);
+        } else {
+          c = sqrt((gamma + beta) / (gamma * 2));
+          sn = p / (gamma * c * 2);
+        }
+        for (int q = 0; q < 12; ++q) {
+          const double t0 = c * U[i][q] + sn * U[j][q], t1 = -sn * U[i][q] + c * U[j][q];
+          U[i][q] = t0;
+          U[j][q] = t1;
+        }
+        for (int q = 0; q < 12; ++q) tmp[q] = U[i][q] * U[i][q];
+        W[i] = host_tree16(tmp);
+        for (int q = 0; q < 12; ++q) tmp[q] = U[j][q] * U[j][q];
+        W[j] = host_tree16(tmp);
+        changed = true;
+      }
+    if (!changed) break;
+  }
+  int ord[12];
+  for (int i = 0; i < 12; ++i) {
+    for (int q = 0; q < 12; ++q) tmp[q] = U[i][q] * U[i][q];
+    W[i] = sqrt(host_tree16(tmp));
+    ord[i] = i;
+  }
+  for (int i = 0; i < 11; ++i) {
+    int j = i;
+    for (int q = i + 1; q < 12; ++q)
+      if (W[j] < W[q]) j = q;
+    if (j != i) {
+      const double tw = W[i]; W[i] = W[j]; W[j] = tw;
+      const int to = ord[i]; ord[i] = ord[j]; ord[j] = to;
+    }
+  }
+  double row[12][12];
+  for (int r = 0; r < 12; ++r)
+    for (int q = 0; q < 12; ++q) row[r][q] = U[ord[r]][q];
+  uint64_t rng = 0x12345678ull;
+  for (int i = 0; i < 12; ++i) {
+    double sd = W[i];
+    for (int ii = 0; ii < 100 && sd <= kDblMin; ++ii) {
+      for (int e = 0; e < 12; ++e) row[i][e] = (cv_rng_next(rng) & 256) != 0 ? 1.0 / 12 : -1.0 / 12;
+      for (int it2 = 0; it2 < 2; ++it2)
+        for (int j = 0; j < i; ++j) {
+          for (int q = 0; q < 12; ++q) tmp[q] = row[i][q] * row[j][q];
+          sd = host_tree16(tmp);
+          for (int q = 0; q < 12; ++q) row[i][q] = row[i][q] - sd * row[j][q];
+          for (int q = 0; q < 12; ++q) tmp[q] = fabs(row[i][q]);
+          double asum = host_tree16(tmp);
+          asum = asum > eps * 100 ? 1.0 / asum : 0.0;
+          for (int q = 0; q < 12; ++q) row[i][q] *= asum;
+        }
+      for (int q = 0; q < 12; ++q) tmp[q] = row[i][q] * row[i][q];
+      sd = sqrt(host_tree16(tmp));
+    }
+    const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
+    for (int q = 0; q < 12; ++q) row[i][q] *= sc;
+  }
+  for (int q = 0; q < 4; ++q)
+    for (int m = 0; m < 12; ++m) ut[q][m] = row[11 - q][m];
+}
+
 // ---- EPnP (epnp::compute_pose) on 5 correspondences, one wave ----------
 struct EpnpIn {
   double pw[kModel][3];
@@ -173,7 +379,7 @@ __host__ __device__ void gauss_newton(const double (&L)[6][10], const double (&r
 }
 
 // (every lane of the wave computes the same: wave-uniform control flow)
-__host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double R[9], double t[3]) {
+__host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, double R[9], double t[3]) {
   // choose_control_points: centroid + PCA (cv::SVD of PW0^T PW0)
   double cws[4][3];
 #pragma unroll
@@ -246,38 +452,56 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double R[9], d
     alpha[p][0] = 1.0 - alpha[p][1] - alpha[p][2] - alpha[p][3];
   }
   // M^T M (cvMulTransposed: the rows of M summed in order), then cv::SVD of
-  // it with OpenCV's sequential sums -- the 5-point problem leaves a 2-D
-  // (near-)null space whose basis any reordering of the sums would rotate
+  // it.  The 5-point problem leaves a 2-D (near-)null space whose basis any
+  // change of rounding rotates, so the device and the oracle fix one order:
+  // sequential over the rows of M, the 16-lane butterfly over the 12 entries
+  // of a row of At (cv_svd12_lanes; oracle cv_svd(tree=True)).
   double ut[4][12];  // ut[q] = OpenCV's ut row 11 - q
   {
+    double M1[kModel][12], M2[kModel][12];
+#pragma unroll
+    for (int p = 0; p < kModel; ++p)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        M1[p][3 * jj] = alpha[p][jj] * k.fu; M1[p][3 * jj + 1] = 0.0;
+        M1[p][3 * jj + 2] = alpha[p][jj] * (k.uc - in.us[p][0]);
+        M2[p][3 * jj] = 0.0; M2[p][3 * jj + 1] = alpha[p][jj] * k.fv;
+        M2[p][3 * jj + 2] = alpha[p][jj] * (k.vc - in.us[p][1]);
+      }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // lane col (mod 16) holds column col of M^T M = entry col of every row of At
+    const int col = threadIdx.x & 15;
+    double u[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int p = 0; p < kModel; ++p) {
+        double mc1 = 0.0, mc2 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) { mc1 = c == col ? M1[p][c] : mc1; mc2 = c == col ? M2[p][c] : mc2; }
+        acc = acc + M1[p][i] * mc1;
+        acc = acc + M2[p][i] * mc2;
+      }
+      u[i] = col < 12 ? acc : 0.0;
+    }
+    cv_svd12_lanes(u, lds, ut);
+#else
     double MtM[12][12];
 #pragma unroll
     for (int x = 0; x < 12; ++x)
 #pragma unroll
-      for (int y = 0; y < 12; ++y) MtM[x][y] = 0.0;
+      for (int y = 0; y < 12; ++y) {
+        double acc = 0.0;
 #pragma unroll
-    for (int p = 0; p < kModel; ++p) {
-      double M1[12], M2[12];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        M1[3 * jj] = alpha[p][jj] * k.fu; M1[3 * jj + 1] = 0.0; M1[3 * jj + 2] = alpha[p][jj] * (k.uc - in.us[p][0]);
-        M2[3 * jj] = 0.0; M2[3 * jj + 1] = alpha[p][jj] * k.fv; M2[3 * jj + 2] = alpha[p][jj] * (k.vc - in.us[p][1]);
+        for (int p = 0; p < kModel; ++p) {
+          acc = acc + M1[p][x] * M1[p][y];
+          acc = acc + M2[p][x] * M2[p][y];
+        }
+        MtM[x][y] = acc;
       }
-#pragma unroll
-      for (int x = 0; x < 12; ++x)
-#pragma unroll
-        for (int y = 0; y < 12; ++y) MtM[x][y] = MtM[x][y] + M1[x] * M1[y];
-#pragma unroll
-      for (int x = 0; x < 12; ++x)
-#pragma unroll
-        for (int y = 0; y < 12; ++y) MtM[x][y] = MtM[x][y] + M2[x] * M2[y];
-    }
-    double U[12][12], w[12], Vt[12][12];
-    cv_svd<12, 12>(MtM, U, w, Vt);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int m = 0; m < 12; ++m) ut[q][m] = U[11 - q][m];
+    host_svd12_tree(MtM, ut);
+#endif
   }
   double L[6][10], rho[6];
   {
@@ -380,6 +604,7 @@ __global__ void k_pnp_subsets(int n, int iters, int* __restrict__ sub) {
 // One wave per hypothesis: EPnP on its subset -> model (rvec 3 | tvec 3).
 __global__ __launch_bounds__(64) void k_pnp_epnp(const double* __restrict__ obj, const double* __restrict__ img,
                                                  const int* __restrict__ sub, PnPCam k, double* __restrict__ model) {
+  __shared__ double lds[48];
   const int it = blockIdx.x;
   EpnpIn in;
 #pragma unroll
@@ -394,7 +619,7 @@ __global__ __launch_bounds__(64) void k_pnp_epnp(const double* __restrict__ obj,
     in.us[p][1] = double(yn) * k.fv + k.vc;
   }
   double R[9], t[3], r[3];
-  epnp5(in, k, R, t);
+  epnp5(in, k, lds, R, t);
   rodrigues_m2v(R, r);
   if (threadIdx.x == 0) {
     double* o = model + 6 * it;

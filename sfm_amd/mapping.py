@@ -89,8 +89,15 @@ class IncrementalMapper:
         self.tr_uv = np.zeros((0, 2), np.float32)   # live tracks: current position
         self.tr_id = np.zeros(0, np.int64)          # ... and track id
         self.next_id = 0
-        self.obs: dict[int, list] = {}              # track id -> [(keyframe, u, v)]
-        self.pt_of: dict[int, int] = {}             # track id -> map point
+        # keyframe observations in append (= keyframe-major) order
+        self.obs_kf = np.zeros(0, np.int32)
+        self.obs_tid = np.zeros(0, np.int64)
+        self.obs_uv = np.zeros((0, 2), np.float64)
+        # per track id: map point (-1: none), first keyframe observation, count
+        self.pt_of = np.zeros(0, np.int64)
+        self.first_kf = np.zeros(0, np.int32)
+        self.first_uv = np.zeros((0, 2), np.float64)
+        self.nobs = np.zeros(0, np.int32)
         self.X = np.zeros((0, 3))
         self.kf_frames: list[int] = []
         self.kf_rot: list[np.ndarray] = []
@@ -125,9 +132,10 @@ class IncrementalMapper:
         t1 = time.perf_counter()
         self.times["track"] += t1 - t0
         if k > 0 and self.X.shape[0]:
-            has = np.array([tid in self.pt_of for tid in self.tr_id], bool)
+            pid = self.pt_of[self.tr_id]
+            has = pid >= 0
             if has.sum() >= 5:
-                obj = self.X[[self.pt_of[tid] for tid in self.tr_id[has]]]
+                obj = self.X[pid[has]]
                 found, r, t, inl = solvePnPRansac(obj, self.tr_uv[has].astype(np.float64), self.K,
                                                   device=self.device)
                 if found:
@@ -150,29 +158,32 @@ class IncrementalMapper:
         self.kf_frames.append(k)
         self.kf_rot.append(np.asarray(rot, np.float64))
         self.kf_t.append(np.asarray(t, np.float64))
-        for (u, v), tid in zip(self.tr_uv, self.tr_id):
-            self.obs.setdefault(int(tid), []).append((j, float(u), float(v)))
-        # new map points: tracks seen by two keyframes without one
-        cand = [tid for tid, o in self.obs.items() if len(o) >= 2 and tid not in self.pt_of and o[-1][0] == j]
-        if cand and j >= 1:
+        n_live = len(self.tr_id)
+        if n_live:
+            self.obs_kf = np.concatenate([self.obs_kf, np.full(n_live, j, np.int32)])
+            self.obs_tid = np.concatenate([self.obs_tid, self.tr_id])
+            self.obs_uv = np.vstack([self.obs_uv, self.tr_uv.astype(np.float64)])
+            self.nobs[self.tr_id] += 1
+        # new map points: live tracks seen by two keyframes without one
+        cand = self.tr_id[(self.nobs[self.tr_id] >= 2) & (self.pt_of[self.tr_id] < 0)] if n_live else self.tr_id
+        if len(cand) and j >= 1:
             P = np.stack([self.K @ np.hstack([_rodrigues(r), tt.reshape(3, 1)]) for r, tt in zip(self.kf_rot, self.kf_t)])
-            c0 = [self.obs[tid][0][0] for tid in cand]
-            c1 = [j] * len(cand)
-            uv0 = [self.obs[tid][0][1:] for tid in cand]
-            uv1 = [self.obs[tid][-1][1:] for tid in cand]
+            c0 = self.first_kf[cand]
+            c1 = np.full(len(cand), j, np.int32)
+            uv0 = self.first_uv[cand]
+            uv1 = self.tr_uv[(self.nobs[self.tr_id] >= 2) & (self.pt_of[self.tr_id] < 0)].astype(np.float64)
             Xn = triangulate_points(c0, c1, uv0, uv1, P, device=self.device)
             ok = np.ones(len(cand), bool)
             for cam, uvs in ((c0, uv0), (c1, uv1)):
-                Rm = np.stack([_rodrigues(self.kf_rot[c]) for c in cam])
-                Tm = np.stack([self.kf_t[c] for c in cam])
+                Rm = np.stack([_rodrigues(self.kf_rot[c]) for c in range(len(self.kf_rot))])[cam]
+                Tm = np.stack(self.kf_t)[cam]
                 Xc = np.einsum("nij,nj->ni", Rm, Xn) + Tm
                 proj = Xc[:, :2] / Xc[:, 2:] * F_PIX + self.video.c
-                err = np.linalg.norm(proj - np.asarray(uvs), axis=1)
+                err = np.linalg.norm(proj - uvs, axis=1)
                 ok &= (Xc[:, 2] > 0) & (err <= 7.0) & np.isfinite(err)
-            for tid, x, good in zip(cand, Xn, ok):
-                if good:
-                    self.pt_of[tid] = self.X.shape[0]
-                    self.X = np.vstack([self.X, x[None]])
+            new = cand[ok]
+            self.pt_of[new] = self.X.shape[0] + np.arange(len(new))
+            self.X = np.vstack([self.X, Xn[ok]])
         # replenish: new corners away from the live tracks
         corners = self.tracker.detect_features()
         if len(corners) and len(self.tr_uv) < self.max_tracks:
@@ -182,8 +193,14 @@ class IncrementalMapper:
             corners = corners[: self.max_tracks - len(self.tr_uv)]
             ids = np.arange(self.next_id, self.next_id + len(corners))
             self.next_id += len(corners)
-            for (u, v), tid in zip(corners, ids):
-                self.obs[int(tid)] = [(j, float(u), float(v))]
+            # a new track's first keyframe observation is this keyframe
+            self.pt_of = np.concatenate([self.pt_of, np.full(len(ids), -1, np.int64)])
+            self.first_kf = np.concatenate([self.first_kf, np.full(len(ids), j, np.int32)])
+            self.first_uv = np.vstack([self.first_uv, corners.astype(np.float64)])
+            self.nobs = np.concatenate([self.nobs, np.ones(len(ids), np.int32)])
+            self.obs_kf = np.concatenate([self.obs_kf, np.full(len(ids), j, np.int32)])
+            self.obs_tid = np.concatenate([self.obs_tid, ids])
+            self.obs_uv = np.vstack([self.obs_uv, corners.astype(np.float64)])
             self.tr_uv = np.vstack([self.tr_uv, corners]).astype(np.float32)
             self.tr_id = np.concatenate([self.tr_id, ids])
         if j >= 1 and self.X.shape[0]:
@@ -193,20 +210,13 @@ class IncrementalMapper:
 
     def _bundle_adjust(self) -> None:
         """CSfM::bundleAdjustment over every keyframe (frame-major gather)."""
-        uv, cam, pt = [], [], []
-        for j in range(len(self.kf_frames)):
-            for tid, o in self.obs.items():
-                p = self.pt_of.get(tid)
-                if p is None:
-                    continue
-                for (jj, u, v) in o:
-                    if jj == j:
-                        uv.append((u, v))
-                        cam.append(j)
-                        pt.append(p)
-        uv = np.asarray(uv, np.float64)
-        cam = np.asarray(cam, np.int32)
-        pt = np.asarray(pt, np.int32)
+        # observations are appended keyframe by keyframe: the mask keeps the
+        # frame-major order of CSfM::bundleAdjustment's gather
+        pid = self.pt_of[self.obs_tid]
+        m = pid >= 0
+        uv = np.ascontiguousarray(self.obs_uv[m])
+        cam = np.ascontiguousarray(self.obs_kf[m])
+        pt = np.ascontiguousarray(pid[m].astype(np.int32))
         C = len(self.kf_frames)
         K9 = np.tile(self.K.reshape(1, 9), (C, 1))
         rot = np.stack(self.kf_rot)

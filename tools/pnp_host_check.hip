@@ -21,7 +21,7 @@ int main() {
     in.us[p][1] = double(yn) * k.fv + k.vc;
   }
   double R[9], t[3];
-  sfm::epnp5(in, k, R, t);
+  sfm::epnp5(in, k, nullptr, R, t);
   for (int i = 0; i < 9; ++i) printf("%.17g ", R[i]);
   for (int i = 0; i < 3; ++i) printf("%.17g ", t[i]);
   printf("\n");
