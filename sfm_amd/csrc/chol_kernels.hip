@@ -441,15 +441,21 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 
 // X = T W^T for one 64x64 tile (T and W in LDS, W lower triangular): wave w
 // gets row block w, x[Cb] = block (w, Cb) in the mfma16 D layout.
+// The four column blocks' MFMA chains are interleaved (same k order per
+// block: bitwise the chained sums).
 __device__ __forceinline__ void trsm_lds(const double* T, const double* Wl, f64x4 x[4], int lane) {
-  const int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
 #pragma unroll
-  for (int Cb = 0; Cb < 4; ++Cb) {
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int M = 0; M <= Cb; ++M)
-      acc = mfma16(T + 16 * M * TS + 16 * w, 1, TS, Wl + 16 * M * TS + 16 * Cb, TS, 1, acc, lane);
-    x[Cb] = acc;
-  }
+  for (int Cb = 0; Cb < 4; ++Cb) x[Cb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int k = 16 * M + 4 * s4 + kk;
+      const double a = T[k * TS + 16 * w + li];
+#pragma unroll
+      for (int Cb = M; Cb < 4; ++Cb) x[Cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * TS + 16 * Cb + li], x[Cb], 0, 0, 0);
+    }
 }
 __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) {
   const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
@@ -500,18 +506,34 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     }
     __syncthreads();
     if (j > 0) {
-      // T -= L_j,j-1 L_j,j-1^T on the ten lower 16x16 blocks
-      for (int q = w; q < 10; q += 4) {
-        int J = 0, qq = q;
-        while (qq >= 4 - J) { qq -= 4 - J; ++J; }
-        const int I = J + qq;
-        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      // T -= L_j,j-1 L_j,j-1^T on the ten lower 16x16 blocks: wave w owns
+      // blocks w, w + 4 (and w + 8 for w < 2); their MFMA chains are
+      // interleaved, so no MFMA waits on the accumulator of the one before
+      // (same k order per block as a chain: bitwise the same sums)
+      const int nq = w < 2 ? 3 : 2;  // wave-uniform
+      int Iq[3], Jq[3];
 #pragma unroll
-        for (int M = 0; M < 4; ++M)
-          acc = mfma16(Ls + 16 * M * TS + 16 * I, 1, TS, Ls + 16 * M * TS + 16 * J, TS, 1, acc, lane);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) T[(16 * J + li) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
+      for (int qi = 0; qi < 3; ++qi) {
+        int J = 0, qq = w + 4 * qi;
+        while (qq >= 4 - J && J < 4) { qq -= 4 - J; ++J; }
+        Jq[qi] = J < 4 ? J : 0;
+        Iq[qi] = J < 4 ? J + qq : 0;
       }
+      f64x4 acc[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+      for (int M = 0; M < 4; ++M)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const double* row = Ls + (16 * M + 4 * s4 + kk) * TS + li;
+#pragma unroll
+          for (int qi = 0; qi < 3; ++qi)
+            if (qi < nq) acc[qi] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16 * Iq[qi]], row[16 * Jq[qi]], acc[qi], 0, 0, 0);
+        }
+#pragma unroll
+      for (int qi = 0; qi < 3; ++qi)
+        if (qi < nq)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) T[(16 * Jq[qi] + li) * TS + 16 * Iq[qi] + 4 * rr + kk] -= acc[qi][rr];
       __syncthreads();
     }
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n) : potrf_tile<false>(T, Wl, scr, j0, n);
