@@ -624,41 +624,49 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
 }
 
 // Back substitution L^T y = z (z = row n of the augmented factor, i.e.
-// L^-1 rhs), ONE launch: workgroup b owns block row b (64 unknowns) and
-//   y_b = W_b^T (z_b - sum_{k>b} L_kb^T y_k).
-// y_k are published block by block (descending) through device-scope flags
-// (producer: stores, fence, release store of the flag; consumer: acquire
-// poll by one lane, barrier, plain loads).  Every L_kb tile is prefetched
-// before its y_k is awaited, so the chain costs one flag hand-off per block
-// instead of one kernel launch per block.  All nb workgroups are co-resident
-// (nb <= a few hundred, one CU each); every wait is bounded and a timeout
-// sets bit 1 of *fail (reported as an error, never a hang).
+// L^-1 rhs), ONE launch: workgroup b owns block row b (64 unknowns),
+//   y_b = W_b^T (z_b - sum_{k>b} L_kb^T y_k),
+// and every L_kb tile is prefetched before y_k is awaited.  The entries of
+// y are their own flags: y is filled with a signalling-NaN sentinel before
+// the launch (arithmetic never yields one), the producer stores each entry
+// once, write-through, and a consumer's wave 0 polls the 64 entries of y_k
+// (agent-scope loads) until none is the sentinel, then passes them through
+// LDS.  Against a flag after the data this drops the producer's drain and
+// the consumer's invalidate + reload: one memory round trip per hand-off
+// instead of three (127 -> 98 us at n = 3000 for LDS staging alone, see
+// DESIGN.md).  Chunked consumption or several blocks per workgroup measured
+// slower: whatever runs after the awaited block arrives is on the chain.
+// All workgroups are co-resident (nb <= a few hundred, one CU each); every
+// wait is bounded and a timeout sets bit 1 of *fail (an error, never a hang).
+constexpr uint32_t kYSentinelWord = 0x7FF4DEADu;  // both halves: a signalling NaN
+constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWord;
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
-                                                   int* __restrict__ flags, int epoch, int* __restrict__ fail) {
+                                                   int* __restrict__ fail) {
   __shared__ double v[NB];
+  __shared__ double yl[2][NB];
   __shared__ int timed_out;
-  const int b = nb - 1 - blockIdx.x;  // the chain's first block is the first workgroup
+  const int b = nb - 1 - int(blockIdx.x);  // the chain's first block is the first workgroup
   const int k0 = b * NB;
   const int nreal = (n - k0) < NB ? (n - k0) : NB;
   const int t = threadIdx.x, col = t >> 2, seg = t & 3;
   if (t == 0) timed_out = 0;
-  // off the chain: this block's z entry and W_b row (thread t < 64 -> y_b[t])
+  // off the chain: z entry and the W_b column segment W(16 seg + i, col)
   const double zc = (seg == 0 && col < nreal) ? A[size_t(k0 + col) * ld + n] : 0.0;
-  double wr[NB];
-  if (t < NB) {
-    const double* Wr = Winv + size_t(b) * NB * NB + size_t(t) * NB;  // W(c, t), c = 0..63
+  double wr[16];
+  {
+    const double* Wr = Winv + size_t(b) * NB * NB + size_t(col) * NB + 16 * seg;
 #pragma unroll
-    for (int c = 0; c < NB; c += 2) {
-      const double2 q = *reinterpret_cast<const double2*>(Wr + c);
-      wr[c] = q.x;
-      wr[c + 1] = q.y;
+    for (int i = 0; i < 16; i += 2) {
+      const double2 q = *reinterpret_cast<const double2*>(Wr + i);
+      wr[i] = q.x;
+      wr[i + 1] = q.y;
     }
   }
   __syncthreads();
   double acc = 0.0;
-  // column k0 + col, rows 64k + 16 seg .. +16 of tile (k, b)
+  // column k0 + col, rows 64 k + 16 seg .. +16 of tile (k, b)
   const double* colp = A + size_t(k0 + col) * ld + 16 * seg;
   for (int k = nb - 1; k > b; --k) {
     double lv[16];
@@ -668,39 +676,45 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
       lv[i] = q.x;
       lv[i + 1] = q.y;
     }
+    double* yb = yl[k & 1];  // double-buffered: one barrier per block
     if (wave0()) {  // scalar branch (see block_wait)
-      if (!spin_until(flags + k, epoch)) timed_out = 1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
+      const int lane = threadIdx.x & 63;
+      const double* p = y + size_t(k) * NB + lane;
+      double yv = 0.0;
+      for (long spins = 0;; ++spins) {
+        yv = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_ballot_w64(__builtin_bit_cast(uint64_t, yv) == kYSentinel) == 0) break;
+        if (spins > kFlagSpins) {
+          timed_out = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      yb[lane] = yv;
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(timed_out)) break;
-    const double* yk = y + size_t(k) * NB + 16 * seg;
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const double2 q = *reinterpret_cast<const double2*>(yk + i);
-      acc = fma(lv[i], q.x, acc);
-      acc = fma(lv[i + 1], q.y, acc);
-    }
+    for (int i = 0; i < 16; ++i) acc = fma(lv[i], yb[16 * seg + i], acc);
   }
   // the four row segments of a column sit in adjacent lanes
   acc += __shfl_xor(acc, 1);
   acc += __shfl_xor(acc, 2);
   if (seg == 0) v[col] = (col < nreal) ? zc - acc : 0.0;
   __syncthreads();
-  if (t < NB) {
-    // y_b[t] = sum_c W(c, t) v[c]: four interleaved chains (the step is on
-    // the hand-off chain; one 64-deep FMA chain cost ~0.25 us)
-    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+  // y_b[col] = sum_c W(c, col) v[c]: 16 terms per lane in four chains, then
+  // the four segments
+  double p4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int c = 0; c < NB; ++c) s4[c & 3] = fma(wr[c], v[c], s4[c & 3]);
-    const double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-    // write-through (sc1): the flag then needs no L2 write-back (the
-    // walker's producer form, block_publish_wt)
-    st_wt(y + size_t(k0) + t, (t < nreal) ? s : 0.0);
-  }
+  for (int i = 0; i < 16; ++i) p4[i & 3] = fma(wr[i], v[16 * seg + i], p4[i & 3]);
+  double sum = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+  sum += __shfl_xor(sum, 1);
+  sum += __shfl_xor(sum, 2);
+  // write-through (sc1) relaxed store of the final value: the consumers'
+  // polls see it when it lands, with nothing to order after it
+  if (seg == 0) __hip_atomic_store(y + size_t(k0) + col, col < nreal ? sum : 0.0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
   if (wave0() && timed_out) atomicOr(fail, 2);
-  block_publish_wt(flags + b, epoch);
 }
 
 }  // namespace
@@ -714,9 +728,12 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
                                          epoch, nhelp, d.fail);
 }
 
-void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s) {
+void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s) {
   const int nb_real = (d.n + NB - 1) / NB;
-  if (nb_real > 0) k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.flags, epoch, d.fail);
+  if (nb_real <= 0) return;
+  // the sentinel in every entry of y the launch produces (ld >= 64 nb_real)
+  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
+  k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail);
 }
 
 }  // namespace sfm
