@@ -427,8 +427,9 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t
 
 // Per-iteration point factorisation (depends on the trust-region radius),
 // one lane per point: V_p + D_p^2 = L L^T, z = L^-1 b_p -> ptL.
-// With ptS != nullptr it also writes the point's 128-B Schur record
-// (X 3 | Jacobi scale 3 | L 6 | 1/l_ii 3 | pad) for k_schur_pts.
+// With ptS != nullptr it also writes the point's 128-B record for the
+// camera-side passes (X 3 | Jacobi scale 3 | l10 l20 l21 | 1/l_ii 3 | z 3 |
+// pad): everything obs_recompute and k_schur_pts read of a point, one line.
 __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* __restrict__ ptV,
                                                            const double* __restrict__ diag_p, double radius,
                                                            double* __restrict__ ptL, double* __restrict__ part_bad,
@@ -457,8 +458,8 @@ __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* 
       const double* x = X + 3 * size_t(p);
       const double* sp = scale_p + 3 * size_t(p);
       st2(o, x[0], x[1]); st2(o + 2, x[2], sp[0]); st2(o + 4, sp[1], sp[2]);
-      st2(o + 6, l00, l10); st2(o + 8, l11, l20); st2(o + 10, l21, l22);
-      st2(o + 12, 1.0 / l00, 1.0 / l11); st2(o + 14, 1.0 / l22, 0.0);
+      st2(o + 6, l10, l20); st2(o + 8, l21, 1.0 / l00); st2(o + 10, 1.0 / l11, 1.0 / l22);
+      st2(o + 12, z0, z1); st2(o + 14, z2, 0.0);
     }
   }
   const double r = block_reduce(bad, sh, true);
@@ -481,14 +482,15 @@ struct ObsRC {
 __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const double* __restrict__ camR,
                                               const double* __restrict__ cam, const double* __restrict__ Kc,
                                               const double* __restrict__ scale_c, const double* __restrict__ ptS,
-                                              const double* __restrict__ ptL, ObsRC& o) {
+                                              ObsRC& o) {
   // camera (wave-uniform: scalar loads)
   const double* cr = camR + size_t(kCamR) * c;
   const double* k = Kc + 5 * size_t(c);
   const double* tc = cam + 6 * size_t(c) + 3;
   const double* sc = scale_c + 6 * size_t(c);
   const double fx = k[0], sk = k[1], cx = k[2], fy = k[3], cy = k[4];
-  // point: one 128-B Schur record (X, scale, L, 1/l_ii) and z from ptL
+  // point: one 128-B Schur record (X, scale, L's off-diagonal, 1/l_ii, z):
+  // one line per observation
   const double* rp = ptS + size_t(kPtS) * p;
   double q[16];
 #pragma unroll
@@ -496,8 +498,6 @@ __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const d
     const double2 x = ld2(rp + f);
     q[f] = x.x; q[f + 1] = x.y;
   }
-  const double2 z01 = ld2(ptL + size_t(kPtL) * p + 6);
-  const double z2 = ptL[size_t(kPtL) * p + 8];
   const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
   // jac_record's formulas with one reciprocal (1/z) for the projection
   const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
@@ -525,12 +525,12 @@ __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const d
   }
   rec[kJC + 3] = a0 * sc[3]; rec[kJC + 4] = a1 * sc[4]; rec[kJC + 5] = a2 * sc[5];
   rec[kJC + 9] = 0.0;        rec[kJC + 10] = b1 * sc[4]; rec[kJC + 11] = b2 * sc[5];
-  const double l10 = q[7], l20 = q[9], l21 = q[10], i00 = q[12], i11 = q[13], i22 = q[14];
+  const double l10 = q[6], l20 = q[7], l21 = q[8], i00 = q[9], i11 = q[10], i22 = q[11];
   const double* e = rec + kJX;
   o.M[0] = e[0] * i00; o.M[1] = (e[1] - l10 * o.M[0]) * i11; o.M[2] = (e[2] - l20 * o.M[0] - l21 * o.M[1]) * i22;
   o.M[3] = e[3] * i00; o.M[4] = (e[4] - l10 * o.M[3]) * i11; o.M[5] = (e[5] - l20 * o.M[3] - l21 * o.M[4]) * i22;
-  o.h0 = o.M[0] * z01.x + o.M[1] * z01.y + o.M[2] * z2;
-  o.h1 = o.M[3] * z01.x + o.M[4] * z01.y + o.M[5] * z2;
+  o.h0 = o.M[0] * q[12] + o.M[1] * q[13] + o.M[2] * q[14];
+  o.h1 = o.M[3] * q[12] + o.M[4] * q[13] + o.M[5] * q[14];
 }
 
 // Per observation (camera-major, one wavefront = 64 positions of ONE camera):
@@ -547,14 +547,14 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
                                                           const double* __restrict__ Kc,
                                                           const double* __restrict__ scale_c,
                                                           const double* __restrict__ ptS,
-                                                          const double* __restrict__ ptL, double* __restrict__ dpart) {
+                                                          double* __restrict__ dpart) {
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
   if (i0 >= N_pad) return;  // wave-uniform, no barriers below
   const int64_t i = i0 + l;
   const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
   ObsRC o;
-  obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, ptL, o);
+  obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, o);
   const double* jc = o.rec + kJC;
   double F[18];  // 6 x 3
 #pragma unroll
@@ -591,7 +591,6 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
                                                            const double* __restrict__ Kc,
                                                            const double* __restrict__ scale_c,
                                                            const double* __restrict__ ptS,
-                                                           const double* __restrict__ ptL,
                                                            const double* __restrict__ ysol, double* __restrict__ eu,
                                                            double* __restrict__ part_model) {
   __shared__ double sh[4];
@@ -602,7 +601,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
     const int64_t i = i0 + l;
     const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
     ObsRC o;
-    obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, ptL, o);
+    obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, o);
     const double* y = ysol + 6 * size_t(c);
     const double* J = o.rec + kJC;
     double e0 = 0.0, e1 = 0.0;
@@ -631,7 +630,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
 // lanes own one block: the two cameras' constants (R, dR/dw, t, K, Jacobi
 // scale: 50 doubles each) sit in LDS as wave-uniform broadcasts, and each
 // lane takes one pair per step, gathering only its point's 128-B record
-// (X, scale, L_p, 1/l_ii: one line, 25.6 MB in all at C3, so L2/MALL
+// (X, scale, L_p, 1/l_ii, z: one line, 25.6 MB in all at C3, so L2/MALL
 // resident) and recomputing both scaled Jacobians with the Jacobian pass's
 // own arithmetic (jac_record).  A gathered-F formulation fetched a fresh
 // 144-B F record per pair from a 293-MB array (~2.9 GB of HBM traffic per
@@ -650,7 +649,7 @@ __device__ __forceinline__ void stage_cam(double* cs, int c, const double* __res
 }
 
 // One side of a pair: scaled J_c (2x6) and M = J_X L^-T (2x3, rows m | n).
-__device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], const double sp[3], const double Lp[9],
+__device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], const double sp[3], const double Lp[6],
                                           double M[6], double jc[12]) {
   // jac_record's Jacobian columns, with one reciprocal for the projection
   // (1/z) instead of three divisions
@@ -680,7 +679,7 @@ __device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], 
   }
   jc[3] = a0 * sc[3]; jc[4] = a1 * sc[4]; jc[5] = a2 * sc[5];
   jc[9] = 0.0;        jc[10] = b1 * sc[4]; jc[11] = b2 * sc[5];
-  const double l10 = Lp[1], l20 = Lp[3], l21 = Lp[4], i00 = Lp[6], i11 = Lp[7], i22 = Lp[8];
+  const double l10 = Lp[0], l20 = Lp[1], l21 = Lp[2], i00 = Lp[3], i11 = Lp[4], i22 = Lp[5];
   M[0] = e[0] * i00; M[1] = (e[1] - l10 * M[0]) * i11; M[2] = (e[2] - l20 * M[0] - l21 * M[1]) * i22;
   M[3] = e[3] * i00; M[4] = (e[4] - l10 * M[3]) * i11; M[5] = (e[5] - l20 * M[3] - l21 * M[4]) * i22;
 }
@@ -759,14 +758,14 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
     const bool valid = k < ke;
     const int p = valid ? bpts[k] : 0;
     const double* r = ptS + size_t(kPtS) * p;
-    double q[16];
+    double q[12];  // X, scale, l10 l20 l21, 1/l_ii (z, the last 32 B, unused here)
 #pragma unroll
-    for (int f = 0; f < 16; f += 2) {
+    for (int f = 0; f < 12; f += 2) {
       const double2 x = ld2(r + f);
       q[f] = x.x; q[f + 1] = x.y;
     }
     const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
-    const double Lp[9] = {q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14]};
+    const double Lp[6] = {q[6], q[7], q[8], q[9], q[10], q[11]};
     double M1[6], J1[12], M2[6], J2[12];
     pair_side(cs1, Xp, sp, Lp, M1, J1);
     pair_side(cs2, Xp, sp, Lp, M2, J2);
@@ -1151,7 +1150,7 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   launch_point_factor(d, radius, s);
   if (d.N_pad)
     k_obs_prep_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
-                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.ptL, d.dpart);
+                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.dpart);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
@@ -1190,8 +1189,8 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
   if (d.N_pad && cams_var)
     k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
-                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ptL,
-                                                                     d.ysol, d.eu, slot(d, kPModel));
+                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ysol, d.eu,
+                                                                     slot(d, kPModel));
   else if (d.N_pad) {
     (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.N), s);
     (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
