@@ -648,40 +648,45 @@ __device__ __forceinline__ void stage_cam(double* cs, int c, const double* __res
   else if (l < 50) cs[l] = scale_c[6 * size_t(c) + (l - 44)];
 }
 
-// One side of a pair: scaled J_c (2x6) and M = J_X L^-T (2x3, rows m | n).
-__device__ __forceinline__ void pair_side(const double* cs, const double Xp[3], const double sp[3], const double Lp[6],
-                                          double M[6], double jc[12]) {
-  // jac_record's Jacobian columns, with one reciprocal for the projection
-  // (1/z) instead of three divisions
+// One side of a pair: M = J_X L^-T (2x3, rows m | n) and the projection
+// coefficients (a0 a1 a2 | b1 b2) its scaled J_c columns are made of
+// (jac_record's Jacobian, with one reciprocal 1/z instead of three divisions).
+__device__ __forceinline__ void pair_side_m(const double* cs, const double Xp[3], const double sp[3],
+                                            const double Lp[6], double M[6], double ab[5]) {
   const double* cr = cs;
   const double fx = cs[39], sk = cs[40], fy = cs[42];
-  const double* sc = cs + 44;
   const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + cs[36];
   const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + cs[37];
   const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + cs[38];
   const double iz = 1.0 / pc2, xp = pc0 * iz, yp = pc1 * iz;
   const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
   const double b1 = fy * iz, b2 = -fy * yp * iz;
+  ab[0] = a0; ab[1] = a1; ab[2] = a2; ab[3] = b1; ab[4] = b2;
   double e[6];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     e[j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
     e[3 + j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
   }
-#pragma unroll
-  for (int kk = 0; kk < 3; ++kk) {
-    const double* D = cr + 9 + 9 * kk;
-    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
-    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
-    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
-    jc[kk] = (a0 * q0 + a1 * q1 + a2 * q2) * sc[kk];
-    jc[6 + kk] = (b1 * q1 + b2 * q2) * sc[kk];
-  }
-  jc[3] = a0 * sc[3]; jc[4] = a1 * sc[4]; jc[5] = a2 * sc[5];
-  jc[9] = 0.0;        jc[10] = b1 * sc[4]; jc[11] = b2 * sc[5];
   const double l10 = Lp[0], l20 = Lp[1], l21 = Lp[2], i00 = Lp[3], i11 = Lp[4], i22 = Lp[5];
   M[0] = e[0] * i00; M[1] = (e[1] - l10 * M[0]) * i11; M[2] = (e[2] - l20 * M[0] - l21 * M[1]) * i22;
   M[3] = e[3] * i00; M[4] = (e[4] - l10 * M[3]) * i11; M[5] = (e[5] - l20 * M[3] - l21 * M[4]) * i22;
+}
+// Column kk of the scaled J_c (rows m | n): ju = J_c[kk], jv = J_c[6 + kk].
+__device__ __forceinline__ void pair_jc(const double* cs, const double Xp[3], const double ab[5], int kk,
+                                        double& ju, double& jv) {
+  const double* sc = cs + 44;
+  if (kk < 3) {
+    const double* D = cs + 9 + 9 * kk;
+    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+    ju = (ab[0] * q0 + ab[1] * q1 + ab[2] * q2) * sc[kk];
+    jv = (ab[3] * q1 + ab[4] * q2) * sc[kk];
+  } else {
+    ju = ab[kk - 3] * sc[kk];
+    jv = kk == 3 ? 0.0 : ab[kk - 1] * sc[kk];
+  }
 }
 
 // Sums of 32 values over the kSub lanes of a segment by recursive halving
@@ -712,7 +717,7 @@ __device__ __forceinline__ double seg_sum(double v) {
 }
 
 template <int kSub>
-__global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int2* __restrict__ blk,
+__global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_blk, const int2* __restrict__ blk,
                                                         const int32_t* __restrict__ seg,
                                                         const int32_t* __restrict__ bpts,
                                                         const double* __restrict__ ptS,
@@ -756,7 +761,10 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
     asm volatile("" ::: "memory");
     const int k = kb + k0 + sl;
     const bool valid = k < ke;
-    const int p = valid ? bpts[k] : 0;
+    // unconditional load of a clamped index (a past-the-end step reads a
+    // real point, masked by w = 0): a predicated load becomes a branch whose
+    // join drains vmcnt
+    const int p = bpts[valid ? k : 0];
     const double* r = ptS + size_t(kPtS) * p;
     double q[12];  // X, scale, l10 l20 l21, 1/l_ii (z, the last 32 B, unused here)
 #pragma unroll
@@ -766,9 +774,17 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
     }
     const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
     const double Lp[6] = {q[6], q[7], q[8], q[9], q[10], q[11]};
-    double M1[6], J1[12], M2[6], J2[12];
-    pair_side(cs1, Xp, sp, Lp, M1, J1);
-    pair_side(cs2, Xp, sp, Lp, M2, J2);
+    // side 2 in full (J_c2 feeds every accumulator row); side 1 keeps M_1 and
+    // its five coefficients, its J_c columns made row by row below (12 fewer
+    // live doubles: 3 waves per SIMD instead of 2)
+    double M1[6], ab1[5], M2[6], ab2[5], J2[12];
+    pair_side_m(cs1, Xp, sp, Lp, M1, ab1);
+    pair_side_m(cs2, Xp, sp, Lp, M2, ab2);
+    // (a scheduling fence: without it the LDS reads of both J_c hoist above
+    // and 168 VGPRs spill)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) pair_jc(cs2, Xp, ab2, kk, J2[kk], J2[6 + kk]);
     const double w = valid ? 1.0 : 0.0;
     const double g00 = (M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2]) * w;
     const double g01 = (M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5]) * w;
@@ -776,7 +792,9 @@ __global__ __launch_bounds__(kThreads) void k_schur_pts(int64_t n_blk, const int
     const double g11 = (M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5]) * w;
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
-      const double h0 = J1[u] * g00 + J1[6 + u] * g10, h1 = J1[u] * g01 + J1[6 + u] * g11;
+      double j1u, j1v;
+      pair_jc(cs1, Xp, ab1, u, j1u, j1v);
+      const double h0 = j1u * g00 + j1v * g10, h1 = j1u * g01 + j1v * g11;
 #pragma unroll
       for (int v = 0; v < 6; ++v) acc[6 * u + v] += h0 * J2[v] + h1 * J2[6 + v];
     }
