@@ -249,6 +249,45 @@ int sfm_matcher_last_time(sfm_matcher* h, double* ms2);
 int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const int32_t* row_off, int32_t n_pts,
                                    int32_t desc_bytes, int32_t* best, uint8_t* out);
 
+/* CMap's observation store, resident on the device (SURVEY.md §8f row 2;
+ * map_store.hip): points, (frame, keypoint) observations in the multimap's
+ * emplace order, descriptor rows per point.  Replaces the multimap gathers
+ * of CMap.cpp:145-295 on the tracking path (CSfM.cpp:648-669).  Point
+ * indices are the CMap's _lastPtNo numbering (0, 1, ... in creation order).
+ * desc_bytes: 8 x a power of two (BRISK 64). */
+typedef struct sfm_map sfm_map;
+int sfm_map_create(int32_t device, int32_t desc_bytes, sfm_map** out);
+int sfm_map_destroy(sfm_map* h);
+int sfm_map_size(sfm_map* h, int32_t* n_pts, int64_t* n_obs, int64_t* n_desc_rows);
+/* CMap::addNewPoints (CMap.cpp:36-78): pts3d [n_pts][3], frame_no
+ * [n_frames], pts2d_idx [n_frames][n_pts] (the reference's
+ * vector<vector<int>>, frame-major); new indices out (may be NULL). */
+int sfm_map_add_new_points(sfm_map* h, int32_t n_pts, const double* pts3d, int32_t n_frames, const int32_t* frame_no,
+                           const int32_t* pts2d_idx, int32_t* pts3d_idx);
+/* CMap::addPointMatches (CMap.cpp:118-132). */
+int sfm_map_add_point_matches(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const int32_t* pts2d_idx,
+                              int32_t frame_no);
+/* CMap::addDescriptors (CMap.cpp:308-315): one row [desc_bytes] per point. */
+int sfm_map_add_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const uint8_t* desc);
+/* CMap::getPointsAtIdx (CMap.cpp:134-143) and its inverse (BA write-back). */
+int sfm_map_get_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, double* pts3d);
+int sfm_map_set_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const double* pts3d);
+/* CMap::getPointsInFrames(pts3DIdx, frameNo) (CMap.cpp:277-295): sorted
+ * unique points observed in any of the frames.  *n_out = the count; an error
+ * when it exceeds capacity. */
+int sfm_map_points_in_frames(sfm_map* h, int32_t n_frames, const int32_t* frame_no, int32_t capacity,
+                             int32_t* pts3d_idx, int32_t* n_out);
+/* CMap::getPointsInFrame(pts3DIdx, pts2DIdx, frameNo) (CMap.cpp:225-240):
+ * the frame's equal_range in multimap order; per entry, every 2D index the
+ * point has in the frame (so n2 > n3 when a point was matched twice). */
+int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int32_t* pts3d_idx, int32_t* n3_out,
+                            int32_t* pts2d_idx, int32_t* n2_out);
+/* CMap::getRepresentativeDescriptors (CMap.cpp:345-381) from the resident
+ * rows: desc_out [n][desc_bytes]; best_row (optional) = the row within the
+ * point's rows (append order), first on ties.  Every point needs a row. */
+int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,
+                                       int32_t* best_row);
+
 /* Per-frame pose: cv::solvePnPRansac(objectPoints, imagePoints, K, dist = 0,
  * rvec, tvec, false, iterations, reproj_err, confidence, inliers,
  * SOLVEPNP_ITERATIVE) as CSfM::tracking calls it (CSfM.cpp:553-565:

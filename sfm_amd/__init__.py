@@ -11,9 +11,9 @@ from .ba import BundleAdjuster, make_options, solve, STRUCT_ONLY, POSE_ONLY, STR
 from .ctracker import CTracker
 from . import scene, video
 from .klt import KLTTracker, calc_optical_flow_pyr_lk
-from .cmap import CMap, representative_descriptors
+from .cmap import CMap, DeviceMap, representative_descriptors
 from .pnp import solvePnPRansac
 
-__all__ = ["BundleAdjuster", "CTracker", "CMap", "solvePnPRansac", "representative_descriptors", "KLTTracker", "calc_optical_flow_pyr_lk", "video", "BAOptions", "BASummary", "BAIteration", "SfmError", "make_options",
+__all__ = ["BundleAdjuster", "CTracker", "CMap", "DeviceMap", "solvePnPRansac", "representative_descriptors", "KLTTracker", "calc_optical_flow_pyr_lk", "video", "BAOptions", "BASummary", "BAIteration", "SfmError", "make_options",
            "solve", "default_options", "device_count", "exported_symbols", "lib", "scene", "LIB_PATH",
            "STRUCT_ONLY", "POSE_ONLY", "STRUCT_AND_POSE"]

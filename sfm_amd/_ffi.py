@@ -150,6 +150,18 @@ _SIGNATURES = {
                                  c_void_p]),
     "sfm_matcher_last_time": (c_int, [c_void_p, c_void_p]),
     "sfm_representative_descriptors": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "sfm_map_create": (c_int, [c_int32, c_int32, POINTER(c_void_p)]),
+    "sfm_map_destroy": (c_int, [c_void_p]),
+    "sfm_map_size": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int64), POINTER(c_int64)]),
+    "sfm_map_add_new_points": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "sfm_map_add_point_matches": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int32]),
+    "sfm_map_add_descriptors": (c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "sfm_map_get_points": (c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "sfm_map_set_points": (c_int, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "sfm_map_points_in_frames": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, POINTER(c_int32)]),
+    "sfm_map_points_in_frame": (c_int, [c_void_p, c_int32, c_int32, c_void_p, POINTER(c_int32), c_void_p,
+                                        POINTER(c_int32)]),
+    "sfm_map_representative_descriptors": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "sfm_pnp_ransac": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_double, c_double,
                                c_void_p, c_void_p, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "sfm_triangulate_points": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

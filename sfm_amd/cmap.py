@@ -59,3 +59,95 @@ class CMap:
         row_off[1:] = np.cumsum([m.shape[0] for m in mats])
         _, out = representative_descriptors(np.vstack(mats), row_off, self.device)
         return out
+
+
+class DeviceMap:
+    """CMap's observation store resident on the device (sfm_map_*, SURVEY.md
+    §8f row 2): the multimap gathers of the tracking path (CMap.cpp:145-295,
+    CSfM.cpp:648-669) as device queries, with CMap's method names."""
+
+    def __init__(self, desc_bytes: int = 64, device: int = 0):
+        self.desc_bytes = int(desc_bytes)
+        h = ctypes.c_void_p()
+        check(lib().sfm_map_create(device, self.desc_bytes, ctypes.byref(h)), "sfm_map_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().sfm_map_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self):
+        n_pts, n_obs, n_rows = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().sfm_map_size(self._h, ctypes.byref(n_pts), ctypes.byref(n_obs), ctypes.byref(n_rows)),
+              "sfm_map_size")
+        return n_pts.value, n_obs.value, n_rows.value
+
+    def addNewPoints(self, pts3D, pts2DIdx, frameNo) -> np.ndarray:
+        """pts2DIdx [n_frames][n_pts] (the reference's vector<vector<int>>)."""
+        X = np.ascontiguousarray(np.asarray(pts3D, np.float64).reshape(-1, 3))
+        n = int(X.shape[0])
+        fr = np.ascontiguousarray(np.asarray(frameNo, np.int32).reshape(-1))
+        i2 = np.ascontiguousarray(np.asarray(pts2DIdx, np.int32).reshape(len(fr), n))
+        out = np.zeros(max(1, n), np.int32)
+        check(lib().sfm_map_add_new_points(self._h, n, ptr(X), len(fr), ptr(fr), ptr(i2), ptr(out)),
+              "sfm_map_add_new_points")
+        return out[:n].copy()
+
+    def addPointMatches(self, pts3DIdx, pts2DIdx, frameNo: int) -> None:
+        a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
+        b = np.ascontiguousarray(np.asarray(pts2DIdx, np.int32).reshape(-1))
+        check(lib().sfm_map_add_point_matches(self._h, len(a), ptr(a), ptr(b), int(frameNo)),
+              "sfm_map_add_point_matches")
+
+    def addDescriptors(self, pts3DIdx, descriptors) -> None:
+        a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
+        d = np.ascontiguousarray(np.asarray(descriptors, np.uint8).reshape(len(a), self.desc_bytes))
+        check(lib().sfm_map_add_descriptors(self._h, len(a), ptr(a), ptr(d)), "sfm_map_add_descriptors")
+
+    def getPointsAtIdx(self, pts3DIdx) -> np.ndarray:
+        a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
+        X = np.zeros((max(1, len(a)), 3))
+        check(lib().sfm_map_get_points(self._h, len(a), ptr(a), ptr(X)), "sfm_map_get_points")
+        return X[:len(a)].copy()
+
+    def setPointsAtIdx(self, pts3DIdx, pts3D) -> None:
+        a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
+        X = np.ascontiguousarray(np.asarray(pts3D, np.float64).reshape(len(a), 3))
+        check(lib().sfm_map_set_points(self._h, len(a), ptr(a), ptr(X)), "sfm_map_set_points")
+
+    def getPointsInFrames(self, frameNo) -> np.ndarray:
+        fr = np.ascontiguousarray(np.asarray(frameNo, np.int32).reshape(-1))
+        cap = max(1, self.size()[0])
+        out = np.zeros(cap, np.int32)
+        n = ctypes.c_int32()
+        check(lib().sfm_map_points_in_frames(self._h, len(fr), ptr(fr), cap, ptr(out), ctypes.byref(n)),
+              "sfm_map_points_in_frames")
+        return out[:n.value].copy()
+
+    def getPointsInFrame(self, frameNo: int):
+        """(pts3DIdx, pts2DIdx) of CMap::getPointsInFrame(pts3DIdx, pts2DIdx, frameNo)."""
+        cap = max(1, self.size()[1])
+        p3 = np.zeros(cap, np.int32)
+        p2 = np.zeros(cap, np.int32)
+        n3, n2 = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().sfm_map_points_in_frame(self._h, int(frameNo), cap, ptr(p3), ctypes.byref(n3), ptr(p2),
+                                            ctypes.byref(n2)), "sfm_map_points_in_frame")
+        return p3[:n3.value].copy(), p2[:n2.value].copy()
+
+    def getRepresentativeDescriptors(self, pts3DIdx, return_best: bool = False):
+        a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
+        out = np.zeros((max(1, len(a)), self.desc_bytes), np.uint8)
+        best = np.zeros(max(1, len(a)), np.int32)
+        if len(a):
+            check(lib().sfm_map_representative_descriptors(self._h, len(a), ptr(a), ptr(out), ptr(best)),
+                  "sfm_map_representative_descriptors")
+        if return_best:
+            return out[:len(a)].copy(), best[:len(a)].copy()
+        return out[:len(a)].copy()

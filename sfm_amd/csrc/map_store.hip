@@ -1,0 +1,518 @@
+// CMap's observation store on the device: the map
+// points, their (frame, keypoint) observations and their descriptor rows,
+// resident in HBM, with the queries the live tracking path makes of CMap:
+//
+//   addNewPoints       CMap.cpp:36-78   points + one observation per frame,
+//                                       emplaced point-major (i, then j)
+//   addPointMatches    CMap.cpp:118-132 one observation per point
+//   addDescriptors     CMap.cpp:308-315 one descriptor row per point
+//   getPointsAtIdx     CMap.cpp:134-143 (and the BA write-back)
+//   getPointsInFrames  CMap.cpp:277-295 sorted unique points seen in any of
+//                                       the frames (CSfM.cpp:648)
+//   getPointsInFrame   CMap.cpp:145-240 multimap equal_range order; for
+//                                       every entry, EVERY 2D index the point
+//                                       has in that frame (a point matched
+//                                       twice in a frame yields 2 x 2)
+//   getRepresentativeDescriptors  CMap.cpp:345-381 (CSfM.cpp:669)
+//
+// Layout: observations are kept in global emplace order, which is the
+// multimap's order within one key (std::multimap inserts at the upper bound
+// of the equal range) and the order of each point's _frameNo/_pts2DIdx
+// lists.  Descriptor rows are kept in append order with their point.  The
+// per-point CSRs (observations, descriptor rows) are rebuilt lazily by a
+// stable radix sort after appends.  Queries are flag + stable compaction
+// (hipcub DeviceSelect), so every result keeps the reference's order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+#include "../../include/sfm_amd.h"
+
+void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
+
+namespace sfm {
+namespace {
+
+int mapfail(int code, const std::string& m) {
+  sfm_internal_set_error("sfm_map: " + m);
+  return code;
+}
+
+__global__ void k_mark_frames(int64_t n, const int32_t* __restrict__ ob_pt, const int32_t* __restrict__ ob_frame,
+                              const int32_t* __restrict__ fset, int nf, uint8_t* __restrict__ mark) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int f = ob_frame[e];
+  int lo = 0, hi = nf;  // fset ascending
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (fset[mid] < f) lo = mid + 1; else hi = mid;
+  }
+  if (lo < nf && fset[lo] == f) mark[ob_pt[e]] = 1;  // idempotent plain store
+}
+
+__global__ void k_flag_frame(int64_t n, const int32_t* __restrict__ ob_frame, int f, uint8_t* __restrict__ flag) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < n) flag[e] = ob_frame[e] == f;
+}
+
+__global__ void k_count_keys(int64_t n, const int32_t* __restrict__ key, int32_t* __restrict__ cnt) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < n) atomicAdd(cnt + key[e], 1);
+}
+
+__global__ void k_iota(int64_t n, int32_t* __restrict__ v) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < n) v[e] = int32_t(e);
+}
+
+// entry e of the frame's equal range (observation sel[e] of point p): how
+// many of p's observations are in frame f
+__global__ void k_dup_count(int n_sel, const int32_t* __restrict__ sel, const int32_t* __restrict__ ob_pt,
+                            const int32_t* __restrict__ ob_frame, const int32_t* __restrict__ orow,
+                            const int32_t* __restrict__ ooff, int f, int32_t* __restrict__ cnt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_sel) return;
+  const int p = ob_pt[sel[e]];
+  int c = 0;
+  for (int q = ooff[p]; q < ooff[p + 1]; ++q) c += ob_frame[orow[q]] == f;
+  cnt[e] = c;
+}
+
+__global__ void k_dup_fill(int n_sel, const int32_t* __restrict__ sel, const int32_t* __restrict__ ob_pt,
+                           const int32_t* __restrict__ ob_frame, const int32_t* __restrict__ ob_idx,
+                           const int32_t* __restrict__ orow, const int32_t* __restrict__ ooff, int f,
+                           const int32_t* __restrict__ off2, int32_t* __restrict__ out3, int32_t* __restrict__ out2) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_sel) return;
+  const int p = ob_pt[sel[e]];
+  out3[e] = p;
+  int w = off2[e];
+  for (int q = ooff[p]; q < ooff[p + 1]; ++q) {
+    const int o = orow[q];
+    if (ob_frame[o] == f) out2[w++] = ob_idx[o];
+  }
+}
+
+// one wave per queried point: the point's row (in append order) with the
+// smallest sum of Hamming distances to its other rows, the first on ties
+// (CMap.cpp:345-381)
+template <int W>
+__global__ __launch_bounds__(64) void k_map_repr(const uint64_t* __restrict__ desc, const int32_t* __restrict__ drow,
+                                                 const int32_t* __restrict__ doff, const int32_t* __restrict__ qpt,
+                                                 int n, int32_t* __restrict__ best_local,
+                                                 uint64_t* __restrict__ out) {
+  const int i = blockIdx.x, l = threadIdx.x;
+  if (i >= n) return;
+  const int p = qpt[i];
+  const int r0 = doff[p], k = doff[p + 1] - r0;
+  unsigned long long key = ~0ull;  // (sum << 32 | local row)
+  for (int r = l; r - l < k; r += 64) {
+    uint64_t x[W];
+    const uint64_t* xr = desc + size_t(drow[r0 + (r < k ? r : 0)]) * W;
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = xr[w];
+    unsigned int sum = 0;
+    for (int q = 0; q < k; ++q) {
+      const uint64_t* y = desc + size_t(drow[r0 + q]) * W;
+#pragma unroll
+      for (int w = 0; w < W; ++w) sum += __popcll(x[w] ^ y[w]);
+    }
+    if (r < k) key = min(key, (static_cast<unsigned long long>(sum) << 32) | unsigned(r));
+  }
+  for (int o = 32; o >= 1; o >>= 1) key = min(key, static_cast<unsigned long long>(__shfl_xor(key, o)));
+  const int b = int(key & 0xffffffffu);
+  if (l == 0) best_local[i] = b;
+  if (l < W) out[size_t(i) * W + l] = desc[size_t(drow[r0 + b]) * W + l];
+}
+
+inline unsigned grid(int64_t n, int b = 256) { return unsigned((n + b - 1) / b); }
+
+template <class T>
+struct DVec {
+  T* p = nullptr;
+  int64_t n = 0, cap = 0;
+};
+
+}  // namespace
+}  // namespace sfm
+
+using namespace sfm;
+
+struct sfm_map {
+  int device = 0, desc_bytes = 0, W = 0;
+  hipStream_t s = nullptr;
+  DVec<int32_t> ob_pt, ob_frame, ob_idx;  // observations, emplace order
+  DVec<double> X;                          // [n_pts][3]
+  int32_t n_pts = 0;
+  DVec<uint64_t> desc;                     // [rows][W]
+  DVec<int32_t> desc_pt;                   // point of each row
+  bool ocsr = false, dcsr = false;         // per-point CSRs current?
+  int32_t *orow = nullptr, *ooff = nullptr, *drow = nullptr, *doff = nullptr;
+  std::map<std::string, std::pair<void*, size_t>> scratch;
+};
+
+namespace {
+
+void* scratch(sfm_map* h, const char* name, size_t bytes, int* rc) {
+  auto& e = h->scratch[name];
+  if (e.second >= bytes && e.first) return e.first;
+  if (e.first) { (void)hipStreamSynchronize(h->s); (void)hipFree(e.first); e.first = nullptr; e.second = 0; }
+  void* p = nullptr;
+  if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) {
+    *rc = mapfail(SFM_ENOMEM, std::string("hipMalloc failed (") + name + ")");
+    return nullptr;
+  }
+  e = {p, std::max<size_t>(bytes, 256)};
+  return p;
+}
+
+template <class T>
+int grow(sfm_map* h, DVec<T>& v, int64_t need) {
+  if (need <= v.cap) return 0;
+  const int64_t cap = std::max<int64_t>({need, 2 * v.cap, 1024});
+  T* p = nullptr;
+  if (hipMalloc(&p, size_t(cap) * sizeof(T)) != hipSuccess) return mapfail(SFM_ENOMEM, "hipMalloc failed (growth)");
+  if (v.n) (void)hipMemcpyAsync(p, v.p, size_t(v.n) * sizeof(T), hipMemcpyDeviceToDevice, h->s);
+  (void)hipStreamSynchronize(h->s);
+  if (v.p) (void)hipFree(v.p);
+  v.p = p;
+  v.cap = cap;
+  return 0;
+}
+
+template <class T>
+int append(sfm_map* h, DVec<T>& v, const T* src, int64_t n) {
+  if (int rc = grow(h, v, v.n + n)) return rc;
+  if (n && hipMemcpyAsync(v.p + v.n, src, size_t(n) * sizeof(T), hipMemcpyHostToDevice, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "upload failed");
+  v.n += n;
+  return 0;
+}
+
+int sync(sfm_map* h) {
+  return hipStreamSynchronize(h->s) == hipSuccess ? 0 : mapfail(SFM_EIO, "kernel or copy failed");
+}
+
+// CSR by point of `key` (n entries, keys < P): rows (entry ids grouped by
+// key, ascending within a key = append order) and offsets [P+1]
+int build_csr(sfm_map* h, const char* tag, const int32_t* key, int64_t n, int32_t** rows_out, int32_t** off_out) {
+  int rc = 0;
+  const int P = h->n_pts;
+  std::string t(tag);
+  auto* kk = static_cast<uint32_t*>(scratch(h, (t + "k").c_str(), sizeof(uint32_t) * std::max<int64_t>(n, 1), &rc));
+  auto* iv = static_cast<int32_t*>(scratch(h, (t + "i").c_str(), sizeof(int32_t) * std::max<int64_t>(n, 1), &rc));
+  auto* rows = static_cast<int32_t*>(scratch(h, (t + "r").c_str(), sizeof(int32_t) * std::max<int64_t>(n, 1), &rc));
+  auto* cnt = static_cast<int32_t*>(scratch(h, (t + "c").c_str(), sizeof(int32_t) * (size_t(P) + 1), &rc));
+  auto* off = static_cast<int32_t*>(scratch(h, (t + "o").c_str(), sizeof(int32_t) * (size_t(P) + 1), &rc));
+  if (rc) return rc;
+  (void)hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t(P) + 1), h->s);
+  if (n) {
+    k_count_keys<<<grid(n), 256, 0, h->s>>>(n, key, cnt);
+    k_iota<<<grid(n), 256, 0, h->s>>>(n, iv);
+    int bits = 1;
+    while (bits < 32 && (1ll << bits) < P) ++bits;
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, reinterpret_cast<const uint32_t*>(key), kk, iv, rows,
+                                             int(n), 0, bits, h->s);
+    void* tmp = scratch(h, (t + "t").c_str(), bytes, &rc);
+    if (rc) return rc;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, bytes, reinterpret_cast<const uint32_t*>(key), kk, iv, rows, int(n),
+                                           0, bits, h->s) != hipSuccess)
+      return mapfail(SFM_EIO, "radix sort failed");
+  }
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, off, P + 1, h->s);
+  void* tmp = scratch(h, (t + "s").c_str(), bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, off, P + 1, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "scan failed");
+  *rows_out = rows;
+  *off_out = off;
+  return 0;
+}
+
+int check_pts(const sfm_map* h, int32_t n, const int32_t* idx) {
+  for (int32_t i = 0; i < n; ++i)
+    if (idx[i] < 0 || idx[i] >= h->n_pts)
+      return mapfail(SFM_EINVAL, "point index " + std::to_string(idx[i]) + " out of range at " + std::to_string(i));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sfm_map_create(int32_t device, int32_t desc_bytes, sfm_map** out) {
+  if (!out) return mapfail(SFM_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (desc_bytes <= 0 || desc_bytes > 512 || desc_bytes % 8 || ((desc_bytes / 8) & (desc_bytes / 8 - 1)))
+    return mapfail(SFM_EINVAL, "desc_bytes must be 8 x a power of two, <= 512 (BRISK: 64, ORB: 32)");
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return mapfail(SFM_ENODEV, "no such device");
+  if (hipSetDevice(device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  auto* h = new sfm_map;
+  h->device = device;
+  h->desc_bytes = desc_bytes;
+  h->W = desc_bytes / 8;
+  if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return mapfail(SFM_EIO, "hipStreamCreate failed");
+  }
+  *out = h;
+  return 0;
+}
+
+int sfm_map_destroy(sfm_map* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->s);
+  for (void* p : {(void*)h->ob_pt.p, (void*)h->ob_frame.p, (void*)h->ob_idx.p, (void*)h->X.p, (void*)h->desc.p,
+                  (void*)h->desc_pt.p})
+    if (p) (void)hipFree(p);
+  for (auto& e : h->scratch)
+    if (e.second.first) (void)hipFree(e.second.first);
+  (void)hipStreamDestroy(h->s);
+  delete h;
+  return 0;
+}
+
+int sfm_map_size(sfm_map* h, int32_t* n_pts, int64_t* n_obs, int64_t* n_desc_rows) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n_pts) *n_pts = h->n_pts;
+  if (n_obs) *n_obs = h->ob_pt.n;
+  if (n_desc_rows) *n_desc_rows = h->desc.n / h->W;
+  return 0;
+}
+
+int sfm_map_add_new_points(sfm_map* h, int32_t n_pts, const double* pts3d, int32_t n_frames, const int32_t* frame_no,
+                           const int32_t* pts2d_idx, int32_t* pts3d_idx) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n_pts < 0 || n_frames < 0) return mapfail(SFM_EINVAL, "negative size");
+  if (n_pts == 0) return 0;
+  if (!pts3d || (n_frames && (!frame_no || !pts2d_idx))) return mapfail(SFM_EINVAL, "NULL argument");
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  // emplace order of CMap.cpp:50-68: point i, then its frames j
+  const int64_t m = int64_t(n_pts) * n_frames;
+  std::vector<int32_t> pt(m), fr(m), ix(m);
+  for (int32_t i = 0; i < n_pts; ++i)
+    for (int32_t j = 0; j < n_frames; ++j) {
+      const int64_t e = int64_t(i) * n_frames + j;
+      pt[e] = h->n_pts + i;
+      fr[e] = frame_no[j];
+      ix[e] = pts2d_idx[int64_t(j) * n_pts + i];
+    }
+  if (int rc = append(h, h->X, pts3d, int64_t(n_pts) * 3)) return rc;
+  if (int rc = append(h, h->ob_pt, pt.data(), m)) return rc;
+  if (int rc = append(h, h->ob_frame, fr.data(), m)) return rc;
+  if (int rc = append(h, h->ob_idx, ix.data(), m)) return rc;
+  if (pts3d_idx)
+    for (int32_t i = 0; i < n_pts; ++i) pts3d_idx[i] = h->n_pts + i;
+  h->n_pts += n_pts;
+  h->ocsr = h->dcsr = false;
+  return sync(h);
+}
+
+int sfm_map_add_point_matches(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const int32_t* pts2d_idx,
+                              int32_t frame_no) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n < 0) return mapfail(SFM_EINVAL, "negative size");
+  if (n == 0) return 0;
+  if (!pts3d_idx || !pts2d_idx) return mapfail(SFM_EINVAL, "NULL argument");
+  if (int rc = check_pts(h, n, pts3d_idx)) return rc;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  std::vector<int32_t> fr(size_t(n), frame_no);
+  if (int rc = append(h, h->ob_pt, pts3d_idx, n)) return rc;
+  if (int rc = append(h, h->ob_frame, fr.data(), n)) return rc;
+  if (int rc = append(h, h->ob_idx, pts2d_idx, n)) return rc;
+  h->ocsr = false;
+  return sync(h);
+}
+
+int sfm_map_add_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const uint8_t* desc) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n < 0) return mapfail(SFM_EINVAL, "negative size");
+  if (n == 0) return 0;
+  if (!pts3d_idx || !desc) return mapfail(SFM_EINVAL, "NULL argument");
+  if (int rc = check_pts(h, n, pts3d_idx)) return rc;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  // rows are desc_bytes = 8 W bytes: copy as words (unaligned host bytes)
+  std::vector<uint64_t> words(size_t(n) * h->W);
+  std::memcpy(words.data(), desc, size_t(n) * h->desc_bytes);
+  if (int rc = append(h, h->desc, words.data(), int64_t(n) * h->W)) return rc;
+  if (int rc = append(h, h->desc_pt, pts3d_idx, n)) return rc;
+  h->dcsr = false;
+  return sync(h);
+}
+
+int sfm_map_get_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, double* pts3d) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n <= 0) return n < 0 ? mapfail(SFM_EINVAL, "negative size") : 0;
+  if (!pts3d_idx || !pts3d) return mapfail(SFM_EINVAL, "NULL argument");
+  if (int rc = check_pts(h, n, pts3d_idx)) return rc;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  std::vector<double> all(size_t(h->n_pts) * 3);
+  if (hipMemcpyAsync(all.data(), h->X.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "download failed");
+  if (int rc = sync(h)) return rc;
+  for (int32_t i = 0; i < n; ++i) std::memcpy(pts3d + 3 * size_t(i), all.data() + 3 * size_t(pts3d_idx[i]), 24);
+  return 0;
+}
+
+int sfm_map_set_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const double* pts3d) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n <= 0) return n < 0 ? mapfail(SFM_EINVAL, "negative size") : 0;
+  if (!pts3d_idx || !pts3d) return mapfail(SFM_EINVAL, "NULL argument");
+  if (int rc = check_pts(h, n, pts3d_idx)) return rc;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  for (int32_t i = 0; i < n; ++i)
+    if (hipMemcpyAsync(h->X.p + 3 * size_t(pts3d_idx[i]), pts3d + 3 * size_t(i), 24, hipMemcpyHostToDevice, h->s) !=
+        hipSuccess)
+      return mapfail(SFM_EIO, "upload failed");
+  return sync(h);
+}
+
+int sfm_map_points_in_frames(sfm_map* h, int32_t n_frames, const int32_t* frame_no, int32_t capacity,
+                             int32_t* pts3d_idx, int32_t* n_out) {
+  if (!h || !n_out) return mapfail(SFM_EINVAL, "NULL argument");
+  *n_out = 0;
+  if (n_frames < 0) return mapfail(SFM_EINVAL, "negative size");
+  if (n_frames == 0 || h->n_pts == 0 || h->ob_pt.n == 0) return 0;
+  if (!frame_no) return mapfail(SFM_EINVAL, "NULL frame list");
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  const int P = h->n_pts;
+  std::vector<int32_t> fs(frame_no, frame_no + n_frames);
+  std::sort(fs.begin(), fs.end());
+  fs.erase(std::unique(fs.begin(), fs.end()), fs.end());
+  auto* fset = static_cast<int32_t*>(scratch(h, "fset", sizeof(int32_t) * fs.size(), &rc));
+  auto* mark = static_cast<uint8_t*>(scratch(h, "mark", size_t(P), &rc));
+  auto* out = static_cast<int32_t*>(scratch(h, "pout", sizeof(int32_t) * size_t(P), &rc));
+  auto* dn = static_cast<int32_t*>(scratch(h, "pn", sizeof(int32_t), &rc));
+  if (rc) return rc;
+  (void)hipMemcpyAsync(fset, fs.data(), sizeof(int32_t) * fs.size(), hipMemcpyHostToDevice, h->s);
+  (void)hipMemsetAsync(mark, 0, size_t(P), h->s);
+  k_mark_frames<<<grid(h->ob_pt.n), 256, 0, h->s>>>(h->ob_pt.n, h->ob_pt.p, h->ob_frame.p, fset, int(fs.size()),
+                                                    mark);
+  hipcub::CountingInputIterator<int32_t> it(0);
+  size_t bytes = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, bytes, it, mark, out, dn, P, h->s);
+  void* tmp = scratch(h, "psel", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceSelect::Flagged(tmp, bytes, it, mark, out, dn, P, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "select failed");
+  int32_t n = 0;
+  (void)hipMemcpyAsync(&n, dn, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  *n_out = n;
+  if (n > capacity) return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(n));
+  if (n && (!pts3d_idx || hipMemcpy(pts3d_idx, out, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost) != hipSuccess))
+    return mapfail(SFM_EIO, "download failed");
+  return 0;
+}
+
+int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int32_t* pts3d_idx, int32_t* n3_out,
+                            int32_t* pts2d_idx, int32_t* n2_out) {
+  if (!h || !n3_out || !n2_out) return mapfail(SFM_EINVAL, "NULL argument");
+  *n3_out = *n2_out = 0;
+  const int64_t N = h->ob_pt.n;
+  if (N == 0) return 0;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  if (!h->ocsr) {
+    if (int r = build_csr(h, "ob", h->ob_pt.p, N, &h->orow, &h->ooff)) return r;
+    h->ocsr = true;
+  }
+  const int32_t *orow = h->orow, *ooff = h->ooff;
+  auto* flag = static_cast<uint8_t*>(scratch(h, "fflag", size_t(N), &rc));
+  auto* sel = static_cast<int32_t*>(scratch(h, "fsel", sizeof(int32_t) * size_t(N), &rc));
+  auto* dn = static_cast<int32_t*>(scratch(h, "fn", sizeof(int32_t), &rc));
+  if (rc) return rc;
+  k_flag_frame<<<grid(N), 256, 0, h->s>>>(N, h->ob_frame.p, frame_no, flag);
+  hipcub::CountingInputIterator<int32_t> it(0);
+  size_t bytes = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, bytes, it, flag, sel, dn, int(N), h->s);
+  void* tmp = scratch(h, "fselt", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceSelect::Flagged(tmp, bytes, it, flag, sel, dn, int(N), h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "select failed");
+  int32_t n = 0;
+  (void)hipMemcpyAsync(&n, dn, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  if (n == 0) return 0;
+  auto* cnt = static_cast<int32_t*>(scratch(h, "fcnt", sizeof(int32_t) * size_t(n), &rc));
+  auto* off2 = static_cast<int32_t*>(scratch(h, "foff", sizeof(int32_t) * size_t(n), &rc));
+  auto* out3 = static_cast<int32_t*>(scratch(h, "fo3", sizeof(int32_t) * size_t(n), &rc));
+  if (rc) return rc;
+  k_dup_count<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, orow, ooff, frame_no, cnt);
+  bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, off2, n, h->s);
+  tmp = scratch(h, "fscan", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, off2, n, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "scan failed");
+  int32_t last[2] = {0, 0};
+  (void)hipMemcpyAsync(last, off2 + n - 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
+  (void)hipMemcpyAsync(last + 1, cnt + n - 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  const int32_t n2 = last[0] + last[1];
+  auto* out2 = static_cast<int32_t*>(scratch(h, "fo2", sizeof(int32_t) * size_t(std::max(n2, 1)), &rc));
+  if (rc) return rc;
+  k_dup_fill<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->ob_idx.p, orow, ooff, frame_no, off2,
+                                        out3, out2);
+  if (int r = sync(h)) return r;
+  *n3_out = n;
+  *n2_out = n2;
+  if (n > capacity || n2 > capacity)
+    return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(std::max(n, n2)));
+  if (!pts3d_idx || !pts2d_idx) return mapfail(SFM_EINVAL, "NULL output");
+  if (hipMemcpy(pts3d_idx, out3, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost) != hipSuccess ||
+      (n2 && hipMemcpy(pts2d_idx, out2, sizeof(int32_t) * size_t(n2), hipMemcpyDeviceToHost) != hipSuccess))
+    return mapfail(SFM_EIO, "download failed");
+  return 0;
+}
+
+int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,
+                                       int32_t* best_row) {
+  if (!h) return mapfail(SFM_EINVAL, "NULL handle");
+  if (n <= 0) return n < 0 ? mapfail(SFM_EINVAL, "negative size") : 0;
+  if (!pts3d_idx || !desc_out) return mapfail(SFM_EINVAL, "NULL argument");
+  if (int rc = check_pts(h, n, pts3d_idx)) return rc;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  const int64_t rows = h->desc.n / h->W;
+  if (!h->dcsr) {
+    if (int r = build_csr(h, "de", h->desc_pt.p, rows, &h->drow, &h->doff)) return r;
+    h->dcsr = true;
+  }
+  const int32_t *drow = h->drow, *doff = h->doff;
+  // every queried point needs a row (the reference reads row -1 otherwise)
+  std::vector<int32_t> off(size_t(h->n_pts) + 1);
+  (void)hipMemcpyAsync(off.data(), doff, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  for (int32_t i = 0; i < n; ++i)
+    if (off[size_t(pts3d_idx[i]) + 1] == off[size_t(pts3d_idx[i])])
+      return mapfail(SFM_EINVAL, "point " + std::to_string(pts3d_idx[i]) + " has no descriptor row");
+  auto* q = static_cast<int32_t*>(scratch(h, "rq", sizeof(int32_t) * size_t(n), &rc));
+  auto* best = static_cast<int32_t*>(scratch(h, "rb", sizeof(int32_t) * size_t(n), &rc));
+  auto* out = static_cast<uint64_t*>(scratch(h, "ro", sizeof(uint64_t) * size_t(n) * h->W, &rc));
+  if (rc) return rc;
+  (void)hipMemcpyAsync(q, pts3d_idx, sizeof(int32_t) * size_t(n), hipMemcpyHostToDevice, h->s);
+  switch (h->W) {
+#define CASE(w) case w: k_map_repr<w><<<n, 64, 0, h->s>>>(h->desc.p, drow, doff, q, n, best, out); break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
+#undef CASE
+    default: return mapfail(SFM_EINVAL, "descriptor width");  // excluded by sfm_map_create
+  }
+  (void)hipMemcpyAsync(desc_out, out, size_t(n) * h->desc_bytes, hipMemcpyDeviceToHost, h->s);
+  std::vector<int32_t> b(static_cast<size_t>(n));
+  (void)hipMemcpyAsync(b.data(), best, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  if (best_row) std::memcpy(best_row, b.data(), sizeof(int32_t) * size_t(n));
+  return 0;
+}
+
+}  // extern "C"
