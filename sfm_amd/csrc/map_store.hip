@@ -129,6 +129,16 @@ __global__ __launch_bounds__(64) void k_map_repr(const uint64_t* __restrict__ de
   if (l < W) out[size_t(i) * W + l] = desc[size_t(drow[r0 + b]) * W + l];
 }
 
+__global__ void k_scatter_points(int n, const int32_t* __restrict__ idx, const double* __restrict__ v,
+                                 double* __restrict__ X) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t p = size_t(idx[i]) * 3;
+  X[p] = v[3 * size_t(i)];
+  X[p + 1] = v[3 * size_t(i) + 1];
+  X[p + 2] = v[3 * size_t(i) + 2];
+}
+
 inline unsigned grid(int64_t n, int b = 256) { return unsigned((n + b - 1) / b); }
 
 template <class T>
@@ -368,10 +378,14 @@ int sfm_map_set_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, const do
   if (!pts3d_idx || !pts3d) return mapfail(SFM_EINVAL, "NULL argument");
   if (int rc = check_pts(h, n, pts3d_idx)) return rc;
   if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
-  for (int32_t i = 0; i < n; ++i)
-    if (hipMemcpyAsync(h->X.p + 3 * size_t(pts3d_idx[i]), pts3d + 3 * size_t(i), 24, hipMemcpyHostToDevice, h->s) !=
-        hipSuccess)
-      return mapfail(SFM_EIO, "upload failed");
+  int rc = 0;
+  auto* di = static_cast<int32_t*>(scratch(h, "si", sizeof(int32_t) * size_t(n), &rc));
+  auto* dv = static_cast<double*>(scratch(h, "sv", sizeof(double) * 3 * size_t(n), &rc));
+  if (rc) return rc;
+  if (hipMemcpyAsync(di, pts3d_idx, sizeof(int32_t) * size_t(n), hipMemcpyHostToDevice, h->s) != hipSuccess ||
+      hipMemcpyAsync(dv, pts3d, sizeof(double) * 3 * size_t(n), hipMemcpyHostToDevice, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "upload failed");
+  k_scatter_points<<<grid(n), 256, 0, h->s>>>(n, di, dv, h->X.p);  // (indices expected unique)
   return sync(h);
 }
 

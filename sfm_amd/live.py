@@ -1,0 +1,362 @@
+"""The reference's LIVE tracking path (CSfM::tracking + CSfM::mapping,
+/root/reference/CSfM.cpp:109-261, 500-692) on the device stages, fed by
+synthetic detector output (BRISK itself, row T8, is not built: its
+arithmetic lives in the absent BRISK library).
+
+Per frame (CSfM::tracking):
+  1. the frame's keypoints + descriptors go up once (sfm_matcher_push_frame);
+  2. matchFeatures(prev matched 2D idx, all current) -- the live
+     frame-to-frame call of CSfM.cpp:518 (sfm_matcher_match_subset, window
+     (1.5, 40) px, ratio 0.8);
+  3. the matched previous keypoints' map points + current positions ->
+     solvePnPRansac(20, 7 px, 0.99) (sfm_pnp_ransac); inliers become the
+     frame's map associations (CSfM.cpp:553-582);
+  4. findMapPointsInCurrentFrame (CSfM.cpp:634-692): points of every
+     keyframe (CMap::getPointsInFrames on the device map store) minus the
+     frame's, projected with the PnP pose, their representative descriptors
+     (device) matched against the unmatched keypoints in the (0, 7) window
+     (sfm_matcher_match);
+  5. addKeyFrame (CSfM.cpp:481-497: >= 10 frames after the last keyframe,
+     >= 50 matched, < 90% of the last keyframe's) -> addPointMatches +
+     addDescriptors, then mapping.
+Per keyframe (CSfM::mapping): against every earlier keyframe, match their
+unmatched keypoints (member window), triangulate (sfm_triangulate_points),
+filter, addNewPoints / addDescriptors, re-find the new points in the
+keyframes in between (0, 7) window, add them to the new keyframe; then
+bundle adjustment over all keyframes, gathered frame-major through
+CMap::getPointsInFrame as CSfM::bundleAdjustment does (CSfM.cpp:310-348),
+one-shot sfm_ba_solve, poses and points written back.
+
+Scope notes: the initial map comes from the stream's known poses of the
+first two keyframes (CSfM::init's homography / fundamental estimation is
+OpenCV's, out of scope); GeometryUtils (filterMatches, projectPoints) is not
+in the reference tree, so filterMatches is restated from its call site
+(CSfM.cpp:164-165) as positive depth in both keyframes and the point-to-
+epipolar-line distance <= _maxReprErr both ways; map-point and keyframe
+culling (CSfM.cpp:232-246) are not restated.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from . import ba as _ba
+from .cmap import DeviceMap
+from .mapping import F_PIX, _rodrigues, triangulate_points
+from .matcher import FeatureMatcher
+from .pnp import solvePnPRansac
+
+MAX_REPR_ERR = 7.0     # CSfM.cpp:35
+KF_TIME_LAG = 10       # CSfM.cpp:44
+MIN_FEATURES = 10      # CTracker::_minFeatures (PnP needs >= 5 correspondences)
+
+
+class KeypointStream:
+    """Synthetic detector output: `n_landmarks` 3D points with a fixed
+    512-bit descriptor each, seen by a 1280x720 pinhole camera translating
+    ~2 px per frame with a slow roll.  A landmark is detectable during its
+    lifetime only (`lifetime` frames from a uniform birth over `horizon`),
+    as detector features come and go with viewpoint and lighting: the view's
+    content turns over at a few percent per frame, so CSfM's keyframe rule
+    (< 90% of the last keyframe's matches) fires while consecutive
+    keyframes are still inside the member match window (40 px).  Per frame
+    every live visible landmark is detected with probability `p_detect`
+    (0.3-px noise, `bit_noise` flipped descriptor bits) and `spurious` random
+    keypoints are mixed in; the order is shuffled.  Closed-form ground
+    truth: pose(k), landmark of each keypoint."""
+
+    def __init__(self, n_landmarks: int = 15000, seed: int = 7, p_detect: float = 0.85, bit_noise: int = 8,
+                 spurious: float = 0.15, px_sigma: float = 0.3, step: float = 0.0196, desc_bytes: int = 64,
+                 lifetime=(40, 100), horizon: int = 400):
+        rng = np.random.default_rng(seed)
+        self.w, self.h = 1280, 720
+        self.K = np.array([[F_PIX, 0.0, 640.0], [0.0, F_PIX, 360.0], [0.0, 0.0, 1.0]])
+        self.L = np.column_stack([rng.uniform(-6.0, 14.0, n_landmarks), rng.uniform(-4.0, 4.0, n_landmarks),
+                                  rng.uniform(8.0, 14.0, n_landmarks)])
+        self.D = rng.integers(0, 256, size=(n_landmarks, desc_bytes), dtype=np.uint8)
+        self.birth = rng.integers(-lifetime[1], horizon, size=n_landmarks)
+        self.death = self.birth + rng.integers(lifetime[0], lifetime[1] + 1, size=n_landmarks)
+        self.seed, self.p_detect, self.bit_noise = seed, p_detect, bit_noise
+        self.spurious, self.px_sigma, self.step, self.desc_bytes = spurious, px_sigma, step, desc_bytes
+
+    def pose(self, k: int):
+        """(rvec, t) of frame k: x_cam = R X + t (frame 0 at the origin)."""
+        c = np.array([self.step * k, 0.15 * np.sin(0.02 * k), 0.0])
+        r = np.array([0.0, 0.0, 0.0008 * k])
+        R = _rodrigues(r)
+        return r, -R @ c
+
+    def frame(self, k: int):
+        rng = np.random.default_rng((self.seed, k))
+        r, t = self.pose(k)
+        Xc = self.L @ _rodrigues(r).T + t
+        uv = Xc[:, :2] / Xc[:, 2:3] * F_PIX + self.K[:2, 2]
+        vis = (Xc[:, 2] > 0.5) & (uv[:, 0] >= 16) & (uv[:, 0] < self.w - 16) & (uv[:, 1] >= 16) & \
+              (uv[:, 1] < self.h - 16) & (self.birth <= k) & (k < self.death) & (rng.random(len(uv)) < self.p_detect)
+        lid = np.flatnonzero(vis)
+        pts = uv[lid] + rng.normal(0.0, self.px_sigma, size=(len(lid), 2))
+        desc = self.D[lid].copy()
+        nb = self.desc_bytes * 8
+        for _ in range(self.bit_noise):
+            bit = rng.integers(0, nb, size=len(lid))
+            desc[np.arange(len(lid)), bit // 8] ^= (1 << (bit % 8)).astype(np.uint8)
+        ns = int(self.spurious * len(lid))
+        pts = np.vstack([pts, np.column_stack([rng.uniform(16, self.w - 16, ns), rng.uniform(16, self.h - 16, ns)])])
+        desc = np.vstack([desc, rng.integers(0, 256, size=(ns, self.desc_bytes), dtype=np.uint8)])
+        lid = np.concatenate([lid, np.full(ns, -1)])
+        perm = rng.permutation(len(lid))
+        return pts[perm], desc[perm], lid[perm]
+
+
+class _Frame:
+    """CFrame: keypoints (undistorted), descriptors, 3D index per keypoint
+    (-1: unmatched), pose."""
+
+    def __init__(self, no, pts, desc):
+        self.no, self.pts, self.desc = no, pts, desc
+        self.pt3d = np.full(len(pts), -1, np.int64)
+        self.rot, self.t = np.zeros(3), np.zeros(3)
+
+    def n_matched(self) -> int:
+        return int((self.pt3d >= 0).sum())
+
+    def copy(self):
+        f = _Frame(self.no, self.pts, self.desc)
+        f.pt3d, f.rot, f.t = self.pt3d.copy(), self.rot.copy(), self.t.copy()
+        return f
+
+    def P(self, K):
+        return K @ np.hstack([_rodrigues(self.rot), self.t.reshape(3, 1)])
+
+
+def _project(K, rot, t, X):
+    Xc = X @ _rodrigues(rot).T + t
+    return Xc[:, :2] / Xc[:, 2:3] * np.array([K[0, 0], K[1, 1]]) + K[:2, 2], Xc[:, 2]
+
+
+def _filter_matches(K, f0, f1, uv0, uv1, X, max_err):
+    """filterMatches restated from its call site (CSfM.cpp:164-165): positive
+    depth in both keyframes, point-to-epipolar-line distance <= max_err both
+    ways (F of the two poses)."""
+    R0, R1 = _rodrigues(f0.rot), _rodrigues(f1.rot)
+    R = R1 @ R0.T
+    tt = f1.t - R @ f0.t
+    tx = np.array([[0, -tt[2], tt[1]], [tt[2], 0, -tt[0]], [-tt[1], tt[0], 0]])
+    Ki = np.linalg.inv(K)
+    F = Ki.T @ tx @ R @ Ki
+    h0 = np.column_stack([uv0, np.ones(len(uv0))])
+    h1 = np.column_stack([uv1, np.ones(len(uv1))])
+    l1 = h0 @ F.T          # lines in image 1
+    l0 = h1 @ F            # lines in image 0
+    d1 = np.abs((l1 * h1).sum(1)) / np.hypot(l1[:, 0], l1[:, 1])
+    d0 = np.abs((l0 * h0).sum(1)) / np.hypot(l0[:, 0], l0[:, 1])
+    z0 = (X @ R0.T + f0.t)[:, 2]
+    z1 = (X @ R1.T + f1.t)[:, 2]
+    return (z0 > 0) & (z1 > 0) & (d0 <= max_err) & (d1 <= max_err) & np.isfinite(X).all(1)
+
+
+class LiveSfM:
+    def __init__(self, stream: KeypointStream | None = None, device: int = 0, init_gap: int = 5):
+        self.stream = stream if stream is not None else KeypointStream()
+        self.K = self.stream.K
+        self.device = device
+        self.init_gap = int(init_gap)
+        self.matcher = FeatureMatcher(self.stream.desc_bytes, device=device)
+        self.map = DeviceMap(self.stream.desc_bytes, device=device)
+        self.kfs: list[_Frame] = []
+        self.prev: _Frame | None = None
+        self.frame_no = -1
+        self.lost = 0
+        self.ba_log: list[dict] = []
+        self.stats = {"frames": 0, "tracked": 0, "pnp_inliers": 0, "map_matches": 0, "new_points": 0}
+        self.times = {"stream": 0.0, "track": 0.0, "map_match": 0.0, "mapping": 0.0, "ba": 0.0}
+        self._pending: _Frame | None = None
+
+    # ---- driver --------------------------------------------------------------
+    def run(self, n_frames: int) -> None:
+        for k in range(n_frames):
+            t0 = time.perf_counter()
+            pts, desc, _ = self.stream.frame(k)
+            self.times["stream"] += time.perf_counter() - t0
+            self.process(k, pts, desc)
+
+    def process(self, k: int, pts, desc) -> None:
+        self.frame_no = k
+        self.stats["frames"] += 1
+        if not self.kfs:
+            f = _Frame(k, pts, desc)
+            self.kfs.append(f)                  # first keyframe at the origin (CFrame.cpp:229-235)
+            self.matcher.push_frame(pts, desc)
+            self.prev = f
+            return
+        if len(self.kfs) == 1:
+            if k < self.init_gap:
+                return
+            self._initialise(k, pts, desc)
+            return
+        self._tracking(k, pts, desc)
+
+    # ---- initial map (bootstrap: known poses of the first two keyframes) ------
+    def _initialise(self, k, pts, desc) -> None:
+        f0 = self.kfs[0]
+        f1 = _Frame(k, pts, desc)
+        f1.rot, f1.t = self.stream.pose(k)
+        self.matcher.push_frame(pts, desc)
+        i0, i1 = self.matcher.match(f0.pts, f0.desc, f1.pts, f1.desc)
+        X = triangulate_points(np.zeros(len(i0), np.int32), np.ones(len(i0), np.int32), f0.pts[i0], f1.pts[i1],
+                               np.stack([f0.P(self.K), f1.P(self.K)]), device=self.device)
+        ok = _filter_matches(self.K, f0, f1, f0.pts[i0], f1.pts[i1], X, MAX_REPR_ERR)
+        i0, i1, X = i0[ok], i1[ok], X[ok]
+        idx = self.map.addNewPoints(X, np.stack([i0, i1]), [f0.no, f1.no])
+        self.map.addDescriptors(idx, f0.desc[i0])
+        self.map.addDescriptors(idx, f1.desc[i1])
+        f0.pt3d[i0] = idx
+        f1.pt3d[i1] = idx
+        self.kfs.append(f1.copy())
+        self.stats["new_points"] += len(idx)
+        self._bundle_adjust()
+        self.prev = f1
+        self.prev.rot, self.prev.t = self.kfs[-1].rot.copy(), self.kfs[-1].t.copy()
+
+    # ---- CSfM::tracking ----------------------------------------------------------
+    def _tracking(self, k, pts, desc) -> None:
+        t0 = time.perf_counter()
+        cur = _Frame(k, pts, desc)
+        self.matcher.push_frame(pts, desc)
+        prev_idx = np.flatnonzero(self.prev.pt3d >= 0).astype(np.int32)
+        pm, cm = self.matcher.match_subset(prev_idx, np.arange(len(pts), dtype=np.int32))
+        if len(cm) < MIN_FEATURES:
+            # lost: keep matching against the previous frame (no swap)
+            self.lost += 1
+            self.matcher.push_frame(self.prev.pts, self.prev.desc)
+            self.times["track"] += time.perf_counter() - t0
+            return
+        self.lost = 0
+        m3 = self.prev.pt3d[pm]
+        obj = self.map.getPointsAtIdx(m3)
+        found, r, t, inl = solvePnPRansac(obj, pts[cm], self.K, 20, MAX_REPR_ERR, 0.99, device=self.device)
+        cur.rot, cur.t = np.asarray(r, float), np.asarray(t, float)
+        cur.pt3d[cm[inl]] = m3[inl]
+        self.stats["tracked"] += 1
+        self.stats["pnp_inliers"] += len(inl)
+        t1 = time.perf_counter()
+        self.times["track"] += t1 - t0
+        self._find_map_points(cur)
+        self.times["map_match"] += time.perf_counter() - t1
+        if self._add_keyframe(cur):
+            kf = cur.copy()
+            self.kfs.append(kf)
+            m = np.flatnonzero(kf.pt3d >= 0)
+            self.map.addPointMatches(kf.pt3d[m], m, kf.no)
+            self.map.addDescriptors(kf.pt3d[m], kf.desc[m])
+            t2 = time.perf_counter()
+            self._mapping()
+            self.times["mapping"] += time.perf_counter() - t2
+            # CSfM.cpp:261: the previous frame takes the adjusted keyframe pose
+            cur.rot, cur.t = self.kfs[-1].rot.copy(), self.kfs[-1].t.copy()
+        self.prev = cur
+
+    def _find_map_points(self, cur: _Frame) -> None:
+        """CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692)."""
+        cov = self.map.getPointsInFrames([f.no for f in self.kfs])
+        existing = np.unique(cur.pt3d[cur.pt3d >= 0])
+        new = np.setdiff1d(cov, existing, assume_unique=True).astype(np.int32)
+        un = np.flatnonzero(cur.pt3d < 0)
+        if not len(new) or len(un) < 2:
+            return
+        X = self.map.getPointsAtIdx(new)
+        desc = self.map.getRepresentativeDescriptors(new)
+        uv, _ = _project(self.K, cur.rot, cur.t, X)
+        mi, fi = self.matcher.match(uv, desc, cur.pts[un], cur.desc[un], 0.8, 0.0, MAX_REPR_ERR)
+        cur.pt3d[un[fi]] = new[mi]
+        self.stats["map_matches"] += len(mi)
+
+    def _add_keyframe(self, cur: _Frame) -> bool:
+        """CSfM::addKeyFrame (CSfM.cpp:481-497)."""
+        last = self.kfs[-1]
+        a = cur.no >= last.no + KF_TIME_LAG
+        b = cur.n_matched() >= 50
+        c = cur.n_matched() < 0.9 * last.n_matched()
+        return a and b and c
+
+    # ---- CSfM::mapping -------------------------------------------------------------
+    def _mapping(self) -> None:
+        new_kf = self.kfs[-1]
+        for i in range(len(self.kfs) - 1):
+            kf = self.kfs[i]
+            cu = np.flatnonzero(new_kf.pt3d < 0)
+            pu = np.flatnonzero(kf.pt3d < 0)
+            if len(cu) < 2 or len(pu) < 2:
+                continue
+            pi, ci = self.matcher.match(kf.pts[pu], kf.desc[pu], new_kf.pts[cu], new_kf.desc[cu])
+            if not len(pi):
+                continue
+            uv0, uv1 = kf.pts[pu[pi]], new_kf.pts[cu[ci]]
+            X = triangulate_points(np.zeros(len(pi), np.int32), np.ones(len(pi), np.int32), uv0, uv1,
+                                   np.stack([kf.P(self.K), new_kf.P(self.K)]), device=self.device)
+            ok = _filter_matches(self.K, kf, new_kf, uv0, uv1, X, MAX_REPR_ERR)
+            if not ok.any():
+                continue
+            p2, c2, Xf = pu[pi[ok]], cu[ci[ok]], X[ok]
+            idx = self.map.addNewPoints(Xf, p2.reshape(1, -1), [kf.no])
+            kf.pt3d[p2] = idx
+            pdesc, cdesc = kf.desc[p2], new_kf.desc[c2]
+            self.map.addDescriptors(idx, pdesc)
+            # re-find the new points in the keyframes in between (CSfM.cpp:189-221)
+            for j in range(i + 1, len(self.kfs) - 1):
+                kj = self.kfs[j]
+                uj = np.flatnonzero(kj.pt3d < 0)
+                if len(uj) < 2:
+                    continue
+                uv, _ = _project(self.K, kj.rot, kj.t, Xf)
+                d = pdesc if abs(kj.no - kf.no) < abs(kj.no - new_kf.no) else cdesc
+                m0, m1 = self.matcher.match(uv, d, kj.pts[uj], kj.desc[uj], 0.8, 0.0, MAX_REPR_ERR)
+                if len(m0):
+                    self.map.addPointMatches(idx[m0], uj[m1], kj.no)
+                    kj.pt3d[uj[m1]] = idx[m0]
+                    self.map.addDescriptors(idx[m0], kj.desc[uj[m1]])
+            self.map.addPointMatches(idx, c2, new_kf.no)
+            new_kf.pt3d[c2] = idx
+            self.map.addDescriptors(idx, cdesc)
+            self.stats["new_points"] += len(idx)
+        t0 = time.perf_counter()
+        self._bundle_adjust()
+        self.times["ba"] += time.perf_counter() - t0
+
+    def _bundle_adjust(self) -> None:
+        """CSfM::bundleAdjustment over all keyframes (CSfM.cpp:300-348): per
+        keyframe, CMap::getPointsInFrame on the device map store, parameter
+        blocks deduplicated first-seen, one-shot sfm_ba_solve, write-back."""
+        uv, cam, p3 = [], [], []
+        for c, kf in enumerate(self.kfs):
+            a3, a2 = self.map.getPointsInFrame(kf.no)
+            n = min(len(a3), len(a2))  # obs j pairs entry j with 2D index j (CSfM.cpp:320-330)
+            uv.append(kf.pts[a2[:n]])
+            cam.append(np.full(n, c, np.int32))
+            p3.append(a3[:n])
+        uv, cam, p3 = np.vstack(uv), np.concatenate(cam), np.concatenate(p3)
+        if not len(p3):
+            return
+        uniq, first = np.unique(p3, return_index=True)
+        order = uniq[np.argsort(first)]          # first-seen order of the gather
+        remap = np.empty(int(order.max()) + 1, np.int32)
+        remap[order] = np.arange(len(order), dtype=np.int32)
+        pt = remap[p3]
+        X = self.map.getPointsAtIdx(order)
+        C = len(self.kfs)
+        rot = np.stack([f.rot for f in self.kfs])
+        t = np.stack([f.t for f in self.kfs])
+        K9 = np.tile(self.K.reshape(1, 9), (C, 1))
+        rec = {"uv": uv.copy(), "cam_idx": cam.copy(), "pt_idx": pt.copy(), "K": K9, "rot": rot.copy(), "t": t.copy(),
+               "X": X.copy()}
+        sm, tr = _ba.solve(uv, cam, pt, K9, rot, t, X)
+        rec.update({"summary": sm, "trace": tr, "rot_out": rot.copy(), "t_out": t.copy(), "X_out": X.copy()})
+        self.ba_log.append(rec)
+        for c, f in enumerate(self.kfs):
+            f.rot, f.t = rot[c].copy(), t[c].copy()
+        self.map.setPointsAtIdx(order, X)
+
+    def close(self) -> None:
+        self.matcher.close()
+        self.map.close()
