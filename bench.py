@@ -304,6 +304,50 @@ def c5_pipeline_leg(device: int, cpu: bool, n_frames: int = 300) -> dict:
     return out
 
 
+def live_path_leg(device: int, cpu: bool, n_frames: int = 300) -> dict:
+    """The reference's live tracking path (sfm_amd.live.LiveSfM: CSfM::tracking
+    + CSfM::mapping) on synthetic detector output (~1100 keypoints, 64-B
+    descriptors per frame; BRISK itself is not built): per frame
+    matchFeatures(prevIdx, currIdx) + PnP + map-point re-finding through the
+    device map store, per keyframe KF-pair matching, triangulation and BA over
+    all keyframes.  Keypoint frames are generated before the timed region."""
+    from sfm_amd.live import KeypointStream, LiveSfM
+    st = KeypointStream()
+    frames = [st.frame(k)[:2] for k in range(n_frames)]
+    warm = LiveSfM(st, device=device)
+    for k in range(25):
+        warm.process(k, *frames[k])
+    warm.close()
+    s = LiveSfM(st, device=device)
+    t0 = time.perf_counter()
+    for k in range(n_frames):
+        s.process(k, *frames[k])
+    wall = time.perf_counter() - t0
+    last = s.ba_log[-1] if s.ba_log else None
+    n_pts, n_obs, _ = s.map.size()
+    out = {"workload": f"live path: {n_frames} frames of synthetic detector output (~1100 keypoints, 64-B descriptors), "
+                       "matchFeatures(prevIdx, currIdx) + solvePnPRansac + findMapPointsInCurrentFrame per frame, "
+                       "mapping + BA over all keyframes per keyframe",
+           "frames_per_s": n_frames / wall, "ms_per_frame": wall / n_frames * 1e3, "keyframes": len(s.kfs),
+           "map_points": int(n_pts), "map_observations": int(n_obs), "tracked_frames": s.stats["tracked"],
+           "last_ba": None if last is None else {"cams": int(last["rot"].shape[0]), "points": int(last["X"].shape[0]),
+                                                  "obs": int(len(last["uv"])),
+                                                  "lm_iterations": last["summary"].num_iterations},
+           "host_s": {k: round(val, 4) for k, val in s.times.items() if k != "stream"}, "cpu_baseline": None}
+    if cpu and s.ba_log:
+        from oracle import ffi as O
+        t0 = time.perf_counter()
+        for rec in s.ba_log:
+            r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
+            O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], r, t, X)
+        cw = time.perf_counter() - t0
+        out["cpu_baseline"] = {"ba_s_all_keyframes": cw, "gpu_ba_s_all_keyframes": s.times["ba"], "cores": 1,
+                               "kind": "port", "sample": f"the {len(s.ba_log)} keyframe BA problems of this run "
+                                                         "re-solved by oracle/ba_oracle.cpp, 1 thread"}
+    s.close()
+    return out
+
+
 def oneshot_leg(sc, reps: int = 3) -> dict:
     """One-shot C3 solve as the drop-in is called: host arrays in,
     sfm_ba_solve (problem setup + upload + LM + download) -- the reference
@@ -615,6 +659,7 @@ def main() -> int:
         out["incremental_ba"] = incremental_ba_leg(local_rank, not args.no_cpu_baseline)
         out["pnp"] = pnp_leg(local_rank, not args.no_cpu_baseline)
         out["c5_pipeline"] = c5_pipeline_leg(local_rank, not args.no_cpu_baseline)
+        out["live_path"] = live_path_leg(local_rank, not args.no_cpu_baseline)
     if args.phases and rank == 0:
         print(json.dumps(phases, indent=1), file=sys.stderr)
     if rank == 0:
