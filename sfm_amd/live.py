@@ -49,7 +49,7 @@ from .pnp import solvePnPRansac
 
 MAX_REPR_ERR = 7.0     # CSfM.cpp:35
 KF_TIME_LAG = 10       # CSfM.cpp:44
-MIN_FEATURES = 10      # CTracker::_minFeatures (PnP needs >= 5 correspondences)
+MIN_FEATURES = 5       # CTracker::_minFeatures (CTracker.cpp:32)
 
 
 class KeypointStream:
