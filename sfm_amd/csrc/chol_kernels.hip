@@ -288,7 +288,7 @@ __device__ __forceinline__ void block_publish_wt(int* f, int epoch) {
 // Wave 0 finds how many of k = k_from.. (<= K) have both F(i,k) and F(j,k)
 // final (waiting until at least one has); the block gets the new bound.
 __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, int k_from, int K, int epoch,
-                                           int* sh, int* fail) {
+                                           int* sh, int* fail, int i2 = -1) {
   if (wave0()) {
     const int lane = threadIdx.x;
     long spins = 0;
@@ -298,7 +298,8 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
       bool ok = true;
       if (k <= K)
         ok = __hip_atomic_load(F + i * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-             __hip_atomic_load(F + j * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+             __hip_atomic_load(F + j * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+             (i2 < 0 || __hip_atomic_load(F + i2 * nb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
       const unsigned long long miss = __ballot(!ok);
       const int run = miss ? __builtin_ctzll(miss) : 64;
       bound = k_from + run;
@@ -421,6 +422,130 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
       for (int reg = 0; reg < 4; ++reg)
         st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr, acc[a][bb][reg]);
   block_publish_wt(F + i * nb + j, epoch);
+}
+
+// Helper: the vertical pair of final tiles (i, j), (i+1, j) (i >= j + 2).
+// Both share the L_jk operand of every update step, so a step loads three
+// panel tiles for two tile updates (four as single tiles): at n = 12000 the
+// helpers, 62% MFMA-busy, fetch 43.7 GB per factor re-reading panels.  Each
+// tile's update order (k, then ks) is the single-tile form's, so the factor
+// is bitwise unchanged.  A's values of the two tiles are read at the end
+// (nobody else writes them before this task publishes).
+__device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld, int nb,
+                                                  const double* __restrict__ Winv, int* __restrict__ F, int epoch,
+                                                  int i, int j, double* T0, double* T1, int* sh,
+                                                  int* __restrict__ fail) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int i0 = i * NB, i1 = i0 + NB, j0 = j * NB;
+  const int K = j - 1;
+  f64x4 acc[2][2][2];  // [tile][a][bb]
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) acc[u][a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+  int kr = 0;
+  for (int k = 0; k <= K; ++k) {
+    if (k >= kr) kr = ready_bound(F, nb, i, j, k, K, epoch, sh, fail, i + 1);
+    const int k0 = k * NB;
+    double xa[2][16], yb[2][2][16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const size_t colbase = size_t(k0 + 4 * ks + lk) * ld;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) xa[a][ks] = A[colbase + j0 + cb + 16 * a + lr];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        yb[0][bb][ks] = A[colbase + i0 + rb + 16 * bb + lr];
+        yb[1][bb][ks] = A[colbase + i1 + rb + 16 * bb + lr];
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb)
+            acc[u][a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[u][bb][ks], acc[u][a][bb], 0, 0, 0);
+  }
+  // T_u = A - acc -> LDS
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    double* Tu = u ? T1 : T0;
+    const int iu = u ? i1 : i0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int c = cb + 16 * a + lk + 4 * reg, r = rb + 16 * bb + lr;
+          Tu[c * TS + r] = A[size_t(j0 + c) * ld + iu + r] - acc[u][a][bb][reg];
+        }
+  }
+  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+  const double* Wk = Winv + size_t(j) * NB * NB;
+  double xa[2][16], yb[2][2][16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int m = 4 * ks + lk;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      yb[0][bb][ks] = T0[m * TS + rb + 16 * bb + lr];
+      yb[1][bb][ks] = T1[m * TS + rb + 16 * bb + lr];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) acc[u][a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+          acc[u][a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[u][bb][ks], acc[u][a][bb], 0, 0, 0);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+          st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + (u ? i1 : i0) + rb + 16 * bb + lr,
+                acc[u][a][bb][reg]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave0()) {
+    __hip_atomic_store(F + i * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F + (i + 1) * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Helper tasks of column j: the diagonal tile, the subdiagonal tile (both
+// partial, for the walker), then the vertical pairs of final tiles (a last
+// single tile when the column's count is odd).
+__host__ __device__ __forceinline__ int col_tasks(int nb, int j) {
+  const int m = nb - j;
+  return m <= 2 ? m : 2 + (m - 1) / 2;
+}
+__host__ __device__ __forceinline__ int chol_tasks(int nb) {
+  int s = 0;
+  for (int j = 0; j < nb; ++j) s += col_tasks(nb, j);
+  return s;
 }
 
 // X = T W^T for one 64x64 tile (T and W in LDS, W lower triangular): wave w
@@ -582,7 +707,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, fail);
     return;
   }
-  const int ntask = nb * (nb + 1) / 2;
+  const int ntask = chol_tasks(nb);
   // every launch takes exactly ntask + nhelp tickets (one failing grab per helper)
   const unsigned long long base = (unsigned long long)(epoch - 1) * (unsigned long long)(ntask + nhelp);
   while (true) {
@@ -602,8 +727,14 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     __syncthreads();
     if (tk >= ntask) break;
     int j = 0, r = tk;
-    while (r >= nb - j) { r -= nb - j; ++j; }
-    fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
+    while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
+    if (r < 2) {
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
+    } else {
+      const int i = j + 2 + 2 * (r - 2);
+      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail);
+      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail);
+    }
   }
 }
 
@@ -705,7 +836,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
-  const int nb = d.nblk, ntask = nb * (nb + 1) / 2;
+  const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (the walker + helpers must be co-resident)
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
