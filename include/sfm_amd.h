@@ -288,6 +288,17 @@ int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int3
 int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,
                                        int32_t* best_row);
 
+/* BRISK descriptor (CTracker::detectFeatures' _descriptor->compute,
+ * CTracker.cpp:284): BRISK as published in its
+ * reference implementation's form (oracle/brisk_oracle.py; the reference's
+ * ethz-asl BRISK 2 library is absent, so parity with it is unpinned).
+ * img [h][w] 8-bit grey; kps [n][3] = (x, y, size) as cv::KeyPoint.
+ * Keypoints nearer the border than their scale's pattern are dropped (as
+ * the reference's compute does): kept [n_kept] = their input indices,
+ * angle [n_kept] degrees in [0, 360), desc [n_kept][64]. */
+int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, const float* kps, int32_t n,
+                       int32_t* kept, float* angle, uint8_t* desc, int32_t* n_kept);
+
 /* Per-frame pose: cv::solvePnPRansac(objectPoints, imagePoints, K, dist = 0,
  * rvec, tvec, false, iterations, reproj_err, confidence, inliers,
  * SOLVEPNP_ITERATIVE) as CSfM::tracking calls it (CSfM.cpp:553-565:
