@@ -299,6 +299,20 @@ int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts
 int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, const float* kps, int32_t n,
                        int32_t* kept, float* angle, uint8_t* desc, int32_t* n_kept);
 
+/* BRISK detection (+ description): CTracker::detectFeatures
+ * (CTracker.cpp:275-287) with BriskFeatureDetector(threshold 60, octaves 6,
+ * suppressScaleNonmaxima) -- the published scale-space FAST detector with
+ * the simplifications named in oracle/brisk_oracle.py (unpinned vs the
+ * absent ethz-asl library).  kps [capacity][5] = (x, y, size, angle,
+ * response), octave [capacity] = layer.  desc [capacity][64] or NULL: with
+ * NULL, detection only (angle -1, no border removal); otherwise the
+ * descriptor's border rule drops keypoints as the reference's compute does.
+ * Keypoints come in BRISK's order (layer, then row-major).  *n_out = the
+ * count (an error when it exceeds capacity). */
+int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, int32_t threshold,
+                              int32_t octaves, int32_t capacity, float* kps, int32_t* octave, uint8_t* desc,
+                              int32_t* n_out);
+
 /* Per-frame pose: cv::solvePnPRansac(objectPoints, imagePoints, K, dist = 0,
  * rvec, tvec, false, iterations, reproj_err, confidence, inliers,
  * SOLVEPNP_ITERATIVE) as CSfM::tracking calls it (CSfM.cpp:553-565:

@@ -229,3 +229,198 @@ def describe(img: np.ndarray, kps: np.ndarray, pattern=None):
         angles.append(float(angle))
         descs.append(desc)
     return np.array(kept, np.int64), np.array(angles, np.float32), np.array(descs, np.uint8).reshape(-1, n_bytes)
+
+
+# ---------------------------------------------------------------------------
+# Detector
+_CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+           (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]  # (x, y), OpenCV offsets16
+
+
+def halfsample(img):
+    """2x area average, (a + b + c + d + 2) >> 2 (an odd last row / column is dropped)."""
+    h2, w2 = img.shape[0] // 2, img.shape[1] // 2
+    a = img[:2 * h2, :2 * w2].astype(np.int32)
+    s = a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2]
+    return ((s + 2) >> 2).astype(np.uint8)
+
+
+def twothirdsample(img):
+    """2/3 area average: every 3x3 block -> 2x2 with weights (4, 2, 2, 1) / 9,
+    rounded ((x + 4) / 9); the remainder rows / columns are dropped."""
+    h3, w3 = img.shape[0] // 3, img.shape[1] // 3
+    a = img[:3 * h3, :3 * w3].astype(np.int32)
+    p = [[a[r::3, c::3] for c in range(3)] for r in range(3)]
+    out = np.zeros((2 * h3, 2 * w3), np.int32)
+    out[0::2, 0::2] = 4 * p[0][0] + 2 * p[0][1] + 2 * p[1][0] + p[1][1]
+    out[0::2, 1::2] = 4 * p[0][2] + 2 * p[0][1] + 2 * p[1][2] + p[1][1]
+    out[1::2, 0::2] = 4 * p[2][0] + 2 * p[1][0] + 2 * p[2][1] + p[1][1]
+    out[1::2, 1::2] = 4 * p[2][2] + 2 * p[1][2] + 2 * p[2][1] + p[1][1]
+    return ((out + 4) // 9).astype(np.uint8)
+
+
+def pyramid(img, octaves: int = 6):
+    """BriskScaleSpace::constructPyramid: [(layer image, scale, offset)]
+    c0, d0 = 2/3 c0, then every layer halves the one two before it."""
+    f32 = np.float32
+    L = [(np.ascontiguousarray(img, np.uint8), f32(1.0), f32(0.0))]
+    n = max(1, 2 * octaves)
+    if n > 1:
+        s = f32(1.5)
+        L.append((twothirdsample(img), s, f32(f32(0.5) * s - f32(0.5))))
+    for i in range(2, n, 2):
+        for b in (i - 2, i - 1):
+            s = f32(L[b][1] * f32(2.0))
+            L.append((halfsample(L[b][0]), s, f32(f32(0.5) * s - f32(0.5))))
+    return L
+
+
+def fast_score(img):
+    """R = cornerScore<16>(p, threshold 0) when >= 1, else 0 (BriskLayer::
+    getAgastScore(x, y, 1)); 0 within 3 pixels of the border."""
+    h, w = img.shape
+    R = np.zeros((h, w), np.int32)
+    if h < 7 or w < 7:
+        return R
+    v = img[3:h - 3, 3:w - 3].astype(np.int32)
+    d = np.stack([v - img[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx].astype(np.int32) for (dx, dy) in _CIRCLE])
+    dark = np.full(v.shape, -10 ** 6, np.int32)
+    bright = np.full(v.shape, -10 ** 6, np.int32)
+    for s in range(16):
+        arc = d[[(s + m) % 16 for m in range(9)]]
+        dark = np.maximum(dark, arc.min(0))
+        bright = np.maximum(bright, (-arc).min(0))
+    sc = np.maximum(np.maximum(dark, bright), 0) - 1
+    R[3:h - 3, 3:w - 3] = np.where(sc >= 1, sc, 0)
+    return R
+
+
+def _is_max2d(S, x, y):
+    """BriskScaleSpace::isMax2D on the thresholded score map S."""
+    c = S[y, x]
+    nb = [(-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1)]
+    for dx, dy in nb:
+        if S[y + dy, x + dx] > c:
+            return False
+    eq = [(dx, dy) for dx, dy in nb if S[y + dy, x + dx] == c]
+    if not eq:
+        return True
+
+    def smooth(cx, cy):
+        w = ((1, 2, 1), (2, 4, 2), (1, 2, 1))
+        return sum(w[j][i] * int(S[cy - 1 + j, cx - 1 + i]) for j in range(3) for i in range(3))
+
+    sc = smooth(x, y)
+    for dx, dy in eq:
+        if smooth(x + dx, y + dy) > sc:
+            return False
+    return True
+
+
+def subpixel2d(s):
+    """BriskScaleSpace::subpixel2D on the 3x3 scores s[row][col] -> (dx, dy,
+    max), float32 step for step (the reference's delta_y = delta_x1 / _x2
+    assignment in the clamped branch included)."""
+    f = np.float32
+    s_0_0, s_0_1, s_0_2 = int(s[0][0]), int(s[0][1]), int(s[0][2])
+    s_1_0, s_1_1, s_1_2 = int(s[1][0]), int(s[1][1]), int(s[1][2])
+    s_2_0, s_2_1, s_2_2 = int(s[2][0]), int(s[2][1]), int(s[2][2])
+    tmp1 = s_0_0 + s_0_2 - 2 * s_1_1 + s_2_0 + s_2_2
+    coeff1 = 3 * (tmp1 + s_0_1 - ((s_1_0 + s_1_2) << 1) + s_2_1)
+    coeff2 = 3 * (tmp1 - ((s_0_1 + s_2_1) << 1) + s_1_0 + s_1_2)
+    tmp2 = s_0_2 - s_2_0
+    tmp3 = s_0_0 + tmp2 - s_2_2
+    tmp4 = tmp3 - 2 * tmp2
+    coeff3 = -3 * (tmp3 + s_0_1 - s_2_1)
+    coeff4 = -3 * (tmp4 + s_1_0 - s_1_2)
+    coeff5 = (s_0_0 - s_0_2 - s_2_0 + s_2_2) << 2
+    coeff6 = -((s_0_0 + s_0_2 - ((s_1_0 + s_0_1 + s_1_2 + s_2_1) << 1) - 5 * s_1_1 + s_2_0 + s_2_2) << 1)
+    H_det = 4 * coeff1 * coeff2 - coeff5 * coeff5
+
+    def quad(dx, dy):
+        v = f(f(f(coeff1) * dx) * dx)
+        v = f(v + f(f(f(coeff2) * dy) * dy))
+        v = f(v + f(f(coeff3) * dx))
+        v = f(v + f(f(coeff4) * dy))
+        v = f(v + f(f(f(coeff5) * dx) * dy))
+        v = f(v + f(coeff6))
+        return f(v / f(18.0))
+
+    if H_det == 0:
+        return f(0.0), f(0.0), f(f(coeff6) / f(18.0))
+    if not (H_det > 0 and coeff1 < 0):
+        tmp_max = coeff3 + coeff4 + coeff5
+        dx, dy = f(1.0), f(1.0)
+        t = -coeff3 + coeff4 - coeff5
+        if t > tmp_max:
+            tmp_max, dx, dy = t, f(-1.0), f(1.0)
+        t = coeff3 - coeff4 - coeff5
+        if t > tmp_max:
+            tmp_max, dx, dy = t, f(1.0), f(-1.0)
+        t = -coeff3 - coeff4 + coeff5
+        if t > tmp_max:
+            tmp_max, dx, dy = t, f(-1.0), f(-1.0)
+        return dx, dy, f(f(tmp_max + coeff1 + coeff2 + coeff6) / f(18.0))
+    dx = f(f(2 * coeff2 * coeff3 - coeff4 * coeff5) / f(-H_det))
+    dy = f(f(2 * coeff1 * coeff4 - coeff3 * coeff5) / f(-H_det))
+    tx, tx_, ty, ty_ = dx > 1.0, dx < -1.0 and not dx > 1.0, dy > 1.0, dy < -1.0
+    if tx or tx_ or ty or ty_:
+        dx1 = dx2 = dy1 = dy2 = f(0.0)
+        if tx:
+            dx1 = f(1.0)
+            dy1 = f(-f(coeff4 + coeff5) / f(2 * coeff2))
+        elif tx_:
+            dx1 = f(-1.0)
+            dy1 = f(-f(coeff4 - coeff5) / f(2 * coeff2))
+        dy1 = f(min(max(dy1, f(-1.0)), f(1.0)))
+        if ty:
+            dy2 = f(1.0)
+            dx2 = f(-f(coeff3 + coeff5) / f(2 * coeff1))
+        elif ty_:
+            dy2 = f(-1.0)
+            dx2 = f(-f(coeff3 - coeff5) / f(2 * coeff1))
+        dx2 = f(min(max(dx2, f(-1.0)), f(1.0)))
+        m1, m2 = quad(dx1, dy1), quad(dx2, dy2)
+        if m1 > m2:
+            return dx1, dx1, m1
+        return dx2, dx2, m2
+    return dx, dy, quad(dx, dy)
+
+
+def detect(img, threshold: int = 60, octaves: int = 6):
+    """-> keypoints [n][5] (x, y, size, response, octave) float32, in layer
+    order, row-major within a layer (the order BRISK emits them)."""
+    f = np.float32
+    L = pyramid(img, octaves)
+    R = [fast_score(l[0]) for l in L]
+    S = [np.where(r >= threshold, r, 0) for r in R]
+    out = []
+    for i, (li, sc, off) in enumerate(L):
+        h, w = li.shape
+        ys, xs = np.nonzero(S[i])
+        for y, x in zip(ys.tolist(), xs.tolist()):
+            if not _is_max2d(S[i], x, y):
+                continue
+            c = S[i][y, x]
+            ok = True
+            for j in (i - 1, i + 1):
+                if j < 0 or j >= len(L):
+                    continue
+                _, scj, offj = L[j]
+                hj, wj = S[j].shape
+                X = f(f(f(x) * sc) + off)
+                Y = f(f(f(y) * sc) + off)
+                xj = int(f(f(f(X - offj) / scj) + f(0.5)))
+                yj = int(f(f(f(Y - offj) / scj) + f(0.5)))
+                x0, x1 = max(xj - 1, 0), min(xj + 1, wj - 1)
+                y0, y1 = max(yj - 1, 0), min(yj + 1, hj - 1)
+                if x0 <= x1 and y0 <= y1 and S[j][y0:y1 + 1, x0:x1 + 1].max() > c:
+                    ok = False
+                    break
+            if not ok:
+                continue
+            dx, dy, mx = subpixel2d(R[i][y - 1:y + 2, x - 1:x + 2])
+            kx = f(f(f(f(x) + dx) * sc) + off)
+            ky = f(f(f(f(y) + dy) * sc) + off)
+            out.append((kx, ky, f(f(BASIC_SIZE) * sc), mx, f(i)))
+    return np.array(out, np.float32).reshape(-1, 5)

@@ -31,3 +31,22 @@ def describe(img, keypoints, device: int = 0):
                                    ptr(desc), ctypes.byref(m)), "sfm_brisk_describe")
     k = m.value
     return kept[:k].copy(), ang[:k].copy(), desc[:k].copy()
+
+
+def detect(img, threshold: int = 60, octaves: int = 6, describe: bool = True, device: int = 0):
+    """CTracker::detectFeatures: BriskFeatureDetector(threshold, octaves,
+    true) + the descriptor.  -> (keypoints [n][5] (x, y, size, angle,
+    response) float32, layer [n], descriptors uint8 [n][64] or None)."""
+    im = np.ascontiguousarray(img, np.uint8)
+    if im.ndim != 2:
+        raise ValueError("img must be 2-D 8-bit grey")
+    cap = max(1024, im.shape[0] * im.shape[1] // 64)
+    kps = np.zeros((cap, 5), np.float32)
+    lay = np.zeros(cap, np.int32)
+    desc = np.zeros((cap, DESC_BYTES), np.uint8) if describe else None
+    n = ctypes.c_int32()
+    check(lib().sfm_brisk_detect_describe(device, ptr(im), im.shape[1], im.shape[0], int(threshold), int(octaves), cap,
+                                          ptr(kps), ptr(lay), ptr(desc) if describe else None, ctypes.byref(n)),
+          "sfm_brisk_detect_describe")
+    k = n.value
+    return kps[:k].copy(), lay[:k].copy(), (desc[:k].copy() if describe else None)

@@ -282,6 +282,269 @@ __global__ __launch_bounds__(64) void k_brisk_describe(const uint8_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Detector (BriskScaleSpace): layers c_i / d_i, FAST 9-16 scores, 2-D
+// maxima with isMax2D's tie-break, the scale test against the adjacent
+// layers, subpixel2D (see oracle/brisk_oracle.py for the simplifications).
+constexpr int kMaxLayers = 16;
+__constant__ int2 kCircle[16] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                                 {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+struct Layer {
+  const uint8_t* img;
+  const uint8_t* R;  // scores (cornerScore when >= 1, else 0)
+  int w, h;
+  float scale, offset;
+};
+struct Layers {
+  Layer l[kMaxLayers];
+  int n;
+};
+
+__global__ void k_halfsample(const uint8_t* __restrict__ src, int sw, uint8_t* __restrict__ dst, int dw, int dh) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= dw || y >= dh) return;
+  const uint8_t* a = src + size_t(2 * y) * sw + 2 * x;
+  dst[size_t(y) * dw + x] = uint8_t((int(a[0]) + a[1] + a[sw] + a[sw + 1] + 2) >> 2);
+}
+__global__ void k_twothirdsample(const uint8_t* __restrict__ src, int sw, uint8_t* __restrict__ dst, int dw, int dh) {
+  const int bx = blockIdx.x * blockDim.x + threadIdx.x, by = blockIdx.y;  // 3x3 block -> 2x2
+  if (2 * bx >= dw || 2 * by >= dh) return;
+  const uint8_t* a = src + size_t(3 * by) * sw + 3 * bx;
+  const int p00 = a[0], p01 = a[1], p02 = a[2], p10 = a[sw], p11 = a[sw + 1], p12 = a[sw + 2];
+  const int p20 = a[2 * sw], p21 = a[2 * sw + 1], p22 = a[2 * sw + 2];
+  uint8_t* o = dst + size_t(2 * by) * dw + 2 * bx;
+  o[0] = uint8_t((4 * p00 + 2 * p01 + 2 * p10 + p11 + 4) / 9);
+  o[1] = uint8_t((4 * p02 + 2 * p01 + 2 * p12 + p11 + 4) / 9);
+  o[dw] = uint8_t((4 * p20 + 2 * p10 + 2 * p21 + p11 + 4) / 9);
+  o[dw + 1] = uint8_t((4 * p22 + 2 * p12 + 2 * p21 + p11 + 4) / 9);
+}
+
+// cornerScore<16>(p, 0) = max(0, darkest / brightest 9-arc contrast) - 1,
+// kept when >= 1 (getAgastScore(x, y, 1)); 0 within 3 pixels of the border
+__global__ void k_fast_score(const uint8_t* __restrict__ img, int w, int h, uint8_t* __restrict__ R) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  int out = 0;
+  if (x >= 3 && y >= 3 && x < w - 3 && y < h - 3) {
+    const int v = img[size_t(y) * w + x];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - int(img[size_t(y + kCircle[k].y) * w + x + kCircle[k].x]);
+    int dark = -1000000, bright = -1000000;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      int mn = 1000000, mx = -1000000;
+#pragma unroll
+      for (int m = 0; m < 9; ++m) {
+        mn = min(mn, d[(s + m) & 15]);
+        mx = max(mx, d[(s + m) & 15]);
+      }
+      dark = max(dark, mn);
+      bright = max(bright, -mx);
+    }
+    const int sc = max(max(dark, bright), 0) - 1;
+    out = sc >= 1 ? sc : 0;
+  }
+  R[size_t(y) * w + x] = uint8_t(out);
+}
+
+__device__ __forceinline__ int s_at(const Layer& L, int x, int y, int thr) {
+  if (x < 0 || y < 0 || x >= L.w || y >= L.h) return 0;
+  const int r = L.R[size_t(y) * L.w + x];
+  return r >= thr ? r : 0;
+}
+
+// BriskScaleSpace::subpixel2D (float step for step; the reference's
+// delta_y = delta_x1 / _x2 in the clamped branch kept)
+__device__ float subpixel2d(const int s[3][3], float& dx_out, float& dy_out) {
+  const int s_0_0 = s[0][0], s_0_1 = s[0][1], s_0_2 = s[0][2], s_1_0 = s[1][0], s_1_1 = s[1][1], s_1_2 = s[1][2];
+  const int s_2_0 = s[2][0], s_2_1 = s[2][1], s_2_2 = s[2][2];
+  const int tmp1 = s_0_0 + s_0_2 - 2 * s_1_1 + s_2_0 + s_2_2;
+  const int coeff1 = 3 * (tmp1 + s_0_1 - ((s_1_0 + s_1_2) << 1) + s_2_1);
+  const int coeff2 = 3 * (tmp1 - ((s_0_1 + s_2_1) << 1) + s_1_0 + s_1_2);
+  const int tmp2 = s_0_2 - s_2_0;
+  const int tmp3 = s_0_0 + tmp2 - s_2_2;
+  const int tmp4 = tmp3 - 2 * tmp2;
+  const int coeff3 = -3 * (tmp3 + s_0_1 - s_2_1);
+  const int coeff4 = -3 * (tmp4 + s_1_0 - s_1_2);
+  const int coeff5 = (s_0_0 - s_0_2 - s_2_0 + s_2_2) << 2;
+  const int coeff6 = -((s_0_0 + s_0_2 - ((s_1_0 + s_0_1 + s_1_2 + s_2_1) << 1) - 5 * s_1_1 + s_2_0 + s_2_2) << 1);
+  const int H_det = 4 * coeff1 * coeff2 - coeff5 * coeff5;
+  auto quad = [&](float dx, float dy) {
+    return (coeff1 * dx * dx + coeff2 * dy * dy + coeff3 * dx + coeff4 * dy + coeff5 * dx * dy + coeff6) / 18.0f;
+  };
+  if (H_det == 0) {
+    dx_out = 0.0f;
+    dy_out = 0.0f;
+    return float(coeff6) / 18.0f;
+  }
+  if (!(H_det > 0 && coeff1 < 0)) {
+    int tmp_max = coeff3 + coeff4 + coeff5;
+    float dx = 1.0f, dy = 1.0f;
+    int t = -coeff3 + coeff4 - coeff5;
+    if (t > tmp_max) { tmp_max = t; dx = -1.0f; dy = 1.0f; }
+    t = coeff3 - coeff4 - coeff5;
+    if (t > tmp_max) { tmp_max = t; dx = 1.0f; dy = -1.0f; }
+    t = -coeff3 - coeff4 + coeff5;
+    if (t > tmp_max) { tmp_max = t; dx = -1.0f; dy = -1.0f; }
+    dx_out = dx;
+    dy_out = dy;
+    return float(tmp_max + coeff1 + coeff2 + coeff6) / 18.0f;
+  }
+  float dx = float(2 * coeff2 * coeff3 - coeff4 * coeff5) / float(-H_det);
+  float dy = float(2 * coeff1 * coeff4 - coeff3 * coeff5) / float(-H_det);
+  bool tx = false, tx_ = false, ty = false, ty_ = false;
+  if (dx > 1.0f) tx = true;
+  else if (dx < -1.0f) tx_ = true;
+  if (dy > 1.0f) ty = true;
+  if (dy < -1.0f) ty_ = true;
+  if (tx || tx_ || ty || ty_) {
+    float dx1 = 0.0f, dx2 = 0.0f, dy1 = 0.0f, dy2 = 0.0f;
+    if (tx) {
+      dx1 = 1.0f;
+      dy1 = -float(coeff4 + coeff5) / float(2 * coeff2);
+    } else if (tx_) {
+      dx1 = -1.0f;
+      dy1 = -float(coeff4 - coeff5) / float(2 * coeff2);
+    }
+    dy1 = fminf(fmaxf(dy1, -1.0f), 1.0f);
+    if (ty) {
+      dy2 = 1.0f;
+      dx2 = -float(coeff3 + coeff5) / float(2 * coeff1);
+    } else if (ty_) {
+      dy2 = -1.0f;
+      dx2 = -float(coeff3 - coeff5) / float(2 * coeff1);
+    }
+    dx2 = fminf(fmaxf(dx2, -1.0f), 1.0f);
+    const float m1 = quad(dx1, dy1), m2 = quad(dx2, dy2);
+    if (m1 > m2) {
+      dx_out = dx1;
+      dy_out = dx1;
+      return m1;
+    }
+    dx_out = dx2;
+    dy_out = dx2;
+    return m2;
+  }
+  dx_out = dx;
+  dy_out = dy;
+  return quad(dx, dy);
+}
+
+struct Cand {
+  unsigned long long key;  // layer << 42 | y << 21 | x: BRISK's emission order
+  float x, y, size, response;
+  int layer, pad;
+};
+
+__global__ void k_detect_layer(Layers LS, int i, int thr, Cand* __restrict__ out, int cap, int* __restrict__ count) {
+  const Layer& L = LS.l[i];
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= L.w || y >= L.h) return;
+  const int c = s_at(L, x, y, thr);
+  if (c == 0) return;
+  // isMax2D
+  int eq = 0;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      if (!dx && !dy) continue;
+      const int v = s_at(L, x + dx, y + dy, thr);
+      if (v > c) return;
+      if (v == c) eq |= 1 << ((dy + 1) * 3 + dx + 1);
+    }
+  if (eq) {
+    auto smooth = [&](int cx, int cy) {
+      return s_at(L, cx - 1, cy - 1, thr) + 2 * s_at(L, cx, cy - 1, thr) + s_at(L, cx + 1, cy - 1, thr) +
+             2 * s_at(L, cx - 1, cy, thr) + 4 * s_at(L, cx, cy, thr) + 2 * s_at(L, cx + 1, cy, thr) +
+             s_at(L, cx - 1, cy + 1, thr) + 2 * s_at(L, cx, cy + 1, thr) + s_at(L, cx + 1, cy + 1, thr);
+    };
+    const int sc = smooth(x, y);
+    for (int b = 0; b < 9; ++b)
+      if ((eq >> b) & 1)
+        if (smooth(x + b % 3 - 1, y + b / 3 - 1) > sc) return;
+  }
+  // scale test against the adjacent layers (nearest sample, 3x3 max)
+  for (int j = i - 1; j <= i + 1; j += 2) {
+    if (j < 0 || j >= LS.n) continue;
+    const Layer& M = LS.l[j];
+    const float X = float(x) * L.scale + L.offset, Y = float(y) * L.scale + L.offset;
+    const int xj = int((X - M.offset) / M.scale + 0.5f), yj = int((Y - M.offset) / M.scale + 0.5f);
+    const int x0 = max(xj - 1, 0), x1 = min(xj + 1, M.w - 1), y0 = max(yj - 1, 0), y1 = min(yj + 1, M.h - 1);
+    for (int yy = y0; yy <= y1; ++yy)
+      for (int xx = x0; xx <= x1; ++xx)
+        if (s_at(M, xx, yy, thr) > c) return;
+  }
+  int s3[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) s3[r][q] = L.R[size_t(y - 1 + r) * L.w + x - 1 + q];
+  float ddx, ddy;
+  const float mx = subpixel2d(s3, ddx, ddy);
+  const int k = atomicAdd(count, 1);
+  if (k >= cap) return;
+  Cand cd;
+  cd.key = (static_cast<unsigned long long>(i) << 42) | (static_cast<unsigned long long>(y) << 21) |
+           static_cast<unsigned long long>(x);
+  cd.x = (float(x) + ddx) * L.scale + L.offset;
+  cd.y = (float(y) + ddy) * L.scale + L.offset;
+  cd.size = kBasicSize * L.scale;
+  cd.response = mx;
+  cd.layer = i;
+  cd.pad = 0;
+  out[k] = cd;
+}
+
+__global__ void k_gather_cands(const Cand* __restrict__ c, const int32_t* __restrict__ order, int n,
+                               float* __restrict__ kps3, float* __restrict__ resp, int32_t* __restrict__ layer) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const Cand& q = c[order[k]];
+  kps3[3 * k] = q.x;
+  kps3[3 * k + 1] = q.y;
+  kps3[3 * k + 2] = q.size;
+  resp[k] = q.response;
+  layer[k] = q.layer;
+}
+__global__ void k_cand_keys(const Cand* __restrict__ c, int n, unsigned long long* __restrict__ key,
+                            int32_t* __restrict__ idx) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  key[k] = c[k].key;
+  idx[k] = k;
+}
+
+// grow-only per-device workspace of the detector (one frame per call)
+struct BriskWork {
+  std::vector<std::pair<void*, size_t>> buf;
+  void* get(int slot, size_t bytes, int* rc) {
+    if (int(buf.size()) <= slot) buf.resize(slot + 1, {nullptr, 0});
+    auto& e = buf[slot];
+    if (e.second < bytes) {
+      if (e.first) (void)hipFree(e.first);
+      e = {nullptr, 0};
+      if (hipMalloc(&e.first, std::max<size_t>(bytes, 256)) != hipSuccess) {
+        *rc = bfail(SFM_ENOMEM, "hipMalloc failed (detector workspace)");
+        return nullptr;
+      }
+      e.second = std::max<size_t>(bytes, 256);
+    }
+    return e.first;
+  }
+};
+BriskWork* work_for(int device) {
+  static std::vector<BriskWork*> w(64, nullptr);
+  if (!w[device]) w[device] = new BriskWork;
+  return w[device];
+}
+std::mutex& work_mutex() {
+  static std::mutex m;
+  return m;
+}
+
 }  // namespace
 }  // namespace sfm
 
@@ -337,4 +600,125 @@ extern "C" int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w,
   for (void* p : {(void*)d_img, (void*)d_ii, (void*)d_kps, (void*)d_keep, (void*)d_ang, (void*)d_desc})
     if (p) (void)hipFree(p);
   return ok ? 0 : bfail(SFM_EIO, "allocation, kernel or copy failed");
+}
+
+extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, int32_t threshold,
+                                         int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
+                                         uint8_t* desc, int32_t* n_out) {
+  if (!n_out) return bfail(SFM_EINVAL, "n_out is NULL");
+  *n_out = 0;
+  if (w < 8 || h < 8 || threshold < 1 || threshold > 255 || octaves < 0 || 2 * octaves > kMaxLayers || capacity < 0)
+    return bfail(SFM_EINVAL, "bad sizes (w, h >= 8; threshold 1..255; octaves 0..8)");
+  if (!img || (capacity && (!kps || !octave))) return bfail(SFM_EINVAL, "NULL argument");
+  if (hipSetDevice(device) != hipSuccess) return bfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  DevPattern* P = nullptr;
+  if (desc && !(P = device_pattern(device, &rc))) return rc;
+  std::lock_guard<std::mutex> lock(work_mutex());
+  BriskWork* W = work_for(device);
+  // layer geometry (BriskScaleSpace::constructPyramid)
+  const int nl = std::max(1, 2 * octaves);
+  int lw[kMaxLayers], lh[kMaxLayers];
+  float lsc[kMaxLayers], loff[kMaxLayers];
+  size_t loff_px[kMaxLayers + 1];
+  lw[0] = w; lh[0] = h; lsc[0] = 1.0f; loff[0] = 0.0f;
+  int nuse = 1;
+  for (int i = 1; i < nl; ++i) {
+    if (i == 1) { lw[1] = 2 * (w / 3); lh[1] = 2 * (h / 3); lsc[1] = 1.5f; }
+    else { lw[i] = lw[i - 2] / 2; lh[i] = lh[i - 2] / 2; lsc[i] = lsc[i - 2] * 2.0f; }
+    loff[i] = 0.5f * lsc[i] - 0.5f;
+    nuse = i + 1;
+  }
+  loff_px[0] = 0;
+  for (int i = 0; i < nuse; ++i) loff_px[i + 1] = loff_px[i] + size_t(lw[i]) * lh[i];
+  const size_t total = loff_px[nuse];
+  auto* limg = static_cast<uint8_t*>(W->get(0, total, &rc));
+  auto* lR = static_cast<uint8_t*>(W->get(1, total, &rc));
+  const int cap_c = int(std::min<size_t>(size_t(w) * h / 4 + 1024, size_t(1) << 22));
+  auto* cand = static_cast<Cand*>(W->get(2, sizeof(Cand) * size_t(cap_c), &rc));
+  auto* cnt = static_cast<int32_t*>(W->get(3, sizeof(int32_t), &rc));
+  if (rc) return rc;
+  if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess) return bfail(SFM_EIO, "upload failed");
+  for (int i = 1; i < nuse; ++i) {
+    if (lw[i] < 1 || lh[i] < 1) continue;
+    if (i == 1) {
+      dim3 g(unsigned((lw[1] / 2 + 127) / 128), unsigned(lh[1] / 2));
+      k_twothirdsample<<<g, 128>>>(limg, w, limg + loff_px[1], lw[1], lh[1]);
+    } else {
+      dim3 g(unsigned((lw[i] + 255) / 256), unsigned(lh[i]));
+      k_halfsample<<<g, 256>>>(limg + loff_px[i - 2], lw[i - 2], limg + loff_px[i], lw[i], lh[i]);
+    }
+  }
+  Layers LS;
+  LS.n = nuse;
+  for (int i = 0; i < nuse; ++i) {
+    if (lw[i] >= 1 && lh[i] >= 1) {
+      dim3 g(unsigned((lw[i] + 255) / 256), unsigned(lh[i]));
+      k_fast_score<<<g, 256>>>(limg + loff_px[i], lw[i], lh[i], lR + loff_px[i]);
+    }
+    LS.l[i] = Layer{limg + loff_px[i], lR + loff_px[i], lw[i], lh[i], lsc[i], loff[i]};
+  }
+  (void)hipMemset(cnt, 0, sizeof(int32_t));
+  for (int i = 0; i < nuse; ++i) {
+    if (lw[i] < 1 || lh[i] < 1) continue;
+    dim3 g(unsigned((lw[i] + 255) / 256), unsigned(lh[i]));
+    k_detect_layer<<<g, 256>>>(LS, i, threshold, cand, cap_c, cnt);
+  }
+  int32_t n = 0;
+  if (hipMemcpy(&n, cnt, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return bfail(SFM_EIO, "kernel failed");
+  if (n > cap_c) return bfail(SFM_EIO, "candidate buffer overflow");
+  if (n == 0) return 0;
+  // BRISK's order: layer, then row-major (stable radix sort on the key)
+  auto* key = static_cast<unsigned long long*>(W->get(4, sizeof(unsigned long long) * 2 * size_t(n), &rc));
+  auto* idx = static_cast<int32_t*>(W->get(5, sizeof(int32_t) * 2 * size_t(n), &rc));
+  auto* kp3 = static_cast<float*>(W->get(6, sizeof(float) * 3 * size_t(n), &rc));
+  auto* resp = static_cast<float*>(W->get(7, sizeof(float) * size_t(n), &rc));
+  auto* lay = static_cast<int32_t*>(W->get(8, sizeof(int32_t) * size_t(n), &rc));
+  if (rc) return rc;
+  k_cand_keys<<<(n + 255) / 256, 256>>>(cand, n, key, idx);
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key + n, idx, idx + n, n, 0, 46);
+  void* tmp = W->get(9, tb, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key + n, idx, idx + n, n, 0, 46) != hipSuccess)
+    return bfail(SFM_EIO, "sort failed");
+  k_gather_cands<<<(n + 255) / 256, 256>>>(cand, idx + n, n, kp3, resp, lay);
+  std::vector<float> hk(3 * size_t(n)), hr(n);
+  std::vector<int32_t> hl(n), hkeep(n, 1);
+  std::vector<float> hang(n, -1.0f);
+  std::vector<uint8_t> hd;
+  if (desc) {
+    const int n_bytes = ((P->n_short + 127) / 128) * 16;
+    auto* keep = static_cast<int32_t*>(W->get(10, sizeof(int32_t) * size_t(n), &rc));
+    auto* ang = static_cast<float*>(W->get(11, sizeof(float) * size_t(n), &rc));
+    auto* ii = static_cast<int32_t*>(W->get(12, sizeof(int32_t) * size_t(w + 1) * (h + 1), &rc));
+    auto* dd = static_cast<uint8_t*>(W->get(13, size_t(n) * n_bytes, &rc));
+    if (rc) return rc;
+    k_integral_rows<<<(h + 1 + 255) / 256, 256>>>(limg, w, h, ii);
+    k_integral_cols<<<(w + 1 + 255) / 256, 256>>>(w, h, ii);
+    k_brisk_describe<<<n, 64>>>(limg, w, h, ii, *P, kp3, n, keep, ang, dd);
+    hd.resize(size_t(n) * n_bytes);
+    if (hipMemcpy(hkeep.data(), keep, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hang.data(), ang, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hd.data(), dd, hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return bfail(SFM_EIO, "download failed");
+  }
+  if (hipMemcpy(hk.data(), kp3, sizeof(float) * 3 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(hr.data(), resp, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(hl.data(), lay, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess)
+    return bfail(SFM_EIO, "download failed");
+  int m = 0;
+  for (int k = 0; k < n; ++k) {
+    if (!hkeep[k]) continue;
+    if (m < capacity) {
+      float* o = kps + 5 * size_t(m);
+      o[0] = hk[3 * k]; o[1] = hk[3 * k + 1]; o[2] = hk[3 * k + 2]; o[3] = hang[k]; o[4] = hr[k];
+      octave[m] = hl[k];
+      if (desc) std::memcpy(desc + size_t(m) * 64, hd.data() + size_t(k) * 64, 64);
+    }
+    ++m;
+  }
+  *n_out = m;
+  if (m > capacity) return bfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(m));
+  return 0;
 }

@@ -62,3 +62,31 @@ def test_bad_keypoints_are_rejected():
         brisk.describe(img, [[10.0, 10.0, -1.0]])
     k, a, d = brisk.describe(img, np.zeros((0, 3)))
     assert len(k) == 0
+
+
+@pytest.mark.parametrize("frame,thr", [(0, 60), (5, 60), (9, 30)])
+def test_detector_matches_restatement(frame, thr):
+    """Same keypoints in BRISK's order (layer, row-major): layer, response
+    and position bit-equal (float32 step for step)."""
+    from sfm_amd import brisk
+    img = _frame(frame)
+    kp, lay, _ = brisk.detect(img, threshold=thr, describe=False)
+    ok = B.detect(img, threshold=thr)
+    assert len(kp) == len(ok) and len(kp) > 500
+    assert lay.tolist() == ok[:, 4].astype(int).tolist()
+    np.testing.assert_array_equal(kp[:, [0, 1, 2, 4]], ok[:, [0, 1, 2, 3]])
+    assert (kp[:, 3] == -1).all()
+
+
+def test_detect_describe_end_to_end(pattern):
+    """detectFeatures as the reference runs it: the descriptor's border rule
+    drops keypoints; the kept ones carry the restatement's descriptors."""
+    from sfm_amd import brisk
+    img = _frame(2)
+    kp, lay, desc = brisk.detect(img)
+    ok = B.detect(img)
+    kept, oang, odesc = B.describe(img, ok[:, :3], pattern)
+    assert len(kp) == len(kept) > 300
+    np.testing.assert_array_equal(kp[:, :3], ok[kept, :3])
+    np.testing.assert_array_equal(kp[:, 3], oang)
+    assert (desc == odesc).all()
