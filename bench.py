@@ -348,6 +348,34 @@ def live_path_leg(device: int, cpu: bool, n_frames: int = 300) -> dict:
     return out
 
 
+def brisk_leg(device: int, cpu: bool, n_frames: int = 20) -> dict:
+    """CTracker::detectFeatures on the device (sfm_brisk_detect_describe:
+    BRISK threshold 60, 6 octaves, 64-B descriptors) on rendered 1280x720
+    frames of the synthetic video (rendered before the timed region)."""
+    from sfm_amd import brisk
+    from sfm_amd.video import SyntheticVideo
+    v = SyntheticVideo(speed=2.0)
+    frames = [v.frame(k) for k in range(n_frames)]
+    brisk.detect(frames[0])  # pattern upload, workspace
+    t0 = time.perf_counter()
+    nk = 0
+    for f in frames:
+        kp, _, _ = brisk.detect(f)
+        nk += len(kp)
+    wall = time.perf_counter() - t0
+    out = {"workload": f"BRISK detect + describe (threshold 60, 6 octaves) on {n_frames} rendered 1280x720 frames, "
+                       "host image in, keypoints + 64-B descriptors out",
+           "ms_per_frame": wall / n_frames * 1e3, "keypoints_per_frame": nk / n_frames, "cpu_baseline": None}
+    if cpu:
+        from oracle import brisk_oracle as B
+        t0 = time.perf_counter()
+        B.detect(frames[0])
+        out["cpu_baseline"] = {"detect_ms_one_frame": (time.perf_counter() - t0) * 1e3, "cores": 1, "kind": "port",
+                               "sample": "detection only on one frame by oracle/brisk_oracle.py (numpy restatement: "
+                                         "not a speed reference for the reference's C++ library)"}
+    return out
+
+
 def oneshot_leg(sc, reps: int = 3) -> dict:
     """One-shot C3 solve as the drop-in is called: host arrays in,
     sfm_ba_solve (problem setup + upload + LM + download) -- the reference
@@ -660,6 +688,7 @@ def main() -> int:
         out["pnp"] = pnp_leg(local_rank, not args.no_cpu_baseline)
         out["c5_pipeline"] = c5_pipeline_leg(local_rank, not args.no_cpu_baseline)
         out["live_path"] = live_path_leg(local_rank, not args.no_cpu_baseline)
+        out["brisk"] = brisk_leg(local_rank, not args.no_cpu_baseline)
     if args.phases and rank == 0:
         print(json.dumps(phases, indent=1), file=sys.stderr)
     if rank == 0:

@@ -109,6 +109,30 @@ class KeypointStream:
         return pts[perm], desc[perm], lid[perm]
 
 
+class BriskVideoStream:
+    """Detector output of the device BRISK (sfm_brisk_detect_describe,
+    row T8) on the rendered synthetic video (sfm_amd.video: a textured plane
+    at depth 10, ~2.6 px of motion per frame at speed 2), with the video's
+    closed-form poses: the live loop on real detections."""
+
+    def __init__(self, video=None, threshold: int = 60, octaves: int = 6, device: int = 0, depth: float = 10.0):
+        from .video import SyntheticVideo
+        self.video = video if video is not None else SyntheticVideo(speed=2.0)
+        self.threshold, self.octaves, self.device, self.depth = int(threshold), int(octaves), device, float(depth)
+        c = self.video.c
+        self.K = np.array([[F_PIX, 0.0, c[0]], [0.0, F_PIX, c[1]], [0.0, 0.0, 1.0]])
+        self.desc_bytes = 64
+
+    def pose(self, k: int):
+        from .mapping import video_gt_pose
+        return video_gt_pose(self.video, k, self.depth)
+
+    def frame(self, k: int):
+        from . import brisk
+        kp, _, desc = brisk.detect(self.video.frame(k), self.threshold, self.octaves, device=self.device)
+        return kp[:, :2].astype(np.float64), desc, np.full(len(kp), -1)
+
+
 class _Frame:
     """CFrame: keypoints (undistorted), descriptors, 3D index per keypoint
     (-1: unmatched), pose."""

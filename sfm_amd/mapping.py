@@ -62,6 +62,20 @@ def triangulate_points(cam0, cam1, uv0, uv1, P, device: int = 0) -> np.ndarray:
     return X[:n].copy()
 
 
+def video_gt_pose(video, k: int, depth: float = 10.0):
+    """(rvec, t) of frame k of sfm_amd.video.SyntheticVideo relative to frame 0:
+    a pinhole camera rolling about its optical axis and translating over the
+    textured plane at `depth` (closed form of the video's similarity)."""
+    s0, th0, t0 = video.pose(0)
+    sk, thk, tk = video.pose(k)
+    s, th = sk / s0, thk - th0
+    B = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+    d = tk - B @ t0
+    tz = depth / s - depth
+    t = np.array([d[0] * depth / (s * F_PIX), d[1] * depth / (s * F_PIX), tz])
+    return np.array([0.0, 0.0, th]), t
+
+
 def _rodrigues(r):
     r = np.asarray(r, np.float64)
     th = float(np.sqrt(r @ r))
@@ -109,14 +123,7 @@ class IncrementalMapper:
 
     # ---- ground truth of the synthetic video --------------------------------
     def gt_pose(self, k: int):
-        s0, th0, t0 = self.video.pose(0)
-        sk, thk, tk = self.video.pose(k)
-        s, th = sk / s0, thk - th0
-        B = s * np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
-        d = tk - B @ t0
-        tz = self.depth / s - self.depth
-        t = np.array([d[0] * self.depth / (s * F_PIX), d[1] * self.depth / (s * F_PIX), tz])
-        return np.array([0.0, 0.0, th]), t
+        return video_gt_pose(self.video, k, self.depth)
 
     # ---- per frame ----------------------------------------------------------------
     def process_frame(self, grey: np.ndarray) -> None:

@@ -114,3 +114,38 @@ def test_associations_and_geometry_match_ground_truth(run80):
     dm = np.linalg.norm(np.diff(sc * C @ R.T, axis=0), axis=1)
     dg = np.linalg.norm(np.diff(Cg, axis=0), axis=1)
     assert np.max(np.abs(dm - dg) / dg) < 0.05
+
+
+@pytest.fixture(scope="module")
+def run_brisk():
+    from sfm_amd.live import BriskVideoStream
+    st = BriskVideoStream()
+    s = LiveSfM(st)
+    s.run(40)
+    yield s
+    s.close()
+
+
+def test_live_path_on_device_brisk_detections(run_brisk):
+    """The live loop fed by the device BRISK (row T8) on the rendered video:
+    every frame tracked, keyframes every 10 frames, each keyframe BA equal to
+    the oracle's, keyframe-to-keyframe motion within 10% of the ground truth
+    (Sim(3) alignment on the keyframe centres)."""
+    s = run_brisk
+    st = s.stream
+    assert s.lost == 0 and s.stats["tracked"] == 40 - 5 - 1
+    assert [f.no for f in s.kfs][:4] == [0, 5, 15, 25]
+    assert s.map.size()[0] > 1000
+    for rec in s.ba_log:
+        r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
+        sm_o, _ = O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], r, t, X)
+        assert rec["summary"].num_iterations == sm_o["num_iterations"]
+        assert abs(rec["summary"].final_cost - sm_o["final_cost"]) <= 1e-9 * max(sm_o["final_cost"], 1e-300)
+        assert _rel(rec["X_out"], X) < 1e-6
+    C = np.array([-_rodrigues(f.rot).T @ f.t for f in s.kfs])
+    Cg = np.array([-_rodrigues(st.pose(f.no)[0]).T @ st.pose(f.no)[1] for f in s.kfs])
+    sc, R, t = _umeyama(C, Cg)
+    dm = np.linalg.norm(np.diff(sc * C @ R.T, axis=0), axis=1)
+    dg = np.linalg.norm(np.diff(Cg, axis=0), axis=1)
+    print("brisk live: kf motion rel err", np.abs(dm - dg) / dg)
+    assert np.max(np.abs(dm - dg) / dg) < 0.1
