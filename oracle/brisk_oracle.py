@@ -318,7 +318,8 @@ def _is_max2d(S, x, y):
 
 
 def subpixel2d(s):
-    """BriskScaleSpace::subpixel2D on the 3x3 scores s[row][col] -> (dx, dy,
+    """BriskScaleSpace::subpixel2D on the 3x3 scores s[i][j] = score at
+    (x + i - 1, y + j - 1) (the reference's s_i_j: i along x) -> (dx, dy,
     max), float32 step for step (the reference's delta_y = delta_x1 / _x2
     assignment in the clamped branch included)."""
     f = np.float32
@@ -419,7 +420,8 @@ def detect(img, threshold: int = 60, octaves: int = 6):
                     break
             if not ok:
                 continue
-            dx, dy, mx = subpixel2d(R[i][y - 1:y + 2, x - 1:x + 2])
+            # s_i_j of subpixel2D is the score at (x + i - 1, y + j - 1)
+            dx, dy, mx = subpixel2d(R[i][y - 1:y + 2, x - 1:x + 2].T)
             kx = f(f(f(f(x) + dx) * sc) + off)
             ky = f(f(f(f(y) + dy) * sc) + off)
             out.append((kx, ky, f(f(BASIC_SIZE) * sc), mx, f(i)))

@@ -477,11 +477,11 @@ __global__ void k_detect_layer(Layers LS, int i, int thr, Cand* __restrict__ out
       for (int xx = x0; xx <= x1; ++xx)
         if (s_at(M, xx, yy, thr) > c) return;
   }
-  int s3[3][3];
+  int s3[3][3];  // s_i_j of subpixel2D: the score at (x + i - 1, y + j - 1)
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) s3[r][q] = L.R[size_t(y - 1 + r) * L.w + x - 1 + q];
+    for (int q = 0; q < 3; ++q) s3[q][r] = L.R[size_t(y - 1 + r) * L.w + x - 1 + q];
   float ddx, ddy;
   const float mx = subpixel2d(s3, ddx, ddy);
   const int k = atomicAdd(count, 1);
