@@ -123,6 +123,13 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 #pragma unroll
       for (int j = 0; j < 16; ++j) p[j] = wl ? ((j == r) ? 1.0 : 0.0) : T[(g0 + j) * TS + r];
       double d = bcast(p[0], g0);
+      // column j's LDS-fed updates (p[c], c >= j + 2) are applied one step
+      // late, right before they are first needed, so the LDS round trip
+      // overlaps the next pivot's rsqrt chain; every p[c] still takes its
+      // column updates in column order (bitwise the eager form)
+      double lp = 0.0, lcp[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) lcp[c] = 0.0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int g = g0 + j;
@@ -132,17 +139,19 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         const double l = p[j] * inv;
         p[j] = l;
         T[g * TS + r] = l;
+        if (j >= 1 && j < 15) {
+#pragma unroll
+          for (int c = j + 1; c < 16; ++c) p[c] = fma(-lp, lcp[c], p[c]);  // column j - 1
+        }
         if (j < 15) {
           const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
           const double l1 = bcast(l, g + 1);
           p[j + 1] = fma(-l, l1, p[j + 1]);
           if (j < 14) {
-            double lc[16];
 #pragma unroll
-            for (int c = j + 2; c < 16; ++c) lc[c] = T[g * TS + g0 + c];
-#pragma unroll
-            for (int c = j + 2; c < 16; ++c) p[c] = fma(-l, lc[c], p[c]);
+            for (int c = j + 2; c < 16; ++c) lcp[c] = T[g * TS + g0 + c];
           }
+          lp = l;
           d = dn;
         }
       }
@@ -159,6 +168,9 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         wc[j] = (j == r) ? 1.0 : 0.0;
       }
       double d = bcast(p[0], g0);
+      double lp = 0.0, lcp[16];  // deferred LDS-fed updates, as in panels 1..3
+#pragma unroll
+      for (int c = 0; c < 16; ++c) lcp[c] = 0.0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int g = g0 + j;
@@ -169,6 +181,13 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         p[j] = l;
         T[g * TS + r] = l;
         wc[j] *= inv;
+        if (j >= 1 && j < 15) {
+#pragma unroll
+          for (int c = j + 1; c < 16; ++c) {  // column j - 1
+            p[c] = fma(-lp, lcp[c], p[c]);
+            wc[c] = fma(-lcp[c], wc[j - 1], wc[c]);
+          }
+        }
         if (j < 15) {
           // critical path by readlane only: the next pivot (lane g+1's own
           // a - l*l) and the next column's L(g+1, g) for every lane
@@ -177,15 +196,10 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
           p[j + 1] = fma(-l, l1, p[j + 1]);
           wc[j + 1] = fma(-l1, wc[j], wc[j + 1]);
           if (j < 14) {
-            double lc[16];
 #pragma unroll
-            for (int c = j + 2; c < 16; ++c) lc[c] = T[g * TS + g0 + c];
-#pragma unroll
-            for (int c = j + 2; c < 16; ++c) {
-              p[c] = fma(-l, lc[c], p[c]);
-              wc[c] = fma(-lc[c], wc[j], wc[c]);
-            }
+            for (int c = j + 2; c < 16; ++c) lcp[c] = T[g * TS + g0 + c];
           }
+          lp = l;
           d = dn;
         }
       }
