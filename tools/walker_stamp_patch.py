@@ -25,10 +25,10 @@ s = s.replace('''    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, s
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n) : potrf_tile<false>(T, Wl, scr, j0, n);
     WSTAMP(j, 2);
     if (bad) atomicOr(fail, 1);''', 1)
-s = s.replace('''    block_publish_wt(F + j * nb + j, epoch);
-    if (j + 1 == nb) break;''', '''    block_publish_wt(F + j * nb + j, epoch);
-    WSTAMP(j, 3);
-    if (j + 1 == nb) break;''', 1)
+s = s.replace('''    if (j + 1 == nb) break;
+    // subdiagonal tile''', '''    WSTAMP(j, 3);
+    if (j + 1 == nb) break;
+    // subdiagonal tile''', 1)
 s = s.replace('''    block_wait(Pf + (j + 1) * nb + j, epoch, fail);
     load_tile(T, A, ld, i0, j0);''', '''    block_wait(Pf + (j + 1) * nb + j, epoch, fail);
     WSTAMP(j, 4);
