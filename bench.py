@@ -487,6 +487,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pts-per-gpu", type=int, default=PTS_PER_GPU)
     ap.add_argument("--cams", type=int, default=CAMS)
+    ap.add_argument("--total-pts", type=int, default=0,
+                    help="strong scaling: this many points in total, split into landmark shards over the ranks "
+                         "(BASELINE config C4: --cams 2000 --total-pts 1000000); default: --pts-per-gpu per rank")
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
     ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
     ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
@@ -509,8 +512,15 @@ def main() -> int:
     import sfm_amd
     from sfm_amd import scene as S
 
-    P = args.pts_per_gpu
-    sc = S.generate(args.cams, P * world, seed=SEED, p_begin=rank * P, p_end=(rank + 1) * P)
+    strong = args.total_pts > 0
+    if strong:
+        P_total = args.total_pts
+        p_begin, p_end = rank * P_total // world, (rank + 1) * P_total // world
+    else:
+        P_total = args.pts_per_gpu * world
+        p_begin, p_end = rank * args.pts_per_gpu, (rank + 1) * args.pts_per_gpu
+    P = p_end - p_begin
+    sc = S.generate(args.cams, P_total, seed=SEED, p_begin=p_begin, p_end=p_end)
     ba = sfm_amd.BundleAdjuster(device=local_rank)
     if world > 1:
         uid = [sfm_amd.BundleAdjuster.unique_id() if rank == 0 else None]
@@ -558,8 +568,8 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    n_obs_total = sc.n_obs * world
-    n_pts_total = P * world
+    n_obs_total = sc.n_obs * world if not strong else VIEWS * P_total   # every point has VIEWS observations
+    n_pts_total = P_total
     res_only = evals - jevals   # residual-only (candidate) evaluations
     value = n_obs_total * res_only / elapsed
     jac = phases["jacobian"]
@@ -645,12 +655,14 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded object-scanning scene, SURVEY.md §8d; K from main/main.cpp:47-50)",
         "config": {
-            "workload": "C3 per GPU: full BA solve (LM + DENSE_SCHUR, Ceres default options)",
+            "workload": (f"{args.cams} cams / {P_total} points in total, landmark-sharded over the ranks (strong "
+                         "scaling): full BA solve (LM + DENSE_SCHUR, Ceres default options)") if strong else
+                        "C3 per GPU: full BA solve (LM + DENSE_SCHUR, Ceres default options)",
             "cams": sc.n_cams, "points": n_pts_total, "observations": n_obs_total,
             "points_per_gpu": sc.n_pts, "obs_per_gpu": sc.n_obs, "views_per_point": VIEWS,
             "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
