@@ -96,10 +96,60 @@ __device__ __forceinline__ void w_offdiag(const double* T, double* Wl, double* s
   for (int rr = 0; rr < 4; ++rr) Wl[(16 * J + j) * TS + 16 * I + 4 * rr + kk] = -acc2[rr];
 }
 
+// Row 3 of W in two halves, so that the sum runs during panel 3:
+// scr = sum_{K=J}^{2} L_3K W_KJ (needs only L rows 48.. of panels 0-2 and W
+// rows 0-2), then W_3J = -W_33 scr once panel 3 is out.  Same MFMA order
+// as w_offdiag(T, Wl, scr, 3, J): bitwise the same W.
+__device__ __forceinline__ void w_row3_sum(const double* T, const double* Wl, double* scr, int J, int lane) {
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int K = J; K < 3; ++K) acc = mfma16(T + (16 * K) * TS + 48, 1, TS, Wl + (16 * J) * TS + 16 * K, 1, TS, acc, lane);
+  const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) scr[(4 * rr + kk) * 16 + j] = acc[rr];
+}
+__device__ __forceinline__ void w_row3_finish(double* Wl, const double* scr, int J, int lane) {
+  f64x4 acc2 = {0.0, 0.0, 0.0, 0.0};
+  acc2 = mfma16(Wl + 48 * TS + 48, 1, TS, scr, 16, 1, acc2, lane);
+  const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) Wl[(16 * J + j) * TS + 48 + 4 * rr + kk] = -acc2[rr];
+}
+
+// The walker's last update T -= Ls Ls^T (Ls = L_j,j-1 in LDS) of the lower
+// 16x16 blocks (I, J) = (Ib[q], Jb[q]), q < nq, by one wavefront; the MFMA
+// chains of the blocks are interleaved (same k order per block as a chain).
+template <int kMax>
+__device__ __forceinline__ void last_update(double* T, const double* Ls, const int* Ib, const int* Jb, int nq, int lane) {
+  const int li = lane & 15, kk = lane >> 4;
+  f64x4 acc[kMax];
+#pragma unroll
+  for (int q = 0; q < kMax; ++q) acc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const double* row = Ls + (16 * M + 4 * s4 + kk) * TS + li;
+#pragma unroll
+      for (int q = 0; q < kMax; ++q)
+        if (q < nq) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16 * Ib[q]], row[16 * Jb[q]], acc[q], 0, 0, 0);
+    }
+#pragma unroll
+  for (int q = 0; q < kMax; ++q)
+    if (q < nq)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) T[(16 * Jb[q] + li) * TS + 16 * Ib[q] + 4 * rr + kk] -= acc[q][rr];
+}
+
 // The factorisation proper, on the tile image T in LDS (256 threads; Wl is
 // cleared here).  Returns this thread's bad-pivot flag; ends with a barrier.
+// Ls != nullptr: the walker's last update of the blocks right of column
+// block 0 is still due (the walker applied it to column block 0 only);
+// waves 1-3 apply it while wave 0 factors panel 0, before the trailing
+// update of panel 0 touches those blocks (every block keeps its update
+// order: bitwise the same factor).
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
-__device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n) {
+__device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
+                                           const double* Ls = nullptr) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -206,8 +256,22 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       if (r < 16)
 #pragma unroll
         for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = wc[c];
-    } else if (b >= 2 && w - 1 < b - 1) {
-      w_offdiag(T, Wl, scr[w], b - 1, w - 1, lane);  // row b-1 of W (its diagonal block is done)
+    } else if (b == 0) {
+      if (Ls != nullptr) {
+        // deferred last update: wave 1 blocks (1,1) (2,2), wave 2 (2,1) (3,2),
+        // wave 3 (3,1) (3,3)  [(I, J)]
+        const int Ib[2] = {w, w + 1 < 4 ? w + 1 : 3}, Jb[2] = {1, w == 1 ? 2 : (w == 2 ? 2 : 3)};
+        last_update<2>(T, Ls, Ib, Jb, 2, lane);
+      }
+    } else if (b == 2 && w <= 1) {
+      w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
+    } else if (b == 3) {
+      // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
+      if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      w_row3_sum(T, Wl, scr[w], w - 1, lane);
     }
     __syncthreads();
     // ---- trailing update: blocks (I, J), b < J <= I <= 3 ----
@@ -229,8 +293,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       __syncthreads();
     }
   }
-  // ---- W row 3 off the diagonal ----
-  if (w < 3) w_offdiag(T, Wl, scr[w], 3, w, lane);
+  // ---- W row 3 off the diagonal: the products with W_33 ----
+  if (w >= 1) w_row3_finish(Wl, scr[w], w - 1, lane);
   __syncthreads();
   return bad;
 }
@@ -611,7 +675,6 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
                              double* Ls, double (*scr)[256], int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int li = lane & 15, kk = lane >> 4;
   // the next diagonal tile travels in registers (prefetched one step ahead)
   double nx[16];
   block_wait(Pf, epoch, fail);
@@ -629,37 +692,14 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     }
     __syncthreads();
     if (j > 0) {
-      // T -= L_j,j-1 L_j,j-1^T on the ten lower 16x16 blocks: wave w owns
-      // blocks w, w + 4 (and w + 8 for w < 2); their MFMA chains are
-      // interleaved, so no MFMA waits on the accumulator of the one before
-      // (same k order per block as a chain: bitwise the same sums)
-      const int nq = w < 2 ? 3 : 2;  // wave-uniform
-      int Iq[3], Jq[3];
-#pragma unroll
-      for (int qi = 0; qi < 3; ++qi) {
-        int J = 0, qq = w + 4 * qi;
-        while (qq >= 4 - J && J < 4) { qq -= 4 - J; ++J; }
-        Jq[qi] = J < 4 ? J : 0;
-        Iq[qi] = J < 4 ? J + qq : 0;
-      }
-      f64x4 acc[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-#pragma unroll
-      for (int M = 0; M < 4; ++M)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const double* row = Ls + (16 * M + 4 * s4 + kk) * TS + li;
-#pragma unroll
-          for (int qi = 0; qi < 3; ++qi)
-            if (qi < nq) acc[qi] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16 * Iq[qi]], row[16 * Jq[qi]], acc[qi], 0, 0, 0);
-        }
-#pragma unroll
-      for (int qi = 0; qi < 3; ++qi)
-        if (qi < nq)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) T[(16 * Jq[qi] + li) * TS + 16 * Iq[qi] + 4 * rr + kk] -= acc[qi][rr];
+      // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
+      // blocks right of it are updated inside potrf_tile, during panel 0
+      const int Ib[1] = {w}, Jb[1] = {0};
+      last_update<1>(T, Ls, Ib, Jb, 1, lane);
       __syncthreads();
     }
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n) : potrf_tile<false>(T, Wl, scr, j0, n);
+    const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl) : potrf_tile<false>(T, Wl, scr, j0, n, dl);
     if (bad) atomicOr(fail, 1);
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
