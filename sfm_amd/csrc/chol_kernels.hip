@@ -140,6 +140,18 @@ __device__ __forceinline__ void last_update(double* T, const double* Ls, const i
       for (int rr = 0; rr < 4; ++rr) T[(16 * Jb[q] + li) * TS + 16 * Ib[q] + 4 * rr + kk] -= acc[q][rr];
 }
 
+// Trailing update of the 16x16 block (I, J) by the panel at columns g0..g0+15,
+// one wavefront: C_IJ -= P_I P_J^T.
+__device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int lane) {
+  const double* P = T + g0 * TS;  // P(row, kk) = L(row, g0 + kk) = P[kk*TS + row]
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  // A(i, k) = L(16I + i, g0 + k), B(k, j) = L(16J + j, g0 + k)
+  acc = mfma16(P + 16 * I, 1, TS, P + 16 * J, TS, 1, acc, lane);
+  const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) T[(16 * J + j) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
+}
+
 // The factorisation proper, on the tile image T in LDS (256 threads; Wl is
 // cleared here).  Returns this thread's bad-pivot flag; ends with a barrier.
 // Ls != nullptr: the walker's last update of the blocks right of column
@@ -263,8 +275,13 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         const int Ib[2] = {w, w + 1 < 4 ? w + 1 : 3}, Jb[2] = {1, w == 1 ? 2 : (w == 2 ? 2 : 3)};
         last_update<2>(T, Ls, Ib, Jb, 2, lane);
       }
-    } else if (b == 2 && w <= 1) {
+    } else if (b == 1) {
+      // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
+      trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
+    } else if (b == 2 && w == 1) {
       w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
+    } else if (b == 2 && w == 3) {
+      trail_block(T, 16, 3, 3, lane);  // panel 1's trailing update of block (3,3)
     } else if (b == 3) {
       // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
       if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
@@ -274,22 +291,10 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
     }
     __syncthreads();
-    // ---- trailing update: blocks (I, J), b < J <= I <= 3 ----
+    // ---- trailing update of column block b+1 (the next panel's); the
+    // blocks right of it follow during the next panel (look-ahead) ----
     if (b < 3) {
-      const int nJ = 3 - b, nq = nJ * (nJ + 1) / 2;
-      for (int q = w; q < nq; q += 4) {
-        // q -> (J, I) column-major over the trailing lower triangle
-        int J = b + 1, qq = q;
-        while (qq >= 4 - J) { qq -= 4 - J; ++J; }
-        const int I = J + qq;
-        const double* P = T + g0 * TS;  // P(row, kk) = L(row, g0 + kk) = P[kk*TS + row]
-        f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-        // A(i, k) = L(16I + i, g0 + k), B(k, j) = L(16J + j, g0 + k)
-        acc = mfma16(P + 16 * I, 1, TS, P + 16 * J, TS, 1, acc, lane);
-        const int j = lane & 15, kk = lane >> 4;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) T[(16 * J + j) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
-      }
+      if (w < 3 - b) trail_block(T, g0, b + 1 + w, b + 1, lane);
       __syncthreads();
     }
   }
