@@ -405,6 +405,51 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
   return b;
 }
 
+// The helpers' TRSM X = T W^T for U stacked tiles (T_u in LDS, W = L_jj^-1
+// lower triangular in global memory, column-major: W(c, m) at m*NB + c).
+// Wave w takes row block w of every tile and forms X^T (column block C) =
+// sum_{M <= C} W_CM T_wM^T on MFMA: 40 MFMAs per tile instead of 64 (the
+// products with W's zero upper blocks are skipped; they came last in the
+// k order, so the sums are bitwise the full ones), the W operand shared by
+// the U tiles.  x[u][C] reg rr holds X(16w + (lane & 15), 16C + 4rr + (lane >> 4)).
+template <int U>
+__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double* __restrict__ Wk, f64x4 (*x)[4],
+                                          int lane) {
+  const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int C = 0; C < 4; ++C) x[u][C] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int k = 16 * M + 4 * s4 + kk;
+      double bt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) bt[u] = Tp[u][k * TS + 16 * w + li];
+#pragma unroll
+      for (int C = M; C < 4; ++C) {
+        const double a = Wk[k * NB + 16 * C + li];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u][C] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bt[u], x[u][C], 0, 0, 0);
+      }
+    }
+}
+// Write-through stores of trsm_rows' tiles to rows i0 + 64u.. of column
+// block j0 (16 lanes per 128-B column run).
+template <int U>
+__device__ __forceinline__ void put_rows(double* __restrict__ A, int ld, int i0, int j0, const f64x4 (*x)[4], int lane) {
+  const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int C = 0; C < 4; ++C)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        st_wt(A + size_t(j0 + 16 * C + 4 * rr + kk) * ld + i0 + NB * u + 16 * w + li, x[u][C][rr]);
+}
+
 // Helper: one tile (i, j).  Wave w owns the 32x32 quadrant (c in cb.., r in
 // rb..), accumulated transposed: D[c][r] = sum_l L_jk[c][l] L_ik[r][l], so the MFMA's D
 // column (lane & 15) walks the tile's rows (128-B column runs of A).
@@ -477,33 +522,10 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
         T[(cb + 16 * a + lk + 4 * reg) * TS + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
   block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
   const double* Wk = Winv + size_t(j) * NB * NB;
-  double xa[2][16], yb[2][16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const int m = 4 * ks + lk;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = T[m * TS + rb + 16 * bb + lr];
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb)
-        acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr, acc[a][bb][reg]);
+  const double* Tp[1] = {T};
+  f64x4 x[1][4];
+  trsm_rows<1>(Tp, Wk, x, lane);
+  put_rows<1>(A, ld, i0, j0, x, lane);
   block_publish_wt(F + i * nb + j, epoch);
 }
 
@@ -573,43 +595,10 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
   }
   block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
   const double* Wk = Winv + size_t(j) * NB * NB;
-  double xa[2][16], yb[2][2][16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const int m = 4 * ks + lk;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) xa[a][ks] = Wk[m * NB + cb + 16 * a + lr];
-#pragma unroll
-    for (int bb = 0; bb < 2; ++bb) {
-      yb[0][bb][ks] = T0[m * TS + rb + 16 * bb + lr];
-      yb[1][bb][ks] = T1[m * TS + rb + 16 * bb + lr];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) acc[u][a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-          acc[u][a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[u][bb][ks], acc[u][a][bb], 0, 0, 0);
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg)
-          st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + (u ? i1 : i0) + rb + 16 * bb + lr,
-                acc[u][a][bb][reg]);
+  const double* Tp[2] = {T0, T1};
+  f64x4 x[2][4];
+  trsm_rows<2>(Tp, Wk, x, lane);
+  put_rows<2>(A, ld, i0, j0, x, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (wave0()) {
@@ -619,11 +608,12 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
 }
 
 // Helper tasks of column j: the diagonal tile, the subdiagonal tile (both
-// partial, for the walker), then the vertical pairs of final tiles (a last
-// single tile when the column's count is odd).
+// partial, for the walker), the first final tile (j+2, j) alone (it feeds
+// the walker two steps ahead, so its TRSM is on the chain), then the
+// vertical pairs of final tiles (a last single tile when the count is odd).
 __host__ __device__ __forceinline__ int col_tasks(int nb, int j) {
   const int m = nb - j;
-  return m <= 2 ? m : 2 + (m - 1) / 2;
+  return m <= 2 ? m : 3 + (m - 3) / 2 + ((m - 3) & 1);
 }
 __host__ __device__ __forceinline__ int chol_tasks(int nb) {
   int s = 0;
@@ -787,10 +777,10 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     if (tk >= ntask) break;
     int j = 0, r = tk;
     while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
-    if (r < 2) {
+    if (r < 3) {
       fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
     } else {
-      const int i = j + 2 + 2 * (r - 2);
+      const int i = j + 3 + 2 * (r - 3);
       if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail);
       else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail);
     }
