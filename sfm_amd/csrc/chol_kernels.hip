@@ -159,9 +159,14 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
 // waves 1-3 apply it while wave 0 factors panel 0, before the trailing
 // update of panel 0 touches those blocks (every block keeps its update
 // order: bitwise the same factor).
+// pf_sub != nullptr: wave 3 polls the flags of the walker's next two
+// partial tiles once during panel 3 and leaves in *rdy whether both are out,
+// so the walker can load them beside W_j's publication (a poll during panel
+// 2 mostly came too early: the tile (j+1, j) waits for L_j,j-1).
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
 __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
-                                           const double* Ls = nullptr) {
+                                           const double* Ls, const int* pf_sub, const int* pf_diag, int epoch,
+                                           int* rdy) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -289,6 +294,9 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
+      if (w == 3 && pf_sub != nullptr)
+        *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     }
     __syncthreads();
     // ---- trailing update of column block b+1 (the next panel's); the
@@ -663,14 +671,18 @@ __device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i
 
 // The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
 // TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
+// When the POTRF's poll found the partial tiles (j+1, j) and (j+1, j+1)
+// already out, their loads are issued beside W_j's write-through stores and
+// share one drain with them; the stores of L_j+1,j drain during the next
+// step's first update, and their flag goes out after it.
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
-                             double* Ls, double (*scr)[256], int* __restrict__ fail) {
+                             double* Ls, double (*scr)[256], int* rdy, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // the next diagonal tile travels in registers (prefetched one step ahead)
+  // the next diagonal tile travels in registers (loaded one step ahead)
   double nx[16];
   block_wait(Pf, epoch, fail);
 #pragma unroll
@@ -685,17 +697,35 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
       T[c * TS + r] = nx[q];
     }
+    if (t == 0) *rdy = 0;
     __syncthreads();
     if (j > 0) {
       // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
       // blocks right of it are updated inside potrf_tile, during panel 0
       const int Ib[1] = {w}, Jb[1] = {0};
       last_update<1>(T, Ls, Ib, Jb, 1, lane);
-      __syncthreads();
+      // L_j,j-1 (stored at the end of the last step) has drained: its flag
+      block_publish_wt(F + j * nb + j - 1, epoch);
     }
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl) : potrf_tile<false>(T, Wl, scr, j0, n, dl);
+    const bool more = j + 1 < nb;
+    const int i0 = j0 + NB;
+    const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
+    const int* fdiag = more ? Pf + (j + 1) * nb + j + 1 : nullptr;
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
+                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
     if (bad) atomicOr(fail, 1);
+    const bool early = more && __builtin_amdgcn_readfirstlane(*rdy) != 0;
+    double sub[16];
+    if (early) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        sub[q] = A[size_t(j0 + c) * ld + i0 + r];
+        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+      }
+    }
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -704,32 +734,44 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       // from set_problem (one memset), 37% fewer bytes on the chain
       if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
-    // W_j out at once: the helpers' TRSMs of column j feed the last updates
-    // of the diagonal tiles two steps ahead (a chain as long as a step)
-    block_publish_wt(F + j * nb + j, epoch);
-    // L_jj is read by nobody (the helpers' TRSMs and the back substitution
-    // use W_j; the next Schur pass rewrites the lower triangle) except in the
-    // tile that holds the augmented row n: its z entries feed k_backsolve.
-    // The next publish's drain covers these stores.
-    if (j0 <= n && n < j0 + NB) {
+    if (early) {
+      // T (L_jj) is read by nobody from here on (see below): it takes the
+      // subdiagonal tile
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+        T[c * TS + r] = sub[q];
       }
     }
-    if (j + 1 == nb) break;
-    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
-    const int i0 = j0 + NB;
-    block_wait(Pf + (j + 1) * nb + j, epoch, fail);
-    load_tile(T, A, ld, i0, j0);
-    // prefetch the next diagonal tile (the loads overlap the TRSM)
-    block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+    // W_j out at once: the helpers' TRSMs of column j feed the last updates
+    // of the diagonal tiles two steps ahead (a chain as long as a step)
+    block_publish_wt(F + j * nb + j, epoch);
+    if (!more) {
+      // L_jj is read by nobody (the helpers' TRSMs and the back substitution
+      // use W_j; the next Schur pass rewrites the lower triangle) except in
+      // the tile that holds the augmented row n -- the last one: its z
+      // entries feed k_backsolve (the kernel's end drains the stores).
+      if (j0 <= n && n < j0 + NB) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        for (int q = 0; q < 16; ++q) {
+          const int e = t + 256 * q, c = e >> 6, r = e & 63;
+          st_wt(A + size_t(j0 + c) * ld + j0 + r, T[c * TS + r]);
+        }
+      }
+      break;
     }
+    if (!early) {
+      // the poll missed: wait for the partial tiles here
+      block_wait(Pf + (j + 1) * nb + j, epoch, fail);
+      load_tile(T, A, ld, i0, j0);
+      block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+      }
+    }
+    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
     f64x4 x[4];
     trsm_lds(T, Wl, x, lane);
     put_tile(Ls, x, lane);
@@ -739,7 +781,6 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
       st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
     }
-    block_publish_wt(F + (j + 1) * nb + j, epoch);
   }
 }
 
@@ -753,7 +794,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   __shared__ double scr[4][256];
   __shared__ int sh[2];
   if (blockIdx.x == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, fail);
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
     return;
   }
   const int ntask = chol_tasks(nb);
