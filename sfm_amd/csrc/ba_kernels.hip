@@ -268,9 +268,11 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
       const double cl = jac_record(cr, cam[6 * c + 3], cam[6 * c + 4], cam[6 * c + 5], k[0], k[1], k[2], k[3], k[4],
                                    sc, spc, Xc, uv_cur, rec);
       cost += (l < cnt) ? cl : 0.0;
-      double* mine = wst + l * kJRec;
+      if (write_rec) {  // staged for jac_flush (wave-uniform)
+        double* mine = wst + l * kJRec;
 #pragma unroll
-      for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
+        for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
+      }
       if (jpart) {
         // the chunk's share of U_c = sum J_c^T J_c (21, packed upper) and
         // b_c = sum J_c^T r (6): one reduce-scatter over the wave, lane 2e
