@@ -757,16 +757,20 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_blk, const 
   int len = ke - kb;
 #pragma unroll
   for (int off = kSub; off < 64; off <<= 1) len = max(len, __shfl_xor(len, off));
+  // unconditional loads of clamped indices (a past-the-end step reads a real
+  // point, masked by w = 0): a predicated load becomes a branch whose join
+  // drains vmcnt.  The next step's index is loaded one step ahead, so each
+  // step's record gather waits on one dependent load instead of two
+  // (263 -> 251 us per C3 launch, S bitwise unchanged).
+  int p_nx = bpts[kb + sl < ke ? kb + sl : 0];
   for (int k0 = 0; k0 < len; k0 += kSub) {
     // the camera constants are re-read from LDS each step (hoisted, they
     // would hold 200 VGPRs)
     asm volatile("" ::: "memory");
     const int k = kb + k0 + sl;
     const bool valid = k < ke;
-    // unconditional load of a clamped index (a past-the-end step reads a
-    // real point, masked by w = 0): a predicated load becomes a branch whose
-    // join drains vmcnt
-    const int p = bpts[valid ? k : 0];
+    const int p = p_nx;
+    p_nx = bpts[k + kSub < ke ? k + kSub : 0];
     const double* r = ptS + size_t(kPtS) * p;
     double q[12];  // X, scale, l10 l20 l21, 1/l_ii (z, the last 32 B, unused here)
 #pragma unroll
