@@ -358,6 +358,68 @@ __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* 
 // and the camera's R, t, K (L2-resident):
 // mode 0: Jacobi scale of the point columns; mode 1: V_p, b_p, LM diagonal,
 // gradient max-norm and |X|^2.
+// Camera constants of the point-major passes, by base pointer and stride per
+// camera: R (9), t (3) and K (fx sk cx fy cy), from the global arrays or from
+// an LDS copy (k_point_eval_lds).
+struct CamView {
+  const double* R; const double* t; const double* K;
+  int sR, sT, sK;
+};
+
+__device__ __forceinline__ void point_eval_body(int p, const int32_t* __restrict__ pt_off,
+                                                const int32_t* __restrict__ cam_pm,
+                                                const double* __restrict__ uv_pm, const CamView cv,
+                                                const double* __restrict__ X, double* __restrict__ scale_p,
+                                                double* __restrict__ diag_p, double* __restrict__ ptV,
+                                                double min_diag, double max_diag, int mode, int reuse, double& g,
+                                                double& xn) {
+  double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+  const double Xp[3] = {X[3 * size_t(p)], X[3 * size_t(p) + 1], X[3 * size_t(p) + 2]};
+  double sp[3] = {1.0, 1.0, 1.0};
+  if (mode == 1)
+    for (int k = 0; k < 3; ++k) sp[k] = scale_p[3 * size_t(p) + k];
+  const int q0 = pt_off[p], q1 = pt_off[p + 1];
+  for (int q = q0; q < q1; ++q) {
+    const int c = cam_pm[q];
+    const double2 uvo = ld2(uv_pm + 2 * size_t(q));
+    const double* cr = cv.R + size_t(cv.sR) * c;
+    const double* k5 = cv.K + size_t(cv.sK) * c;
+    const double* tc = cv.t + size_t(cv.sT) * c;
+    const double fx = k5[0], sk = k5[1], cx = k5[2], fy = k5[3], cy = k5[4];
+    const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
+    const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc[1];
+    const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc[2];
+    const double xp = pc0 / pc2, yp = pc1 / pc2;
+    const double r0 = fx * xp + sk * yp + cx - uvo.x;
+    const double r1 = fy * yp + cy - uvo.y;
+    const double iz = 1.0 / pc2;
+    const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
+    const double b1 = fy * iz, b2 = -fy * yp * iz;
+    double u[3], v[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      u[j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
+      v[j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
+    }
+    V[0] += u[0] * u[0] + v[0] * v[0];
+    V[1] += u[1] * u[0] + v[1] * v[0]; V[2] += u[1] * u[1] + v[1] * v[1];
+    V[3] += u[2] * u[0] + v[2] * v[0]; V[4] += u[2] * u[1] + v[2] * v[1]; V[5] += u[2] * u[2] + v[2] * v[2];
+    b[0] += u[0] * r0 + v[0] * r1; b[1] += u[1] * r0 + v[1] * r1; b[2] += u[2] * r0 + v[2] * r1;
+  }
+  const double cn[3] = {V[0], V[2], V[5]};
+  if (mode == 0) {
+    for (int k = 0; k < 3; ++k) scale_p[3 * size_t(p) + k] = 1.0 / (1.0 + sqrt(cn[k]));
+  } else {
+    for (int k = 0; k < 3; ++k) {
+      if (!reuse) diag_p[3 * size_t(p) + k] = fmin(fmax(cn[k], min_diag), max_diag);
+      g = fmax(g, fabs(b[k] / scale_p[3 * size_t(p) + k]));
+      xn += X[3 * size_t(p) + k] * X[3 * size_t(p) + k];
+    }
+    double* o = ptV + size_t(kPtV) * p;
+    st2(o, V[0], V[1]); st2(o + 2, V[2], V[3]); st2(o + 4, V[4], V[5]); st2(o + 6, b[0], b[1]); st2(o + 8, b[2], 0.0);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t* __restrict__ pt_off,
                                                             const int32_t* __restrict__ cam_pm,
                                                             const double* __restrict__ uv_pm,
@@ -372,53 +434,48 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double g = 0.0, xn = 0.0;
-  if (p < P) {
-    double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    const double Xp[3] = {X[3 * size_t(p)], X[3 * size_t(p) + 1], X[3 * size_t(p) + 2]};
-    double sp[3] = {1.0, 1.0, 1.0};
-    if (mode == 1)
-      for (int k = 0; k < 3; ++k) sp[k] = scale_p[3 * size_t(p) + k];
-    const int q0 = pt_off[p], q1 = pt_off[p + 1];
-    for (int q = q0; q < q1; ++q) {
-      const int c = cam_pm[q];
-      const double2 uvo = ld2(uv_pm + 2 * size_t(q));
-      const double* cr = camR + size_t(kCamR) * c;
-      const double* k5 = Kc + 5 * size_t(c);
-      const double* tc = cam + 6 * size_t(c) + 3;
-      const double fx = k5[0], sk = k5[1], cx = k5[2], fy = k5[3], cy = k5[4];
-      const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
-      const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc[1];
-      const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc[2];
-      const double xp = pc0 / pc2, yp = pc1 / pc2;
-      const double r0 = fx * xp + sk * yp + cx - uvo.x;
-      const double r1 = fy * yp + cy - uvo.y;
-      const double iz = 1.0 / pc2;
-      const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
-      const double b1 = fy * iz, b2 = -fy * yp * iz;
-      double u[3], v[3];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        u[j] = (a0 * cr[j] + a1 * cr[3 + j] + a2 * cr[6 + j]) * sp[j];
-        v[j] = (b1 * cr[3 + j] + b2 * cr[6 + j]) * sp[j];
-      }
-      V[0] += u[0] * u[0] + v[0] * v[0];
-      V[1] += u[1] * u[0] + v[1] * v[0]; V[2] += u[1] * u[1] + v[1] * v[1];
-      V[3] += u[2] * u[0] + v[2] * v[0]; V[4] += u[2] * u[1] + v[2] * v[1]; V[5] += u[2] * u[2] + v[2] * v[2];
-      b[0] += u[0] * r0 + v[0] * r1; b[1] += u[1] * r0 + v[1] * r1; b[2] += u[2] * r0 + v[2] * r1;
-    }
-    const double cn[3] = {V[0], V[2], V[5]};
-    if (mode == 0) {
-      for (int k = 0; k < 3; ++k) scale_p[3 * size_t(p) + k] = 1.0 / (1.0 + sqrt(cn[k]));
-    } else {
-      for (int k = 0; k < 3; ++k) {
-        if (!reuse) diag_p[3 * size_t(p) + k] = fmin(fmax(cn[k], min_diag), max_diag);
-        g = fmax(g, fabs(b[k] / scale_p[3 * size_t(p) + k]));
-        xn += X[3 * size_t(p) + k] * X[3 * size_t(p) + k];
-      }
-      double* o = ptV + size_t(kPtV) * p;
-      st2(o, V[0], V[1]); st2(o + 2, V[2], V[3]); st2(o + 4, V[4], V[5]); st2(o + 6, b[0], b[1]); st2(o + 8, b[2], 0.0);
-    }
+  if (p < P)
+    point_eval_body(p, pt_off, cam_pm, uv_pm, CamView{camR, cam + 3, Kc, kCamR, 6, 5}, X, scale_p, diag_p, ptV,
+                    min_diag, max_diag, mode, reuse, g, xn);
+  if (mode == 1) {
+    const double rg = block_reduce(g, sh, true);
+    if (threadIdx.x == 0) part_grad[blockIdx.x] = rg;
+    const double rx = block_reduce(xn, sh, false);
+    if (threadIdx.x == 0) part_xn[blockIdx.x] = rx;
   }
+}
+
+// The same pass with every camera's R, t, K (17 doubles) staged in LDS first
+// (C <= kMaxC).  One lane per point gathers ~10 different cameras, so the
+// global-memory form issues ~13 camera loads per observation that each touch
+// up to 64 cache lines: the texture-address path, not latency, bounds it
+// (index/constant prefetching measured no change).  From LDS the same values,
+// in the same arithmetic, are bitwise identical.
+constexpr int kCamE = 17;
+template <int kMaxC>
+__global__ __launch_bounds__(kThreads) void k_point_eval_lds(int P, int C, const int32_t* __restrict__ pt_off,
+                                                             const int32_t* __restrict__ cam_pm,
+                                                             const double* __restrict__ uv_pm,
+                                                             const double* __restrict__ camR,
+                                                             const double* __restrict__ cam,
+                                                             const double* __restrict__ Kc,
+                                                             const double* __restrict__ X,
+                                                             double* __restrict__ scale_p, double* __restrict__ diag_p,
+                                                             double* __restrict__ ptV, double min_diag, double max_diag,
+                                                             int mode, int reuse, double* __restrict__ part_grad,
+                                                             double* __restrict__ part_xn) {
+  __shared__ double sh[4];
+  __shared__ double cst[kMaxC * kCamE];
+  for (int i = threadIdx.x; i < C * kCamE; i += blockDim.x) {
+    const int c = i / kCamE, j = i - c * kCamE;
+    cst[i] = j < 9 ? camR[size_t(kCamR) * c + j] : j < 12 ? cam[6 * size_t(c) + 3 + (j - 9)] : Kc[5 * size_t(c) + (j - 12)];
+  }
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double g = 0.0, xn = 0.0;
+  if (p < P)
+    point_eval_body(p, pt_off, cam_pm, uv_pm, CamView{cst, cst + 9, cst + 12, kCamE, kCamE, kCamE}, X, scale_p,
+                    diag_p, ptV, min_diag, max_diag, mode, reuse, g, xn);
   if (mode == 1) {
     const double rg = block_reduce(g, sh, true);
     if (threadIdx.x == 0) part_grad[blockIdx.x] = rg;
@@ -1161,10 +1218,19 @@ void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool co
 }
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
   if (d.P == 0) return;
-  k_point_eval_rc<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam,
-                                                                 d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag,
-                                                                 mode, reuse_diag ? 1 : 0, slot(d, kPGradPt),
-                                                                 slot(d, kPXNormPt));
+  const int nb = blocks_for(d.P, kThreads);
+  // camera constants from LDS while they fit (C3: 500 cameras, 68 KB)
+#define SFM_PE_LDS(M_)                                                                                              \
+  k_point_eval_lds<M_><<<nb, kThreads, 0, s>>>(d.P, d.C, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X,      \
+                                               d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag, mode,           \
+                                               reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt))
+  if (d.C <= 64) SFM_PE_LDS(64);
+  else if (d.C <= 512) SFM_PE_LDS(512);
+  else
+    k_point_eval_rc<<<nb, kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X, d.scale_p,
+                                            d.diag_p, d.ptV, d.min_diag, d.max_diag, mode, reuse_diag ? 1 : 0,
+                                            slot(d, kPGradPt), slot(d, kPXNormPt));
+#undef SFM_PE_LDS
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
