@@ -9,9 +9,15 @@ explicit:
   _frameViewsPointIdx.emplace(frameNo[j], p);
 * addPointMatches (CMap.cpp:118-132): the same three appends per match;
 * addDescriptors (CMap.cpp:308-315): _descriptor[p].push_back(row);
-* std::multimap::emplace inserts at the upper bound of the equal range, so
-  equal_range(f) yields the entries of key f in insertion order -- the
-  multimap is kept as the list of (frame, point) entries in emplace order;
+* the reference's container is an std::unordered_multimap (CMap.h:96-97),
+  whose equal_range order is implementation-defined: libc++ (the
+  reference's Xcode toolchain) keeps equal keys in insertion order, while
+  libstdc++ links a new equal key in next to its existing group rather than
+  at its end, so it does not yield insertion order.  This restatement
+  adopts insertion order (libc++); that order is the BA observation order
+  of CSfM::bundleAdjustment, so the choice is part of the unpinned parity.
+  The multimap is kept as the list of (frame, point) entries in emplace
+  order;
 * getPointsInFrames(pts3DIdx, frameNo) (CMap.cpp:277-295): the points of
   every frame's equal_range appended, then sort + unique;
 * getPointsInFrame(pts3DIdx, pts2DIdx, frameNo) (CMap.cpp:225-240): per

@@ -133,12 +133,22 @@ class DeviceMap:
 
     def getPointsInFrame(self, frameNo: int):
         """(pts3DIdx, pts2DIdx) of CMap::getPointsInFrame(pts3DIdx, pts2DIdx, frameNo)."""
+        # The 2D list can outgrow the observation count: a point matched k
+        # times in this frame emits k 2D indices per entry, k^2 in all
+        # (CMap.cpp:225-240).  The call reports both counts before it rejects
+        # a short buffer, so a second call with those sizes always fits.
         cap = max(1, self.size()[1])
-        p3 = np.zeros(cap, np.int32)
-        p2 = np.zeros(cap, np.int32)
-        n3, n2 = ctypes.c_int32(), ctypes.c_int32()
-        check(lib().sfm_map_points_in_frame(self._h, int(frameNo), cap, ptr(p3), ctypes.byref(n3), ptr(p2),
-                                            ctypes.byref(n2)), "sfm_map_points_in_frame")
+        for _ in range(2):
+            p3 = np.zeros(cap, np.int32)
+            p2 = np.zeros(cap, np.int32)
+            n3, n2 = ctypes.c_int32(), ctypes.c_int32()
+            rc = lib().sfm_map_points_in_frame(self._h, int(frameNo), cap, ptr(p3), ctypes.byref(n3), ptr(p2),
+                                               ctypes.byref(n2))
+            need = max(n3.value, n2.value)
+            if rc == 0 or need <= cap:
+                break
+            cap = need
+        check(rc, "sfm_map_points_in_frame")
         return p3[:n3.value].copy(), p2[:n2.value].copy()
 
     def getRepresentativeDescriptors(self, pts3DIdx, return_best: bool = False):

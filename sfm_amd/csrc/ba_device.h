@@ -107,7 +107,8 @@ struct DevProblem {
   double* Spack = nullptr;    // [n(n+1)/2 + n] packed upper triangle + rhs (cross-rank all-reduce)
   double* invL = nullptr;     // [nblk][64][64] inverses of the diagonal tiles
   double* ysol = nullptr;     // [ld] solution of S y = rhs (camera part)
-  int32_t* fail = nullptr;    // [1] bit 0: Cholesky pivot not positive; bit 1: back-substitution hand-off timeout
+  int32_t* fail = nullptr;    // [1] 1: Cholesky pivot not positive; 2: back-substitution hand-off timeout;
+                              //     4: Cholesky tile hand-off timeout
   int32_t* flags = nullptr;   // [nblk] back-substitution hand-off flags (epoch-stamped)
   int32_t* cflags = nullptr;  // [2][nblk][nblk] fused Cholesky: final (F) and partial (P) tile flags
   unsigned long long* cticket = nullptr;  // fused Cholesky tile ticket (monotone across launches)

@@ -896,7 +896,11 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
       sm.num_linear_solves++;
       int chol_fail = 0;
       std::memcpy(&chol_fail, sc + kNumScalars, sizeof(int));
-      if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out");
+      // The persistent grids need every workgroup co-resident: device work on
+      // other streams that holds CUs while a solve runs can starve them, and
+      // their bounded waits then report here.
+      if (chol_fail & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid not co-resident)");
+      if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid not co-resident)");
       const bool solve_ok = chol_fail == 0 && !(sc[kBadStep] > 0.0) && !(sc[kBadCam] > 0.0) && !(sc[kBadBack] > 0.0);
       const double model_cost_change = sc[kModelChange] + sc[kModelChangePt];
       itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;

@@ -328,7 +328,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // (flag P); every other tile finishes with its TRSM against W_j (F(j,j)).
 // Tickets are taken in an order in which every dependency was taken
 // earlier, all workgroups are co-resident (grid <= CU count, one per CU),
-// so the waits always drain; every wait is bounded anyway (fail bit 1).
+// so the waits always drain; every wait is bounded anyway (a timeout sets
+// fail bit value 4; the back substitution's own timeout sets 2).
 // Polls are relaxed agent-scope atomic loads (coherent across the XCDs'
 // L2s); the acquire fence comes once, after the flag is seen.  (An acquire
 // load per poll would invalidate the poller's L2 on every spin.)
@@ -355,7 +356,7 @@ __device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(
 // barrier orders the other waves' loads after it).
 __device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
   if (wave0()) {
-    if (!spin_until(f, epoch)) atomicOr(fail, 2);
+    if (!spin_until(f, epoch)) atomicOr(fail, 4);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
   }
@@ -398,7 +399,7 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
       __builtin_amdgcn_s_sleep(1);
     }
     if (bound == k_from) {  // timed out: proceed (garbage), reported as an error
-      atomicOr(fail, 2);
+      atomicOr(fail, 4);
       bound = k_from + 1;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

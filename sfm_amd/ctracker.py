@@ -64,13 +64,29 @@ class CTracker:
         return sm
 
     # ---- matching --------------------------------------------------------
-    def _m(self, nbytes: int = 64):
-        from .matcher import FeatureMatcher
-        if self._matcher is None or self._matcher.desc_bytes != nbytes:
-            if self._matcher is not None:
-                self._matcher.close()
-            self._matcher = FeatureMatcher(nbytes, device=self.device)
+    def _resident(self):
+        """The frame-resident matcher (created by setKeyPoints); the
+        resident-frame overloads use its own descriptor width."""
+        if self._matcher is None:
+            raise RuntimeError("matchFeatures: setKeyPoints() the previous and current frames first")
         return self._matcher
+
+    def _m(self, nbytes: int):
+        """A matcher of descriptor width `nbytes` for explicit-data calls: the
+        resident one when the width agrees, else a separate one, so a call
+        with another width never discards the resident frames."""
+        from .matcher import FeatureMatcher
+        if self._matcher is not None and self._matcher.desc_bytes == nbytes:
+            return self._matcher
+        if self._matcher is None:
+            self._matcher = FeatureMatcher(nbytes, device=self.device)
+            return self._matcher
+        other = getattr(self, "_other", None)
+        if other is None or other.desc_bytes != nbytes:
+            if other is not None:
+                other.close()
+            self._other = other = FeatureMatcher(nbytes, device=self.device)
+        return other
 
     @staticmethod
     def _nbytes(desc0, desc1) -> int:
@@ -89,8 +105,15 @@ class CTracker:
         detectFeatures, CTracker.cpp:275-287): undistorted positions,
         descriptors, distorted positions.  They stay resident on the device;
         the previous current frame becomes _prevFrame (CSfM.cpp:626-629)."""
+        from .matcher import FeatureMatcher
         d = np.asarray(desc)
-        self._m(int(d.shape[1]) if d.ndim == 2 and d.shape[1] else 64).push_frame(pts, desc, pts_distorted)
+        nbytes = int(d.shape[1]) if d.ndim == 2 and d.shape[1] else 64
+        if self._matcher is not None and self._matcher.desc_bytes != nbytes:
+            self._matcher.close()        # a new descriptor width starts a new frame pair
+            self._matcher = None
+        if self._matcher is None:
+            self._matcher = FeatureMatcher(nbytes, device=self.device)
+        self._matcher.push_frame(pts, desc, pts_distorted)
 
     def matchFeatures(self, *args):
         """Overloads of CTracker::matchFeatures:
@@ -105,11 +128,11 @@ class CTracker:
         (prevPts, prevDesc, currPts, currDesc, prevIdx, currIdx)   the
            index-subset rule on explicit frame data (no resident frames)."""
         if len(args) == 0:
-            self._prevIdx, self._currIdx = self._m().match_frames(True, self._ratioTest, self._minMatchDistance,
+            self._prevIdx, self._currIdx = self._resident().match_frames(True, self._ratioTest, self._minMatchDistance,
                                                                   self._maxMatchDistance)
             return len(self._prevIdx) >= self._minFeatures
         if len(args) == 2:
-            return self._m().match_subset(args[0], args[1], self._ratioTest, self._minMatchDistance,
+            return self._resident().match_subset(args[0], args[1], self._ratioTest, self._minMatchDistance,
                                           self._maxMatchDistance)
         if len(args) == 4:
             return self._match(*args, self._minMatchDistance, self._maxMatchDistance)

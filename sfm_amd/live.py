@@ -1,7 +1,7 @@
 """The reference's LIVE tracking path (CSfM::tracking + CSfM::mapping,
 /root/reference/CSfM.cpp:109-261, 500-692) on the device stages, fed by
-synthetic detector output (BRISK itself, row T8, is not built: its
-arithmetic lives in the absent BRISK library).
+synthetic detector output (KeypointStream) or the device BRISK detector on
+rendered frames (BriskVideoStream, row T8).
 
 Per frame (CSfM::tracking):
   1. the frame's keypoints + descriptors go up once (sfm_matcher_push_frame);
@@ -355,7 +355,14 @@ class LiveSfM:
         uv, cam, p3 = [], [], []
         for c, kf in enumerate(self.kfs):
             a3, a2 = self.map.getPointsInFrame(kf.no)
-            n = min(len(a3), len(a2))  # obs j pairs entry j with 2D index j (CSfM.cpp:320-330)
+            # Deliberate departure from the reference: CSfM.cpp:331-340 appends
+            # pts3d and pts2d over ALL frames and pairs them globally, so after
+            # a point matched twice in one keyframe (getPointsInFrame emits k^2
+            # 2D indices, CMap.cpp:225-240) every later observation is paired
+            # with a shifted 2D point and CTracker.cpp:676-677 reads camIdx[i]
+            # past its end (undefined behaviour).  Here entry j of a keyframe
+            # pairs with its 2D index j and the surplus is dropped, per frame.
+            n = min(len(a3), len(a2))
             uv.append(kf.pts[a2[:n]])
             cam.append(np.full(n, c, np.int32))
             p3.append(a3[:n])

@@ -98,6 +98,25 @@ def test_duplicate_match_quirk_on_the_device():
         dm.close()
 
 
+def test_points_in_frame_when_2d_list_outgrows_observations():
+    """n2 = sum of k^2 over a frame's points can exceed n_obs."""
+    import sfm_amd
+    from oracle.cmap_oracle import CMapOracle
+    dm = sfm_amd.DeviceMap(64)
+    om = CMapOracle()
+    try:
+        for m in (dm, om):
+            m.addNewPoints(np.zeros((1, 3)), [[5], [6]], [10, 20])
+            m.addPointMatches([0, 0, 0], [40, 41, 42], 30)
+        assert dm.size()[1] == 5
+        p3, p2 = dm.getPointsInFrame(30)
+        o3, o2 = om.getPointsInFrame(30)
+        assert p3.tolist() == list(o3) == [0, 0, 0]
+        assert p2.tolist() == list(o2) == [40, 41, 42] * 3
+    finally:
+        dm.close()
+
+
 def test_set_points_round_trip_and_errors():
     import sfm_amd
     dm = sfm_amd.DeviceMap(64)
