@@ -393,6 +393,235 @@ class OpticalFlowTracker {
   int rc_ = SFM_OK;
 };
 
+// Drop-in for the body of CTracker::detectFeatures (CTracker.h:47,
+// CTracker.cpp:275-287): _detector->detect + _descriptor->compute with
+// BriskFeatureDetector(60, 6, true) (CTracker.cpp:43-45) on the current
+// frame's grey image, then CFrame::setKeyPoints with the survivors:
+//   bool CTracker::detectFeatures() {
+//     std::vector<cv::KeyPoint> kp; cv::Mat desc;
+//     std::vector<uint8_t> d;
+//     if (sfm_compat::detectFeatures(_currFrame.getFrameGrey(), kp, d)) return false;
+//     desc = cv::Mat(int(kp.size()), 64, CV_8U, d.data()).clone();
+//     _currFrame.setKeyPoints(kp, desc);             // unchanged (CTracker.cpp:286)
+//     return true;
+//   }
+// GreyMat: .data (uint8), .step (row bytes), .cols, .rows; KeyPoint:
+// cv::KeyPoint's public fields (.pt.x, .pt.y, .size, .angle, .response,
+// .octave).  Keypoints come in BRISK's order with the descriptor's border
+// rule applied, as compute() leaves them; `descriptors` receives
+// [kp.size()][64] bytes.  Returns the ABI code (0 on success).  Parity is
+// with BRISK as published (oracle/brisk_oracle.py); the ethz-asl BRISK 2
+// library the reference links is absent, so parity with it is unpinned.
+template <class GreyMat, class KeyPoint>
+inline int detectFeatures(const GreyMat& grey, std::vector<KeyPoint>& keypoints, std::vector<uint8_t>& descriptors,
+                          int threshold = 60, int octaves = 6, int32_t capacity = 20000, int32_t device = 0) {
+  keypoints.clear();
+  descriptors.clear();
+  const int32_t w = int32_t(grey.cols), h = int32_t(grey.rows);
+  const size_t step = static_cast<size_t>(grey.step);
+  const uint8_t* img = static_cast<const uint8_t*>(grey.data);
+  std::vector<uint8_t> packed;
+  if (step != size_t(w)) {  // the ABI takes a continuous [h][w] image
+    packed.resize(size_t(w) * size_t(h));
+    for (int32_t y = 0; y < h; ++y)
+      std::copy(img + size_t(y) * step, img + size_t(y) * step + size_t(w), packed.begin() + size_t(y) * size_t(w));
+    img = packed.data();
+  }
+  std::vector<float> k(5 * size_t(capacity));
+  std::vector<int32_t> oct(static_cast<size_t>(capacity));
+  std::vector<uint8_t> d(64 * size_t(capacity));
+  int32_t n = 0;
+  const int rc = sfm_brisk_detect_describe(device, img, w, h, threshold, octaves, capacity, k.data(), oct.data(),
+                                           d.data(), &n);
+  if (rc) return rc;
+  keypoints.resize(size_t(n));
+  for (int32_t i = 0; i < n; ++i) {
+    keypoints[i].pt.x = k[5 * size_t(i)];
+    keypoints[i].pt.y = k[5 * size_t(i) + 1];
+    keypoints[i].size = k[5 * size_t(i) + 2];
+    keypoints[i].angle = k[5 * size_t(i) + 3];
+    keypoints[i].response = k[5 * size_t(i) + 4];
+    keypoints[i].octave = oct[i];
+  }
+  descriptors.assign(d.begin(), d.begin() + 64 * size_t(n));
+  return SFM_OK;
+}
+
+// CMap's observation store on the device (CMap.h:36-99, CMap.cpp), for the
+// CMap methods the tracking and BA paths call.  CMap keeps its host members
+// (_pts3D and the rest); this object replaces the two multimaps, the
+// per-point _frameNo / _pts2DIdx lists and the _descriptor rows
+// (INTEGRATION.md §4f).  Point indices are CMap's _lastPtNo numbering.
+// Every method returns the ABI code (0 on success); the output vectors are
+// APPENDED to, as the reference's push_back loops do.
+class MapStore {
+ public:
+  explicit MapStore(int32_t descBytes = 64, int32_t device = 0) : desc_bytes_(descBytes) {
+    rc_ = sfm_map_create(device, descBytes, &h_);
+  }
+  ~MapStore() {
+    if (h_) sfm_map_destroy(h_);
+  }
+  MapStore(const MapStore&) = delete;
+  MapStore& operator=(const MapStore&) = delete;
+  int status() const { return rc_; }
+
+  // CMap::getNPoints (CMap.cpp:114-116)
+  int getNPoints() const {
+    int32_t np = 0;
+    int64_t no = 0, nd = 0;
+    return h_ && sfm_map_size(h_, &np, &no, &nd) == SFM_OK ? int(np) : 0;
+  }
+
+  // CMap::addNewPoints (CMap.cpp:36-78): pts2DIdx[j][i] = frame j's 2D
+  // index of new point i; pts3DIdx receives the new indices.  Matx31 needs
+  // .val[3] (cv::Matx31d).
+  template <class Matx31>
+  int addNewPoints(const std::vector<Matx31>& pts3D, const std::vector<std::vector<int>>& pts2DIdx,
+                   const std::vector<int>& frameNo, std::vector<int>& pts3DIdx) {
+    if (!h_) return rc_;
+    const size_t n = pts3D.size(), nf = frameNo.size();
+    if (pts2DIdx.size() != nf) return SFM_EINVAL;
+    std::vector<double> X(3 * n);
+    for (size_t i = 0; i < n; ++i)
+      for (int m = 0; m < 3; ++m) X[3 * i + m] = pts3D[i].val[m];
+    std::vector<int32_t> flat(nf * n);
+    for (size_t j = 0; j < nf; ++j) {
+      if (pts2DIdx[j].size() < n) return SFM_EINVAL;
+      std::copy(pts2DIdx[j].begin(), pts2DIdx[j].begin() + n, flat.begin() + j * n);
+    }
+    std::vector<int32_t> idx(std::max<size_t>(1, n));
+    const int rc = sfm_map_add_new_points(h_, int32_t(n), n ? X.data() : nullptr, int32_t(nf), frameNo.data(),
+                                          flat.data(), idx.data());
+    if (rc) return rc;
+    pts3DIdx.insert(pts3DIdx.end(), idx.begin(), idx.begin() + n);
+    return SFM_OK;
+  }
+
+  // CMap::addPointMatches (CMap.cpp:118-132)
+  int addPointMatches(const std::vector<int>& pts3DIdx, const std::vector<int>& pts2DIdx, int frameNo) {
+    if (!h_) return rc_;
+    if (pts2DIdx.size() < pts3DIdx.size()) return SFM_EINVAL;
+    return sfm_map_add_point_matches(h_, int32_t(pts3DIdx.size()), pts3DIdx.data(), pts2DIdx.data(), frameNo);
+  }
+
+  // CMap::addDescriptors (CMap.cpp:308-315): row i of `descriptors` (.rows,
+  // .cols = descBytes, .data; cv::Mat CV_8U, continuous) to point pts3DIdx[i].
+  template <class DescMat>
+  int addDescriptors(const std::vector<int>& pts3DIdx, const DescMat& descriptors) {
+    if (!h_) return rc_;
+    if (size_t(descriptors.rows) < pts3DIdx.size() || int32_t(descriptors.cols) != desc_bytes_) return SFM_EINVAL;
+    return sfm_map_add_descriptors(h_, int32_t(pts3DIdx.size()), pts3DIdx.data(),
+                                   static_cast<const uint8_t*>(descriptors.data));
+  }
+
+  // CMap::getPointsInFrames(pts3DIdx, frameNo) (CMap.cpp:270-288): appends
+  // the points seen in any of the frames, then the reference's sort + unique
+  // over the whole vector.
+  int getPointsInFrames(std::vector<int>& pts3DIdx, const std::vector<int>& frameNo) {
+    if (!h_) return rc_;
+    std::vector<int32_t> out(std::max(1, getNPoints()));
+    int32_t n = 0;
+    const int rc = sfm_map_points_in_frames(h_, int32_t(frameNo.size()), frameNo.data(), int32_t(out.size()),
+                                            out.data(), &n);
+    if (rc) return rc;
+    pts3DIdx.insert(pts3DIdx.end(), out.begin(), out.begin() + n);
+    std::sort(pts3DIdx.begin(), pts3DIdx.end());
+    pts3DIdx.erase(std::unique(pts3DIdx.begin(), pts3DIdx.end()), pts3DIdx.end());
+    return SFM_OK;
+  }
+
+  // CMap::getPointsInFrame(pts3DIdx, pts2DIdx, frameNo) (CMap.cpp:225-240):
+  // per equal_range entry its point, then every 2D index the point has in
+  // that frame (a point matched k times in the frame gives k entries with k
+  // 2D indices each).
+  int getPointsInFrame(std::vector<int>& pts3DIdx, std::vector<int>& pts2DIdx, int frameNo) {
+    if (!h_) return rc_;
+    int32_t np = 0;
+    int64_t no = 0, nd = 0;
+    if (int rc = sfm_map_size(h_, &np, &no, &nd)) return rc;
+    int32_t cap = int32_t(std::max<int64_t>(1, no));
+    for (int attempt = 0; attempt < 2; ++attempt) {  // the 2D list can outgrow n_obs: retry at the reported size
+      std::vector<int32_t> a(static_cast<size_t>(cap)), b(static_cast<size_t>(cap));
+      int32_t n3 = 0, n2 = 0;
+      const int rc = sfm_map_points_in_frame(h_, frameNo, cap, a.data(), &n3, b.data(), &n2);
+      if (rc == SFM_OK) {
+        pts3DIdx.insert(pts3DIdx.end(), a.begin(), a.begin() + n3);
+        pts2DIdx.insert(pts2DIdx.end(), b.begin(), b.begin() + n2);
+        return SFM_OK;
+      }
+      if (std::max(n3, n2) <= cap) return rc;
+      cap = std::max(n3, n2);
+    }
+    return SFM_EINVAL;
+  }
+
+  // CMap::getPointsInFrame_Mutable(pts3D, pts2DIdx, frameNo) (CMap.cpp:206-223),
+  // the BA gather of CSfM::bundleAdjustment (CSfM.cpp:331): one pointer per
+  // entry into the caller's point storage (CMap::_pts3D, Matx31 .val[3]).
+  template <class Matx31>
+  int getPointsInFrame_Mutable(std::vector<Matx31>& hostPts3D, std::vector<double*>& pts3D,
+                               std::vector<int>& pts2DIdx, int frameNo) {
+    std::vector<int> idx;
+    const int rc = getPointsInFrame(idx, pts2DIdx, frameNo);
+    if (rc) return rc;
+    for (int p : idx) {
+      if (p < 0 || size_t(p) >= hostPts3D.size()) return SFM_EINVAL;
+      pts3D.push_back(hostPts3D[size_t(p)].val);
+    }
+    return SFM_OK;
+  }
+
+  // The device copy of the points after BA wrote the host ones back through
+  // the pointers (CSfM.cpp:343), and the reverse: CMap::getPointsAtIdx
+  // restated with its argument honoured (CMap.cpp:134-143 loops over every
+  // point and ignores pts3DIdx, a reference bug not replicated).
+  template <class Matx31>
+  int setPointsAtIdx(const std::vector<int>& pts3DIdx, const std::vector<Matx31>& pts3D) {
+    if (!h_) return rc_;
+    const size_t n = pts3DIdx.size();
+    if (pts3D.size() < n) return SFM_EINVAL;
+    std::vector<double> X(3 * std::max<size_t>(1, n));
+    for (size_t i = 0; i < n; ++i)
+      for (int m = 0; m < 3; ++m) X[3 * i + m] = pts3D[i].val[m];
+    return sfm_map_set_points(h_, int32_t(n), pts3DIdx.data(), X.data());
+  }
+  template <class Matx31>
+  int getPointsAtIdx(const std::vector<int>& pts3DIdx, std::vector<Matx31>& pts3D) {
+    if (!h_) return rc_;
+    const size_t n = pts3DIdx.size();
+    std::vector<double> X(3 * std::max<size_t>(1, n));
+    if (n)
+      if (int rc = sfm_map_get_points(h_, int32_t(n), pts3DIdx.data(), X.data())) return rc;
+    for (size_t i = 0; i < n; ++i) {
+      Matx31 m;
+      for (int k = 0; k < 3; ++k) m.val[k] = X[3 * i + k];
+      pts3D.push_back(m);
+    }
+    return SFM_OK;
+  }
+
+  // CMap::getRepresentativeDescriptors (CMap.cpp:345-381): per point, its row
+  // with the smallest sum of Hamming distances to the others (first on
+  // ties), appended to `descriptors` as [n][descBytes] bytes (wrap with
+  // cv::Mat(n, descBytes, CV_8U, ptr) for the reference's Mat).
+  int getRepresentativeDescriptors(const std::vector<int>& pts3DIdx, std::vector<uint8_t>& descriptors) {
+    if (!h_) return rc_;
+    const size_t n = pts3DIdx.size();
+    if (n == 0) return SFM_OK;
+    std::vector<uint8_t> d(n * size_t(desc_bytes_));
+    const int rc = sfm_map_representative_descriptors(h_, int32_t(n), pts3DIdx.data(), d.data(), nullptr);
+    if (rc) return rc;
+    descriptors.insert(descriptors.end(), d.begin(), d.end());
+    return SFM_OK;
+  }
+
+ private:
+  sfm_map* h_ = nullptr;
+  int rc_ = SFM_OK;
+  int32_t desc_bytes_ = 64;
+};
+
 }  // namespace sfm_compat
 
 #endif  // SFM_CTRACKER_COMPAT_HPP_

@@ -16,8 +16,18 @@
 //                           currIdx, ...) (CSfM.cpp:518), matchFeatures()
 //                           (CSfM.cpp:823) and the (pts, desc, ..., 0, 7)
 //                           overload (CSfM.cpp:673).
+//   compat_gpu pnp <dir>    solvePnPRansac as CSfM::tracking calls it
+//                           (CSfM.cpp:553-565), cv::Matx31d object points.
+//   compat_gpu brisk <dir>  the detectFeatures body (CTracker.cpp:275-287):
+//                           keypoints as cv::KeyPoint + descriptor rows.
+//   compat_gpu map <dir>    a CMap-shaped store (CMap.cpp:36-381) driven by a
+//                           script of addNewPoints / addPointMatches /
+//                           addDescriptors calls and queries, as CSfM::mapping
+//                           and CSfM::tracking make them.
 #include <cstdint>
 #include <cstdio>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -29,6 +39,7 @@ struct M33 { double val[9]; };              // cv::Matx33d
 struct M31 { double val[3]; };              // cv::Matx31d (CMap::_pts3D element)
 struct Grey { const unsigned char* data; size_t step; int cols, rows; };
 struct Desc { const unsigned char* data; int rows, cols; };   // cv::Mat CV_8U fields used
+struct KeyPoint { Pt2f pt; float size, angle, response; int octave, class_id; };   // cv::KeyPoint
 
 template <class T>
 static std::vector<T> rd(const std::string& dir, const char* name) {
@@ -185,10 +196,176 @@ static int run_match(const std::string& dir) {
   return 0;
 }
 
+// meta.i32 = [n, iterations]; par.f64 = [reprojectionError, confidence];
+// obj.f64 [n][3]; img.f64 [n][2]; K.f64 [9]
+static int run_pnp(const std::string& dir) {
+  auto meta = rd<int32_t>(dir, "meta.i32");
+  auto par = rd<double>(dir, "par.f64");
+  const int n = meta[0], iters = meta[1];
+  auto ob = rd<double>(dir, "obj.f64"), im = rd<double>(dir, "img.f64"), kk = rd<double>(dir, "K.f64");
+  std::vector<M31> currMatch3D(n);
+  std::vector<Pt> currMatch2D(n);
+  for (int i = 0; i < n; ++i) {
+    for (int k = 0; k < 3; ++k) currMatch3D[i].val[k] = ob[3 * i + k];
+    currMatch2D[i] = Pt{im[2 * i], im[2 * i + 1]};
+  }
+  M33 K;
+  for (int k = 0; k < 9; ++k) K.val[k] = kk[k];
+  double rv[3] = {0, 0, 0}, tv[3] = {0, 0, 0};
+  std::vector<int> inlierIdx;
+  const bool found = sfm_compat::solvePnPRansac(currMatch3D, currMatch2D, K, rv, tv, inlierIdx, iters, par[0], par[1]);
+  wr(dir, "out_found.i32", std::vector<int32_t>{found ? 1 : 0});
+  wr(dir, "out_pose.f64", std::vector<double>{rv[0], rv[1], rv[2], tv[0], tv[1], tv[2]});
+  wr(dir, "out_inliers.i32", inlierIdx);
+  return 0;
+}
+
+// meta.i32 = [w, h, threshold, octaves, step]; img.u8 [h][step] (rows padded
+// to `step` bytes, as a cv::Mat ROI of a wider image would be)
+static int run_brisk(const std::string& dir) {
+  auto meta = rd<int32_t>(dir, "meta.i32");
+  auto img = rd<uint8_t>(dir, "img.u8");
+  Grey g{img.data(), size_t(meta[4]), meta[0], meta[1]};
+  std::vector<KeyPoint> kp;
+  std::vector<uint8_t> desc;
+  const int rc = sfm_compat::detectFeatures(g, kp, desc, meta[2], meta[3]);
+  if (rc) { std::printf("brisk rc=%d %s\n", rc, sfm_last_error()); return 1; }
+  std::vector<float> k;
+  std::vector<int32_t> oct;
+  for (auto& p : kp) {
+    k.insert(k.end(), {p.pt.x, p.pt.y, p.size, p.angle, p.response});
+    oct.push_back(p.octave);
+  }
+  wr(dir, "out_kp.f32", k);
+  wr(dir, "out_octave.i32", oct);
+  wr(dir, "out_desc.u8", desc);
+  return 0;
+}
+
+// script.txt: one call per line (see tests/test_gpu_compat.py), answers of
+// the queries to out.txt, one line each.
+static int run_map(const std::string& dir) {
+  std::ifstream in(dir + "/script.txt");
+  std::ofstream out(dir + "/out.txt");
+  sfm_compat::MapStore cmap(64);
+  if (cmap.status()) { std::printf("map create rc=%d\n", cmap.status()); return 1; }
+  std::vector<M31> pts3DHost;  // CMap::_pts3D (host member, the BA pointers' target)
+  std::string line;
+  auto ints = [](std::istringstream& is, int n) { std::vector<int> v(n); for (auto& x : v) is >> x; return v; };
+  auto hexrow = [](const std::string& h) {
+    std::vector<uint8_t> b(h.size() / 2);
+    for (size_t i = 0; i < b.size(); ++i) b[i] = uint8_t(std::stoi(h.substr(2 * i, 2), nullptr, 16));
+    return b;
+  };
+  auto tohex = [](const std::vector<uint8_t>& b) {
+    static const char* hx = "0123456789abcdef";
+    std::string s;
+    for (uint8_t c : b) { s += hx[c >> 4]; s += hx[c & 15]; }
+    return s;
+  };
+  int rc = 0;
+  while (std::getline(in, line)) {
+    std::istringstream is(line);
+    std::string op;
+    is >> op;
+    if (op == "N") {           // addNewPoints: nf n frames[nf] idx2d[nf][n] X[n][3]
+      int nf, n;
+      is >> nf >> n;
+      auto frames = ints(is, nf);
+      std::vector<std::vector<int>> p2(nf);
+      for (auto& v : p2) v = ints(is, n);
+      std::vector<M31> X(n);
+      for (auto& m : X) is >> m.val[0] >> m.val[1] >> m.val[2];
+      std::vector<int> idx;
+      if ((rc = cmap.addNewPoints(X, p2, frames, idx))) break;
+      pts3DHost.insert(pts3DHost.end(), X.begin(), X.end());
+      out << "N";
+      for (int i : idx) out << ' ' << i;
+      out << '\n';
+    } else if (op == "M") {    // addPointMatches: frame n p3[n] p2[n]
+      int f, n;
+      is >> f >> n;
+      auto a = ints(is, n), b = ints(is, n);
+      if ((rc = cmap.addPointMatches(a, b, f))) break;
+    } else if (op == "D") {    // addDescriptors: n p3[n] hex rows
+      int n;
+      is >> n;
+      auto a = ints(is, n);
+      std::vector<uint8_t> rows;
+      for (int i = 0; i < n; ++i) { std::string h; is >> h; auto r = hexrow(h); rows.insert(rows.end(), r.begin(), r.end()); }
+      Desc d{rows.data(), n, 64};
+      if ((rc = cmap.addDescriptors(a, d))) break;
+    } else if (op == "QF") {   // getPointsInFrames: nf frames
+      int nf;
+      is >> nf;
+      auto frames = ints(is, nf);
+      std::vector<int> p;
+      if ((rc = cmap.getPointsInFrames(p, frames))) break;
+      out << "QF";
+      for (int i : p) out << ' ' << i;
+      out << '\n';
+    } else if (op == "Q") {    // getPointsInFrame(pts3DIdx, pts2DIdx, f)
+      int f;
+      is >> f;
+      std::vector<int> a, b;
+      if ((rc = cmap.getPointsInFrame(a, b, f))) break;
+      out << "Q " << a.size();
+      for (int i : a) out << ' ' << i;
+      out << ' ' << b.size();
+      for (int i : b) out << ' ' << i;
+      out << '\n';
+    } else if (op == "QM") {   // getPointsInFrame_Mutable: the pointers, as point indices
+      int f;
+      is >> f;
+      std::vector<double*> ptr;
+      std::vector<int> b;
+      if ((rc = cmap.getPointsInFrame_Mutable(pts3DHost, ptr, b, f))) break;
+      out << "QM " << ptr.size();
+      for (double* q : ptr) out << ' ' << (q - pts3DHost[0].val) / 3;
+      out << ' ' << b.size();
+      for (int i : b) out << ' ' << i;
+      out << '\n';
+    } else if (op == "R") {    // getRepresentativeDescriptors: n p3
+      int n;
+      is >> n;
+      auto a = ints(is, n);
+      std::vector<uint8_t> d;
+      if ((rc = cmap.getRepresentativeDescriptors(a, d))) break;
+      out << "R " << tohex(d) << '\n';
+    } else if (op == "S") {    // setPointsAtIdx (BA write-back): n p3 X
+      int n;
+      is >> n;
+      auto a = ints(is, n);
+      std::vector<M31> X(n);
+      for (auto& m : X) is >> m.val[0] >> m.val[1] >> m.val[2];
+      if ((rc = cmap.setPointsAtIdx(a, X))) break;
+    } else if (op == "G") {    // getPointsAtIdx: n p3
+      int n;
+      is >> n;
+      auto a = ints(is, n);
+      std::vector<M31> X;
+      if ((rc = cmap.getPointsAtIdx(a, X))) break;
+      char buf[64];
+      out << "G";
+      for (auto& m : X)
+        for (double v : m.val) { std::snprintf(buf, sizeof buf, " %.17g", v); out << buf; }
+      out << '\n';
+    } else if (op == "C") {    // getNPoints
+      out << "C " << cmap.getNPoints() << '\n';
+    } else if (!op.empty()) {
+      std::printf("map: bad op %s\n", op.c_str());
+      return 2;
+    }
+  }
+  if (rc) { std::printf("map rc=%d %s\n", rc, sfm_last_error()); return 1; }
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  if (argc != 3) { std::printf("usage: compat_gpu ba|flow|match <dir>\n"); return 64; }
+  if (argc != 3) { std::printf("usage: compat_gpu ba|flow|match|pnp|brisk|map <dir>\n"); return 64; }
   const std::string mode = argv[1], dir = argv[2];
-  int rc = mode == "ba" ? run_ba(dir) : mode == "flow" ? run_flow(dir) : mode == "match" ? run_match(dir) : 64;
+  int rc = mode == "ba" ? run_ba(dir) : mode == "flow" ? run_flow(dir) : mode == "match" ? run_match(dir)
+         : mode == "pnp" ? run_pnp(dir) : mode == "brisk" ? run_brisk(dir) : mode == "map" ? run_map(dir) : 64;
   if (rc == 0) std::printf("compat_gpu %s ok\n", mode.c_str());
   return rc;
 }

@@ -12,7 +12,15 @@ oracle:
     (bit-exact corners and index lists);
   * the frame-resident matcher drop-ins: matchFeatures(prevIdx, currIdx, ...)
     (CSfM.cpp:518), matchFeatures() (CSfM.cpp:823), the (0, 7) window
-    (CSfM.cpp:673) and the one-shot member-window overload (bit-exact).
+    (CSfM.cpp:673) and the one-shot member-window overload (bit-exact);
+  * sfm_compat::solvePnPRansac with cv::Matx31d object points as
+    CSfM::tracking passes them (CSfM.cpp:553-565) vs oracle/pnp_oracle.py
+    (found flag, inlier list, pose 1e-6);
+  * the detectFeatures body (CTracker.cpp:275-287) on a padded-stride frame,
+    keypoints as cv::KeyPoint vs oracle/brisk_oracle.py (bit-exact);
+  * sfm_compat::MapStore, a CMap-shaped wrapper of the device map store,
+    driven through the CMap calls CSfM::mapping / tracking make, every query
+    vs oracle/cmap_oracle.py (exact), the point matched twice included.
 """
 import os
 import subprocess
@@ -137,3 +145,162 @@ def test_matcher_drop_ins(tmp_path):
     a, b = O.match_features(p0, d0, p1, d1)
     assert np.array_equal(ri("out_free_a.i32"), a) and np.array_equal(ri("out_free_b.i32"), b)
     assert len(a) > 300
+
+
+def test_pnp_drop_in_as_tracking_calls_it(tmp_path):
+    from oracle import pnp_oracle as PO
+    from tests.pnp_cases import K, scene as pnp_scene
+    for n, seed, outl, iters, thr in ((600, 3, 0.3, 20, 7.0), (40, 8, 0.1, 100, 2.0), (5, 2, 0.0, 20, 7.0)):
+        d = tmp_path / f"pnp{n}"
+        d.mkdir()
+        X, uv, _, _ = pnp_scene(n, seed, noise=0.5, outliers=outl)
+        _w(d, "meta.i32", np.array([n, iters], np.int32))
+        _w(d, "par.f64", np.array([thr, 0.99]))
+        _w(d, "obj.f64", np.asarray(X, np.float64))
+        _w(d, "img.f64", np.asarray(uv, np.float64))
+        _w(d, "K.f64", np.asarray(K, np.float64).reshape(9))
+        _run("pnp", d)
+        ok, r, t, inl = PO.solve_pnp_ransac(X, uv, K, iterations=iters, reproj_err=thr)
+        assert _r(d, "out_found.i32", np.int32)[0] == int(ok)
+        assert np.array_equal(_r(d, "out_inliers.i32", np.int32), inl)
+        pose = _r(d, "out_pose.f64", np.float64)
+        assert np.max(np.abs(pose[:3] - r)) <= 1e-6 * max(1.0, np.max(np.abs(r)))
+        assert np.max(np.abs(pose[3:] - t)) <= 1e-6 * max(1.0, np.max(np.abs(t)))
+
+
+def test_detect_features_drop_in(tmp_path):
+    from oracle import brisk_oracle as B
+    v = SyntheticVideo()
+    img = v.frame(4)
+    h, w = img.shape
+    step = w + 40                                          # a cv::Mat ROI of a wider image
+    padded = np.full((h, step), 77, np.uint8)
+    padded[:, :w] = img
+    _w(tmp_path, "meta.i32", np.array([w, h, 60, 6, step], np.int32))
+    _w(tmp_path, "img.u8", padded)
+    _run("brisk", tmp_path)
+    kp = _r(tmp_path, "out_kp.f32", np.float32).reshape(-1, 5)
+    oc = _r(tmp_path, "out_octave.i32", np.int32)
+    desc = _r(tmp_path, "out_desc.u8", np.uint8).reshape(-1, 64)
+    ok = B.detect(img)
+    kept, oang, odesc = B.describe(img, ok[:, :3], B.make_pattern())
+    assert len(kp) == len(kept) > 300
+    np.testing.assert_array_equal(kp[:, :3], ok[kept, :3])
+    np.testing.assert_array_equal(kp[:, 3], oang)
+    np.testing.assert_array_equal(kp[:, 4], ok[kept, 3])
+    assert oc.tolist() == ok[kept, 4].astype(int).tolist()
+    assert (desc == odesc).all()
+
+
+def _map_script(seed=5):
+    """CSfM-like call sequence: a two-view bootstrap, then keyframes that
+    add new points seen by (previous, new) and re-find old points, with
+    descriptors per observation; one point is matched twice in a frame
+    (the getPointsInFrame quirk) and queries come between the writes."""
+    rng = np.random.default_rng(seed)
+    lines, n_pts = [], 0
+
+    def hexrows(d):
+        return " ".join(r.tobytes().hex() for r in d)
+
+    def add_new(frames, n):
+        nonlocal n_pts
+        idx2 = rng.integers(0, 2000, (len(frames), n))
+        X = rng.normal(0, 1, (n, 3))
+        lines.append(f"N {len(frames)} {n} " + " ".join(map(str, frames)) + " " +
+                     " ".join(map(str, idx2.ravel())) + " " + " ".join(repr(float(x)) for x in X.ravel()))
+        ids = list(range(n_pts, n_pts + n))
+        n_pts += n
+        for f in frames:
+            d = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+            lines.append(f"D {n} " + " ".join(map(str, ids)) + " " + hexrows(d))
+        return ids
+
+    add_new([0, 10], 300)
+    for kf in (20, 30, 40, 50):
+        add_new([kf - 10, kf], 150)
+        old = rng.choice(n_pts - 150, 120, replace=False)
+        p2 = rng.integers(0, 2000, 120)
+        lines.append(f"M {kf} 120 " + " ".join(map(str, old)) + " " + " ".join(map(str, p2)))
+        d = rng.integers(0, 256, (120, 64), dtype=np.uint8)
+        lines.append(f"D 120 " + " ".join(map(str, old)) + " " + hexrows(d))
+        lines.append(f"Q {kf}")
+        lines.append(f"QF 3 {kf - 20} {kf - 10} {kf}")
+    dup = int(rng.integers(0, n_pts))
+    lines.append(f"M 50 2 {dup} {dup} 1999 1998")           # matched twice more in frame 50
+    q = rng.choice(n_pts, 200, replace=False)
+    for f in (0, 10, 20, 30, 40, 50, 60):
+        lines += [f"Q {f}", f"QM {f}"]
+    lines.append("QF 7 0 10 20 30 40 50 60")
+    lines.append(f"R 200 " + " ".join(map(str, q)))
+    Xn = rng.normal(0, 1, (50, 3))
+    lines.append(f"S 50 " + " ".join(map(str, q[:50])) + " " + " ".join(repr(float(x)) for x in Xn.ravel()))
+    lines.append(f"G 200 " + " ".join(map(str, q)))
+    lines.append("C")
+    return lines
+
+
+def _apply_oracle(lines):
+    from oracle.cmap_oracle import CMapOracle
+    m = CMapOracle()
+    out = []
+    for ln in lines:
+        t = ln.split()
+        op = t[0]
+        if op == "N":
+            nf, n = int(t[1]), int(t[2])
+            frames = list(map(int, t[3:3 + nf]))
+            idx2 = np.array(t[3 + nf:3 + nf + nf * n], int).reshape(nf, n)
+            X = np.array(t[3 + nf + nf * n:], float).reshape(n, 3)
+            out.append("N " + " ".join(map(str, m.addNewPoints(X, idx2, frames))))
+        elif op == "M":
+            f, n = int(t[1]), int(t[2])
+            m.addPointMatches(list(map(int, t[3:3 + n])), list(map(int, t[3 + n:3 + 2 * n])), f)
+        elif op == "D":
+            n = int(t[1])
+            ids = list(map(int, t[2:2 + n]))
+            rows = [np.frombuffer(bytes.fromhex(h), np.uint8) for h in t[2 + n:]]
+            m.addDescriptors(ids, rows)
+        elif op == "QF":
+            nf = int(t[1])
+            out.append("QF " + " ".join(map(str, m.getPointsInFrames(list(map(int, t[2:2 + nf]))))))
+        elif op in ("Q", "QM"):
+            p3, p2 = m.getPointsInFrame(int(t[1]))
+            out.append(f"{op} {len(p3)} " + " ".join(map(str, p3)) + f" {len(p2)} " + " ".join(map(str, p2)))
+        elif op == "R":
+            n = int(t[1])
+            _, rows = m.getRepresentativeDescriptors(list(map(int, t[2:2 + n])))
+            out.append("R " + rows.tobytes().hex())
+        elif op == "S":
+            n = int(t[1])
+            ids = list(map(int, t[2:2 + n]))
+            X = np.array(t[2 + n:], float).reshape(n, 3)
+            for i, p in enumerate(ids):
+                m.pts3D[p] = X[i].copy()
+        elif op == "G":
+            n = int(t[1])
+            X = m.getPointsAtIdx(list(map(int, t[2:2 + n])))
+            out.append("G " + " ".join(repr(float(x)) for x in X.ravel()))
+        elif op == "C":
+            out.append(f"C {len(m.pts3D)}")
+    return out
+
+
+def test_map_store_drop_in_as_csfm_calls_it(tmp_path):
+    lines = _map_script()
+    (tmp_path / "script.txt").write_text("\n".join(lines) + "\n")
+    _run("map", tmp_path)
+    got = (tmp_path / "out.txt").read_text().split("\n")[:-1]
+    want = _apply_oracle(lines)
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        gt, wt = g.split(), w.split()
+        if gt[0] == "G":
+            np.testing.assert_array_equal(np.array(gt[1:], float), np.array(wt[1:], float))
+        else:
+            assert gt == wt, (gt[:8], wt[:8])
+    queries = [ln for ln in lines if ln.split()[0] in ("N", "QF", "Q", "QM", "R", "G", "C")]
+    assert len(queries) == len(want)
+    toks = [w for q, w in zip(queries, want) if q == "Q 50"][-1].split()
+    n3 = int(toks[1])
+    assert int(toks[2 + n3]) > n3                    # the matched-twice 2D surplus

@@ -132,6 +132,29 @@ def test_one_rank_rccl_communicator_is_exact(mode):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.timeout(300)
+def test_one_rank_rccl_communicator_at_c4_is_exact():
+    """C4 (2000 cams / 1M points / 10M obs) through a one-rank RCCL
+    communicator: the 576-MB packed reduced system, U_c and every scalar
+    go through ncclAllReduce (identities on one rank), so the solve must
+    equal the communicator-free C4 solve bitwise."""
+    s = scene.config("C4")
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm1, tr1 = ba.solve()
+        p1 = ba.parameters()
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm2, tr2 = ba.solve()
+        p2 = ba.parameters()
+    assert sm1.num_iterations == sm2.num_iterations >= 2
+    assert sm1.final_cost == sm2.final_cost
+    assert [t["cost"] for t in tr1] == [t["cost"] for t in tr2]
+    for a, b in zip(p1, p2):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("kind", ["cam", "pt", "uv"])
 def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
     """The device-side validation of sfm_ba_set_problem (ba_setup.hip

@@ -87,3 +87,86 @@ def test_sharded_solve_on_one_gpu_matches_single(world, mode):
     assert rel(res[0][4], rot1) < 1e-6 and rel(res[0][5], t1) < 1e-6
     X_sh = np.concatenate([r[6] for r in res])
     assert rel(X_sh, X1) < 1e-6
+
+
+# ---- BASELINE config C4 (2000 cams / 1M points / 10M obs), the config the
+# 8-GPU scaling run uses: the sharded path at full size with two ranks ----
+C4_C, C4_P = 2000, 1_000_000
+C4_SEED = 0x5F3D2017 + 4          # scene.config("C4")
+
+
+def _c4_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    import sfm_amd
+    from sfm_amd import scene
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = C4_P // world
+    sc = scene.generate(C4_C, C4_P, seed=C4_SEED, p_begin=rank * per, p_end=(rank + 1) * per)
+    calls = {"n": 0, "max_count": 0}
+
+    def allreduce(arr, op):
+        calls["n"] += 1
+        calls["max_count"] = max(calls["max_count"], arr.size)
+        t = torch.from_numpy(arr)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM)
+
+    with sfm_amd.BundleAdjuster(0) as ba:
+        ba.set_host_comm(world, rank, allreduce)
+        ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
+        dist.barrier()  # both shards resident before either solves
+        sm, tr = ba.solve()
+        rot, t, X = ba.parameters()
+    q.put((rank, sm.num_iterations, sm.final_cost, [x["step_is_successful"] for x in tr],
+           [x["cost"] for x in tr], rot, t, X, calls["n"], calls["max_count"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_c4_two_rank_sharded_solve_matches_single_rank():
+    """C4 split into two landmark shards (500k points / 5M observations each)
+    on one GPU, cross-rank sums through sfm_ba_set_host_comm: the 12000x12000
+    reduced system goes through the packed all-reduce (72M doubles, 576 MB),
+    every rank factors it and back-substitutes its own 500k points.  Against
+    the single-rank C4 solve: the same accept/reject sequence, per-iteration
+    and final cost within 1e-9, parameters within 1e-6, and bitwise equal
+    cameras on both ranks (the replicated LM decisions)."""
+    import sfm_amd
+    from sfm_amd import scene
+    full = scene.generate(C4_C, C4_P, seed=C4_SEED)
+    with sfm_amd.BundleAdjuster(0) as ba:
+        ba.set_problem(full.uv, full.cam_idx, full.pt_idx, full.K, full.rot, full.t, full.X)
+        sm, tr = ba.solve()
+        rot1, t1, X1 = ba.parameters()
+    del full
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=540) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+
+    def rel(a, b):
+        return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-3)))
+
+    n = 6 * C4_C
+    for r in res:
+        assert r[9] == n * (n + 1) // 2 + n        # the packed S + rhs went through the hook
+        assert r[1] == sm.num_iterations
+        assert r[3] == [x["step_is_successful"] for x in tr]
+        for a, b in zip(r[4], [x["cost"] for x in tr]):
+            assert abs(a - b) <= 1e-9 * b
+        assert abs(r[2] - sm.final_cost) <= 1e-9 * sm.final_cost
+        assert np.array_equal(r[5], res[0][5]) and np.array_equal(r[6], res[0][6])
+    assert rel(res[0][5], rot1) < 1e-6 and rel(res[0][6], t1) < 1e-6
+    assert rel(np.concatenate([r[7] for r in res]), X1) < 1e-6
