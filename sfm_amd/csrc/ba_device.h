@@ -27,6 +27,8 @@ constexpr int kPtL = 10;
 constexpr int kPtS = 16;
 // Cholesky tile size.
 constexpr int kNB = 64;
+// Threads per workgroup of the observation / point kernels.
+constexpr int kThreads = 256;
 
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
@@ -124,7 +126,8 @@ struct DevProblem {
   int2* blk = nullptr;        // [n_blk]
   int32_t* seg = nullptr;     // [n_blk + 1]
   int32_t* bpts = nullptr;    // [n_pairs]
-  int32_t* bperm = nullptr;   // [n_blk] blocks by descending pair count (k_schur_pts wave balance)
+  int32_t* bperm = nullptr;   // [n_bslots] k_schur_pts work order (XCD-aware row groups; -1: empty slot)
+  int64_t n_bslots = 0;
   double* ptS = nullptr;      // [P][kPtS] X 3, scale 3, l10 l20 l21, 1/l_ii 3, z 3, pad
   int32_t schur_pts_sub = 8;  // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
   // per-wave diagonal-block / rhs partials from k_obs_prep_rc ([N_pad/64][27])

@@ -23,7 +23,6 @@ namespace sfm {
 
 namespace {
 
-constexpr int kThreads = 256;
 
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -776,7 +775,7 @@ __device__ __forceinline__ double seg_sum(double v) {
 }
 
 template <int kSub>
-__global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_blk, const int2* __restrict__ blk,
+__global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, const int2* __restrict__ blk,
                                                         const int32_t* __restrict__ seg,
                                                         const int32_t* __restrict__ bpts,
                                                         const double* __restrict__ ptS,
@@ -791,17 +790,21 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_blk, const 
   const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
   // (no early exit: a wave past the end runs empty lists, so every wave
   // reaches the publishing barrier)
-  // bperm: blocks taken in descending pair count, so the kPer segments of a
-  // wave run lists of nearly equal length (the wave steps to the longest)
-  auto blk_at = [&](int64_t k) -> int64_t { return bperm ? int64_t(bperm[k]) : k; };
-  const int64_t b = blk_at(min(wb + g, n_blk - 1));
-  const bool own = wb + g < n_blk;
+  // bperm: the XCD-aware work order of set_problem (blocks of one row group
+  // in the workgroups one XCD is dealt, descending pair count within a row,
+  // so the kPer segments of a wave run lists of nearly equal length); -1 is
+  // an empty slot
+  auto slot_blk = [&](int64_t k) -> int32_t { return k < n_slots ? bperm[k] : -1; };
+  const int32_t bs = slot_blk(wb + g);
+  const bool own = bs >= 0;
+  const int64_t b = own ? bs : 0;
   const int2 cc = blk[b];
   double* cs1 = cst[wv][g];
   double* cs2 = cs1 + kCamS;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    const int2 cq = blk[blk_at(min(wb + q, n_blk - 1))];
+    const int32_t bq = slot_blk(wb + q);
+    const int2 cq = blk[bq >= 0 ? bq : 0];
     stage_cam(cst[wv][q], cq.x, camR, cam, Kc, scale_c, l);
     stage_cam(cst[wv][q] + kCamS, cq.y, camR, cam, Kc, scale_c, l);
   }
@@ -1250,9 +1253,9 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
                                         d.n, 1);
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
-  const int nb = int((d.n_blk + per - 1) / per);
+  const int nb = int((d.n_bslots + per - 1) / per);
 #define SFM_PTS(S_)                                                                                           \
-  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_blk, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
+  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
                                           d.S, d.ld, d.bperm)
   if (sub == 8) SFM_PTS(8);
   else if (sub == 16) SFM_PTS(16);

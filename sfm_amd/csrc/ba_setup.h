@@ -41,6 +41,5 @@ void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm,
                       const int32_t* pt_off, const int64_t* off, int C, uint32_t* key, int32_t* val, hipStream_t s);
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s);
 void launch_blk(int C, int2* blk, hipStream_t s);
-void launch_bperm_keys(int64_t n_blk, const int32_t* seg, uint32_t* key, int32_t* iota, hipStream_t s);
 
 }  // namespace sfm

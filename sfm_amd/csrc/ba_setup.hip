@@ -204,15 +204,6 @@ __global__ __launch_bounds__(kT) void k_blk(int C, int2* __restrict__ blk) {
     blk[rs + c2] = make_int2(c1, c2);
 }
 
-// Blocks by descending pair count: ascending key INT32_MAX - count, stable.
-__global__ __launch_bounds__(kT) void k_bperm_keys(int64_t n_blk, const int32_t* __restrict__ seg,
-                                                   uint32_t* __restrict__ key, int32_t* __restrict__ iota) {
-  const int64_t b = int64_t(blockIdx.x) * kT + threadIdx.x;
-  if (b >= n_blk) return;
-  key[b] = uint32_t(INT32_MAX - (seg[b + 1] - seg[b]));
-  iota[b] = int32_t(b);
-}
-
 int bits_for(uint64_t max_key) {
   int b = 1;
   while (b < 64 && (max_key >> b) != 0) ++b;
@@ -298,9 +289,6 @@ void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* se
 }
 void launch_blk(int C, int2* blk, hipStream_t s) {
   if (C > 0) k_blk<<<dim3(unsigned((C + kT - 1) / kT), unsigned(C)), kT, 0, s>>>(C, blk);
-}
-void launch_bperm_keys(int64_t n_blk, const int32_t* seg, uint32_t* key, int32_t* iota, hipStream_t s) {
-  if (n_blk > 0) k_bperm_keys<<<nblocks(n_blk), kT, 0, s>>>(n_blk, seg, key, iota);
 }
 
 }  // namespace sfm

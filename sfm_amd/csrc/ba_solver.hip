@@ -659,10 +659,20 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
   d.n_blk = int64_t(C) * (C + 1) / 2;
   d.n_pairs = n_pairs;
+  // lanes per Schur block ~ a tenth of the mean pair count, 8..64 (measured
+  // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
+  if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
+    const int v = std::atoi(ss);
+    d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
+  } else {
+    const double avg = d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0;
+    int sub = 8;
+    while (sub < 64 && sub < avg / 10.0) sub *= 2;
+    d.schur_pts_sub = sub;
+  }
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
   ALLOC(d.seg, size_t(d.n_blk) + 1);
   ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
-  ALLOC(d.bperm, std::max<size_t>(1, size_t(d.n_blk)));
   {
     uint32_t *bk_a = nullptr, *bk_b = nullptr;
     int32_t* bv = nullptr;
@@ -682,19 +692,51 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
                       s));
     launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
     launch_blk(C, d.blk, s);
-    launch_bperm_keys(d.n_blk, d.seg, bk_a, iota, s);
-    HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, iota, d.bperm, d.n_blk, uint64_t(INT32_MAX), s));
   }
-  // lanes per Schur block ~ a tenth of the mean pair count, 8..64 (measured
-  // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
-  if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
-    const int v = std::atoi(ss);
-    d.schur_pts_sub = v == 64 ? 64 : v == 32 ? 32 : v == 8 ? 8 : 16;
-  } else {
-    const double avg = d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0;
-    int sub = 8;
-    while (sub < 64 && sub < avg / 10.0) sub *= 2;
-    d.schur_pts_sub = sub;
+  // ---- k_schur_pts work order: XCD-aware.  Block (c1, c2)'s pairs gather
+  // records of points camera c1 sees, so a row c1 (its blocks c2 >= c1) reads
+  // one camera's ~N/C point records (C3: ~0.5 MB).  Rows go to 8 groups of
+  // contiguous rows with equal pair totals; group x's blocks, row by row
+  // (descending pair count within a row, so a wave's kPer blocks run lists of
+  // nearly equal length), fill workgroups x, x + 8, x + 16, ... -- the ones
+  // dealt to one XCD (round-robin placement: a speed assumption only,
+  // MI355X_MICROARCH.md), so a row's records stay in that XCD's L2 while its
+  // blocks run.  Slots past a group's end hold -1 (an empty list).
+  {
+    std::vector<int32_t> seg_h(size_t(d.n_blk) + 1);
+    HCHK(hipMemcpyAsync(seg_h.data(), d.seg, sizeof(int32_t) * seg_h.size(), hipMemcpyDeviceToHost, s));
+    HCHK(hipStreamSynchronize(s));
+    const int per = 64 / d.schur_pts_sub * (kThreads / 64);
+    std::vector<int64_t> row_pairs(size_t(C) + 1, 0);
+    std::vector<int64_t> row_first(size_t(C) + 1, 0);
+    for (int c1 = 0, b = 0; c1 < C; ++c1) {
+      row_first[c1] = b;
+      row_pairs[c1] = seg_h[size_t(b) + size_t(C - c1)] - seg_h[b];
+      b += C - c1;
+    }
+    row_first[C] = d.n_blk;
+    std::vector<std::vector<int32_t>> lists(8);
+    int64_t cum = 0;
+    std::vector<int32_t> row_blocks;
+    for (int c1 = 0; c1 < C; ++c1) {
+      const int x = n_pairs ? int(std::min<int64_t>(7, (8 * (cum + row_pairs[c1] / 2)) / std::max<int64_t>(1, n_pairs))) : c1 % 8;
+      cum += row_pairs[c1];
+      row_blocks.clear();
+      for (int64_t b = row_first[c1]; b < row_first[c1 + 1]; ++b) row_blocks.push_back(int32_t(b));
+      std::stable_sort(row_blocks.begin(), row_blocks.end(), [&](int32_t a, int32_t b) {
+        return seg_h[a + 1] - seg_h[a] > seg_h[b + 1] - seg_h[b];
+      });
+      lists[x].insert(lists[x].end(), row_blocks.begin(), row_blocks.end());
+    }
+    size_t m_max = 0;
+    for (auto& L : lists) m_max = std::max(m_max, (L.size() + per - 1) / per);
+    d.n_bslots = int64_t(std::max<size_t>(1, m_max)) * 8 * per;
+    std::vector<int32_t> slots(size_t(d.n_bslots), -1);
+    for (int x = 0; x < 8; ++x)
+      for (size_t i = 0; i < lists[x].size(); ++i) slots[((i / per) * 8 + x) * per + i % per] = lists[x][i];
+    ALLOC(d.bperm, slots.size());
+    HCHK(hipMemcpyAsync(d.bperm, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, s));
+    HCHK(hipStreamSynchronize(s));
   }
   // ---- parameters, per-iteration arrays, dense system ----
   d.n = 6 * C;
