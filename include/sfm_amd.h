@@ -282,6 +282,14 @@ int sfm_map_points_in_frames(sfm_map* h, int32_t n_frames, const int32_t* frame_
  * point has in the frame (so n2 > n3 when a point was matched twice). */
 int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int32_t* pts3d_idx, int32_t* n3_out,
                             int32_t* pts2d_idx, int32_t* n2_out);
+/* The BA gather of CSfM::bundleAdjustment (CSfM.cpp:321-340): getPointsInFrame
+ * for every frame of frame_no (distinct) in ONE call.  Frame i's output of
+ * sfm_map_points_in_frame is pts3d_idx[off3[i] .. off3[i+1]) and
+ * pts2d_idx[off2[i] .. off2[i+1]); off3 / off2 [n_frames + 1].  Capacity
+ * bounds both arrays; when it is too small the totals are still set in
+ * off3[n_frames] / off2[n_frames] and SFM_EINVAL is returned. */
+int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* frame_no, int64_t capacity,
+                                  int32_t* pts3d_idx, int32_t* off3, int32_t* pts2d_idx, int32_t* off2);
 /* CMap::getRepresentativeDescriptors (CMap.cpp:345-381) from the resident
  * rows: desc_out [n][desc_bytes]; best_row (optional) = the row within the
  * point's rows (append order), first on ties.  Every point needs a row. */

@@ -165,6 +165,8 @@ _SIGNATURES = {
     "sfm_map_points_in_frames": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, POINTER(c_int32)]),
     "sfm_map_points_in_frame": (c_int, [c_void_p, c_int32, c_int32, c_void_p, POINTER(c_int32), c_void_p,
                                         POINTER(c_int32)]),
+    "sfm_map_points_in_frame_multi": (c_int, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]),
     "sfm_map_representative_descriptors": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "sfm_pnp_ransac": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_double, c_double,
                                c_void_p, c_void_p, c_void_p, POINTER(c_int32), POINTER(c_int32)]),

@@ -151,6 +151,26 @@ class DeviceMap:
         check(rc, "sfm_map_points_in_frame")
         return p3[:n3.value].copy(), p2[:n2.value].copy()
 
+    def getPointsInFrameMulti(self, frameNo):
+        """[(pts3DIdx, pts2DIdx) of getPointsInFrame(f) for f in frameNo], in
+        one device query (the per-keyframe gather of CSfM::bundleAdjustment,
+        CSfM.cpp:321-340)."""
+        fr = np.ascontiguousarray(np.asarray(frameNo, np.int32).reshape(-1))
+        nf = len(fr)
+        off3 = np.zeros(nf + 1, np.int32)
+        off2 = np.zeros(nf + 1, np.int32)
+        cap = max(1, self.size()[1])
+        for _ in range(2):
+            p3 = np.zeros(cap, np.int32)
+            p2 = np.zeros(cap, np.int32)
+            rc = lib().sfm_map_points_in_frame_multi(self._h, nf, ptr(fr), cap, ptr(p3), ptr(off3), ptr(p2), ptr(off2))
+            need = int(max(off3[-1], off2[-1]))
+            if rc == 0 or need <= cap:
+                break
+            cap = need
+        check(rc, "sfm_map_points_in_frame_multi")
+        return [(p3[off3[i]:off3[i + 1]].copy(), p2[off2[i]:off2[i + 1]].copy()) for i in range(nf)]
+
     def getRepresentativeDescriptors(self, pts3DIdx, return_best: bool = False):
         a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
         out = np.zeros((max(1, len(a)), self.desc_bytes), np.uint8)

@@ -15,16 +15,18 @@
 //                                       twice in a frame yields 2 x 2)
 //   getRepresentativeDescriptors  CMap.cpp:345-381 (CSfM.cpp:669)
 //
-// Layout: observations are kept in global emplace order, which is the
-// multimap's order within one key (std::multimap inserts at the upper bound
-// of the equal range) and the order of each point's _frameNo/_pts2DIdx
-// lists.  Descriptor rows are kept in append order with their point.  The
+// Layout: observations are kept in global emplace order, which is taken as
+// the multimap's order within one key (the reference's container is an
+// unordered_multimap, CMap.h:96-97, whose equal_range order is
+// implementation-defined; libc++, the reference's toolchain, keeps insertion
+// order) and is the order of each point's _frameNo/_pts2DIdx lists.  Descriptor rows are kept in append order with their point.  The
 // per-point CSRs (observations, descriptor rows) are rebuilt lazily by a
 // stable radix sort after appends.  Queries are flag + stable compaction
 // (hipcub DeviceSelect), so every result keeps the reference's order.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <map>
 #include <string>
@@ -59,6 +61,22 @@ __global__ void k_flag_frame(int64_t n, const int32_t* __restrict__ ob_frame, in
   if (e < n) flag[e] = ob_frame[e] == f;
 }
 
+// rank of each observation's frame in the query list (fr sorted by frame,
+// with the query position alongside), nf when the frame is not queried
+__global__ void k_frame_rank(int64_t n, const int32_t* __restrict__ ob_frame, const int2* __restrict__ fr, int nf,
+                             uint32_t* __restrict__ key, int32_t* __restrict__ iota) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int f = ob_frame[e];
+  int lo = 0, hi = nf;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (fr[mid].x < f) lo = mid + 1; else hi = mid;
+  }
+  key[e] = uint32_t(lo < nf && fr[lo].x == f ? fr[lo].y : nf);
+  iota[e] = int32_t(e);
+}
+
 __global__ void k_count_keys(int64_t n, const int32_t* __restrict__ key, int32_t* __restrict__ cnt) {
   const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (e < n) atomicAdd(cnt + key[e], 1);
@@ -77,8 +95,9 @@ __global__ void k_dup_count(int n_sel, const int32_t* __restrict__ sel, const in
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_sel) return;
   const int p = ob_pt[sel[e]];
+  const int fe = f == INT32_MIN ? ob_frame[sel[e]] : f;  // INT32_MIN: the entry's own frame (multi-frame query)
   int c = 0;
-  for (int q = ooff[p]; q < ooff[p + 1]; ++q) c += ob_frame[orow[q]] == f;
+  for (int q = ooff[p]; q < ooff[p + 1]; ++q) c += ob_frame[orow[q]] == fe;
   cnt[e] = c;
 }
 
@@ -89,11 +108,12 @@ __global__ void k_dup_fill(int n_sel, const int32_t* __restrict__ sel, const int
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_sel) return;
   const int p = ob_pt[sel[e]];
+  const int fe = f == INT32_MIN ? ob_frame[sel[e]] : f;
   out3[e] = p;
   int w = off2[e];
   for (int q = ooff[p]; q < ooff[p + 1]; ++q) {
     const int o = orow[q];
-    if (ob_frame[o] == f) out2[w++] = ob_idx[o];
+    if (ob_frame[o] == fe) out2[w++] = ob_idx[o];
   }
 }
 
@@ -487,6 +507,85 @@ int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int3
       (n2 && hipMemcpy(pts2d_idx, out2, sizeof(int32_t) * size_t(n2), hipMemcpyDeviceToHost) != hipSuccess))
     return mapfail(SFM_EIO, "download failed");
   return 0;
+}
+
+int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* frame_no, int64_t capacity,
+                                  int32_t* pts3d_idx, int32_t* off3, int32_t* pts2d_idx, int32_t* off2) {
+  if (!h || !off3 || !off2 || (n_frames > 0 && !frame_no)) return mapfail(SFM_EINVAL, "NULL argument");
+  if (n_frames < 0) return mapfail(SFM_EINVAL, "negative size");
+  for (int i = 0; i <= n_frames; ++i) off3[i] = off2[i] = 0;
+  const int64_t N = h->ob_pt.n;
+  if (N == 0 || n_frames == 0) return 0;
+  std::vector<int2> fr(static_cast<size_t>(n_frames));
+  for (int i = 0; i < n_frames; ++i) fr[i] = make_int2(frame_no[i], i);
+  std::sort(fr.begin(), fr.end(), [](int2 a, int2 b) { return a.x < b.x || (a.x == b.x && a.y < b.y); });
+  for (int i = 1; i < n_frames; ++i)
+    if (fr[i].x == fr[i - 1].x) return mapfail(SFM_EINVAL, "frame " + std::to_string(fr[i].x) + " queried twice");
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  if (!h->ocsr) {
+    if (int r = build_csr(h, "ob", h->ob_pt.p, N, &h->orow, &h->ooff)) return r;
+    h->ocsr = true;
+  }
+  // every observation keyed by its frame's position in the query list; a
+  // stable sort groups them frame by frame, each frame's in emplace order
+  // (its equal_range)
+  auto* dfr = static_cast<int2*>(scratch(h, "mfr", sizeof(int2) * size_t(n_frames), &rc));
+  auto* key = static_cast<uint32_t*>(scratch(h, "mk", sizeof(uint32_t) * size_t(N), &rc));
+  auto* key2 = static_cast<uint32_t*>(scratch(h, "mk2", sizeof(uint32_t) * size_t(N), &rc));
+  auto* iv = static_cast<int32_t*>(scratch(h, "mi", sizeof(int32_t) * size_t(N), &rc));
+  auto* sel = static_cast<int32_t*>(scratch(h, "msel", sizeof(int32_t) * size_t(N), &rc));
+  auto* fcnt = static_cast<int32_t*>(scratch(h, "mfc", sizeof(int32_t) * (size_t(n_frames) + 1), &rc));
+  if (rc) return rc;
+  (void)hipMemcpyAsync(dfr, fr.data(), sizeof(int2) * fr.size(), hipMemcpyHostToDevice, h->s);
+  (void)hipMemsetAsync(fcnt, 0, sizeof(int32_t) * (size_t(n_frames) + 1), h->s);
+  k_frame_rank<<<grid(N), 256, 0, h->s>>>(N, h->ob_frame.p, dfr, n_frames, key, iv);
+  k_count_keys<<<grid(N), 256, 0, h->s>>>(N, reinterpret_cast<const int32_t*>(key), fcnt);
+  int bits = 1;
+  while ((1 << bits) <= n_frames) ++bits;
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, key, key2, iv, sel, int(N), 0, bits, h->s);
+  void* tmp = scratch(h, "msort", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, bytes, key, key2, iv, sel, int(N), 0, bits, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "sort failed");
+  std::vector<int32_t> cnt_h(size_t(n_frames) + 1);
+  (void)hipMemcpyAsync(cnt_h.data(), fcnt, sizeof(int32_t) * cnt_h.size(), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  for (int i = 0; i < n_frames; ++i) off3[i + 1] = off3[i] + cnt_h[i];
+  const int32_t n = off3[n_frames];
+  if (n == 0) return 0;
+  // per entry: how many 2D indices its point has in the entry's frame
+  auto* cnt = static_cast<int32_t*>(scratch(h, "mcnt", sizeof(int32_t) * size_t(n), &rc));
+  auto* eoff = static_cast<int32_t*>(scratch(h, "moff", sizeof(int32_t) * size_t(n), &rc));
+  auto* out3 = static_cast<int32_t*>(scratch(h, "mo3", sizeof(int32_t) * size_t(n), &rc));
+  if (rc) return rc;
+  k_dup_count<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->orow, h->ooff, INT32_MIN, cnt);
+  bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, eoff, n, h->s);
+  tmp = scratch(h, "mscan", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, eoff, n, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "scan failed");
+  std::vector<int32_t> ecnt(static_cast<size_t>(n));
+  (void)hipMemcpyAsync(ecnt.data(), cnt, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  for (int i = 0; i < n_frames; ++i) {
+    int32_t s2 = 0;
+    for (int32_t e = off3[i]; e < off3[i + 1]; ++e) s2 += ecnt[e];
+    off2[i + 1] = off2[i] + s2;
+  }
+  const int32_t n2 = off2[n_frames];
+  if (int64_t(n) > capacity || int64_t(n2) > capacity)
+    return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(std::max(n, n2)));
+  if (!pts3d_idx || !pts2d_idx) return mapfail(SFM_EINVAL, "NULL output");
+  auto* out2 = static_cast<int32_t*>(scratch(h, "mo2", sizeof(int32_t) * size_t(std::max(n2, 1)), &rc));
+  if (rc) return rc;
+  k_dup_fill<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->ob_idx.p, h->orow, h->ooff, INT32_MIN,
+                                        eoff, out3, out2);
+  (void)hipMemcpyAsync(pts3d_idx, out3, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
+  if (n2) (void)hipMemcpyAsync(pts2d_idx, out2, sizeof(int32_t) * size_t(n2), hipMemcpyDeviceToHost, h->s);
+  return sync(h);
 }
 
 int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,

@@ -353,8 +353,9 @@ class LiveSfM:
         keyframe, CMap::getPointsInFrame on the device map store, parameter
         blocks deduplicated first-seen, one-shot sfm_ba_solve, write-back."""
         uv, cam, p3 = [], [], []
+        per_frame = self.map.getPointsInFrameMulti([kf.no for kf in self.kfs])
         for c, kf in enumerate(self.kfs):
-            a3, a2 = self.map.getPointsInFrame(kf.no)
+            a3, a2 = per_frame[c]
             # Deliberate departure from the reference: CSfM.cpp:331-340 appends
             # pts3d and pts2d over ALL frames and pairs them globally, so after
             # a point matched twice in one keyframe (getPointsInFrame emits k^2

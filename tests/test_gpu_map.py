@@ -117,6 +117,38 @@ def test_points_in_frame_when_2d_list_outgrows_observations():
         dm.close()
 
 
+def test_points_in_frame_multi_equals_per_frame_queries():
+    """The one-call BA gather (sfm_map_points_in_frame_multi) against one
+    getPointsInFrame per frame and the oracle, duplicates included."""
+    import sfm_amd
+    from oracle.cmap_oracle import CMapOracle
+    rng = np.random.default_rng(3)
+    dm = sfm_amd.DeviceMap(64)
+    om = CMapOracle()
+    try:
+        for m in (dm, om):
+            m.addNewPoints(rng.normal(0, 1, (40, 3)), rng.integers(0, 500, (2, 40)), [0, 10])
+        for f in (20, 30):
+            idx = rng.choice(40, 25, replace=False)
+            p2 = rng.integers(0, 500, 25)
+            for m in (dm, om):
+                m.addPointMatches(idx, p2, f)
+        for m in (dm, om):
+            m.addPointMatches([3, 3, 7], [1, 2, 3], 30)
+        frames = [30, 0, 20, 10, 99]
+        multi = dm.getPointsInFrameMulti(frames)
+        for f, (a3, a2) in zip(frames, multi):
+            b3, b2 = dm.getPointsInFrame(f)
+            o3, o2 = om.getPointsInFrame(f)
+            assert a3.tolist() == b3.tolist() == list(o3)
+            assert a2.tolist() == b2.tolist() == list(o2)
+        assert len(multi[-1][0]) == 0
+        with pytest.raises(Exception):
+            dm.getPointsInFrameMulti([10, 10])
+    finally:
+        dm.close()
+
+
 def test_set_points_round_trip_and_errors():
     import sfm_amd
     dm = sfm_amd.DeviceMap(64)
