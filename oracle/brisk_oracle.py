@@ -8,7 +8,10 @@ BRISK 2 library, which is NOT in /root/reference (no source, no fixtures):
 parity against it is UNPINNED.  What is restated here is BRISK as published
 (Leutenegger, Chli, Siegwart, "BRISK: Binary Robust Invariant Scalable
 Keypoints", ICCV 2011) in the form of its reference implementation (the
-code OpenCV ships as cv::BRISK, version 1 of the same authors' library):
+code OpenCV ships as cv::BRISK, version 1 of the same authors' library).
+What the reference's BRISK 2 / briskV2 descriptor changes over version 1
+is not documented in any published description available here, so no
+difference is restated (unpinned):
 
 Descriptor (BRISK_Impl::generateKernel / smoothedIntensity /
 computeDescriptorsAndOrOrientation):
@@ -25,14 +28,41 @@ computeDescriptorsAndOrOrientation):
   quantised orientation (64 bytes for the 512 short pairs of this pattern);
 * keypoints nearer the border than the scale's pattern size are removed.
 
-Detector (BriskScaleSpace): 2 * octaves layers (c_i: halving; d_i: 2/3 of
-c_0, then halving; OpenCV resizes INTER_AREA), FAST 9-16 corner score
-(OpenCV's cornerScore<16>) per layer, candidates with score >= threshold
-that are 3x3 maxima of their layer and not below the score at the same
-position of the layers above and below (nearest sample), refined by
-BRISK's subpixel2D quadratic fit.  The published detector's 3-D refinement
-(refine3D with interpolated neighbour-layer scores) is replaced by that
-nearest-sample scale test: documented simplification, unpinned either way.
+Detector (BriskScaleSpace::constructPyramid / getKeypoints / refine3D):
+* pyramid: 2 * octaves layers, c_0 the image, d_0 = 2/3 of it, every later
+  layer half the one two before; each resampled by OpenCV 3.0's
+  resize(INTER_AREA) (what cv::BRISK's halfsample / twothirdsample call):
+  the exact 2x2 average (a + b + c + d + 2) >> 2 when both ratios are 2,
+  else the general area filter (computeResizeAreaTab's float weights,
+  float accumulation in table order, cvRound);
+* candidates: FAST 9-16 corners at the threshold after FAST's own 3x3
+  non-maximum suppression (strictly above every neighbouring corner score),
+  in FAST's row-major order; BRISK's isMax2D on the layer's score image
+  then always passes (a suppressed neighbour scores strictly lower and a
+  non-corner scores below the threshold), so it is not restated;
+* scores: s(x, y) = cornerScore<16> with threshold 0, kept when >= 1
+  (BriskLayer::getAgastScore(x, y, 1)), 0 within 3 pixels of the border;
+  between pixels, the bilinear float interpolation of getAgastScore(xf, yf)
+  truncated to uchar; layer 0's virtual lower layer uses the 5-8 score
+  (cornerScore<8>, radius 1, getAgastScore_5_8);
+* 3-D non-maximum suppression and scale refinement (refine3D): the
+  interpolated scores of the neighbouring layers over the candidate's
+  footprint (getScoreMaxAbove / getScoreMaxBelow, with the footprint
+  transforms derived from the layers' scale and offset), any sample above
+  the candidate's score rejects it; subpixel2D on the best neighbour-layer
+  sample and on the candidate's own 3x3; a parabola through the three
+  layers' maxima gives the scale (refine1D at 3/4, 1, 3/2 around an octave,
+  refine1D_1 at 2/3, 1, 4/3 around an intra-octave, refine1D_2 at 2/3, 1,
+  3/2 on layer 0), the position is interpolated between the layers'
+  subpixel offsets; kept when the refined score exceeds the threshold;
+  the last layer is refined in 2-D against the layer below only.
+Choices where the published description leaves the arithmetic open (and
+the reference's library cannot be consulted): every footprint sample is
+tested against the candidate's score (all rows); the below-layer offsets
+map back through the exact inverse transforms; the layer-0 virtual layer
+sits at scale 2/3 (refine1D_2's sample points); a negative cornerScore
+(no corner even at threshold 0) is taken as 0, not wrapped to 255 by a
+uchar cast; keypoint size = 12 x scale (BRISK's basicSize).
 """
 from __future__ import annotations
 
@@ -237,26 +267,59 @@ _CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
            (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]  # (x, y), OpenCV offsets16
 
 
-def halfsample(img):
-    """2x area average, (a + b + c + d + 2) >> 2 (an odd last row / column is dropped)."""
-    h2, w2 = img.shape[0] // 2, img.shape[1] // 2
-    a = img[:2 * h2, :2 * w2].astype(np.int32)
-    s = a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2]
-    return ((s + 2) >> 2).astype(np.uint8)
+def _area_tab(ssize: int, dsize: int, scale: float):
+    """computeResizeAreaTab (OpenCV 3.0 imgwarp.cpp) for one axis: per
+    destination index the (source index, float32 weight) entries in table
+    order (double geometry, float weights)."""
+    tab = [[] for _ in range(dsize)]
+    for dx in range(dsize):
+        fsx1 = dx * scale
+        fsx2 = fsx1 + scale
+        cell = min(scale, ssize - fsx1)
+        sx1, sx2 = math.ceil(fsx1), math.floor(fsx2)
+        sx2 = min(sx2, ssize - 1)
+        sx1 = min(sx1, sx2)
+        if sx1 - fsx1 > 1e-3:
+            tab[dx].append((sx1 - 1, np.float32((sx1 - fsx1) / cell)))
+        for sx in range(sx1, sx2):
+            tab[dx].append((sx, np.float32(1.0 / cell)))
+        if fsx2 - sx2 > 1e-3:
+            tab[dx].append((sx2, np.float32(min(min(fsx2 - sx2, 1.0), cell) / cell)))
+    return tab
 
 
-def twothirdsample(img):
-    """2/3 area average: every 3x3 block -> 2x2 with weights (4, 2, 2, 1) / 9,
-    rounded ((x + 4) / 9); the remainder rows / columns are dropped."""
-    h3, w3 = img.shape[0] // 3, img.shape[1] // 3
-    a = img[:3 * h3, :3 * w3].astype(np.int32)
-    p = [[a[r::3, c::3] for c in range(3)] for r in range(3)]
-    out = np.zeros((2 * h3, 2 * w3), np.int32)
-    out[0::2, 0::2] = 4 * p[0][0] + 2 * p[0][1] + 2 * p[1][0] + p[1][1]
-    out[0::2, 1::2] = 4 * p[0][2] + 2 * p[0][1] + 2 * p[1][2] + p[1][1]
-    out[1::2, 0::2] = 4 * p[2][0] + 2 * p[1][0] + 2 * p[2][1] + p[1][1]
-    out[1::2, 1::2] = 4 * p[2][2] + 2 * p[1][2] + 2 * p[2][1] + p[1][1]
-    return ((out + 4) // 9).astype(np.uint8)
+def area_resize(img, dw: int, dh: int):
+    """resize(img, (dw, dh), INTER_AREA) for 8-bit downscaling, OpenCV 3.0:
+    ratios of exactly 2 take resizeAreaFast's (a + b + c + d + 2) >> 2; any
+    other ratio the general area filter: per source row, buf[dx] += S * alpha
+    (float32, table order), per destination row sum = sum of beta * buf
+    (float32, table order), then cvRound (half to even)."""
+    sh, sw = img.shape
+    scale_x = 1.0 / (dw / sw)
+    scale_y = 1.0 / (dh / sh)
+    if scale_x == 2.0 and scale_y == 2.0:
+        a = img[:2 * dh, :2 * dw].astype(np.int32)
+        s4 = a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2]
+        return ((s4 + 2) >> 2).astype(np.uint8)
+    xt, yt = _area_tab(sw, dw, scale_x), _area_tab(sh, dh, scale_y)
+    kx = max(len(t) for t in xt)
+    xs = np.zeros((kx, dw), np.int64)
+    xa = np.zeros((kx, dw), np.float32)
+    for dx, t in enumerate(xt):
+        for k, (sx, al) in enumerate(t):
+            xs[k, dx], xa[k, dx] = sx, al
+    out = np.zeros((dh, dw), np.uint8)
+    f = np.float32
+    for dy, t in enumerate(yt):
+        acc = np.zeros(dw, np.float32)
+        for sy, beta in t:
+            row = img[sy].astype(np.float32)
+            buf = np.zeros(dw, np.float32)
+            for k in range(kx):  # padding entries add 0 * S = 0 (exact)
+                buf = (buf + (row[xs[k]] * xa[k]).astype(f)).astype(f)
+            acc = (acc + (f(beta) * buf).astype(f)).astype(f)
+        out[dy] = np.clip(np.rint(acc), 0, 255).astype(np.uint8)
+    return out
 
 
 def pyramid(img, octaves: int = 6):
@@ -265,13 +328,15 @@ def pyramid(img, octaves: int = 6):
     f32 = np.float32
     L = [(np.ascontiguousarray(img, np.uint8), f32(1.0), f32(0.0))]
     n = max(1, 2 * octaves)
+    h, w = img.shape
     if n > 1:
         s = f32(1.5)
-        L.append((twothirdsample(img), s, f32(f32(0.5) * s - f32(0.5))))
+        L.append((area_resize(img, 2 * (w // 3), 2 * (h // 3)), s, f32(f32(0.5) * s - f32(0.5))))
     for i in range(2, n, 2):
         for b in (i - 2, i - 1):
             s = f32(L[b][1] * f32(2.0))
-            L.append((halfsample(L[b][0]), s, f32(f32(0.5) * s - f32(0.5))))
+            src = L[b][0]
+            L.append((area_resize(src, src.shape[1] // 2, src.shape[0] // 2), s, f32(f32(0.5) * s - f32(0.5))))
     return L
 
 
@@ -295,26 +360,43 @@ def fast_score(img):
     return R
 
 
-def _is_max2d(S, x, y):
-    """BriskScaleSpace::isMax2D on the thresholded score map S."""
-    c = S[y, x]
-    nb = [(-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1)]
-    for dx, dy in nb:
-        if S[y + dy, x + dx] > c:
-            return False
-    eq = [(dx, dy) for dx, dy in nb if S[y + dy, x + dx] == c]
-    if not eq:
-        return True
+_CIRCLE8 = [(1, 0), (1, 1), (0, 1), (-1, 1), (-1, 0), (-1, -1), (0, -1), (1, -1)]  # OpenCV offsets8
 
-    def smooth(cx, cy):
-        w = ((1, 2, 1), (2, 4, 2), (1, 2, 1))
-        return sum(w[j][i] * int(S[cy - 1 + j, cx - 1 + i]) for j in range(3) for i in range(3))
 
-    sc = smooth(x, y)
-    for dx, dy in eq:
-        if smooth(x + dx, y + dy) > sc:
-            return False
-    return True
+def fast58_score(img):
+    """BriskLayer::getAgastScore_5_8(x, y, 1): cornerScore<8> (5 contiguous
+    of the 8 radius-1 neighbours) with threshold 0, kept when >= 1; 0 within
+    2 pixels of the border."""
+    h, w = img.shape
+    R = np.zeros((h, w), np.int32)
+    if h < 5 or w < 5:
+        return R
+    v = img[2:h - 2, 2:w - 2].astype(np.int32)
+    d = np.stack([v - img[2 + dy:h - 2 + dy, 2 + dx:w - 2 + dx].astype(np.int32) for (dx, dy) in _CIRCLE8])
+    dark = np.full(v.shape, -10 ** 6, np.int32)
+    bright = np.full(v.shape, -10 ** 6, np.int32)
+    for st in range(8):
+        arc = d[[(st + m) % 8 for m in range(5)]]
+        dark = np.maximum(dark, arc.min(0))
+        bright = np.maximum(bright, (-arc).min(0))
+    sc = np.maximum(np.maximum(dark, bright), 0) - 1
+    R[2:h - 2, 2:w - 2] = np.where(sc >= 1, sc, 0)
+    return R
+
+
+def fast_nms_candidates(R, threshold: int):
+    """FAST 9-16 corners at `threshold` after FAST's 3x3 non-maximum
+    suppression (strictly above every neighbouring corner's score), in
+    row-major order -> (ys, xs)."""
+    S = np.where(R >= threshold, R, 0)
+    h, w = S.shape
+    keep = S > 0
+    P = np.pad(S, 1)
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            if dx or dy:
+                keep &= S > P[1 + dy:1 + dy + h, 1 + dx:1 + dx + w]
+    return np.nonzero(keep)
 
 
 def subpixel2d(s):
@@ -388,41 +470,234 @@ def subpixel2d(s):
     return dx, dy, quad(dx, dy)
 
 
-def detect(img, threshold: int = 60, octaves: int = 6):
-    """-> keypoints [n][5] (x, y, size, response, octave) float32, in layer
-    order, row-major within a layer (the order BRISK emits them)."""
+class _Layer:
+    def __init__(self, img, scale, offset):
+        self.img, self.scale, self.offset = img, scale, offset
+        self.h, self.w = img.shape
+        self.R = fast_score(img)
+
+    def score(self, x: int, y: int) -> int:
+        """getAgastScore(x, y, 1)"""
+        if x < 3 or y < 3 or x >= self.w - 3 or y >= self.h - 3:
+            return 0
+        return int(self.R[y, x])
+
+    def score_f(self, xf, yf) -> int:
+        """getAgastScore(xf, yf, 1, scale 1): bilinear in float32, truncated
+        to uchar (int() truncates toward zero, as the C++ casts)."""
+        f = np.float32
+        xf, yf = f(xf), f(yf)
+        x, y = int(xf), int(yf)
+        rx1 = f(xf - f(x))
+        rx = f(f(1.0) - rx1)
+        ry1 = f(yf - f(y))
+        ry = f(f(1.0) - ry1)
+        v = f(f(rx * ry) * f(self.score(x, y)))
+        v = f(v + f(f(rx1 * ry) * f(self.score(x + 1, y))))
+        v = f(v + f(f(rx * ry1) * f(self.score(x, y + 1))))
+        v = f(v + f(f(rx1 * ry1) * f(self.score(x + 1, y + 1))))
+        return int(v) & 0xFF
+
+
+def _patch(get, cx, cy):
+    """s[i][j] = score at (cx + i - 1, cy + j - 1) (subpixel2D's s_i_j)."""
+    return [[get(cx + i - 1, cy + j - 1) for j in range(3)] for i in range(3)]
+
+
+def _footprint(layer: int, x: int, y: int, above: bool):
+    """The candidate's footprint in the neighbouring layer (float32 bounds),
+    from the layers' scale / offset: octave layer -> intra above (x'' =
+    (4x - 1) / 6, +-2/6) or intra below (x' = (8x + 1) / 6, +-4/6); intra
+    layer -> octave above ((6x - 1) / 8, +-3/8) or octave below ((6x + 1) /
+    4, +-3/4)."""
     f = np.float32
-    L = pyramid(img, octaves)
-    R = [fast_score(l[0]) for l in L]
-    S = [np.where(r >= threshold, r, 0) for r in R]
+    if above:
+        a, b, c, d = (4, -1, 2, 6) if layer % 2 == 0 else (6, -1, 3, 8)
+    else:
+        a, b, c, d = (8, 1, 4, 6) if layer % 2 == 0 else (6, 1, 3, 4)
+    return (f(f(a * x + b - c) / f(d)), f(f(a * x + b + c) / f(d)),
+            f(f(a * y + b - c) / f(d)), f(f(a * y + b + c) / f(d)))
+
+
+def _back(layer: int, real: np.float32, coord: int, above: bool):
+    """The neighbouring layer's coordinate mapped back to this layer, minus
+    the candidate's (the inverse of _footprint's transform)."""
+    f = np.float32
+    if above:
+        m, o, dv = (6, 1, 4) if layer % 2 == 0 else (8, 1, 6)
+    else:
+        m, o, dv = (6, -1, 8) if layer % 2 == 0 else (4, -1, 6)
+    return f(f(f(f(real * f(m)) + f(o)) / f(dv)) - f(coord))
+
+
+def score_max_neighbour(L, layer: int, x: int, y: int, thr: int, above: bool):
+    """getScoreMaxAbove / getScoreMaxBelow: -> (ismax, score, dx, dy).
+    Scans the footprint (corners and edges interpolated, inner samples on
+    the grid) in BRISK's order; any sample above `thr` (the candidate's
+    score) rejects."""
+    f = np.float32
+    M = L[layer + 1] if above else L[layer - 1]
+    x_1, x1, y_1, y1 = _footprint(layer, x, y, above)
+    ix_1, ix1, iy_1, iy1 = int(x_1), int(x1), int(y_1), int(y1)
+    max_x, max_y = ix_1 + 1, iy_1 + 1
+    best = f(M.score_f(x_1, y_1))
+    if best > thr:
+        return False, f(0), f(0), f(0)
+
+    def take(v, mx, my):
+        nonlocal best, max_x, max_y
+        if v > best:
+            best, max_x, max_y = v, mx, my
+
+    for xx in range(ix_1 + 1, ix1 + 1):
+        v = f(M.score_f(f(xx), y_1))
+        if v > thr:
+            return False, f(0), f(0), f(0)
+        take(v, xx, max_y)
+    v = f(M.score_f(x1, y_1))
+    if v > thr:
+        return False, f(0), f(0), f(0)
+    take(v, ix1, max_y)
+    for yy in range(iy_1 + 1, iy1 + 2):  # middle rows, then the bottom row at y1
+        last = yy == iy1 + 1
+        yv = y1 if last else f(yy)
+        yi = iy1 if last else yy
+        v = f(M.score_f(x_1, yv))
+        if v > thr:
+            return False, f(0), f(0), f(0)
+        take(v, int(f(x_1 + f(1.0))), yi)
+        for xx in range(ix_1 + 1, ix1 + 1):
+            v = f(M.score(xx, yy)) if not last else f(M.score_f(f(xx), yv))
+            if v > thr:
+                return False, f(0), f(0), f(0)
+            take(v, xx, yi)
+        v = f(M.score_f(x1, yv))
+        if v > thr:
+            return False, f(0), f(0), f(0)
+        take(v, ix1, yi)
+    dx1, dy1, refined = subpixel2d(_patch(M.score, max_x, max_y))
+    real_x = f(f(max_x) + dx1)
+    real_y = f(f(max_y) + dy1)
+    ret_refined = True
+    if real_x > x1:
+        ret_refined, real_x = False, x1
+    if real_x < x_1:
+        ret_refined, real_x = False, x_1
+    if real_y > y1:
+        ret_refined, real_y = False, y1
+    if real_y < y_1:
+        ret_refined, real_y = False, y_1
+    dx = _back(layer, real_x, x, above)
+    dy = _back(layer, real_y, y, above)
+    dx = f(min(max(dx, f(-1.0)), f(1.0)))
+    dy = f(min(max(dy, f(-1.0)), f(1.0)))
+    return True, (f(max(refined, best)) if ret_refined else best), dx, dy
+
+
+def _refine1d(s_05, s0, s05, kind: int):
+    """refine1D (kind 0: samples at 3/4, 1, 3/2), refine1D_1 (kind 1: 2/3, 1,
+    4/3), refine1D_2 (kind 2: 2/3, 1, 3/2): the parabola through the three
+    layers' maxima -> (relative scale, refined maximum)."""
+    f = np.float32
+    i_05 = int(1024.0 * float(s_05) + 0.5)
+    i0 = int(1024.0 * float(s0) + 0.5)
+    i05 = int(1024.0 * float(s05) + 0.5)
+    if kind == 0:
+        A, B, C, lo, hi, den = (16, -24, 8), (-40, 54, -14), (24, -27, 6), f(0.75), f(1.5), f(3072.0)
+    elif kind == 1:
+        A, B, C, lo, hi, den = (9, -18, 9), (-21, 36, -15), (12, -16, 6), f(2.0 / 3.0), f(4.0 / 3.0), f(2048.0)
+    else:
+        A, B, C, lo, hi, den = (18, -30, 12), (-45, 65, -20), (27, -30, 8), f(2.0 / 3.0), f(1.5), f(5120.0)
+    a = A[0] * i_05 + A[1] * i0 + A[2] * i05
+    if a >= 0:
+        if s0 >= s_05 and s0 >= s05:
+            return f(1.0), f(s0)
+        if s_05 >= s0 and s_05 >= s05:
+            return lo, f(s_05)
+        if s05 >= s0 and s05 >= s_05:
+            return hi, f(s05)
+    b = B[0] * i_05 + B[1] * i0 + B[2] * i05
+    r = f(-f(b) / f(2 * a))
+    if r < lo:
+        r = lo
+    elif r > hi:
+        r = hi
+    c = C[0] * i_05 + C[1] * i0 + C[2] * i05
+    mx = f(f(f(c) + f(f(f(a) * r) * r)) + f(f(b) * r))
+    return r, f(mx / den)
+
+
+def refine3d(L, R58, layer: int, x: int, y: int):
+    """BriskScaleSpace::refine3D -> None (not a 3-D maximum) or (score, x,
+    y, scale) in image coordinates."""
+    f = np.float32
+    T = L[layer]
+    center = T.score(x, y)
+    ok, max_above, dxa, dya = score_max_neighbour(L, layer, x, y, center, True)
+    if not ok:
+        return None
+    if layer % 2 == 0 and layer == 0:
+        def s58(px, py):
+            return int(R58[py, px]) if 0 <= px < T.w and 0 <= py < T.h else 0
+        patch = _patch(s58, x, y)
+        max_below = f(max(max(r) for r in patch))
+        dxb, dyb, _ = subpixel2d(patch)
+    else:
+        ok, max_below, dxb, dyb = score_max_neighbour(L, layer, x, y, center, False)
+        if not ok:
+            return None
+    dxl, dyl, max_layer = subpixel2d(_patch(T.score, x, y))
+    mid = f(max(f(center), max_layer))
+    kind = 2 if layer == 0 else (0 if layer % 2 == 0 else 1)
+    scale, mx = _refine1d(max_below, mid, max_above, kind)
+    if layer % 2 == 0:
+        if scale > 1.0:
+            r0 = f(f(f(1.5) - scale) / f(0.5))
+            r_o, odx, ody = f(f(1.0) - r0), dxa, dya
+        else:
+            lo = f(2.0 / 3.0) if layer == 0 else f(0.75)
+            r0 = f(f(scale - lo) / f(f(1.0) - lo))
+            r_o, odx, ody = f(f(1.0) - r0), dxb, dyb
+    else:
+        if scale > 1.0:
+            r0 = f(f(4.0) - f(scale * f(3.0)))
+            r_o, odx, ody = f(f(1.0) - r0), dxa, dya
+        else:
+            r0 = f(f(scale * f(3.0)) - f(2.0))
+            r_o, odx, ody = f(f(1.0) - r0), dxb, dyb
+    kx = f(f(f(f(r0 * dxl) + f(r_o * odx)) + f(x)) * T.scale) + T.offset
+    ky = f(f(f(f(r0 * dyl) + f(r_o * ody)) + f(y)) * T.scale) + T.offset
+    return mx, f(kx), f(ky), f(scale * T.scale)
+
+
+def detect(img, threshold: int = 60, octaves: int = 6):
+    """-> keypoints [n][5] (x, y, size, response, octave) float32 in the
+    order BRISK emits them (layer, then FAST's row-major candidate order)."""
+    f = np.float32
+    L = [_Layer(im, sc, off) for (im, sc, off) in pyramid(img, octaves)]
+    R58 = fast58_score(L[0].img)
+    n = len(L)
     out = []
-    for i, (li, sc, off) in enumerate(L):
-        h, w = li.shape
-        ys, xs = np.nonzero(S[i])
+    for i, T in enumerate(L):
+        ys, xs = fast_nms_candidates(T.R, threshold)
         for y, x in zip(ys.tolist(), xs.tolist()):
-            if not _is_max2d(S[i], x, y):
+            if n == 1:
+                dx, dy, mx = subpixel2d(_patch(T.score, x, y))
+                out.append((f(f(f(x) + dx) * T.scale + T.offset), f(f(f(y) + dy) * T.scale + T.offset),
+                            f(f(BASIC_SIZE) * T.scale), mx, f(i)))
                 continue
-            c = S[i][y, x]
-            ok = True
-            for j in (i - 1, i + 1):
-                if j < 0 or j >= len(L):
+            if i == n - 1:
+                ok, _, _, _ = score_max_neighbour(L, i, x, y, T.score(x, y), False)
+                if not ok:
                     continue
-                _, scj, offj = L[j]
-                hj, wj = S[j].shape
-                X = f(f(f(x) * sc) + off)
-                Y = f(f(f(y) * sc) + off)
-                xj = int(f(f(f(X - offj) / scj) + f(0.5)))
-                yj = int(f(f(f(Y - offj) / scj) + f(0.5)))
-                x0, x1 = max(xj - 1, 0), min(xj + 1, wj - 1)
-                y0, y1 = max(yj - 1, 0), min(yj + 1, hj - 1)
-                if x0 <= x1 and y0 <= y1 and S[j][y0:y1 + 1, x0:x1 + 1].max() > c:
-                    ok = False
-                    break
-            if not ok:
+                dx, dy, mx = subpixel2d(_patch(T.score, x, y))
+                out.append((f(f(f(f(x) + dx) * T.scale) + T.offset), f(f(f(f(y) + dy) * T.scale) + T.offset),
+                            f(f(BASIC_SIZE) * T.scale), mx, f(i)))
                 continue
-            # s_i_j of subpixel2D is the score at (x + i - 1, y + j - 1)
-            dx, dy, mx = subpixel2d(R[i][y - 1:y + 2, x - 1:x + 2].T)
-            kx = f(f(f(f(x) + dx) * sc) + off)
-            ky = f(f(f(f(y) + dy) * sc) + off)
-            out.append((kx, ky, f(f(BASIC_SIZE) * sc), mx, f(i)))
+            r = refine3d(L, R58, i, x, y)
+            if r is None:
+                continue
+            mx, kx, ky, sc = r
+            if mx > f(threshold):
+                out.append((kx, ky, f(f(BASIC_SIZE) * sc), mx, f(i)))
     return np.array(out, np.float32).reshape(-1, 5)

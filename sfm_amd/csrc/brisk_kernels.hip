@@ -283,9 +283,13 @@ __global__ __launch_bounds__(64) void k_brisk_describe(const uint8_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// Detector (BriskScaleSpace): layers c_i / d_i, FAST 9-16 scores, 2-D
-// maxima with isMax2D's tie-break, the scale test against the adjacent
-// layers, subpixel2D (see oracle/brisk_oracle.py for the simplifications).
+// Detector (BriskScaleSpace, oracle/brisk_oracle.py): layers c_i / d_i
+// resampled by OpenCV's resize(INTER_AREA), FAST 9-16 scores, FAST's 3x3
+// non-maximum suppression, then per candidate (one thread) BRISK's 3-D
+// refinement (refine3D): interpolated scores of the neighbouring layers
+// over the candidate's footprint, subpixel2D in each layer, the parabola
+// through the three layers' maxima for the scale, the interpolated position;
+// layer 0's virtual lower layer from the 5-8 FAST score.
 constexpr int kMaxLayers = 16;
 __constant__ int2 kCircle[16] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
                                  {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
@@ -298,6 +302,7 @@ struct Layer {
 };
 struct Layers {
   Layer l[kMaxLayers];
+  const uint8_t* R58;  // layer 0's 5-8 scores
   int n;
 };
 
@@ -307,17 +312,41 @@ __global__ void k_halfsample(const uint8_t* __restrict__ src, int sw, uint8_t* _
   const uint8_t* a = src + size_t(2 * y) * sw + 2 * x;
   dst[size_t(y) * dw + x] = uint8_t((int(a[0]) + a[1] + a[sw] + a[sw + 1] + 2) >> 2);
 }
-__global__ void k_twothirdsample(const uint8_t* __restrict__ src, int sw, uint8_t* __restrict__ dst, int dw, int dh) {
-  const int bx = blockIdx.x * blockDim.x + threadIdx.x, by = blockIdx.y;  // 3x3 block -> 2x2
-  if (2 * bx >= dw || 2 * by >= dh) return;
-  const uint8_t* a = src + size_t(3 * by) * sw + 3 * bx;
-  const int p00 = a[0], p01 = a[1], p02 = a[2], p10 = a[sw], p11 = a[sw + 1], p12 = a[sw + 2];
-  const int p20 = a[2 * sw], p21 = a[2 * sw + 1], p22 = a[2 * sw + 2];
-  uint8_t* o = dst + size_t(2 * by) * dw + 2 * bx;
-  o[0] = uint8_t((4 * p00 + 2 * p01 + 2 * p10 + p11 + 4) / 9);
-  o[1] = uint8_t((4 * p02 + 2 * p01 + 2 * p12 + p11 + 4) / 9);
-  o[dw] = uint8_t((4 * p20 + 2 * p10 + 2 * p21 + p11 + 4) / 9);
-  o[dw + 1] = uint8_t((4 * p22 + 2 * p12 + 2 * p21 + p11 + 4) / 9);
+// resize(INTER_AREA) for a ratio other than exactly 2 (OpenCV 3.0
+// resizeArea_): per destination pixel, its computeResizeAreaTab entries per
+// axis (double geometry, float weights), buf = sum_x S * alpha per source
+// row and sum = sum_y beta * buf (float, table order), then cvRound.
+struct AreaTab {
+  int n;
+  int si[6];
+  float al[6];
+};
+__device__ AreaTab area_tab(int d, int ssize, double scale) {
+  AreaTab t;
+  t.n = 0;
+  const double fs1 = d * scale, fs2 = fs1 + scale;
+  const double cell = fmin(scale, ssize - fs1);
+  int s1 = int(ceil(fs1)), s2 = int(floor(fs2));
+  s2 = min(s2, ssize - 1);
+  s1 = min(s1, s2);
+  if (s1 - fs1 > 1e-3) { t.si[t.n] = s1 - 1; t.al[t.n++] = float((s1 - fs1) / cell); }
+  for (int q = s1; q < s2 && t.n < 5; ++q) { t.si[t.n] = q; t.al[t.n++] = float(1.0 / cell); }
+  if (fs2 - s2 > 1e-3) { t.si[t.n] = s2; t.al[t.n++] = float(fmin(fmin(fs2 - s2, 1.0), cell) / cell); }
+  return t;
+}
+__global__ void k_area_resize(const uint8_t* __restrict__ src, int sw, int sh, uint8_t* __restrict__ dst, int dw,
+                              int dh, double scale_x, double scale_y) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= dw || y >= dh) return;
+  const AreaTab tx = area_tab(x, sw, scale_x), ty = area_tab(y, sh, scale_y);
+  float acc = 0.0f;
+  for (int j = 0; j < ty.n; ++j) {
+    const uint8_t* row = src + size_t(ty.si[j]) * sw;
+    float buf = 0.0f;
+    for (int k = 0; k < tx.n; ++k) buf = buf + float(row[tx.si[k]]) * tx.al[k];
+    acc = acc + ty.al[j] * buf;
+  }
+  dst[size_t(y) * dw + x] = uint8_t(fminf(fmaxf(rintf(acc), 0.0f), 255.0f));
 }
 
 // cornerScore<16>(p, 0) = max(0, darkest / brightest 9-arc contrast) - 1,
@@ -339,6 +368,37 @@ __global__ void k_fast_score(const uint8_t* __restrict__ img, int w, int h, uint
       for (int m = 0; m < 9; ++m) {
         mn = min(mn, d[(s + m) & 15]);
         mx = max(mx, d[(s + m) & 15]);
+      }
+      dark = max(dark, mn);
+      bright = max(bright, -mx);
+    }
+    const int sc = max(max(dark, bright), 0) - 1;
+    out = sc >= 1 ? sc : 0;
+  }
+  R[size_t(y) * w + x] = uint8_t(out);
+}
+
+// getAgastScore_5_8(x, y, 1): cornerScore<8> (5 contiguous of the 8
+// radius-1 neighbours) with threshold 0, kept when >= 1; 0 within 2 pixels
+// of the border (layer 0's virtual lower layer in refine3D)
+__constant__ int2 kCircle8[8] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {-1, 0}, {-1, -1}, {0, -1}, {1, -1}};
+__global__ void k_fast58_score(const uint8_t* __restrict__ img, int w, int h, uint8_t* __restrict__ R) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  int out = 0;
+  if (x >= 2 && y >= 2 && x < w - 2 && y < h - 2) {
+    const int v = img[size_t(y) * w + x];
+    int d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = v - int(img[size_t(y + kCircle8[k].y) * w + x + kCircle8[k].x]);
+    int dark = -1000000, bright = -1000000;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      int mn = 1000000, mx = -1000000;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        mn = min(mn, d[(st + m) & 7]);
+        mx = max(mx, d[(st + m) & 7]);
       }
       dark = max(dark, mn);
       bright = max(bright, -mx);
@@ -438,61 +498,218 @@ struct Cand {
   int layer, pad;
 };
 
+// getAgastScore(x, y, 1) and getAgastScore(xf, yf, 1, 1) (bilinear in
+// float, truncated like the C++ (uchar) cast of the restatement)
+__device__ __forceinline__ int lsc(const Layer& L, int x, int y) {
+  if (x < 3 || y < 3 || x >= L.w - 3 || y >= L.h - 3) return 0;
+  return L.R[size_t(y) * L.w + x];
+}
+__device__ int lsc_f(const Layer& L, float xf, float yf) {
+  const int x = int(xf), y = int(yf);
+  const float rx1 = xf - float(x), rx = 1.0f - rx1;
+  const float ry1 = yf - float(y), ry = 1.0f - ry1;
+  float v = (rx * ry) * float(lsc(L, x, y));
+  v = v + (rx1 * ry) * float(lsc(L, x + 1, y));
+  v = v + (rx * ry1) * float(lsc(L, x, y + 1));
+  v = v + (rx1 * ry1) * float(lsc(L, x + 1, y + 1));
+  return int(v) & 0xFF;
+}
+__device__ __forceinline__ void patch3(const Layer& L, int cx, int cy, int s[3][3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s[i][j] = lsc(L, cx + i - 1, cy + j - 1);
+}
+
+// getScoreMaxAbove / getScoreMaxBelow (oracle score_max_neighbour): false
+// when a footprint sample exceeds thr; else the neighbour layer's refined
+// maximum and the offset it implies in this layer
+__device__ bool score_max_nb(const Layers& LS, int layer, int x, int y, int thr, bool above, float& out_max,
+                             float& odx, float& ody) {
+  const Layer& M = LS.l[above ? layer + 1 : layer - 1];
+  int a, b, c, d;
+  if (above) {
+    if (layer % 2 == 0) { a = 4; b = -1; c = 2; d = 6; } else { a = 6; b = -1; c = 3; d = 8; }
+  } else {
+    if (layer % 2 == 0) { a = 8; b = 1; c = 4; d = 6; } else { a = 6; b = 1; c = 3; d = 4; }
+  }
+  const float x_1 = float(a * x + b - c) / float(d), x1 = float(a * x + b + c) / float(d);
+  const float y_1 = float(a * y + b - c) / float(d), y1 = float(a * y + b + c) / float(d);
+  const int ix_1 = int(x_1), ix1 = int(x1), iy_1 = int(y_1), iy1 = int(y1);
+  int max_x = ix_1 + 1, max_y = iy_1 + 1;
+  float best = float(lsc_f(M, x_1, y_1));
+  if (best > float(thr)) return false;
+  auto take = [&](float v, int mx, int my) {
+    if (v > best) { best = v; max_x = mx; max_y = my; }
+  };
+  for (int xx = ix_1 + 1; xx <= ix1; ++xx) {
+    const float v = float(lsc_f(M, float(xx), y_1));
+    if (v > float(thr)) return false;
+    take(v, xx, max_y);
+  }
+  {
+    const float v = float(lsc_f(M, x1, y_1));
+    if (v > float(thr)) return false;
+    take(v, ix1, max_y);
+  }
+  for (int yy = iy_1 + 1; yy <= iy1 + 1; ++yy) {
+    const bool last = yy == iy1 + 1;  // the bottom row at y1
+    const float yv = last ? y1 : float(yy);
+    const int yi = last ? iy1 : yy;
+    float v = float(lsc_f(M, x_1, yv));
+    if (v > float(thr)) return false;
+    take(v, int(x_1 + 1.0f), yi);
+    for (int xx = ix_1 + 1; xx <= ix1; ++xx) {
+      v = last ? float(lsc_f(M, float(xx), yv)) : float(lsc(M, xx, yy));
+      if (v > float(thr)) return false;
+      take(v, xx, yi);
+    }
+    v = float(lsc_f(M, x1, yv));
+    if (v > float(thr)) return false;
+    take(v, ix1, yi);
+  }
+  int s3[3][3];
+  patch3(M, max_x, max_y, s3);
+  float dx1, dy1;
+  const float refined = subpixel2d(s3, dx1, dy1);
+  float real_x = float(max_x) + dx1, real_y = float(max_y) + dy1;
+  bool ret_refined = true;
+  if (real_x > x1) { ret_refined = false; real_x = x1; }
+  if (real_x < x_1) { ret_refined = false; real_x = x_1; }
+  if (real_y > y1) { ret_refined = false; real_y = y1; }
+  if (real_y < y_1) { ret_refined = false; real_y = y_1; }
+  int m, o, dv;
+  if (above) {
+    if (layer % 2 == 0) { m = 6; o = 1; dv = 4; } else { m = 8; o = 1; dv = 6; }
+  } else {
+    if (layer % 2 == 0) { m = 6; o = -1; dv = 8; } else { m = 4; o = -1; dv = 6; }
+  }
+  float ddx = (real_x * float(m) + float(o)) / float(dv) - float(x);
+  float ddy = (real_y * float(m) + float(o)) / float(dv) - float(y);
+  odx = fminf(fmaxf(ddx, -1.0f), 1.0f);
+  ody = fminf(fmaxf(ddy, -1.0f), 1.0f);
+  out_max = ret_refined ? fmaxf(refined, best) : best;
+  return true;
+}
+
+// refine1D (kind 0: samples at 3/4, 1, 3/2), refine1D_1 (1: 2/3, 1, 4/3),
+// refine1D_2 (2: 2/3, 1, 3/2)
+__device__ float refine1d(float s_05, float s0, float s05, int kind, float& mx) {
+  const int i_05 = int(1024.0 * double(s_05) + 0.5), i0 = int(1024.0 * double(s0) + 0.5),
+            i05 = int(1024.0 * double(s05) + 0.5);
+  int A0, A1, A2, B0, B1, B2, C0, C1, C2;
+  float lo, hi, den;
+  if (kind == 0) {
+    A0 = 16; A1 = -24; A2 = 8; B0 = -40; B1 = 54; B2 = -14; C0 = 24; C1 = -27; C2 = 6;
+    lo = 0.75f; hi = 1.5f; den = 3072.0f;
+  } else if (kind == 1) {
+    A0 = 9; A1 = -18; A2 = 9; B0 = -21; B1 = 36; B2 = -15; C0 = 12; C1 = -16; C2 = 6;
+    lo = float(2.0 / 3.0); hi = float(4.0 / 3.0); den = 2048.0f;
+  } else {
+    A0 = 18; A1 = -30; A2 = 12; B0 = -45; B1 = 65; B2 = -20; C0 = 27; C1 = -30; C2 = 8;
+    lo = float(2.0 / 3.0); hi = 1.5f; den = 5120.0f;
+  }
+  const int a = A0 * i_05 + A1 * i0 + A2 * i05;
+  if (a >= 0) {
+    if (s0 >= s_05 && s0 >= s05) { mx = s0; return 1.0f; }
+    if (s_05 >= s0 && s_05 >= s05) { mx = s_05; return lo; }
+    if (s05 >= s0 && s05 >= s_05) { mx = s05; return hi; }
+  }
+  const int b = B0 * i_05 + B1 * i0 + B2 * i05;
+  float r = -float(b) / float(2 * a);
+  if (r < lo) r = lo;
+  else if (r > hi) r = hi;
+  const int c = C0 * i_05 + C1 * i0 + C2 * i05;
+  mx = ((float(c) + (float(a) * r) * r) + float(b) * r) / den;
+  return r;
+}
+
+// One thread per pixel of layer i: FAST's 3x3 non-maximum suppression on the
+// corner scores, then refine3D (or, on the last layer, the 2-D refinement
+// against the layer below) -- oracle/brisk_oracle.py detect().
 __global__ void k_detect_layer(Layers LS, int i, int thr, Cand* __restrict__ out, int cap, int* __restrict__ count) {
   const Layer& L = LS.l[i];
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= L.w || y >= L.h) return;
   const int c = s_at(L, x, y, thr);
   if (c == 0) return;
-  // isMax2D
-  int eq = 0;
 #pragma unroll
   for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      if (!dx && !dy) continue;
-      const int v = s_at(L, x + dx, y + dy, thr);
-      if (v > c) return;
-      if (v == c) eq |= 1 << ((dy + 1) * 3 + dx + 1);
+    for (int dx = -1; dx <= 1; ++dx)
+      if ((dx || dy) && !(c > s_at(L, x + dx, y + dy, thr))) return;
+  const int n = LS.n;
+  float kx, ky, ksize, kresp;
+  int s3[3][3];
+  patch3(L, x, y, s3);
+  if (n == 1 || i == n - 1) {
+    float mb, bdx, bdy;
+    if (n > 1 && !score_max_nb(LS, i, x, y, lsc(L, x, y), false, mb, bdx, bdy)) return;
+    float ddx, ddy;
+    kresp = subpixel2d(s3, ddx, ddy);
+    kx = (float(x) + ddx) * L.scale + L.offset;
+    ky = (float(y) + ddy) * L.scale + L.offset;
+    ksize = kBasicSize * L.scale;
+  } else {
+    const int center = lsc(L, x, y);
+    float max_above, dxa, dya;
+    if (!score_max_nb(LS, i, x, y, center, true, max_above, dxa, dya)) return;
+    float max_below, dxb, dyb;
+    if (i == 0) {
+      int p58[3][3], mb = 0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const int px = x + a - 1, py = y + b - 1;
+          p58[a][b] = (px >= 0 && py >= 0 && px < L.w && py < L.h) ? LS.R58[size_t(py) * L.w + px] : 0;
+          mb = max(mb, p58[a][b]);
+        }
+      subpixel2d(p58, dxb, dyb);
+      max_below = float(mb);
+    } else if (!score_max_nb(LS, i, x, y, center, false, max_below, dxb, dyb)) {
+      return;
     }
-  if (eq) {
-    auto smooth = [&](int cx, int cy) {
-      return s_at(L, cx - 1, cy - 1, thr) + 2 * s_at(L, cx, cy - 1, thr) + s_at(L, cx + 1, cy - 1, thr) +
-             2 * s_at(L, cx - 1, cy, thr) + 4 * s_at(L, cx, cy, thr) + 2 * s_at(L, cx + 1, cy, thr) +
-             s_at(L, cx - 1, cy + 1, thr) + 2 * s_at(L, cx, cy + 1, thr) + s_at(L, cx + 1, cy + 1, thr);
-    };
-    const int sc = smooth(x, y);
-    for (int b = 0; b < 9; ++b)
-      if ((eq >> b) & 1)
-        if (smooth(x + b % 3 - 1, y + b / 3 - 1) > sc) return;
+    float dxl, dyl;
+    const float max_layer = subpixel2d(s3, dxl, dyl);
+    const float mid = fmaxf(float(center), max_layer);
+    const int kind = i == 0 ? 2 : (i % 2 == 0 ? 0 : 1);
+    float mx;
+    const float scale = refine1d(max_below, mid, max_above, kind, mx);
+    float r0, ro, odx, ody;
+    if (i % 2 == 0) {
+      if (scale > 1.0f) {
+        r0 = (1.5f - scale) / 0.5f;
+        ro = 1.0f - r0; odx = dxa; ody = dya;
+      } else {
+        const float lo = i == 0 ? float(2.0 / 3.0) : 0.75f;
+        r0 = (scale - lo) / (1.0f - lo);
+        ro = 1.0f - r0; odx = dxb; ody = dyb;
+      }
+    } else {
+      if (scale > 1.0f) {
+        r0 = 4.0f - scale * 3.0f;
+        ro = 1.0f - r0; odx = dxa; ody = dya;
+      } else {
+        r0 = scale * 3.0f - 2.0f;
+        ro = 1.0f - r0; odx = dxb; ody = dyb;
+      }
+    }
+    if (!(mx > float(thr))) return;
+    kx = ((r0 * dxl + ro * odx) + float(x)) * L.scale + L.offset;
+    ky = ((r0 * dyl + ro * ody) + float(y)) * L.scale + L.offset;
+    ksize = kBasicSize * (scale * L.scale);
+    kresp = mx;
   }
-  // scale test against the adjacent layers (nearest sample, 3x3 max)
-  for (int j = i - 1; j <= i + 1; j += 2) {
-    if (j < 0 || j >= LS.n) continue;
-    const Layer& M = LS.l[j];
-    const float X = float(x) * L.scale + L.offset, Y = float(y) * L.scale + L.offset;
-    const int xj = int((X - M.offset) / M.scale + 0.5f), yj = int((Y - M.offset) / M.scale + 0.5f);
-    const int x0 = max(xj - 1, 0), x1 = min(xj + 1, M.w - 1), y0 = max(yj - 1, 0), y1 = min(yj + 1, M.h - 1);
-    for (int yy = y0; yy <= y1; ++yy)
-      for (int xx = x0; xx <= x1; ++xx)
-        if (s_at(M, xx, yy, thr) > c) return;
-  }
-  int s3[3][3];  // s_i_j of subpixel2D: the score at (x + i - 1, y + j - 1)
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int q = 0; q < 3; ++q) s3[q][r] = L.R[size_t(y - 1 + r) * L.w + x - 1 + q];
-  float ddx, ddy;
-  const float mx = subpixel2d(s3, ddx, ddy);
   const int k = atomicAdd(count, 1);
   if (k >= cap) return;
   Cand cd;
   cd.key = (static_cast<unsigned long long>(i) << 42) | (static_cast<unsigned long long>(y) << 21) |
            static_cast<unsigned long long>(x);
-  cd.x = (float(x) + ddx) * L.scale + L.offset;
-  cd.y = (float(y) + ddy) * L.scale + L.offset;
-  cd.size = kBasicSize * L.scale;
-  cd.response = mx;
+  cd.x = kx;
+  cd.y = ky;
+  cd.size = ksize;
+  cd.response = kresp;
   cd.layer = i;
   cd.pad = 0;
   out[k] = cd;
@@ -641,16 +858,28 @@ extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int
   if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess) return bfail(SFM_EIO, "upload failed");
   for (int i = 1; i < nuse; ++i) {
     if (lw[i] < 1 || lh[i] < 1) continue;
-    if (i == 1) {
-      dim3 g(unsigned((lw[1] / 2 + 127) / 128), unsigned(lh[1] / 2));
-      k_twothirdsample<<<g, 128>>>(limg, w, limg + loff_px[1], lw[1], lh[1]);
-    } else {
+    // resize(INTER_AREA): OpenCV's scales are 1 / (dsize / ssize); exactly 2
+    // on both axes takes the 2x2 average, anything else the area filter
+    const int src = i == 1 ? 0 : i - 2;
+    const int sw = i == 1 ? w : lw[src], sh = i == 1 ? h : lh[src];
+    const double scx = 1.0 / (double(lw[i]) / sw), scy = 1.0 / (double(lh[i]) / sh);
+    if (scx == 2.0 && scy == 2.0) {
       dim3 g(unsigned((lw[i] + 255) / 256), unsigned(lh[i]));
-      k_halfsample<<<g, 256>>>(limg + loff_px[i - 2], lw[i - 2], limg + loff_px[i], lw[i], lh[i]);
+      k_halfsample<<<g, 256>>>(limg + loff_px[src], sw, limg + loff_px[i], lw[i], lh[i]);
+    } else {
+      dim3 g(unsigned((lw[i] + 127) / 128), unsigned(lh[i]));
+      k_area_resize<<<g, 128>>>(limg + loff_px[src], sw, sh, limg + loff_px[i], lw[i], lh[i], scx, scy);
     }
   }
   Layers LS;
   LS.n = nuse;
+  auto* R58 = static_cast<uint8_t*>(W->get(14, size_t(w) * h, &rc));
+  if (rc) return rc;
+  {
+    dim3 g(unsigned((w + 255) / 256), unsigned(h));
+    k_fast58_score<<<g, 256>>>(limg, w, h, R58);
+  }
+  LS.R58 = R58;
   for (int i = 0; i < nuse; ++i) {
     if (lw[i] >= 1 && lh[i] >= 1) {
       dim3 g(unsigned((lw[i] + 255) / 256), unsigned(lh[i]));

@@ -35,12 +35,33 @@ def test_layers_follow_brisk_scale_space():
     assert [float(l[2]) for l in L][:3] == [0.0, 0.25, 0.5]
 
 
-def test_downsampling_rounds_area_averages():
+def test_area_resize_matches_inter_area():
+    """resize(INTER_AREA): ratio 2 on both axes is resizeAreaFast's
+    (a + b + c + d + 2) >> 2; an exact 3/2 ratio gives the (4, 2, 2, 1) / 9
+    weights (cvRound: N / 9 never ties); a constant image stays constant at
+    any ratio; 1280 -> 852 columns (BRISK's d0 width) uses fractional cells."""
     a = np.array([[0, 1, 2], [3, 4, 5], [6, 7, 8]], np.uint8)
-    assert B.halfsample(a).tolist() == [[2]]        # (0 + 1 + 3 + 4 + 2) >> 2
-    t = B.twothirdsample(a)
-    assert t.tolist() == [[(4 * 0 + 2 * 1 + 2 * 3 + 4 + 4) // 9, (4 * 2 + 2 * 1 + 2 * 5 + 4 + 4) // 9],
-                          [(4 * 6 + 2 * 3 + 2 * 7 + 4 + 4) // 9, (4 * 8 + 2 * 5 + 2 * 7 + 4 + 4) // 9]]
+    assert B.area_resize(np.array([[0, 1], [3, 4]], np.uint8), 1, 1).tolist() == [[2]]
+    t = B.area_resize(a, 2, 2)
+    assert t.tolist() == [[round((4 * 0 + 2 * 1 + 2 * 3 + 4) / 9), round((4 * 2 + 2 * 1 + 2 * 5 + 4) / 9)],
+                          [round((4 * 6 + 2 * 3 + 2 * 7 + 4) / 9), round((4 * 8 + 2 * 5 + 2 * 7 + 4) / 9)]]
+    c = np.full((30, 1280), 137, np.uint8)
+    assert (B.area_resize(c, 852, 20) == 137).all()
+    tab = B._area_tab(1280, 852, 1.0 / (852 / 1280))
+    assert all(abs(sum(float(al) for _, al in t) - 1.0) < 1e-6 for t in tab)
+    assert len(tab[1]) == 3 and tab[1][0][0] == 1        # a cell straddling three source columns
+    ramp = np.tile(np.arange(1280, dtype=np.float64) % 256, (3, 1)).astype(np.uint8)
+    r = B.area_resize(ramp, 852, 2)
+    assert abs(int(r[0, 100]) - np.mean(ramp[0, 150:152])) <= 1
+
+
+def test_refine1d_finds_the_parabola_vertex():
+    """refine1D / _1 / _2: samples of a parabola peaking at scale 1.1 (octave),
+    1.05 (intra), 0.9 (layer 0) give back the vertex and its height."""
+    for kind, xs, peak in ((0, (0.75, 1.0, 1.5), 1.1), (1, (2 / 3, 1.0, 4 / 3), 1.05), (2, (2 / 3, 1.0, 1.5), 0.9)):
+        s = [np.float32(90.0 - 200.0 * (x - peak) ** 2) for x in xs]
+        r, m = B._refine1d(*s, kind)
+        assert abs(float(r) - peak) < 2e-3 and abs(float(m) - 90.0) < 0.05
 
 
 def test_fast_score_of_a_constructed_corner():
