@@ -41,12 +41,17 @@ def detect(img, threshold: int = 60, octaves: int = 6, describe: bool = True, de
     if im.ndim != 2:
         raise ValueError("img must be 2-D 8-bit grey")
     cap = max(1024, im.shape[0] * im.shape[1] // 64)
-    kps = np.zeros((cap, 5), np.float32)
-    lay = np.zeros(cap, np.int32)
-    desc = np.zeros((cap, DESC_BYTES), np.uint8) if describe else None
-    n = ctypes.c_int32()
-    check(lib().sfm_brisk_detect_describe(device, ptr(im), im.shape[1], im.shape[0], int(threshold), int(octaves), cap,
-                                          ptr(kps), ptr(lay), ptr(desc) if describe else None, ctypes.byref(n)),
-          "sfm_brisk_detect_describe")
+    for _ in range(2):  # the call reports the count before it rejects a short buffer
+        kps = np.zeros((cap, 5), np.float32)
+        lay = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, DESC_BYTES), np.uint8) if describe else None
+        n = ctypes.c_int32()
+        rc = lib().sfm_brisk_detect_describe(device, ptr(im), im.shape[1], im.shape[0], int(threshold), int(octaves),
+                                             cap, ptr(kps), ptr(lay), ptr(desc) if describe else None,
+                                             ctypes.byref(n))
+        if rc == 0 or n.value <= cap:
+            break
+        cap = n.value
+    check(rc, "sfm_brisk_detect_describe")
     k = n.value
     return kps[:k].copy(), lay[:k].copy(), (desc[:k].copy() if describe else None)

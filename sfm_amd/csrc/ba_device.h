@@ -126,7 +126,8 @@ struct DevProblem {
   int2* blk = nullptr;        // [n_blk]
   int32_t* seg = nullptr;     // [n_blk + 1]
   int32_t* bpts = nullptr;    // [n_pairs]
-  int32_t* bperm = nullptr;   // [n_bslots] k_schur_pts work order (XCD-aware row groups; -1: empty slot)
+  int32_t* bperm = nullptr;   // [n_bslots] k_schur_pts work order (XCD-aware row groups; -1: empty slot;
+                              // nullptr: plain block order, small systems)
   int64_t n_bslots = 0;
   double* ptS = nullptr;      // [P][kPtS] X 3, scale 3, l10 l20 l21, 1/l_ii 3, z 3, pad
   int32_t schur_pts_sub = 8;  // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)

@@ -790,11 +790,12 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
   const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
   // (no early exit: a wave past the end runs empty lists, so every wave
   // reaches the publishing barrier)
-  // bperm: the XCD-aware work order of set_problem (blocks of one row group
+  // bperm: the XCD-aware work order of set_problem (nullptr: the plain
+  // block order of a small system) -- blocks of one row group
   // in the workgroups one XCD is dealt, descending pair count within a row,
   // so the kPer segments of a wave run lists of nearly equal length); -1 is
   // an empty slot
-  auto slot_blk = [&](int64_t k) -> int32_t { return k < n_slots ? bperm[k] : -1; };
+  auto slot_blk = [&](int64_t k) -> int32_t { return k < n_slots ? (bperm ? bperm[k] : int32_t(k)) : -1; };
   const int32_t bs = slot_blk(wb + g);
   const bool own = bs >= 0;
   const int64_t b = own ? bs : 0;

@@ -193,6 +193,10 @@ struct HostTimer {
   }
 };
 
+// Reduced systems with more camera blocks than this take the XCD-aware
+// k_schur_pts order (C3: 125k blocks); smaller ones the plain order.
+constexpr int64_t kSchurXcdMinBlocks = 8192;
+
 bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
 
 size_t packed_size(int n) { return size_t(n) * (n + 1) / 2 + size_t(n); }
@@ -701,8 +705,12 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // nearly equal length), fill workgroups x, x + 8, x + 16, ... -- the ones
   // dealt to one XCD (round-robin placement: a speed assumption only,
   // MI355X_MICROARCH.md), so a row's records stay in that XCD's L2 while its
-  // blocks run.  Slots past a group's end hold -1 (an empty list).
-  {
+  // blocks run.  Slots past a group's end hold -1 (an empty list).  Small
+  // reduced systems (keyframe-sized solves: everything fits one L2) keep the
+  // plain block order and skip the extra round trip (bperm = nullptr).
+  d.bperm = nullptr;
+  d.n_bslots = d.n_blk;
+  if (d.n_blk > kSchurXcdMinBlocks) {
     std::vector<int32_t> seg_h(size_t(d.n_blk) + 1);
     HCHK(hipMemcpyAsync(seg_h.data(), d.seg, sizeof(int32_t) * seg_h.size(), hipMemcpyDeviceToHost, s));
     HCHK(hipStreamSynchronize(s));

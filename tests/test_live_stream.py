@@ -52,3 +52,24 @@ def test_filter_matches_keeps_true_and_drops_wrong_pairs():
     behind[:, 2] *= -1
     assert not _filter_matches(s.K, f0, f1, uv0, uv1, behind, 7.0).any()
     assert np.allclose(_rodrigues(f0.rot), np.eye(3))
+
+
+def test_pair_frame_observations_recovers_each_observation():
+    """live._bundle_adjust's pairing of getPointsInFrame's 3D and 2D lists
+    (points matched two and three times in one frame: k^2 2D entries) gives
+    every observation its own 2D index, in the frame's emplace order."""
+    from oracle.cmap_oracle import CMapOracle
+    from sfm_amd.live import pair_frame_observations
+    m = CMapOracle()
+    m.addNewPoints(np.zeros((6, 3)), [[10, 11, 12, 13, 14, 15]], [0])
+    adds = [([0, 1, 2], [20, 21, 22]), ([1], [30]), ([3, 1, 4], [40, 41, 42]), ([5], [50])]
+    truth = []
+    for pts, uv in adds:
+        m.addPointMatches(pts, uv, 7)
+        truth += list(zip(pts, uv))
+    p3, p2 = m.getPointsInFrame(7)
+    assert len(p2) > len(p3)                            # 3^2 entries for point 1
+    i2 = pair_frame_observations(p3, p2)
+    assert list(zip(np.asarray(p3).tolist(), np.asarray(i2).tolist())) == truth
+    p3, p2 = m.getPointsInFrame(0)                      # no duplicates: p2 itself
+    assert np.asarray(pair_frame_observations(p3, p2)).tolist() == list(p2)
