@@ -208,12 +208,17 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
   // XCD dispatch puts each slice on one XCD, whose 4-MB L2 then holds that
   // slice's X (0.6 MB at C3) instead of every XCD gathering all 4.8 MB.
   // (Placement is a speed assumption only; any mapping is correct.)
+  // Within a slice the chunks are camera-major, and each wave takes one
+  // contiguous run of them, so it reduces the U_c / b_c partials once per
+  // camera it meets instead of once per chunk.
   const int grp = blockIdx.x & 7;
   const int nbg = (int(gridDim.x) - 1 - grp) / 8 + 1;
-  const int n_chunks = grp_off[grp + 1];
-  const int stride = nbg * (kThreads / 64);
+  const int nw = nbg * (kThreads / 64);
+  const int wi = (blockIdx.x >> 3) * (kThreads / 64) + wv;
+  const int g0 = grp_off[grp], glen = grp_off[grp + 1] - g0;
+  int t = g0 + int(int64_t(glen) * wi / nw);
+  const int n_chunks = g0 + int(int64_t(glen) * (wi + 1) / nw);  // end of this wave's run
   double cost = 0.0;
-  int t = grp_off[grp] + (blockIdx.x >> 3) * (kThreads / 64) + wv;
   // Lanes past the real observations of a camera's last chunk compute the
   // padding slots (copies of its last observation): every load and store is
   // unpredicated, so nothing forces an early wait; padding records are never
@@ -223,14 +228,14 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
   // one issued a whole chunk earlier (vmcnt counts loads and stores in issue
   // order: waiting on a young load would also wait on the stores before it).
   auto chunk_at = [&](int tt) { return chunks[tt < n_chunks ? tt : t]; };
-  int p_nxt = 0;                              // point index of chunk t + stride
+  int p_nxt = 0;                              // point index of chunk t + 1
   double2 uv_cur = make_double2(0.0, 0.0);    // chunk t
   double Xc[3] = {0.0, 0.0, 1.0}, spc[3] = {1.0, 1.0, 1.0};
   if (t < n_chunks) {
     const int64_t i = int64_t(chunks[t].y) + l;
     const int p0 = cm_p[i];
     uv_cur = ld2(uv_cm + 2 * i);
-    p_nxt = cm_p[int64_t(chunk_at(t + stride).y) + l];
+    p_nxt = cm_p[int64_t(chunk_at(t + 1).y) + l];
 #pragma unroll
     for (int j = 0; j < 3; ++j) Xc[j] = X[3 * size_t(p0) + j];
     if (scaled)
@@ -242,7 +247,10 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
   // the prologue and back-edge states conservatively)
   asm volatile("" : "+v"(Xc[0]), "+v"(Xc[1]), "+v"(Xc[2]), "+v"(spc[0]), "+v"(spc[1]), "+v"(spc[2]), "+v"(uv_cur.x),
                "+v"(uv_cur.y), "+v"(p_nxt));
-  for (; t < n_chunks; t += stride) {
+  double acc[32];  // this lane's share of the current camera's U_c (21) and b_c (6)
+#pragma unroll
+  for (int e = 0; e < 32; ++e) acc[e] = 0.0;
+  for (; t < n_chunks; ++t) {
     const int4 ch = chunks[t];
     const int c = ch.x, cnt = ch.z;
     const int64_t ib = ch.y;
@@ -254,8 +262,9 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
     if (scaled)
 #pragma unroll
       for (int j = 0; j < 3; ++j) spn[j] = scale_p[3 * size_t(p_nxt) + j];
-    const double2 uv_nxt = ld2(uv_cm + 2 * (int64_t(chunk_at(t + stride).y) + l));
-    const int p_nn = cm_p[int64_t(chunk_at(t + 2 * stride).y) + l];
+    const int4 ch_n = chunk_at(t + 1);
+    const double2 uv_nxt = ld2(uv_cm + 2 * (int64_t(ch_n.y) + l));
+    const int p_nn = cm_p[int64_t(chunk_at(t + 2).y) + l];
     // ---- chunk t ----
     const double* cr = camR + size_t(kCamR) * c;  // camera data: wave-uniform -> scalar loads
     const double* k = Kc + 5 * size_t(c);
@@ -274,23 +283,27 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
       }
       if (jpart) {
         // the chunk's share of U_c = sum J_c^T J_c (21, packed upper) and
-        // b_c = sum J_c^T r (6): one reduce-scatter over the wave, lane 2e
-        // stores entry e of the chunk's partial (k_cam_sum adds a camera's
-        // chunks in order) -- no second pass over the records
+        // b_c = sum J_c^T r (6), accumulated per lane; at the end of the
+        // camera's run one reduce-scatter over the wave, lane 2e stores entry
+        // e into the run's last chunk slot, the run's other slots get zeros
+        // (k_cam_sum adds a camera's slots in order) -- no second pass over
+        // the records
         const bool real = l < cnt;
         const double* j0 = rec + kJC;
         const double* j1 = rec + kJC + 6;
-        double v[32];
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = a; b < 6; ++b, ++q) v[q] = real ? j0[a] * j0[b] + j1[a] * j1[b] : 0.0;
+          for (int b = a; b < 6; ++b, ++q) acc[q] += real ? j0[a] * j0[b] + j1[a] * j1[b] : 0.0;
 #pragma unroll
-        for (int a = 0; a < 6; ++a) v[21 + a] = real ? j0[a] * rec[kRes] + j1[a] * rec[kRes + 1] : 0.0;
+        for (int a = 0; a < 6; ++a) acc[21 + a] += real ? j0[a] * rec[kRes] + j1[a] * rec[kRes + 1] : 0.0;
+        double tot = 0.0;
+        if (t + 1 >= n_chunks || ch_n.x != c) {  // wave-uniform
+          tot = wave_sum32(acc, l);
 #pragma unroll
-        for (int e = 27; e < 32; ++e) v[e] = 0.0;
-        const double tot = wave_sum32(v, l);
+          for (int e = 0; e < 32; ++e) acc[e] = 0.0;
+        }
         if (!(l & 1) && (l >> 1) < 27) jpart[size_t(ib / 64) * 27 + (l >> 1)] = tot;
       }
     }

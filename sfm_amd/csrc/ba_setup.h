@@ -41,5 +41,14 @@ void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm,
                       const int32_t* pt_off, const int64_t* off, int C, uint32_t* key, int32_t* val, hipStream_t s);
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s);
 void launch_blk(int C, int2* blk, hipStream_t s);
+// k_schur_pts work order (XCD-aware, set_problem step 5): bperm (room for
+// bperm_slots_bound slots) gets every block in its slot, -1 elsewhere; grp
+// [16] = each group's first block and block count (the launch's grid is
+// max_x ceil(count_x / per) * 8 workgroups).  key_a / key_b / iota / sorted
+// hold n_blk items, row_x C; sort_tmp as setup_sort_bytes(n_blk, 32).
+int64_t bperm_slots_bound(int64_t n_blk, int per);
+hipError_t launch_bperm(int C, int64_t n_blk, int64_t n_pairs, const int32_t* seg, const int2* blk, int per,
+                        uint32_t* key_a, uint32_t* key_b, int32_t* iota, int32_t* sorted, int32_t* row_x,
+                        int64_t* grp, void* sort_tmp, size_t sort_bytes, int32_t* bperm, hipStream_t s);
 
 }  // namespace sfm

@@ -23,6 +23,7 @@
 // Integer work only; every output is deterministic (no atomics decide an
 // order: the counters are commutative integer adds).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <hipcub/hipcub.hpp>
 #include <climits>
 #include <cmath>
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(kT) void k_fill_cm(int64_t N_pad, const int32_t* __
   if (j < n_c) pos[q] = int32_t(i);
 }
 
-// Chunk t of the (piece-major, camera-minor) chunk list: its XCD group is
+// Chunk t of the (camera-major) chunk list: its XCD group is
 // the point slice of its first observation (.w holds that observation's
 // camera-major index until the gather clears it).
 __global__ __launch_bounds__(kT) void k_chunk_keys(int n, const int4* __restrict__ ch,
@@ -204,6 +205,85 @@ __global__ __launch_bounds__(kT) void k_blk(int C, int2* __restrict__ blk) {
     blk[rs + c2] = make_int2(c1, c2);
 }
 
+// ---- k_schur_pts work order (set_problem step 5) ----
+// One workgroup: rows' pair totals (block counts when there are no pairs)
+// scanned kT rows at a time; row c1 goes to group x = the eighth of the total
+// its middle falls in (monotone in c1, so a group is a contiguous block
+// range).  grp[x] = the group's first block, grp[8 + x] = its block count.
+__global__ __launch_bounds__(kT) void k_bperm_rows(int C, const int32_t* __restrict__ seg, int64_t n_pairs,
+                                                   int64_t n_blk, int32_t* __restrict__ row_x,
+                                                   int64_t* __restrict__ grp) {
+  __shared__ int64_t sc[kT];
+  __shared__ int64_t carry;
+  __shared__ unsigned long long gfirst[8], gsize[8];
+  const int t = threadIdx.x;
+  if (t < 8) {
+    gfirst[t] = ~0ull;
+    gsize[t] = 0;
+  }
+  if (t == 0) carry = 0;
+  __syncthreads();
+  const int64_t total = n_pairs > 0 ? n_pairs : n_blk;
+  for (int base = 0; base < C; base += kT) {
+    const int c1 = base + t;
+    int64_t first = 0, nb = 0, w = 0;
+    if (c1 < C) {
+      first = row_start(c1, C);
+      nb = C - c1;
+      w = n_pairs > 0 ? int64_t(seg[first + nb]) - seg[first] : nb;
+    }
+    sc[t] = w;
+    __syncthreads();
+    for (int o = 1; o < kT; o <<= 1) {
+      const int64_t v = t >= o ? sc[t - o] : 0;
+      __syncthreads();
+      sc[t] += v;
+      __syncthreads();
+    }
+    const int64_t before = carry + sc[t] - w;
+    if (c1 < C) {
+      const int x = int(min<int64_t>(7, (8 * (before + w / 2)) / max<int64_t>(1, total)));
+      row_x[c1] = x;
+      atomicMin(&gfirst[x], (unsigned long long)first);
+      atomicAdd(&gsize[x], (unsigned long long)nb);
+    }
+    __syncthreads();
+    if (t == kT - 1) carry += sc[kT - 1];
+    __syncthreads();
+  }
+  if (t < 8) {
+    grp[t] = gsize[t] ? int64_t(gfirst[t]) : 0;
+    grp[8 + t] = int64_t(gsize[t]);
+  }
+}
+
+// key = (row, descending pair count): a stable sort keeps every row's block
+// range in place and orders its blocks longest list first
+__global__ __launch_bounds__(kT) void k_bperm_keys(int64_t n_blk, const int2* __restrict__ blk,
+                                                   const int32_t* __restrict__ seg, int cbits,
+                                                   uint32_t* __restrict__ key, int32_t* __restrict__ iota) {
+  const int64_t b = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (b >= n_blk) return;
+  const uint32_t cmax = (1u << cbits) - 1u;
+  const uint32_t cnt = min(uint32_t(seg[b + 1] - seg[b]), cmax);
+  key[b] = (uint32_t(blk[b].x) << cbits) | (cmax - cnt);
+  iota[b] = int32_t(b);
+}
+
+// group x's i-th block goes to slot ((i / per) * 8 + x) * per + i % per:
+// workgroups x, x + 8, x + 16, ... (one XCD under round-robin placement)
+__global__ __launch_bounds__(kT) void k_bperm_fill(int64_t n_blk, const int32_t* __restrict__ sorted,
+                                                   const int2* __restrict__ blk, const int32_t* __restrict__ row_x,
+                                                   const int64_t* __restrict__ grp, int per,
+                                                   int32_t* __restrict__ bperm) {
+  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (p >= n_blk) return;
+  const int32_t b = sorted[p];
+  const int x = row_x[blk[b].x];
+  const int64_t i = p - grp[x];
+  bperm[((i / per) * 8 + x) * per + i % per] = b;
+}
+
 int bits_for(uint64_t max_key) {
   int b = 1;
   while (b < 64 && (max_key >> b) != 0) ++b;
@@ -289,6 +369,20 @@ void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* se
 }
 void launch_blk(int C, int2* blk, hipStream_t s) {
   if (C > 0) k_blk<<<dim3(unsigned((C + kT - 1) / kT), unsigned(C)), kT, 0, s>>>(C, blk);
+}
+int64_t bperm_slots_bound(int64_t n_blk, int per) { return std::max<int64_t>(1, (n_blk + per - 1) / per) * 8 * per; }
+hipError_t launch_bperm(int C, int64_t n_blk, int64_t n_pairs, const int32_t* seg, const int2* blk, int per,
+                        uint32_t* key_a, uint32_t* key_b, int32_t* iota, int32_t* sorted, int32_t* row_x,
+                        int64_t* grp, void* sort_tmp, size_t sort_bytes, int32_t* bperm, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(bperm, 0xFF, sizeof(int32_t) * size_t(bperm_slots_bound(n_blk, per)), s);
+  if (e != hipSuccess || n_blk <= 0) return e;
+  k_bperm_rows<<<1, kT, 0, s>>>(C, seg, n_pairs, n_blk, row_x, grp);
+  const int cbits = 32 - bits_for(uint64_t(std::max(1, C)) - 1);
+  k_bperm_keys<<<nblocks(n_blk), kT, 0, s>>>(n_blk, blk, seg, cbits, key_a, iota);
+  e = sort_pairs32(sort_tmp, sort_bytes, key_a, key_b, iota, sorted, n_blk, ~uint64_t(0) >> 32, s);
+  if (e != hipSuccess) return e;
+  k_bperm_fill<<<nblocks(n_blk), kT, 0, s>>>(n_blk, sorted, blk, row_x, grp, per, bperm);
+  return hipGetLastError();
 }
 
 }  // namespace sfm

@@ -551,8 +551,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     }
   }
   // ---- camera runs: camera-major, each camera's run padded to a whole
-  // number of 64-wide wavefront chunks; the chunk table piece-major across
-  // cameras (grouped into 8 point slices on the device, one per XCD) ----
+  // number of 64-wide wavefront chunks; the chunk table camera-major
+  // (grouped into 8 point slices on the device, one per XCD) ----
   std::vector<int32_t> cam_off(size_t(C) + 1, 0), cam_rng(2 * size_t(C));
   int64_t npad = 0;
   for (int c = 0; c < C; ++c) {
@@ -567,16 +567,14 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   for (int c = 0; c < C; ++c)
     for (int64_t w = cam_rng[2 * c] / 64; w < (int64_t(cam_rng[2 * c]) + cam_off[c + 1] - cam_off[c] + 63) / 64; ++w)
       wcam[w] = c;
-  std::vector<int4> chunks;  // (camera, first position, count, first observation's camera-major index)
-  for (int32_t k = 0;; ++k) {
-    bool any = false;
-    for (int c = 0; c < C; ++c) {
-      const int32_t n_c = cam_off[c + 1] - cam_off[c];
-      if (64 * k >= n_c) continue;
-      any = true;
+  // (camera, first position, count, first observation's camera-major index),
+  // camera-major: a k_jacobian wave runs through consecutive chunks of a
+  // slice and reduces once per camera
+  std::vector<int4> chunks;
+  for (int c = 0; c < C; ++c) {
+    const int32_t n_c = cam_off[c + 1] - cam_off[c];
+    for (int32_t k = 0; 64 * k < n_c; ++k)
       chunks.push_back(make_int4(c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), cam_off[c] + 64 * k));
-    }
-    if (!any) break;
   }
   d.n_jchunks = int32_t(chunks.size());
   d.jac_blocks_rec = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
@@ -645,7 +643,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // camera-major order of the point-major ids: stable sort by camera
   HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
   launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
-  // chunk table grouped by point slice (stable: piece-major order kept)
+  // chunk table grouped by point slice (stable: camera-major order kept)
   launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
   HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
   launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
@@ -674,6 +672,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     while (sub < 64 && sub < avg / 10.0) sub *= 2;
     d.schur_pts_sub = sub;
   }
+  if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1 + 16)) != hipSuccess) {
+    d.scal_host = nullptr;
+    return bail(fail(SFM_ENOMEM, "hipHostMalloc failed"));
+  }
+  // the pinned mirror's 16-slot tail: the k_schur_pts group sizes
+  int64_t* grp_host = reinterpret_cast<int64_t*>(d.scal_host + kNumScalars + 1);
+  int bperm_per = 0;
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
   ALLOC(d.seg, size_t(d.n_blk) + 1);
   ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
@@ -696,55 +701,34 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
                       s));
     launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
     launch_blk(C, d.blk, s);
-  }
-  // ---- k_schur_pts work order: XCD-aware.  Block (c1, c2)'s pairs gather
-  // records of points camera c1 sees, so a row c1 (its blocks c2 >= c1) reads
-  // one camera's ~N/C point records (C3: ~0.5 MB).  Rows go to 8 groups of
-  // contiguous rows with equal pair totals; group x's blocks, row by row
-  // (descending pair count within a row, so a wave's kPer blocks run lists of
-  // nearly equal length), fill workgroups x, x + 8, x + 16, ... -- the ones
-  // dealt to one XCD (round-robin placement: a speed assumption only,
-  // MI355X_MICROARCH.md), so a row's records stay in that XCD's L2 while its
-  // blocks run.  Slots past a group's end hold -1 (an empty list).  Small
-  // reduced systems (keyframe-sized solves: everything fits one L2) keep the
-  // plain block order and skip the extra round trip (bperm = nullptr).
-  d.bperm = nullptr;
-  d.n_bslots = d.n_blk;
-  if (d.n_blk > kSchurXcdMinBlocks) {
-    std::vector<int32_t> seg_h(size_t(d.n_blk) + 1);
-    HCHK(hipMemcpyAsync(seg_h.data(), d.seg, sizeof(int32_t) * seg_h.size(), hipMemcpyDeviceToHost, s));
-    HCHK(hipStreamSynchronize(s));
-    const int per = 64 / d.schur_pts_sub * (kThreads / 64);
-    std::vector<int64_t> row_pairs(size_t(C) + 1, 0);
-    std::vector<int64_t> row_first(size_t(C) + 1, 0);
-    for (int c1 = 0, b = 0; c1 < C; ++c1) {
-      row_first[c1] = b;
-      row_pairs[c1] = seg_h[size_t(b) + size_t(C - c1)] - seg_h[b];
-      b += C - c1;
+    // ---- k_schur_pts work order: XCD-aware (ba_setup.hip k_bperm_*).
+    // Block (c1, c2)'s pairs gather records of points camera c1 sees, so a
+    // row c1 (its blocks c2 >= c1) reads one camera's ~N/C point records
+    // (C3: ~0.5 MB).  Rows go to 8 groups of contiguous rows with equal pair
+    // totals; group x's blocks, row by row (descending pair count within a
+    // row, so a wave's blocks run lists of nearly equal length), fill
+    // workgroups x, x + 8, x + 16, ... -- the ones dealt to one XCD
+    // (round-robin placement: a speed assumption only, MI355X_MICROARCH.md),
+    // so a row's records stay in that XCD's L2 while its blocks run.  Slots
+    // past a group's end hold -1 (an empty list).  Small reduced systems
+    // (keyframe-sized solves: everything fits one L2) keep the plain block
+    // order (bperm = nullptr).  The group sizes come back with the final
+    // synchronisation of set_problem.
+    d.bperm = nullptr;
+    d.n_bslots = d.n_blk;
+    if (d.n_blk > kSchurXcdMinBlocks) {
+      const int per = 64 / d.schur_pts_sub * (kThreads / 64);
+      int32_t *sorted = nullptr, *row_x = nullptr;
+      int64_t* grp = nullptr;
+      TMP(sorted, size_t(d.n_blk));
+      TMP(row_x, size_t(C));
+      TMP(grp, 16);
+      ALLOC(d.bperm, size_t(bperm_slots_bound(d.n_blk, per)));
+      HCHK(launch_bperm(C, d.n_blk, n_pairs, d.seg, d.blk, per, bk_a, bk_b, bv, sorted, row_x, grp, sort_tmp,
+                        sort_bytes, d.bperm, s));
+      HCHK(hipMemcpyAsync(grp_host, grp, sizeof(int64_t) * 16, hipMemcpyDeviceToHost, s));
+      bperm_per = per;
     }
-    row_first[C] = d.n_blk;
-    std::vector<std::vector<int32_t>> lists(8);
-    int64_t cum = 0;
-    std::vector<int32_t> row_blocks;
-    for (int c1 = 0; c1 < C; ++c1) {
-      const int x = n_pairs ? int(std::min<int64_t>(7, (8 * (cum + row_pairs[c1] / 2)) / std::max<int64_t>(1, n_pairs))) : c1 % 8;
-      cum += row_pairs[c1];
-      row_blocks.clear();
-      for (int64_t b = row_first[c1]; b < row_first[c1 + 1]; ++b) row_blocks.push_back(int32_t(b));
-      std::stable_sort(row_blocks.begin(), row_blocks.end(), [&](int32_t a, int32_t b) {
-        return seg_h[a + 1] - seg_h[a] > seg_h[b + 1] - seg_h[b];
-      });
-      lists[x].insert(lists[x].end(), row_blocks.begin(), row_blocks.end());
-    }
-    size_t m_max = 0;
-    for (auto& L : lists) m_max = std::max(m_max, (L.size() + per - 1) / per);
-    d.n_bslots = int64_t(std::max<size_t>(1, m_max)) * 8 * per;
-    std::vector<int32_t> slots(size_t(d.n_bslots), -1);
-    for (int x = 0; x < 8; ++x)
-      for (size_t i = 0; i < lists[x].size(); ++i) slots[((i / per) * 8 + x) * per + i % per] = lists[x][i];
-    ALLOC(d.bperm, slots.size());
-    HCHK(hipMemcpyAsync(d.bperm, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, s));
-    HCHK(hipStreamSynchronize(s));
   }
   // ---- parameters, per-iteration arrays, dense system ----
   d.n = 6 * C;
@@ -787,10 +771,6 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
 #undef ALLOC
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
-  if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1)) != hipSuccess) {
-    d.scal_host = nullptr;
-    return bail(fail(SFM_ENOMEM, "hipHostMalloc failed"));
-  }
   if (C) {
     HCHK(hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, s));
@@ -811,6 +791,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   h->bs_epoch = 0;
   d.n_cu = device_cus(h->device);
   HCHK(hipStreamSynchronize(s));
+  if (bperm_per) {
+    int64_t m_max = 1;
+    for (int x = 0; x < 8; ++x) m_max = std::max<int64_t>(m_max, (grp_host[8 + x] + bperm_per - 1) / bperm_per);
+    d.n_bslots = m_max * 8 * bperm_per;
+  }
 #undef HCHK
   retire_tmps(h);
   timer.mark("pair lists + uploads (device)");

@@ -97,7 +97,15 @@ def test_branch_trajectory_matches_oracle(name):
 @pytest.mark.parametrize("name", ["gauge_1e15", "gauge_1e16"])
 def test_gauge_runs_agree_on_gauge_invariants(name):
     c, s, (sm_o, tr_o, sol_o), (sm_g, tr_g, sol_g) = _solve_both(name)
-    k = L.decisive_prefix(tr_o)
+    # With D^2 = diag / 3e15 the step's gauge component is rounding
+    # amplified, so even a decision whose cost change is well above the cost's
+    # own rounding can flip with the summation order: reordering the U_c sums
+    # of the Jacobian pass alone (same values, per-camera instead of
+    # per-chunk reduction) turned the oracle's 'AAR' into 'ARA' at iteration
+    # 2, whose cost change is 4.3e-5 of the cost (measured on MI355X).  Only
+    # decisions above 1e-4 of the cost are compared step by step; the
+    # optimum and the gauge invariants below are compared tightly.
+    k = L.decisive_prefix(tr_o, rel=1e-4)
     assert seq_of(tr_g)[:k] == seq_of(tr_o)[:k]
     # (the prefix steps are taken with D^2 = diag / 3e15: their gauge
     # components are rounding amplified by ~1e15, so the costs after them

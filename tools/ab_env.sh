@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B kernel stats of tools/ab_solve.py (C3 solve) under environment variants:
+#   bash tools/ab_env.sh label1='SFM_OBS_RUNS=1' label2='SFM_AMD_LIB=tools/var_head.so SFM_OBS_RUNS=4' ...
+# each variant twice in alternation (same box); prints the final cost and the
+# top kernels of each run.
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+for pass in 1 2; do
+for spec in "$@"; do
+  label=${spec%%=*}; vars=${spec#*=}
+  rm -rf $R/gpurun_out/ab_${label}_$pass
+  (
+    for kv in $vars; do
+      case $kv in SFM_AMD_LIB=*) export SFM_AMD_LIB=$R/${kv#SFM_AMD_LIB=} ;; *) export "$kv" ;; esac
+    done
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ab_${label}_$pass -- python3 $R/tools/ab_solve.py > $R/gpurun_out/ab_${label}_$pass.log 2>&1
+  ) || { echo "$label failed"; tail $R/gpurun_out/ab_${label}_$pass.log; exit 1; }
+  grep final_cost $R/gpurun_out/ab_${label}_$pass.log | sed "s/^/$label /"
+  python3 $R/tools/kstats.py $R/gpurun_out/ab_${label}_$pass | grep -E "k_jacobian|k_obs_prep|k_cam_sum|k_schur_diag|k_chol|k_schur_pts" | sed "s/^/$label /"
+done
+done
