@@ -369,6 +369,23 @@ def brisk_leg(device: int, cpu: bool, n_frames: int = 20) -> dict:
     out = {"workload": f"BRISK detect + describe (threshold 60, 6 octaves) on {n_frames} rendered 1280x720 frames, "
                        "host image in, keypoints + 64-B descriptors out",
            "ms_per_frame": wall / n_frames * 1e3, "keypoints_per_frame": nk / n_frames, "cpu_baseline": None}
+    # one upload per frame: the KLT handle's push (pyramid + derivatives)
+    # then BRISK on its resident frame (sfm_klt_brisk_detect_describe)
+    from sfm_amd.klt import KLTTracker
+    klt = KLTTracker(frames[0].shape[1], frames[0].shape[0], device=device)
+    try:
+        klt.push_frame(frames[0])
+        brisk.detect_resident(klt)
+        t0 = time.perf_counter()
+        for f in frames:
+            klt.push_frame(f)
+            brisk.detect_resident(klt)
+        wall_r = time.perf_counter() - t0
+    finally:
+        klt.close()
+    out["resident_klt_frame"] = {"ms_per_frame": wall_r / n_frames * 1e3,
+                                 "workload": "per frame: sfm_klt_push_frame (the one upload: pyramid + Scharr "
+                                             "derivatives) + BRISK detect + describe on the resident frame"}
     if cpu:
         from oracle import brisk_oracle as B
         t0 = time.perf_counter()

@@ -415,6 +415,14 @@ typedef struct sfm_gftt_params {
   double subpix_epsilon;   /* 0.03 TermCriteria EPS (CTracker.cpp:256) */
 } sfm_gftt_params;
 void sfm_gftt_default_params(sfm_gftt_params* p);
+/* CTracker::detectFeatures (CTracker.cpp:275-287) on the handle's current
+ * frame (the one sfm_klt_push_frame uploaded): the same BRISK detector and
+ * descriptor as sfm_brisk_detect_describe, with no second upload of the
+ * image -- one upload per frame serves the KLT pyramid, the corner detector
+ * and BRISK.  Outputs and errors as sfm_brisk_detect_describe. */
+int sfm_klt_brisk_detect_describe(sfm_klt_handle* h, int32_t threshold, int32_t octaves, int32_t capacity,
+                                  float* kps, int32_t* octave, uint8_t* desc, int32_t* n_out);
+
 /* Corners of the handle's current frame (after sfm_klt_push_frame), in the
  * reference's order (response descending), refined to subpixel; pts
  * [capacity][2] float, capacity >= max_corners (<= 4096). */

@@ -152,6 +152,8 @@ _SIGNATURES = {
     "sfm_representative_descriptors": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "sfm_brisk_describe": (c_int, [c_int32, c_void_p, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_void_p,
                                    c_void_p, POINTER(c_int32)]),
+    "sfm_klt_brisk_detect_describe": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]),
     "sfm_brisk_detect_describe": (c_int, [c_int32, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                           c_void_p, c_void_p, POINTER(c_int32)]),
     "sfm_map_create": (c_int, [c_int32, c_int32, POINTER(c_void_p)]),

@@ -33,6 +33,19 @@ def describe(img, keypoints, device: int = 0):
     return kept[:k].copy(), ang[:k].copy(), desc[:k].copy()
 
 
+def _detect_call(call, cap: int, describe: bool):
+    for _ in range(2):  # the call reports the count before it rejects a short buffer
+        kps = np.zeros((cap, 5), np.float32)
+        lay = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, DESC_BYTES), np.uint8) if describe else None
+        n = ctypes.c_int32()
+        rc = call(cap, kps, lay, desc, n)
+        if rc == 0 or n.value <= cap:
+            break
+        cap = n.value
+    return rc, kps, lay, desc, n.value
+
+
 def detect(img, threshold: int = 60, octaves: int = 6, describe: bool = True, device: int = 0):
     """CTracker::detectFeatures: BriskFeatureDetector(threshold, octaves,
     true) + the descriptor.  -> (keypoints [n][5] (x, y, size, angle,
@@ -40,18 +53,22 @@ def detect(img, threshold: int = 60, octaves: int = 6, describe: bool = True, de
     im = np.ascontiguousarray(img, np.uint8)
     if im.ndim != 2:
         raise ValueError("img must be 2-D 8-bit grey")
-    cap = max(1024, im.shape[0] * im.shape[1] // 64)
-    for _ in range(2):  # the call reports the count before it rejects a short buffer
-        kps = np.zeros((cap, 5), np.float32)
-        lay = np.zeros(cap, np.int32)
-        desc = np.zeros((cap, DESC_BYTES), np.uint8) if describe else None
-        n = ctypes.c_int32()
-        rc = lib().sfm_brisk_detect_describe(device, ptr(im), im.shape[1], im.shape[0], int(threshold), int(octaves),
-                                             cap, ptr(kps), ptr(lay), ptr(desc) if describe else None,
-                                             ctypes.byref(n))
-        if rc == 0 or n.value <= cap:
-            break
-        cap = n.value
+    rc, kps, lay, desc, k = _detect_call(
+        lambda cap, kps, lay, desc, n: lib().sfm_brisk_detect_describe(
+            device, ptr(im), im.shape[1], im.shape[0], int(threshold), int(octaves), cap, ptr(kps), ptr(lay),
+            ptr(desc) if desc is not None else None, ctypes.byref(n)),
+        max(1024, im.shape[0] * im.shape[1] // 64), describe)
     check(rc, "sfm_brisk_detect_describe")
-    k = n.value
+    return kps[:k].copy(), lay[:k].copy(), (desc[:k].copy() if describe else None)
+
+
+def detect_resident(klt, threshold: int = 60, octaves: int = 6, describe: bool = True):
+    """detect() on the current frame of a KLTTracker (sfm_klt_brisk_detect_
+    describe): the frame sfm_klt_push_frame uploaded, no second upload."""
+    rc, kps, lay, desc, k = _detect_call(
+        lambda cap, kps, lay, desc, n: lib().sfm_klt_brisk_detect_describe(
+            klt._h, int(threshold), int(octaves), cap, ptr(kps), ptr(lay), ptr(desc) if desc is not None else None,
+            ctypes.byref(n)),
+        max(1024, klt.width * klt.height // 64), describe)
+    check(rc, "sfm_klt_brisk_detect_describe")
     return kps[:k].copy(), lay[:k].copy(), (desc[:k].copy() if describe else None)

@@ -819,9 +819,13 @@ extern "C" int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w,
   return ok ? 0 : bfail(SFM_EIO, "allocation, kernel or copy failed");
 }
 
-extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, int32_t threshold,
-                                         int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
-                                         uint8_t* desc, int32_t* n_out) {
+// BRISK on an 8-bit frame that is either in host memory (uploaded here) or
+// already resident on the device (sfm_klt_brisk_detect_describe: the KLT
+// handle's current frame, copied device to device).
+namespace sfm {
+int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_device, int32_t w, int32_t h,
+                               int32_t threshold, int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
+                               uint8_t* desc, int32_t* n_out) {
   if (!n_out) return bfail(SFM_EINVAL, "n_out is NULL");
   *n_out = 0;
   if (w < 8 || h < 8 || threshold < 1 || threshold > 255 || octaves < 0 || 2 * octaves > kMaxLayers || capacity < 0)
@@ -855,7 +859,9 @@ extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int
   auto* cand = static_cast<Cand*>(W->get(2, sizeof(Cand) * size_t(cap_c), &rc));
   auto* cnt = static_cast<int32_t*>(W->get(3, sizeof(int32_t), &rc));
   if (rc) return rc;
-  if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess) return bfail(SFM_EIO, "upload failed");
+  if (hipMemcpy(limg, img, size_t(w) * h, img_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return bfail(SFM_EIO, "frame copy failed");
   for (int i = 1; i < nuse; ++i) {
     if (lw[i] < 1 || lh[i] < 1) continue;
     // resize(INTER_AREA): OpenCV's scales are 1 / (dsize / ssize); exactly 2
@@ -950,4 +956,11 @@ extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int
   *n_out = m;
   if (m > capacity) return bfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(m));
   return 0;
+}
+}  // namespace sfm
+
+extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, int32_t threshold,
+                                         int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
+                                         uint8_t* desc, int32_t* n_out) {
+  return brisk_detect_describe_impl(device, img, false, w, h, threshold, octaves, capacity, kps, octave, desc, n_out);
 }

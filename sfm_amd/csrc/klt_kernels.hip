@@ -326,6 +326,13 @@ int pyramid_levels(int w, int h, int max_level, int win) {
 
 }  // namespace
 
+namespace sfm {
+// brisk_kernels.hip
+int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_device, int32_t w, int32_t h,
+                               int32_t threshold, int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
+                               uint8_t* desc, int32_t* n_out);
+}  // namespace sfm
+
 struct sfm_klt_handle {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -517,6 +524,17 @@ int sfm_klt_push_frame(sfm_klt_handle* h, const uint8_t* grey, int32_t stride) {
   ++h->n_frames;
   h->timed_push = true;
   return 0;
+}
+
+int sfm_klt_brisk_detect_describe(sfm_klt_handle* h, int32_t threshold, int32_t octaves, int32_t capacity,
+                                  float* kps, int32_t* octave, uint8_t* desc, int32_t* n_out) {
+  if (!h || !n_out) return kfail(SFM_EINVAL, "NULL argument");
+  if (h->n_frames == 0) return kfail(SFM_EINVAL, "no frame pushed");
+  hipSetDevice(h->device);
+  // (push_frame left its stream drained; this keeps any later use ordered)
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return kfail(SFM_EIO, "klt stream failed");
+  return sfm::brisk_detect_describe_impl(h->device, h->img[h->cur], true, h->w, h->h, threshold, octaves, capacity,
+                                         kps, octave, desc, n_out);
 }
 
 int sfm_klt_get_level(sfm_klt_handle* h, int32_t which, int32_t level, uint8_t* img, int16_t* dxy, int32_t* w,

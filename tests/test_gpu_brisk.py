@@ -90,3 +90,26 @@ def test_detect_describe_end_to_end(pattern):
     np.testing.assert_array_equal(kp[:, :3], ok[kept, :3])
     np.testing.assert_array_equal(kp[:, 3], oang)
     assert (desc == odesc).all()
+
+
+def test_detector_on_the_resident_klt_frame():
+    """sfm_klt_brisk_detect_describe: BRISK on the frame the KLT handle
+    already holds (one upload per frame) equals the host-image call exactly,
+    for the current frame after several pushes (ping-pong slots)."""
+    from sfm_amd import brisk
+    from sfm_amd.klt import KLTTracker
+    img0 = _frame(3)
+    klt = KLTTracker(img0.shape[1], img0.shape[0])
+    try:
+        for k in (3, 4, 5):
+            img = _frame(k)
+            klt.push_frame(img)
+            a = brisk.detect_resident(klt)
+            b = brisk.detect(img)
+            assert len(a[0]) > 300
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+        # the corner detector and LK keep working on the same resident frame
+        assert len(klt.detect_features()) > 100
+    finally:
+        klt.close()

@@ -1,29 +1,87 @@
-"""Where the one-shot keyframe-sized solve spends its time (C1: 20 cams /
-2k pts / 20k obs): handle creation, set_problem, the resident solve,
-parameter download, destroy; then the resident solve alone."""
-import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import sfm_amd
-from sfm_amd import scene as S
+"""C1 keyframe-sized one-shot solve latency (bench incremental_ba leg): wall
+time per sfm_ba_solve, and with --trace the kernel / copy timeline of the
+last solve from a rocprofv3 kernel + memory-copy trace directory.
+    python tools/c1_latency.py                 # timing only
+    rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -- python3 tools/c1_latency.py
+    python tools/c1_latency.py --summarise DIR"""
+import glob
+import os
+import sys
+import time
 
-sc = S.config(os.environ.get("CFG", "C1"))
-for rep in range(4):
-    t = [time.perf_counter()]
-    ba = sfm_amd.BundleAdjuster(0); t.append(time.perf_counter())
-    ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X); t.append(time.perf_counter())
-    sm, _ = ba.solve(); t.append(time.perf_counter())
-    ba.parameters(); t.append(time.perf_counter())
-    ba.close(); t.append(time.perf_counter())
-    d = np.diff(t) * 1e3
-    print("create %.3f set_problem %.3f solve %.3f params %.3f destroy %.3f ms" % tuple(d), flush=True)
-ba = sfm_amd.BundleAdjuster(0)
-ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
-ba.solve()
-ba.set_profiling(True)
-t0 = time.perf_counter()
-for _ in range(20):
-    ba.reset(); sm, _ = ba.solve()
-ba.sync()
-print("resident solve %.3f ms, %d iterations" % ((time.perf_counter() - t0) / 20 * 1e3, sm.num_iterations))
-print({k: round(v["ms"] / 20, 4) for k, v in ba.phase_times().items()})
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run():
+    import numpy as np
+    import sfm_amd
+    from sfm_amd import scene as S
+    sc = S.config("C1")
+    walls = []
+    for k in range(30):
+        r, t, X = sc.rot.copy(), sc.t.copy(), sc.X.copy()
+        t0 = time.perf_counter()
+        sm, _ = sfm_amd.solve(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, r, t, X)
+        walls.append(time.perf_counter() - t0)
+    w = np.array(walls[5:]) * 1e3
+    print(f"C1 one-shot: median {np.median(w):.3f} ms, min {w.min():.3f} ms, iterations {sm.num_iterations}")
+    ba = sfm_amd.BundleAdjuster(0)
+    ts, tv, tg = [], [], []
+    for k in range(30):
+        t0 = time.perf_counter()
+        ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
+        t1 = time.perf_counter()
+        sm, _ = ba.solve()
+        t2 = time.perf_counter()
+        ba.parameters()
+        t3 = time.perf_counter()
+        ts.append(t1 - t0); tv.append(t2 - t1); tg.append(t3 - t2)
+    f = lambda a: float(np.median(np.array(a[5:]) * 1e3))
+    print(f"resident: set_problem {f(ts):.3f} ms, solve {f(tv):.3f} ms, get_parameters {f(tg):.3f} ms")
+    ba.close()
+
+
+def summarise(d):
+    import csv
+    kf = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)
+    mf = glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True)
+    ev = []
+    for f in kf:
+        for r in csv.DictReader(open(f)):
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("sfm::", "")
+            n = n.split("(")[0] if not n.startswith("void rocprim") else "rocprim " + n.split("detail::")[2][:30]
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K " + n[:44]))
+    for f in mf:
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C " + r.get("Direction", "copy")))
+    ev.sort()
+    # the last 25 solves (the first 5 are warm-up): per-solve averages
+    nsolve = 25
+    per = len(ev) // 30
+    last = ev[len(ev) - per * nsolve:]
+    t0 = last[0][0]
+    busy = sum(e[1] - e[0] for e in last)
+    print(f"per solve: {len(last) / nsolve:.0f} events, span {(last[-1][1] - t0) / 1e3 / nsolve:.1f} us, "
+          f"busy {busy / 1e3 / nsolve:.1f} us")
+    kinds = {}
+    for s_, e_, n in last:
+        kinds.setdefault(n, [0, 0])
+        kinds[n][0] += 1
+        kinds[n][1] += e_ - s_
+    for n, (c, tt) in sorted(kinds.items(), key=lambda x: -x[1][1])[:30]:
+        print(f"  {n:46s} x{c / nsolve:5.1f} {tt / 1e3 / nsolve:8.1f} us")
+    prev = t0
+    gaps = []
+    for s_, e_, n in last:
+        gaps.append((s_ - prev, n))
+        prev = max(prev, e_)
+    gaps.sort(reverse=True)
+    print("gap total per solve (us):", round(sum(g for g, _ in gaps) / 1e3 / nsolve, 1))
+    print("largest gaps before:", [(round(g / 1e3, 1), n) for g, n in gaps[:12]])
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--summarise":
+        summarise(sys.argv[2])
+    else:
+        run()
