@@ -336,7 +336,8 @@ def live_path_leg(device: int, cpu: bool, n_frames: int = 300) -> dict:
            "last_ba": None if last is None else {"cams": int(last["rot"].shape[0]), "points": int(last["X"].shape[0]),
                                                   "obs": int(len(last["uv"])),
                                                   "lm_iterations": last["summary"].num_iterations},
-           "host_s": {k: round(val, 4) for k, val in s.times.items() if k != "stream"}, "cpu_baseline": None}
+           "host_s": {k: round(val, 4) for k, val in s.times.items() if k != "stream"},
+           "ba_solves": len(s.ba_log), "ba_lm_iterations": int(s.stats.get("ba_iterations", 0)), "cpu_baseline": None}
     if cpu and s.ba_log:
         from oracle import ffi as O
         t0 = time.perf_counter()

@@ -190,13 +190,16 @@ namespace {
 void* scratch(sfm_map* h, const char* name, size_t bytes, int* rc) {
   auto& e = h->scratch[name];
   if (e.second >= bytes && e.first) return e.first;
+  // grow by half again at least: the map grows every keyframe, and a
+  // reallocation costs a stream synchronisation plus hipFree / hipMalloc
+  const size_t want = std::max<size_t>({bytes, e.second + e.second / 2, 256});
   if (e.first) { (void)hipStreamSynchronize(h->s); (void)hipFree(e.first); e.first = nullptr; e.second = 0; }
   void* p = nullptr;
-  if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) {
+  if (hipMalloc(&p, want) != hipSuccess) {
     *rc = mapfail(SFM_ENOMEM, std::string("hipMalloc failed (") + name + ")");
     return nullptr;
   }
-  e = {p, std::max<size_t>(bytes, 256)};
+  e = {p, want};
   return p;
 }
 

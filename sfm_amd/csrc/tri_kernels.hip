@@ -8,6 +8,7 @@
 // so the K[R|t] composition is the build's reading (parity unpinned; oracle:
 // oracle/pnp_oracle.py triangulate_points).  One lane per point.
 #include <hip/hip_runtime.h>
+#include <map>
 #include <string>
 #include "../../include/sfm_amd.h"
 #include "cv_linalg.h"
@@ -44,6 +45,41 @@ __global__ __launch_bounds__(256) void k_triangulate(int n, const int32_t* __res
   if (w4) w4[i] = h;
 }
 
+// Per calling thread and device: a stream and a grow-only buffer, kept
+// between calls (triangulation runs once per keyframe pair in the mapping
+// loop: creating a stream and allocating per call cost ~4 ms per call).
+struct TriCtx {
+  hipStream_t s = nullptr;
+  char* buf = nullptr;
+  size_t cap = 0;
+};
+struct TriCache {
+  std::map<int, TriCtx> by_dev;
+  ~TriCache() {
+    for (auto& kv : by_dev) {
+      (void)hipSetDevice(kv.first);
+      if (kv.second.s) (void)hipStreamDestroy(kv.second.s);
+      if (kv.second.buf) (void)hipFree(kv.second.buf);
+    }
+  }
+};
+TriCtx* tri_ctx(int device, size_t bytes) {
+  static thread_local TriCache cache;
+  TriCtx& c = cache.by_dev[device];
+  if (!c.s && hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess) {
+    c.s = nullptr;
+    return nullptr;
+  }
+  if (c.cap < bytes) {
+    if (c.buf) (void)hipFree(c.buf);
+    c.buf = nullptr;
+    c.cap = 0;
+    if (hipMalloc(&c.buf, bytes) != hipSuccess) return nullptr;
+    c.cap = bytes;
+  }
+  return &c;
+}
+
 }  // namespace
 }  // namespace sfm
 
@@ -65,30 +101,28 @@ extern "C" int sfm_triangulate_points(int32_t device, int32_t n, const int32_t* 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return fail(SFM_ENODEV, "no device");
   if (hipSetDevice(device) != hipSuccess) return fail(SFM_ENODEV, "hipSetDevice failed");
-  // one allocation for inputs and output (keyframe-sized batches)
+  // one buffer for inputs and output (keyframe-sized batches), kept per thread
   const size_t b_idx = sizeof(int32_t) * 2 * size_t(n), b_uv = sizeof(double) * 4 * size_t(n),
                b_P = sizeof(double) * 12 * size_t(n_cams), b_X = sizeof(double) * 3 * size_t(n);
-  char* buf = nullptr;
-  if (hipMalloc(&buf, b_idx + b_uv + b_P + b_X + 64) != hipSuccess) return fail(SFM_ENOMEM, "hipMalloc failed");
+  TriCtx* ctx = tri_ctx(device, b_idx + b_uv + b_P + b_X + 64);
+  if (!ctx) return fail(SFM_ENOMEM, "stream or device buffer allocation failed");
+  char* buf = ctx->buf;
   int32_t* d_c = reinterpret_cast<int32_t*>(buf);
   double* d_uv = reinterpret_cast<double*>(buf + ((b_idx + 15) & ~size_t(15)));
   double* d_P = d_uv + 4 * size_t(n);
   double* d_X = d_P + 12 * size_t(n_cams);
-  hipStream_t s = nullptr;
+  hipStream_t s = ctx->s;
   int rc = 0;
-  if (hipStreamCreate(&s) != hipSuccess) rc = fail(SFM_EIO, "hipStreamCreate failed");
-  if (!rc && (hipMemcpyAsync(d_c, cam0, sizeof(int32_t) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-              hipMemcpyAsync(d_c + n, cam1, sizeof(int32_t) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-              hipMemcpyAsync(d_uv, uv0, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-              hipMemcpyAsync(d_uv + 2 * size_t(n), uv1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-              hipMemcpyAsync(d_P, P, b_P, hipMemcpyHostToDevice, s) != hipSuccess))
+  if (hipMemcpyAsync(d_c, cam0, sizeof(int32_t) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_c + n, cam1, sizeof(int32_t) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_uv, uv0, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_uv + 2 * size_t(n), uv1, sizeof(double) * 2 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d_P, P, b_P, hipMemcpyHostToDevice, s) != hipSuccess)
     rc = fail(SFM_EIO, "upload failed");
   if (!rc) {
     k_triangulate<<<(n + 255) / 256, 256, 0, s>>>(n, d_c, d_c + n, d_uv, d_uv + 2 * size_t(n), d_P, d_X, nullptr);
     if (hipMemcpyAsync(X, d_X, b_X, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
       rc = fail(SFM_EIO, "triangulation failed");
   }
-  if (s) hipStreamDestroy(s);
-  hipFree(buf);
   return rc;
 }

@@ -145,8 +145,8 @@ def pair_frame_observations(p3, p2):
     p3 = np.asarray(p3)
     p2 = np.asarray(p2)
     n = len(p3)
-    if n == 0:
-        return p2[:0]
+    if n == len(p2):  # no point twice in the frame (k = 1 everywhere)
+        return p2
     _, inv, cnt = np.unique(p3, return_inverse=True, return_counts=True)
     k = cnt[inv]
     o = np.concatenate([[0], np.cumsum(k)[:-1]])
@@ -408,7 +408,10 @@ class LiveSfM:
         K9 = np.tile(self.K.reshape(1, 9), (C, 1))
         rec = {"uv": uv.copy(), "cam_idx": cam.copy(), "pt_idx": pt.copy(), "K": K9, "rot": rot.copy(), "t": t.copy(),
                "X": X.copy()}
+        t_s = time.perf_counter()
         sm, tr = _ba.solve(uv, cam, pt, K9, rot, t, X)
+        self.times["ba_solve"] = self.times.get("ba_solve", 0.0) + time.perf_counter() - t_s
+        self.stats["ba_iterations"] = self.stats.get("ba_iterations", 0) + sm.num_iterations
         rec.update({"summary": sm, "trace": tr, "rot_out": rot.copy(), "t_out": t.copy(), "X_out": X.copy()})
         self.ba_log.append(rec)
         for c, f in enumerate(self.kfs):
