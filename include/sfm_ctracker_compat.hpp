@@ -295,6 +295,23 @@ class FeatureMatcher {
   int32_t n_[2] = {0, 0};
 };
 
+// sfm_brisk_detect_describe's packed output -> cv::KeyPoint-like objects
+template <class KeyPoint>
+inline void unpack_keypoints(const std::vector<float>& k, const std::vector<int32_t>& oct,
+                             const std::vector<uint8_t>& d, int32_t n, std::vector<KeyPoint>& keypoints,
+                             std::vector<uint8_t>& descriptors) {
+  keypoints.resize(size_t(n));
+  for (int32_t i = 0; i < n; ++i) {
+    keypoints[i].pt.x = k[5 * size_t(i)];
+    keypoints[i].pt.y = k[5 * size_t(i) + 1];
+    keypoints[i].size = k[5 * size_t(i) + 2];
+    keypoints[i].angle = k[5 * size_t(i) + 3];
+    keypoints[i].response = k[5 * size_t(i) + 4];
+    keypoints[i].octave = oct[i];
+  }
+  descriptors.assign(d.begin(), d.begin() + 64 * size_t(n));
+}
+
 // Drop-in for CTracker::computeOpticalFlow (CTracker.h:60,
 // CTracker.cpp:480-562).  The reference reads its member frames
 // (_prevFrame/_currFrame: getFrameGrey(), getPointsDistorted()) and fills
@@ -362,6 +379,25 @@ class OpticalFlowTracker {
     }
     if (rc_out) *rc_out = rc;
     return rc == SFM_OK && int(pts.size()) >= minFeatures;
+  }
+
+  // CTracker::detectFeatures (CTracker.cpp:275-287) on the frame pushed
+  // last, without a second upload (sfm_klt_brisk_detect_describe): the same
+  // outputs as sfm_compat::detectFeatures(grey, ...) below.
+  template <class KeyPoint>
+  int detectFeaturesBrisk(std::vector<KeyPoint>& keypoints, std::vector<uint8_t>& descriptors, int threshold = 60,
+                          int octaves = 6, int32_t capacity = 20000) {
+    keypoints.clear();
+    descriptors.clear();
+    if (!h_) return rc_;
+    std::vector<float> k(5 * size_t(capacity));
+    std::vector<int32_t> oct(static_cast<size_t>(capacity));
+    std::vector<uint8_t> d(64 * size_t(capacity));
+    int32_t n = 0;
+    const int rc = sfm_klt_brisk_detect_describe(h_, threshold, octaves, capacity, k.data(), oct.data(), d.data(), &n);
+    if (rc) return rc;
+    unpack_keypoints(k, oct, d, n, keypoints, descriptors);
+    return SFM_OK;
   }
 
   template <class Point2>
@@ -434,16 +470,7 @@ inline int detectFeatures(const GreyMat& grey, std::vector<KeyPoint>& keypoints,
   const int rc = sfm_brisk_detect_describe(device, img, w, h, threshold, octaves, capacity, k.data(), oct.data(),
                                            d.data(), &n);
   if (rc) return rc;
-  keypoints.resize(size_t(n));
-  for (int32_t i = 0; i < n; ++i) {
-    keypoints[i].pt.x = k[5 * size_t(i)];
-    keypoints[i].pt.y = k[5 * size_t(i) + 1];
-    keypoints[i].size = k[5 * size_t(i) + 2];
-    keypoints[i].angle = k[5 * size_t(i) + 3];
-    keypoints[i].response = k[5 * size_t(i) + 4];
-    keypoints[i].octave = oct[i];
-  }
-  descriptors.assign(d.begin(), d.begin() + 64 * size_t(n));
+  unpack_keypoints(k, oct, d, n, keypoints, descriptors);
   return SFM_OK;
 }
 
@@ -552,6 +579,39 @@ class MapStore {
       }
       if (std::max(n3, n2) <= cap) return rc;
       cap = std::max(n3, n2);
+    }
+    return SFM_EINVAL;
+  }
+
+  // getPointsInFrame for every frame of frameNo in one device query (the
+  // per-keyframe loop of CSfM::bundleAdjustment, CSfM.cpp:321-340):
+  // pts3DIdx[k] / pts2DIdx[k] receive frame frameNo[k]'s lists, as
+  // getPointsInFrame would append them.  A frame may not be listed twice.
+  int getPointsInFrameMulti(const std::vector<int>& frameNo, std::vector<std::vector<int>>& pts3DIdx,
+                            std::vector<std::vector<int>>& pts2DIdx) {
+    if (!h_) return rc_;
+    const size_t nf = frameNo.size();
+    pts3DIdx.resize(nf);
+    pts2DIdx.resize(nf);
+    int32_t np = 0;
+    int64_t no = 0, nd = 0;
+    if (int rc = sfm_map_size(h_, &np, &no, &nd)) return rc;
+    std::vector<int32_t> fr(frameNo.begin(), frameNo.end()), o3(nf + 1), o2(nf + 1);
+    int64_t cap = std::max<int64_t>(1, no);
+    for (int attempt = 0; attempt < 2; ++attempt) {  // the 2D lists can outgrow n_obs: retry at the reported size
+      std::vector<int32_t> a(static_cast<size_t>(cap)), b(static_cast<size_t>(cap));
+      const int rc = sfm_map_points_in_frame_multi(h_, int32_t(nf), fr.data(), cap, a.data(), o3.data(), b.data(),
+                                                   o2.data());
+      if (rc == SFM_OK) {
+        for (size_t k = 0; k < nf; ++k) {
+          pts3DIdx[k].insert(pts3DIdx[k].end(), a.begin() + o3[k], a.begin() + o3[k + 1]);
+          pts2DIdx[k].insert(pts2DIdx[k].end(), b.begin() + o2[k], b.begin() + o2[k + 1]);
+        }
+        return SFM_OK;
+      }
+      const int64_t need = std::max<int64_t>(o3[nf], o2[nf]);
+      if (need <= cap) return rc;
+      cap = need;
     }
     return SFM_EINVAL;
   }

@@ -239,6 +239,25 @@ static int run_brisk(const std::string& dir) {
   wr(dir, "out_kp.f32", k);
   wr(dir, "out_octave.i32", oct);
   wr(dir, "out_desc.u8", desc);
+  // the same frame pushed into the optical-flow tracker, BRISK on its
+  // resident copy (OpticalFlowTracker::detectFeaturesBrisk: one upload)
+  sfm_compat::OpticalFlowTracker flow(meta[0], meta[1]);
+  if (flow.status() || flow.pushFrame(g)) { std::printf("brisk flow rc=%d %s\n", flow.status(), sfm_last_error()); return 1; }
+  std::vector<KeyPoint> kr;
+  std::vector<uint8_t> dr;
+  if (int r2 = flow.detectFeaturesBrisk(kr, dr, meta[2], meta[3])) {
+    std::printf("brisk resident rc=%d %s\n", r2, sfm_last_error());
+    return 1;
+  }
+  k.clear();
+  oct.clear();
+  for (auto& p : kr) {
+    k.insert(k.end(), {p.pt.x, p.pt.y, p.size, p.angle, p.response});
+    oct.push_back(p.octave);
+  }
+  wr(dir, "out_kp_res.f32", k);
+  wr(dir, "out_octave_res.i32", oct);
+  wr(dir, "out_desc_res.u8", dr);
   return 0;
 }
 
@@ -313,6 +332,20 @@ static int run_map(const std::string& dir) {
       for (int i : a) out << ' ' << i;
       out << ' ' << b.size();
       for (int i : b) out << ' ' << i;
+      out << '\n';
+    } else if (op == "QB") {   // getPointsInFrameMulti (the BA gather): nf frames -> one line
+      int nf;
+      is >> nf;
+      auto frames = ints(is, nf);
+      std::vector<std::vector<int>> a, b;
+      if ((rc = cmap.getPointsInFrameMulti(frames, a, b))) break;
+      out << "QB";
+      for (int k = 0; k < nf; ++k) {
+        out << ' ' << a[k].size();
+        for (int i : a[k]) out << ' ' << i;
+        out << ' ' << b[k].size();
+        for (int i : b[k]) out << ' ' << i;
+      }
       out << '\n';
     } else if (op == "QM") {   // getPointsInFrame_Mutable: the pointers, as point indices
       int f;

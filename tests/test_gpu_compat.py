@@ -190,6 +190,10 @@ def test_detect_features_drop_in(tmp_path):
     np.testing.assert_array_equal(kp[:, 4], ok[kept, 3])
     assert oc.tolist() == ok[kept, 4].astype(int).tolist()
     assert (desc == odesc).all()
+    # OpticalFlowTracker::detectFeaturesBrisk on the pushed (resident) frame
+    np.testing.assert_array_equal(_r(tmp_path, "out_kp_res.f32", np.float32).reshape(-1, 5), kp)
+    np.testing.assert_array_equal(_r(tmp_path, "out_octave_res.i32", np.int32), oc)
+    np.testing.assert_array_equal(_r(tmp_path, "out_desc_res.u8", np.uint8).reshape(-1, 64), desc)
 
 
 def _map_script(seed=5):
@@ -232,6 +236,7 @@ def _map_script(seed=5):
     for f in (0, 10, 20, 30, 40, 50, 60):
         lines += [f"Q {f}", f"QM {f}"]
     lines.append("QF 7 0 10 20 30 40 50 60")
+    lines.append("QB 7 60 0 20 10 50 40 30")                  # the BA gather, listed out of order
     lines.append(f"R 200 " + " ".join(map(str, q)))
     Xn = rng.normal(0, 1, (50, 3))
     lines.append(f"S 50 " + " ".join(map(str, q[:50])) + " " + " ".join(repr(float(x)) for x in Xn.ravel()))
@@ -267,6 +272,12 @@ def _apply_oracle(lines):
         elif op in ("Q", "QM"):
             p3, p2 = m.getPointsInFrame(int(t[1]))
             out.append(f"{op} {len(p3)} " + " ".join(map(str, p3)) + f" {len(p2)} " + " ".join(map(str, p2)))
+        elif op == "QB":
+            toks = ["QB"]
+            for f in map(int, t[2:2 + int(t[1])]):
+                p3, p2 = m.getPointsInFrame(f)
+                toks += [str(len(p3))] + list(map(str, p3)) + [str(len(p2))] + list(map(str, p2))
+            out.append(" ".join(toks))
         elif op == "R":
             n = int(t[1])
             _, rows = m.getRepresentativeDescriptors(list(map(int, t[2:2 + n])))
@@ -299,7 +310,7 @@ def test_map_store_drop_in_as_csfm_calls_it(tmp_path):
             np.testing.assert_array_equal(np.array(gt[1:], float), np.array(wt[1:], float))
         else:
             assert gt == wt, (gt[:8], wt[:8])
-    queries = [ln for ln in lines if ln.split()[0] in ("N", "QF", "Q", "QM", "R", "G", "C")]
+    queries = [ln for ln in lines if ln.split()[0] in ("N", "QF", "Q", "QM", "QB", "R", "G", "C")]
     assert len(queries) == len(want)
     toks = [w for q, w in zip(queries, want) if q == "Q 50"][-1].split()
     n3 = int(toks[1])
