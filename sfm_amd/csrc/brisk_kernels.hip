@@ -132,32 +132,74 @@ DevPattern* device_pattern(int device, int* rc) {
   return d;
 }
 
-// integral image [h+1][w+1] (int32: 255 * 1280 * 720 < 2^31)
-__global__ void k_integral_rows(const uint8_t* __restrict__ img, int w, int h, int32_t* __restrict__ ii) {
-  const int y = blockIdx.x * blockDim.x + threadIdx.x;
-  if (y > h) return;
+// integral image [h+1][w+1] (int32: 255 * 1280 * 720 < 2^31), exact
+// integer sums in three passes: (1) one workgroup per row, the row's prefix
+// sums (each thread a contiguous segment, a block scan of the segment
+// totals); (2) per column, the sums of bands of kIIBand rows; (3) per
+// (band, column), the previous bands' totals plus a running sum down the
+// band, in place.
+constexpr int kIIBand = 32;
+__global__ __launch_bounds__(256) void k_integral_rows(const uint8_t* __restrict__ img, int w, int h,
+                                                       int32_t* __restrict__ ii) {
+  __shared__ int32_t sc[256];
+  const int y = blockIdx.x, t = threadIdx.x;
   int32_t* row = ii + size_t(y) * (w + 1);
-  row[0] = 0;
-  int32_t s = 0;
+  const int per = (w + 255) / 256;
+  const int x0 = min(w, t * per), x1 = min(w, x0 + per);
   if (y == 0) {
-    for (int x = 0; x < w; ++x) row[x + 1] = 0;
+    for (int x = t; x <= w; x += 256) row[x] = 0;
     return;
   }
   const uint8_t* src = img + size_t(y - 1) * w;
-  for (int x = 0; x < w; ++x) {
+  int32_t tot = 0;
+  for (int x = x0; x < x1; ++x) tot += src[x];
+  sc[t] = tot;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int32_t v = t >= o ? sc[t - o] : 0;
+    __syncthreads();
+    sc[t] += v;
+    __syncthreads();
+  }
+  int32_t s = sc[t] - tot;  // exclusive prefix of the segments before this one
+  if (t == 0) row[0] = 0;
+  for (int x = x0; x < x1; ++x) {
     s += src[x];
     row[x + 1] = s;
   }
 }
-__global__ void k_integral_cols(int w, int h, int32_t* __restrict__ ii) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_integral_bandsum(int w, int h, const int32_t* __restrict__ ii,
+                                                          int32_t* __restrict__ band) {
+  const int x = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (x > w) return;
+  const int y0 = 1 + b * kIIBand, y1 = min(h, y0 + kIIBand - 1);
+  int32_t s = 0;
+  for (int y = y0; y <= y1; ++y) s += ii[size_t(y) * (w + 1) + x];
+  band[size_t(b) * (w + 1) + x] = s;
+}
+__global__ __launch_bounds__(256) void k_integral_cols(int w, int h, const int32_t* __restrict__ band,
+                                                       int32_t* __restrict__ ii) {
+  const int x = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
   if (x > w) return;
   int32_t s = 0;
-  for (int y = 1; y <= h; ++y) {
+  for (int q = 0; q < b; ++q) s += band[size_t(q) * (w + 1) + x];
+  const int y0 = 1 + b * kIIBand, y1 = min(h, y0 + kIIBand - 1);
+  for (int y = y0; y <= y1; ++y) {
     s += ii[size_t(y) * (w + 1) + x];
     ii[size_t(y) * (w + 1) + x] = s;
   }
 }
+// the three passes; band: ceil(h / kIIBand) x (w + 1) int32 scratch
+void integral_image(const uint8_t* img, int w, int h, int32_t* ii, int32_t* band, hipStream_t s = nullptr) {
+  const int nb = (h + kIIBand - 1) / kIIBand;
+  k_integral_rows<<<h + 1, 256, 0, s>>>(img, w, h, ii);
+  if (nb > 0) {
+    const dim3 g(unsigned((w + 1 + 255) / 256), unsigned(nb));
+    k_integral_bandsum<<<g, 256, 0, s>>>(w, h, ii, band);
+    k_integral_cols<<<g, 256, 0, s>>>(w, h, band, ii);
+  }
+}
+size_t integral_band_ints(int w, int h) { return size_t((h + kIIBand - 1) / kIIBand + 1) * size_t(w + 1); }
 
 // BRISK_Impl::smoothedIntensity for one pattern point
 __device__ int smoothed(const uint8_t* __restrict__ img, const int32_t* __restrict__ ii, int cols, float key_x,
@@ -792,9 +834,13 @@ extern "C" int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w,
   if (ok) {
     ok = hipMemcpy(d_img, img, npx, hipMemcpyHostToDevice) == hipSuccess &&
          hipMemcpy(d_kps, kps, size_t(n) * 12, hipMemcpyHostToDevice) == hipSuccess;
-    k_integral_rows<<<(h + 1 + 255) / 256, 256>>>(d_img, w, h, d_ii);
-    k_integral_cols<<<(w + 1 + 255) / 256, 256>>>(w, h, d_ii);
-    k_brisk_describe<<<n, 64>>>(d_img, w, h, d_ii, *P, d_kps, n, d_keep, d_ang, d_desc);
+    int32_t* d_band = nullptr;
+    ok = hipMalloc(&d_band, sizeof(int32_t) * integral_band_ints(w, h)) == hipSuccess;
+    if (ok) {
+      integral_image(d_img, w, h, d_ii, d_band);
+      k_brisk_describe<<<n, 64>>>(d_img, w, h, d_ii, *P, d_kps, n, d_keep, d_ang, d_desc);
+    }
+    if (d_band) (void)hipFree(d_band);
     std::vector<int32_t> kp(n);
     std::vector<float> an(n);
     std::vector<uint8_t> de(size_t(n) * n_bytes);
@@ -928,9 +974,9 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
     auto* ang = static_cast<float*>(W->get(11, sizeof(float) * size_t(n), &rc));
     auto* ii = static_cast<int32_t*>(W->get(12, sizeof(int32_t) * size_t(w + 1) * (h + 1), &rc));
     auto* dd = static_cast<uint8_t*>(W->get(13, size_t(n) * n_bytes, &rc));
+    auto* band = static_cast<int32_t*>(W->get(15, sizeof(int32_t) * integral_band_ints(w, h), &rc));
     if (rc) return rc;
-    k_integral_rows<<<(h + 1 + 255) / 256, 256>>>(limg, w, h, ii);
-    k_integral_cols<<<(w + 1 + 255) / 256, 256>>>(w, h, ii);
+    integral_image(limg, w, h, ii, band);
     k_brisk_describe<<<n, 64>>>(limg, w, h, ii, *P, kp3, n, keep, ang, dd);
     hd.resize(size_t(n) * n_bytes);
     if (hipMemcpy(hkeep.data(), keep, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
