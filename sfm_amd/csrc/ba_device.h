@@ -143,6 +143,12 @@ struct DevProblem {
   int32_t max_blocks = 0;
   double* scal = nullptr;     // [kNumScalars]
   double* scal_host = nullptr;  // pinned host mirror
+  // device-driven LM loop (sfm_ba_solve_resident on an unsharded problem):
+  // the gate of the phase being enqueued (kernels return at once when
+  // *gate == 0) and the trust-region radius the kernels read; both nullptr
+  // on the host-driven path
+  const int32_t* gate = nullptr;
+  const double* radius_dev = nullptr;
 };
 
 // Partial-sum slots (each max_blocks doubles).

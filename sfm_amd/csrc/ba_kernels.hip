@@ -97,7 +97,8 @@ __device__ void rotation(const double w[3], double R[9], double* dR) {
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __restrict__ cam,
-                                                       double* __restrict__ camR, double* __restrict__ part_xn) {
+                                                       double* __restrict__ camR, double* __restrict__ part_xn, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   double xn = 0.0;
@@ -196,7 +197,8 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ scale_p, int scaled,
                                                        double* __restrict__ jrec, double* __restrict__ part_cost,
-                                                       double* __restrict__ jpart, int write_rec) {
+                                                       double* __restrict__ jpart, int write_rec, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   __shared__ __attribute__((aligned(16))) double stage[kThreads * kJRec];  // 10 KB per wave
   const int l = threadIdx.x & 63;
@@ -326,7 +328,8 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
 // U_c and b_c from k_jacobian's per-chunk partials (jpart): lane t sums
 // chunks w0 + t, w0 + t + 64, ..., then one reduce-scatter over the wave.
 __global__ __launch_bounds__(64) void k_cam_sum(const int32_t* __restrict__ cam_rng,
-                                                const double* __restrict__ jpart, double* __restrict__ Ucam) {
+                                                const double* __restrict__ jpart, double* __restrict__ Ucam, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int c = blockIdx.x, t = threadIdx.x;
   const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
   double v[32];
@@ -344,7 +347,8 @@ __global__ __launch_bounds__(64) void k_cam_sum(const int32_t* __restrict__ cam_
 __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* __restrict__ Ucam,
                                                            double* __restrict__ scale_c, double* __restrict__ diag_c,
                                                            double min_diag, double max_diag, int mode, int reuse,
-                                                           double* __restrict__ part_grad) {
+                                                           double* __restrict__ part_grad, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   double g = 0.0;
@@ -442,7 +446,8 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t
                                                             double* __restrict__ scale_p, double* __restrict__ diag_p,
                                                             double* __restrict__ ptV, double min_diag, double max_diag,
                                                             int mode, int reuse, double* __restrict__ part_grad,
-                                                            double* __restrict__ part_xn) {
+                                                            double* __restrict__ part_xn, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double g = 0.0, xn = 0.0;
@@ -475,7 +480,8 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_lds(int P, int C, const
                                                              double* __restrict__ scale_p, double* __restrict__ diag_p,
                                                              double* __restrict__ ptV, double min_diag, double max_diag,
                                                              int mode, int reuse, double* __restrict__ part_grad,
-                                                             double* __restrict__ part_xn) {
+                                                             double* __restrict__ part_xn, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   __shared__ double cst[kMaxC * kCamE];
   for (int i = threadIdx.x; i < C * kCamE; i += blockDim.x) {
@@ -506,7 +512,9 @@ __global__ __launch_bounds__(kThreads) void k_point_factor(int P, const double* 
                                                            double* __restrict__ ptL, double* __restrict__ part_bad,
                                                            const double* __restrict__ X,
                                                            const double* __restrict__ scale_p,
-                                                           double* __restrict__ ptS) {
+                                                           double* __restrict__ ptS, const int* __restrict__ gate, const double* __restrict__ radius_dev) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double bad = 0.0;
@@ -618,7 +626,8 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
                                                           const double* __restrict__ Kc,
                                                           const double* __restrict__ scale_c,
                                                           const double* __restrict__ ptS,
-                                                          double* __restrict__ dpart) {
+                                                          double* __restrict__ dpart, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
   if (i0 >= N_pad) return;  // wave-uniform, no barriers below
@@ -663,7 +672,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
                                                            const double* __restrict__ scale_c,
                                                            const double* __restrict__ ptS,
                                                            const double* __restrict__ ysol, double* __restrict__ eu,
-                                                           double* __restrict__ part_model) {
+                                                           double* __restrict__ part_model, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
@@ -796,7 +806,8 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
                                                         const double* __restrict__ cam, const double* __restrict__ Kc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int ld,
-                                                        const int32_t* __restrict__ bperm) {
+                                                        const int32_t* __restrict__ bperm, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   constexpr int kPer = 64 / kSub;  // blocks per wave
   __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
@@ -913,7 +924,9 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        const double* __restrict__ Ucam,
                                                        const double* __restrict__ diag_c, double radius,
                                                        int add_diag, double* __restrict__ S, int ld, int n,
-                                                       int init) {
+                                                       int init, const int* __restrict__ gate, const double* __restrict__ radius_dev) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   const int c = blockIdx.x, t = threadIdx.x;
   const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
   // lane t sums waves w0 + t, w0 + t + 64, ... (coalesced 216-B rows), then
@@ -969,7 +982,8 @@ __global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, doub
 // Identity padding beyond the augmented row n (column-major lower view).
 // Identity padding of the augmented system, and the Cholesky failure flag
 // cleared (saves the separate memset dispatch before k_chol_fused).
-__global__ void k_pad_init(double* __restrict__ S, int ld, int n, int* __restrict__ fail) {
+__global__ void k_pad_init(double* __restrict__ S, int ld, int n, int* __restrict__ fail, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int j = blockIdx.x;
   if (j == 0 && threadIdx.x == 0) *fail = 0;
   for (int i = (j > n ? j : n + 1) + threadIdx.x; i < ld; i += blockDim.x) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
@@ -982,7 +996,8 @@ __global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __
                                                          const double* __restrict__ ysol,
                                                          const double* __restrict__ scale_c,
                                                          double* __restrict__ cam_new, double* __restrict__ camRn,
-                                                         double* __restrict__ part_step, double* __restrict__ part_bad) {
+                                                         double* __restrict__ part_step, double* __restrict__ part_bad, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0;
@@ -1017,7 +1032,9 @@ __global__ __launch_bounds__(kThreads) void k_cam_update(int C, const double* __
 // non-finite pivot sets fail bit 0, as a failed dense LLT does.
 __global__ __launch_bounds__(kThreads) void k_cam_solve(int C, const double* __restrict__ Ucam,
                                                         const double* __restrict__ diag_c, double radius,
-                                                        double* __restrict__ ysol, int* __restrict__ fail) {
+                                                        double* __restrict__ ysol, int* __restrict__ fail, const int* __restrict__ gate, const double* __restrict__ radius_dev) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double* U = Ucam + size_t(kUcam) * c;
@@ -1080,7 +1097,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
                                                         const double* __restrict__ X, double* __restrict__ X_new,
                                                         double* __restrict__ ypt, double* __restrict__ part_step,
                                                         double* __restrict__ part_bad,
-                                                        double* __restrict__ part_model) {
+                                                        double* __restrict__ part_model, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0, model = 0.0;
@@ -1142,7 +1160,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
                                                         const double* __restrict__ Kc,
                                                         const double* __restrict__ X_new,
                                                         const double* __restrict__ camRn,
-                                                        double* __restrict__ part_cost) {
+                                                        double* __restrict__ part_cost, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
@@ -1176,7 +1195,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
 // to seven launches and two copies (~5-6 us of dispatch each).
 __global__ __launch_bounds__(1024) void k_reduce_batch(const double* __restrict__ partials, int64_t max_blocks,
                                                        ReduceBatch b, double* __restrict__ scal,
-                                                       const int* __restrict__ fail) {
+                                                       const int* __restrict__ fail, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[16];
   const ReduceJob j = b.job[blockIdx.x];
   const double* src = partials + size_t(j.slot) * max_blocks;
@@ -1217,21 +1237,21 @@ int blocks_for(int64_t n, int threads) { return int((n + threads - 1) / threads)
 static inline double* slot(const DevProblem& d, int s) { return d.partials + size_t(s) * d.max_blocks; }
 
 void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s) {
-  k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr);
+  k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr, d.gate);
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records) {
   // the record-writing variant (evaluate API) runs on its own, smaller grid
   k_jacobian<<<write_records ? d.jac_blocks_rec : d.jac_blocks, kThreads, 0, s>>>(
       d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X, d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
-      slot(d, kPCost), d.jpart, write_records ? 1 : 0);
+      slot(d, kPCost), d.jpart, write_records ? 1 : 0, d.gate);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
-  if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam);
+  if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.gate);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
                                                                reuse_diag ? 1 : 0,
-                                                               count_grad ? slot(d, kPGradCam) : nullptr);
+                                                               count_grad ? slot(d, kPGradCam) : nullptr, d.gate);
 }
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
   if (d.P == 0) return;
@@ -1240,37 +1260,37 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 #define SFM_PE_LDS(M_)                                                                                              \
   k_point_eval_lds<M_><<<nb, kThreads, 0, s>>>(d.P, d.C, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X,      \
                                                d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag, mode,           \
-                                               reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt))
+                                               reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt), d.gate)
   if (d.C <= 64) SFM_PE_LDS(64);
   else if (d.C <= 512) SFM_PE_LDS(512);
   else
     k_point_eval_rc<<<nb, kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X, d.scale_p,
                                             d.diag_p, d.ptV, d.min_diag, d.max_diag, mode, reuse_diag ? 1 : 0,
-                                            slot(d, kPGradPt), slot(d, kPXNormPt));
+                                            slot(d, kPGradPt), slot(d, kPXNormPt), d.gate);
 #undef SFM_PE_LDS
 }
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
   if (d.P) k_point_factor<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.ptV, d.diag_p, radius, d.ptL,
-                                                                         slot(d, kPBad), d.X, d.scale_p, d.ptS);
+                                                                         slot(d, kPBad), d.X, d.scale_p, d.ptS, d.gate, d.radius_dev);
 }
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   launch_point_factor(d, radius, s);
   if (d.N_pad)
     k_obs_prep_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
-                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.dpart);
+                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.dpart, d.gate);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
   // the off-diagonal blocks, which add a block's same-camera duplicate pairs
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
-                                        d.n, 1);
+                                        d.n, 1, d.gate, d.radius_dev);
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
   const int nb = int((d.n_bslots + per - 1) / per);
 #define SFM_PTS(S_)                                                                                           \
   k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                          d.S, d.ld, d.bperm)
+                                          d.S, d.ld, d.bperm, d.gate)
   if (sub == 8) SFM_PTS(8);
   else if (sub == 16) SFM_PTS(16);
   else if (sub == 32) SFM_PTS(32);
@@ -1282,22 +1302,22 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S);
   else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack);
 }
-void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail); }
+void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail, d.gate); }
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
   k_cam_update<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.cam, d.ysol, d.scale_c, d.cam_new, d.camRn,
                                                              count_norm ? slot(d, kPStepCam) : nullptr,
-                                                             slot(d, kPBadCam));
+                                                             slot(d, kPBadCam), d.gate);
 }
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
   (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
-  if (d.C) k_cam_solve<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.diag_c, radius, d.ysol, d.fail);
+  if (d.C) k_cam_solve<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.diag_c, radius, d.ysol, d.fail, d.gate, d.radius_dev);
 }
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
   if (d.N_pad && cams_var)
     k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
                                                                      d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ysol, d.eu,
-                                                                     slot(d, kPModel));
+                                                                     slot(d, kPModel), d.gate);
   else if (d.N_pad) {
     (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.N), s);
     (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
@@ -1305,7 +1325,7 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   if (d.P && pts_var) {
     k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.ptL, d.ptV, d.scale_p,
                                                                d.X, d.X_new, d.ypt, slot(d, kPStepPt),
-                                                               slot(d, kPBadBack), slot(d, kPModelPt));
+                                                               slot(d, kPBadBack), slot(d, kPModelPt), d.gate);
   } else if (d.P) {
     // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
     const size_t nbP = size_t(blocks_for(d.P, kThreads));
@@ -1317,14 +1337,14 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   }
   if (d.N_pad)
     k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
-                                                                   d.X_new, d.camRn, slot(d, kPNewCost));
+                                                                   d.X_new, d.camRn, slot(d, kPNewCost), d.gate);
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);
 }
 void launch_reduce_batch(const DevProblem& d, const ReduceBatch& b, bool copy_fail, hipStream_t s) {
   if (b.n > 0)
-    k_reduce_batch<<<b.n, 1024, 0, s>>>(d.partials, d.max_blocks, b, d.scal, copy_fail ? d.fail : nullptr);
+    k_reduce_batch<<<b.n, 1024, 0, s>>>(d.partials, d.max_blocks, b, d.scal, copy_fail ? d.fail : nullptr, d.gate);
 }
 
 }  // namespace sfm

@@ -53,6 +53,17 @@ using namespace sfm;
 
 enum Phase { kPhJac = 0, kPhCamRed, kPhPtEval, kPhPtPrep, kPhSchur, kPhChol, kPhBack, kPhBacksub, kPhOther, kNumPh };
 
+// device LM loop state (k_lm_decide / k_lm_post; see "device-driven LM loop")
+struct LmCtl {
+  int32_t run_step, run_eval, done, termination, error;
+  int32_t iteration, num_consecutive_invalid;
+  int32_t n_succ, n_unsucc, n_invalid, n_resid, n_jac, n_lin, trace_len;
+  double radius, decrease_factor, cost, grad_max, x_norm;
+  sfm_ba_iteration pending;  // an accepted iteration, completed after its evaluation
+  int32_t max_iter, max_invalid;
+  double ftol, gtol, ptol, max_radius, min_radius, min_rel_dec;
+};
+
 struct sfm_ba_handle {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -73,6 +84,12 @@ struct sfm_ba_handle {
   sfm_allreduce_fn host_fn = nullptr;
   void* host_user = nullptr;
   std::vector<double> host_buf;
+  // device-driven LM loop (unsharded solves): control block, its pinned
+  // mirror and the device trace buffer (grown to the iteration cap)
+  LmCtl* lm_ctl = nullptr;
+  LmCtl* lm_ctl_host = nullptr;
+  sfm_ba_iteration* lm_trace = nullptr;
+  int lm_trace_cap = 0;
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -193,6 +210,147 @@ struct HostTimer {
   }
 };
 
+// ---- device-driven LM loop ----
+// The trust-region bookkeeping of the host loop in sfm_ba_solve_resident,
+// restated on the device so that an unsharded solve enqueues several
+// iterations per host synchronisation.  k_lm_decide follows compute_step's
+// reductions, k_lm_accept and the evaluation kernels run only when the step
+// was accepted (gate run_eval), k_lm_post completes the accepted iteration
+// after its evaluation; compute_step's kernels run only while the loop is
+// not done (gate run_step).  The arithmetic is the host loop's, operation
+// for operation (contraction off), so both loops take the same decisions.
+
+
+__device__ void lm_push(LmCtl* c, sfm_ba_iteration* trace, int cap, const sfm_ba_iteration& it) {
+  if (c->trace_len < cap) trace[c->trace_len] = it;
+  ++c->trace_len;
+}
+__device__ void lm_finish(LmCtl* c, int term) {
+  c->termination = term;
+  c->done = 1;
+  c->run_step = 0;
+  c->run_eval = 0;
+}
+
+// after compute_step's reduction (scal: model change, candidate cost, step
+// norms, bad-step flags; the Cholesky failure int after the scalars)
+__global__ void k_lm_decide(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+#pragma clang fp contract(off)
+  if (c->done) {
+    c->run_eval = 0;
+    return;
+  }
+  ++c->iteration;
+  sfm_ba_iteration itr;
+  itr.iteration = c->iteration;
+  itr.step_is_valid = 0;
+  itr.step_is_successful = 0;
+  itr.reserved = 0;
+  itr.cost = 0.0;
+  itr.cost_change = 0.0;
+  itr.gradient_max_norm = 0.0;
+  itr.step_norm = 0.0;
+  itr.relative_decrease = 0.0;
+  itr.trust_region_radius = 0.0;
+  c->n_lin++;
+  const int chol_fail = *reinterpret_cast<const int*>(scal + kNumScalars);
+  if (chol_fail & 6) {  // a persistent grid's hand-off timed out: the host reports it
+    c->error = chol_fail & 6;
+    lm_finish(c, SFM_FAILURE);
+    return;
+  }
+  const bool solve_ok = chol_fail == 0 && !(scal[kBadStep] > 0.0) && !(scal[kBadCam] > 0.0) && !(scal[kBadBack] > 0.0);
+  const double model_cost_change = scal[kModelChange] + scal[kModelChangePt];
+  itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;
+  if (!itr.step_is_valid) {
+    ++c->num_consecutive_invalid;
+    c->n_invalid++;
+    if (c->num_consecutive_invalid >= c->max_invalid) {
+      itr.cost = c->cost; itr.gradient_max_norm = c->grad_max; itr.trust_region_radius = c->radius;
+      lm_push(c, trace, cap, itr);
+      lm_finish(c, SFM_FAILURE);
+      return;
+    }
+    itr.cost = c->cost;
+    itr.gradient_max_norm = c->grad_max;
+  } else {
+    c->num_consecutive_invalid = 0;
+    double new_cost = scal[kNewCost];
+    if (!isfinite(new_cost)) new_cost = DBL_MAX;
+    c->n_resid++;
+    itr.step_norm = sqrt(scal[kStep2Cam] + scal[kStep2Pt]);
+    const double step_size_tolerance = c->ptol * (c->x_norm + c->ptol);
+    if (itr.step_norm <= step_size_tolerance) {
+      itr.cost = c->cost; itr.gradient_max_norm = c->grad_max; itr.trust_region_radius = c->radius;
+      lm_push(c, trace, cap, itr);
+      lm_finish(c, SFM_CONVERGENCE);
+      return;
+    }
+    itr.cost_change = c->cost - new_cost;
+    if (fabs(itr.cost_change) <= c->ftol * c->cost) {
+      itr.cost = c->cost; itr.gradient_max_norm = c->grad_max; itr.trust_region_radius = c->radius;
+      lm_push(c, trace, cap, itr);
+      lm_finish(c, SFM_CONVERGENCE);
+      return;
+    }
+    itr.relative_decrease = itr.cost_change / model_cost_change;
+    itr.step_is_successful = itr.relative_decrease > c->min_rel_dec;
+  }
+  if (itr.step_is_successful) {
+    c->n_succ++;
+    const double q = 2.0 * itr.relative_decrease - 1.0;
+    double radius = c->radius / fmax(1.0 / 3.0, 1.0 - q * q * q);
+    c->radius = fmin(c->max_radius, radius);
+    c->decrease_factor = 2.0;
+    c->pending = itr;  // cost, gradient and radius after the evaluation (k_lm_post)
+    c->run_eval = 1;
+    return;
+  }
+  c->n_unsucc++;
+  c->radius = c->radius / c->decrease_factor;
+  c->decrease_factor *= 2.0;
+  c->run_eval = 0;
+  itr.gradient_max_norm = c->grad_max;
+  itr.cost = c->cost;
+  itr.trust_region_radius = c->radius;
+  lm_push(c, trace, cap, itr);
+  if (c->radius < c->min_radius) { lm_finish(c, SFM_CONVERGENCE); return; }
+  if (c->iteration >= c->max_iter) { lm_finish(c, SFM_NO_CONVERGENCE); return; }
+}
+
+// the accepted candidate becomes the current point (the host loop swaps the
+// buffers; enqueued iterations hold fixed pointers, so this copies)
+__global__ void k_lm_accept(const int32_t* __restrict__ gate, int C, int P, const double* __restrict__ cam_new,
+                            double* __restrict__ cam, const double* __restrict__ X_new, double* __restrict__ X) {
+  if (*gate == 0) return;
+  const int64_t n_c = 6 * int64_t(C), n = n_c + 3 * int64_t(P);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    if (i < n_c) cam[i] = cam_new[i];
+    else X[i - n_c] = X_new[i - n_c];
+  }
+}
+
+// after the accepted step's evaluation (scal: cost, gradient max norms, |x|^2)
+__global__ void k_lm_post(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+#pragma clang fp contract(off)
+  if (!c->run_eval) return;
+  c->run_eval = 0;
+  c->n_jac++;
+  c->n_resid++;
+  const double cost = scal[kCost];
+  c->cost = cost;
+  if (!isfinite(cost)) { lm_finish(c, SFM_FAILURE); return; }
+  c->grad_max = fmax(scal[kGradMaxCam], scal[kGradMaxPt]);
+  c->x_norm = sqrt(scal[kXNorm2Cam] + scal[kXNorm2Pt]);
+  sfm_ba_iteration itr = c->pending;
+  itr.gradient_max_norm = c->grad_max;
+  itr.cost = cost;
+  itr.trust_region_radius = c->radius;
+  lm_push(c, trace, cap, itr);
+  if (c->grad_max <= c->gtol) { lm_finish(c, SFM_CONVERGENCE); return; }
+  if (c->iteration >= c->max_iter) { lm_finish(c, SFM_NO_CONVERGENCE); return; }
+}
+
 // Reduced systems with more camera blocks than this take the XCD-aware
 // k_schur_pts order (C3: 125k blocks); smaller ones the plain order.
 constexpr int64_t kSchurXcdMinBlocks = 8192;
@@ -228,7 +386,7 @@ int fetch_scalars(sfm_ba_handle* h) {
 
 // Evaluate cost, Jacobian, Jacobi scale (first call), per-block normal
 // equations, LM diagonal and gradient at the current parameters.
-int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
+int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
@@ -290,12 +448,16 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
     if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
     if ((rc = allreduce(h, d.scal + kXNorm2Pt, 1, ncclSum))) return rc;
   }
+  return 0;
+}
+int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
+  if (int rc = evaluate_enqueue(h, first, jacobi_scaling)) return rc;
   return fetch_scalars(h);
 }
 
 // One trust-region step: factor, Schur, dense Cholesky, back substitution,
 // model cost change and candidate cost.
-int compute_step(sfm_ba_handle* h, double radius) {
+int compute_step_enqueue(sfm_ba_handle* h, double radius) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
@@ -365,6 +527,10 @@ int compute_step(sfm_ba_handle* h, double radius) {
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
     if ((rc = allreduce(h, d.scal + kModelChangePt, 1, ncclSum))) return rc;
   }
+  return 0;
+}
+int compute_step(sfm_ba_handle* h, double radius) {
+  if (int rc = compute_step_enqueue(h, radius)) return rc;
   return fetch_scalars(h);
 }
 
@@ -389,6 +555,110 @@ const char* invalid_option(const sfm_ba_options& o) {
   if (!(o.max_lm_diagonal >= 0)) return "max_lm_diagonal >= 0";
   if (!(o.min_lm_diagonal <= o.max_lm_diagonal)) return "min_lm_diagonal <= max_lm_diagonal";
   return nullptr;
+}
+
+// The device-driven LM loop of sfm_ba_solve_resident (unsharded problems):
+// state in LmCtl, iterations enqueued in batches (3, then 2; SFM_LM_BATCH
+// fixes the size), the host reads the control block once per batch.  The gated
+// kernels of iterations enqueued past the end return at once.
+template <class Push>
+int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, double grad_max, double x_norm,
+                  sfm_ba_summary* sm, Push& push) {
+  DevProblem& d = h->d;
+  hipStream_t s = h->stream;
+  if (opts.max_num_iterations <= 0) {
+    sm->termination_type = SFM_NO_CONVERGENCE;
+    sm->num_iterations = 0;
+    return 0;
+  }
+  if (!h->lm_ctl) {
+    if (hipMalloc(reinterpret_cast<void**>(&h->lm_ctl), sizeof(LmCtl)) != hipSuccess) {
+      h->lm_ctl = nullptr;
+      return fail(SFM_ENOMEM, "hipMalloc failed (LM control)");
+    }
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->lm_ctl_host), sizeof(LmCtl)) != hipSuccess) {
+      h->lm_ctl_host = nullptr;
+      return fail(SFM_ENOMEM, "hipHostMalloc failed (LM control)");
+    }
+  }
+  const int cap = opts.max_num_iterations + 1;
+  if (h->lm_trace_cap < cap) {
+    if (h->lm_trace) (void)hipFree(h->lm_trace);
+    h->lm_trace = nullptr;
+    h->lm_trace_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&h->lm_trace), sizeof(sfm_ba_iteration) * size_t(cap)) != hipSuccess) {
+      h->lm_trace = nullptr;
+      return fail(SFM_ENOMEM, "hipMalloc failed (LM trace)");
+    }
+    h->lm_trace_cap = cap;
+  }
+  LmCtl& c = *h->lm_ctl_host;
+  std::memset(&c, 0, sizeof(c));
+  c.run_step = 1;
+  c.radius = opts.initial_trust_region_radius;
+  c.decrease_factor = 2.0;
+  c.cost = *cost;
+  c.grad_max = grad_max;
+  c.x_norm = x_norm;
+  c.max_iter = opts.max_num_iterations;
+  c.max_invalid = opts.max_num_consecutive_invalid_steps;
+  c.ftol = opts.function_tolerance;
+  c.gtol = opts.gradient_tolerance;
+  c.ptol = opts.parameter_tolerance;
+  c.max_radius = opts.max_trust_region_radius;
+  c.min_radius = opts.min_trust_region_radius;
+  c.min_rel_dec = opts.min_relative_decrease;
+  HIPCHK(hipMemcpyAsync(h->lm_ctl, &c, sizeof(LmCtl), hipMemcpyHostToDevice, s));
+  // 3 iterations first (a keyframe or C3 solve typically ends there), then 2
+  // at a time: each gated iteration past the end still costs its launches
+  // (measured per C1 solve: batch 3 0.49 ms, 4 0.52, 6 0.62; host loop 0.54)
+  int batch = 3, batch_next = 2;
+  if (const char* b = std::getenv("SFM_LM_BATCH")) batch = batch_next = std::max(1, std::min(64, std::atoi(b)));
+  const bool jac_scaling = opts.jacobi_scaling != 0;
+  const int acc_blocks = std::max(1, std::min(1024, blocks_for(6 * int64_t(d.C) + 3 * int64_t(d.P), 256)));
+  d.radius_dev = &h->lm_ctl->radius;
+  int rc = 0;
+  while (rc == 0) {
+    for (int b = 0; b < batch && rc == 0; ++b) {
+      d.gate = &h->lm_ctl->run_step;
+      if ((rc = compute_step_enqueue(h, c.radius))) break;
+      d.gate = nullptr;
+      k_lm_decide<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
+      d.gate = &h->lm_ctl->run_eval;
+      k_lm_accept<<<acc_blocks, 256, 0, s>>>(d.gate, d.C, d.P, d.cam_new, d.cam, d.X_new, d.X);
+      if ((rc = evaluate_enqueue(h, false, jac_scaling))) break;
+      d.gate = nullptr;
+      k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
+    }
+    if (rc) break;
+    if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = fail(SFM_EIO, "LM control readback failed");
+      break;
+    }
+    collect_marks(h);
+    if (c.done) break;
+    batch = batch_next;
+  }
+  d.gate = nullptr;
+  d.radius_dev = nullptr;
+  if (rc) return rc;
+  if (c.error & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid not co-resident)");
+  if (c.error & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid not co-resident)");
+  const int n_tr = std::min(c.trace_len, h->lm_trace_cap);
+  std::vector<sfm_ba_iteration> tr(static_cast<size_t>(std::max(1, n_tr)));
+  if (n_tr) HIPCHK(hipMemcpy(tr.data(), h->lm_trace, sizeof(sfm_ba_iteration) * size_t(n_tr), hipMemcpyDeviceToHost));
+  for (int i = 0; i < n_tr; ++i) push(tr[i]);
+  sm->termination_type = c.termination;
+  sm->num_iterations = c.iteration;
+  sm->num_successful_steps += c.n_succ;
+  sm->num_unsuccessful_steps += c.n_unsucc;
+  sm->num_invalid_steps += c.n_invalid;
+  sm->num_residual_evaluations += c.n_resid;
+  sm->num_jacobian_evaluations += c.n_jac;
+  sm->num_linear_solves += c.n_lin;
+  *cost = c.cost;
+  return 0;
 }
 
 }  // namespace
@@ -443,6 +713,9 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   free_problem(h);
   release_pool(h);
   if (h->d.scal_host) hipHostFree(h->d.scal_host);
+  if (h->lm_ctl) hipFree(h->lm_ctl);
+  if (h->lm_ctl_host) hipHostFree(h->lm_ctl_host);
+  if (h->lm_trace) hipFree(h->lm_trace);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -914,6 +1187,13 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   }
   if (grad_max <= opts.gradient_tolerance) {
     sm.termination_type = SFM_CONVERGENCE;
+  } else if (!sharded(h) && !env_flag("SFM_HOST_LM")) {
+    // the same loop with its decisions on the device (k_lm_decide /
+    // k_lm_post): iterations are enqueued in batches, one host
+    // synchronisation per batch instead of two per iteration
+    const double tl0 = now_s();
+    if ((rc = run_device_lm(h, opts, &cost, grad_max, x_norm, &sm, push))) return rc;
+    sm.linear_solver_time_s += now_s() - tl0;
   } else {
     double radius = opts.initial_trust_region_radius;
     double decrease_factor = 2.0;
@@ -976,7 +1256,8 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
       }
       if (itr.step_is_successful) {
         sm.num_successful_steps++;
-        radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * itr.relative_decrease - 1.0, 3));
+        const double q = 2.0 * itr.relative_decrease - 1.0;  // (2 rho - 1)^3, as k_lm_decide
+        radius = radius / std::max(1.0 / 3.0, 1.0 - q * q * q);
         radius = std::min(opts.max_trust_region_radius, radius);
         decrease_factor = 2.0;
         std::swap(d.cam, d.cam_new);

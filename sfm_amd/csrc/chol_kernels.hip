@@ -788,12 +788,20 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
 __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb,
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
-                                                    int epoch, int nhelp, int* __restrict__ fail) {
+                                                    int epoch, int nhelp, int* __restrict__ fail,
+                                                    const int* __restrict__ gate) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
   __shared__ double scr[4][256];
   __shared__ int sh[2];
+  if (gate && *gate == 0) {
+    // device LM loop, phase skipped: the launch still takes its ntask + nhelp
+    // tickets, so the next epoch's ticket base stays (epoch - 1) (ntask + nhelp)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      atomicAdd(ticket, (unsigned long long)(chol_tasks(nb) + nhelp));
+    return;
+  }
   if (blockIdx.x == 0) {
     fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
     return;
@@ -849,7 +857,8 @@ constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWor
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
-                                                   int* __restrict__ fail) {
+                                                   int* __restrict__ fail, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double v[NB];
   __shared__ double yl[2][NB];
   __shared__ int timed_out;
@@ -931,7 +940,7 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   // one persistent workgroup per CU (the walker + helpers must be co-resident)
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
-                                         epoch, nhelp, d.fail);
+                                         epoch, nhelp, d.fail, d.gate);
 }
 
 void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s) {
@@ -939,7 +948,7 @@ void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s) {
   if (nb_real <= 0) return;
   // the sentinel in every entry of y the launch produces (ld >= 64 nb_real)
   (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
-  k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail);
+  k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail, d.gate);
 }
 
 }  // namespace sfm

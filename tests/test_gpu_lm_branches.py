@@ -168,3 +168,31 @@ def test_evaluate_after_solve_reports_the_current_cost():
     assert abs(cost - 0.5 * np.sum(res ** 2)) <= 1e-10 * cost
     r_o = _residuals(s.uv, s.cam_idx, s.pt_idx, s.K, rot, t, X)
     assert abs(cost - 0.5 * np.sum(r_o ** 2)) <= 1e-10 * cost
+
+
+@pytest.mark.parametrize("name", sorted(FIX))
+def test_device_loop_equals_host_loop(name, monkeypatch):
+    """The device-driven LM loop (k_lm_decide / k_lm_post, iterations
+    enqueued in batches) against the host-driven loop (SFM_HOST_LM=1) on
+    every branch scene: the same trace and bitwise the same parameters."""
+    c = FIX[name]
+    build, _, mode = L.cases()[name]
+    s = build()
+    out = {}
+    for host in (False, True):
+        if host:
+            monkeypatch.setenv("SFM_HOST_LM", "1")
+        else:
+            monkeypatch.delenv("SFM_HOST_LM", raising=False)
+        r, t, X = s.copy_params()
+        sm, tr = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X, mode=mode,
+                               options=sfm_amd.make_options(**c["options"]))
+        out[host] = (sm, tr, (r, t, X))
+    (sa, ta, pa), (sb, tb, pb) = out[False], out[True]
+    assert ta == tb
+    for f in ("termination_type", "num_iterations", "num_successful_steps", "num_unsuccessful_steps",
+              "num_invalid_steps", "num_residual_evaluations", "num_jacobian_evaluations", "num_linear_solves"):
+        assert getattr(sa, f) == getattr(sb, f), f
+    assert sa.final_cost == sb.final_cost
+    for a, b in zip(pa, pb):
+        assert np.array_equal(a, b)
