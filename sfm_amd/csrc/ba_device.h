@@ -131,6 +131,7 @@ struct DevProblem {
   int64_t n_bslots = 0;
   double* ptS = nullptr;      // [P][kPtS] X 3, scale 3, l10 l20 l21, 1/l_ii 3, z 3, pad
   int32_t schur_pts_sub = 8;  // lanes per block (8, 16, 32 or 64; C3: 1.07 / 1.09 / 1.21 / 1.49 ms per solve)
+  bool schur_wg_blocks = false;  // one block per 4-wave workgroup (small systems with long pair lists)
   // per-wave diagonal-block / rhs partials from k_obs_prep_rc ([N_pad/64][27])
   double* dpart = nullptr;
   // per-chunk U_c / b_c partials from k_jacobian ([N_pad/64][27])

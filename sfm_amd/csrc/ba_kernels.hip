@@ -797,7 +797,11 @@ __device__ __forceinline__ double seg_sum(double v) {
   return v;
 }
 
-template <int kSub>
+// kWpb = 4: one block per workgroup, its pairs dealt over the 4 waves (64
+// lanes each, kSub = 64) and the 4 partial blocks added in LDS in wave
+// order -- for small reduced systems (few blocks, long pair lists), where
+// one wave per block leaves most CUs idle.
+template <int kSub, int kWpb = 1>
 __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, const int2* __restrict__ blk,
                                                         const int32_t* __restrict__ seg,
                                                         const int32_t* __restrict__ bpts,
@@ -808,10 +812,13 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
                                                         int ld,
                                                         const int32_t* __restrict__ bperm, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  static_assert(kWpb == 1 || (kWpb == kThreads / 64 && kSub == 64), "4 waves per block take 64 lanes each");
   constexpr int kPer = 64 / kSub;  // blocks per wave
   __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
-  const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
+  const int64_t wb = kWpb == 1 ? (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer : int64_t(blockIdx.x);
+  constexpr int kStride = kSub * kWpb;          // pair stride of a lane
+  const int lane0 = kWpb == 1 ? sl : 64 * wv + sl;  // this lane's first pair of the block
   // (no early exit: a wave past the end runs empty lists, so every wave
   // reaches the publishing barrier)
   // bperm: the XCD-aware work order of set_problem (nullptr: the plain
@@ -847,15 +854,15 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
   // drains vmcnt.  The next step's index is loaded one step ahead, so each
   // step's record gather waits on one dependent load instead of two
   // (263 -> 251 us per C3 launch, S bitwise unchanged).
-  int p_nx = bpts[kb + sl < ke ? kb + sl : 0];
-  for (int k0 = 0; k0 < len; k0 += kSub) {
+  int p_nx = bpts[kb + lane0 < ke ? kb + lane0 : 0];
+  for (int k0 = 0; k0 < len; k0 += kStride) {
     // the camera constants are re-read from LDS each step (hoisted, they
     // would hold 200 VGPRs)
     asm volatile("" ::: "memory");
-    const int k = kb + k0 + sl;
+    const int k = kb + k0 + lane0;
     const bool valid = k < ke;
     const int p = p_nx;
-    p_nx = bpts[k + kSub < ke ? k + kSub : 0];
+    p_nx = bpts[k + kStride < ke ? k + kStride : 0];
     const double* r = ptS + size_t(kPtS) * p;
     double q[12];  // X, scale, l10 l20 l21, 1/l_ii (z, the last 32 B, unused here)
 #pragma unroll
@@ -894,8 +901,28 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
 #pragma unroll
   for (int e = 0; e < 32; ++e) v32[e] = acc[e];
   seg_reduce32<kSub>(v32, l);
-  const double t32 = seg_sum<kSub>(acc[32]), t33 = seg_sum<kSub>(acc[33]), t34 = seg_sum<kSub>(acc[34]),
-               t35 = seg_sum<kSub>(acc[35]);
+  double t32 = seg_sum<kSub>(acc[32]), t33 = seg_sum<kSub>(acc[33]), t34 = seg_sum<kSub>(acc[34]),
+         t35 = seg_sum<kSub>(acc[35]);
+  if (kWpb > 1) {
+    // the waves' partial blocks, added in wave order by wave 0
+    __shared__ double red[kWpb][36];
+    if (!(sl & 1)) red[wv][sl >> 1] = v32[0];
+    if (sl == 0) { red[wv][32] = t32; red[wv][33] = t33; red[wv][34] = t34; red[wv][35] = t35; }
+    __syncthreads();
+    if (wv != 0) return;
+    if (!(sl & 1)) {
+      double a = red[0][sl >> 1];
+#pragma unroll
+      for (int q = 1; q < kWpb; ++q) a += red[q][sl >> 1];
+      v32[0] = a;
+    }
+    if (sl < 4) {
+      double a = red[0][32 + sl];
+#pragma unroll
+      for (int q = 1; q < kWpb; ++q) a += red[q][32 + sl];
+      if (sl == 0) t32 = a; else if (sl == 1) t33 = a; else if (sl == 2) t34 = a; else t35 = a;
+    }
+  }
   if (own) {
     // a diagonal block (same-camera duplicate pairs only) is added to what
     // k_schur_diag_sum wrote before this launch, else stored
@@ -1291,6 +1318,12 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
 #define SFM_PTS(S_)                                                                                           \
   k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
                                           d.S, d.ld, d.bperm, d.gate)
+  if (d.schur_wg_blocks) {  // small systems: one block per workgroup
+    k_schur_pts<64, kThreads / 64><<<int(d.n_bslots), kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS,
+                                                                       d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
+                                                                       d.bperm, d.gate);
+    return;
+  }
   if (sub == 8) SFM_PTS(8);
   else if (sub == 16) SFM_PTS(16);
   else if (sub == 32) SFM_PTS(32);

@@ -945,6 +945,11 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     while (sub < 64 && sub < avg / 10.0) sub *= 2;
     d.schur_pts_sub = sub;
   }
+  // few blocks with long lists (keyframe-sized: C1 210 blocks of ~460
+  // pairs): a workgroup per block instead of a wave (SFM_SCHUR_WG=0/1 forces)
+  d.schur_wg_blocks = d.schur_pts_sub == 64 && d.n_blk <= 4 * 256 &&
+                      (d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0) >= 256.0;
+  if (const char* sw = std::getenv("SFM_SCHUR_WG")) d.schur_wg_blocks = sw[0] == '1' && d.schur_pts_sub == 64;
   if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1 + 16)) != hipSuccess) {
     d.scal_host = nullptr;
     return bail(fail(SFM_ENOMEM, "hipHostMalloc failed"));
