@@ -1,3 +1,5 @@
+"""sfm_ba_set_problem wall time at C3, four times (SFM_TIMING=1 adds the
+host phase breakdown on stderr):  SFM_TIMING=1 python tools/c3_setup_timing.py"""
 import os, sys, time
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import numpy as np
