@@ -992,14 +992,16 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
 // image, and none of the stale factor entries outside the triangle.
 __device__ __forceinline__ size_t packed_row(int i, int n) { return size_t(i) * (n + 1) - size_t(i) * (i - 1) / 2; }
 
-__global__ void k_pack_upper(const double* __restrict__ S, int ld, int n, double* __restrict__ P) {
+__global__ void k_pack_upper(const double* __restrict__ S, int ld, int n, double* __restrict__ P, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int i = blockIdx.x;
   const double* row = S + size_t(i) * ld;
   double* dst = P + packed_row(i, n) - i;
   for (int j = i + threadIdx.x; j <= n; j += blockDim.x) dst[j] = row[j];
 }
 
-__global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, double* __restrict__ S) {
+__global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, double* __restrict__ S, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int i = blockIdx.x;
   double* row = S + size_t(i) * ld;
   const double* src = P + packed_row(i, n) - i;
@@ -1332,8 +1334,8 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
 }
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (d.n == 0) return;
-  if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S);
-  else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack);
+  if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S, d.gate);
+  else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack, d.gate);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail, d.gate); }
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {

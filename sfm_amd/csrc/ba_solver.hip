@@ -557,7 +557,8 @@ const char* invalid_option(const sfm_ba_options& o) {
   return nullptr;
 }
 
-// The device-driven LM loop of sfm_ba_solve_resident (unsharded problems):
+// The device-driven LM loop of sfm_ba_solve_resident (all but the
+// host-callback collective):
 // state in LmCtl, iterations enqueued in batches (3, then 2; SFM_LM_BATCH
 // fixes the size), the host reads the control block once per batch.  The gated
 // kernels of iterations enqueued past the end return at once.
@@ -1192,10 +1193,13 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   }
   if (grad_max <= opts.gradient_tolerance) {
     sm.termination_type = SFM_CONVERGENCE;
-  } else if (!sharded(h) && !env_flag("SFM_HOST_LM")) {
+  } else if (!h->host_fn && !env_flag("SFM_HOST_LM")) {
     // the same loop with its decisions on the device (k_lm_decide /
     // k_lm_post): iterations are enqueued in batches, one host
-    // synchronisation per batch instead of two per iteration
+    // synchronisation per batch instead of two per iteration.  With an RCCL
+    // communicator the all-reduces are enqueued on the same stream and every
+    // rank decides from the same reduced scalars; only the host-callback
+    // collective (tests) needs the host loop.
     const double tl0 = now_s();
     if ((rc = run_device_lm(h, opts, &cost, grad_max, x_norm, &sm, push))) return rc;
     sm.linear_solver_time_s += now_s() - tl0;
