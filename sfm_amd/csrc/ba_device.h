@@ -29,6 +29,10 @@ constexpr int kPtS = 16;
 constexpr int kNB = 64;
 // Threads per workgroup of the observation / point kernels.
 constexpr int kThreads = 256;
+// k_backsolve's "not yet produced" value of a y entry (both halves: a
+// signalling NaN, which arithmetic never yields)
+constexpr uint32_t kYSentinelWord = 0x7FF4DEADu;
+constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWord;
 
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
@@ -183,6 +187,7 @@ int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
-void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s);
+// sentinel_set: y already holds kYSentinel (k_pad_init wrote it)
+void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set = false);
 
 }  // namespace sfm

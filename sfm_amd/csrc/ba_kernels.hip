@@ -1011,10 +1011,12 @@ __global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, doub
 // Identity padding beyond the augmented row n (column-major lower view).
 // Identity padding of the augmented system, and the Cholesky failure flag
 // cleared (saves the separate memset dispatch before k_chol_fused).
-__global__ void k_pad_init(double* __restrict__ S, int ld, int n, int* __restrict__ fail, const int* __restrict__ gate) {
+__global__ void k_pad_init(double* __restrict__ S, int ld, int n, int* __restrict__ fail,
+                           unsigned long long* __restrict__ ysol, int n_y, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int j = blockIdx.x;
   if (j == 0 && threadIdx.x == 0) *fail = 0;
+  if (threadIdx.x == 0 && j < n_y) ysol[j] = kYSentinel;  // k_backsolve's "not yet produced"
   for (int i = (j > n ? j : n + 1) + threadIdx.x; i < ld; i += blockDim.x) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
   if (j == n && threadIdx.x == 0) S[size_t(n) * ld + n] = 1.0;
 }
@@ -1337,7 +1339,11 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S, d.gate);
   else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack, d.gate);
 }
-void launch_pad_init(const DevProblem& d, hipStream_t s) { k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail, d.gate); }
+void launch_pad_init(const DevProblem& d, hipStream_t s) {
+  // (also the back substitution's sentinel: 64 per real block of y)
+  const int n_y = (d.n + kNB - 1) / kNB * kNB;
+  k_pad_init<<<d.ld, 64, 0, s>>>(d.S, d.ld, d.n, d.fail, reinterpret_cast<unsigned long long*>(d.ysol), n_y, d.gate);
+}
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s) {
   k_cam_update<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.cam, d.ysol, d.scale_c, d.cam_new, d.camRn,
                                                              count_norm ? slot(d, kPStepCam) : nullptr,

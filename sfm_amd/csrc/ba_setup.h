@@ -18,6 +18,15 @@ hipError_t sort_pairs32(void* tmp, size_t bytes, const uint32_t* kin, uint32_t* 
 hipError_t exclusive_sum32(void* tmp, size_t bytes, const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
 hipError_t exclusive_sum64(void* tmp, size_t bytes, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
 
+// Several 32-bit fills in one launch (set_problem's initialisations: one
+// kernel instead of one hipMemset each).
+struct Fill32Set {
+  struct Job { uint32_t* p; int64_t n; uint32_t v; } job[8];
+  int n = 0;
+  void add(void* p, size_t bytes, uint32_t v) { job[n++] = Job{static_cast<uint32_t*>(p), int64_t(bytes / 4), v}; }
+};
+void launch_fill32(const Fill32Set& fs, hipStream_t s);
+
 // err[0..2] = first observation with a bad camera index / point index /
 // non-finite uv (INT32_MAX: none); per-camera and per-point counts of the
 // observations with valid indices.

@@ -284,6 +284,16 @@ __global__ __launch_bounds__(kT) void k_bperm_fill(int64_t n_blk, const int32_t*
   bperm[((i / per) * 8 + x) * per + i % per] = b;
 }
 
+__global__ __launch_bounds__(kT) void k_fill32(Fill32Set fs) {
+  const Fill32Set::Job f = fs.job[blockIdx.y];
+  // 16-B stores for the bulk (device allocations are 256-B aligned), then the tail
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(f.p) & 15) ? 0 : f.n / 4;
+  const uint4 v4 = make_uint4(f.v, f.v, f.v, f.v);
+  const int64_t t0 = int64_t(blockIdx.x) * kT + threadIdx.x, st = int64_t(gridDim.x) * kT;
+  for (int64_t i = t0; i < n4; i += st) reinterpret_cast<uint4*>(f.p)[i] = v4;
+  for (int64_t i = 4 * n4 + t0; i < f.n; i += st) f.p[i] = f.v;
+}
+
 int bits_for(uint64_t max_key) {
   int b = 1;
   while (b < 64 && (max_key >> b) != 0) ++b;
@@ -366,6 +376,13 @@ void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm,
 }
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s) {
   k_seg<<<nblocks(n_blk + 1), kT, 0, s>>>(n_blk, key, n_pairs, seg);
+}
+void launch_fill32(const Fill32Set& fs, hipStream_t s) {
+  if (fs.n == 0) return;
+  int64_t mx = 1;
+  for (int i = 0; i < fs.n; ++i) mx = std::max(mx, fs.job[i].n);
+  const unsigned gx = unsigned(std::min<int64_t>(1024, (mx + kT - 1) / kT));
+  k_fill32<<<dim3(gx, unsigned(fs.n)), kT, 0, s>>>(fs);
 }
 void launch_blk(int C, int2* blk, hipStream_t s) {
   if (C > 0) k_blk<<<dim3(unsigned((C + kT - 1) / kT), unsigned(C)), kT, 0, s>>>(C, blk);

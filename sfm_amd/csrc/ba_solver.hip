@@ -475,12 +475,12 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
       if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
       launch_pack_upper(d, true, s);
     }
-    launch_pad_init(d, s);  // also clears the failure flag
+    launch_pad_init(d, s);  // also clears the failure flag and sets y's sentinel
     mark_begin(h, kPhChol);
     launch_cholesky(d, ++h->chol_epoch, s, false);
     mark_end(h);
     mark_begin(h, kPhBack);
-    launch_backsolve(d, ++h->bs_epoch, s);
+    launch_backsolve(d, ++h->bs_epoch, s, true);
     mark_end(h);
   } else if (h->mode == SFM_BA_POSE_ONLY) {
     // block-diagonal camera system from the all-reduced U_c (same on every rank)
@@ -804,9 +804,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(in_pt, pt_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
   }
-  HCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), INT32_MAX, 4, s));
-  HCHK(hipMemsetAsync(cnt_c, 0, sizeof(int32_t) * (size_t(C) + 1), s));
-  HCHK(hipMemsetAsync(cnt_p, 0, sizeof(int32_t) * (size_t(P) + 1), s));
+  {
+    Fill32Set fs;
+    fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
+    fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
+    fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
+    launch_fill32(fs, s);
+  }
   launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
   // one round trip: the first bad observation and the per-camera counts
   // (the host lays out the C camera runs and the wavefront chunk table)
@@ -1059,13 +1063,17 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HCHK(hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, s));
   }
-  HCHK(hipMemsetAsync(d.S, 0, sizeof(double) * size_t(d.ld) * d.ld, s));
-  // the walker stores only the lower 16x16 blocks of each W_k (k_chol_fused)
-  HCHK(hipMemsetAsync(d.invL, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB, s));
-  HCHK(hipMemsetAsync(d.flags, 0, sizeof(int32_t) * size_t(d.nblk), s));
-  HCHK(hipMemsetAsync(d.cflags, 0, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, s));
-  HCHK(hipMemsetAsync(d.cticket, 0, sizeof(unsigned long long), s));
-  HCHK(hipMemsetAsync(d.partials, 0, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, s));
+  {
+    // the walker stores only the lower 16x16 blocks of each W_k (k_chol_fused)
+    Fill32Set fs;
+    fs.add(d.S, sizeof(double) * size_t(d.ld) * d.ld, 0);
+    fs.add(d.invL, sizeof(double) * size_t(d.nblk) * kNB * kNB, 0);
+    fs.add(d.flags, sizeof(int32_t) * size_t(d.nblk), 0);
+    fs.add(d.cflags, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, 0);
+    fs.add(d.cticket, sizeof(unsigned long long), 0);
+    fs.add(d.partials, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, 0);
+    launch_fill32(fs, s);
+  }
   h->chol_epoch = 0;
   h->bs_epoch = 0;
   d.n_cu = device_cus(h->device);

@@ -852,8 +852,6 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
 // slower: whatever runs after the awaited block arrives is on the chain.
 // All workgroups are co-resident (nb <= a few hundred, one CU each); every
 // wait is bounded and a timeout sets bit 1 of *fail (an error, never a hang).
-constexpr uint32_t kYSentinelWord = 0x7FF4DEADu;  // both halves: a signalling NaN
-constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWord;
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
@@ -943,11 +941,13 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
                                          epoch, nhelp, d.fail, d.gate);
 }
 
-void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s) {
+void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s, bool sentinel_set) {
   const int nb_real = (d.n + NB - 1) / NB;
   if (nb_real <= 0) return;
-  // the sentinel in every entry of y the launch produces (ld >= 64 nb_real)
-  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
+  // the sentinel in every entry of y the launch produces (ld >= 64 nb_real;
+  // the solve's k_pad_init writes it, saving a launch)
+  if (!sentinel_set)
+    (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
   k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail, d.gate);
 }
 
