@@ -170,6 +170,9 @@ void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write
 void launch_cam_reduce(const DevProblem& d, hipStream_t s);
 // mode 0: unscaled pass -> compute scale_c from colnorms; mode 1: diag (if !reuse) + gradient
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s);
+// launch_cam_reduce + launch_cam_finalize (reuse_diag false) in one launch
+// (unsharded: no U_c all-reduce between them); gradient partials per camera
+void launch_cam_sum_finalize(const DevProblem& d, int mode, bool count_grad, hipStream_t s);
 // mode 0: unscaled pass -> scale_p; mode 1: V, b, diag (if !reuse), gradient, x-norm
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s);
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s);

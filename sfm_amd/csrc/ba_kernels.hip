@@ -344,6 +344,46 @@ __global__ __launch_bounds__(64) void k_cam_sum(const int32_t* __restrict__ cam_
   if (!(t & 1) && (t >> 1) < 27) Ucam[size_t(kUcam) * c + (t >> 1)] = sum;
 }
 
+// k_cam_sum + k_cam_finalize in one launch (no cross-rank U_c sum between
+// them): the wave's reduce-scatter leaves entry e in lane 2e, lanes 0..5
+// take their column's diagonal and gradient entries by shuffle, and the
+// camera's gradient max-norm goes to partial slot c (the max over cameras
+// is order-free: the same result as k_cam_finalize's per-block partials).
+__global__ __launch_bounds__(64) void k_cam_sum_finalize(const int32_t* __restrict__ cam_rng,
+                                                         const double* __restrict__ jpart, double* __restrict__ Ucam,
+                                                         double* __restrict__ scale_c, double* __restrict__ diag_c,
+                                                         double min_diag, double max_diag, int mode,
+                                                         double* __restrict__ part_grad,
+                                                         const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+  double v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v[e] = 0.0;
+  for (int w = w0 + t; w < w1; w += 64) {
+    const double* src = jpart + size_t(w) * 27;
+#pragma unroll
+    for (int e = 0; e < 27; ++e) v[e] += src[e];
+  }
+  const double sum = wave_sum32(v, t);
+  if (!(t & 1) && (t >> 1) < 27) Ucam[size_t(kUcam) * c + (t >> 1)] = sum;
+  const int a = t < 6 ? t : 0;
+  const double cn = __shfl(sum, 2 * up6(a, a)), ga = __shfl(sum, 2 * (21 + a));
+  double g = 0.0;
+  if (t < 6) {
+    if (mode == 0) {
+      scale_c[6 * c + a] = 1.0 / (1.0 + sqrt(cn));
+    } else {
+      diag_c[6 * c + a] = fmin(fmax(cn, min_diag), max_diag);
+      g = fabs(ga / scale_c[6 * c + a]);
+    }
+  }
+#pragma unroll
+  for (int off = 4; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off));
+  if (t == 0 && part_grad) part_grad[c] = g;
+}
+
 __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* __restrict__ Ucam,
                                                            double* __restrict__ scale_c, double* __restrict__ diag_c,
                                                            double min_diag, double max_diag, int mode, int reuse,
@@ -1278,6 +1318,11 @@ void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.gate);
+}
+void launch_cam_sum_finalize(const DevProblem& d, int mode, bool count_grad, hipStream_t s) {
+  if (d.C)
+    k_cam_sum_finalize<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
+                                          count_grad ? slot(d, kPGradCam) : nullptr, d.gate);
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,

@@ -400,13 +400,19 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   mark_begin(h, kPhJac);
   launch_jacobian(d, !first || !jacobi_scaling ? true : false, s);
   mark_end(h);
+  // unsharded: the U_c sums and their finalisation in one launch
+  const bool fuse_cam = !sharded(h);
   if (first && jacobi_scaling) {
     if (cams_var) {
       mark_begin(h, kPhCamRed);
-      launch_cam_reduce(d, s);
+      if (fuse_cam) {
+        launch_cam_sum_finalize(d, 0, false, s);
+      } else {
+        launch_cam_reduce(d, s);
+        if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+        launch_cam_finalize(d, 0, false, false, s);
+      }
       mark_end(h);
-      if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
-      launch_cam_finalize(d, 0, false, false, s);
     }
     if (pts_var) launch_point_eval(d, 0, false, s);
     mark_begin(h, kPhJac);
@@ -415,10 +421,14 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   }
   if (cams_var) {
     mark_begin(h, kPhCamRed);
-    launch_cam_reduce(d, s);
+    if (fuse_cam) {
+      launch_cam_sum_finalize(d, 1, true, s);
+    } else {
+      launch_cam_reduce(d, s);
+      if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+      launch_cam_finalize(d, 1, false, true, s);
+    }
     mark_end(h);
-    if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
-    launch_cam_finalize(d, 1, false, true, s);
   } else {
     hipMemsetAsync(d.partials + size_t(kPGradCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
     hipMemsetAsync(d.partials + size_t(kPXNormCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
@@ -438,7 +448,7 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   }
   ReduceBatch rb;
   rb.add(kPCost, d.jac_blocks, 0, kCost);
-  rb.add(kPGradCam, nbC, 1, kGradMaxCam);
+  rb.add(kPGradCam, cams_var && fuse_cam ? std::max(1, d.C) : nbC, 1, kGradMaxCam);
   rb.add(kPGradPt, nbP, 1, kGradMaxPt);
   rb.add(kPXNormCam, nbC, 0, kXNorm2Cam);
   rb.add(kPXNormPt, nbP, 0, kXNorm2Pt);
@@ -1017,7 +1027,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.n = 6 * C;
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
   d.nblk = d.ld / kNB;
-  d.max_blocks = std::max({1, blocks_for(N, 256), blocks_for(P, 256), blocks_for(C, 256), d.jac_blocks,
+  d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
                            d.jac_blocks_rec, blocks_for(npad, 256)});
   ALLOC(d.Kc, 5 * size_t(C));
   ALLOC(d.cam, 6 * size_t(C));
