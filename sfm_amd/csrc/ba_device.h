@@ -100,7 +100,9 @@ struct DevProblem {
   double* camRn = nullptr;    // [C][12] candidate R (9) + t (3)
   double* jrec = nullptr;     // [N_pad][20] at camera-major position (J_X 6 | r 2 | J_c 12): evaluate API only,
                               // allocated on first use (the solve writes no records)
-  double* eu = nullptr;       // [N][kEU] back substitution pass A output (point-major)
+  double* eu = nullptr;       // [N][kEU] back substitution pass A output (point-major), or
+                              // [N_pad][kEU] at camera-major positions (eu_cm)
+  bool eu_cm = false;
   double* ypt = nullptr;      // [P][3] point steps y_p (scaled space)
   int32_t* wcam = nullptr;    // [N_pad / 64] camera of each camera-major wavefront (runs padded to 64)
   double* ptV = nullptr;      // [P][10]

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
                                                            const double* __restrict__ scale_c,
                                                            const double* __restrict__ ptS,
                                                            const double* __restrict__ ysol, double* __restrict__ eu,
-                                                           double* __restrict__ part_model, const int* __restrict__ gate) {
+                                                           int eu_cm, double* __restrict__ part_model, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -734,7 +734,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
       // u goes to the observation's POINT-major slot (32 B): pass B then
       // streams a point's u contiguously instead of gathering 48-B records
       const double* M = o.M;
-      double* dst = eu + 4 * size_t(qo);
+      double* dst = eu + 4 * (eu_cm ? size_t(i) : size_t(qo));
       st2(dst, M[0] * e0 + M[3] * e1, M[1] * e0 + M[4] * e1);
       dst[2] = M[2] * e0 + M[5] * e1;
     }
@@ -1162,6 +1162,7 @@ __global__ __launch_bounds__(kThreads) void k_cam_solve(int C, const double* __r
 
 __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __restrict__ pt_off,
                                                         const double* __restrict__ eu,
+                                                        const int32_t* __restrict__ eu_pos,
                                                         const double* __restrict__ ptL,
                                                         const double* __restrict__ ptV,
                                                         const double* __restrict__ scale_p,
@@ -1180,7 +1181,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;  // sum of u = L^-1 J_X^T e
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
     for (int q = q0; q < q1; ++q) {
-      const double* u = eu + 4 * size_t(q);  // point-major slot (pass A)
+      // pass A's u: at the point-major slot, or (eu_pos) at the camera-major position
+      const double* u = eu + 4 * (eu_pos ? size_t(eu_pos[q]) : size_t(q));
       const double2 u01 = ld2(u);
       const double u2 = u[2];
       w0 -= u01.x;
@@ -1403,13 +1405,14 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
   if (d.N_pad && cams_var)
     k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
                                                                      d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ysol, d.eu,
-                                                                     slot(d, kPModel), d.gate);
+                                                                     d.eu_cm ? 1 : 0, slot(d, kPModel), d.gate);
   else if (d.N_pad) {
-    (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.N), s);
+    (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.eu_cm ? d.N_pad : d.N), s);
     (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
   }
   if (d.P && pts_var) {
-    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.ptL, d.ptV, d.scale_p,
+    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.eu_cm ? d.pos : nullptr,
+                                                               d.ptL, d.ptV, d.scale_p,
                                                                d.X, d.X_new, d.ypt, slot(d, kPStepPt),
                                                                slot(d, kPBadBack), slot(d, kPModelPt), d.gate);
   } else if (d.P) {
