@@ -117,6 +117,37 @@ __global__ void k_dup_fill(int n_sel, const int32_t* __restrict__ sel, const int
   }
 }
 
+// k_dup_count over the rank-sorted observations of a multi-frame query:
+// entries of the queried frames (rank < nf) count their point's
+// observations in their own frame, the rest 0
+__global__ void k_dup_count_ranked(int64_t n, const int32_t* __restrict__ sel, const uint32_t* __restrict__ rank,
+                                   int nf, const int32_t* __restrict__ ob_pt, const int32_t* __restrict__ ob_frame,
+                                   const int32_t* __restrict__ orow, const int32_t* __restrict__ ooff,
+                                   int32_t* __restrict__ cnt) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  int c = 0;
+  if (int(rank[e]) < nf) {
+    const int o = sel[e], p = ob_pt[o], f = ob_frame[o];
+    for (int q = ooff[p]; q < ooff[p + 1]; ++q) c += ob_frame[orow[q]] == f;
+  }
+  cnt[e] = c;
+}
+
+// the frames' entry offsets (exclusive scan of the per-rank counts) and 2D
+// offsets (the entry scan at each frame's first entry): offs[0..nf] and
+// offs[nf+1 .. 2nf+1]
+__global__ void k_frame_offsets(int nf, const int32_t* __restrict__ fcnt, int64_t n, const int32_t* __restrict__ cnt,
+                                const int32_t* __restrict__ eoff, int32_t* __restrict__ offs) {
+  const int32_t total2 = n ? eoff[n - 1] + cnt[n - 1] : 0;
+  int32_t o = 0;
+  for (int i = 0; i <= nf; ++i) {
+    offs[i] = o;
+    offs[nf + 1 + i] = o < n ? eoff[o] : total2;
+    if (i < nf) o += fcnt[i];
+  }
+}
+
 // one wave per queried point: the point's row (in append order) with the
 // smallest sum of Hamming distances to its other rows, the first on ties
 // (CMap.cpp:345-381)
@@ -552,36 +583,35 @@ int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* f
   if (rc) return rc;
   if (hipcub::DeviceRadixSort::SortPairs(tmp, bytes, key, key2, iv, sel, int(N), 0, bits, h->s) != hipSuccess)
     return mapfail(SFM_EIO, "sort failed");
-  std::vector<int32_t> cnt_h(size_t(n_frames) + 1);
-  (void)hipMemcpyAsync(cnt_h.data(), fcnt, sizeof(int32_t) * cnt_h.size(), hipMemcpyDeviceToHost, h->s);
-  if (int r = sync(h)) return r;
-  for (int i = 0; i < n_frames; ++i) off3[i + 1] = off3[i] + cnt_h[i];
-  const int32_t n = off3[n_frames];
-  if (n == 0) return 0;
-  // per entry: how many 2D indices its point has in the entry's frame
-  auto* cnt = static_cast<int32_t*>(scratch(h, "mcnt", sizeof(int32_t) * size_t(n), &rc));
-  auto* eoff = static_cast<int32_t*>(scratch(h, "moff", sizeof(int32_t) * size_t(n), &rc));
-  auto* out3 = static_cast<int32_t*>(scratch(h, "mo3", sizeof(int32_t) * size_t(n), &rc));
+  // per sorted entry: how many 2D indices its point has in the entry's frame
+  // (0 past the queried frames), their exclusive scan, then the frames'
+  // offsets on the device: one readback of 2 (nf + 1) ints
+  auto* cnt = static_cast<int32_t*>(scratch(h, "mcnt", sizeof(int32_t) * size_t(N), &rc));
+  auto* eoff = static_cast<int32_t*>(scratch(h, "moff", sizeof(int32_t) * size_t(N), &rc));
+  auto* offs = static_cast<int32_t*>(scratch(h, "moffs", sizeof(int32_t) * 2 * (size_t(n_frames) + 1), &rc));
   if (rc) return rc;
-  k_dup_count<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->orow, h->ooff, INT32_MIN, cnt);
+  k_dup_count_ranked<<<grid(N), 256, 0, h->s>>>(N, sel, key2, n_frames, h->ob_pt.p, h->ob_frame.p, h->orow, h->ooff,
+                                                 cnt);
   bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, eoff, n, h->s);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, eoff, int(N), h->s);
   tmp = scratch(h, "mscan", bytes, &rc);
   if (rc) return rc;
-  if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, eoff, n, h->s) != hipSuccess)
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, eoff, int(N), h->s) != hipSuccess)
     return mapfail(SFM_EIO, "scan failed");
-  std::vector<int32_t> ecnt(static_cast<size_t>(n));
-  (void)hipMemcpyAsync(ecnt.data(), cnt, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
+  k_frame_offsets<<<1, 1, 0, h->s>>>(n_frames, fcnt, N, cnt, eoff, offs);
+  std::vector<int32_t> offs_h(2 * (size_t(n_frames) + 1));
+  (void)hipMemcpyAsync(offs_h.data(), offs, sizeof(int32_t) * offs_h.size(), hipMemcpyDeviceToHost, h->s);
   if (int r = sync(h)) return r;
-  for (int i = 0; i < n_frames; ++i) {
-    int32_t s2 = 0;
-    for (int32_t e = off3[i]; e < off3[i + 1]; ++e) s2 += ecnt[e];
-    off2[i + 1] = off2[i] + s2;
+  for (int i = 0; i <= n_frames; ++i) {
+    off3[i] = offs_h[i];
+    off2[i] = offs_h[n_frames + 1 + i];
   }
-  const int32_t n2 = off2[n_frames];
+  const int32_t n = off3[n_frames], n2 = off2[n_frames];
+  if (n == 0) return 0;
   if (int64_t(n) > capacity || int64_t(n2) > capacity)
     return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(std::max(n, n2)));
   if (!pts3d_idx || !pts2d_idx) return mapfail(SFM_EINVAL, "NULL output");
+  auto* out3 = static_cast<int32_t*>(scratch(h, "mo3", sizeof(int32_t) * size_t(n), &rc));
   auto* out2 = static_cast<int32_t*>(scratch(h, "mo2", sizeof(int32_t) * size_t(std::max(n2, 1)), &rc));
   if (rc) return rc;
   k_dup_fill<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->ob_idx.p, h->orow, h->ooff, INT32_MIN,

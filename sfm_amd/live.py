@@ -396,8 +396,13 @@ class LiveSfM:
         uv, cam, p3 = np.vstack(uv), np.concatenate(cam), np.concatenate(p3)
         if not len(p3):
             return
-        uniq, first = np.unique(p3, return_index=True)
-        order = uniq[np.argsort(first)]          # first-seen order of the gather
+        # first-seen order of the gather (np.minimum.at: each point's first
+        # entry; O(n) instead of np.unique's sort)
+        n_e = len(p3)
+        first = np.full(int(p3.max()) + 1, n_e, np.int64)
+        np.minimum.at(first, p3, np.arange(n_e))
+        seen = np.flatnonzero(first < n_e)
+        order = seen[np.argsort(first[seen], kind="stable")]
         remap = np.empty(int(order.max()) + 1, np.int32)
         remap[order] = np.arange(len(order), dtype=np.int32)
         pt = remap[p3]
