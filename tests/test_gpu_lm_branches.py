@@ -196,3 +196,32 @@ def test_device_loop_equals_host_loop(name, monkeypatch):
     assert sa.final_cost == sb.final_cost
     for a, b in zip(pa, pb):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("max_iter", [1, 2, 7])
+def test_device_loop_batches_and_iteration_cap(max_iter, monkeypatch):
+    """The device-driven loop with batch sizes 1, 2 and 5 and a small
+    iteration cap (NO_CONVERGENCE inside or at the end of a batch) against
+    the host-driven loop: identical traces, counts and parameters."""
+    name = sorted(n for n in FIX if not n.startswith("gauge"))[0]
+    c = FIX[name]
+    build, _, mode = L.cases()[name]
+    s = build()
+    opts = dict(c["options"], max_num_iterations=max_iter)
+    ref = None
+    for env in ({"SFM_HOST_LM": "1"}, {"SFM_LM_BATCH": "1"}, {"SFM_LM_BATCH": "2"}, {"SFM_LM_BATCH": "5"}):
+        monkeypatch.delenv("SFM_HOST_LM", raising=False)
+        monkeypatch.delenv("SFM_LM_BATCH", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        r, t, X = s.copy_params()
+        sm, tr = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X, mode=mode,
+                               options=sfm_amd.make_options(**opts))
+        got = (sm.termination_type, sm.num_iterations, sm.num_successful_steps, sm.num_unsuccessful_steps,
+               sm.num_invalid_steps, sm.num_residual_evaluations, sm.num_jacobian_evaluations, sm.final_cost, tr,
+               r.tobytes(), t.tobytes(), X.tobytes())
+        if ref is None:
+            ref = got
+            assert sm.num_iterations <= max_iter
+        else:
+            assert got == ref, env
