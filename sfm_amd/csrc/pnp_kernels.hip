@@ -89,9 +89,25 @@ __host__ __device__ void rodrigues_m2v(const double R[9], double r[3]) {
 // (shfl_xor 8, 4, 2, 1 -- every lane ends with the same value, floating
 // addition being commutative), which oracle/pnp_oracle.py cv_svd(tree=True)
 // reproduces.  Otherwise JacobiSVDImpl_ step for step (no V).
+// The partner values come by DPP row rotation (row_ror 8, 4, 2, 1 within
+// each 16-lane row) instead of ds_bpermute.  Rotating by 8 is xor 8; after
+// the levels above distance d, a lane's partial sum depends only on L mod 2d,
+// and (L + d) mod 2d == (L ^ d) mod 2d, so rotating by d delivers exactly
+// the xor partner's partial: the sum is bitwise the xor butterfly's (the
+// oracle's tree order), at a few cycles per level instead of an LDS round
+// trip.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), kCtrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double tree16(double v) {
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+  constexpr int kRowRor = 0x120;  // DPP row_ror:n = 0x120 + n
+  v += dpp_f64<kRowRor + 8>(v);
+  v += dpp_f64<kRowRor + 4>(v);
+  v += dpp_f64<kRowRor + 2>(v);
+  v += dpp_f64<kRowRor + 1>(v);
   return v;
 }
 
