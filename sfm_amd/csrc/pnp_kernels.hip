@@ -199,7 +199,7 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
     const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
     row[i] *= sc;
   }
-  if (k < 12 && threadIdx.x < 16)
+  if (k < 12 && (threadIdx.x & 63) < 16)
 #pragma unroll
     for (int q = 0; q < 4; ++q) lds[q * 12 + k] = row[11 - q];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -394,8 +394,18 @@ __host__ __device__ void gauss_newton(const double (&L)[6][10], const double (&r
   }
 }
 
-// (every lane of the wave computes the same: wave-uniform control flow)
-__host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, double R[9], double t[3]) {
+// EPnP of one 5-point subset, in three parts: the control points, the
+// barycentric coordinates, the null space of M (the 12x12 SVD) and the
+// distance constraints (epnp5_common), then the three beta solutions (N = 0,
+// 1, 2 in OpenCV's order; epnp5_case), then the one with the smallest
+// reprojection error.  Every lane of a wave computes the same (wave-uniform
+// control flow); k_pnp_epnp runs the three cases in three waves.
+struct EpnpCommon {
+  double alpha[kModel][4];
+  double ut[4][12];  // ut[q] = OpenCV's ut row 11 - q
+  double L[6][10], rho[6];
+};
+__host__ __device__ void epnp5_common(const EpnpIn& in, const PnPCam& k, double* lds, EpnpCommon& cm) {
   // choose_control_points: centroid + PCA (cv::SVD of PW0^T PW0)
   double cws[4][3];
 #pragma unroll
@@ -458,7 +468,7 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
       }
     }
   }
-  double alpha[kModel][4];
+  double (&alpha)[kModel][4] = cm.alpha;
 #pragma unroll
   for (int p = 0; p < kModel; ++p) {
 #pragma unroll
@@ -472,7 +482,7 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
   // change of rounding rotates, so the device and the oracle fix one order:
   // sequential over the rows of M, the 16-lane butterfly over the 12 entries
   // of a row of At (cv_svd12_lanes; oracle cv_svd(tree=True)).
-  double ut[4][12];  // ut[q] = OpenCV's ut row 11 - q
+  double (&ut)[4][12] = cm.ut;
   {
     double M1[kModel][12], M2[kModel][12];
 #pragma unroll
@@ -519,7 +529,8 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
     host_svd12_tree(MtM, ut);
 #endif
   }
-  double L[6][10], rho[6];
+  double (&L)[6][10] = cm.L;
+  double (&rho)[6] = cm.rho;
   {
     const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
 #pragma unroll
@@ -538,8 +549,15 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
       rho[i] = d0 * d0 + d1 * d1 + d2 * d2;
     }
   }
-  double Rs[3][9], ts[3][3], err[3];
-  {
+}
+
+__host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, const EpnpCommon& cm, double R[9],
+                                      double t[3]) {
+  const double (&alpha)[kModel][4] = cm.alpha;
+  const double (&ut)[4][12] = cm.ut;
+  const double (&L)[6][10] = cm.L;
+  const double (&rho)[6] = cm.rho;
+  if (N == 0) {
     double A4[6][4], b4[4];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { A4[i][0] = L[i][0]; A4[i][1] = L[i][1]; A4[i][2] = L[i][3]; A4[i][3] = L[i][6]; }
@@ -551,9 +569,8 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
       be[0] = sqrt(b4[0]); be[1] = b4[1] / be[0]; be[2] = b4[2] / be[0]; be[3] = b4[3] / be[0];
     }
     gauss_newton(L, rho, be);
-    err[0] = r_and_t(in, alpha, ut, be, k, Rs[0], ts[0]);
-  }
-  {
+    return r_and_t(in, alpha, ut, be, k, R, t);
+  } else if (N == 1) {
     double A3[6][3], b3[3];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { A3[i][0] = L[i][0]; A3[i][1] = L[i][1]; A3[i][2] = L[i][2]; }
@@ -564,9 +581,8 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
     if (b3[1] < 0) be[0] = -be[0];
     be[2] = 0.0; be[3] = 0.0;
     gauss_newton(L, rho, be);
-    err[1] = r_and_t(in, alpha, ut, be, k, Rs[1], ts[1]);
-  }
-  {
+    return r_and_t(in, alpha, ut, be, k, R, t);
+  } else {
     double A5[6][5], b5[5];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -580,8 +596,16 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
     be[2] = b5[3] / be[0];
     be[3] = 0.0;
     gauss_newton(L, rho, be);
-    err[2] = r_and_t(in, alpha, ut, be, k, Rs[2], ts[2]);
+    return r_and_t(in, alpha, ut, be, k, R, t);
   }
+}
+
+__host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, double R[9], double t[3]) {
+  EpnpCommon cm;
+  epnp5_common(in, k, lds, cm);
+  double Rs[3][9], ts[3][3], err[3];
+#pragma unroll
+  for (int n = 0; n < 3; ++n) err[n] = epnp5_case(n, in, k, cm, Rs[n], ts[n]);
   int N = 0;
   if (err[1] < err[0]) N = 1;
   if (err[2] < err[N]) N = 2;
@@ -617,11 +641,17 @@ __global__ void k_pnp_subsets(int n, int iters, int* __restrict__ sub) {
   }
 }
 
-// One wave per hypothesis: EPnP on its subset -> model (rvec 3 | tvec 3).
-__global__ __launch_bounds__(64) void k_pnp_epnp(const double* __restrict__ obj, const double* __restrict__ img,
-                                                 const int* __restrict__ sub, PnPCam k, double* __restrict__ model) {
-  __shared__ double lds[48];
+// One workgroup of three waves per hypothesis: EPnP on its subset -> model
+// (rvec 3 | tvec 3).  Every wave computes the common part (the SVD of M is
+// the long pole and a wave-wide exchange); wave w then solves beta case w,
+// and wave 0 picks the case with the smallest reprojection error as epnp5
+// does (err[1] < err[0], then err[2] < err[N]).
+__global__ __launch_bounds__(192) void k_pnp_epnp(const double* __restrict__ obj, const double* __restrict__ img,
+                                                  const int* __restrict__ sub, PnPCam k, double* __restrict__ model) {
+  __shared__ double lds[3][48];
+  __shared__ double res[3][13];
   const int it = blockIdx.x;
+  const int w = threadIdx.x >> 6;
   EpnpIn in;
 #pragma unroll
   for (int p = 0; p < kModel; ++p) {
@@ -634,8 +664,26 @@ __global__ __launch_bounds__(64) void k_pnp_epnp(const double* __restrict__ obj,
     in.us[p][0] = double(xn) * k.fu + k.uc;
     in.us[p][1] = double(yn) * k.fv + k.vc;
   }
+  EpnpCommon cm;
+  epnp5_common(in, k, lds[w], cm);
   double R[9], t[3], r[3];
-  epnp5(in, k, lds, R, t);
+  const double e = epnp5_case(w, in, k, cm, R, t);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) res[w][i] = R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) res[w][9 + i] = t[i];
+    res[w][12] = e;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  int N = 0;
+  if (res[1][12] < res[0][12]) N = 1;
+  if (res[2][12] < res[N][12]) N = 2;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = res[N][i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = res[N][9 + i];
   rodrigues_m2v(R, r);
   if (threadIdx.x == 0) {
     double* o = model + 6 * it;
@@ -799,7 +847,7 @@ extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, cons
       hipMemcpyAsync(c->img, img, sizeof(double) * 2 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess)
     return pfail(SFM_EIO, "upload failed");
   k_pnp_subsets<<<1, 64, 0, s>>>(n, iters, c->sub);
-  k_pnp_epnp<<<iters, 64, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
+  k_pnp_epnp<<<iters, 192, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
   k_pnp_count<<<iters, 256, 0, s>>>(n, c->obj, c->img, c->model, k, thr, c->cnt);
   k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->res, c->inl);
   int res[4] = {0, -1, 0, 0};
