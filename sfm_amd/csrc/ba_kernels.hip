@@ -755,7 +755,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
 // resident) and recomputing both scaled Jacobians with the Jacobian pass's
 // own arithmetic (jac_record).  A gathered-F formulation fetched a fresh
 // 144-B F record per pair from a 293-MB array (~2.9 GB of HBM traffic per
-// launch at C3); this one trades that for ~400 fp64 ops per pair.  The
+// launch at C3); this one trades that for ~320 fp64 ops per pair.  The
 // block's lanes end with a fixed-order recursive-halving reduction, so S is
 // bitwise reproducible run to run.
 constexpr int kCamS = 50;  // R 9 | dR/dw 27 | t 3 | K 5 | scale 6
@@ -793,23 +793,6 @@ __device__ __forceinline__ void pair_side_m(const double* cs, const double Xp[3]
   M[0] = e[0] * i00; M[1] = (e[1] - l10 * M[0]) * i11; M[2] = (e[2] - l20 * M[0] - l21 * M[1]) * i22;
   M[3] = e[3] * i00; M[4] = (e[4] - l10 * M[3]) * i11; M[5] = (e[5] - l20 * M[3] - l21 * M[4]) * i22;
 }
-// Column kk of the scaled J_c (rows m | n): ju = J_c[kk], jv = J_c[6 + kk].
-__device__ __forceinline__ void pair_jc(const double* cs, const double Xp[3], const double ab[5], int kk,
-                                        double& ju, double& jv) {
-  const double* sc = cs + 44;
-  if (kk < 3) {
-    const double* D = cs + 9 + 9 * kk;
-    const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
-    const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
-    const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
-    ju = (ab[0] * q0 + ab[1] * q1 + ab[2] * q2) * sc[kk];
-    jv = (ab[3] * q1 + ab[4] * q2) * sc[kk];
-  } else {
-    ju = ab[kk - 3] * sc[kk];
-    jv = kk == 3 ? 0.0 : ab[kk - 1] * sc[kk];
-  }
-}
-
 // Sums of 32 values over the kSub lanes of a segment by recursive halving
 // (see wave_sum32): afterwards lane l holds in v[0 .. kR) the sums of values
 // kR * (l % kSub) + r (kSub <= 32, kR = 32 / kSub), or of value l >> 1
@@ -912,30 +895,58 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
     }
     const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
     const double Lp[6] = {q[6], q[7], q[8], q[9], q[10], q[11]};
-    // side 2 in full (J_c2 feeds every accumulator row); side 1 keeps M_1 and
-    // its five coefficients, its J_c columns made row by row below (12 fewer
-    // live doubles: 3 waves per SIMD instead of 2)
-    double M1[6], ab1[5], M2[6], ab2[5], J2[12];
+    double M1[6], ab1[5], M2[6], ab2[5];
     pair_side_m(cs1, Xp, sp, Lp, M1, ab1);
     pair_side_m(cs2, Xp, sp, Lp, M2, ab2);
-    // (a scheduling fence: without it the LDS reads of both J_c hoist above
-    // and 168 VGPRs spill)
+    // (a scheduling fence: without it the LDS reads of both cameras' dR/dw
+    // hoist above and the VGPRs spill)
     asm volatile("" ::: "memory");
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) pair_jc(cs2, Xp, ab2, kk, J2[kk], J2[6 + kk]);
     const double w = valid ? 1.0 : 0.0;
     const double g00 = (M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2]) * w;
     const double g01 = (M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5]) * w;
     const double g10 = (M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2]) * w;
     const double g11 = (M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5]) * w;
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      double j1u, j1v;
-      pair_jc(cs1, Xp, ab1, u, j1u, j1v);
-      const double h0 = j1u * g00 + j1v * g10, h1 = j1u * g01 + j1v * g11;
-#pragma unroll
-      for (int v = 0; v < 6; ++v) acc[6 * u + v] += h0 * J2[v] + h1 * J2[6 + v];
+    // J_c,i = A_i [Q_i | I] diag(sc_i), A_i = dr/dpc = [a0 a1 a2; 0 b1 b2],
+    // Q_i = [dR_0 X | dR_1 X | dR_2 X]; so the pair adds
+    //   [Q_1 | I]^T H [Q_2 | I],  H = A_1^T G A_2 (3x3),
+    // and the Jacobi scales are applied once per block, at the store.
+    double H[3][3];
+    {
+      const double t00 = g00 * ab2[0], t01 = g00 * ab2[1] + g01 * ab2[3], t02 = g00 * ab2[2] + g01 * ab2[4];
+      const double t10 = g10 * ab2[0], t11 = g10 * ab2[1] + g11 * ab2[3], t12 = g10 * ab2[2] + g11 * ab2[4];
+      H[0][0] = ab1[0] * t00; H[0][1] = ab1[0] * t01; H[0][2] = ab1[0] * t02;
+      H[1][0] = ab1[1] * t00 + ab1[3] * t10; H[1][1] = ab1[1] * t01 + ab1[3] * t11; H[1][2] = ab1[1] * t02 + ab1[3] * t12;
+      H[2][0] = ab1[2] * t00 + ab1[4] * t10; H[2][1] = ab1[2] * t01 + ab1[4] * t11; H[2][2] = ab1[2] * t02 + ab1[4] * t12;
     }
+    double HQ[3][3];  // H Q_2
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double* D = cs2 + 9 + 9 * k;
+      const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+      const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+      const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) HQ[i][k] = H[i][0] * q0 + H[i][1] * q1 + H[i][2] * q2;
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const double* D = cs1 + 9 + 9 * u;
+      const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+      const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+      const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        acc[6 * u + v] += q0 * HQ[0][v] + q1 * HQ[1][v] + q2 * HQ[2][v];
+        acc[6 * u + 3 + v] += q0 * H[0][v] + q1 * H[1][v] + q2 * H[2][v];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        acc[6 * (3 + u) + v] += HQ[u][v];
+        acc[6 * (3 + u) + 3 + v] += H[u][v];
+      }
   }
   double v32[32];
 #pragma unroll
@@ -968,8 +979,12 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
     // k_schur_diag_sum wrote before this launch, else stored
     double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
     const bool add = cc.x == cc.y;
+    // the Jacobi scales of both cameras (staged in LDS by this segment)
+    const double* sc1 = cst[wv][g] + 44;
+    const double* sc2 = sc1 + kCamS;
     auto put = [&](int e, double v) {
       double* q = Sb + size_t(e / 6) * ld + e % 6;
+      v = v * sc1[e / 6] * sc2[e % 6];
       *q = add ? *q - v : -v;
     };
     constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
