@@ -12,6 +12,33 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+// One job of a batched scalar reduction (a 1024-thread workgroup, fixed
+// order: bitwise reproducible): scal[j.dst] = sum / max of the job's
+// partials; `fail` != nullptr also copies the Cholesky failure int into the
+// slot after the scalars.  k_reduce_batch and the device LM loop's
+// k_reduce_batch_lm (ba_solver.hip) share it.
+__device__ __forceinline__ void reduce_batch_job(const double* __restrict__ partials, int64_t max_blocks,
+                                                 const ReduceJob& j, double* __restrict__ scal,
+                                                 const int* __restrict__ fail, double* sh) {
+  const double* src = partials + size_t(j.slot) * max_blocks;
+  double v = 0.0;
+  for (int i = threadIdx.x; i < j.nb; i += 1024) v = j.op ? fmax(v, src[i]) : v + src[i];
+  v = j.op ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = sh[0];
+    for (int i = 1; i < 16; ++i) r = j.op ? fmax(r, sh[i]) : r + sh[i];
+    scal[j.dst] = r;
+    if (fail) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
+  }
+}
 // Wave sums of 32 values at once by recursive halving (reduce-scatter): at
 // each of the 5 exchange distances 32..2 a lane keeps half of its values and
 // trades the other half with its partner, then the two lanes of a pair add

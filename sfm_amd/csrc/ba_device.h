@@ -166,7 +166,9 @@ enum PartialSlot {
 };
 
 // ---- launchers (ba_kernels.hip) ----
-void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s);
+void launch_cam_prep(const DevProblem& d, double* cam, bool count_norm, hipStream_t s);
+// the device LM loop's accept folded in: cam_new -> cam, X_new -> X (grid >= the copy's workgroups)
+void launch_cam_prep_accept(const DevProblem& d, bool count_norm, int grid, hipStream_t s);
 // write_records: also store the 160-B records (evaluate API, bench roofline)
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records = false);
 void launch_cam_reduce(const DevProblem& d, hipStream_t s);

@@ -23,13 +23,6 @@ namespace sfm {
 
 namespace {
 
-
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  return v;
-}
-
 // Fixed-order block reduction; result valid in thread 0.  `sh` >= 4 doubles.
 __device__ __forceinline__ double block_reduce(double v, double* sh, bool is_max) {
   v = is_max ? wave_max(v) : wave_sum(v);
@@ -96,20 +89,34 @@ __device__ void rotation(const double w[3], double R[9], double* dR) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_cam_prep(int C, const double* __restrict__ cam,
-                                                       double* __restrict__ camR, double* __restrict__ part_xn, const int* __restrict__ gate) {
+// With cam_src (the device LM loop's accepted step, k_lm_accept folded in)
+// the cameras are read from cam_src and stored to cam, and the grid also
+// copies X_src -> X_dst (n_x doubles); only the first ceil(C / kThreads)
+// workgroups hold cameras and write |x|^2 partials.
+__global__ __launch_bounds__(kThreads) void k_cam_prep(int C, double* __restrict__ cam,
+                                                       double* __restrict__ camR, double* __restrict__ part_xn, const int* __restrict__ gate,
+                                                       const double* __restrict__ cam_src, const double* __restrict__ X_src,
+                                                       double* __restrict__ X_dst, int64_t n_x) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n_x; i += int64_t(gridDim.x) * blockDim.x)
+    X_dst[i] = X_src[i];
+  if (int64_t(blockIdx.x) * blockDim.x >= C) return;  // workgroup-uniform: no camera in this one
   double xn = 0.0;
   if (c < C) {
-    const double w[3] = {cam[6 * c], cam[6 * c + 1], cam[6 * c + 2]};
+    const double* cs = cam_src ? cam_src : cam;
+    double x6[6];
+    for (int k = 0; k < 6; ++k) x6[k] = cs[6 * c + k];
+    if (cam_src)
+      for (int k = 0; k < 6; ++k) cam[6 * c + k] = x6[k];
+    const double w[3] = {x6[0], x6[1], x6[2]};
     double R[9], dR[27];
     rotation(w, R, dR);
     double* o = camR + size_t(kCamR) * c;
     for (int i = 0; i < 9; ++i) o[i] = R[i];
     for (int i = 0; i < 27; ++i) o[9 + i] = dR[i];
-    for (int k = 0; k < 6; ++k) xn += cam[6 * c + k] * cam[6 * c + k];
+    for (int k = 0; k < 6; ++k) xn += x6[k] * x6[k];
   }
   const double r = block_reduce(xn, sh, false);
   if (threadIdx.x == 0 && part_xn) part_xn[blockIdx.x] = r;
@@ -1006,10 +1013,30 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        const double* __restrict__ Ucam,
                                                        const double* __restrict__ diag_c, double radius,
                                                        int add_diag, double* __restrict__ S, int ld, int n,
-                                                       int init, const int* __restrict__ gate, const double* __restrict__ radius_dev) {
+                                                       int init, const int* __restrict__ gate, const double* __restrict__ radius_dev,
+                                                       int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   const int c = blockIdx.x, t = threadIdx.x;
+  // k_pad_init folded in (one launch fewer per LM iteration): the identity
+  // padding below row n of this camera's six columns and y's sentinel
+  // there; the last camera also takes columns n.. (the identity block, the
+  // pivot (n, n) = 1), the rest of the sentinel and the failure flag.  None
+  // of these entries is written by the Schur passes.
+  for (int j = 6 * c; j < 6 * c + 6; ++j) {
+    for (int i = n + 1 + t; i < ld; i += 64) S[size_t(j) * ld + i] = 0.0;
+    if (t == 0 && j < n_y) ysol[j] = kYSentinel;  // k_backsolve's "not yet produced"
+  }
+  if (c == gridDim.x - 1) {
+    for (int j = n; j < ld; ++j) {
+      for (int i = (j > n ? j : n + 1) + t; i < ld; i += 64) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
+      if (t == 0 && j < n_y) ysol[j] = kYSentinel;
+    }
+    if (t == 0) {
+      S[size_t(n) * ld + n] = 1.0;
+      *fail = 0;
+    }
+  }
   const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
   // lane t sums waves w0 + t, w0 + t + 64, ... (coalesced 216-B rows), then
   // one reduce-scatter over the wave: lane 2e ends with entry e
@@ -1286,20 +1313,7 @@ __global__ __launch_bounds__(1024) void k_reduce_batch(const double* __restrict_
                                                        const int* __restrict__ fail, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[16];
-  const ReduceJob j = b.job[blockIdx.x];
-  const double* src = partials + size_t(j.slot) * max_blocks;
-  double v = 0.0;
-  for (int i = threadIdx.x; i < j.nb; i += 1024) v = j.op ? fmax(v, src[i]) : v + src[i];
-  v = j.op ? wave_max(v) : wave_sum(v);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  if (l == 0) sh[w] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double r = sh[0];
-    for (int i = 1; i < 16; ++i) r = j.op ? fmax(r, sh[i]) : r + sh[i];
-    scal[j.dst] = r;
-    if (fail && blockIdx.x == 0) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
-  }
+  reduce_batch_job(partials, max_blocks, b.job[blockIdx.x], scal, blockIdx.x == 0 ? fail : nullptr, sh);
 }
 
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ src, int nb, int op,
@@ -1324,8 +1338,13 @@ int blocks_for(int64_t n, int threads) { return int((n + threads - 1) / threads)
 
 static inline double* slot(const DevProblem& d, int s) { return d.partials + size_t(s) * d.max_blocks; }
 
-void launch_cam_prep(const DevProblem& d, const double* cam, bool count_norm, hipStream_t s) {
-  k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr, d.gate);
+void launch_cam_prep(const DevProblem& d, double* cam, bool count_norm, hipStream_t s) {
+  k_cam_prep<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr, d.gate,
+                                                            nullptr, nullptr, nullptr, 0);
+}
+void launch_cam_prep_accept(const DevProblem& d, bool count_norm, int grid, hipStream_t s) {
+  k_cam_prep<<<std::max(grid, blocks_for(d.C, kThreads)), kThreads, 0, s>>>(
+      d.C, d.cam, d.camR, count_norm ? slot(d, kPXNormCam) : nullptr, d.gate, d.cam_new, d.X_new, d.X, 3 * int64_t(d.P));
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records) {
   // the record-writing variant (evaluate API) runs on its own, smaller grid
@@ -1377,7 +1396,8 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
   // the off-diagonal blocks, which add a block's same-camera duplicate pairs
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
-                                        d.n, 1, d.gate, d.radius_dev);
+                                        d.n, 1, d.gate, d.radius_dev, d.fail,
+                                        reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB);
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
   const int nb = int((d.n_bslots + per - 1) / per);

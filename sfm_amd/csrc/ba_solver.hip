@@ -26,6 +26,7 @@
 
 #include "ba_device.h"
 #include "ba_setup.h"
+#include "ba_common.h"
 #include "../../include/sfm_amd.h"
 
 namespace {
@@ -62,6 +63,8 @@ struct LmCtl {
   sfm_ba_iteration pending;  // an accepted iteration, completed after its evaluation
   int32_t max_iter, max_invalid;
   double ftol, gtol, ptol, max_radius, min_radius, min_rel_dec;
+  uint32_t red_count;  // workgroups of k_reduce_batch_lm done (reset by the last)
+  double init_cost, init_grad;  // the initial evaluation (k_lm_init), for the host's summary
 };
 
 struct sfm_ba_handle {
@@ -90,6 +93,20 @@ struct sfm_ba_handle {
   LmCtl* lm_ctl_host = nullptr;
   sfm_ba_iteration* lm_trace = nullptr;
   int lm_trace_cap = 0;
+  // pinned staging for every host <-> device transfer of set_problem,
+  // get_parameters and the LM trace: a pageable copy goes through the
+  // runtime's own staging (C1: the 320-KB uv upload took 131 us, the 49-KB
+  // parameter download ~100 us), a pinned one is a single DMA.  Grown
+  // geometrically, only while the stream is idle.
+  uint8_t* stage = nullptr;
+  size_t stage_cap = 0;
+  // device LM loop without a collective: the phase reductions run the
+  // bookkeeping in their last workgroup (k_reduce_batch_lm)
+  bool fuse_lm = false;
+  // device LM loop: the evaluation's k_cam_prep also makes the accepted
+  // candidate current (k_lm_accept folded in; its grid covers the copy)
+  int accept_grid = 0;
+  int n_cu = 0;  // compute units of the device (queried once)
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -138,6 +155,31 @@ void retire_tmps(sfm_ba_handle* h) {
   for (auto& a : h->tmps) h->pool.insert(a);
   h->tmps.clear();
 }
+
+// The pinned staging buffer with room for `bytes` (the caller has synchronised
+// the stream: nothing may still read or write the old buffer).
+int stage_reserve(sfm_ba_handle* h, size_t bytes) {
+  if (bytes <= h->stage_cap) return 0;
+  const size_t cap = std::max<size_t>({bytes, size_t(1) << 20, 2 * h->stage_cap});
+  if (h->stage) (void)hipHostFree(h->stage);
+  h->stage = nullptr;
+  h->stage_cap = 0;
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->stage), cap) != hipSuccess) {
+    h->stage = nullptr;
+    return fail(SFM_ENOMEM, "hipHostMalloc failed (staging buffer)");
+  }
+  h->stage_cap = cap;
+  return 0;
+}
+// byte offsets of a packed staging layout (256-B aligned pieces)
+struct StageLayout {
+  size_t bytes = 0;
+  size_t add(size_t n) {
+    const size_t o = bytes;
+    bytes += (n + 255) & ~size_t(255);
+    return o;
+  }
+};
 
 void release_pool(sfm_ba_handle* h) {
   for (auto& kv : h->pool) hipFree(kv.second);
@@ -214,7 +256,9 @@ struct HostTimer {
 // The trust-region bookkeeping of the host loop in sfm_ba_solve_resident,
 // restated on the device so that an unsharded solve enqueues several
 // iterations per host synchronisation.  k_lm_decide follows compute_step's
-// reductions, k_lm_accept and the evaluation kernels run only when the step
+// reductions; the accept copy (cam_new -> cam, X_new -> X: enqueued
+// iterations hold fixed pointers, where the host loop swaps them) and the
+// evaluation kernels run only when the step
 // was accepted (gate run_eval), k_lm_post completes the accepted iteration
 // after its evaluation; compute_step's kernels run only while the loop is
 // not done (gate run_step).  The arithmetic is the host loop's, operation
@@ -234,7 +278,7 @@ __device__ void lm_finish(LmCtl* c, int term) {
 
 // after compute_step's reduction (scal: model change, candidate cost, step
 // norms, bad-step flags; the Cholesky failure int after the scalars)
-__global__ void k_lm_decide(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+__device__ void lm_decide(LmCtl* c, const double* scal, sfm_ba_iteration* trace, int cap) {
 #pragma clang fp contract(off)
   if (c->done) {
     c->run_eval = 0;
@@ -317,21 +361,12 @@ __global__ void k_lm_decide(LmCtl* c, const double* __restrict__ scal, sfm_ba_it
   if (c->radius < c->min_radius) { lm_finish(c, SFM_CONVERGENCE); return; }
   if (c->iteration >= c->max_iter) { lm_finish(c, SFM_NO_CONVERGENCE); return; }
 }
-
-// the accepted candidate becomes the current point (the host loop swaps the
-// buffers; enqueued iterations hold fixed pointers, so this copies)
-__global__ void k_lm_accept(const int32_t* __restrict__ gate, int C, int P, const double* __restrict__ cam_new,
-                            double* __restrict__ cam, const double* __restrict__ X_new, double* __restrict__ X) {
-  if (*gate == 0) return;
-  const int64_t n_c = 6 * int64_t(C), n = n_c + 3 * int64_t(P);
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    if (i < n_c) cam[i] = cam_new[i];
-    else X[i - n_c] = X_new[i - n_c];
-  }
+__global__ void k_lm_decide(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+  lm_decide(c, scal, trace, cap);
 }
 
 // after the accepted step's evaluation (scal: cost, gradient max norms, |x|^2)
-__global__ void k_lm_post(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+__device__ void lm_post(LmCtl* c, const double* scal, sfm_ba_iteration* trace, int cap) {
 #pragma clang fp contract(off)
   if (!c->run_eval) return;
   c->run_eval = 0;
@@ -350,10 +385,88 @@ __global__ void k_lm_post(LmCtl* c, const double* __restrict__ scal, sfm_ba_iter
   if (c->grad_max <= c->gtol) { lm_finish(c, SFM_CONVERGENCE); return; }
   if (c->iteration >= c->max_iter) { lm_finish(c, SFM_NO_CONVERGENCE); return; }
 }
+__global__ void k_lm_post(LmCtl* c, const double* __restrict__ scal, sfm_ba_iteration* trace, int cap) {
+  lm_post(c, scal, trace, cap);
+}
+
+// after the initial evaluation (scal: cost, gradient max norms, |x|^2): the
+// loop state the host loop derives from its first evaluate(), so that the
+// solve needs no host round trip before the first iteration.  Error bit 8:
+// the initial cost is not finite (the host reports it).
+__device__ void lm_init(LmCtl* c, const double* scal) {
+#pragma clang fp contract(off)
+  const double cost = scal[kCost];
+  c->cost = cost;
+  c->init_cost = cost;
+  c->grad_max = fmax(scal[kGradMaxCam], scal[kGradMaxPt]);
+  c->init_grad = c->grad_max;
+  c->x_norm = sqrt(scal[kXNorm2Cam] + scal[kXNorm2Pt]);
+  if (!isfinite(cost)) {
+    c->error |= 8;
+    lm_finish(c, SFM_FAILURE);
+  } else if (c->grad_max <= c->gtol) {
+    lm_finish(c, SFM_CONVERGENCE);
+  } else if (c->max_iter <= 0) {
+    lm_finish(c, SFM_NO_CONVERGENCE);
+  }
+}
+__global__ void k_lm_init(LmCtl* c, const double* __restrict__ scal) { lm_init(c, scal); }
+
+// A phase's batched reduction fused with the bookkeeping that follows it
+// (unsharded device loop: no collective sits between them): every
+// workgroup reduces its job (reduce_batch_job, as k_reduce_batch), and the
+// last one to finish runs k_lm_decide's (kPost: k_lm_post's) body on the
+// reduced scalars -- one launch instead of two, ~4.5 us of dispatch each.
+// The scalars are re-read through agent-scope loads after the count (the
+// other workgroups' stores were fenced before their increment); the count
+// lives in the control block, which the loop's upload zeroes, and the last
+// workgroup resets it.  Gated like the reduction: with the phase skipped the
+// bookkeeping is a no-op too (run_step = 0 only once done, run_eval = 0).
+enum LmTail { kTailDecide = 0, kTailPost = 1, kTailInit = 2 };
+template <int kTail>
+__global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restrict__ partials, int64_t max_blocks,
+                                                          ReduceBatch b, double* __restrict__ scal,
+                                                          const int* __restrict__ fail, const int* __restrict__ gate,
+                                                          LmCtl* c, sfm_ba_iteration* trace, int cap) {
+  if (gate && *gate == 0) return;
+  __shared__ double sh[16];
+  __shared__ double sc[kNumScalars + 1];
+  __shared__ int last;
+  reduce_batch_job(partials, max_blocks, b.job[blockIdx.x], scal, blockIdx.x == 0 ? fail : nullptr, sh);
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&c->red_count, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x <= kNumScalars)
+    sc[threadIdx.x] = __hip_atomic_load(scal + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c->red_count = 0;
+    if (kTail == kTailPost) lm_post(c, sc, trace, cap);
+    else if (kTail == kTailInit) lm_init(c, sc);
+    else lm_decide(c, sc, trace, cap);
+  }
+}
 
 // Reduced systems with more camera blocks than this take the XCD-aware
 // k_schur_pts order (C3: 125k blocks); smaller ones the plain order.
 constexpr int64_t kSchurXcdMinBlocks = 8192;
+
+// Host layout path (ba_setup_host.hip) for keyframe-sized problems: up to
+// kHostSetupMaxObs observations (SFM_HOST_SETUP_MAX_OBS) and few enough
+// camera blocks for the plain k_schur_pts order.  SFM_HOST_SETUP=0 / 1
+// forces the device / host path (the latter within the block bound).
+constexpr int64_t kHostSetupMaxObs = 65536;
+bool use_host_setup(int64_t N, int C) {
+  if (int64_t(C) * (C + 1) / 2 > kSchurXcdMinBlocks) return false;
+  if (const char* e = std::getenv("SFM_HOST_SETUP")) return e[0] == '1';
+  int64_t mx = kHostSetupMaxObs;
+  if (const char* m = std::getenv("SFM_HOST_SETUP_MAX_OBS")) mx = std::atoll(m);
+  return N <= mx;
+}
 
 bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
 
@@ -384,6 +497,26 @@ int fetch_scalars(sfm_ba_handle* h) {
   return 0;
 }
 
+// A phase's closing reduction; in the fused device loop (h->fuse_lm) with
+// the bookkeeping that follows it: k_lm_decide after compute_step
+// (kTailDecide), k_lm_post after an evaluation (kTailPost), k_lm_init after
+// the initial one (kTailInit).
+void reduce_phase(sfm_ba_handle* h, const ReduceBatch& rb, bool copy_fail, int tail) {
+  DevProblem& d = h->d;
+  if (h->fuse_lm && rb.n > 0) {
+#define SFM_RB_LM(T_)                                                                                      \
+  k_reduce_batch_lm<T_><<<rb.n, 1024, 0, h->stream>>>(d.partials, d.max_blocks, rb, d.scal,                 \
+                                                      copy_fail ? d.fail : nullptr, d.gate, h->lm_ctl,      \
+                                                      h->lm_trace, h->lm_trace_cap)
+    if (tail == kTailPost) SFM_RB_LM(kTailPost);
+    else if (tail == kTailInit) SFM_RB_LM(kTailInit);
+    else SFM_RB_LM(kTailDecide);
+#undef SFM_RB_LM
+    return;
+  }
+  launch_reduce_batch(d, rb, copy_fail, h->stream);
+}
+
 // Evaluate cost, Jacobian, Jacobi scale (first call), per-block normal
 // equations, LM diagonal and gradient at the current parameters.
 int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
@@ -396,7 +529,8 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   const bool cams_var = h->mode != SFM_BA_STRUCT_ONLY, pts_var = h->mode != SFM_BA_POSE_ONLY;
   const int nbP = std::max(1, blocks_for(d.P, 256)),
             nbC = std::max(1, blocks_for(d.C, 256));
-  launch_cam_prep(d, d.cam, cams_var, s);
+  if (h->accept_grid > 0) launch_cam_prep_accept(d, cams_var, h->accept_grid, s);
+  else launch_cam_prep(d, d.cam, cams_var, s);
   mark_begin(h, kPhJac);
   launch_jacobian(d, !first || !jacobi_scaling ? true : false, s);
   mark_end(h);
@@ -452,7 +586,7 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   rb.add(kPGradPt, nbP, 1, kGradMaxPt);
   rb.add(kPXNormCam, nbC, 0, kXNorm2Cam);
   rb.add(kPXNormPt, nbP, 0, kXNorm2Pt);
-  launch_reduce_batch(d, rb, false, s);
+  reduce_phase(h, rb, false, first ? kTailInit : kTailPost);
   if (sharded(h)) {
     if ((rc = allreduce(h, d.scal + kCost, 1, ncclSum))) return rc;
     if ((rc = allreduce(h, d.scal + kGradMaxCam, 2, ncclMax))) return rc;
@@ -485,7 +619,9 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
       if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
       launch_pack_upper(d, true, s);
     }
-    launch_pad_init(d, s);  // also clears the failure flag and sets y's sentinel
+    // (k_schur_diag_sum also wrote the identity padding, y's sentinel and
+    // the cleared failure flag; without cameras the separate launch does)
+    if (!d.C) launch_pad_init(d, s);
     mark_begin(h, kPhChol);
     launch_cholesky(d, ++h->chol_epoch, s, false);
     mark_end(h);
@@ -531,7 +667,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
   rb.add(kPBadBack, nbP, 1, kBadBack);
   rb.add(kPModelPt, nbP, 0, kModelChangePt);
   // ... and the Cholesky failure flag (an int) into the slot after the scalars
-  launch_reduce_batch(d, rb, true, s);
+  reduce_phase(h, rb, true, kTailDecide);
   if (sharded(h)) {
     if ((rc = allreduce(h, d.scal + kModelChange, 4, ncclSum))) return rc;  // model, new cost, step pt, step cam
     if ((rc = allreduce(h, d.scal + kBadStep, 4, ncclMax))) return rc;
@@ -568,20 +704,18 @@ const char* invalid_option(const sfm_ba_options& o) {
 }
 
 // The device-driven LM loop of sfm_ba_solve_resident (all but the
-// host-callback collective):
-// state in LmCtl, iterations enqueued in batches (3, then 2; SFM_LM_BATCH
-// fixes the size), the host reads the control block once per batch.  The gated
-// kernels of iterations enqueued past the end return at once.
+// host-callback collective), initial evaluation included:
+// state in LmCtl, initialised on the device from the initial evaluation
+// (k_lm_init: no host round trip before the first iteration), iterations
+// enqueued in batches (3, then 2; SFM_LM_BATCH fixes the size), the host
+// reads the control block once per batch.  The gated kernels of iterations
+// enqueued past the end return at once.  *nonfinite: the initial cost was
+// not finite (the summary is then the host loop's FAILURE).
 template <class Push>
-int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, double grad_max, double x_norm,
-                  sfm_ba_summary* sm, Push& push) {
+int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sfm_ba_summary* sm, Push& push,
+                  bool* nonfinite) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
-  if (opts.max_num_iterations <= 0) {
-    sm->termination_type = SFM_NO_CONVERGENCE;
-    sm->num_iterations = 0;
-    return 0;
-  }
   if (!h->lm_ctl) {
     if (hipMalloc(reinterpret_cast<void**>(&h->lm_ctl), sizeof(LmCtl)) != hipSuccess) {
       h->lm_ctl = nullptr;
@@ -592,7 +726,7 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, do
       return fail(SFM_ENOMEM, "hipHostMalloc failed (LM control)");
     }
   }
-  const int cap = opts.max_num_iterations + 1;
+  const int cap = std::max(1, opts.max_num_iterations + 1);
   if (h->lm_trace_cap < cap) {
     if (h->lm_trace) (void)hipFree(h->lm_trace);
     h->lm_trace = nullptr;
@@ -608,9 +742,6 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, do
   c.run_step = 1;
   c.radius = opts.initial_trust_region_radius;
   c.decrease_factor = 2.0;
-  c.cost = *cost;
-  c.grad_max = grad_max;
-  c.x_norm = x_norm;
   c.max_iter = opts.max_num_iterations;
   c.max_invalid = opts.max_num_consecutive_invalid_steps;
   c.ftol = opts.function_tolerance;
@@ -625,21 +756,31 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, do
   // (measured per C1 solve: batch 3 0.49 ms, 4 0.52, 6 0.62; host loop 0.54)
   int batch = 3, batch_next = 2;
   if (const char* b = std::getenv("SFM_LM_BATCH")) batch = batch_next = std::max(1, std::min(64, std::atoi(b)));
+  if (opts.max_num_iterations <= 0) batch = 0;  // k_lm_init ends the solve (NO_CONVERGENCE unless converged)
   const bool jac_scaling = opts.jacobi_scaling != 0;
   const int acc_blocks = std::max(1, std::min(1024, blocks_for(6 * int64_t(d.C) + 3 * int64_t(d.P), 256)));
   d.radius_dev = &h->lm_ctl->radius;
-  int rc = 0;
+  // without a collective between a phase's reduction and the bookkeeping,
+  // the two are one launch (k_reduce_batch_lm)
+  h->fuse_lm = !sharded(h) && !env_flag("SFM_LM_UNFUSED");
+  // the initial evaluation (Jacobi scaling on first use); its scalars
+  // initialise the loop state on the device
+  d.gate = nullptr;
+  int rc = evaluate_enqueue(h, true, jac_scaling);
+  if (rc == 0 && !h->fuse_lm) k_lm_init<<<1, 1, 0, s>>>(h->lm_ctl, d.scal);
   while (rc == 0) {
     for (int b = 0; b < batch && rc == 0; ++b) {
       d.gate = &h->lm_ctl->run_step;
       if ((rc = compute_step_enqueue(h, c.radius))) break;
       d.gate = nullptr;
-      k_lm_decide<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
+      if (!h->fuse_lm) k_lm_decide<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
       d.gate = &h->lm_ctl->run_eval;
-      k_lm_accept<<<acc_blocks, 256, 0, s>>>(d.gate, d.C, d.P, d.cam_new, d.cam, d.X_new, d.X);
-      if ((rc = evaluate_enqueue(h, false, jac_scaling))) break;
+      h->accept_grid = acc_blocks;  // k_lm_accept's copy inside the evaluation's k_cam_prep
+      rc = evaluate_enqueue(h, false, jac_scaling);
+      h->accept_grid = 0;
+      if (rc) break;
       d.gate = nullptr;
-      k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
+      if (!h->fuse_lm) k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
     }
     if (rc) break;
     if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -653,13 +794,39 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, do
   }
   d.gate = nullptr;
   d.radius_dev = nullptr;
+  h->fuse_lm = false;
   if (rc) return rc;
   if (c.error & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid not co-resident)");
   if (c.error & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid not co-resident)");
+  sm->num_jacobian_evaluations++;  // the initial evaluation
+  sm->num_residual_evaluations++;
+  sm->initial_cost = c.init_cost;
+  if (c.error & 8) {
+    *nonfinite = true;
+    sm->termination_type = SFM_FAILURE;
+    sm->final_cost = c.init_cost;
+    return fail(SFM_EIO, "initial residual evaluation is not finite");
+  }
+  {
+    sfm_ba_iteration it0;
+    std::memset(&it0, 0, sizeof(it0));
+    it0.cost = c.init_cost;
+    it0.gradient_max_norm = c.init_grad;
+    it0.trust_region_radius = opts.initial_trust_region_radius;
+    it0.step_is_valid = 1;
+    it0.step_is_successful = 1;
+    push(it0);
+  }
   const int n_tr = std::min(c.trace_len, h->lm_trace_cap);
-  std::vector<sfm_ba_iteration> tr(static_cast<size_t>(std::max(1, n_tr)));
-  if (n_tr) HIPCHK(hipMemcpy(tr.data(), h->lm_trace, sizeof(sfm_ba_iteration) * size_t(n_tr), hipMemcpyDeviceToHost));
-  for (int i = 0; i < n_tr; ++i) push(tr[i]);
+  if (n_tr) {
+    // (the stream is idle after the last control readback: the stage is free)
+    if (int e = stage_reserve(h, sizeof(sfm_ba_iteration) * size_t(n_tr))) return e;
+    HIPCHK(hipMemcpyAsync(h->stage, h->lm_trace, sizeof(sfm_ba_iteration) * size_t(n_tr), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<sfm_ba_iteration> tr(static_cast<size_t>(n_tr));
+    std::memcpy(tr.data(), h->stage, sizeof(sfm_ba_iteration) * size_t(n_tr));
+    for (int i = 0; i < n_tr; ++i) push(tr[i]);
+  }
   sm->termination_type = c.termination;
   sm->num_iterations = c.iteration;
   sm->num_successful_steps += c.n_succ;
@@ -713,6 +880,7 @@ int sfm_ba_create(int32_t device, sfm_ba_handle** out) {
     delete h;
     return fail(SFM_EIO, "hipStreamCreate failed");
   }
+  h->n_cu = device_cus(device);  // (hipGetDeviceProperties: once, not per set_problem)
   *out = h;
   return 0;
 }
@@ -727,6 +895,7 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_ctl) hipFree(h->lm_ctl);
   if (h->lm_ctl_host) hipHostFree(h->lm_ctl_host);
   if (h->lm_trace) hipFree(h->lm_trace);
+  if (h->stage) hipHostFree(h->stage);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -799,36 +968,64 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     hipError_t e_ = (expr);                                                                       \
     if (e_ != hipSuccess) return bail(fail(SFM_EIO, std::string(#expr) + ": " + hipGetErrorString(e_))); \
   } while (0)
-  // ---- the caller's observation arrays go up as they are; the O(N) layout
-  // work runs on the device (ba_setup.hip) ----
+  // Keyframe-sized problems (the reference's per-keyframe BA: tens of
+  // cameras, a few thousand points) are laid out on the host
+  // (ba_setup_host.hip, bitwise the same arrays), where the device setup is
+  // launch-bound; larger ones upload the caller's arrays and lay out on the
+  // device (ba_setup.hip).  SFM_HOST_SETUP=0/1 forces either.
+  const bool host_setup = use_host_setup(N, C);
+  std::vector<int32_t> cam_cnt(size_t(C) + 4), pt_cnt;
+  uint8_t* stg = nullptr;
   double* in_uv = nullptr;
-  int32_t *in_cam = nullptr, *in_pt = nullptr, *err = nullptr, *cnt_c = nullptr, *cnt_p = nullptr;
-  TMP(in_uv, 2 * size_t(N));
-  TMP(in_cam, size_t(N));
-  TMP(in_pt, size_t(N));
-  TMP(err, 4);
-  TMP(cnt_c, size_t(C) + 1);
-  TMP(cnt_p, size_t(P) + 1);
-  if (N) {
-    HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
-    HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
-    HCHK(hipMemcpyAsync(in_pt, pt_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
+  int32_t *in_cam = nullptr, *in_pt = nullptr, *cnt_p = nullptr;
+  if (host_setup) {
+    int32_t e3[3];
+    host_validate(N, obs_uv, cam_idx, pt_idx, C, P, e3, cam_cnt.data() + 4, pt_cnt);
+    cam_cnt[0] = e3[0];
+    cam_cnt[1] = e3[1];
+    cam_cnt[2] = e3[2];
+    timer.mark("validate (host)");
+  } else {
+    // ---- the caller's observation arrays go up as they are (packed into the
+    // pinned stage: one DMA); the O(N) layout work runs on the device
+    // (ba_setup.hip) ----
+    StageLayout up;
+    const size_t o_uv = up.add(sizeof(double) * 2 * size_t(N)), o_cam = up.add(sizeof(int32_t) * size_t(N)),
+                 o_pt = up.add(sizeof(int32_t) * size_t(N));
+    const size_t in_bytes = up.bytes;
+    if ((rc = stage_reserve(h, std::max(in_bytes, sizeof(int32_t) * (size_t(C) + 4))))) return bail(rc);
+    stg = h->stage;
+    uint8_t* in_blob = nullptr;
+    TMP(in_blob, in_bytes);
+    in_uv = reinterpret_cast<double*>(in_blob + o_uv);
+    in_cam = reinterpret_cast<int32_t*>(in_blob + o_cam);
+    in_pt = reinterpret_cast<int32_t*>(in_blob + o_pt);
+    int32_t* err = nullptr;
+    TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
+    int32_t* cnt_c = err + 4;
+    TMP(cnt_p, size_t(P) + 1);
+    if (N) {
+      std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
+      std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
+      std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
+      HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
+    }
+    {
+      Fill32Set fs;
+      fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
+      fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
+      fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
+      launch_fill32(fs, s);
+    }
+    launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+    // one round trip: the first bad observation and the per-camera counts
+    // (the host lays out the C camera runs and the wavefront chunk table);
+    // the readback lands in the stage after the upload has read it (stream order)
+    HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
+    HCHK(hipStreamSynchronize(s));
+    std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
+    timer.mark("upload + validate");
   }
-  {
-    Fill32Set fs;
-    fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
-    fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
-    fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
-    launch_fill32(fs, s);
-  }
-  launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
-  // one round trip: the first bad observation and the per-camera counts
-  // (the host lays out the C camera runs and the wavefront chunk table)
-  std::vector<int32_t> cam_cnt(size_t(C) + 4);
-  HCHK(hipMemcpyAsync(cam_cnt.data(), err, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, s));
-  if (C) HCHK(hipMemcpyAsync(cam_cnt.data() + 4, cnt_c, sizeof(int32_t) * size_t(C), hipMemcpyDeviceToHost, s));
-  HCHK(hipStreamSynchronize(s));
-  timer.mark("upload + validate");
   {
     const int32_t e0 = cam_cnt[0], e1 = cam_cnt[1], e2 = cam_cnt[2];
     const int32_t first = std::min({e0, e1, e2});
@@ -881,71 +1078,94 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   }
   timer.mark("camera runs (host)");
   // ---- resident arrays of the point-major and camera-major layouts ----
-  ALLOC(d.pt_off, size_t(P) + 1);
-  ALLOC(d.order, size_t(N));
-  ALLOC(d.uv_pm, 2 * size_t(N));
-  ALLOC(d.cam_pm, size_t(N));
-  ALLOC(d.cam_obs, size_t(npad));
-  ALLOC(d.cam_rng, 2 * size_t(C));
-  ALLOC(d.cm_p, size_t(npad));
-  ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
-  ALLOC(d.jgrp, size_t(9));
-  ALLOC(d.uv_cm, 2 * size_t(npad));
-  ALLOC(d.pos, size_t(N));
-  ALLOC(d.wcam, wcam.size());
-  // scratch of the sorts
-  uint64_t *k64a = nullptr, *k64b = nullptr;
-  uint32_t *k32a = nullptr, *k32b = nullptr;
-  int32_t *iota = nullptr, *pt_s = nullptr, *cm_order = nullptr, *d_cam_off = nullptr, *perm = nullptr;
-  int4* ch_in = nullptr;
-  void* sort_tmp = nullptr;
-  const int64_t nch = d.n_jchunks;
-  const int64_t nmax = std::max<int64_t>({N, nch, 1});
-  TMP(k64a, size_t(N));
-  TMP(k64b, size_t(N));
-  TMP(k32a, size_t(nmax));
-  TMP(k32b, size_t(nmax));
-  TMP(iota, size_t(nmax));
-  TMP(pt_s, size_t(N));
-  TMP(cm_order, size_t(N));
-  TMP(d_cam_off, size_t(C) + 1);
-  TMP(perm, size_t(std::max<int64_t>(1, nch)));
-  TMP(ch_in, size_t(std::max<int64_t>(1, nch)));
-  size_t sort_bytes = std::max({setup_sort_bytes(N, 64), setup_sort_bytes(nmax, 32), setup_sort_bytes(P + 1, 1),
-                                setup_sort_bytes(N + 1, 2), size_t(256)});
-  {
-    uint8_t* tb = nullptr;
-    TMP(tb, sort_bytes);
-    sort_tmp = tb;
-  }
-  HCHK(hipMemcpyAsync(d.cam_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size(), hipMemcpyHostToDevice, s));
-  HCHK(hipMemcpyAsync(d_cam_off, cam_off.data(), sizeof(int32_t) * cam_off.size(), hipMemcpyHostToDevice, s));
-  HCHK(hipMemcpyAsync(d.wcam, wcam.data(), sizeof(int32_t) * wcam.size(), hipMemcpyHostToDevice, s));
-  if (nch) HCHK(hipMemcpyAsync(ch_in, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice, s));
-  // point-major order: stable sort by (point, camera)
-  launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
-  HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
-                    uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
-  launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
-  HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
-  // camera-major order of the point-major ids: stable sort by camera
-  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
-  launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
-  // chunk table grouped by point slice (stable: camera-major order kept)
-  launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
-  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
-  launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
-  // Schur pair counts: the second (and last) round trip
-  int64_t* pcnt = nullptr;
-  int64_t* poff = nullptr;
-  TMP(pcnt, size_t(N) + 1);
-  TMP(poff, size_t(N) + 1);
-  launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
-  HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
   int64_t n_pairs = 0;
-  HCHK(hipMemcpyAsync(&n_pairs, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  HCHK(hipStreamSynchronize(s));
-  timer.mark("layouts (device)");
+  int32_t *pt_s = nullptr, *cm_order = nullptr;
+  int64_t* poff = nullptr;
+  void* sort_tmp = nullptr;
+  size_t sort_bytes = 0;
+  HostOrders ho;
+  if (host_setup) {
+    n_pairs = host_orders(N, cam_idx, pt_idx, C, P, pt_cnt, cam_off, ho);
+    timer.mark("orders (host)");
+  } else {
+    ALLOC(d.pt_off, size_t(P) + 1);
+    ALLOC(d.order, size_t(N));
+    ALLOC(d.uv_pm, 2 * size_t(N));
+    ALLOC(d.cam_pm, size_t(N));
+    ALLOC(d.cam_obs, size_t(npad));
+    ALLOC(d.cm_p, size_t(npad));
+    ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
+    ALLOC(d.jgrp, size_t(9));
+    ALLOC(d.uv_cm, 2 * size_t(npad));
+    ALLOC(d.pos, size_t(N));
+    // scratch of the sorts
+    uint64_t *k64a = nullptr, *k64b = nullptr;
+    uint32_t *k32a = nullptr, *k32b = nullptr;
+    int32_t *iota = nullptr, *d_cam_off = nullptr, *perm = nullptr;
+    int4* ch_in = nullptr;
+    const int64_t nch = d.n_jchunks;
+    const int64_t nmax = std::max<int64_t>({N, nch, 1});
+    TMP(k64a, size_t(N));
+    TMP(k64b, size_t(N));
+    TMP(k32a, size_t(nmax));
+    TMP(k32b, size_t(nmax));
+    TMP(iota, size_t(nmax));
+    TMP(pt_s, size_t(N));
+    TMP(cm_order, size_t(N));
+    TMP(perm, size_t(std::max<int64_t>(1, nch)));
+    sort_bytes = std::max({setup_sort_bytes(N, 64), setup_sort_bytes(nmax, 32), setup_sort_bytes(P + 1, 1),
+                                  setup_sort_bytes(N + 1, 2), size_t(256)});
+    {
+      uint8_t* tb = nullptr;
+      TMP(tb, sort_bytes);
+      sort_tmp = tb;
+    }
+    {
+      // the host-made camera runs and chunk table in one resident blob, one
+      // DMA from the stage (the validation readback was consumed above):
+      // cam_rng | wcam (resident), cam_off | chunks (read by the setup only)
+      StageLayout il;
+      const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
+                   o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
+      if ((rc = stage_reserve(h, il.bytes))) return bail(rc);
+      stg = h->stage;
+      uint8_t* ib = nullptr;
+      ALLOC(ib, il.bytes);
+      std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
+      std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
+      std::memcpy(stg + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
+      if (nch) std::memcpy(stg + o_ch, chunks.data(), sizeof(int4) * chunks.size());
+      HCHK(hipMemcpyAsync(ib, stg, il.bytes, hipMemcpyHostToDevice, s));
+      d.cam_rng = reinterpret_cast<int32_t*>(ib + o_rng);
+      d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
+      d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
+      ch_in = reinterpret_cast<int4*>(ib + o_ch);
+    }
+    // point-major order: stable sort by (point, camera)
+    launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
+    HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
+                      uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
+    launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
+    HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
+    // camera-major order of the point-major ids: stable sort by camera
+    HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
+    launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
+    // chunk table grouped by point slice (stable: camera-major order kept)
+    launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
+    HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
+    launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
+    // Schur pair counts: the second (and last) round trip
+    int64_t* pcnt = nullptr;
+    TMP(pcnt, size_t(N) + 1);
+    TMP(poff, size_t(N) + 1);
+    launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
+    HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
+    // (into the stage: stream order puts it after the upload that reads the stage)
+    HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HCHK(hipStreamSynchronize(s));
+    std::memcpy(&n_pairs, stg, sizeof(int64_t));
+    timer.mark("layouts (device)");
+  }
   if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
   d.n_blk = int64_t(C) * (C + 1) / 2;
   d.n_pairs = n_pairs;
@@ -972,55 +1192,106 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // the pinned mirror's 16-slot tail: the k_schur_pts group sizes
   int64_t* grp_host = reinterpret_cast<int64_t*>(d.scal_host + kNumScalars + 1);
   int bperm_per = 0;
-  ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
-  ALLOC(d.seg, size_t(d.n_blk) + 1);
-  ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
-  {
-    uint32_t *bk_a = nullptr, *bk_b = nullptr;
-    int32_t* bv = nullptr;
-    const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});
-    TMP(bk_a, size_t(nk));
-    TMP(bk_b, size_t(nk));
-    TMP(bv, size_t(nk));
-    const size_t need = std::max(setup_sort_bytes(n_pairs, 32), setup_sort_bytes(d.n_blk, 32));
-    if (need > sort_bytes) {
-      uint8_t* tb = nullptr;
-      TMP(tb, need);
-      sort_tmp = tb;
-      sort_bytes = need;
-    }
-    launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
-    HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
-                      s));
-    launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
-    launch_blk(C, d.blk, s);
-    // ---- k_schur_pts work order: XCD-aware (ba_setup.hip k_bperm_*).
-    // Block (c1, c2)'s pairs gather records of points camera c1 sees, so a
-    // row c1 (its blocks c2 >= c1) reads one camera's ~N/C point records
-    // (C3: ~0.5 MB).  Rows go to 8 groups of contiguous rows with equal pair
-    // totals; group x's blocks, row by row (descending pair count within a
-    // row, so a wave's blocks run lists of nearly equal length), fill
-    // workgroups x, x + 8, x + 16, ... -- the ones dealt to one XCD
-    // (round-robin placement: a speed assumption only, MI355X_MICROARCH.md),
-    // so a row's records stay in that XCD's L2 while its blocks run.  Slots
-    // past a group's end hold -1 (an empty list).  Small reduced systems
-    // (keyframe-sized solves: everything fits one L2) keep the plain block
-    // order (bperm = nullptr).  The group sizes come back with the final
-    // synchronisation of set_problem.
-    d.bperm = nullptr;
+  // intrinsics, the parameters and their reset copies: one blob, one DMA
+  // (after the layouts in the stage on the host path: no synchronisation
+  // sits between the two uploads there)
+  StageLayout pl;
+  const size_t o_K = pl.add(sizeof(double) * 5 * size_t(C)), o_c = pl.add(sizeof(double) * 6 * size_t(C)),
+               o_c0 = pl.add(sizeof(double) * 6 * size_t(C)), o_X = pl.add(sizeof(double) * 3 * size_t(P)),
+               o_X0 = pl.add(sizeof(double) * 3 * size_t(P));
+  size_t pl_base = 0;
+  if (host_setup) {
+    // every layout array in one resident blob, written on the host straight
+    // into the pinned stage and uploaded in one DMA
+    StageLayout hl;
+    const size_t o_rng = hl.add(sizeof(int32_t) * cam_rng.size()), o_w = hl.add(sizeof(int32_t) * wcam.size()),
+                 o_ptoff = hl.add(sizeof(int32_t) * (size_t(P) + 1)), o_ord = hl.add(sizeof(int32_t) * size_t(N)),
+                 o_uvpm = hl.add(sizeof(double) * 2 * size_t(N)), o_campm = hl.add(sizeof(int32_t) * size_t(N)),
+                 o_cobs = hl.add(sizeof(int32_t) * size_t(npad)), o_cmp = hl.add(sizeof(int32_t) * size_t(npad)),
+                 o_ch = hl.add(sizeof(int4) * size_t(std::max(1, d.n_jchunks))), o_grp = hl.add(sizeof(int32_t) * 9),
+                 o_uvcm = hl.add(sizeof(double) * 2 * size_t(npad)), o_pos = hl.add(sizeof(int32_t) * size_t(N)),
+                 o_blk = hl.add(sizeof(int2) * size_t(std::max<int64_t>(1, d.n_blk))),
+                 o_seg = hl.add(sizeof(int32_t) * (size_t(d.n_blk) + 1)),
+                 o_bpts = hl.add(sizeof(int32_t) * size_t(std::max<int64_t>(1, n_pairs)));
+    pl_base = hl.bytes;
+    if ((rc = stage_reserve(h, hl.bytes + pl.bytes))) return bail(rc);
+    stg = h->stage;
+    uint8_t* hb = nullptr;
+    ALLOC(hb, hl.bytes);
+    std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
+    std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
+    HostLayoutOut out;
+    auto i32 = [&](size_t o) { return reinterpret_cast<int32_t*>(stg + o); };
+    out.pt_off = i32(o_ptoff); out.order = i32(o_ord); out.cam_pm = i32(o_campm); out.cam_obs = i32(o_cobs);
+    out.cm_p = i32(o_cmp); out.pos = i32(o_pos); out.jgrp = i32(o_grp); out.seg = i32(o_seg); out.bpts = i32(o_bpts);
+    out.uv_pm = reinterpret_cast<double*>(stg + o_uvpm);
+    out.uv_cm = reinterpret_cast<double*>(stg + o_uvcm);
+    out.jchunks = reinterpret_cast<int4*>(stg + o_ch);
+    out.blk = reinterpret_cast<int2*>(stg + o_blk);
+    host_fill(N, obs_uv, C, P, ho, cam_off, cam_rng, wcam, npad, chunks, n_pairs, out);
+    HCHK(hipMemcpyAsync(hb, stg, hl.bytes, hipMemcpyHostToDevice, s));
+    auto d32 = [&](size_t o) { return reinterpret_cast<int32_t*>(hb + o); };
+    d.cam_rng = d32(o_rng); d.wcam = d32(o_w); d.pt_off = d32(o_ptoff); d.order = d32(o_ord); d.cam_pm = d32(o_campm);
+    d.cam_obs = d32(o_cobs); d.cm_p = d32(o_cmp); d.pos = d32(o_pos); d.jgrp = d32(o_grp); d.seg = d32(o_seg);
+    d.bpts = d32(o_bpts);
+    d.uv_pm = reinterpret_cast<double*>(hb + o_uvpm);
+    d.uv_cm = reinterpret_cast<double*>(hb + o_uvcm);
+    d.jchunks = reinterpret_cast<int4*>(hb + o_ch);
+    d.blk = reinterpret_cast<int2*>(hb + o_blk);
+    d.bperm = nullptr;  // (use_host_setup: n_blk <= kSchurXcdMinBlocks, the plain block order)
     d.n_bslots = d.n_blk;
-    if (d.n_blk > kSchurXcdMinBlocks) {
-      const int per = 64 / d.schur_pts_sub * (kThreads / 64);
-      int32_t *sorted = nullptr, *row_x = nullptr;
-      int64_t* grp = nullptr;
-      TMP(sorted, size_t(d.n_blk));
-      TMP(row_x, size_t(C));
-      TMP(grp, 16);
-      ALLOC(d.bperm, size_t(bperm_slots_bound(d.n_blk, per)));
-      HCHK(launch_bperm(C, d.n_blk, n_pairs, d.seg, d.blk, per, bk_a, bk_b, bv, sorted, row_x, grp, sort_tmp,
-                        sort_bytes, d.bperm, s));
-      HCHK(hipMemcpyAsync(grp_host, grp, sizeof(int64_t) * 16, hipMemcpyDeviceToHost, s));
-      bperm_per = per;
+    timer.mark("layout (host) + upload");
+  } else {
+    ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
+    ALLOC(d.seg, size_t(d.n_blk) + 1);
+    ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
+    {
+      uint32_t *bk_a = nullptr, *bk_b = nullptr;
+      int32_t* bv = nullptr;
+      const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});
+      TMP(bk_a, size_t(nk));
+      TMP(bk_b, size_t(nk));
+      TMP(bv, size_t(nk));
+      const size_t need = std::max(setup_sort_bytes(n_pairs, 32), setup_sort_bytes(d.n_blk, 32));
+      if (need > sort_bytes) {
+        uint8_t* tb = nullptr;
+        TMP(tb, need);
+        sort_tmp = tb;
+        sort_bytes = need;
+      }
+      launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
+      HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
+                        s));
+      launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
+      launch_blk(C, d.blk, s);
+      // ---- k_schur_pts work order: XCD-aware (ba_setup.hip k_bperm_*).
+      // Block (c1, c2)'s pairs gather records of points camera c1 sees, so a
+      // row c1 (its blocks c2 >= c1) reads one camera's ~N/C point records
+      // (C3: ~0.5 MB).  Rows go to 8 groups of contiguous rows with equal pair
+      // totals; group x's blocks, row by row (descending pair count within a
+      // row, so a wave's blocks run lists of nearly equal length), fill
+      // workgroups x, x + 8, x + 16, ... -- the ones dealt to one XCD
+      // (round-robin placement: a speed assumption only, MI355X_MICROARCH.md),
+      // so a row's records stay in that XCD's L2 while its blocks run.  Slots
+      // past a group's end hold -1 (an empty list).  Small reduced systems
+      // (keyframe-sized solves: everything fits one L2) keep the plain block
+      // order (bperm = nullptr).  The group sizes come back with the final
+      // synchronisation of set_problem.
+      d.bperm = nullptr;
+      d.n_bslots = d.n_blk;
+      if (d.n_blk > kSchurXcdMinBlocks) {
+        const int per = 64 / d.schur_pts_sub * (kThreads / 64);
+        int32_t *sorted = nullptr, *row_x = nullptr;
+        int64_t* grp = nullptr;
+        TMP(sorted, size_t(d.n_blk));
+        TMP(row_x, size_t(C));
+        TMP(grp, 16);
+        ALLOC(d.bperm, size_t(bperm_slots_bound(d.n_blk, per)));
+        HCHK(launch_bperm(C, d.n_blk, n_pairs, d.seg, d.blk, per, bk_a, bk_b, bv, sorted, row_x, grp, sort_tmp,
+                          sort_bytes, d.bperm, s));
+        HCHK(hipMemcpyAsync(grp_host, grp, sizeof(int64_t) * 16, hipMemcpyDeviceToHost, s));
+        bperm_per = per;
+      }
     }
   }
   // ---- parameters, per-iteration arrays, dense system ----
@@ -1029,13 +1300,17 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.nblk = d.ld / kNB;
   d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
                            d.jac_blocks_rec, blocks_for(npad, 256)});
-  ALLOC(d.Kc, 5 * size_t(C));
-  ALLOC(d.cam, 6 * size_t(C));
+  {
+    uint8_t* pb = nullptr;
+    ALLOC(pb, pl.bytes);
+    d.Kc = reinterpret_cast<double*>(pb + o_K);
+    d.cam = reinterpret_cast<double*>(pb + o_c);
+    d.cam0 = reinterpret_cast<double*>(pb + o_c0);
+    d.X = reinterpret_cast<double*>(pb + o_X);
+    d.X0 = reinterpret_cast<double*>(pb + o_X0);
+  }
   ALLOC(d.cam_new, 6 * size_t(C));
-  ALLOC(d.cam0, 6 * size_t(C));
-  ALLOC(d.X, 3 * size_t(P));
   ALLOC(d.X_new, 3 * size_t(P));
-  ALLOC(d.X0, 3 * size_t(P));
   ALLOC(d.scale_c, 6 * size_t(C));
   ALLOC(d.scale_p, 3 * size_t(P));
   ALLOC(d.diag_c, 6 * size_t(C));
@@ -1071,14 +1346,19 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
 #undef ALLOC
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
-  if (C) {
-    HCHK(hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, s));
-    HCHK(hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, s));
-    HCHK(hipMemcpyAsync(d.cam0, d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToDevice, s));
-  }
-  if (P) {
-    HCHK(hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, s));
-    HCHK(hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, s));
+  if (C || P) {
+    // device path: the stage is free (the n_pairs readback synchronised the
+    // stream); host path: after the layouts, room reserved with them
+    if (!host_setup && (rc = stage_reserve(h, pl.bytes))) return bail(rc);
+    uint8_t* ps = h->stage + pl_base;
+    std::memcpy(ps + o_K, Kc.data(), sizeof(double) * Kc.size());
+    std::memcpy(ps + o_c, cam.data(), sizeof(double) * cam.size());
+    std::memcpy(ps + o_c0, cam.data(), sizeof(double) * cam.size());
+    if (P) {
+      std::memcpy(ps + o_X, X, sizeof(double) * 3 * size_t(P));
+      std::memcpy(ps + o_X0, X, sizeof(double) * 3 * size_t(P));
+    }
+    HCHK(hipMemcpyAsync(d.Kc, ps, pl.bytes, hipMemcpyHostToDevice, s));
   }
   {
     // the walker stores only the lower 16x16 blocks of each W_k (k_chol_fused)
@@ -1093,7 +1373,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   }
   h->chol_epoch = 0;
   h->bs_epoch = 0;
-  d.n_cu = device_cus(h->device);
+  d.n_cu = h->n_cu;
   HCHK(hipStreamSynchronize(s));
   if (bperm_per) {
     int64_t m_max = 1;
@@ -1102,7 +1382,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   }
 #undef HCHK
   retire_tmps(h);
-  timer.mark("pair lists + uploads (device)");
+  timer.mark(host_setup ? "uploads" : "pair lists + uploads (device)");
   h->has_problem = true;
   return 0;
 }
@@ -1119,10 +1399,17 @@ int sfm_ba_get_parameters(sfm_ba_handle* h, double* rot, double* t, double* X) {
   if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
   HIPCHK(hipSetDevice(h->device));
   const DevProblem& d = h->d;
-  std::vector<double> cam(6 * size_t(d.C));
-  if (d.C) HIPCHK(hipMemcpyAsync(cam.data(), d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToHost, h->stream));
-  if (X && d.P) HIPCHK(hipMemcpyAsync(X, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToHost, h->stream));
+  // both arrays through the pinned stage (the stream is drained first: the
+  // stage may be regrown, and nothing in flight may still use it)
   HIPCHK(hipStreamSynchronize(h->stream));
+  StageLayout gl;
+  const size_t o_c = gl.add(sizeof(double) * 6 * size_t(d.C)), o_X = gl.add(sizeof(double) * 3 * size_t(d.P));
+  if (int rc = stage_reserve(h, gl.bytes)) return rc;
+  const double* cam = reinterpret_cast<const double*>(h->stage + o_c);
+  if (d.C) HIPCHK(hipMemcpyAsync(h->stage + o_c, d.cam, sizeof(double) * 6 * size_t(d.C), hipMemcpyDeviceToHost, h->stream));
+  if (X && d.P) HIPCHK(hipMemcpyAsync(h->stage + o_X, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (X && d.P) std::memcpy(X, h->stage + o_X, sizeof(double) * 3 * size_t(d.P));
   for (int c = 0; c < d.C; ++c)
     for (int j = 0; j < 3; ++j) {
       if (rot) rot[3 * c + j] = cam[6 * c + j];
@@ -1191,6 +1478,28 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   if (mode == SFM_BA_STRUCT_ONLY && d.C) HIPCHK(hipMemsetAsync(d.scale_c, 0, sizeof(double) * 6 * d.C, h->stream));
   if (mode == SFM_BA_POSE_ONLY && d.P) HIPCHK(hipMemsetAsync(d.scale_p, 0, sizeof(double) * 3 * d.P, h->stream));
   double* sc = d.scal_host;
+  if (!h->host_fn && !env_flag("SFM_HOST_LM")) {
+    // the same loop with its decisions on the device (k_lm_init /
+    // k_lm_decide / k_lm_post): the initial evaluation and the iterations
+    // are enqueued in batches, one host synchronisation per batch instead
+    // of two per iteration.  With an RCCL communicator the all-reduces are
+    // enqueued on the same stream and every rank decides from the same
+    // reduced scalars; only the host-callback collective (tests) needs the
+    // host loop.
+    double cost = 0.0;
+    bool nonfinite = false;
+    const double tl0 = now_s();
+    rc = run_device_lm(h, opts, &cost, &sm, push, &nonfinite);
+    if (rc) {
+      if (nonfinite && summary) *summary = sm;
+      return rc;
+    }
+    sm.linear_solver_time_s += now_s() - tl0;
+    sm.final_cost = cost;
+    sm.wall_time_s = now_s();
+    if (summary) *summary = sm;
+    return 0;
+  }
   double tj = now_s();
   if ((rc = evaluate(h, true, opts.jacobi_scaling != 0))) return rc;
   sm.jacobian_time_s += now_s() - tj;
@@ -1218,16 +1527,6 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   }
   if (grad_max <= opts.gradient_tolerance) {
     sm.termination_type = SFM_CONVERGENCE;
-  } else if (!h->host_fn && !env_flag("SFM_HOST_LM")) {
-    // the same loop with its decisions on the device (k_lm_decide /
-    // k_lm_post): iterations are enqueued in batches, one host
-    // synchronisation per batch instead of two per iteration.  With an RCCL
-    // communicator the all-reduces are enqueued on the same stream and every
-    // rank decides from the same reduced scalars; only the host-callback
-    // collective (tests) needs the host loop.
-    const double tl0 = now_s();
-    if ((rc = run_device_lm(h, opts, &cost, grad_max, x_norm, &sm, push))) return rc;
-    sm.linear_solver_time_s += now_s() - tl0;
   } else {
     double radius = opts.initial_trust_region_radius;
     double decrease_factor = 2.0;

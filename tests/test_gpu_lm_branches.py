@@ -198,20 +198,27 @@ def test_device_loop_equals_host_loop(name, monkeypatch):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("max_iter", [1, 2, 7])
-def test_device_loop_batches_and_iteration_cap(max_iter, monkeypatch):
-    """The device-driven loop with batch sizes 1, 2 and 5 and a small
-    iteration cap (NO_CONVERGENCE inside or at the end of a batch) against
+@pytest.mark.parametrize("max_iter,gtol", [(0, None), (1, None), (2, None), (7, None), (7, 1e30)])
+def test_device_loop_batches_and_iteration_cap(max_iter, gtol, monkeypatch):
+    """The device-driven loop with batch sizes 1, 2 and 5, with its
+    bookkeeping fused into the phase reductions (default) and as separate
+    launches (SFM_LM_UNFUSED), and a small iteration cap (NO_CONVERGENCE
+    at the initial evaluation, inside or at the end of a batch) or a
+    gradient tolerance met by the initial evaluation (k_lm_init) against
     the host-driven loop: identical traces, counts and parameters."""
     name = sorted(n for n in FIX if not n.startswith("gauge"))[0]
     c = FIX[name]
     build, _, mode = L.cases()[name]
     s = build()
     opts = dict(c["options"], max_num_iterations=max_iter)
+    if gtol is not None:
+        opts["gradient_tolerance"] = gtol
     ref = None
-    for env in ({"SFM_HOST_LM": "1"}, {"SFM_LM_BATCH": "1"}, {"SFM_LM_BATCH": "2"}, {"SFM_LM_BATCH": "5"}):
+    for env in ({"SFM_HOST_LM": "1"}, {"SFM_LM_BATCH": "1"}, {"SFM_LM_BATCH": "2"}, {"SFM_LM_BATCH": "5"},
+                {"SFM_LM_UNFUSED": "1"}, {}):
         monkeypatch.delenv("SFM_HOST_LM", raising=False)
         monkeypatch.delenv("SFM_LM_BATCH", raising=False)
+        monkeypatch.delenv("SFM_LM_UNFUSED", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         r, t, X = s.copy_params()
