@@ -793,6 +793,25 @@ struct BriskWork {
     }
     return e.first;
   }
+  // pinned host staging (the frame upload and the one packed download): a
+  // pageable copy goes through the runtime's own staging at a few GB/s
+  void* host = nullptr;
+  size_t host_cap = 0;
+  void* pinned(size_t bytes, int* rc) {
+    if (host_cap < bytes) {
+      const size_t cap = std::max(bytes, 2 * host_cap);
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      host_cap = 0;
+      if (hipHostMalloc(&host, cap) != hipSuccess) {
+        host = nullptr;
+        *rc = bfail(SFM_ENOMEM, "hipHostMalloc failed (detector staging)");
+        return nullptr;
+      }
+      host_cap = cap;
+    }
+    return host;
+  }
 };
 BriskWork* work_for(int device) {
   static std::vector<BriskWork*> w(64, nullptr);
@@ -905,9 +924,16 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
   auto* cand = static_cast<Cand*>(W->get(2, sizeof(Cand) * size_t(cap_c), &rc));
   auto* cnt = static_cast<int32_t*>(W->get(3, sizeof(int32_t), &rc));
   if (rc) return rc;
-  if (hipMemcpy(limg, img, size_t(w) * h, img_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice) !=
-      hipSuccess)
-    return bfail(SFM_EIO, "frame copy failed");
+  if (img_on_device) {
+    if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyDeviceToDevice) != hipSuccess)
+      return bfail(SFM_EIO, "frame copy failed");
+  } else {
+    auto* st = static_cast<uint8_t*>(W->pinned(size_t(w) * h, &rc));
+    if (rc) return rc;
+    std::memcpy(st, img, size_t(w) * h);
+    if (hipMemcpy(limg, st, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess)
+      return bfail(SFM_EIO, "frame copy failed");
+  }
   for (int i = 1; i < nuse; ++i) {
     if (lw[i] < 1 || lh[i] < 1) continue;
     // resize(INTER_AREA): OpenCV's scales are 1 / (dsize / ssize); exactly 2
@@ -952,10 +978,16 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
   // BRISK's order: layer, then row-major (stable radix sort on the key)
   auto* key = static_cast<unsigned long long*>(W->get(4, sizeof(unsigned long long) * 2 * size_t(n), &rc));
   auto* idx = static_cast<int32_t*>(W->get(5, sizeof(int32_t) * 2 * size_t(n), &rc));
-  auto* kp3 = static_cast<float*>(W->get(6, sizeof(float) * 3 * size_t(n), &rc));
-  auto* resp = static_cast<float*>(W->get(7, sizeof(float) * size_t(n), &rc));
-  auto* lay = static_cast<int32_t*>(W->get(8, sizeof(int32_t) * size_t(n), &rc));
+  // every per-keypoint output in one buffer (descriptors first, 16-B
+  // aligned), downloaded by one copy: desc | kp3 | resp | layer | keep | angle
+  const int n_bytes = desc ? ((P->n_short + 127) / 128) * 16 : 0;
+  const size_t o_kp = size_t(n) * n_bytes, o_resp = o_kp + 12 * size_t(n), o_lay = o_resp + 4 * size_t(n),
+               o_keep = o_lay + 4 * size_t(n), o_ang = o_keep + 4 * size_t(n), out_bytes = o_ang + 4 * size_t(n);
+  auto* ob = static_cast<uint8_t*>(W->get(6, out_bytes, &rc));
   if (rc) return rc;
+  auto* kp3 = reinterpret_cast<float*>(ob + o_kp);
+  auto* resp = reinterpret_cast<float*>(ob + o_resp);
+  auto* lay = reinterpret_cast<int32_t*>(ob + o_lay);
   k_cand_keys<<<(n + 255) / 256, 256>>>(cand, n, key, idx);
   size_t tb = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key + n, idx, idx + n, n, 0, 46);
@@ -964,38 +996,35 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
   if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key + n, idx, idx + n, n, 0, 46) != hipSuccess)
     return bfail(SFM_EIO, "sort failed");
   k_gather_cands<<<(n + 255) / 256, 256>>>(cand, idx + n, n, kp3, resp, lay);
-  std::vector<float> hk(3 * size_t(n)), hr(n);
-  std::vector<int32_t> hl(n), hkeep(n, 1);
-  std::vector<float> hang(n, -1.0f);
-  std::vector<uint8_t> hd;
   if (desc) {
-    const int n_bytes = ((P->n_short + 127) / 128) * 16;
-    auto* keep = static_cast<int32_t*>(W->get(10, sizeof(int32_t) * size_t(n), &rc));
-    auto* ang = static_cast<float*>(W->get(11, sizeof(float) * size_t(n), &rc));
+    auto* keep = reinterpret_cast<int32_t*>(ob + o_keep);
+    auto* ang = reinterpret_cast<float*>(ob + o_ang);
     auto* ii = static_cast<int32_t*>(W->get(12, sizeof(int32_t) * size_t(w + 1) * (h + 1), &rc));
-    auto* dd = static_cast<uint8_t*>(W->get(13, size_t(n) * n_bytes, &rc));
     auto* band = static_cast<int32_t*>(W->get(15, sizeof(int32_t) * integral_band_ints(w, h), &rc));
     if (rc) return rc;
     integral_image(limg, w, h, ii, band);
-    k_brisk_describe<<<n, 64>>>(limg, w, h, ii, *P, kp3, n, keep, ang, dd);
-    hd.resize(size_t(n) * n_bytes);
-    if (hipMemcpy(hkeep.data(), keep, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(hang.data(), ang, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(hd.data(), dd, hd.size(), hipMemcpyDeviceToHost) != hipSuccess)
-      return bfail(SFM_EIO, "download failed");
+    k_brisk_describe<<<n, 64>>>(limg, w, h, ii, *P, kp3, n, keep, ang, ob);
   }
-  if (hipMemcpy(hk.data(), kp3, sizeof(float) * 3 * n, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(hr.data(), resp, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(hl.data(), lay, sizeof(int32_t) * n, hipMemcpyDeviceToHost) != hipSuccess)
+  // one download of the packed outputs (without descriptors: kp3 | resp | layer)
+  const size_t dl_off = desc ? 0 : o_kp, dl_bytes = desc ? out_bytes : o_keep - o_kp;
+  auto* hb = static_cast<uint8_t*>(W->pinned(out_bytes, &rc));
+  if (rc) return rc;
+  if (hipMemcpy(hb + dl_off, ob + dl_off, dl_bytes, hipMemcpyDeviceToHost) != hipSuccess)
     return bfail(SFM_EIO, "download failed");
+  const float* hk = reinterpret_cast<const float*>(hb + o_kp);
+  const float* hr = reinterpret_cast<const float*>(hb + o_resp);
+  const int32_t* hl = reinterpret_cast<const int32_t*>(hb + o_lay);
+  const int32_t* hkeep = desc ? reinterpret_cast<const int32_t*>(hb + o_keep) : nullptr;
+  const float* hang = desc ? reinterpret_cast<const float*>(hb + o_ang) : nullptr;
+  const uint8_t* hd = hb;
   int m = 0;
   for (int k = 0; k < n; ++k) {
-    if (!hkeep[k]) continue;
+    if (hkeep && !hkeep[k]) continue;
     if (m < capacity) {
       float* o = kps + 5 * size_t(m);
-      o[0] = hk[3 * k]; o[1] = hk[3 * k + 1]; o[2] = hk[3 * k + 2]; o[3] = hang[k]; o[4] = hr[k];
+      o[0] = hk[3 * k]; o[1] = hk[3 * k + 1]; o[2] = hk[3 * k + 2]; o[3] = hang ? hang[k] : -1.0f; o[4] = hr[k];
       octave[m] = hl[k];
-      if (desc) std::memcpy(desc + size_t(m) * 64, hd.data() + size_t(k) * 64, 64);
+      if (desc) std::memcpy(desc + size_t(m) * 64, hd + size_t(k) * n_bytes, 64);
     }
     ++m;
   }
