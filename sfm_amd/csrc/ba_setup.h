@@ -4,7 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
-#include <vector>
 
 namespace sfm {
 
@@ -60,26 +59,5 @@ int64_t bperm_slots_bound(int64_t n_blk, int per);
 hipError_t launch_bperm(int C, int64_t n_blk, int64_t n_pairs, const int32_t* seg, const int2* blk, int per,
                         uint32_t* key_a, uint32_t* key_b, int32_t* iota, int32_t* sorted, int32_t* row_x,
                         int64_t* grp, void* sort_tmp, size_t sort_bytes, int32_t* bperm, hipStream_t s);
-
-// ---- host layout path (ba_setup_host.hip): keyframe-sized problems ----
-// The same arrays as the device setup, bitwise, built on the host.
-void host_validate(int64_t N, const double* uv, const int32_t* cam, const int32_t* pt, int C, int P, int32_t err[3],
-                   int32_t* cam_cnt, std::vector<int32_t>& pt_cnt);
-struct HostOrders {
-  std::vector<int32_t> pt_off, order, cam_pm, pt_s, cm_order;
-};
-// point-major and camera-major orders; returns the Schur pair count
-int64_t host_orders(int64_t N, const int32_t* cam, const int32_t* pt, int C, int P, const std::vector<int32_t>& pt_cnt,
-                    const std::vector<int32_t>& cam_off, HostOrders& o);
-// destinations (host memory: the pinned stage) of the resident layout arrays
-struct HostLayoutOut {
-  int32_t *pt_off, *order, *cam_pm, *cam_obs, *cm_p, *pos, *jgrp, *seg, *bpts;
-  double *uv_pm, *uv_cm;
-  int4* jchunks;
-  int2* blk;
-};
-void host_fill(int64_t N, const double* uv, int C, int P, const HostOrders& o, const std::vector<int32_t>& cam_off,
-               const std::vector<int32_t>& cam_rng, const std::vector<int32_t>& wcam, int64_t npad,
-               const std::vector<int4>& chunks, int64_t n_pairs, const HostLayoutOut& out);
 
 }  // namespace sfm

@@ -455,18 +455,6 @@ __global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restri
 // k_schur_pts order (C3: 125k blocks); smaller ones the plain order.
 constexpr int64_t kSchurXcdMinBlocks = 8192;
 
-// Host layout path (ba_setup_host.hip) for keyframe-sized problems: up to
-// kHostSetupMaxObs observations (SFM_HOST_SETUP_MAX_OBS) and few enough
-// camera blocks for the plain k_schur_pts order.  SFM_HOST_SETUP=0 / 1
-// forces the device / host path (the latter within the block bound).
-constexpr int64_t kHostSetupMaxObs = 65536;
-bool use_host_setup(int64_t N, int C) {
-  if (int64_t(C) * (C + 1) / 2 > kSchurXcdMinBlocks) return false;
-  if (const char* e = std::getenv("SFM_HOST_SETUP")) return e[0] == '1';
-  int64_t mx = kHostSetupMaxObs;
-  if (const char* m = std::getenv("SFM_HOST_SETUP_MAX_OBS")) mx = std::atoll(m);
-  return N <= mx;
-}
 
 bool sharded(const sfm_ba_handle* h) { return h->comm != nullptr || h->host_fn != nullptr; }
 
@@ -968,64 +956,49 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     hipError_t e_ = (expr);                                                                       \
     if (e_ != hipSuccess) return bail(fail(SFM_EIO, std::string(#expr) + ": " + hipGetErrorString(e_))); \
   } while (0)
-  // Keyframe-sized problems (the reference's per-keyframe BA: tens of
-  // cameras, a few thousand points) are laid out on the host
-  // (ba_setup_host.hip, bitwise the same arrays), where the device setup is
-  // launch-bound; larger ones upload the caller's arrays and lay out on the
-  // device (ba_setup.hip).  SFM_HOST_SETUP=0/1 forces either.
-  const bool host_setup = use_host_setup(N, C);
-  std::vector<int32_t> cam_cnt(size_t(C) + 4), pt_cnt;
+  std::vector<int32_t> cam_cnt(size_t(C) + 4);
   uint8_t* stg = nullptr;
   double* in_uv = nullptr;
   int32_t *in_cam = nullptr, *in_pt = nullptr, *cnt_p = nullptr;
-  if (host_setup) {
-    int32_t e3[3];
-    host_validate(N, obs_uv, cam_idx, pt_idx, C, P, e3, cam_cnt.data() + 4, pt_cnt);
-    cam_cnt[0] = e3[0];
-    cam_cnt[1] = e3[1];
-    cam_cnt[2] = e3[2];
-    timer.mark("validate (host)");
-  } else {
-    // ---- the caller's observation arrays go up as they are (packed into the
-    // pinned stage: one DMA); the O(N) layout work runs on the device
-    // (ba_setup.hip) ----
-    StageLayout up;
-    const size_t o_uv = up.add(sizeof(double) * 2 * size_t(N)), o_cam = up.add(sizeof(int32_t) * size_t(N)),
-                 o_pt = up.add(sizeof(int32_t) * size_t(N));
-    const size_t in_bytes = up.bytes;
-    if ((rc = stage_reserve(h, std::max(in_bytes, sizeof(int32_t) * (size_t(C) + 4))))) return bail(rc);
-    stg = h->stage;
-    uint8_t* in_blob = nullptr;
-    TMP(in_blob, in_bytes);
-    in_uv = reinterpret_cast<double*>(in_blob + o_uv);
-    in_cam = reinterpret_cast<int32_t*>(in_blob + o_cam);
-    in_pt = reinterpret_cast<int32_t*>(in_blob + o_pt);
-    int32_t* err = nullptr;
-    TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
-    int32_t* cnt_c = err + 4;
-    TMP(cnt_p, size_t(P) + 1);
-    if (N) {
-      std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
-      std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
-      std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
-      HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
-    }
-    {
-      Fill32Set fs;
-      fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
-      fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
-      fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
-      launch_fill32(fs, s);
-    }
-    launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
-    // one round trip: the first bad observation and the per-camera counts
-    // (the host lays out the C camera runs and the wavefront chunk table);
-    // the readback lands in the stage after the upload has read it (stream order)
-    HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
-    HCHK(hipStreamSynchronize(s));
-    std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
-    timer.mark("upload + validate");
+  // ---- the caller's observation arrays go up as they are (packed into the
+  // pinned stage: one DMA); the O(N) layout work runs on the device
+  // (ba_setup.hip) ----
+  StageLayout up;
+  const size_t o_uv = up.add(sizeof(double) * 2 * size_t(N)), o_cam = up.add(sizeof(int32_t) * size_t(N)),
+               o_pt = up.add(sizeof(int32_t) * size_t(N));
+  const size_t in_bytes = up.bytes;
+  if ((rc = stage_reserve(h, std::max(in_bytes, sizeof(int32_t) * (size_t(C) + 4))))) return bail(rc);
+  stg = h->stage;
+  uint8_t* in_blob = nullptr;
+  TMP(in_blob, in_bytes);
+  in_uv = reinterpret_cast<double*>(in_blob + o_uv);
+  in_cam = reinterpret_cast<int32_t*>(in_blob + o_cam);
+  in_pt = reinterpret_cast<int32_t*>(in_blob + o_pt);
+  int32_t* err = nullptr;
+  TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
+  int32_t* cnt_c = err + 4;
+  TMP(cnt_p, size_t(P) + 1);
+  if (N) {
+    std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
+    std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
+    std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
+    HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
   }
+  {
+    Fill32Set fs;
+    fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
+    fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
+    fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
+    launch_fill32(fs, s);
+  }
+  launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+  // one round trip: the first bad observation and the per-camera counts
+  // (the host lays out the C camera runs and the wavefront chunk table);
+  // the readback lands in the stage after the upload has read it (stream order)
+  HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
+  HCHK(hipStreamSynchronize(s));
+  std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
+  timer.mark("upload + validate");
   {
     const int32_t e0 = cam_cnt[0], e1 = cam_cnt[1], e2 = cam_cnt[2];
     const int32_t first = std::min({e0, e1, e2});
@@ -1083,89 +1056,83 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   int64_t* poff = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_bytes = 0;
-  HostOrders ho;
-  if (host_setup) {
-    n_pairs = host_orders(N, cam_idx, pt_idx, C, P, pt_cnt, cam_off, ho);
-    timer.mark("orders (host)");
-  } else {
-    ALLOC(d.pt_off, size_t(P) + 1);
-    ALLOC(d.order, size_t(N));
-    ALLOC(d.uv_pm, 2 * size_t(N));
-    ALLOC(d.cam_pm, size_t(N));
-    ALLOC(d.cam_obs, size_t(npad));
-    ALLOC(d.cm_p, size_t(npad));
-    ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
-    ALLOC(d.jgrp, size_t(9));
-    ALLOC(d.uv_cm, 2 * size_t(npad));
-    ALLOC(d.pos, size_t(N));
-    // scratch of the sorts
-    uint64_t *k64a = nullptr, *k64b = nullptr;
-    uint32_t *k32a = nullptr, *k32b = nullptr;
-    int32_t *iota = nullptr, *d_cam_off = nullptr, *perm = nullptr;
-    int4* ch_in = nullptr;
-    const int64_t nch = d.n_jchunks;
-    const int64_t nmax = std::max<int64_t>({N, nch, 1});
-    TMP(k64a, size_t(N));
-    TMP(k64b, size_t(N));
-    TMP(k32a, size_t(nmax));
-    TMP(k32b, size_t(nmax));
-    TMP(iota, size_t(nmax));
-    TMP(pt_s, size_t(N));
-    TMP(cm_order, size_t(N));
-    TMP(perm, size_t(std::max<int64_t>(1, nch)));
-    sort_bytes = std::max({setup_sort_bytes(N, 64), setup_sort_bytes(nmax, 32), setup_sort_bytes(P + 1, 1),
-                                  setup_sort_bytes(N + 1, 2), size_t(256)});
-    {
-      uint8_t* tb = nullptr;
-      TMP(tb, sort_bytes);
-      sort_tmp = tb;
-    }
-    {
-      // the host-made camera runs and chunk table in one resident blob, one
-      // DMA from the stage (the validation readback was consumed above):
-      // cam_rng | wcam (resident), cam_off | chunks (read by the setup only)
-      StageLayout il;
-      const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
-                   o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
-      if ((rc = stage_reserve(h, il.bytes))) return bail(rc);
-      stg = h->stage;
-      uint8_t* ib = nullptr;
-      ALLOC(ib, il.bytes);
-      std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
-      std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
-      std::memcpy(stg + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
-      if (nch) std::memcpy(stg + o_ch, chunks.data(), sizeof(int4) * chunks.size());
-      HCHK(hipMemcpyAsync(ib, stg, il.bytes, hipMemcpyHostToDevice, s));
-      d.cam_rng = reinterpret_cast<int32_t*>(ib + o_rng);
-      d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
-      d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
-      ch_in = reinterpret_cast<int4*>(ib + o_ch);
-    }
-    // point-major order: stable sort by (point, camera)
-    launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
-    HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
-                      uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
-    launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
-    HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
-    // camera-major order of the point-major ids: stable sort by camera
-    HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
-    launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
-    // chunk table grouped by point slice (stable: camera-major order kept)
-    launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
-    HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
-    launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
-    // Schur pair counts: the second (and last) round trip
-    int64_t* pcnt = nullptr;
-    TMP(pcnt, size_t(N) + 1);
-    TMP(poff, size_t(N) + 1);
-    launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
-    HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
-    // (into the stage: stream order puts it after the upload that reads the stage)
-    HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HCHK(hipStreamSynchronize(s));
-    std::memcpy(&n_pairs, stg, sizeof(int64_t));
-    timer.mark("layouts (device)");
+  ALLOC(d.pt_off, size_t(P) + 1);
+  ALLOC(d.order, size_t(N));
+  ALLOC(d.uv_pm, 2 * size_t(N));
+  ALLOC(d.cam_pm, size_t(N));
+  ALLOC(d.cam_obs, size_t(npad));
+  ALLOC(d.cm_p, size_t(npad));
+  ALLOC(d.jchunks, size_t(std::max(1, d.n_jchunks)));
+  ALLOC(d.jgrp, size_t(9));
+  ALLOC(d.uv_cm, 2 * size_t(npad));
+  ALLOC(d.pos, size_t(N));
+  // scratch of the sorts
+  uint64_t *k64a = nullptr, *k64b = nullptr;
+  uint32_t *k32a = nullptr, *k32b = nullptr;
+  int32_t *iota = nullptr, *d_cam_off = nullptr, *perm = nullptr;
+  int4* ch_in = nullptr;
+  const int64_t nch = d.n_jchunks;
+  const int64_t nmax = std::max<int64_t>({N, nch, 1});
+  TMP(k64a, size_t(N));
+  TMP(k64b, size_t(N));
+  TMP(k32a, size_t(nmax));
+  TMP(k32b, size_t(nmax));
+  TMP(iota, size_t(nmax));
+  TMP(pt_s, size_t(N));
+  TMP(cm_order, size_t(N));
+  TMP(perm, size_t(std::max<int64_t>(1, nch)));
+  sort_bytes = std::max({setup_sort_bytes(N, 64), setup_sort_bytes(nmax, 32), setup_sort_bytes(P + 1, 1),
+                                setup_sort_bytes(N + 1, 2), size_t(256)});
+  {
+    uint8_t* tb = nullptr;
+    TMP(tb, sort_bytes);
+    sort_tmp = tb;
   }
+  {
+    // the host-made camera runs and chunk table in one resident blob, one
+    // DMA from the stage (the validation readback was consumed above):
+    // cam_rng | wcam (resident), cam_off | chunks (read by the setup only)
+    StageLayout il;
+    const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
+                 o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
+    if ((rc = stage_reserve(h, il.bytes))) return bail(rc);
+    stg = h->stage;
+    uint8_t* ib = nullptr;
+    ALLOC(ib, il.bytes);
+    std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
+    std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
+    std::memcpy(stg + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
+    if (nch) std::memcpy(stg + o_ch, chunks.data(), sizeof(int4) * chunks.size());
+    HCHK(hipMemcpyAsync(ib, stg, il.bytes, hipMemcpyHostToDevice, s));
+    d.cam_rng = reinterpret_cast<int32_t*>(ib + o_rng);
+    d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
+    d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
+    ch_in = reinterpret_cast<int4*>(ib + o_ch);
+  }
+  // point-major order: stable sort by (point, camera)
+  launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
+  HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
+                    uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
+  launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
+  HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
+  // camera-major order of the point-major ids: stable sort by camera
+  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
+  launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
+  // chunk table grouped by point slice (stable: camera-major order kept)
+  launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
+  HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
+  launch_chunk_gather(int(nch), perm, ch_in, k32b, d.jchunks, d.jgrp, s);
+  // Schur pair counts: the second (and last) round trip
+  int64_t* pcnt = nullptr;
+  TMP(pcnt, size_t(N) + 1);
+  TMP(poff, size_t(N) + 1);
+  launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
+  HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
+  // (into the stage: stream order puts it after the upload that reads the stage)
+  HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HCHK(hipStreamSynchronize(s));
+  std::memcpy(&n_pairs, stg, sizeof(int64_t));
+  timer.mark("layouts (device)");
   if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
   d.n_blk = int64_t(C) * (C + 1) / 2;
   d.n_pairs = n_pairs;
@@ -1193,105 +1160,59 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   int64_t* grp_host = reinterpret_cast<int64_t*>(d.scal_host + kNumScalars + 1);
   int bperm_per = 0;
   // intrinsics, the parameters and their reset copies: one blob, one DMA
-  // (after the layouts in the stage on the host path: no synchronisation
-  // sits between the two uploads there)
   StageLayout pl;
   const size_t o_K = pl.add(sizeof(double) * 5 * size_t(C)), o_c = pl.add(sizeof(double) * 6 * size_t(C)),
                o_c0 = pl.add(sizeof(double) * 6 * size_t(C)), o_X = pl.add(sizeof(double) * 3 * size_t(P)),
                o_X0 = pl.add(sizeof(double) * 3 * size_t(P));
-  size_t pl_base = 0;
-  if (host_setup) {
-    // every layout array in one resident blob, written on the host straight
-    // into the pinned stage and uploaded in one DMA
-    StageLayout hl;
-    const size_t o_rng = hl.add(sizeof(int32_t) * cam_rng.size()), o_w = hl.add(sizeof(int32_t) * wcam.size()),
-                 o_ptoff = hl.add(sizeof(int32_t) * (size_t(P) + 1)), o_ord = hl.add(sizeof(int32_t) * size_t(N)),
-                 o_uvpm = hl.add(sizeof(double) * 2 * size_t(N)), o_campm = hl.add(sizeof(int32_t) * size_t(N)),
-                 o_cobs = hl.add(sizeof(int32_t) * size_t(npad)), o_cmp = hl.add(sizeof(int32_t) * size_t(npad)),
-                 o_ch = hl.add(sizeof(int4) * size_t(std::max(1, d.n_jchunks))), o_grp = hl.add(sizeof(int32_t) * 9),
-                 o_uvcm = hl.add(sizeof(double) * 2 * size_t(npad)), o_pos = hl.add(sizeof(int32_t) * size_t(N)),
-                 o_blk = hl.add(sizeof(int2) * size_t(std::max<int64_t>(1, d.n_blk))),
-                 o_seg = hl.add(sizeof(int32_t) * (size_t(d.n_blk) + 1)),
-                 o_bpts = hl.add(sizeof(int32_t) * size_t(std::max<int64_t>(1, n_pairs)));
-    pl_base = hl.bytes;
-    if ((rc = stage_reserve(h, hl.bytes + pl.bytes))) return bail(rc);
-    stg = h->stage;
-    uint8_t* hb = nullptr;
-    ALLOC(hb, hl.bytes);
-    std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
-    std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
-    HostLayoutOut out;
-    auto i32 = [&](size_t o) { return reinterpret_cast<int32_t*>(stg + o); };
-    out.pt_off = i32(o_ptoff); out.order = i32(o_ord); out.cam_pm = i32(o_campm); out.cam_obs = i32(o_cobs);
-    out.cm_p = i32(o_cmp); out.pos = i32(o_pos); out.jgrp = i32(o_grp); out.seg = i32(o_seg); out.bpts = i32(o_bpts);
-    out.uv_pm = reinterpret_cast<double*>(stg + o_uvpm);
-    out.uv_cm = reinterpret_cast<double*>(stg + o_uvcm);
-    out.jchunks = reinterpret_cast<int4*>(stg + o_ch);
-    out.blk = reinterpret_cast<int2*>(stg + o_blk);
-    host_fill(N, obs_uv, C, P, ho, cam_off, cam_rng, wcam, npad, chunks, n_pairs, out);
-    HCHK(hipMemcpyAsync(hb, stg, hl.bytes, hipMemcpyHostToDevice, s));
-    auto d32 = [&](size_t o) { return reinterpret_cast<int32_t*>(hb + o); };
-    d.cam_rng = d32(o_rng); d.wcam = d32(o_w); d.pt_off = d32(o_ptoff); d.order = d32(o_ord); d.cam_pm = d32(o_campm);
-    d.cam_obs = d32(o_cobs); d.cm_p = d32(o_cmp); d.pos = d32(o_pos); d.jgrp = d32(o_grp); d.seg = d32(o_seg);
-    d.bpts = d32(o_bpts);
-    d.uv_pm = reinterpret_cast<double*>(hb + o_uvpm);
-    d.uv_cm = reinterpret_cast<double*>(hb + o_uvcm);
-    d.jchunks = reinterpret_cast<int4*>(hb + o_ch);
-    d.blk = reinterpret_cast<int2*>(hb + o_blk);
-    d.bperm = nullptr;  // (use_host_setup: n_blk <= kSchurXcdMinBlocks, the plain block order)
+  ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
+  ALLOC(d.seg, size_t(d.n_blk) + 1);
+  ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
+  {
+    uint32_t *bk_a = nullptr, *bk_b = nullptr;
+    int32_t* bv = nullptr;
+    const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});
+    TMP(bk_a, size_t(nk));
+    TMP(bk_b, size_t(nk));
+    TMP(bv, size_t(nk));
+    const size_t need = std::max(setup_sort_bytes(n_pairs, 32), setup_sort_bytes(d.n_blk, 32));
+    if (need > sort_bytes) {
+      uint8_t* tb = nullptr;
+      TMP(tb, need);
+      sort_tmp = tb;
+      sort_bytes = need;
+    }
+    launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
+    HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
+                      s));
+    launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
+    launch_blk(C, d.blk, s);
+    // ---- k_schur_pts work order: XCD-aware (ba_setup.hip k_bperm_*).
+    // Block (c1, c2)'s pairs gather records of points camera c1 sees, so a
+    // row c1 (its blocks c2 >= c1) reads one camera's ~N/C point records
+    // (C3: ~0.5 MB).  Rows go to 8 groups of contiguous rows with equal pair
+    // totals; group x's blocks, row by row (descending pair count within a
+    // row, so a wave's blocks run lists of nearly equal length), fill
+    // workgroups x, x + 8, x + 16, ... -- the ones dealt to one XCD
+    // (round-robin placement: a speed assumption only, MI355X_MICROARCH.md),
+    // so a row's records stay in that XCD's L2 while its blocks run.  Slots
+    // past a group's end hold -1 (an empty list).  Small reduced systems
+    // (keyframe-sized solves: everything fits one L2) keep the plain block
+    // order (bperm = nullptr).  The group sizes come back with the final
+    // synchronisation of set_problem.
+    d.bperm = nullptr;
     d.n_bslots = d.n_blk;
-    timer.mark("layout (host) + upload");
-  } else {
-    ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
-    ALLOC(d.seg, size_t(d.n_blk) + 1);
-    ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
-    {
-      uint32_t *bk_a = nullptr, *bk_b = nullptr;
-      int32_t* bv = nullptr;
-      const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});
-      TMP(bk_a, size_t(nk));
-      TMP(bk_b, size_t(nk));
-      TMP(bv, size_t(nk));
-      const size_t need = std::max(setup_sort_bytes(n_pairs, 32), setup_sort_bytes(d.n_blk, 32));
-      if (need > sort_bytes) {
-        uint8_t* tb = nullptr;
-        TMP(tb, need);
-        sort_tmp = tb;
-        sort_bytes = need;
-      }
-      launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
-      HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
-                        s));
-      launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
-      launch_blk(C, d.blk, s);
-      // ---- k_schur_pts work order: XCD-aware (ba_setup.hip k_bperm_*).
-      // Block (c1, c2)'s pairs gather records of points camera c1 sees, so a
-      // row c1 (its blocks c2 >= c1) reads one camera's ~N/C point records
-      // (C3: ~0.5 MB).  Rows go to 8 groups of contiguous rows with equal pair
-      // totals; group x's blocks, row by row (descending pair count within a
-      // row, so a wave's blocks run lists of nearly equal length), fill
-      // workgroups x, x + 8, x + 16, ... -- the ones dealt to one XCD
-      // (round-robin placement: a speed assumption only, MI355X_MICROARCH.md),
-      // so a row's records stay in that XCD's L2 while its blocks run.  Slots
-      // past a group's end hold -1 (an empty list).  Small reduced systems
-      // (keyframe-sized solves: everything fits one L2) keep the plain block
-      // order (bperm = nullptr).  The group sizes come back with the final
-      // synchronisation of set_problem.
-      d.bperm = nullptr;
-      d.n_bslots = d.n_blk;
-      if (d.n_blk > kSchurXcdMinBlocks) {
-        const int per = 64 / d.schur_pts_sub * (kThreads / 64);
-        int32_t *sorted = nullptr, *row_x = nullptr;
-        int64_t* grp = nullptr;
-        TMP(sorted, size_t(d.n_blk));
-        TMP(row_x, size_t(C));
-        TMP(grp, 16);
-        ALLOC(d.bperm, size_t(bperm_slots_bound(d.n_blk, per)));
-        HCHK(launch_bperm(C, d.n_blk, n_pairs, d.seg, d.blk, per, bk_a, bk_b, bv, sorted, row_x, grp, sort_tmp,
-                          sort_bytes, d.bperm, s));
-        HCHK(hipMemcpyAsync(grp_host, grp, sizeof(int64_t) * 16, hipMemcpyDeviceToHost, s));
-        bperm_per = per;
-      }
+    if (d.n_blk > kSchurXcdMinBlocks) {
+      const int per = 64 / d.schur_pts_sub * (kThreads / 64);
+      int32_t *sorted = nullptr, *row_x = nullptr;
+      int64_t* grp = nullptr;
+      TMP(sorted, size_t(d.n_blk));
+      TMP(row_x, size_t(C));
+      TMP(grp, 16);
+      ALLOC(d.bperm, size_t(bperm_slots_bound(d.n_blk, per)));
+      HCHK(launch_bperm(C, d.n_blk, n_pairs, d.seg, d.blk, per, bk_a, bk_b, bv, sorted, row_x, grp, sort_tmp,
+                        sort_bytes, d.bperm, s));
+      HCHK(hipMemcpyAsync(grp_host, grp, sizeof(int64_t) * 16, hipMemcpyDeviceToHost, s));
+      bperm_per = per;
     }
   }
   // ---- parameters, per-iteration arrays, dense system ----
@@ -1347,10 +1268,9 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
   if (C || P) {
-    // device path: the stage is free (the n_pairs readback synchronised the
-    // stream); host path: after the layouts, room reserved with them
-    if (!host_setup && (rc = stage_reserve(h, pl.bytes))) return bail(rc);
-    uint8_t* ps = h->stage + pl_base;
+    // the stage is free: the n_pairs readback synchronised the stream
+    if ((rc = stage_reserve(h, pl.bytes))) return bail(rc);
+    uint8_t* ps = h->stage;
     std::memcpy(ps + o_K, Kc.data(), sizeof(double) * Kc.size());
     std::memcpy(ps + o_c, cam.data(), sizeof(double) * cam.size());
     std::memcpy(ps + o_c0, cam.data(), sizeof(double) * cam.size());
@@ -1382,7 +1302,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   }
 #undef HCHK
   retire_tmps(h);
-  timer.mark(host_setup ? "uploads" : "pair lists + uploads (device)");
+  timer.mark("pair lists + uploads (device)");
   h->has_problem = true;
   return 0;
 }

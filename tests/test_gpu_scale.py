@@ -155,15 +155,11 @@ def test_one_rank_rccl_communicator_at_c4_is_exact():
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("setup", ["0", "1"])
 @pytest.mark.parametrize("kind", ["cam", "pt", "uv"])
-def test_set_problem_rejects_bad_observations_at_the_first_index(kind, setup, monkeypatch):
-    """The validation of sfm_ba_set_problem -- on the device (ba_setup.hip
-    k_validate, SFM_HOST_SETUP=0) and on the host layout path
-    (ba_setup_host.hip, SFM_HOST_SETUP=1) -- reports the FIRST offending
-    observation, as a host loop in the caller's order would, and leaves no
-    problem behind."""
-    monkeypatch.setenv("SFM_HOST_SETUP", setup)
+def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
+    """The device-side validation of sfm_ba_set_problem (ba_setup.hip
+    k_validate) reports the FIRST offending observation, as a host loop in
+    the caller's order would, and leaves no problem behind."""
     s = scene.config("C1")
     uv, cam, pt = s.uv.copy(), s.cam_idx.copy(), s.pt_idx.copy()
     bad = [1234, 77, 15000]
@@ -204,55 +200,6 @@ def test_device_layout_keeps_caller_order_of_duplicates():
     assert np.max(np.abs(jac - j_o) / scale) < 1e-10
     o, g = _solve_both(s)
     _assert_parity(o, g)
-
-
-def _solve_with_setup(s, setup, monkeypatch, mode=sfm_amd.STRUCT_AND_POSE):
-    monkeypatch.setenv("SFM_HOST_SETUP", setup)
-    with sfm_amd.BundleAdjuster() as ba:
-        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
-        sm, tr = ba.solve(mode=mode)
-        cost, res, jac = ba.evaluate()
-        params = ba.parameters()
-    return sm, tr, params, (cost, res, jac)
-
-
-@pytest.mark.parametrize("case", ["C1", "shuffled_duplicates", "edges", "pose_only"])
-def test_host_setup_equals_device_setup(case, monkeypatch):
-    """The host layout path of set_problem (ba_setup_host.hip, taken by
-    keyframe-sized problems) builds bitwise the device setup's arrays: the
-    same solve (trace, summary, final parameters) and the same evaluate()
-    outputs in the caller's order, bit for bit, on shuffled input with
-    duplicate (point, camera) observations, a camera without observations,
-    single-view points, and in POSE_ONLY."""
-    mode = sfm_amd.STRUCT_AND_POSE
-    if case == "C1":
-        s = scene.config("C1")
-    else:
-        s = scene.generate(14, 600, views=5, seed=31)
-        rng = np.random.default_rng(9)
-        dup = rng.choice(len(s.pt_idx), 60, replace=False)
-        _append_obs(s, s.cam_idx[dup], s.pt_idx[dup], s.uv[dup] + rng.normal(0, 0.3, (60, 2)))
-        if case in ("edges", "pose_only"):
-            keep = ~(np.isin(s.pt_idx, [5, 6]) & (np.arange(len(s.pt_idx)) % 3 != 0))
-            for p in (5, 6):
-                idx = np.nonzero(s.pt_idx == p)[0]
-                keep[idx[0]] = True
-                keep[idx[1:]] = False
-            keep &= s.cam_idx != 13
-            s.uv, s.cam_idx, s.pt_idx = s.uv[keep], s.cam_idx[keep], s.pt_idx[keep]
-        perm = rng.permutation(len(s.pt_idx))
-        s.uv, s.cam_idx, s.pt_idx = s.uv[perm], s.cam_idx[perm], s.pt_idx[perm]
-        if case == "pose_only":
-            mode = sfm_amd.POSE_ONLY
-    a = _solve_with_setup(s, "1", monkeypatch, mode)
-    b = _solve_with_setup(s, "0", monkeypatch, mode)
-    assert a[0].num_iterations == b[0].num_iterations > 0
-    assert a[0].final_cost == b[0].final_cost and a[0].initial_cost == b[0].initial_cost
-    assert a[1] == b[1]
-    for x, y in zip(a[2], b[2]):
-        assert np.array_equal(x, y)
-    assert a[3][0] == b[3][0]
-    assert np.array_equal(a[3][1], b[3][1]) and np.array_equal(a[3][2], b[3][2])
 
 
 def test_one_shot_solves_reuse_the_cached_handle():
