@@ -793,8 +793,8 @@ struct BriskWork {
     }
     return e.first;
   }
-  // pinned host staging (the frame upload and the one packed download): a
-  // pageable copy goes through the runtime's own staging at a few GB/s
+  // pinned host staging of the one packed download (six pageable copies of
+  // the per-keypoint outputs before: BRISK 1.0 -> 0.74 ms per frame)
   void* host = nullptr;
   size_t host_cap = 0;
   void* pinned(size_t bytes, int* rc) {
@@ -927,12 +927,8 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
   if (img_on_device) {
     if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyDeviceToDevice) != hipSuccess)
       return bfail(SFM_EIO, "frame copy failed");
-  } else {
-    auto* st = static_cast<uint8_t*>(W->pinned(size_t(w) * h, &rc));
-    if (rc) return rc;
-    std::memcpy(st, img, size_t(w) * h);
-    if (hipMemcpy(limg, st, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess)
-      return bfail(SFM_EIO, "frame copy failed");
+  } else if (hipMemcpy(limg, img, size_t(w) * h, hipMemcpyHostToDevice) != hipSuccess) {
+    return bfail(SFM_EIO, "frame copy failed");
   }
   for (int i = 1; i < nuse; ++i) {
     if (lw[i] < 1 || lh[i] < 1) continue;
