@@ -42,7 +42,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F64_MFMA_PEAK_TFS = 78.6   # MI355X fp64 matrix spec
 CAMS, PTS_PER_GPU, VIEWS = 500, 200_000, 10
-SEED = 0x5F3D2017 + 3      # config C3
+C4 = (2000, 1_000_000)     # BASELINE config 4 (cams, points)
+SEED = 0x5F3D2017 + 3      # config C3 (sfm_amd.scene.config); C4 is SEED + 1
 
 
 def jacobian_bytes(n_obs: int, n_cams: int, n_pts: int) -> int:
@@ -500,56 +501,51 @@ def matcher_leg(device: int, steps: int, cpu: bool) -> dict:
     return out
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pts-per-gpu", type=int, default=PTS_PER_GPU)
-    ap.add_argument("--cams", type=int, default=CAMS)
-    ap.add_argument("--total-pts", type=int, default=0,
-                    help="strong scaling: this many points in total, split into landmark shards over the ranks "
-                         "(BASELINE config C4: --cams 2000 --total-pts 1000000); default: --pts-per-gpu per rank")
-    ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
-    ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
-    ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
-    ap.add_argument("--comm", action="store_true",
-                    help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
-    args = ap.parse_args()
+def self_launch(argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N
+    ranks through torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) BEFORE anything touches the GPU, as a child process, and exit
+    with its code (never an exec from a process that could have initialised
+    the GPU)."""
+    import socket
+    import subprocess
+    n = None
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            n = int(argv[i + 1])
+        elif a.startswith("--gpus="):
+            n = int(a.split("=", 1)[1])
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
 
+def measure_ba(cams: int, P_total: int, p_begin: int, p_end: int, seed: int, strong: bool, args, world: int,
+               rank: int, local_rank: int, dist, comm: bool) -> dict:
+    """One BA workload: the scene's landmark shard [p_begin, p_end) set up
+    resident, W untimed solves, then K timed solves (device reset + LM to
+    Ceres' termination) between barriers, max over ranks; then a profiled
+    pass of the same solves for the phase times."""
     import torch
-    import torch.distributed as dist
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
     import sfm_amd
     from sfm_amd import scene as S
-
-    strong = args.total_pts > 0
-    if strong:
-        P_total = args.total_pts
-        p_begin, p_end = rank * P_total // world, (rank + 1) * P_total // world
-    else:
-        P_total = args.pts_per_gpu * world
-        p_begin, p_end = rank * args.pts_per_gpu, (rank + 1) * args.pts_per_gpu
-    P = p_end - p_begin
-    sc = S.generate(args.cams, P_total, seed=SEED, p_begin=p_begin, p_end=p_end)
+    sc = S.generate(cams, P_total, seed=seed, p_begin=p_begin, p_end=p_end)
     ba = sfm_amd.BundleAdjuster(device=local_rank)
     if world > 1:
         uid = [sfm_amd.BundleAdjuster.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ba.set_comm(world, rank, uid[0])
-    elif args.comm:
+    elif comm:
         ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+    t0 = time.perf_counter()
     ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
+    ba.sync()
+    setup_s = time.perf_counter() - t0
     opts = sfm_amd.default_options()
 
     def barrier():
@@ -574,6 +570,10 @@ def main() -> int:
         last = sm
     barrier()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     # phase breakdown from a separate pass of the same solves (the HIP events
     # it records stay out of the timed region above).  That pass runs the
     # host-driven LM loop (the same kernels): the device-driven loop also
@@ -591,22 +591,108 @@ def main() -> int:
         del os.environ["SFM_HOST_LM"]
     else:
         os.environ["SFM_HOST_LM"] = prev_host_lm
+    n_obs_total = VIEWS * P_total   # every point has VIEWS observations
+    res_only = evals - jevals       # residual-only (candidate) evaluations
+    return {"ba": ba, "sc": sc, "elapsed": elapsed, "iters": iters, "evals": evals, "jevals": jevals, "last": last,
+            "phases": phases, "setup_s": setup_s, "n_obs_total": n_obs_total, "n_pts_total": P_total,
+            "res_only": res_only, "value": n_obs_total * res_only / elapsed, "strong": strong}
 
+
+def ba_summary(m: dict, args, world: int) -> dict:
+    """The per-workload fields of a bench line."""
+    sc, phases, last = m["sc"], m["phases"], m["last"]
+    elapsed = m["elapsed"]
+    return {
+        "value": m["value"],
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "scaling": "strong" if m["strong"] else "weak",
+        "lm_iterations_per_s": m["iters"] / elapsed,
+        "jacobian_evals_per_s": m["n_obs_total"] * m["jevals"] / elapsed,
+        "lm_iterations_per_solve": m["iters"] / args.steps,
+        "residual_only_evals_per_solve": m["res_only"] / args.steps,
+        "jacobian_evals_per_solve": m["jevals"] / args.steps,
+        "final_cost": last.final_cost if last else None,
+        "set_problem_s": round(m["setup_s"], 4),
+        "phase_ms_per_solve": {k: round(v["ms"] / args.steps, 4) for k, v in phases.items()},
+        "workload": {"cams": sc.n_cams, "points": m["n_pts_total"], "observations": m["n_obs_total"],
+                     "points_per_gpu": sc.n_pts, "obs_per_gpu": sc.n_obs, "views_per_point": VIEWS,
+                     "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU"},
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pts-per-gpu", type=int, default=0,
+                    help="weak scaling: this many points per rank (default at N=1: C3's 200k)")
+    ap.add_argument("--cams", type=int, default=0, help="cameras (default: C3's 500, or C4's 2000 at N>1)")
+    ap.add_argument("--total-pts", type=int, default=0,
+                    help="strong scaling: this many points in total, split into landmark shards over the ranks "
+                         "(BASELINE config C4: --cams 2000 --total-pts 1000000; the default headline at N>1)")
+    ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
+    ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
+    ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
+    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the C4 (strong-scaling N=1 point) leg")
+    ap.add_argument("--comm", action="store_true",
+                    help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: ranks rendezvous and report the world, no GPU call")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(sys.argv[1:])
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        world = dist.get_world_size()   # n_gpus: the communicator's rank count
+    if args.dry_run:
+        t = torch.tensor([1.0])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": int(t.item()),
+                              "local_rank": local_rank}))
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
-    n_obs_total = sc.n_obs * world if not strong else VIEWS * P_total   # every point has VIEWS observations
-    n_pts_total = P_total
-    res_only = evals - jevals   # residual-only (candidate) evaluations
-    value = n_obs_total * res_only / elapsed
+    # headline workload: C3 at N=1 (BASELINE's single-GPU full-solve config);
+    # at N>1 BASELINE C4 (2000 cams / 1M points / 10M obs) landmark-sharded
+    # over the ranks (strong scaling), with C3-per-GPU weak scaling beside it
+    explicit = args.total_pts > 0 or args.pts_per_gpu > 0
+    if args.total_pts > 0:
+        strong, cams, P_total = True, args.cams or CAMS, args.total_pts
+        seed = SEED + 1 if (cams, P_total) == C4 else SEED
+    elif args.pts_per_gpu > 0:
+        strong, cams, P_total, seed = False, args.cams or CAMS, args.pts_per_gpu * world, SEED
+    elif world > 1:
+        strong, (cams, P_total), seed = True, C4, SEED + 1
+    else:
+        strong, cams, P_total, seed = False, args.cams or CAMS, PTS_PER_GPU, SEED
+    if strong:
+        p_begin, p_end = rank * P_total // world, (rank + 1) * P_total // world
+    else:
+        per = P_total // world
+        p_begin, p_end = rank * per, (rank + 1) * per
+    m = measure_ba(cams, P_total, p_begin, p_end, seed, strong, args, world, rank, local_rank, dist, args.comm)
+    ba, sc, phases = m["ba"], m["sc"], m["phases"]
+    head = ba_summary(m, args, world)
+
     jac = phases["jacobian"]
     # The solve's Jacobian pass is record-free (cost + U_c/b_c partials only;
-    # the later passes recompute residuals and Jacobians), so the HBM
-    # roofline object is the record-WRITING pass, the one whose 364.8 MB of
-    # algorithmic traffic (point index, uv, 160-B record per observation) the
-    # PMC traffic was collected on: timed with HIP events by bench_jacobian.
+    # the later passes recompute residuals and Jacobians)
     jac_solve_ms = jac["ms"] / max(1, jac["count"])
     cnt = np.bincount(sc.cam_idx, minlength=sc.n_cams)
     n_pad = int(((cnt + 63) // 64 * 64).sum())   # camera-major slots, runs padded to 64
@@ -620,7 +706,6 @@ def main() -> int:
     chol_ms = chol["ms"] / max(1, chol["count"])
     n_sys = 6 * sc.n_cams
     chol_tfs = cholesky_flops(n_sys) / (chol_ms * 1e-3) / 1e12
-    total_phase = sum(p["ms"] for p in phases.values())
     dominant = max(phases, key=lambda k: phases[k]["ms"])
 
     # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.sh
@@ -656,16 +741,16 @@ def main() -> int:
     # solver stream over the profiled pass of the same solves
     roof_jac = {"kernel": "k_jacobian (residual + 2x9 Jacobian pass, record-free, as run inside the solve)",
                 "bound": "hbm", "achieved": round(jac_gbs_s, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(jac_gbs_s / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(jac_gbs_s / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian"),
                 "algorithmic_bytes": jac_bytes_s, "avg_launch_ms": round(jac_solve_ms, 5),
                 "valu": {"achieved_tflops": round(jac_tfs_s, 3), "peak_tflops": F64_VALU_PEAK_TFS,
                          "frac": round(jac_tfs_s / F64_VALU_PEAK_TFS, 4),
                          "algorithmic_flops": jacobian_flops_solve(sc.n_obs)},
-                "note": "neither HBM nor fp64-VALU bound: latency (wave reductions of the 27 U_c/b_c partials, "
-                        "X gathers); PMC traffic was collected on the record-writing variant only"}
-    roof_jac_rec = {"kernel": "k_jacobian (record-writing variant, evaluate API)", "bound": "hbm",
-                    "achieved": round(jac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian"),
+                "note": "latency-bound (X gathers, the 27 U_c/b_c wave reductions); traffic: PMC of the "
+                        "record-free launches only (profiles/pmc_c3.json)"}
+    roof_jac_rec = {"kernel": "k_jacobian_rec (record-writing variant, evaluate API; not run by the solve)",
+                    "bound": "hbm", "achieved": round(jac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(jac_gbs / HBM_PEAK_GBS, 4), "traffic": traffic("k_jacobian_rec"),
                     "algorithmic_bytes": jac_bytes, "avg_launch_ms": round(jac_ms, 5),
                     "variant": "timed back to back by sfm_ba_bench_jacobian (warm caches)"}
     roof_chol = {"kernel": "k_chol_fused (dense reduced-camera Cholesky, one persistent launch, f64 MFMA)", "bound": "mfma",
@@ -675,48 +760,67 @@ def main() -> int:
                  "mfma_busy_frac_pmc": (mfma.get("k_chol_fused") or {}).get("mfma_busy_frac")}
     roofline = roof_chol if dominant == "cholesky" else roof_jac
 
+    wl = head.pop("workload")
+    if strong:
+        wname = (f"{cams} cams / {P_total} points / {m['n_obs_total']} obs in total"
+                 + (" (BASELINE C4)" if (cams, P_total) == C4 else "")
+                 + ", landmark-sharded over the ranks (strong scaling): full BA solve (LM + DENSE_SCHUR, "
+                   "Ceres default options)")
+    else:
+        wname = ("C3 per GPU" if (cams, P_total // world) == (CAMS, PTS_PER_GPU) else
+                 f"{cams} cams / {P_total // world} points per GPU") + \
+                ": full BA solve (LM + DENSE_SCHUR, Ceres default options)"
     out = {
         "metric": "BA iterations/sec + residual-evals/sec (cams x pts x obs); 1/2/4/8 GPU",
-        "value": value,
+        "value": head.pop("value"),
         "unit": "residual-evals/s (obs x evaluations)",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head.pop("ms_per_step"),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": head.pop("scaling"),
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded object-scanning scene, SURVEY.md §8d; K from main/main.cpp:47-50)",
-        "config": {
-            "workload": (f"{args.cams} cams / {P_total} points in total, landmark-sharded over the ranks (strong "
-                         "scaling): full BA solve (LM + DENSE_SCHUR, Ceres default options)") if strong else
-                        "C3 per GPU: full BA solve (LM + DENSE_SCHUR, Ceres default options)",
-            "cams": sc.n_cams, "points": n_pts_total, "observations": n_obs_total,
-            "points_per_gpu": sc.n_pts, "obs_per_gpu": sc.n_obs, "views_per_point": VIEWS,
-            "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
-        },
-        "lm_iterations_per_s": iters / elapsed,
-        "jacobian_evals_per_s": n_obs_total * jevals / elapsed,
-        "lm_iterations_per_solve": iters / args.steps,
-        "residual_only_evals_per_solve": res_only / args.steps,
-        "jacobian_evals_per_solve": jevals / args.steps,
-        "final_cost": last.final_cost if last else None,
-        "roofline": roofline,
-        "roofline_jacobian": roof_jac,
-        "roofline_jacobian_records": roof_jac_rec,
-        "roofline_cholesky": roof_chol,
-        "phase_ms_per_solve": {k: round(v["ms"] / args.steps, 4) for k, v in phases.items()},
+        "config": dict({"workload": wname}, **wl),
     }
+    out.update(head)
+    out.update({"roofline": roofline, "roofline_jacobian": roof_jac, "roofline_jacobian_records": roof_jac_rec,
+                "roofline_cholesky": roof_chol})
+    if world > 1 and not explicit:
+        # weak scaling beside the strong headline: C3 per rank
+        ba.close()
+        mw = measure_ba(CAMS, PTS_PER_GPU * world, rank * PTS_PER_GPU, (rank + 1) * PTS_PER_GPU, SEED, False,
+                        args, world, rank, local_rank, dist, False)
+        wk = ba_summary(mw, args, world)
+        wk["workload"] = dict({"workload": "C3 per GPU (weak scaling): full BA solve"}, **wk["workload"])
+        out["weak_c3_per_gpu"] = wk
+        mw["ba"].close()
+        ba = None
     if rank == 0 and world == 1:
         out["stream_copy_gbs"] = round(stream_copy_gbs(local_rank), 1)
     if rank == 0 and world == 1 and not args.no_oneshot:
         ba.close()  # the one-shot path keeps its own cached handle
         out["oneshot"] = oneshot_leg(sc)
+    if world == 1 and not explicit and not args.no_c4:
+        # the N = 1 point of the C4 strong-scaling curve (N > 1 lines report C4)
+        if ba is not None:
+            ba.close()
+        m4 = measure_ba(C4[0], C4[1], 0, C4[1], SEED + 1, True, args, 1, 0, local_rank, dist, False)
+        c4 = ba_summary(m4, args, 1)
+        c4["workload"] = dict({"workload": "BASELINE C4 on one GPU (the N=1 point of the strong-scaling curve)"},
+                              **c4["workload"])
+        ph = m4["phases"]["cholesky"]
+        c4_chol_ms = ph["ms"] / max(1, ph["count"])
+        c4["cholesky_tflops"] = round(cholesky_flops(6 * C4[0]) / (c4_chol_ms * 1e-3) / 1e12, 2)
+        out["c4_strong_n1"] = c4
+        m4["ba"].close()
+        ba = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(sc)
         out["cpu_baseline"] = cpu
-        out["speedup_vs_cpu"] = value / cpu["value"]
+        out["speedup_vs_cpu"] = out["value"] / cpu["value"]
         if "oneshot" in out:
             out["speedup_vs_cpu_oneshot"] = cpu["solve_s"] * 1e3 / out["oneshot"]["ms_per_solve"]
             out["speedup_vs_cpu_oneshot_multi_thread"] = cpu["multi_thread"]["solve_s"] * 1e3 / out["oneshot"]["ms_per_solve"]
@@ -734,7 +838,8 @@ def main() -> int:
         print(json.dumps(phases, indent=1), file=sys.stderr)
     if rank == 0:
         print(json.dumps(out))
-    ba.close()
+    if ba is not None:
+        ba.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -101,6 +101,10 @@ typedef struct sfm_ba_summary {
   double initial_cost;
   double final_cost;
   double wall_time_s;
+  /* Per-phase host times: filled by the host-driven LM loop only
+     (SFM_HOST_LM=1, or a host-callback collective).  The default
+     device-driven loop enqueues its phases asynchronously; it leaves these
+     0 and wall_time_s is the whole solve. */
   double jacobian_time_s;
   double linear_solver_time_s;
   double residual_time_s;

@@ -390,11 +390,22 @@ class OpticalFlowTracker {
     keypoints.clear();
     descriptors.clear();
     if (!h_) return rc_;
-    std::vector<float> k(5 * size_t(capacity));
-    std::vector<int32_t> oct(static_cast<size_t>(capacity));
-    std::vector<uint8_t> d(64 * size_t(capacity));
+    std::vector<float> k;
+    std::vector<int32_t> oct;
+    std::vector<uint8_t> d;
     int32_t n = 0;
-    const int rc = sfm_klt_brisk_detect_describe(h_, threshold, octaves, capacity, k.data(), oct.data(), d.data(), &n);
+    // the call reports the count before it rejects a short buffer: one retry
+    // at that size, so a frame with more keypoints never fails (the
+    // reference's detectFeatures has no cap)
+    int rc = SFM_OK;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      k.assign(5 * size_t(capacity), 0.0f);
+      oct.assign(size_t(capacity), 0);
+      d.assign(64 * size_t(capacity), 0);
+      rc = sfm_klt_brisk_detect_describe(h_, threshold, octaves, capacity, k.data(), oct.data(), d.data(), &n);
+      if (rc == SFM_OK || n <= capacity) break;
+      capacity = n;
+    }
     if (rc) return rc;
     unpack_keypoints(k, oct, d, n, keypoints, descriptors);
     return SFM_OK;
@@ -463,12 +474,20 @@ inline int detectFeatures(const GreyMat& grey, std::vector<KeyPoint>& keypoints,
       std::copy(img + size_t(y) * step, img + size_t(y) * step + size_t(w), packed.begin() + size_t(y) * size_t(w));
     img = packed.data();
   }
-  std::vector<float> k(5 * size_t(capacity));
-  std::vector<int32_t> oct(static_cast<size_t>(capacity));
-  std::vector<uint8_t> d(64 * size_t(capacity));
+  std::vector<float> k;
+  std::vector<int32_t> oct;
+  std::vector<uint8_t> d;
   int32_t n = 0;
-  const int rc = sfm_brisk_detect_describe(device, img, w, h, threshold, octaves, capacity, k.data(), oct.data(),
-                                           d.data(), &n);
+  int rc = SFM_OK;
+  for (int attempt = 0; attempt < 2; ++attempt) {  // one retry at the reported count
+    k.assign(5 * size_t(capacity), 0.0f);
+    oct.assign(size_t(capacity), 0);
+    d.assign(64 * size_t(capacity), 0);
+    rc = sfm_brisk_detect_describe(device, img, w, h, threshold, octaves, capacity, k.data(), oct.data(), d.data(),
+                                   &n);
+    if (rc == SFM_OK || n <= capacity) break;
+    capacity = n;
+  }
   if (rc) return rc;
   unpack_keypoints(k, oct, d, n, keypoints, descriptors);
   return SFM_OK;

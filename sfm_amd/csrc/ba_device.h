@@ -184,6 +184,8 @@ void launch_point_factor(const DevProblem& d, double radius, hipStream_t s);
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
 void launch_pad_init(const DevProblem& d, hipStream_t s);
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
+// dst = scale * src unless *gate == 0 (gate may be nullptr)
+void launch_gated_copy(const double* src, double* dst, int64_t n, double scale, const int32_t* gate, hipStream_t s);
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = true, bool pts_var = true);
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);

@@ -195,6 +195,10 @@ __device__ __forceinline__ double jac_record(const double* cr, double tc0, doubl
 // stores on CDNA, so a wait on a load also covers every older store):
 //   [X_t, uv_t in flight] issue p_{t+1}, uv_{t+1} -> wait X_t -> compute t
 //   -> stage t in LDS -> issue X_{t+1} -> store chunk t.
+// kRec: the record-writing variant of the evaluate API (k_jacobian<true>);
+// the solve runs the record-free k_jacobian<false> (no staging LDS, so the
+// two show up apart in kernel traces and counter passes).
+template <bool kRec>
 __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict__ grp_off,
                                                        const int4* __restrict__ chunks,
                                                        const int32_t* __restrict__ cm_p,
@@ -204,10 +208,10 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ scale_p, int scaled,
                                                        double* __restrict__ jrec, double* __restrict__ part_cost,
-                                                       double* __restrict__ jpart, int write_rec, const int* __restrict__ gate) {
+                                                       double* __restrict__ jpart, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
-  __shared__ __attribute__((aligned(16))) double stage[kThreads * kJRec];  // 10 KB per wave
+  __shared__ __attribute__((aligned(16))) double stage[kRec ? kThreads * kJRec : 2];  // 10 KB per wave
   const int l = threadIdx.x & 63;
   const int wv = wave_uniform(threadIdx.x >> 6);
   double* wst = stage + wv * 64 * kJRec;
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
       const double cl = jac_record(cr, cam[6 * c + 3], cam[6 * c + 4], cam[6 * c + 5], k[0], k[1], k[2], k[3], k[4],
                                    sc, spc, Xc, uv_cur, rec);
       cost += (l < cnt) ? cl : 0.0;
-      if (write_rec) {  // staged for jac_flush (wave-uniform)
+      if (kRec) {  // staged for jac_flush
         double* mine = wst + l * kJRec;
 #pragma unroll
         for (int f = 0; f < kJRec; f += 2) st2(mine + f, rec[f], rec[f + 1]);
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
         if (!(l & 1) && (l >> 1) < 27) jpart[size_t(ib / 64) * 27 + (l >> 1)] = tot;
       }
     }
-    if (write_rec) {  // wave-uniform: no record consumer left in the record-free solve path
+    if (kRec) {  // no record consumer left in the record-free solve path
       wave_lds_sync();
       jac_flush(wst, jrec, ib, l);
       wave_lds_sync();
@@ -1090,6 +1094,15 @@ __global__ void k_unpack_upper(const double* __restrict__ P, int ld, int n, doub
   for (int j = i + threadIdx.x; j <= n; j += blockDim.x) row[j] = src[j];
 }
 
+// dst = scale * src, skipped with its phase (the device LM loop's
+// out-of-place collectives copy their result back through this; scale is
+// the emulated rank count of the tests, a power of two: exact).
+__global__ void k_gated_copy(const double* src, double* dst, int64_t n, double scale, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    dst[i] = src[i] * scale;
+}
+
 // Identity padding beyond the augmented row n (column-major lower view).
 // Identity padding of the augmented system, and the Cholesky failure flag
 // cleared (saves the separate memset dispatch before k_chol_fused).
@@ -1348,9 +1361,14 @@ void launch_cam_prep_accept(const DevProblem& d, bool count_norm, int grid, hipS
 }
 void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write_records) {
   // the record-writing variant (evaluate API) runs on its own, smaller grid
-  k_jacobian<<<write_records ? d.jac_blocks_rec : d.jac_blocks, kThreads, 0, s>>>(
-      d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X, d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
-      slot(d, kPCost), d.jpart, write_records ? 1 : 0, d.gate);
+  if (write_records)
+    k_jacobian<true><<<d.jac_blocks_rec, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR,
+                                                           d.X, d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec,
+                                                           slot(d, kPCost), d.jpart, d.gate);
+  else
+    k_jacobian<false><<<d.jac_blocks, kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.Kc, d.cam, d.camR, d.X,
+                                                        d.scale_c, d.scale_p, scaled ? 1 : 0, d.jrec, slot(d, kPCost),
+                                                        d.jpart, d.gate);
 }
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.gate);
@@ -1420,6 +1438,11 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s) {
   if (d.n == 0) return;
   if (unpack) k_unpack_upper<<<d.n, 256, 0, s>>>(d.Spack, d.ld, d.n, d.S, d.gate);
   else k_pack_upper<<<d.n, 256, 0, s>>>(d.S, d.ld, d.n, d.Spack, d.gate);
+}
+void launch_gated_copy(const double* src, double* dst, int64_t n, double scale, const int32_t* gate, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = int(std::min<int64_t>(1024, (n + 255) / 256));
+  k_gated_copy<<<grid, 256, 0, s>>>(src, dst, n, scale, gate);
 }
 void launch_pad_init(const DevProblem& d, hipStream_t s) {
   // (also the back substitution's sentinel: 64 per real block of y)

@@ -87,6 +87,15 @@ struct sfm_ba_handle {
   sfm_allreduce_fn host_fn = nullptr;
   void* host_user = nullptr;
   std::vector<double> host_buf;
+  // out-of-place target of the collectives enqueued inside a gated phase of
+  // the device LM loop (allreduce below); grown on demand
+  double* ar_tmp = nullptr;
+  size_t ar_tmp_cap = 0;
+  // SFM_EMULATE_IDENTICAL_RANKS=k (tests, read by sfm_ba_set_comm): every sum
+  // collective returns k times its one-rank result, i.e. the sum over k
+  // ranks holding the same shard, so a one-GPU run sees the stale-buffer
+  // hazards of a multi-rank one
+  int emulate_ranks = 1;
   // device-driven LM loop (unsharded solves): control block, its pinned
   // mirror and the device trace buffer (grown to the iteration cap)
   LmCtl* lm_ctl = nullptr;
@@ -478,7 +487,33 @@ int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
     return 0;
   }
   if (!h->comm) return 0;
-  NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, op, h->comm, h->stream));
+  const double scale = op == ncclSum ? double(h->emulate_ranks) : 1.0;
+  // Inside a gated phase of the device LM loop the phase's kernels may return
+  // at once, leaving `buf` holding the previous, already reduced values: an
+  // in-place collective would sum those again (U_c times the rank count after
+  // every rejected step).  So the collective goes out of place and a gated
+  // kernel copies the result back.  The packed S image is scratch (its pack
+  // and unpack are gated themselves) and stays in place.
+  const bool gated = h->d.gate != nullptr && buf != h->d.Spack;
+  if (!gated) {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, op, h->comm, h->stream));
+    if (scale != 1.0) launch_gated_copy(buf, buf, int64_t(count), scale, nullptr, h->stream);
+    return 0;
+  }
+  if (h->ar_tmp_cap < count) {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->ar_tmp) (void)hipFree(h->ar_tmp);
+    h->ar_tmp = nullptr;
+    h->ar_tmp_cap = 0;
+    const size_t cap = std::max<size_t>(count, 4096);
+    if (hipMalloc(reinterpret_cast<void**>(&h->ar_tmp), cap * sizeof(double)) != hipSuccess) {
+      h->ar_tmp = nullptr;
+      return fail(SFM_ENOMEM, "hipMalloc failed (collective scratch)");
+    }
+    h->ar_tmp_cap = cap;
+  }
+  NCCLCHK(ncclAllReduce(buf, h->ar_tmp, count, ncclDouble, op, h->comm, h->stream));
+  launch_gated_copy(h->ar_tmp, buf, int64_t(count), scale, h->d.gate, h->stream);
   return 0;
 }
 
@@ -890,6 +925,7 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_ctl_host) hipHostFree(h->lm_ctl_host);
   if (h->lm_trace) hipFree(h->lm_trace);
   if (h->stage) hipHostFree(h->stage);
+  if (h->ar_tmp) hipFree(h->ar_tmp);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -917,6 +953,8 @@ int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCLCHK(ncclCommInitRank(&h->comm, nranks, uid, rank));
+  h->emulate_ranks = 1;
+  if (const char* e = std::getenv("SFM_EMULATE_IDENTICAL_RANKS")) h->emulate_ranks = std::max(1, std::atoi(e));
   return 0;
 }
 
@@ -1433,13 +1471,12 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
     // host loop.
     double cost = 0.0;
     bool nonfinite = false;
-    const double tl0 = now_s();
     rc = run_device_lm(h, opts, &cost, &sm, push, &nonfinite);
     if (rc) {
       if (nonfinite && summary) *summary = sm;
       return rc;
     }
-    sm.linear_solver_time_s += now_s() - tl0;
+    // (per-phase host times stay 0 here: the phases run asynchronously)
     sm.final_cost = cost;
     sm.wall_time_s = now_s();
     if (summary) *summary = sm;

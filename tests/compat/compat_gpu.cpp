@@ -258,6 +258,20 @@ static int run_brisk(const std::string& dir) {
   wr(dir, "out_kp_res.f32", k);
   wr(dir, "out_octave_res.i32", oct);
   wr(dir, "out_desc_res.u8", dr);
+  // a capacity far below the frame's keypoint count: both entry points retry
+  // once at the reported count and return the same keypoints
+  std::vector<KeyPoint> ks;
+  std::vector<uint8_t> ds;
+  if (int r3 = sfm_compat::detectFeatures(g, ks, ds, meta[2], meta[3], 16)) {
+    std::printf("brisk small-capacity rc=%d %s\n", r3, sfm_last_error());
+    return 1;
+  }
+  if (ks.size() != kp.size() || ds != desc) { std::printf("brisk small-capacity mismatch\n"); return 1; }
+  if (int r4 = flow.detectFeaturesBrisk(ks, ds, meta[2], meta[3], 16)) {
+    std::printf("brisk resident small-capacity rc=%d %s\n", r4, sfm_last_error());
+    return 1;
+  }
+  if (ks.size() != kr.size() || ds != dr) { std::printf("brisk resident small-capacity mismatch\n"); return 1; }
   return 0;
 }
 

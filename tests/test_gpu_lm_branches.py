@@ -232,3 +232,38 @@ def test_device_loop_batches_and_iteration_cap(max_iter, gtol, monkeypatch):
             assert sm.num_iterations <= max_iter
         else:
             assert got == ref, env
+
+
+@pytest.mark.parametrize("name", ["reject_a", "reject_c", "llt_invalid", "pose_only"])
+def test_device_loop_collectives_with_two_emulated_ranks(name, monkeypatch):
+    """with a communicator, the device-driven loop enqueues
+    the collectives of phases its flags then skip (the evaluation after a
+    rejected or invalid step).  An in-place all-reduce there summed the
+    already reduced U_c again.  Emulated here on one GPU: a one-rank RCCL
+    communicator whose sum collectives return twice their input
+    (SFM_EMULATE_IDENTICAL_RANKS=2, i.e. two ranks holding the same shard),
+    so a stale buffer summed again differs from the host-driven loop (which
+    runs every phase).  The device loop must equal the host loop bitwise on
+    scenes with rejected / invalid steps."""
+    c = FIX[name]
+    build, _, mode = L.cases()[name]
+    s = build()
+    monkeypatch.setenv("SFM_EMULATE_IDENTICAL_RANKS", "2")
+    out = {}
+    for host in (False, True):
+        if host:
+            monkeypatch.setenv("SFM_HOST_LM", "1")
+        else:
+            monkeypatch.delenv("SFM_HOST_LM", raising=False)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve(sfm_amd.make_options(**c["options"]), mode=mode)
+            out[host] = (sm, tr, ba.parameters())
+    (sa, ta, pa), (sb, tb, pb) = out[False], out[True]
+    seq = seq_of(tb)
+    assert "R" in seq or "I" in seq, seq  # the scene exercises a skipped evaluation
+    assert ta == tb, (seq_of(ta), seq)
+    assert sa.final_cost == sb.final_cost
+    for a, b in zip(pa, pb):
+        assert np.array_equal(a, b)
