@@ -56,6 +56,13 @@
 namespace oracle {
 
 static int g_threads = 1;
+// Summation order of the reduced camera matrix's diagonal blocks (tests
+// only, oracle_set_order): 0 = Ceres' (the running sum per camera block,
+// point by point: F^T F, then the chunk outer product), 1 = the device
+// solver's association (U_c = sum F^T F first, then + D^2, then minus the
+// outer products) -- the same arithmetic in another valid order, used to
+// show which LM decisions of a near-singular problem rounding decides.
+static int g_order = 0;
 
 // ---------------------------------------------------------------------------
 // Jet<double, N>: restates the arithmetic of ceres/jet.h (value part `a`,
@@ -570,6 +577,19 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
       if (pb.pts_var && pb.cams_var) {
         S.assign(size_t(nf) * nf, 0.0);
         rhs.assign(nf, 0.0);
+        if (g_order == 1) {
+          // U_c = sum_q F^T F (point order), then + D^2
+          for (int p = 0; p < n_pts; ++p)
+            for (int64_t q = pb.pt_off[p]; q < pb.pt_off[p + 1]; ++q) {
+              const int c = cam_idx[pb.order[q]];
+              double F[12];
+              for (int row = 0; row < 2; ++row)
+                for (int k = 0; k < 6; ++k) F[6 * row + k] = Js(q, row, k);
+              for (int a = 0; a < 6; ++a)
+                for (int bb = 0; bb < 6; ++bb)
+                  S[size_t(6 * c + a) * nf + 6 * c + bb] += F[a] * F[bb] + F[6 + a] * F[6 + bb];
+            }
+        }
         for (int i = 0; i < nf; ++i) S[size_t(i) * nf + i] += lm_D[pb.np + i] * lm_D[pb.np + i];
         // Phase 1, per point (independent): ete = D_e^2 + sum E^T E,
         // g = sum E^T b, buffer_f = sum E^T F per distinct camera (slot order
@@ -632,7 +652,7 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
               const int64_t q0 = pb.pt_off[p], q1 = pb.pt_off[p + 1];
               if (q0 == q1) continue;
               // F^T F into S (both 3-blocks of the camera and their coupling)
-              for (int64_t q = q0; q < q1; ++q) {
+              for (int64_t q = q0; q < q1 && g_order == 0; ++q) {
                 const int c = cam_idx[pb.order[q]];
                 if (c < clo || c >= chi) continue;
                 double F[12];
@@ -879,6 +899,11 @@ int oracle_set_threads(int threads) {
   return prev;
 }
 
+int oracle_set_order(int order) {
+  const int prev = g_order;
+  g_order = order;
+  return prev;
+}
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

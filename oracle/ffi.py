@@ -64,6 +64,8 @@ def lib():
         L.oracle_ba_solve.restype = c_int
         L.oracle_set_threads.argtypes = [c_int]
         L.oracle_set_threads.restype = c_int
+        L.oracle_set_order.argtypes = [c_int]
+        L.oracle_set_order.restype = c_int
         L.oracle_knn2_hamming.argtypes = [c_void_p, c_int32, c_void_p, c_int32, c_int32] + [c_void_p] * 4
         L.oracle_knn2_hamming.restype = c_int
         L.oracle_match_features.argtypes = [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
@@ -126,9 +128,12 @@ def residuals_jacobians(uv, cam_idx, pt_idx, K9, rot, t, X, jacobian=True):
     return res, jac
 
 
-def solve(uv, cam_idx, pt_idx, K9, rot, t, X, mode=2, options: Options | None = None, trace_cap=128, threads=1):
+def solve(uv, cam_idx, pt_idx, K9, rot, t, X, mode=2, options: Options | None = None, trace_cap=128, threads=1,
+          order=0):
     """rot, t, X are updated in place (float64, C-contiguous).  threads > 1
-    runs the oracle's OpenMP loops (bitwise the 1-thread result)."""
+    runs the oracle's OpenMP loops (bitwise the 1-thread result).  order=1
+    sums the reduced matrix's diagonal blocks in the device solver's
+    association instead of Ceres' (oracle_set_order; tests only)."""
     uv = np.ascontiguousarray(uv, np.float64)
     cam_idx = np.ascontiguousarray(cam_idx, np.int32)
     pt_idx = np.ascontiguousarray(pt_idx, np.int32)
@@ -138,12 +143,14 @@ def solve(uv, cam_idx, pt_idx, K9, rot, t, X, mode=2, options: Options | None = 
     tr = (Iteration * trace_cap)()
     tl = c_int32(0)
     prev = lib().oracle_set_threads(int(threads))
+    prev_order = lib().oracle_set_order(int(order))
     try:
         rc = lib().oracle_ba_solve(ctypes.byref(o), mode, uv.shape[0], _p(uv), _p(cam_idx), _p(pt_idx), rot.shape[0],
                                    _p(K9), _p(rot), _p(t), X.shape[0], _p(X), ctypes.byref(sm), tr, trace_cap,
                                    ctypes.byref(tl))
     finally:
         lib().oracle_set_threads(prev)
+        lib().oracle_set_order(prev_order)
     if rc != 0:
         raise RuntimeError(f"oracle_ba_solve returned {rc}")
     return sm.as_dict(), [tr[i].as_dict() for i in range(tl.value)]

@@ -3,6 +3,7 @@
 // HBM layout and the per-kernel roofline arithmetic.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 namespace sfm {
@@ -33,6 +34,23 @@ constexpr int kThreads = 256;
 // signalling NaN, which arithmetic never yields)
 constexpr uint32_t kYSentinelWord = 0x7FF4DEADu;
 constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWord;
+
+// The diagonal-tile inverses W_k = L_kk^-1 travel from the Cholesky walker
+// to the helpers as data-tagged granules: before each factorisation every
+// entry of W_k's lower 16x16 blocks holds kYSentinel, and a consumer polls
+// the entries it needs until none is the sentinel (no flag, no drain on the
+// walker).  The upper blocks stay zero (k_backsolve reads whole columns).
+// Part `part` of `nparts` of the fill, by `nt` threads (thread `t`).
+__device__ __forceinline__ void w_sentinel_fill(double* __restrict__ invL, int nblk, int part, int nparts, int t,
+                                                int nt) {
+  const int64_t total = int64_t(nblk) * kNB * kNB;
+  const int64_t per = (total + nparts - 1) / nparts;
+  const int64_t e0 = int64_t(part) * per, e1 = e0 + per < total ? e0 + per : total;
+  for (int64_t e = e0 + t; e < e1; e += nt) {
+    const int r = int(e & (kNB - 1)), c = int((e >> 6) & (kNB - 1));  // W_k(r, c) at k*4096 + c*64 + r
+    if ((r >> 4) >= (c >> 4)) reinterpret_cast<unsigned long long*>(invL)[e] = kYSentinel;
+  }
+}
 
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
@@ -119,7 +137,8 @@ struct DevProblem {
                               //     4: Cholesky tile hand-off timeout
   int32_t* flags = nullptr;   // [nblk] back-substitution hand-off flags (epoch-stamped)
   int32_t* cflags = nullptr;  // [2][nblk][nblk] fused Cholesky: final (F) and partial (P) tile flags
-  unsigned long long* cticket = nullptr;  // fused Cholesky tile ticket (monotone across launches)
+  unsigned long long* cticket = nullptr;  // [3] fused Cholesky tile ticket, its walker-role ticket, the back
+                                          // substitution's row ticket (all monotone across launches)
   int32_t n_cu = 0;           // compute units (co-residency bound of the persistent grids)
   // LM diagonal clamp of the running solve (sfm_ba_options min/max_lm_diagonal)
   double min_diag = 1e-6, max_diag = 1e32;
@@ -188,6 +207,12 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
 void launch_gated_copy(const double* src, double* dst, int64_t n, double scale, const int32_t* gate, hipStream_t s);
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = true, bool pts_var = true);
+// grid of the XCD-ordered observation passes (k_obs_prep_rc, k_backsub_a_rc):
+// one workgroup per 4 chunks, a multiple of 8 (one point slice per XCD)
+inline int obs_xcd_blocks(const DevProblem& d) {
+  const int64_t nb = (d.N_pad / 64 + 3) / 4;
+  return int(8 * std::max<int64_t>(1, (nb + 7) / 8));
+}
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);
@@ -196,6 +221,8 @@ int blocks_for(int64_t n, int threads);
 
 // ---- dense Cholesky (chol_kernels.hip) ----
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
+// W_k granules back to the sentinel (k_schur_diag_sum does this in the solve)
+void launch_w_sentinel(const DevProblem& d, hipStream_t s);
 // sentinel_set: y already holds kYSentinel (k_pad_init wrote it)
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set = false);
 

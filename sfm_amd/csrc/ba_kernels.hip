@@ -663,12 +663,29 @@ __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const d
   o.h1 = o.M[3] * q[12] + o.M[4] * q[13] + o.M[5] * q[14];
 }
 
+// XCD-aware chunk order of the camera-major observation passes (as
+// k_jacobian): the 64-position chunks are grouped into 8 point slices
+// (grp_off), workgroup b serves slice b % 8, so the round-robin workgroup ->
+// XCD dispatch keeps each slice's point records (1/8 of ptS) in one XCD's
+// L2 instead of every XCD gathering all of them.  Wave wi of its slice takes
+// chunks g0 + wi, g0 + wi + nw, ... (placement is a speed assumption only).
+struct XcdChunks {
+  int t, end, stride;
+};
+__device__ __forceinline__ XcdChunks xcd_chunks(const int32_t* __restrict__ grp_off, int wv) {
+  const int grp = blockIdx.x & 7;
+  const int nbg = (int(gridDim.x) - 1 - grp) / 8 + 1;
+  const int wi = (blockIdx.x >> 3) * (kThreads / 64) + wv;
+  return XcdChunks{grp_off[grp] + wi, grp_off[grp + 1], nbg * (kThreads / 64)};
+}
+
 // Per observation (camera-major, one wavefront = 64 positions of ONE camera):
 // F = J_c^T M (M = J_X L_p^-T) and the wave's share of the camera's Schur
 // diagonal block sum F F^T (21) and rhs sum J_c^T (r - h) (6), reduced over
-// its real observations into dpart[wave][27] (fixed tree order).  J, M, h
+// its real observations into dpart[chunk][27] (fixed tree order).  J, M, h
 // are recomputed (ptS is written by k_point_factor just before).
-__global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
+__global__ __launch_bounds__(kThreads) void k_obs_prep_rc(const int32_t* __restrict__ grp_off,
+                                                          const int4* __restrict__ chunks,
                                                           const int32_t* __restrict__ cm_p,
                                                           const double* __restrict__ uv_cm,
                                                           const int32_t* __restrict__ cam_obs,
@@ -680,10 +697,12 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
                                                           double* __restrict__ dpart, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
-  if (i0 >= N_pad) return;  // wave-uniform, no barriers below
+  const XcdChunks xc = xcd_chunks(grp_off, wv);
+  for (int t = xc.t; t < xc.end; t += xc.stride) {  // wave-uniform, no barriers below
+  const int4 ch = chunks[t];
+  const int64_t i0 = ch.y;
   const int64_t i = i0 + l;
-  const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
+  const int c = __builtin_amdgcn_readfirstlane(ch.x);
   ObsRC o;
   obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, o);
   const double* jc = o.rec + kJC;
@@ -709,11 +728,14 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(int64_t N_pad, const i
   for (int e = 27; e < 32; ++e) v[e] = 0.0;
   const double tot = wave_sum32(v, l);
   if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
+  }
 }
 
 // Back substitution pass A (see k_backsub_b): e = J_c y_c, u = M^T e, and
-// the observation's share of the model cost change (J, M recomputed).
-__global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const int32_t* __restrict__ wcam,
+// the observation's share of the model cost change (J, M recomputed); the
+// chunks in the XCD-aware order of k_obs_prep_rc.
+__global__ __launch_bounds__(kThreads) void k_backsub_a_rc(const int32_t* __restrict__ grp_off,
+                                                           const int4* __restrict__ chunks,
                                                            const int32_t* __restrict__ cm_p,
                                                            const double* __restrict__ uv_cm,
                                                            const int32_t* __restrict__ cam_obs,
@@ -727,11 +749,12 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
   double model = 0.0;
-  if (i0 < N_pad) {
-    const int64_t i = i0 + l;
-    const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);
+  const XcdChunks xc = xcd_chunks(grp_off, wv);
+  for (int t = xc.t; t < xc.end; t += xc.stride) {  // wave-uniform
+    const int4 ch = chunks[t];
+    const int64_t i = int64_t(ch.y) + l;
+    const int c = __builtin_amdgcn_readfirstlane(ch.x);
     ObsRC o;
     obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, o);
     const double* y = ysol + 6 * size_t(c);
@@ -741,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(int64_t N_pad, const 
     for (int k = 0; k < 6; ++k) { e0 += J[k] * y[k]; e1 += J[6 + k] * y[k]; }
     const int qo = cam_obs[i];
     if (qo >= 0) {
-      model = e0 * o.rec[kRes] + e1 * o.rec[kRes + 1] - 0.5 * (e0 * e0 + e1 * e1);
+      model += e0 * o.rec[kRes] + e1 * o.rec[kRes + 1] - 0.5 * (e0 * e0 + e1 * e1);
       // u goes to the observation's POINT-major slot (32 B): pass B then
       // streams a point's u contiguously instead of gathering 48-B records
       const double* M = o.M;
@@ -1018,10 +1041,13 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        const double* __restrict__ diag_c, double radius,
                                                        int add_diag, double* __restrict__ S, int ld, int n,
                                                        int init, const int* __restrict__ gate, const double* __restrict__ radius_dev,
-                                                       int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y) {
+                                                       int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y,
+                                                       double* __restrict__ invL, int nblk) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   const int c = blockIdx.x, t = threadIdx.x;
+  // the factorisation's W_k granules back to "not yet produced"
+  w_sentinel_fill(invL, nblk, c, gridDim.x, t, 64);
   // k_pad_init folded in (one launch fewer per LM iteration): the identity
   // padding below row n of this camera's six columns and y's sentinel
   // there; the last camera also takes columns n.. (the identity block, the
@@ -1406,8 +1432,8 @@ void launch_point_factor(const DevProblem& d, double radius, hipStream_t s) {
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
   launch_point_factor(d, radius, s);
   if (d.N_pad)
-    k_obs_prep_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
-                                                                    d.cam, d.Kc, d.scale_c, d.ptS, d.dpart, d.gate);
+    k_obs_prep_rc<<<obs_xcd_blocks(d), kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.cam_obs, d.camR, d.cam,
+                                                         d.Kc, d.scale_c, d.ptS, d.dpart, d.gate);
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
@@ -1415,7 +1441,8 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
                                         d.n, 1, d.gate, d.radius_dev, d.fail,
-                                        reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB);
+                                        reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB,
+                                        d.invL, d.nblk);
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
   const int nb = int((d.n_bslots + per - 1) / per);
@@ -1461,12 +1488,12 @@ void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s) {
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, bool pts_var) {
   // cameras constant (STRUCT_ONLY): e = J_c y_c = 0 and u = 0
   if (d.N_pad && cams_var)
-    k_backsub_a_rc<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cm_p, d.uv_cm, d.cam_obs,
-                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.ptS, d.ysol, d.eu,
-                                                                     d.eu_cm ? 1 : 0, slot(d, kPModel), d.gate);
+    k_backsub_a_rc<<<obs_xcd_blocks(d), kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cm_p, d.uv_cm, d.cam_obs, d.camR,
+                                                          d.cam, d.Kc, d.scale_c, d.ptS, d.ysol, d.eu, d.eu_cm ? 1 : 0,
+                                                          slot(d, kPModel), d.gate);
   else if (d.N_pad) {
     (void)hipMemsetAsync(d.eu, 0, sizeof(double) * 4 * size_t(d.eu_cm ? d.N_pad : d.N), s);
-    (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(blocks_for(d.N_pad, kThreads)), s);
+    (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(obs_xcd_blocks(d)), s);
   }
   if (d.P && pts_var) {
     k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.eu_cm ? d.pos : nullptr,

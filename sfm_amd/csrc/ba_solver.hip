@@ -686,7 +686,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
   const int nbI = std::max(1, blocks_for(d.N_pad, 256));  // k_backsub_c grid
   ReduceBatch rb;
-  rb.add(kPModel, nbI, 0, kModelChange);
+  rb.add(kPModel, d.N_pad ? obs_xcd_blocks(d) : 1, 0, kModelChange);  // k_backsub_a_rc grid
   rb.add(kPNewCost, nbI, 0, kNewCost);
   rb.add(kPStepPt, nbP, 0, kStep2Pt);
   rb.add(kPStepCam, nbC, 0, kStep2Cam);
@@ -1269,7 +1269,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
   d.nblk = d.ld / kNB;
   d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
-                           d.jac_blocks_rec, blocks_for(npad, 256)});
+                           d.jac_blocks_rec, blocks_for(npad, 256), obs_xcd_blocks(d)});
   {
     uint8_t* pb = nullptr;
     ALLOC(pb, pl.bytes);
@@ -1308,7 +1308,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);
-  ALLOC(d.cticket, 1);
+  ALLOC(d.cticket, 3);  // task ticket, walker-role ticket, back-substitution role ticket
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);
@@ -1347,7 +1347,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     fs.add(d.invL, sizeof(double) * size_t(d.nblk) * kNB * kNB, 0);
     fs.add(d.flags, sizeof(int32_t) * size_t(d.nblk), 0);
     fs.add(d.cflags, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, 0);
-    fs.add(d.cticket, sizeof(unsigned long long), 0);
+    fs.add(d.cticket, 3 * sizeof(unsigned long long), 0);
     fs.add(d.partials, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, 0);
     launch_fill32(fs, s);
   }
@@ -1717,8 +1717,8 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   HIPCHK(hipMalloc(&S0, bytes));
   HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
   HIPCHK(hipMemset(invd, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB));
-  HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
-  HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 2)));
+  HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 8)));
+  HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 8)));
   HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
   HIPCHK(hipMalloc(&fl, sizeof(int)));
   HIPCHK(hipMemcpy(S0, img.data(), bytes, hipMemcpyHostToDevice));
@@ -1733,6 +1733,7 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   float total = 0.f;
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipMemcpyAsync(S, S0, bytes, hipMemcpyDeviceToDevice, s));
+    launch_w_sentinel(d, s);
     HIPCHK(hipEventRecord(e0, s));
     launch_cholesky(d, r + 1, s);
     launch_backsolve(d, r + 1, s);

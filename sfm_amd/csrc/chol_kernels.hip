@@ -21,7 +21,28 @@
 #include "ba_common.h"
 
 namespace sfm {
+#ifdef SFM_CHOL_STAMPS
+// development build (tools/chol_stamps.sh): s_memrealtime stamps (100 MHz) of
+// the walker's phases, [step][slot]; slot 7 holds the step's `early` flag
+__device__ unsigned long long g_wstamp[256 * 16];
+#define WSTAMP(j, k) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define WSTAMPV(j, k, v) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = (v); } while (0)
+#else
+#define WSTAMP(j, k) do { } while (0)
+#define WSTAMPV(j, k, v) do { } while (0)
+#endif
 namespace {
+
+// Hand-off forms of the fused Cholesky (kernel argument `opt`, SFM_CHOL_OPT;
+// A/B of the protocol choices on one box):
+//   kOptSc1   the walker loads handed-off tiles with sc1 loads after a flag
+//             poll (no acquire); else acquire + plain loads
+//   kOptWGran W_j as data-tagged granules (load_w); else stores + drain +
+//             flag F(j,j) and an acquire in the helpers
+//   kOptLPub  L_j+1,j stored by waves 1-3, drained and flagged during the
+//             next step's panel 0; else every wave stores and the block
+//             drains and flags after the next step's first update
+constexpr int kOptSc1 = 1, kOptWGran = 2, kOptLPub = 4;
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int NB = kNB;  // 64
@@ -163,10 +184,14 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
 // partial tiles once during panel 3 and leaves in *rdy whether both are out,
 // so the walker can load them beside W_j's publication (a poll during panel
 // 2 mostly came too early: the tile (j+1, j) waits for L_j,j-1).
+// pub_flag != nullptr: waves 1-3 stored L_j,j-1 (the walker's last TRSM
+// result) at the end of the previous step; each drains its own stores during
+// panel 0 and counts itself in pub_cnt (LDS), the last one raises the flag,
+// so wave 0 -- the pivot chain -- never waits for the write-through stores.
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
 __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
                                            const double* Ls, const int* pf_sub, const int* pf_diag, int epoch,
-                                           int* rdy) {
+                                           int* rdy, int* pub_flag, int* pub_cnt) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -280,6 +305,15 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         const int Ib[2] = {w, w + 1 < 4 ? w + 1 : 3}, Jb[2] = {1, w == 1 ? 2 : (w == 2 ? 2 : 3)};
         last_update<2>(T, Ls, Ib, Jb, 2, lane);
       }
+      if (pub_flag != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // every lane adds (lane 0 one, the rest zero): the count is uniform
+        const int old = __builtin_amdgcn_readfirstlane(atomicAdd(pub_cnt, (t & 63) == 0 ? 1 : 0));
+        if (old == 2) {  // the third of waves 1-3
+          *pub_cnt = 0;
+          __hip_atomic_store(pub_flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     } else if (b == 1) {
       // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
       trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
@@ -299,6 +333,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
                __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     }
     __syncthreads();
+    WSTAMP(k0 / 64, 8 + b);
     // ---- trailing update of column block b+1 (the next panel's); the
     // blocks right of it follow during the next panel (look-ahead) ----
     if (b < 3) {
@@ -309,6 +344,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   // ---- W row 3 off the diagonal: the products with W_33 ----
   if (w >= 1) w_row3_finish(Wl, scr[w], w - 1, lane);
   __syncthreads();
+  WSTAMP(k0 / 64, 12);
   return bad;
 }
 
@@ -316,8 +352,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // The whole factorisation in ONE persistent launch (left-looking tiles,
 // device-scope flags instead of kernel boundaries).
 //
-// Workgroup 0 walks the diagonal -- the critical path -- and never waits for
-// a launch: for j = 0, 1, ...
+// The first workgroup to START walks the diagonal -- the critical path --
+// and never waits for a launch: for j = 0, 1, ...
 //   T_jj (updated by the helpers for k <= j-2)  -= L_j,j-1 L_j,j-1^T
 //   POTRF -> L_jj, W_j = L_jj^-1
 //   L_j+1,j = T_j+1,j W_j^T  (kept in LDS for the next update)
@@ -327,13 +363,18 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // (one update short) and (j+1, j) hand the partial tile to the walker
 // (flag P); every other tile finishes with its TRSM against W_j (F(j,j)).
 // Tickets are taken in an order in which every dependency was taken
-// earlier, all workgroups are co-resident (grid <= CU count, one per CU),
-// so the waits always drain; every wait is bounded anyway (a timeout sets
-// fail bit value 4; the back substitution's own timeout sets 2).
+// earlier, and roles go by start order, not by workgroup index (the walker
+// is whoever starts first, a helper takes a task only once running), so
+// every wait is on a workgroup that is already running: the grid finishes
+// even when other streams' kernels hold CUs and only part of it is resident
+// (it then runs slower, never deadlocks).  Every wait is bounded anyway (a
+// timeout sets fail bit value 4; the back substitution's own timeout sets 2).
 // Polls are relaxed agent-scope atomic loads (coherent across the XCDs'
 // L2s); the acquire fence comes once, after the flag is seen.  (An acquire
 // load per poll would invalidate the poller's L2 on every spin.)
-constexpr long kFlagSpins = 1L << 19;
+// 2^20 polls (each a memory round trip + a short sleep: ~1 s), long beyond
+// any co-running kernel of the library, short of a watchdog
+constexpr long kFlagSpins = 1L << 20;
 
 __device__ __forceinline__ bool spin_until(const int* f, int epoch) {
   long spins = 0;
@@ -361,6 +402,21 @@ __device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
   }
   __syncthreads();
+}
+
+// Wave 0 polls one flag, then the block proceeds WITHOUT an acquire: every
+// load of the handed-off bytes after it must be an sc1 load (ld_wt), and the
+// producer stored them sc1, drained every storing wave, then flagged from
+// one lane behind a barrier (MI355X_MICROARCH.md, hand-offs with sc1 loads
+// in place of the acquire; the acquire's L1 invalidate is ~1.5 us).
+__device__ __forceinline__ void block_poll(const int* f, int epoch, int* fail) {
+  if (wave0()) {
+    if (!spin_until(f, epoch)) atomicOr(fail, 4);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Write-through publication (MI355X_MICROARCH.md: a producer that stores
@@ -414,21 +470,56 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
   return b;
 }
 
+// W_j's entries a helper's TRSM reads (lane: W(16C + (lane & 15), k) for
+// k = 16M + 4s4 + (lane >> 4), C >= M; 40 values), handed off as data-tagged
+// granules (ba_device.h w_sentinel_fill): sc1 loads, repeated until none is
+// the sentinel.  No flag, no acquire, no drain on the walker.  False on a
+// timeout (the grid is then not co-resident: reported, never a hang).
+__device__ __forceinline__ void load_w_plain(const double* __restrict__ Wk, double (&wv)[40], int lane) {
+  const int li = lane & 15, kk = lane >> 4;
+  int q = 0;
+#pragma unroll
+  for (int M = 0; M < 4; ++M)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int C = M; C < 4; ++C, ++q) wv[q] = Wk[(16 * M + 4 * s4 + kk) * NB + 16 * C + li];
+}
+__device__ __forceinline__ bool load_w(const double* __restrict__ Wk, double (&wv)[40], int lane) {
+  const int li = lane & 15, kk = lane >> 4;
+  for (long spins = 0;; ++spins) {
+    bool miss = false;
+    int q = 0;
+#pragma unroll
+    for (int M = 0; M < 4; ++M)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int C = M; C < 4; ++C, ++q) {
+          wv[q] = ld_wt(Wk + (16 * M + 4 * s4 + kk) * NB + 16 * C + li);
+          miss |= __builtin_bit_cast(uint64_t, wv[q]) == kYSentinel;
+        }
+    if (__builtin_amdgcn_ballot_w64(miss) == 0) return true;
+    if (spins > kFlagSpins) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // The helpers' TRSM X = T W^T for U stacked tiles (T_u in LDS, W = L_jj^-1
-// lower triangular in global memory, column-major: W(c, m) at m*NB + c).
+// lower triangular, this lane's entries in wv from load_w).
 // Wave w takes row block w of every tile and forms X^T (column block C) =
 // sum_{M <= C} W_CM T_wM^T on MFMA: 40 MFMAs per tile instead of 64 (the
 // products with W's zero upper blocks are skipped; they came last in the
 // k order, so the sums are bitwise the full ones), the W operand shared by
 // the U tiles.  x[u][C] reg rr holds X(16w + (lane & 15), 16C + 4rr + (lane >> 4)).
 template <int U>
-__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double* __restrict__ Wk, f64x4 (*x)[4],
-                                          int lane) {
+__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double (&wv)[40], f64x4 (*x)[4], int lane) {
   const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int C = 0; C < 4; ++C) x[u][C] = f64x4{0.0, 0.0, 0.0, 0.0};
+  int q = 0;
 #pragma unroll
   for (int M = 0; M < 4; ++M)
 #pragma unroll
@@ -438,8 +529,8 @@ __device__ __forceinline__ void trsm_rows(const double* const* Tp, const double*
 #pragma unroll
       for (int u = 0; u < U; ++u) bt[u] = Tp[u][k * TS + 16 * w + li];
 #pragma unroll
-      for (int C = M; C < 4; ++C) {
-        const double a = Wk[k * NB + 16 * C + li];
+      for (int C = M; C < 4; ++C, ++q) {
+        const double a = wv[q];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u][C] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bt[u], x[u][C], 0, 0, 0);
       }
@@ -464,7 +555,7 @@ __device__ __forceinline__ void put_rows(double* __restrict__ A, int ld, int i0,
 // column (lane & 15) walks the tile's rows (128-B column runs of A).
 __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
-                                  int* sh, int* __restrict__ fail) {
+                                  int* sh, int* __restrict__ fail, int opt) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -529,11 +620,17 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
         T[(cb + 16 * a + lk + 4 * reg) * TS + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
-  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
-  const double* Wk = Winv + size_t(j) * NB * NB;
+  double wv[40];
+  if (opt & kOptWGran) {
+    if (!load_w(Winv + size_t(j) * NB * NB, wv, lane)) atomicOr(fail, 4);
+    __syncthreads();  // the LDS writes of T
+  } else {
+    block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+    load_w_plain(Winv + size_t(j) * NB * NB, wv, lane);
+  }
   const double* Tp[1] = {T};
   f64x4 x[1][4];
-  trsm_rows<1>(Tp, Wk, x, lane);
+  trsm_rows<1>(Tp, wv, x, lane);
   put_rows<1>(A, ld, i0, j0, x, lane);
   block_publish_wt(F + i * nb + j, epoch);
 }
@@ -548,7 +645,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld, int nb,
                                                   const double* __restrict__ Winv, int* __restrict__ F, int epoch,
                                                   int i, int j, double* T0, double* T1, int* sh,
-                                                  int* __restrict__ fail) {
+                                                  int* __restrict__ fail, int opt) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -602,11 +699,17 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
           Tu[c * TS + r] = A[size_t(j0 + c) * ld + iu + r] - acc[u][a][bb][reg];
         }
   }
-  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
-  const double* Wk = Winv + size_t(j) * NB * NB;
+  double wv[40];
+  if (opt & kOptWGran) {
+    if (!load_w(Winv + size_t(j) * NB * NB, wv, lane)) atomicOr(fail, 4);
+    __syncthreads();  // the LDS writes of T0, T1
+  } else {
+    block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+    load_w_plain(Winv + size_t(j) * NB * NB, wv, lane);
+  }
   const double* Tp[2] = {T0, T1};
   f64x4 x[2][4];
-  trsm_rows<2>(Tp, Wk, x, lane);
+  trsm_rows<2>(Tp, wv, x, lane);
   put_rows<2>(A, ld, i0, j0, x, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -655,44 +758,38 @@ __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) 
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) D[(16 * Cb + li) * TS + 16 * w + 4 * rr + kk] = x[Cb][rr];
 }
-__device__ __forceinline__ void load_tile(double* D, const double* __restrict__ A, int ld, int i0, int j0) {
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
-    D[c * TS + r] = A[size_t(j0 + c) * ld + i0 + r];
-  }
-}
-__device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i0, int j0, const double* D) {
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
-    A[size_t(j0 + c) * ld + i0 + r] = D[c * TS + r];
-  }
-}
-
 // The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
 // TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
 // When the POTRF's poll found the partial tiles (j+1, j) and (j+1, j+1)
-// already out, their loads are issued beside W_j's write-through stores and
-// share one drain with them; the stores of L_j+1,j drain during the next
-// step's first update, and their flag goes out after it.
+// already out, their loads are issued beside W_j's write-through stores.
+// Hand-offs on the walker's path carry no acquire (sc1 loads of the partial
+// tiles after a flag poll) and no drain: W_j goes out as data-tagged
+// granules (load_w), L_j+1,j is stored by waves 1-3, which drain during the
+// next step's panel 0 and flag it (potrf_tile).
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
-                             double* Ls, double (*scr)[256], int* rdy, int* __restrict__ fail) {
+                             double* Ls, double (*scr)[256], int* rdy, int* pub_cnt, int* __restrict__ fail,
+                             int opt) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const bool sc1 = opt & kOptSc1, wgran = opt & kOptWGran, lpub = opt & kOptLPub;
+  // loads of handed-off tiles: sc1 after a poll, or plain after an acquire
+  auto ldh = [&](const double* p) { return sc1 ? ld_wt(p) : *p; };
   // the next diagonal tile travels in registers (loaded one step ahead)
   double nx[16];
-  block_wait(Pf, epoch, fail);
+  if (t == 0) *pub_cnt = 0;
+  if (sc1) block_poll(Pf, epoch, fail);
+  else block_wait(Pf, epoch, fail);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    nx[q] = A[size_t(c) * ld + r];
+    nx[q] = ldh(A + size_t(c) * ld + r);
   }
   for (int j = 0; j < nb; ++j) {
     const int j0 = j * NB;
+    WSTAMP(j, 0);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
@@ -705,34 +802,38 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       // blocks right of it are updated inside potrf_tile, during panel 0
       const int Ib[1] = {w}, Jb[1] = {0};
       last_update<1>(T, Ls, Ib, Jb, 1, lane);
-      // L_j,j-1 (stored at the end of the last step) has drained: its flag
-      block_publish_wt(F + j * nb + j - 1, epoch);
+      if (lpub) __syncthreads();
+      else block_publish_wt(F + j * nb + j - 1, epoch);  // L_j,j-1 (stored at the end of the last step)
     }
+    WSTAMP(j, 1);
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
+    int* pub = (j > 0 && lpub) ? F + j * nb + j - 1 : nullptr;  // L_j,j-1, flagged by waves 1-3
     const bool more = j + 1 < nb;
     const int i0 = j0 + NB;
     const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
     const int* fdiag = more ? Pf + (j + 1) * nb + j + 1 : nullptr;
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
-                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pub, pub_cnt)
+                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pub, pub_cnt);
+    WSTAMP(j, 2);
     if (bad) atomicOr(fail, 1);
     const bool early = more && __builtin_amdgcn_readfirstlane(*rdy) != 0;
+    WSTAMPV(j, 7, early ? 1 : 0);
     double sub[16];
     if (early) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (!sc1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        sub[q] = A[size_t(j0 + c) * ld + i0 + r];
-        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        sub[q] = ldh(A + size_t(j0 + c) * ld + i0 + r);
+        nx[q] = ldh(A + size_t(i0 + c) * ld + i0 + r);
       }
     }
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      // lower 16x16 blocks only: the upper blocks of every W_k stay zero
-      // from set_problem (one memset), 37% fewer bytes on the chain
+      // lower 16x16 blocks only (the upper blocks stay zero from set_problem);
+      // each entry is its own flag (load_w): no drain, no flag
       if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
     if (early) {
@@ -744,9 +845,9 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
         T[c * TS + r] = sub[q];
       }
     }
-    // W_j out at once: the helpers' TRSMs of column j feed the last updates
-    // of the diagonal tiles two steps ahead (a chain as long as a step)
-    block_publish_wt(F + j * nb + j, epoch);
+    if (wgran) __syncthreads();
+    else block_publish_wt(F + j * nb + j, epoch);  // W_j out at once (the helpers' TRSMs of column j)
+    WSTAMP(j, 3);
     if (!more) {
       // L_jj is read by nobody (the helpers' TRSMs and the back substitution
       // use W_j; the next Schur pass rewrites the lower triangle) except in
@@ -763,25 +864,42 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     }
     if (!early) {
       // the poll missed: wait for the partial tiles here
-      block_wait(Pf + (j + 1) * nb + j, epoch, fail);
-      load_tile(T, A, ld, i0, j0);
-      block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+      if (sc1) block_poll(Pf + (j + 1) * nb + j, epoch, fail);
+      else block_wait(Pf + (j + 1) * nb + j, epoch, fail);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        T[c * TS + r] = ldh(A + size_t(j0 + c) * ld + i0 + r);
+      }
+      // (its barrier also closes T's writes)
+      if (sc1) block_poll(Pf + (j + 1) * nb + j + 1, epoch, fail);
+      else block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        nx[q] = ldh(A + size_t(i0 + c) * ld + i0 + r);
       }
     }
+    WSTAMP(j, 4);
     // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
     f64x4 x[4];
     trsm_lds(T, Wl, x, lane);
     put_tile(Ls, x, lane);
     __syncthreads();
+    WSTAMP(j, 5);
+    if (!lpub) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+      }
+    } else if (w > 0) {  // waves 1-3 store it (write-through); drained and flagged in the next step's panel 0
+      for (int e = t - 64; e < NB * NB; e += 192) {
+        const int c = e >> 6, r = e & 63;
+        st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+      }
     }
+    WSTAMP(j, 6);
   }
 }
 
@@ -789,21 +907,34 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
                                                     int epoch, int nhelp, int* __restrict__ fail,
-                                                    const int* __restrict__ gate) {
+                                                    const int* __restrict__ gate, int opt) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
   __shared__ double scr[4][256];
-  __shared__ int sh[2];
+  __shared__ int sh[3];
   if (gate && *gate == 0) {
     // device LM loop, phase skipped: the launch still takes its ntask + nhelp
-    // tickets, so the next epoch's ticket base stays (epoch - 1) (ntask + nhelp)
-    if (blockIdx.x == 0 && threadIdx.x == 0)
+    // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
+    // (epoch - 1) (ntask + nhelp) and (epoch - 1) (1 + nhelp)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       atomicAdd(ticket, (unsigned long long)(chol_tasks(nb) + nhelp));
+      atomicAdd(ticket + 1, (unsigned long long)(1 + nhelp));
+    }
     return;
   }
-  if (blockIdx.x == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
+  // role by start order: the first workgroup to run walks the diagonal
+  if (wave0()) {
+    const unsigned long long v = atomicAdd(ticket + 1, threadIdx.x == 0 ? 1ULL : 0ULL);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
+    const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
+    sh[1] = int(((unsigned long long)hi << 32 | lo) - (unsigned long long)(epoch - 1) * (unsigned long long)(1 + nhelp));
+  }
+  __syncthreads();
+  const int role = __builtin_amdgcn_readfirstlane(sh[1]);
+  __syncthreads();
+  if (role == 0) {
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, sh + 2, fail, opt);
     return;
   }
   const int ntask = chol_tasks(nb);
@@ -828,11 +959,11 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     int j = 0, r = tk;
     while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
     if (r < 3) {
-      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail, opt);
     } else {
       const int i = j + 3 + 2 * (r - 3);
-      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail);
-      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail);
+      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail, opt);
+      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail, opt);
     }
   }
 }
@@ -855,12 +986,22 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
-                                                   int* __restrict__ fail, const int* __restrict__ gate) {
-  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+                                                   int* __restrict__ fail, const int* __restrict__ gate,
+                                                   unsigned long long* __restrict__ rticket, int epoch) {
+  if (gate && *gate == 0) {  // device LM loop: phase skipped (its row tickets still taken)
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(rticket, (unsigned long long)nb);
+    return;
+  }
   __shared__ double v[NB];
   __shared__ double yl[2][NB];
   __shared__ int timed_out;
-  const int b = nb - 1 - int(blockIdx.x);  // the chain's first block is the first workgroup
+  __shared__ int row;
+  // block row by start order: the chain's first row goes to the first
+  // workgroup to run, so every row a workgroup awaits belongs to one that
+  // is already running (any residency, any dispatch order)
+  if (threadIdx.x == 0) row = int(atomicAdd(rticket, 1ULL) - (unsigned long long)(epoch - 1) * (unsigned long long)nb);
+  __syncthreads();
+  const int b = nb - 1 - __builtin_amdgcn_readfirstlane(row);
   const int k0 = b * NB;
   const int nreal = (n - k0) < NB ? (n - k0) : NB;
   const int t = threadIdx.x, col = t >> 2, seg = t & 3;
@@ -890,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
       lv[i + 1] = q.y;
     }
     double* yb = yl[k & 1];  // double-buffered: one barrier per block
-    if (wave0()) {  // scalar branch (see block_wait)
+    if (wave0()) {  // scalar branch (see wave0)
       const int lane = threadIdx.x & 63;
       const double* p = y + size_t(k) * NB + lane;
       double yv = 0.0;
@@ -937,18 +1078,36 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (the walker + helpers must be co-resident)
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+  static const int opt = [] {
+    const char* e = std::getenv("SFM_CHOL_OPT");
+    return e ? std::atoi(e) : (kOptSc1 | kOptWGran | kOptLPub);
+  }();
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
-                                         epoch, nhelp, d.fail, d.gate);
+                                         epoch, nhelp, d.fail, d.gate, opt);
 }
 
-void launch_backsolve(const DevProblem& d, int /*epoch*/, hipStream_t s, bool sentinel_set) {
+__global__ void k_w_sentinel(double* __restrict__ invL, int nblk) {
+  w_sentinel_fill(invL, nblk, blockIdx.x, gridDim.x, threadIdx.x, blockDim.x);
+}
+void launch_w_sentinel(const DevProblem& d, hipStream_t s) {
+  if (d.nblk > 0) k_w_sentinel<<<std::min(1024, d.nblk * 4), 256, 0, s>>>(d.invL, d.nblk);
+}
+
+void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
   const int nb_real = (d.n + NB - 1) / NB;
   if (nb_real <= 0) return;
   // the sentinel in every entry of y the launch produces (ld >= 64 nb_real;
   // the solve's k_pad_init writes it, saving a launch)
   if (!sentinel_set)
     (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
-  k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail, d.gate);
+  k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail, d.gate, d.cticket + 2, epoch);
 }
 
 }  // namespace sfm
+
+#ifdef SFM_CHOL_STAMPS
+extern "C" int sfm_debug_stamps(unsigned long long* out, int n) {
+  if (n > 256 * 16) n = 256 * 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_wstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
+}
+#endif

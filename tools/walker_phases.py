@@ -1,27 +1,36 @@
-"""Diagonal-walker phase times of the fused Cholesky at n=3000 from the
-stamped variant tools/var_ws.so (tools/mkvar.sh ws "$(cat tools/walker_stamp_patch.py)" chol_kernels.hip)."""
+"""Diagonal-walker phase times of the fused Cholesky from the stamped
+variant tools/var_stamps.so (tools/chol_stamps.sh).  Usage:
+  SFM_CHOL_OPT=<bits> python tools/walker_phases.py [n]"""
 import ctypes, os, sys
 import numpy as np
 R = os.environ.get('GRAFT_REPO_ROOT', os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, R)
-os.environ.setdefault("SFM_AMD_LIB", os.path.join(R, "tools", "var_ws.so"))
+os.environ.setdefault("SFM_AMD_LIB", os.path.join(R, "tools", "var_stamps.so"))
 from sfm_amd.ba import dense_spd_solve
-n = 3000
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
 rng = np.random.default_rng(n)
 B = rng.uniform(-1, 1, (n, n)); A = B + B.T; A[np.diag_indices(n)] += 2.0 * n; b = rng.standard_normal(n)
 y, ms, fail = dense_spd_solve(A, b, reps=3)
-print('ms', ms, 'fail', fail)
 L = ctypes.CDLL(os.environ["SFM_AMD_LIB"])
-buf = (ctypes.c_ulonglong * (64 * 16))()
-assert L.sfm_debug_stamps(buf, 64 * 16) == 0
-st = np.array(buf[:], dtype=np.float64).reshape(64, 16) / 100.0  # 100 MHz -> us
-nb = 47
-names = ["load+update", "potrf", "store+publish F(j,j)", "wait P(j+1,j)", "load+wait P(j+1,j+1)", "nx+trsm",
-         "store+publish F(j+1,j)"]
-d = {nm: np.mean([st[j, k + 1] - st[j, k] for j in range(1, nb - 2)]) for k, nm in enumerate(names)}
+buf = (ctypes.c_ulonglong * (256 * 16))()
+assert L.sfm_debug_stamps(buf, 256 * 16) == 0
+raw = np.array(buf[:], dtype=np.float64).reshape(256, 16)
+nb = (n + 1 + 63) // 64
+st = raw / 100.0  # 100 MHz -> us
+js = range(1, nb - 2)
+names = ["step start->LU done", "potrf", "early loads + W out", "fallback waits+loads", "trsm", "L stores issued",
+         "-> next step"]
+seg = {}
+for k, nm in enumerate(names[:-1]):
+    seg[nm] = np.mean([st[j, k + 1] - st[j, k] for j in js])
+seg[names[-1]] = np.mean([st[j + 1, 0] - st[j, 6] for j in js])
+early = np.mean([raw[j, 7] for j in js])
 step = np.mean(np.diff(st[1:nb - 2, 0]))
-print("per-step mean us:", {k: round(float(v), 2) for k, v in d.items()}, "step", round(float(step), 2))
-
-inner = [(1, 8, "panel0"), (8, 12, "trail0"), (12, 9, "panel1"), (9, 13, "trail1"), (13, 10, "panel2"),
-         (10, 14, "trail2"), (14, 11, "panel3"), (11, 15, "Wrow3"), (15, 2, "ret")]
-print("potrf inner us:", {nm: round(float(np.mean([st[j, b] - st[j, a] for j in range(1, nb - 2)])), 2) for a, b, nm in inner})
+inner = {"panel0": np.mean([st[j, 8] - st[j, 1] for j in js])}
+for b_ in range(1, 4):
+    inner[f"panel{b_}"] = np.mean([st[j, 8 + b_] - st[j, 7 + b_] for j in js])
+inner["Wrow3"] = np.mean([st[j, 12] - st[j, 11] for j in js])
+print(f"n={n} ms={ms:.3f} fail={fail} opt={os.environ.get('SFM_CHOL_OPT', 'default')} step={step:.2f} us "
+      f"early={early:.2f}")
+print("  walker:", {k: round(float(v), 2) for k, v in seg.items()})
+print("  potrf :", {k: round(float(v), 2) for k, v in inner.items()})
