@@ -635,7 +635,10 @@ def main() -> int:
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
     ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
     ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
-    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the C4 (strong-scaling N=1 point) leg")
+    ap.add_argument("--c4-n1", action="store_true",
+                    help="N=1: also measure BASELINE C4 on this GPU (the N=1 point of the strong-scaling curve the "
+                         "N>1 lines report; off by default so that a kernel trace of the default command holds the "
+                         "C3 headline's kernels only)")
     ap.add_argument("--comm", action="store_true",
                     help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
     ap.add_argument("--dry-run", action="store_true",
@@ -803,7 +806,7 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_oneshot:
         ba.close()  # the one-shot path keeps its own cached handle
         out["oneshot"] = oneshot_leg(sc)
-    if world == 1 and not explicit and not args.no_c4:
+    if world == 1 and not explicit and args.c4_n1:
         # the N = 1 point of the C4 strong-scaling curve (N > 1 lines report C4)
         if ba is not None:
             ba.close()

@@ -27,22 +27,15 @@ namespace sfm {
 __device__ unsigned long long g_wstamp[256 * 16];
 #define WSTAMP(j, k) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define WSTAMPV(j, k, v) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = (v); } while (0)
+// helpers' publication times: [i][j][0] partial tile (i, j) out, [1] final tile (i, j) out
+__device__ unsigned long long g_hstamp[64 * 64 * 2];
+#define HSTAMP(i, j, k) do { if (threadIdx.x == 0 && (i) < 64 && (j) < 64) g_hstamp[((i) * 64 + (j)) * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define HSTAMP(i, j, k) do { } while (0)
 #define WSTAMP(j, k) do { } while (0)
 #define WSTAMPV(j, k, v) do { } while (0)
 #endif
 namespace {
-
-// Hand-off forms of the fused Cholesky (kernel argument `opt`, SFM_CHOL_OPT;
-// A/B of the protocol choices on one box):
-//   kOptSc1   the walker loads handed-off tiles with sc1 loads after a flag
-//             poll (no acquire); else acquire + plain loads
-//   kOptWGran W_j as data-tagged granules (load_w); else stores + drain +
-//             flag F(j,j) and an acquire in the helpers
-//   kOptLPub  L_j+1,j stored by waves 1-3, drained and flagged during the
-//             next step's panel 0; else every wave stores and the block
-//             drains and flags after the next step's first update
-constexpr int kOptSc1 = 1, kOptWGran = 2, kOptLPub = 4;
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int NB = kNB;  // 64
@@ -173,6 +166,50 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
   for (int rr = 0; rr < 4; ++rr) T[(16 * J + j) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
 }
 
+// 2^20 polls (each a memory round trip + a short sleep: ~1 s), long beyond
+// any co-running kernel of the library, short of a watchdog
+constexpr long kFlagSpins = 1L << 20;
+
+__device__ __forceinline__ bool spin_until(const int* f, int epoch) {
+  long spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    if (++spins > kFlagSpins) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// Branches around barriers are kept SCALAR: "this is wave 0" is tested on
+// readfirstlane(threadIdx.x) (an SGPR), and everything inside runs on all 64
+// lanes (same flag, same value).  A per-lane `if (threadIdx.x == 0)` inside a
+// loop that also holds barriers lets the compiler split the loop by lane
+// masks, so that lanes 1..63 of wave 0 pass the barrier without lane 0
+// (seen on gfx950: a hang on a stale ticket).
+__device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64; }
+
+// Wave 0 polls one flag, then the block proceeds WITHOUT an acquire: every
+// load of the handed-off bytes after it must be an sc1 load (ld_wt), and the
+// producer stored them sc1, drained every storing wave, then flagged from
+// one lane behind a barrier (MI355X_MICROARCH.md, hand-offs with sc1 loads
+// in place of the acquire; the acquire's L1 invalidate is ~1.5 us).
+__device__ __forceinline__ void block_poll(const int* f, int epoch, int* fail) {
+  if (wave0()) {
+    if (!spin_until(f, epoch)) atomicOr(fail, 4);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Write-through publication (MI355X_MICROARCH.md: a producer that stores
+// every handed-off byte sc1 and drains every wave before the flag needs no
+// agent release; the consumers keep their acquire): every tile the walker
+// and the helpers hand off, so no publication pays an L2 write-back (the
+// release form, buffer_wbl2 + drain, wrote back the XCD's whole L2).
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // The factorisation proper, on the tile image T in LDS (256 threads; Wl is
 // cleared here).  Returns this thread's bad-pivot flag; ends with a barrier.
 // Ls != nullptr: the walker's last update of the blocks right of column
@@ -180,18 +217,70 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
 // waves 1-3 apply it while wave 0 factors panel 0, before the trailing
 // update of panel 0 touches those blocks (every block keeps its update
 // order: bitwise the same factor).
-// pf_sub != nullptr: wave 3 polls the flags of the walker's next two
-// partial tiles once during panel 3 and leaves in *rdy whether both are out,
-// so the walker can load them beside W_j's publication (a poll during panel
-// 2 mostly came too early: the tile (j+1, j) waits for L_j,j-1).
-// pub_flag != nullptr: waves 1-3 stored L_j,j-1 (the walker's last TRSM
-// result) at the end of the previous step; each drains its own stores during
-// panel 0 and counts itself in pub_cnt (LDS), the last one raises the flag,
-// so wave 0 -- the pivot chain -- never waits for the write-through stores.
+// io.pub_flag != nullptr: waves 1-3 stored L_j,j-1 (the walker's last TRSM
+// result) at the end of the previous step; each drains its own stores at the
+// start of panel 0 and counts itself in io.pub_cnt (LDS), the last one raises
+// the flag, so wave 0 -- the pivot chain -- never waits for the write-through
+// stores.
+// io.sub / io.diag: the walker's next two partial tiles, (j+1, j) and
+// (j+1, j+1); waves 1-3 poll their flags after their chores of panels 1-3 and
+// copy their third of a tile into LDS (sc1 loads) as soon as it is out, so
+// its load latency hides under the pivot chain (the walker finishes what is
+// left after the POTRF).
+struct PartialTile {
+  const int* flag = nullptr;    // nullptr: nothing to fetch
+  const double* src = nullptr;  // tile in A (column-major, ld)
+  double* dst = nullptr;        // LDS image (TS stride)
+  bool got = false;             // this wave's share is in LDS (wave-uniform)
+};
+struct WalkerIO {
+  int ld = 0, epoch = 0;
+  int* pub_flag = nullptr;
+  int* pub_cnt = nullptr;
+  PartialTile sub, diag;
+};
+
+// Wave w (1..3) copies columns w-1, w+2, ... of a handed-off tile into LDS
+// with sc1 loads (every load of the hand-off is sc1: no acquire needed).
+// Running addresses, made opaque per call: per-column offsets would be
+// loop invariants of the walker, and hoisting 2 x 22 of them out of its loop
+// spilled the kernel's registers.
+__device__ __forceinline__ void fetch_third(const double* __restrict__ src, int ld, double* dst, int w, int lane) {
+  const double* p = src + size_t(w - 1) * ld + lane;
+  int o = (w - 1) * TS + lane;
+  asm volatile("" : "+v"(p), "+v"(o));
+  const size_t step = size_t(3) * ld;
+  const int nc = (NB - (w - 1) + 2) / 3;  // 22 or 21 columns
+  double v[22];
+#pragma unroll
+  for (int m = 0; m < 22; ++m) {
+    v[m] = m < nc ? ld_wt(p) : 0.0;
+    p += step;
+  }
+#pragma unroll
+  for (int m = 0; m < 22; ++m) {
+    if (m < nc) dst[o] = v[m];
+    o += 3 * TS;
+  }
+}
+// Non-blocking: fetch this wave's share if the tile's flag is out.
+__device__ __forceinline__ void try_fetch(PartialTile& pt, int ld, int epoch, int w, int lane) {
+  if (pt.flag == nullptr || pt.got) return;
+  if (__hip_atomic_load(pt.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) return;
+  fetch_third(pt.src, ld, pt.dst, w, lane);
+  pt.got = true;
+}
+// Blocking: wait for the flag (bounded), then fetch this wave's share.
+__device__ __forceinline__ void must_fetch(PartialTile& pt, int ld, int epoch, int w, int lane, int* fail) {
+  if (pt.flag == nullptr || pt.got) return;
+  if (!spin_until(pt.flag, epoch)) atomicOr(fail, 4);
+  fetch_third(pt.src, ld, pt.dst, w, lane);
+  pt.got = true;
+}
+
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
 __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
-                                           const double* Ls, const int* pf_sub, const int* pf_diag, int epoch,
-                                           int* rdy, int* pub_flag, int* pub_cnt) {
+                                           const double* Ls, WalkerIO& io) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -209,7 +298,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       // L(g0+c, g)), so one FMA stream updates both -- half the pivot work of
       // the separate wc[] registers.  Their T writes land in the tile's
       // strictly upper part, which nothing reads.
-      const int r = lane;
+      int r = lane;
+      asm volatile("" : "+v"(r));  // (no loop-invariant identity rows hoisted out of the walker's loop)
       const bool wl = r < 16;
       double p[16];
 #pragma unroll
@@ -252,7 +342,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = p[c];
     } else if (w == 0) {
       // ---- panel 0 factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
-      const int r = lane;
+      int r = lane;
+      asm volatile("" : "+v"(r));
       double p[16], wc[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -299,38 +390,43 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 #pragma unroll
         for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = wc[c];
     } else if (b == 0) {
+      if (io.pub_flag != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // every lane adds (lane 0 one, the rest zero): the count is uniform
+        const int old = __builtin_amdgcn_readfirstlane(atomicAdd(io.pub_cnt, (t & 63) == 0 ? 1 : 0));
+        if (old == 2) {  // the third of waves 1-3
+          *io.pub_cnt = 0;
+          __hip_atomic_store(io.pub_flag, io.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       if (Ls != nullptr) {
         // deferred last update: wave 1 blocks (1,1) (2,2), wave 2 (2,1) (3,2),
         // wave 3 (3,1) (3,3)  [(I, J)]
         const int Ib[2] = {w, w + 1 < 4 ? w + 1 : 3}, Jb[2] = {1, w == 1 ? 2 : (w == 2 ? 2 : 3)};
         last_update<2>(T, Ls, Ib, Jb, 2, lane);
       }
-      if (pub_flag != nullptr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // every lane adds (lane 0 one, the rest zero): the count is uniform
-        const int old = __builtin_amdgcn_readfirstlane(atomicAdd(pub_cnt, (t & 63) == 0 ? 1 : 0));
-        if (old == 2) {  // the third of waves 1-3
-          *pub_cnt = 0;
-          __hip_atomic_store(pub_flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
     } else if (b == 1) {
       // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
       trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
-    } else if (b == 2 && w == 1) {
-      w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
-    } else if (b == 2 && w == 3) {
-      trail_block(T, 16, 3, 3, lane);  // panel 1's trailing update of block (3,3)
+      // (Ls is read by nobody from here on: the sub tile may land on it)
+      try_fetch(io.diag, io.ld, io.epoch, w, lane);
+      try_fetch(io.sub, io.ld, io.epoch, w, lane);
+    } else if (b == 2) {
+      if (w == 1) w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
+      if (w == 3) trail_block(T, 16, 3, 3, lane);       // panel 1's trailing update of block (3,3)
+      try_fetch(io.diag, io.ld, io.epoch, w, lane);
+      try_fetch(io.sub, io.ld, io.epoch, w, lane);
     } else if (b == 3) {
       // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
+      try_fetch(io.diag, io.ld, io.epoch, w, lane);
+      try_fetch(io.sub, io.ld, io.epoch, w, lane);
       if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
-      if (w == 3 && pf_sub != nullptr)
-        *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      try_fetch(io.diag, io.ld, io.epoch, w, lane);
+      try_fetch(io.sub, io.ld, io.epoch, w, lane);
     }
     __syncthreads();
     WSTAMP(k0 / 64, 8 + b);
@@ -372,61 +468,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // Polls are relaxed agent-scope atomic loads (coherent across the XCDs'
 // L2s); the acquire fence comes once, after the flag is seen.  (An acquire
 // load per poll would invalidate the poller's L2 on every spin.)
-// 2^20 polls (each a memory round trip + a short sleep: ~1 s), long beyond
-// any co-running kernel of the library, short of a watchdog
-constexpr long kFlagSpins = 1L << 20;
-
-__device__ __forceinline__ bool spin_until(const int* f, int epoch) {
-  long spins = 0;
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-    if (++spins > kFlagSpins) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
-
-// Branches around barriers are kept SCALAR: "this is wave 0" is tested on
-// readfirstlane(threadIdx.x) (an SGPR), and everything inside runs on all 64
-// lanes (same flag, same value).  A per-lane `if (threadIdx.x == 0)` inside a
-// loop that also holds barriers lets the compiler split the loop by lane
-// masks, so that lanes 1..63 of wave 0 pass the barrier without lane 0
-// (seen on gfx950: a hang on a stale ticket).
-__device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64; }
-
-// Wave 0 waits for one flag, then the block proceeds (acquire by wave 0; the
-// barrier orders the other waves' loads after it).
-__device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
-  if (wave0()) {
-    if (!spin_until(f, epoch)) atomicOr(fail, 4);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
-  }
-  __syncthreads();
-}
-
-// Wave 0 polls one flag, then the block proceeds WITHOUT an acquire: every
-// load of the handed-off bytes after it must be an sc1 load (ld_wt), and the
-// producer stored them sc1, drained every storing wave, then flagged from
-// one lane behind a barrier (MI355X_MICROARCH.md, hand-offs with sc1 loads
-// in place of the acquire; the acquire's L1 invalidate is ~1.5 us).
-__device__ __forceinline__ void block_poll(const int* f, int epoch, int* fail) {
-  if (wave0()) {
-    if (!spin_until(f, epoch)) atomicOr(fail, 4);
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Write-through publication (MI355X_MICROARCH.md: a producer that stores
-// every handed-off byte sc1 and drains every wave before the flag needs no
-// agent release; the consumers keep their acquire): every tile the walker
-// and the helpers hand off, so no publication pays an L2 write-back (the
-// release form, buffer_wbl2 + drain, wrote back the XCD's whole L2).
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void block_publish_wt(int* f, int epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -470,56 +511,48 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
   return b;
 }
 
-// W_j's entries a helper's TRSM reads (lane: W(16C + (lane & 15), k) for
-// k = 16M + 4s4 + (lane >> 4), C >= M; 40 values), handed off as data-tagged
-// granules (ba_device.h w_sentinel_fill): sc1 loads, repeated until none is
-// the sentinel.  No flag, no acquire, no drain on the walker.  False on a
-// timeout (the grid is then not co-resident: reported, never a hang).
-__device__ __forceinline__ void load_w_plain(const double* __restrict__ Wk, double (&wv)[40], int lane) {
-  const int li = lane & 15, kk = lane >> 4;
-  int q = 0;
-#pragma unroll
-  for (int M = 0; M < 4; ++M)
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-      for (int C = M; C < 4; ++C, ++q) wv[q] = Wk[(16 * M + 4 * s4 + kk) * NB + 16 * C + li];
-}
-__device__ __forceinline__ bool load_w(const double* __restrict__ Wk, double (&wv)[40], int lane) {
-  const int li = lane & 15, kk = lane >> 4;
+// W_j into LDS for a helper's TRSM: its lower 16x16 blocks (10 entries per
+// thread), handed off as data-tagged granules (ba_device.h w_sentinel_fill):
+// sc1 loads, repeated until none is the sentinel.  No flag, no acquire, no
+// drain on the walker.  Ends with a barrier.  A timeout sets fail bit 4 (the
+// grid is then not making progress: reported, never a hang).
+__device__ __forceinline__ void stage_w(const double* __restrict__ Wk, double* Wd, int* fail) {
+  const int t = threadIdx.x;
   for (long spins = 0;; ++spins) {
     bool miss = false;
-    int q = 0;
 #pragma unroll
-    for (int M = 0; M < 4; ++M)
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int C = M; C < 4; ++C, ++q) {
-          wv[q] = ld_wt(Wk + (16 * M + 4 * s4 + kk) * NB + 16 * C + li);
-          miss |= __builtin_bit_cast(uint64_t, wv[q]) == kYSentinel;
-        }
-    if (__builtin_amdgcn_ballot_w64(miss) == 0) return true;
-    if (spins > kFlagSpins) return false;
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      if ((r >> 4) >= (c >> 4)) {
+        const double v = ld_wt(Wk + c * NB + r);
+        miss |= __builtin_bit_cast(uint64_t, v) == kYSentinel;
+        Wd[c * TS + r] = v;
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(miss) == 0) break;
+    if (spins > kFlagSpins) {
+      atomicOr(fail, 4);
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
+  __syncthreads();
 }
 
-// The helpers' TRSM X = T W^T for U stacked tiles (T_u in LDS, W = L_jj^-1
-// lower triangular, this lane's entries in wv from load_w).
+// The helpers' TRSM X = T W^T for U stacked tiles (T_u and W = L_jj^-1,
+// lower triangular, in LDS).
 // Wave w takes row block w of every tile and forms X^T (column block C) =
 // sum_{M <= C} W_CM T_wM^T on MFMA: 40 MFMAs per tile instead of 64 (the
 // products with W's zero upper blocks are skipped; they came last in the
 // k order, so the sums are bitwise the full ones), the W operand shared by
 // the U tiles.  x[u][C] reg rr holds X(16w + (lane & 15), 16C + 4rr + (lane >> 4)).
 template <int U>
-__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double (&wv)[40], f64x4 (*x)[4], int lane) {
+__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double* Wd, f64x4 (*x)[4], int lane) {
   const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int C = 0; C < 4; ++C) x[u][C] = f64x4{0.0, 0.0, 0.0, 0.0};
-  int q = 0;
 #pragma unroll
   for (int M = 0; M < 4; ++M)
 #pragma unroll
@@ -529,8 +562,8 @@ __device__ __forceinline__ void trsm_rows(const double* const* Tp, const double 
 #pragma unroll
       for (int u = 0; u < U; ++u) bt[u] = Tp[u][k * TS + 16 * w + li];
 #pragma unroll
-      for (int C = M; C < 4; ++C, ++q) {
-        const double a = wv[q];
+      for (int C = M; C < 4; ++C) {
+        const double a = Wd[k * TS + 16 * C + li];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u][C] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bt[u], x[u][C], 0, 0, 0);
       }
@@ -555,7 +588,7 @@ __device__ __forceinline__ void put_rows(double* __restrict__ A, int ld, int i0,
 // column (lane & 15) walks the tile's rows (128-B column runs of A).
 __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
-                                  int* sh, int* __restrict__ fail, int opt) {
+                                  double* Wd, int* sh, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -610,6 +643,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
             st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr, cv[a][bb][reg] - acc[a][bb][reg]);
     }
     block_publish_wt(Pf + i * nb + j, epoch);
+    HSTAMP(i, j, 0);
     return;
   }
   // final tile: T -> LDS, then X = T W_j^T on MFMA once W_j is out
@@ -620,19 +654,13 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
         T[(cb + 16 * a + lk + 4 * reg) * TS + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
-  double wv[40];
-  if (opt & kOptWGran) {
-    if (!load_w(Winv + size_t(j) * NB * NB, wv, lane)) atomicOr(fail, 4);
-    __syncthreads();  // the LDS writes of T
-  } else {
-    block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
-    load_w_plain(Winv + size_t(j) * NB * NB, wv, lane);
-  }
+  stage_w(Winv + size_t(j) * NB * NB, Wd, fail);  // (its barrier also closes the LDS writes of T)
   const double* Tp[1] = {T};
   f64x4 x[1][4];
-  trsm_rows<1>(Tp, wv, x, lane);
+  trsm_rows<1>(Tp, Wd, x, lane);
   put_rows<1>(A, ld, i0, j0, x, lane);
   block_publish_wt(F + i * nb + j, epoch);
+  HSTAMP(i, j, 1);
 }
 
 // Helper: the vertical pair of final tiles (i, j), (i+1, j) (i >= j + 2).
@@ -645,7 +673,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld, int nb,
                                                   const double* __restrict__ Winv, int* __restrict__ F, int epoch,
                                                   int i, int j, double* T0, double* T1, int* sh,
-                                                  int* __restrict__ fail, int opt) {
+                                                  double* Wd, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -699,23 +727,18 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
           Tu[c * TS + r] = A[size_t(j0 + c) * ld + iu + r] - acc[u][a][bb][reg];
         }
   }
-  double wv[40];
-  if (opt & kOptWGran) {
-    if (!load_w(Winv + size_t(j) * NB * NB, wv, lane)) atomicOr(fail, 4);
-    __syncthreads();  // the LDS writes of T0, T1
-  } else {
-    block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
-    load_w_plain(Winv + size_t(j) * NB * NB, wv, lane);
-  }
+  stage_w(Winv + size_t(j) * NB * NB, Wd, fail);  // (its barrier also closes the LDS writes of T0, T1)
   const double* Tp[2] = {T0, T1};
   f64x4 x[2][4];
-  trsm_rows<2>(Tp, wv, x, lane);
+  trsm_rows<2>(Tp, Wd, x, lane);
   put_rows<2>(A, ld, i0, j0, x, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (wave0()) {
     __hip_atomic_store(F + i * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F + (i + 1) * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    HSTAMP(i, j, 1);
+    HSTAMP(i + 1, j, 1);
   }
 }
 
@@ -760,94 +783,74 @@ __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) 
 }
 // The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
 // TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
-// When the POTRF's poll found the partial tiles (j+1, j) and (j+1, j+1)
-// already out, their loads are issued beside W_j's write-through stores.
-// Hand-offs on the walker's path carry no acquire (sc1 loads of the partial
-// tiles after a flag poll) and no drain: W_j goes out as data-tagged
-// granules (load_w), L_j+1,j is stored by waves 1-3, which drain during the
-// next step's panel 0 and flag it (potrf_tile).
+// Hand-offs on the walker's path carry no acquire and no drain:
+//   * the partial tiles (j+1, j) and (j+1, j+1) are copied into LDS by waves
+//     1-3 during the POTRF as soon as their flags are out (sc1 loads;
+//     potrf_tile), the sub tile onto L_j,j-1's buffer once the last update
+//     has read it, the next diagonal tile into the buffer the next step
+//     factors (the two tile buffers swap);
+//   * W_j goes out as data-tagged granules (stage_w);
+//   * L_j+1,j is stored by waves 1-3, which drain and flag it at the start of
+//     the next step's panel 0.
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
-                             int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
-                             double* Ls, double (*scr)[256], int* rdy, int* pub_cnt, int* __restrict__ fail,
-                             int opt) {
+                                             int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* Ta,
+                                             double* Tb, double* Wl, double* Ls, double (*scr)[256], int* pub_cnt,
+                                             int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const bool sc1 = opt & kOptSc1, wgran = opt & kOptWGran, lpub = opt & kOptLPub;
-  // loads of handed-off tiles: sc1 after a poll, or plain after an acquire
-  auto ldh = [&](const double* p) { return sc1 ? ld_wt(p) : *p; };
-  // the next diagonal tile travels in registers (loaded one step ahead)
-  double nx[16];
+  double* T = Ta;   // the tile being factored
+  double* Tn = Tb;  // the next diagonal tile (prefetched)
   if (t == 0) *pub_cnt = 0;
-  if (sc1) block_poll(Pf, epoch, fail);
-  else block_wait(Pf, epoch, fail);
+  // tile (0, 0): every wave fetches its columns after the flag
+  block_poll(Pf, epoch, fail);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    nx[q] = ldh(A + size_t(c) * ld + r);
+    T[c * TS + r] = ld_wt(A + size_t(c) * ld + r);
   }
+  __syncthreads();
   for (int j = 0; j < nb; ++j) {
     const int j0 = j * NB;
     WSTAMP(j, 0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      T[c * TS + r] = nx[q];
-    }
-    if (t == 0) *rdy = 0;
-    __syncthreads();
     if (j > 0) {
       // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
       // blocks right of it are updated inside potrf_tile, during panel 0
       const int Ib[1] = {w}, Jb[1] = {0};
       last_update<1>(T, Ls, Ib, Jb, 1, lane);
-      if (lpub) __syncthreads();
-      else block_publish_wt(F + j * nb + j - 1, epoch);  // L_j,j-1 (stored at the end of the last step)
+      __syncthreads();
     }
     WSTAMP(j, 1);
-    const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
-    int* pub = (j > 0 && lpub) ? F + j * nb + j - 1 : nullptr;  // L_j,j-1, flagged by waves 1-3
     const bool more = j + 1 < nb;
     const int i0 = j0 + NB;
-    const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
-    const int* fdiag = more ? Pf + (j + 1) * nb + j + 1 : nullptr;
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pub, pub_cnt)
-                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pub, pub_cnt);
+    WalkerIO io;
+    io.ld = ld;
+    io.epoch = epoch;
+    if (j > 0) {  // L_j,j-1, stored by waves 1-3 at the end of the last step
+      io.pub_flag = F + j * nb + j - 1;
+      io.pub_cnt = pub_cnt;
+    }
+    if (more && w > 0) {
+      io.sub = PartialTile{Pf + (j + 1) * nb + j, A + size_t(j0) * ld + i0, Ls, false};
+      io.diag = PartialTile{Pf + (j + 1) * nb + j + 1, A + size_t(i0) * ld + i0, Tn, false};
+    }
+    const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, io)
+                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, io);
     WSTAMP(j, 2);
     if (bad) atomicOr(fail, 1);
-    const bool early = more && __builtin_amdgcn_readfirstlane(*rdy) != 0;
-    WSTAMPV(j, 7, early ? 1 : 0);
-    double sub[16];
-    if (early) {
-      if (!sc1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        sub[q] = ldh(A + size_t(j0 + c) * ld + i0 + r);
-        nx[q] = ldh(A + size_t(i0 + c) * ld + i0 + r);
-      }
-    }
+    // W_j out: lower 16x16 blocks only (the upper blocks stay zero from
+    // set_problem); each entry is its own flag (stage_w): no drain, no flag
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      // lower 16x16 blocks only (the upper blocks stay zero from set_problem);
-      // each entry is its own flag (load_w): no drain, no flag
       if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
-    if (early) {
-      // T (L_jj) is read by nobody from here on (see below): it takes the
-      // subdiagonal tile
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        T[c * TS + r] = sub[q];
-      }
-    }
-    if (wgran) __syncthreads();
-    else block_publish_wt(F + j * nb + j, epoch);  // W_j out at once (the helpers' TRSMs of column j)
-    WSTAMP(j, 3);
+#ifdef SFM_CHOL_STAMPS
+    if (t == 64 && j < 256) g_wstamp[j * 16 + 7] = (io.sub.got ? 1 : 0) + (io.diag.got ? 2 : 0);  // wave 1's view
+#endif
     if (!more) {
       // L_jj is read by nobody (the helpers' TRSMs and the back substitution
       // use W_j; the next Schur pass rewrites the lower triangle) except in
@@ -862,44 +865,30 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       }
       break;
     }
-    if (!early) {
-      // the poll missed: wait for the partial tiles here
-      if (sc1) block_poll(Pf + (j + 1) * nb + j, epoch, fail);
-      else block_wait(Pf + (j + 1) * nb + j, epoch, fail);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        T[c * TS + r] = ldh(A + size_t(j0 + c) * ld + i0 + r);
-      }
-      // (its barrier also closes T's writes)
-      if (sc1) block_poll(Pf + (j + 1) * nb + j + 1, epoch, fail);
-      else block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        nx[q] = ldh(A + size_t(i0 + c) * ld + i0 + r);
-      }
+    // what the POTRF's polls did not catch (waves 1-3, their own shares)
+    if (w > 0) {
+      must_fetch(io.sub, ld, epoch, w, lane, fail);
+      must_fetch(io.diag, ld, epoch, w, lane, fail);
     }
-    WSTAMP(j, 4);
-    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
+    __syncthreads();
+    WSTAMP(j, 3);
+    // subdiagonal tile: L_j+1,j = T_j+1,j W_j^T in place (wave w reads and
+    // writes only row block w of it), kept as Ls for the next update
     f64x4 x[4];
-    trsm_lds(T, Wl, x, lane);
+    trsm_lds(Ls, Wl, x, lane);
     put_tile(Ls, x, lane);
     __syncthreads();
     WSTAMP(j, 5);
-    if (!lpub) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
-      }
-    } else if (w > 0) {  // waves 1-3 store it (write-through); drained and flagged in the next step's panel 0
+    if (w > 0) {  // waves 1-3 store it (write-through); drained and flagged in the next step's panel 0
       for (int e = t - 64; e < NB * NB; e += 192) {
         const int c = e >> 6, r = e & 63;
         st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
       }
     }
     WSTAMP(j, 6);
+    double* tmp = T;
+    T = Tn;
+    Tn = tmp;
   }
 }
 
@@ -907,10 +896,11 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
                                                     int epoch, int nhelp, int* __restrict__ fail,
-                                                    const int* __restrict__ gate, int opt) {
+                                                    const int* __restrict__ gate) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
+  __shared__ double Tn[NB * TS];  // the walker's second diagonal-tile buffer
   __shared__ double scr[4][256];
   __shared__ int sh[3];
   if (gate && *gate == 0) {
@@ -934,7 +924,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, sh + 2, fail, opt);
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Tn, Wl, Ls, scr, sh + 2, fail);
     return;
   }
   const int ntask = chol_tasks(nb);
@@ -959,11 +949,11 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     int j = 0, r = tk;
     while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
     if (r < 3) {
-      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail, opt);
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, Ls, sh, fail);
     } else {
       const int i = j + 3 + 2 * (r - 3);
-      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail, opt);
-      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail, opt);
+      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, Ls, fail);
+      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, Ls, sh, fail);
     }
   }
 }
@@ -1078,12 +1068,8 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (the walker + helpers must be co-resident)
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
-  static const int opt = [] {
-    const char* e = std::getenv("SFM_CHOL_OPT");
-    return e ? std::atoi(e) : (kOptSc1 | kOptWGran | kOptLPub);
-  }();
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
-                                         epoch, nhelp, d.fail, d.gate, opt);
+                                         epoch, nhelp, d.fail, d.gate);
 }
 
 __global__ void k_w_sentinel(double* __restrict__ invL, int nblk) {
@@ -1109,5 +1095,9 @@ void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentin
 extern "C" int sfm_debug_stamps(unsigned long long* out, int n) {
   if (n > 256 * 16) n = 256 * 16;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_wstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
+}
+extern "C" int sfm_debug_hstamps(unsigned long long* out, int n) {
+  if (n > 64 * 64 * 2) n = 64 * 64 * 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_hstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
 }
 #endif

@@ -12,14 +12,23 @@ PnP, the device map store and the BA, on synthetic detector output.
   adjusted keyframe poses and map points match the stream's ground truth
   after a similarity alignment (the reference's BA holds no block constant,
   CTracker.cpp:670-702, so the gauge floats)."""
+import json
+import os
+
 import numpy as np
 import pytest
 
+import lm_cases as L
 from oracle import ffi as O
 from sfm_amd.live import KeypointStream, LiveSfM, _project
 from sfm_amd.mapping import _rodrigues
 
 pytestmark = pytest.mark.gpu
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+
+
+def _residuals(uv, cam_idx, pt_idx, K, rot, t, X):
+    return O.residuals_jacobians(uv, cam_idx, pt_idx, K, rot, t, X, jacobian=False)[0]
 
 
 def _rel(a, b, floor=1e-3):
@@ -137,6 +146,7 @@ def test_live_path_on_device_brisk_detections(run_brisk):
     assert [f.no for f in s.kfs][:4] == [0, 5, 15, 25]
     assert s.map.size()[0] > 1000
     rng = np.random.default_rng(0)
+    table = []
     for k, rec in enumerate(s.ba_log):
         r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
         sm_o, _ = O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], r, t, X)
@@ -152,15 +162,30 @@ def test_live_path_on_device_brisk_detections(run_brisk):
         sens_x = _rel(Xp, X)
         d = abs(rec["summary"].final_cost - sm_o["final_cost"]) / sm_o["final_cost"]
         dx = _rel(rec["X_out"], X)
+        # gauge-invariant distances of the two solutions (SURVEY.md §7 hard
+        # part 2): per-observation residuals (px) and camera centres + points
+        # after a Sim(3) alignment
+        sc_ = type("S", (), dict(uv=rec["uv"], cam_idx=rec["cam_idx"], pt_idx=rec["pt_idx"], K=rec["K"]))
+        res, al = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]), (r, t, X))
+        table.append(dict(ba=k, obs=len(rec["uv"]), iterations=sm_o["num_iterations"],
+                          termination=sm_o["termination_type"], cost_rel=d, cost_sensitivity=sens, X_rel=dx,
+                          X_sensitivity=sens_x, residual_max_px=res, sim3_aligned_rel=al))
         print(f"keyframe BA {k}: {len(rec['uv'])} obs, iterations {sm_o['num_iterations']} "
               f"({sm_o['termination_type']}), cost rel diff {d:.2e} (oracle rounding sensitivity {sens:.2e}), "
-              f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e})")
+              f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e}), residuals {res:.1e} px, Sim(3)-aligned {al:.1e}")
         assert rec["summary"].num_iterations == sm_o["num_iterations"]
         # (measured: BA 0-2 agree to 3e-14 in cost / 3e-7 in X; BA 3 runs
         # into the 50-iteration cap along a flat direction, where 2 ulp of
-        # start perturbation move the oracle's own result by 8e-9 in cost)
-        assert d <= max(1e-9, 20 * sens), (k, d, sens)
-        assert dx <= max(1e-6, 20 * sens_x), (k, dx, sens_x)
+        # start perturbation move the oracle's own result by 8e-9 in cost).
+        # The rounding-sensitivity allowance is capped: cost 1e-6, X 1e-5
+        # relative whatever the sensitivity (north-star tolerance 1e-6).
+        assert d <= min(1e-6, max(1e-9, 20 * sens)), (k, d, sens)
+        assert dx <= min(1e-5, max(1e-6, 20 * sens_x)), (k, dx, sens_x)
+        assert res <= 1e-6 and al <= 1e-6, (k, res, al)
+    # the per-keyframe table (committed as profiles/r04_live_brisk_ba_parity.json)
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, "live_brisk_ba_parity.json"), "w") as f:
+        json.dump(table, f, indent=1)
     # The scene is one textured plane at depth 10 seen over 0.1-0.3-unit
     # baselines, where a lateral translation and a small rotation move the
     # image almost alike: the camera centres alone are weakly determined

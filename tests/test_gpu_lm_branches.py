@@ -97,21 +97,32 @@ def test_branch_trajectory_matches_oracle(name):
 @pytest.mark.parametrize("name", ["gauge_1e15", "gauge_1e16"])
 def test_gauge_runs_agree_on_gauge_invariants(name):
     c, s, (sm_o, tr_o, sol_o), (sm_g, tr_g, sol_g) = _solve_both(name)
-    # With D^2 = diag / 3e15 the step's gauge component is rounding
-    # amplified, so even a decision whose cost change is well above the cost's
-    # own rounding can flip with the summation order: reordering the U_c sums
-    # of the Jacobian pass alone (same values, per-camera instead of
-    # per-chunk reduction) turned the oracle's 'AAR' into 'ARA' at iteration
-    # 2, whose cost change is 4.3e-5 of the cost (measured on MI355X).  Only
-    # decisions above 1e-4 of the cost are compared step by step; the
-    # optimum and the gauge invariants below are compared tightly.
-    k = L.decisive_prefix(tr_o, rel=1e-4)
-    assert seq_of(tr_g)[:k] == seq_of(tr_o)[:k]
-    # (the prefix steps are taken with D^2 = diag / 3e15: their gauge
-    # components are rounding amplified by ~1e15, so the costs after them
-    # agree only loosely; the optimum below is rounding-tight)
-    for a, b in zip(tr_g[:k + 1], tr_o[:k + 1]):
-        assert abs(a["cost"] - b["cost"]) <= 1e-3 * b["cost"]
+    # With D^2 = diag / 1e15 the step's gauge component is rounding
+    # amplified ~1e15, so decisions are compared step by step only where
+    # (a) the cost change exceeds 1e-6 of the cost (the north-star
+    # tolerance) AND (b) the reference algorithm itself takes the same
+    # decision in another valid summation order: the oracle with its
+    # reduced camera matrix's diagonal blocks summed in the device solver's
+    # association (oracle order=1, the same arithmetic) -- on gauge_1e15 that
+    # one reordering turns the oracle's third decision (cost change 6.3e-6
+    # of the cost, inside the 1e-6 prefix) into an invalid step
+    # (profiles/r04_gauge_order_probe.txt).  Past that prefix the decisions
+    # are rounding noise; the optimum and the gauge invariants below are
+    # compared tightly.
+    build, _, mode = L.cases()[name]
+    r1, t1, X1 = s.copy_params()
+    _, tr_o1 = O.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r1, t1, X1, mode=mode,
+                       options=O.default_options(**c["options"]), order=1)
+    a, b = seq_of(tr_o), seq_of(tr_o1)
+    k_ord = next((i for i in range(min(len(a), len(b))) if a[i] != b[i]), min(len(a), len(b)))
+    k6 = L.decisive_prefix(tr_o, rel=1e-6)
+    k = min(k6, k_ord)
+    assert seq_of(tr_g)[:k] == seq_of(tr_o)[:k], (seq_of(tr_g)[:k6], seq_of(tr_o)[:k6], k6, k_ord)
+    # (the prefix steps are taken with D^2 = diag / 1e15: their gauge
+    # components are rounding amplified, so the costs after them agree only
+    # loosely; the optimum below is rounding-tight)
+    for a_, b_ in zip(tr_g[:k + 1], tr_o[:k + 1]):
+        assert abs(a_["cost"] - b_["cost"]) <= 1e-3 * b_["cost"]
     # both reach the same optimum (rounding-level final costs) ...
     assert abs(sm_g.final_cost - sm_o["final_cost"]) <= 1e-10 * sm_o["final_cost"]
     # ... and the radius clamp where the oracle does
@@ -120,9 +131,11 @@ def test_gauge_runs_agree_on_gauge_invariants(name):
     res, al = L.gauge_invariant_diff(_residuals, s, sol_g, sol_o)
     assert res <= 1e-6, res
     assert al <= 1e-6, al
-    raw = max(_rel(a, b) for a, b in zip(sol_g, sol_o))
-    print(f"{name}: GPU {seq_of(tr_g)} / oracle {seq_of(tr_o)}; raw parameter drift {raw:.2e} "
-          f"(gauge), residuals {res:.1e} px, Sim(3)-aligned {al:.1e}")
+    raw = max(_rel(a_, b_) for a_, b_ in zip(sol_g, sol_o))
+    print(f"{name}: GPU {seq_of(tr_g)[:24]} / oracle {a[:24]} / oracle order=1 {b[:24]}; compared prefix {k} "
+          f"(1e-6 prefix {k6}, order-robust prefix {k_ord}, GPU matches the 1e-6 prefix: "
+          f"{seq_of(tr_g)[:k6] == a[:k6]}); raw parameter drift {raw:.2e} (gauge), residuals {res:.1e} px, "
+          f"Sim(3)-aligned {al:.1e}")
 
 
 def test_resident_api_takes_the_same_branches():

@@ -95,3 +95,25 @@ def test_oracle_refuses_invalid_options(bad):
     r, t, X = s.copy_params()
     with pytest.raises(RuntimeError, match="-22"):
         O.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X, options=O.default_options(**bad))
+
+
+@pytest.mark.parametrize("name", sorted(n for n in FIX if not n.startswith("gauge")))
+def test_oracle_summation_order_variant_takes_the_same_branches(name):
+    """oracle order=1 (the reduced matrix's diagonal blocks summed in the
+    device solver's association: the same arithmetic in another valid order)
+    takes every branch scene's decisions as the Ceres order does; the gauge
+    scenes are where it does not (tests/test_gpu_lm_branches.py,
+    profiles/r04_gauge_order_probe.txt)."""
+    c = FIX[name]
+    build, _, mode = L.cases()[name]
+    s = build()
+    out = []
+    for order in (0, 1):
+        r, t, X = s.copy_params()
+        sm, tr = O.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X, mode=mode,
+                         options=O.default_options(**c["options"]), order=order)
+        out.append((sm, tr))
+    (s0, t0), (s1, t1) = out
+    seq = lambda tr: [(it["step_is_valid"], it["step_is_successful"]) for it in tr]
+    assert seq(t0) == seq(t1)
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-8 * s0["final_cost"]

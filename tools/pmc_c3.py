@@ -8,6 +8,9 @@ import sfm_amd
 from sfm_amd import scene as S
 
 what = sys.argv[1] if len(sys.argv) > 1 else "all"
+# the host-driven LM loop: the device-driven one also enqueues phases its
+# flags then skip, whose near-empty launches would enter the per-launch means
+os.environ["SFM_HOST_LM"] = "1"
 sc = S.config("C3")
 ba = sfm_amd.BundleAdjuster(0)
 ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
