@@ -313,9 +313,10 @@ int sfm_brisk_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h,
 
 /* BRISK detection (+ description): CTracker::detectFeatures
  * (CTracker.cpp:275-287) with BriskFeatureDetector(threshold 60, octaves 6,
- * suppressScaleNonmaxima) -- the published scale-space FAST detector with
- * the simplifications named in oracle/brisk_oracle.py (unpinned vs the
- * absent ethz-asl library).  kps [capacity][5] = (x, y, size, angle,
+ * suppressScaleNonmaxima) -- the published scale-space FAST detector in its
+ * reference implementation's form (INTER_AREA layers, FAST non-maximum
+ * suppression, refine3D; oracle/brisk_oracle.py), unpinned vs the absent
+ * ethz-asl BRISK 2 library.  kps [capacity][5] = (x, y, size, angle,
  * response), octave [capacity] = layer.  desc [capacity][64] or NULL: with
  * NULL, detection only (angle -1, no border removal); otherwise the
  * descriptor's border rule drops keypoints as the reference's compute does.

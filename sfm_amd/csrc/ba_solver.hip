@@ -102,6 +102,7 @@ struct sfm_ba_handle {
   LmCtl* lm_ctl_host = nullptr;
   sfm_ba_iteration* lm_trace = nullptr;
   int lm_trace_cap = 0;
+  hipGraphExec_t lm_graph = nullptr;  // SFM_LM_GRAPH: the captured batch (updated per batch)
   // pinned staging for every host <-> device transfer of set_problem,
   // get_parameters and the LM trace: a pageable copy goes through the
   // runtime's own staging (C1: the 320-KB uv upload took 131 us, the 49-KB
@@ -246,8 +247,9 @@ bool env_flag(const char* name) {
   return v && v[0] == '1';
 }
 
-// Compute units of the device: the persistent grids (fused Cholesky) must
-// stay co-resident, one workgroup per CU.
+// Compute units of the device: the persistent grids (fused Cholesky) size
+// themselves to one workgroup per CU (they also finish when only part of the
+// grid is resident: roles go by start order).
 int device_cus(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess || prop.multiProcessorCount < 2) return 2;
@@ -797,7 +799,14 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   d.gate = nullptr;
   int rc = evaluate_enqueue(h, true, jac_scaling);
   if (rc == 0 && !h->fuse_lm) k_lm_init<<<1, 1, 0, s>>>(h->lm_ctl, d.scal);
+  // SFM_LM_GRAPH=1 (experiment): each batch's launches are captured into a
+  // hipGraph and launched as one (the batch takes no host decision)
+  const bool use_graph = !sharded(h) && !h->profiling && env_flag("SFM_LM_GRAPH");
   while (rc == 0) {
+    if (use_graph && hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      rc = fail(SFM_EIO, "hipStreamBeginCapture failed");
+      break;
+    }
     for (int b = 0; b < batch && rc == 0; ++b) {
       d.gate = &h->lm_ctl->run_step;
       if ((rc = compute_step_enqueue(h, c.radius))) break;
@@ -810,6 +819,25 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
       if (rc) break;
       d.gate = nullptr;
       if (!h->fuse_lm) k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
+    }
+    if (use_graph) {
+      hipGraph_t g = nullptr;
+      const hipError_t ec = hipStreamEndCapture(s, &g);
+      if (rc == 0 && ec != hipSuccess) rc = fail(SFM_EIO, "hipStreamEndCapture failed");
+      if (rc == 0) {
+        hipGraphExecUpdateResult ur;
+        hipGraphNode_t en = nullptr;
+        if (!h->lm_graph || hipGraphExecUpdate(h->lm_graph, g, &en, &ur) != hipSuccess) {
+          if (h->lm_graph) (void)hipGraphExecDestroy(h->lm_graph);
+          h->lm_graph = nullptr;
+          if (hipGraphInstantiate(&h->lm_graph, g, nullptr, nullptr, 0) != hipSuccess) {
+            h->lm_graph = nullptr;
+            rc = fail(SFM_EIO, "hipGraphInstantiate failed");
+          }
+        }
+        if (rc == 0 && hipGraphLaunch(h->lm_graph, s) != hipSuccess) rc = fail(SFM_EIO, "hipGraphLaunch failed");
+      }
+      if (g) (void)hipGraphDestroy(g);
     }
     if (rc) break;
     if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -825,8 +853,8 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   d.radius_dev = nullptr;
   h->fuse_lm = false;
   if (rc) return rc;
-  if (c.error & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid not co-resident)");
-  if (c.error & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid not co-resident)");
+  if (c.error & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid made no progress)");
+  if (c.error & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid made no progress)");
   sm->num_jacobian_evaluations++;  // the initial evaluation
   sm->num_residual_evaluations++;
   sm->initial_cost = c.init_cost;
@@ -926,6 +954,7 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_trace) hipFree(h->lm_trace);
   if (h->stage) hipHostFree(h->stage);
   if (h->ar_tmp) hipFree(h->ar_tmp);
+  if (h->lm_graph) hipGraphExecDestroy(h->lm_graph);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -1526,11 +1555,11 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
       sm.num_linear_solves++;
       int chol_fail = 0;
       std::memcpy(&chol_fail, sc + kNumScalars, sizeof(int));
-      // The persistent grids need every workgroup co-resident: device work on
-      // other streams that holds CUs while a solve runs can starve them, and
-      // their bounded waits then report here.
-      if (chol_fail & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid not co-resident)");
-      if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid not co-resident)");
+      // The persistent grids' waits are bounded (roles go by start order, so
+      // a partly resident grid still progresses); a timeout reports here
+      // (INTEGRATION.md §2).
+      if (chol_fail & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid made no progress)");
+      if (chol_fail & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid made no progress)");
       const bool solve_ok = chol_fail == 0 && !(sc[kBadStep] > 0.0) && !(sc[kBadCam] > 0.0) && !(sc[kBadBack] > 0.0);
       const double model_cost_change = sc[kModelChange] + sc[kModelChangePt];
       itr.step_is_valid = (solve_ok && model_cost_change >= 0.0) ? 1 : 0;

@@ -232,12 +232,16 @@ struct PartialTile {
   const double* src = nullptr;  // tile in A (column-major, ld)
   double* dst = nullptr;        // LDS image (TS stride)
   bool got = false;             // this wave's share is in LDS (wave-uniform)
+  int* landed = nullptr;        // LDS count of waves whose share has landed (or nullptr)
 };
 struct WalkerIO {
   int ld = 0, epoch = 0;
   int* pub_flag = nullptr;
   int* pub_cnt = nullptr;
   PartialTile sub, diag;
+  // SFM_CHOL_EXT: the sub tile's TRSM runs blockwise during the panels
+  const double* Wl = nullptr;
+  int* ext_done = nullptr;  // LDS [4]: panels of each 16-row strip of the sub tile already solved
 };
 
 // Wave w (1..3) copies columns w-1, w+2, ... of a handed-off tile into LDS
@@ -263,19 +267,63 @@ __device__ __forceinline__ void fetch_third(const double* __restrict__ src, int 
     o += 3 * TS;
   }
 }
+// This wave's share has landed: count it (its LDS writes ordered before).
+__device__ __forceinline__ void count_landed(PartialTile& pt) {
+  pt.got = true;
+  if (pt.landed == nullptr) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  atomicAdd(pt.landed, (threadIdx.x & 63) == 0 ? 1 : 0);
+}
 // Non-blocking: fetch this wave's share if the tile's flag is out.
 __device__ __forceinline__ void try_fetch(PartialTile& pt, int ld, int epoch, int w, int lane) {
   if (pt.flag == nullptr || pt.got) return;
   if (__hip_atomic_load(pt.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) return;
   fetch_third(pt.src, ld, pt.dst, w, lane);
-  pt.got = true;
+  count_landed(pt);
 }
 // Blocking: wait for the flag (bounded), then fetch this wave's share.
 __device__ __forceinline__ void must_fetch(PartialTile& pt, int ld, int epoch, int w, int lane, int* fail) {
   if (pt.flag == nullptr || pt.got) return;
   if (!spin_until(pt.flag, epoch)) atomicOr(fail, 4);
   fetch_third(pt.src, ld, pt.dst, w, lane);
-  pt.got = true;
+  count_landed(pt);
+}
+
+// Blocked TRSM of the sub tile S = T_j+1,j against L_jj, one 16-row strip s
+// and one 16-column panel p (one wavefront): X = S(s, p) W_pp^T in place
+// (W_pp = L_pp^-1, the panel's diagonal block inverse), then
+// S(s, P) -= X L(P, p)^T for the later panels P.  Run panel by panel as the
+// POTRF finishes them, the strips give L_j+1,j = T_j+1,j L_jj^-T without
+// the full W_j (SFM_CHOL_EXT).
+__device__ __forceinline__ void ext_panel(double* Sb, const double* T, const double* Wl, int s, int p, int lane) {
+  const int j = lane & 15, kk = lane >> 4;
+  f64x4 acc = mfma16(Sb + 16 * p * TS + 16 * s, 1, TS, Wl + 16 * p * TS + 16 * p, TS, 1, f64x4{0.0, 0.0, 0.0, 0.0},
+                     lane);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) Sb[(16 * p + j) * TS + 16 * s + 4 * rr + kk] = acc[rr];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int P = p + 1; P < 4; ++P) {
+    const f64x4 a2 = mfma16(Sb + 16 * p * TS + 16 * s, 1, TS, T + 16 * p * TS + 16 * P, TS, 1,
+                            f64x4{0.0, 0.0, 0.0, 0.0}, lane);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Sb[(16 * P + j) * TS + 16 * s + 4 * rr + kk] -= a2[rr];
+  }
+}
+// During phase b (panels < b done): once every share of the sub tile has
+// landed, wave w (1..3) solves its strips (w - 1, and 3 for wave 3) up to
+// panel b - 1.
+__device__ __forceinline__ void ext_progress(WalkerIO& io, const double* T, int b, int w, int lane) {
+  if (io.ext_done == nullptr || io.sub.landed == nullptr) return;
+  if (__hip_atomic_load(io.sub.landed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int k = 0; k < (w == 3 ? 2 : 1); ++k) {
+    const int sidx = k == 0 ? w - 1 : 3;
+    const int p0 = __builtin_amdgcn_readfirstlane(io.ext_done[sidx]);
+    for (int p = p0; p < b; ++p) ext_panel(io.sub.dst, T, io.Wl, sidx, p, lane);
+    if (p0 < b) io.ext_done[sidx] = b;
+  }
 }
 
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
@@ -411,11 +459,13 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       // (Ls is read by nobody from here on: the sub tile may land on it)
       try_fetch(io.diag, io.ld, io.epoch, w, lane);
       try_fetch(io.sub, io.ld, io.epoch, w, lane);
+      ext_progress(io, T, b, w, lane);
     } else if (b == 2) {
       if (w == 1) w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
       if (w == 3) trail_block(T, 16, 3, 3, lane);       // panel 1's trailing update of block (3,3)
       try_fetch(io.diag, io.ld, io.epoch, w, lane);
       try_fetch(io.sub, io.ld, io.epoch, w, lane);
+      ext_progress(io, T, b, w, lane);
     } else if (b == 3) {
       // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
       try_fetch(io.diag, io.ld, io.epoch, w, lane);
@@ -427,6 +477,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
       try_fetch(io.diag, io.ld, io.epoch, w, lane);
       try_fetch(io.sub, io.ld, io.epoch, w, lane);
+      ext_progress(io, T, b, w, lane);
     }
     __syncthreads();
     WSTAMP(k0 / 64, 8 + b);
@@ -798,7 +849,7 @@ __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) 
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
                                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* Ta,
                                              double* Tb, double* Wl, double* Ls, double (*scr)[256], int* pub_cnt,
-                                             int* __restrict__ fail) {
+                                             int* xsh, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   double* T = Ta;   // the tile being factored
   double* Tn = Tb;  // the next diagonal tile (prefetched)
@@ -814,6 +865,9 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
   for (int j = 0; j < nb; ++j) {
     const int j0 = j * NB;
     WSTAMP(j, 0);
+#ifdef SFM_CHOL_EXT
+    if (t < 5) xsh[t] = 0;  // the sub tile's landed count, its strips' solved panels (barriers follow)
+#endif
     if (j > 0) {
       // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
       // blocks right of it are updated inside potrf_tile, during panel 0
@@ -832,9 +886,15 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       io.pub_cnt = pub_cnt;
     }
     if (more && w > 0) {
-      io.sub = PartialTile{Pf + (j + 1) * nb + j, A + size_t(j0) * ld + i0, Ls, false};
-      io.diag = PartialTile{Pf + (j + 1) * nb + j + 1, A + size_t(i0) * ld + i0, Tn, false};
+      io.sub = PartialTile{Pf + (j + 1) * nb + j, A + size_t(j0) * ld + i0, Ls, false, nullptr};
+      io.diag = PartialTile{Pf + (j + 1) * nb + j + 1, A + size_t(i0) * ld + i0, Tn, false, nullptr};
+#ifdef SFM_CHOL_EXT
+      io.sub.landed = xsh;
+      io.ext_done = xsh + 1;
+      io.Wl = Wl;
+#endif
     }
+    if (j == 0) __syncthreads();  // (xsh reset before any wave of step 0 counts in)
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, io)
                                     : potrf_tile<false>(T, Wl, scr, j0, n, dl, io);
@@ -872,11 +932,19 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     }
     __syncthreads();
     WSTAMP(j, 3);
+#ifdef SFM_CHOL_EXT
+    // the strips' panels the POTRF's phases did not solve: wave w, strip w
+    {
+      const int p0 = __builtin_amdgcn_readfirstlane(xsh[1 + w]);
+      for (int p = p0; p < 4; ++p) ext_panel(Ls, T, Wl, w, p, lane);
+    }
+#else
     // subdiagonal tile: L_j+1,j = T_j+1,j W_j^T in place (wave w reads and
     // writes only row block w of it), kept as Ls for the next update
     f64x4 x[4];
     trsm_lds(Ls, Wl, x, lane);
     put_tile(Ls, x, lane);
+#endif
     __syncthreads();
     WSTAMP(j, 5);
     if (w > 0) {  // waves 1-3 store it (write-through); drained and flagged in the next step's panel 0
@@ -903,6 +971,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   __shared__ double Tn[NB * TS];  // the walker's second diagonal-tile buffer
   __shared__ double scr[4][256];
   __shared__ int sh[3];
+  __shared__ int xsh[8];
   if (gate && *gate == 0) {
     // device LM loop, phase skipped: the launch still takes its ntask + nhelp
     // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
@@ -924,7 +993,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Tn, Wl, Ls, scr, sh + 2, fail);
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Tn, Wl, Ls, scr, sh + 2, xsh, fail);
     return;
   }
   const int ntask = chol_tasks(nb);
@@ -971,8 +1040,10 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
 // instead of three (127 -> 98 us at n = 3000 for LDS staging alone, see
 // DESIGN.md).  Chunked consumption or several blocks per workgroup measured
 // slower: whatever runs after the awaited block arrives is on the chain.
-// All workgroups are co-resident (nb <= a few hundred, one CU each); every
-// wait is bounded and a timeout sets bit 1 of *fail (an error, never a hang).
+// Rows go by start order (the chain's first row to the first workgroup to
+// run), so every awaited row belongs to a running workgroup whatever the
+// residency; every wait is bounded and a timeout sets bit 1 of *fail (an
+// error, never a hang).
 
 __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A, int ld, int n, int nb,
                                                    const double* __restrict__ Winv, double* __restrict__ y,
@@ -1066,7 +1137,8 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   const int nb = d.nblk, ntask = chol_tasks(nb);
-  // one persistent workgroup per CU (the walker + helpers must be co-resident)
+  // one persistent workgroup per CU (roles by start order: a partly resident
+  // grid still finishes)
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
                                          epoch, nhelp, d.fail, d.gate);

@@ -5,4 +5,5 @@ timeout -k 10 60 python3 tools/walker_phases.py 3000 > gpurun_out/stamps.txt 2>&
 timeout -k 10 60 python3 tools/walker_phases.py 6000 >> gpurun_out/stamps.txt 2>&1 && \
 timeout -k 10 60 python tools/gauge_gpu.py > gpurun_out/gauge_gpu.txt 2>&1 && \
 bash tools/ab_bench.sh cur jac2 > gpurun_out/ab_bench.txt 2>&1 && \
+bash tools/ab_pnp.sh prev cur > gpurun_out/ab_pnp.txt 2>&1 && \
 bash tools/gpu_check.sh

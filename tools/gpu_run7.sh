@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+bash tools/ab_libs.sh r3 cur ext > gpurun_out/ab_libs.txt 2>&1 && \
+timeout -k 10 60 python3 tools/walker_phases.py 3000 > gpurun_out/stamps.txt 2>&1 && \
+SFM_AMD_LIB=$GRAFT_REPO_ROOT/tools/var_extst.so timeout -k 10 60 python3 tools/walker_phases.py 3000 >> gpurun_out/stamps.txt 2>&1 && \
+timeout -k 10 60 python tools/gauge_gpu.py > gpurun_out/gauge_gpu.txt 2>&1 && \
+bash tools/ab_bench.sh cur ext jac2 > gpurun_out/ab_bench.txt 2>&1 && \
+bash tools/ab_pnp.sh prev cur > gpurun_out/ab_pnp.txt 2>&1 && \
+timeout -k 10 120 python tools/c1_latency.py > gpurun_out/c1.txt 2>&1 && \
+SFM_LM_GRAPH=1 timeout -k 10 120 python tools/c1_latency.py >> gpurun_out/c1.txt 2>&1 && \
+bash tools/gpu_check.sh
