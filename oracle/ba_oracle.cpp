@@ -56,12 +56,13 @@
 namespace oracle {
 
 static int g_threads = 1;
-// Summation order of the reduced camera matrix's diagonal blocks (tests
-// only, oracle_set_order): 0 = Ceres' (the running sum per camera block,
-// point by point: F^T F, then the chunk outer product), 1 = the device
-// solver's association (U_c = sum F^T F first, then + D^2, then minus the
-// outer products) -- the same arithmetic in another valid order, used to
-// show which LM decisions of a near-singular problem rounding decides.
+// Summation orders (tests only, oracle_set_order; a bit mask, 0 = Ceres'):
+// bit 1: the reduced camera matrix's diagonal blocks in the device solver's
+// association (U_c = sum F^T F first, then + D^2, then minus the outer
+// products) instead of Ceres' running sum per block, point by point;
+// bit 2: the model cost change summed over the observations in reverse.
+// The same arithmetic in other valid orders, used to show which LM
+// decisions of a near-singular problem rounding decides.
 static int g_order = 0;
 
 // ---------------------------------------------------------------------------
@@ -577,7 +578,7 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
       if (pb.pts_var && pb.cams_var) {
         S.assign(size_t(nf) * nf, 0.0);
         rhs.assign(nf, 0.0);
-        if (g_order == 1) {
+        if (g_order & 1) {
           // U_c = sum_q F^T F (point order), then + D^2
           for (int p = 0; p < n_pts; ++p)
             for (int64_t q = pb.pt_off[p]; q < pb.pt_off[p + 1]; ++q) {
@@ -652,7 +653,7 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
               const int64_t q0 = pb.pt_off[p], q1 = pb.pt_off[p + 1];
               if (q0 == q1) continue;
               // F^T F into S (both 3-blocks of the camera and their coupling)
-              for (int64_t q = q0; q < q1 && g_order == 0; ++q) {
+              for (int64_t q = q0; q < q1 && !(g_order & 1); ++q) {
                 const int c = cam_idx[pb.order[q]];
                 if (c < clo || c >= chi) continue;
                 double F[12];
@@ -786,7 +787,8 @@ int oracle_ba_solve(const Options* opts, int mode, int64_t n_obs, const double* 
             for (int k = 0; k < 9; ++k) { const int col = col_of(q, k); if (col >= 0) s += Js(q, row, k) * step[col]; }
             model_res[2 * q + row] = s;
           }
-        for (int64_t q = 0; q < N; ++q) {
+        for (int64_t qq = 0; qq < N; ++qq) {
+          const int64_t q = (g_order & 2) ? N - 1 - qq : qq;  // order bit 2: the other way round
           const double mr[2] = {model_res[2 * q], model_res[2 * q + 1]};
           mc += mr[0] * (r[2 * q] + mr[0] / 2.0) + mr[1] * (r[2 * q + 1] + mr[1] / 2.0);
         }
