@@ -35,23 +35,6 @@ constexpr int kThreads = 256;
 constexpr uint32_t kYSentinelWord = 0x7FF4DEADu;
 constexpr uint64_t kYSentinel = (uint64_t(kYSentinelWord) << 32) | kYSentinelWord;
 
-// The diagonal-tile inverses W_k = L_kk^-1 travel from the Cholesky walker
-// to the helpers as data-tagged granules: before each factorisation every
-// entry of W_k's lower 16x16 blocks holds kYSentinel, and a consumer polls
-// the entries it needs until none is the sentinel (no flag, no drain on the
-// walker).  The upper blocks stay zero (k_backsolve reads whole columns).
-// Part `part` of `nparts` of the fill, by `nt` threads (thread `t`).
-__device__ __forceinline__ void w_sentinel_fill(double* __restrict__ invL, int nblk, int part, int nparts, int t,
-                                                int nt) {
-  const int64_t total = int64_t(nblk) * kNB * kNB;
-  const int64_t per = (total + nparts - 1) / nparts;
-  const int64_t e0 = int64_t(part) * per, e1 = e0 + per < total ? e0 + per : total;
-  for (int64_t e = e0 + t; e < e1; e += nt) {
-    const int r = int(e & (kNB - 1)), c = int((e >> 6) & (kNB - 1));  // W_k(r, c) at k*4096 + c*64 + r
-    if ((r >> 4) >= (c >> 4)) reinterpret_cast<unsigned long long*>(invL)[e] = kYSentinel;
-  }
-}
-
 // Index of scalar results (device array `scal`, doubles).
 enum Scalar {
   kCost = 0,        // cost at current x (Jacobian pass)
@@ -222,7 +205,6 @@ int blocks_for(int64_t n, int threads);
 // ---- dense Cholesky (chol_kernels.hip) ----
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true);
 // W_k granules back to the sentinel (k_schur_diag_sum does this in the solve)
-void launch_w_sentinel(const DevProblem& d, hipStream_t s);
 // sentinel_set: y already holds kYSentinel (k_pad_init wrote it)
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set = false);
 

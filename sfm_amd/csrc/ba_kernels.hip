@@ -1041,13 +1041,10 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        const double* __restrict__ diag_c, double radius,
                                                        int add_diag, double* __restrict__ S, int ld, int n,
                                                        int init, const int* __restrict__ gate, const double* __restrict__ radius_dev,
-                                                       int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y,
-                                                       double* __restrict__ invL, int nblk) {
+                                                       int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
   const int c = blockIdx.x, t = threadIdx.x;
-  // the factorisation's W_k granules back to "not yet produced"
-  w_sentinel_fill(invL, nblk, c, gridDim.x, t, 64);
   // k_pad_init folded in (one launch fewer per LM iteration): the identity
   // padding below row n of this camera's six columns and y's sentinel
   // there; the last camera also takes columns n.. (the identity block, the
@@ -1441,8 +1438,7 @@ void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
                                         d.n, 1, d.gate, d.radius_dev, d.fail,
-                                        reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB,
-                                        d.invL, d.nblk);
+                                        reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB);
   if (!d.n_blk) return;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
   const int nb = int((d.n_bslots + per - 1) / per);

@@ -102,7 +102,6 @@ struct sfm_ba_handle {
   LmCtl* lm_ctl_host = nullptr;
   sfm_ba_iteration* lm_trace = nullptr;
   int lm_trace_cap = 0;
-  hipGraphExec_t lm_graph = nullptr;  // SFM_LM_GRAPH: the captured batch (updated per batch)
   // pinned staging for every host <-> device transfer of set_problem,
   // get_parameters and the LM trace: a pageable copy goes through the
   // runtime's own staging (C1: the 320-KB uv upload took 131 us, the 49-KB
@@ -799,14 +798,7 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   d.gate = nullptr;
   int rc = evaluate_enqueue(h, true, jac_scaling);
   if (rc == 0 && !h->fuse_lm) k_lm_init<<<1, 1, 0, s>>>(h->lm_ctl, d.scal);
-  // SFM_LM_GRAPH=1 (experiment): each batch's launches are captured into a
-  // hipGraph and launched as one (the batch takes no host decision)
-  const bool use_graph = !sharded(h) && !h->profiling && env_flag("SFM_LM_GRAPH");
   while (rc == 0) {
-    if (use_graph && hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-      rc = fail(SFM_EIO, "hipStreamBeginCapture failed");
-      break;
-    }
     for (int b = 0; b < batch && rc == 0; ++b) {
       d.gate = &h->lm_ctl->run_step;
       if ((rc = compute_step_enqueue(h, c.radius))) break;
@@ -819,25 +811,6 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
       if (rc) break;
       d.gate = nullptr;
       if (!h->fuse_lm) k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
-    }
-    if (use_graph) {
-      hipGraph_t g = nullptr;
-      const hipError_t ec = hipStreamEndCapture(s, &g);
-      if (rc == 0 && ec != hipSuccess) rc = fail(SFM_EIO, "hipStreamEndCapture failed");
-      if (rc == 0) {
-        hipGraphExecUpdateResult ur;
-        hipGraphNode_t en = nullptr;
-        if (!h->lm_graph || hipGraphExecUpdate(h->lm_graph, g, &en, &ur) != hipSuccess) {
-          if (h->lm_graph) (void)hipGraphExecDestroy(h->lm_graph);
-          h->lm_graph = nullptr;
-          if (hipGraphInstantiate(&h->lm_graph, g, nullptr, nullptr, 0) != hipSuccess) {
-            h->lm_graph = nullptr;
-            rc = fail(SFM_EIO, "hipGraphInstantiate failed");
-          }
-        }
-        if (rc == 0 && hipGraphLaunch(h->lm_graph, s) != hipSuccess) rc = fail(SFM_EIO, "hipGraphLaunch failed");
-      }
-      if (g) (void)hipGraphDestroy(g);
     }
     if (rc) break;
     if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -954,7 +927,6 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_trace) hipFree(h->lm_trace);
   if (h->stage) hipHostFree(h->stage);
   if (h->ar_tmp) hipFree(h->ar_tmp);
-  if (h->lm_graph) hipGraphExecDestroy(h->lm_graph);
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -1762,7 +1734,6 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   float total = 0.f;
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipMemcpyAsync(S, S0, bytes, hipMemcpyDeviceToDevice, s));
-    launch_w_sentinel(d, s);
     HIPCHK(hipEventRecord(e0, s));
     launch_cholesky(d, r + 1, s);
     launch_backsolve(d, r + 1, s);

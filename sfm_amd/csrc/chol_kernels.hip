@@ -21,20 +21,6 @@
 #include "ba_common.h"
 
 namespace sfm {
-#ifdef SFM_CHOL_STAMPS
-// development build (tools/chol_stamps.sh): s_memrealtime stamps (100 MHz) of
-// the walker's phases, [step][slot]; slot 7 holds the step's `early` flag
-__device__ unsigned long long g_wstamp[256 * 16];
-#define WSTAMP(j, k) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define WSTAMPV(j, k, v) do { if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = (v); } while (0)
-// helpers' publication times: [i][j][0] partial tile (i, j) out, [1] final tile (i, j) out
-__device__ unsigned long long g_hstamp[64 * 64 * 2];
-#define HSTAMP(i, j, k) do { if (threadIdx.x == 0 && (i) < 64 && (j) < 64) g_hstamp[((i) * 64 + (j)) * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define HSTAMP(i, j, k) do { } while (0)
-#define WSTAMP(j, k) do { } while (0)
-#define WSTAMPV(j, k, v) do { } while (0)
-#endif
 namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -166,50 +152,6 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
   for (int rr = 0; rr < 4; ++rr) T[(16 * J + j) * TS + 16 * I + 4 * rr + kk] -= acc[rr];
 }
 
-// 2^20 polls (each a memory round trip + a short sleep: ~1 s), long beyond
-// any co-running kernel of the library, short of a watchdog
-constexpr long kFlagSpins = 1L << 20;
-
-__device__ __forceinline__ bool spin_until(const int* f, int epoch) {
-  long spins = 0;
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-    if (++spins > kFlagSpins) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
-
-// Branches around barriers are kept SCALAR: "this is wave 0" is tested on
-// readfirstlane(threadIdx.x) (an SGPR), and everything inside runs on all 64
-// lanes (same flag, same value).  A per-lane `if (threadIdx.x == 0)` inside a
-// loop that also holds barriers lets the compiler split the loop by lane
-// masks, so that lanes 1..63 of wave 0 pass the barrier without lane 0
-// (seen on gfx950: a hang on a stale ticket).
-__device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64; }
-
-// Wave 0 polls one flag, then the block proceeds WITHOUT an acquire: every
-// load of the handed-off bytes after it must be an sc1 load (ld_wt), and the
-// producer stored them sc1, drained every storing wave, then flagged from
-// one lane behind a barrier (MI355X_MICROARCH.md, hand-offs with sc1 loads
-// in place of the acquire; the acquire's L1 invalidate is ~1.5 us).
-__device__ __forceinline__ void block_poll(const int* f, int epoch, int* fail) {
-  if (wave0()) {
-    if (!spin_until(f, epoch)) atomicOr(fail, 4);
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Write-through publication (MI355X_MICROARCH.md: a producer that stores
-// every handed-off byte sc1 and drains every wave before the flag needs no
-// agent release; the consumers keep their acquire): every tile the walker
-// and the helpers hand off, so no publication pays an L2 write-back (the
-// release form, buffer_wbl2 + drain, wrote back the XCD's whole L2).
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // The factorisation proper, on the tile image T in LDS (256 threads; Wl is
 // cleared here).  Returns this thread's bad-pivot flag; ends with a barrier.
 // Ls != nullptr: the walker's last update of the blocks right of column
@@ -217,118 +159,14 @@ __device__ __forceinline__ void st_wt(double* p, double v) {
 // waves 1-3 apply it while wave 0 factors panel 0, before the trailing
 // update of panel 0 touches those blocks (every block keeps its update
 // order: bitwise the same factor).
-// io.pub_flag != nullptr: waves 1-3 stored L_j,j-1 (the walker's last TRSM
-// result) at the end of the previous step; each drains its own stores at the
-// start of panel 0 and counts itself in io.pub_cnt (LDS), the last one raises
-// the flag, so wave 0 -- the pivot chain -- never waits for the write-through
-// stores.
-// io.sub / io.diag: the walker's next two partial tiles, (j+1, j) and
-// (j+1, j+1); waves 1-3 poll their flags after their chores of panels 1-3 and
-// copy their third of a tile into LDS (sc1 loads) as soon as it is out, so
-// its load latency hides under the pivot chain (the walker finishes what is
-// left after the POTRF).
-struct PartialTile {
-  const int* flag = nullptr;    // nullptr: nothing to fetch
-  const double* src = nullptr;  // tile in A (column-major, ld)
-  double* dst = nullptr;        // LDS image (TS stride)
-  bool got = false;             // this wave's share is in LDS (wave-uniform)
-  int* landed = nullptr;        // LDS count of waves whose share has landed (or nullptr)
-};
-struct WalkerIO {
-  int ld = 0, epoch = 0;
-  int* pub_flag = nullptr;
-  int* pub_cnt = nullptr;
-  PartialTile sub, diag;
-  // SFM_CHOL_EXT: the sub tile's TRSM runs blockwise during the panels
-  const double* Wl = nullptr;
-  int* ext_done = nullptr;  // LDS [4]: panels of each 16-row strip of the sub tile already solved
-};
-
-// Wave w (1..3) copies columns w-1, w+2, ... of a handed-off tile into LDS
-// with sc1 loads (every load of the hand-off is sc1: no acquire needed).
-// Running addresses, made opaque per call: per-column offsets would be
-// loop invariants of the walker, and hoisting 2 x 22 of them out of its loop
-// spilled the kernel's registers.
-__device__ __forceinline__ void fetch_third(const double* __restrict__ src, int ld, double* dst, int w, int lane) {
-  const double* p = src + size_t(w - 1) * ld + lane;
-  int o = (w - 1) * TS + lane;
-  asm volatile("" : "+v"(p), "+v"(o));
-  const size_t step = size_t(3) * ld;
-  const int nc = (NB - (w - 1) + 2) / 3;  // 22 or 21 columns
-  double v[22];
-#pragma unroll
-  for (int m = 0; m < 22; ++m) {
-    v[m] = m < nc ? ld_wt(p) : 0.0;
-    p += step;
-  }
-#pragma unroll
-  for (int m = 0; m < 22; ++m) {
-    if (m < nc) dst[o] = v[m];
-    o += 3 * TS;
-  }
-}
-// This wave's share has landed: count it (its LDS writes ordered before).
-__device__ __forceinline__ void count_landed(PartialTile& pt) {
-  pt.got = true;
-  if (pt.landed == nullptr) return;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  atomicAdd(pt.landed, (threadIdx.x & 63) == 0 ? 1 : 0);
-}
-// Non-blocking: fetch this wave's share if the tile's flag is out.
-__device__ __forceinline__ void try_fetch(PartialTile& pt, int ld, int epoch, int w, int lane) {
-  if (pt.flag == nullptr || pt.got) return;
-  if (__hip_atomic_load(pt.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) return;
-  fetch_third(pt.src, ld, pt.dst, w, lane);
-  count_landed(pt);
-}
-// Blocking: wait for the flag (bounded), then fetch this wave's share.
-__device__ __forceinline__ void must_fetch(PartialTile& pt, int ld, int epoch, int w, int lane, int* fail) {
-  if (pt.flag == nullptr || pt.got) return;
-  if (!spin_until(pt.flag, epoch)) atomicOr(fail, 4);
-  fetch_third(pt.src, ld, pt.dst, w, lane);
-  count_landed(pt);
-}
-
-// Blocked TRSM of the sub tile S = T_j+1,j against L_jj, one 16-row strip s
-// and one 16-column panel p (one wavefront): X = S(s, p) W_pp^T in place
-// (W_pp = L_pp^-1, the panel's diagonal block inverse), then
-// S(s, P) -= X L(P, p)^T for the later panels P.  Run panel by panel as the
-// POTRF finishes them, the strips give L_j+1,j = T_j+1,j L_jj^-T without
-// the full W_j (SFM_CHOL_EXT).
-__device__ __forceinline__ void ext_panel(double* Sb, const double* T, const double* Wl, int s, int p, int lane) {
-  const int j = lane & 15, kk = lane >> 4;
-  f64x4 acc = mfma16(Sb + 16 * p * TS + 16 * s, 1, TS, Wl + 16 * p * TS + 16 * p, TS, 1, f64x4{0.0, 0.0, 0.0, 0.0},
-                     lane);
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) Sb[(16 * p + j) * TS + 16 * s + 4 * rr + kk] = acc[rr];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int P = p + 1; P < 4; ++P) {
-    const f64x4 a2 = mfma16(Sb + 16 * p * TS + 16 * s, 1, TS, T + 16 * p * TS + 16 * P, TS, 1,
-                            f64x4{0.0, 0.0, 0.0, 0.0}, lane);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) Sb[(16 * P + j) * TS + 16 * s + 4 * rr + kk] -= a2[rr];
-  }
-}
-// During phase b (panels < b done): once every share of the sub tile has
-// landed, wave w (1..3) solves its strips (w - 1, and 3 for wave 3) up to
-// panel b - 1.
-__device__ __forceinline__ void ext_progress(WalkerIO& io, const double* T, int b, int w, int lane) {
-  if (io.ext_done == nullptr || io.sub.landed == nullptr) return;
-  if (__hip_atomic_load(io.sub.landed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  for (int k = 0; k < (w == 3 ? 2 : 1); ++k) {
-    const int sidx = k == 0 ? w - 1 : 3;
-    const int p0 = __builtin_amdgcn_readfirstlane(io.ext_done[sidx]);
-    for (int p = p0; p < b; ++p) ext_panel(io.sub.dst, T, io.Wl, sidx, p, lane);
-    if (p0 < b) io.ext_done[sidx] = b;
-  }
-}
-
+// pf_sub != nullptr: wave 3 polls the flags of the walker's next two
+// partial tiles once during panel 3 and leaves in *rdy whether both are out,
+// so the walker can load them beside W_j's publication (a poll during panel
+// 2 mostly came too early: the tile (j+1, j) waits for L_j,j-1).
 template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
 __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
-                                           const double* Ls, WalkerIO& io) {
+                                           const double* Ls, const int* pf_sub, const int* pf_diag, int epoch,
+                                           int* rdy) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -346,8 +184,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       // L(g0+c, g)), so one FMA stream updates both -- half the pivot work of
       // the separate wc[] registers.  Their T writes land in the tile's
       // strictly upper part, which nothing reads.
-      int r = lane;
-      asm volatile("" : "+v"(r));  // (no loop-invariant identity rows hoisted out of the walker's loop)
+      const int r = lane;
       const bool wl = r < 16;
       double p[16];
 #pragma unroll
@@ -390,8 +227,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = p[c];
     } else if (w == 0) {
       // ---- panel 0 factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
-      int r = lane;
-      asm volatile("" : "+v"(r));
+      const int r = lane;
       double p[16], wc[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -438,15 +274,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 #pragma unroll
         for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = wc[c];
     } else if (b == 0) {
-      if (io.pub_flag != nullptr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // every lane adds (lane 0 one, the rest zero): the count is uniform
-        const int old = __builtin_amdgcn_readfirstlane(atomicAdd(io.pub_cnt, (t & 63) == 0 ? 1 : 0));
-        if (old == 2) {  // the third of waves 1-3
-          *io.pub_cnt = 0;
-          __hip_atomic_store(io.pub_flag, io.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
       if (Ls != nullptr) {
         // deferred last update: wave 1 blocks (1,1) (2,2), wave 2 (2,1) (3,2),
         // wave 3 (3,1) (3,3)  [(I, J)]
@@ -456,31 +283,22 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     } else if (b == 1) {
       // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
       trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
-      // (Ls is read by nobody from here on: the sub tile may land on it)
-      try_fetch(io.diag, io.ld, io.epoch, w, lane);
-      try_fetch(io.sub, io.ld, io.epoch, w, lane);
-      ext_progress(io, T, b, w, lane);
-    } else if (b == 2) {
-      if (w == 1) w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
-      if (w == 3) trail_block(T, 16, 3, 3, lane);       // panel 1's trailing update of block (3,3)
-      try_fetch(io.diag, io.ld, io.epoch, w, lane);
-      try_fetch(io.sub, io.ld, io.epoch, w, lane);
-      ext_progress(io, T, b, w, lane);
+    } else if (b == 2 && w == 1) {
+      w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
+    } else if (b == 2 && w == 3) {
+      trail_block(T, 16, 3, 3, lane);  // panel 1's trailing update of block (3,3)
     } else if (b == 3) {
       // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
-      try_fetch(io.diag, io.ld, io.epoch, w, lane);
-      try_fetch(io.sub, io.ld, io.epoch, w, lane);
       if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
-      try_fetch(io.diag, io.ld, io.epoch, w, lane);
-      try_fetch(io.sub, io.ld, io.epoch, w, lane);
-      ext_progress(io, T, b, w, lane);
+      if (w == 3 && pf_sub != nullptr)
+        *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     }
     __syncthreads();
-    WSTAMP(k0 / 64, 8 + b);
     // ---- trailing update of column block b+1 (the next panel's); the
     // blocks right of it follow during the next panel (look-ahead) ----
     if (b < 3) {
@@ -491,7 +309,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   // ---- W row 3 off the diagonal: the products with W_33 ----
   if (w >= 1) w_row3_finish(Wl, scr[w], w - 1, lane);
   __syncthreads();
-  WSTAMP(k0 / 64, 12);
   return bad;
 }
 
@@ -499,8 +316,8 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // The whole factorisation in ONE persistent launch (left-looking tiles,
 // device-scope flags instead of kernel boundaries).
 //
-// The first workgroup to START walks the diagonal -- the critical path --
-// and never waits for a launch: for j = 0, 1, ...
+// Workgroup 0 walks the diagonal -- the critical path -- and never waits for
+// a launch: for j = 0, 1, ...
 //   T_jj (updated by the helpers for k <= j-2)  -= L_j,j-1 L_j,j-1^T
 //   POTRF -> L_jj, W_j = L_jj^-1
 //   L_j+1,j = T_j+1,j W_j^T  (kept in LDS for the next update)
@@ -510,15 +327,52 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
 // (one update short) and (j+1, j) hand the partial tile to the walker
 // (flag P); every other tile finishes with its TRSM against W_j (F(j,j)).
 // Tickets are taken in an order in which every dependency was taken
-// earlier, and roles go by start order, not by workgroup index (the walker
-// is whoever starts first, a helper takes a task only once running), so
-// every wait is on a workgroup that is already running: the grid finishes
-// even when other streams' kernels hold CUs and only part of it is resident
-// (it then runs slower, never deadlocks).  Every wait is bounded anyway (a
-// timeout sets fail bit value 4; the back substitution's own timeout sets 2).
+// earlier, and roles go by start order (the walker is the first workgroup
+// to run, a helper takes tasks only once running), so every awaited tile
+// belongs to a running workgroup and the waits drain whatever the residency;
+// every wait is bounded anyway (a timeout sets fail bit value 4; the back
+// substitution's own timeout sets 2).
 // Polls are relaxed agent-scope atomic loads (coherent across the XCDs'
 // L2s); the acquire fence comes once, after the flag is seen.  (An acquire
 // load per poll would invalidate the poller's L2 on every spin.)
+constexpr long kFlagSpins = 1L << 20;
+
+__device__ __forceinline__ bool spin_until(const int* f, int epoch) {
+  long spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    if (++spins > kFlagSpins) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// Branches around barriers are kept SCALAR: "this is wave 0" is tested on
+// readfirstlane(threadIdx.x) (an SGPR), and everything inside runs on all 64
+// lanes (same flag, same value).  A per-lane `if (threadIdx.x == 0)` inside a
+// loop that also holds barriers lets the compiler split the loop by lane
+// masks, so that lanes 1..63 of wave 0 pass the barrier without lane 0
+// (seen on gfx950: a hang on a stale ticket).
+__device__ __forceinline__ bool wave0() { return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64; }
+
+// Wave 0 waits for one flag, then the block proceeds (acquire by wave 0; the
+// barrier orders the other waves' loads after it).
+__device__ __forceinline__ void block_wait(const int* f, int epoch, int* fail) {
+  if (wave0()) {
+    if (!spin_until(f, epoch)) atomicOr(fail, 4);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes asynchronously
+  }
+  __syncthreads();
+}
+
+// Write-through publication (MI355X_MICROARCH.md: a producer that stores
+// every handed-off byte sc1 and drains every wave before the flag needs no
+// agent release; the consumers keep their acquire): every tile the walker
+// and the helpers hand off, so no publication pays an L2 write-back (the
+// release form, buffer_wbl2 + drain, wrote back the XCD's whole L2).
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void block_publish_wt(int* f, int epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -562,43 +416,16 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
   return b;
 }
 
-// W_j into LDS for a helper's TRSM: its lower 16x16 blocks (10 entries per
-// thread), handed off as data-tagged granules (ba_device.h w_sentinel_fill):
-// sc1 loads, repeated until none is the sentinel.  No flag, no acquire, no
-// drain on the walker.  Ends with a barrier.  A timeout sets fail bit 4 (the
-// grid is then not making progress: reported, never a hang).
-__device__ __forceinline__ void stage_w(const double* __restrict__ Wk, double* Wd, int* fail) {
-  const int t = threadIdx.x;
-  for (long spins = 0;; ++spins) {
-    bool miss = false;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      if ((r >> 4) >= (c >> 4)) {
-        const double v = ld_wt(Wk + c * NB + r);
-        miss |= __builtin_bit_cast(uint64_t, v) == kYSentinel;
-        Wd[c * TS + r] = v;
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(miss) == 0) break;
-    if (spins > kFlagSpins) {
-      atomicOr(fail, 4);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
-}
-
-// The helpers' TRSM X = T W^T for U stacked tiles (T_u and W = L_jj^-1,
-// lower triangular, in LDS).
+// The helpers' TRSM X = T W^T for U stacked tiles (T_u in LDS, W = L_jj^-1
+// lower triangular in global memory, column-major: W(c, m) at m*NB + c).
 // Wave w takes row block w of every tile and forms X^T (column block C) =
 // sum_{M <= C} W_CM T_wM^T on MFMA: 40 MFMAs per tile instead of 64 (the
 // products with W's zero upper blocks are skipped; they came last in the
 // k order, so the sums are bitwise the full ones), the W operand shared by
 // the U tiles.  x[u][C] reg rr holds X(16w + (lane & 15), 16C + 4rr + (lane >> 4)).
 template <int U>
-__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double* Wd, f64x4 (*x)[4], int lane) {
+__device__ __forceinline__ void trsm_rows(const double* const* Tp, const double* __restrict__ Wk, f64x4 (*x)[4],
+                                          int lane) {
   const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -614,7 +441,7 @@ __device__ __forceinline__ void trsm_rows(const double* const* Tp, const double*
       for (int u = 0; u < U; ++u) bt[u] = Tp[u][k * TS + 16 * w + li];
 #pragma unroll
       for (int C = M; C < 4; ++C) {
-        const double a = Wd[k * TS + 16 * C + li];
+        const double a = Wk[k * NB + 16 * C + li];
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u][C] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bt[u], x[u][C], 0, 0, 0);
       }
@@ -639,7 +466,7 @@ __device__ __forceinline__ void put_rows(double* __restrict__ A, int ld, int i0,
 // column (lane & 15) walks the tile's rows (128-B column runs of A).
 __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
-                                  double* Wd, int* sh, int* __restrict__ fail) {
+                                  int* sh, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -694,7 +521,6 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
             st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr, cv[a][bb][reg] - acc[a][bb][reg]);
     }
     block_publish_wt(Pf + i * nb + j, epoch);
-    HSTAMP(i, j, 0);
     return;
   }
   // final tile: T -> LDS, then X = T W_j^T on MFMA once W_j is out
@@ -705,13 +531,13 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
         T[(cb + 16 * a + lk + 4 * reg) * TS + rb + 16 * bb + lr] = cv[a][bb][reg] - acc[a][bb][reg];
-  stage_w(Winv + size_t(j) * NB * NB, Wd, fail);  // (its barrier also closes the LDS writes of T)
+  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+  const double* Wk = Winv + size_t(j) * NB * NB;
   const double* Tp[1] = {T};
   f64x4 x[1][4];
-  trsm_rows<1>(Tp, Wd, x, lane);
+  trsm_rows<1>(Tp, Wk, x, lane);
   put_rows<1>(A, ld, i0, j0, x, lane);
   block_publish_wt(F + i * nb + j, epoch);
-  HSTAMP(i, j, 1);
 }
 
 // Helper: the vertical pair of final tiles (i, j), (i+1, j) (i >= j + 2).
@@ -724,7 +550,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld, int nb,
                                                   const double* __restrict__ Winv, int* __restrict__ F, int epoch,
                                                   int i, int j, double* T0, double* T1, int* sh,
-                                                  double* Wd, int* __restrict__ fail) {
+                                                  int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -778,18 +604,17 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
           Tu[c * TS + r] = A[size_t(j0 + c) * ld + iu + r] - acc[u][a][bb][reg];
         }
   }
-  stage_w(Winv + size_t(j) * NB * NB, Wd, fail);  // (its barrier also closes the LDS writes of T0, T1)
+  block_wait(F + j * nb + j, epoch, fail);  // (its barrier also closes the LDS writes)
+  const double* Wk = Winv + size_t(j) * NB * NB;
   const double* Tp[2] = {T0, T1};
   f64x4 x[2][4];
-  trsm_rows<2>(Tp, Wd, x, lane);
+  trsm_rows<2>(Tp, Wk, x, lane);
   put_rows<2>(A, ld, i0, j0, x, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (wave0()) {
     __hip_atomic_store(F + i * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F + (i + 1) * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    HSTAMP(i, j, 1);
-    HSTAMP(i + 1, j, 1);
   }
 }
 
@@ -832,85 +657,98 @@ __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) 
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) D[(16 * Cb + li) * TS + 16 * w + 4 * rr + kk] = x[Cb][rr];
 }
+__device__ __forceinline__ void load_tile(double* D, const double* __restrict__ A, int ld, int i0, int j0) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
+    D[c * TS + r] = A[size_t(j0 + c) * ld + i0 + r];
+  }
+}
+__device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i0, int j0, const double* D) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int e = threadIdx.x + 256 * q, c = e >> 6, r = e & 63;
+    A[size_t(j0 + c) * ld + i0 + r] = D[c * TS + r];
+  }
+}
+
 // The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
 // TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
-// Hand-offs on the walker's path carry no acquire and no drain:
-//   * the partial tiles (j+1, j) and (j+1, j+1) are copied into LDS by waves
-//     1-3 during the POTRF as soon as their flags are out (sc1 loads;
-//     potrf_tile), the sub tile onto L_j,j-1's buffer once the last update
-//     has read it, the next diagonal tile into the buffer the next step
-//     factors (the two tile buffers swap);
-//   * W_j goes out as data-tagged granules (stage_w);
-//   * L_j+1,j is stored by waves 1-3, which drain and flag it at the start of
-//     the next step's panel 0.
+// When the POTRF's poll found the partial tiles (j+1, j) and (j+1, j+1)
+// already out, their loads are issued beside W_j's write-through stores and
+// share one drain with them; the stores of L_j+1,j drain during the next
+// step's first update, and their flag goes out after it.
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
-                                             int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* Ta,
-                                             double* Tb, double* Wl, double* Ls, double (*scr)[256], int* pub_cnt,
-                                             int* xsh, int* __restrict__ fail) {
+                             int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
+                             double* Ls, double (*scr)[256], int* rdy, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  double* T = Ta;   // the tile being factored
-  double* Tn = Tb;  // the next diagonal tile (prefetched)
-  if (t == 0) *pub_cnt = 0;
-  // tile (0, 0): every wave fetches its columns after the flag
-  block_poll(Pf, epoch, fail);
+  // the next diagonal tile travels in registers (loaded one step ahead)
+  double nx[16];
+  block_wait(Pf, epoch, fail);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    T[c * TS + r] = ld_wt(A + size_t(c) * ld + r);
+    nx[q] = A[size_t(c) * ld + r];
   }
-  __syncthreads();
   for (int j = 0; j < nb; ++j) {
     const int j0 = j * NB;
-    WSTAMP(j, 0);
-#ifdef SFM_CHOL_EXT
-    if (t < 5) xsh[t] = 0;  // the sub tile's landed count, its strips' solved panels (barriers follow)
-#endif
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      T[c * TS + r] = nx[q];
+    }
+    if (t == 0) *rdy = 0;
+    __syncthreads();
     if (j > 0) {
       // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
       // blocks right of it are updated inside potrf_tile, during panel 0
       const int Ib[1] = {w}, Jb[1] = {0};
       last_update<1>(T, Ls, Ib, Jb, 1, lane);
-      __syncthreads();
+      // L_j,j-1 (stored at the end of the last step) has drained: its flag
+      block_publish_wt(F + j * nb + j - 1, epoch);
     }
-    WSTAMP(j, 1);
+    const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
     const bool more = j + 1 < nb;
     const int i0 = j0 + NB;
-    WalkerIO io;
-    io.ld = ld;
-    io.epoch = epoch;
-    if (j > 0) {  // L_j,j-1, stored by waves 1-3 at the end of the last step
-      io.pub_flag = F + j * nb + j - 1;
-      io.pub_cnt = pub_cnt;
-    }
-    if (more && w > 0) {
-      io.sub = PartialTile{Pf + (j + 1) * nb + j, A + size_t(j0) * ld + i0, Ls, false, nullptr};
-      io.diag = PartialTile{Pf + (j + 1) * nb + j + 1, A + size_t(i0) * ld + i0, Tn, false, nullptr};
-#ifdef SFM_CHOL_EXT
-      io.sub.landed = xsh;
-      io.ext_done = xsh + 1;
-      io.Wl = Wl;
-#endif
-    }
-    if (j == 0) __syncthreads();  // (xsh reset before any wave of step 0 counts in)
-    const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, io)
-                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, io);
-    WSTAMP(j, 2);
+    const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
+    const int* fdiag = more ? Pf + (j + 1) * nb + j + 1 : nullptr;
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
+                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
     if (bad) atomicOr(fail, 1);
-    // W_j out: lower 16x16 blocks only (the upper blocks stay zero from
-    // set_problem); each entry is its own flag (stage_w): no drain, no flag
+    const bool early = more && __builtin_amdgcn_readfirstlane(*rdy) != 0;
+    double sub[16];
+    if (early) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        sub[q] = A[size_t(j0 + c) * ld + i0 + r];
+        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+      }
+    }
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      // lower 16x16 blocks only: the upper blocks of every W_k stay zero
+      // from set_problem (one memset), 37% fewer bytes on the chain
       if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
-#ifdef SFM_CHOL_STAMPS
-    if (t == 64 && j < 256) g_wstamp[j * 16 + 7] = (io.sub.got ? 1 : 0) + (io.diag.got ? 2 : 0);  // wave 1's view
-#endif
+    if (early) {
+      // T (L_jj) is read by nobody from here on (see below): it takes the
+      // subdiagonal tile
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        T[c * TS + r] = sub[q];
+      }
+    }
+    // W_j out at once: the helpers' TRSMs of column j feed the last updates
+    // of the diagonal tiles two steps ahead (a chain as long as a step)
+    block_publish_wt(F + j * nb + j, epoch);
     if (!more) {
       // L_jj is read by nobody (the helpers' TRSMs and the back substitution
       // use W_j; the next Schur pass rewrites the lower triangle) except in
@@ -925,38 +763,27 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       }
       break;
     }
-    // what the POTRF's polls did not catch (waves 1-3, their own shares)
-    if (w > 0) {
-      must_fetch(io.sub, ld, epoch, w, lane, fail);
-      must_fetch(io.diag, ld, epoch, w, lane, fail);
-    }
-    __syncthreads();
-    WSTAMP(j, 3);
-#ifdef SFM_CHOL_EXT
-    // the strips' panels the POTRF's phases did not solve: wave w, strip w
-    {
-      const int p0 = __builtin_amdgcn_readfirstlane(xsh[1 + w]);
-      for (int p = p0; p < 4; ++p) ext_panel(Ls, T, Wl, w, p, lane);
-    }
-#else
-    // subdiagonal tile: L_j+1,j = T_j+1,j W_j^T in place (wave w reads and
-    // writes only row block w of it), kept as Ls for the next update
-    f64x4 x[4];
-    trsm_lds(Ls, Wl, x, lane);
-    put_tile(Ls, x, lane);
-#endif
-    __syncthreads();
-    WSTAMP(j, 5);
-    if (w > 0) {  // waves 1-3 store it (write-through); drained and flagged in the next step's panel 0
-      for (int e = t - 64; e < NB * NB; e += 192) {
-        const int c = e >> 6, r = e & 63;
-        st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+    if (!early) {
+      // the poll missed: wait for the partial tiles here
+      block_wait(Pf + (j + 1) * nb + j, epoch, fail);
+      load_tile(T, A, ld, i0, j0);
+      block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = t + 256 * q, c = e >> 6, r = e & 63;
+        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
       }
     }
-    WSTAMP(j, 6);
-    double* tmp = T;
-    T = Tn;
-    Tn = tmp;
+    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
+    f64x4 x[4];
+    trsm_lds(T, Wl, x, lane);
+    put_tile(Ls, x, lane);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
+    }
   }
 }
 
@@ -968,10 +795,8 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
-  __shared__ double Tn[NB * TS];  // the walker's second diagonal-tile buffer
   __shared__ double scr[4][256];
-  __shared__ int sh[3];
-  __shared__ int xsh[8];
+  __shared__ int sh[2];
   if (gate && *gate == 0) {
     // device LM loop, phase skipped: the launch still takes its ntask + nhelp
     // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
@@ -982,7 +807,10 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     }
     return;
   }
-  // role by start order: the first workgroup to run walks the diagonal
+  // role by start order: the first workgroup to run walks the diagonal, so
+  // every tile the walker awaits is owned by a running helper whatever the
+  // residency (a grid only partly resident beside other streams' kernels runs
+  // slower but finishes)
   if (wave0()) {
     const unsigned long long v = atomicAdd(ticket + 1, threadIdx.x == 0 ? 1ULL : 0ULL);
     const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
@@ -993,7 +821,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Tn, Wl, Ls, scr, sh + 2, xsh, fail);
+    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
     return;
   }
   const int ntask = chol_tasks(nb);
@@ -1018,11 +846,11 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     int j = 0, r = tk;
     while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
     if (r < 3) {
-      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, Ls, sh, fail);
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
     } else {
       const int i = j + 3 + 2 * (r - 3);
-      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, Ls, fail);
-      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, Ls, sh, fail);
+      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail);
+      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail);
     }
   }
 }
@@ -1092,7 +920,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
       lv[i + 1] = q.y;
     }
     double* yb = yl[k & 1];  // double-buffered: one barrier per block
-    if (wave0()) {  // scalar branch (see wave0)
+    if (wave0()) {  // scalar branch (see block_wait)
       const int lane = threadIdx.x & 63;
       const double* p = y + size_t(k) * NB + lane;
       double yv = 0.0;
@@ -1144,13 +972,6 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
                                          epoch, nhelp, d.fail, d.gate);
 }
 
-__global__ void k_w_sentinel(double* __restrict__ invL, int nblk) {
-  w_sentinel_fill(invL, nblk, blockIdx.x, gridDim.x, threadIdx.x, blockDim.x);
-}
-void launch_w_sentinel(const DevProblem& d, hipStream_t s) {
-  if (d.nblk > 0) k_w_sentinel<<<std::min(1024, d.nblk * 4), 256, 0, s>>>(d.invL, d.nblk);
-}
-
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
   const int nb_real = (d.n + NB - 1) / NB;
   if (nb_real <= 0) return;
@@ -1162,14 +983,3 @@ void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentin
 }
 
 }  // namespace sfm
-
-#ifdef SFM_CHOL_STAMPS
-extern "C" int sfm_debug_stamps(unsigned long long* out, int n) {
-  if (n > 256 * 16) n = 256 * 16;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_wstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
-}
-extern "C" int sfm_debug_hstamps(unsigned long long* out, int n) {
-  if (n > 64 * 64 * 2) n = 64 * 64 * 2;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_hstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
-}
-#endif

@@ -122,34 +122,30 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
   const double eps = kDblEps * 10;
   for (int iter = 0; iter < 30; ++iter) {
     bool changed = false;
-    // One sweep is straight-line code: a rotation that OpenCV skips
-    // (|p| <= eps sqrt(ab)) is computed anyway and not applied (selects,
-    // bitwise the skipped one), so the sweep is one basic block and the
-    // scheduler overlaps the rotations of disjoint row pairs -- (i, j)
-    // depends only on the last rotations of rows i and j, a dependency
-    // chain of ~2 x 12 instead of 66 rotations.  Every row still sees its
-    // rotations in OpenCV's order: the same values bit for bit.
 #pragma unroll
     for (int i = 0; i < 11; ++i)
 #pragma unroll
       for (int j = i + 1; j < 12; ++j) {
         const double a = W[i], b = W[j];
-        const double p0 = tree16(u[i] * u[j]);
-        const bool skip = fabs(p0) <= eps * sqrt(a * b);
-        const double p = p0 * 2;
+        double p = tree16(u[i] * u[j]);
+        if (fabs(p) <= eps * sqrt(a * b)) continue;
+        p *= 2;
         const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-        const double delta = (gamma - beta) * 0.5;
-        const double sn_n = sqrt(delta / gamma);
-        const double c_p = sqrt((gamma + beta) / (gamma * 2));
-        const double c = beta < 0 ? p / (gamma * sn_n * 2) : c_p;
-        const double sn = beta < 0 ? sn_n : p / (gamma * c_p * 2);
+        double c, sn;
+        if (beta < 0) {
+          const double delta = (gamma - beta) * 0.5;
+          sn = sqrt(delta / gamma);
+          c = p / (gamma * sn * 2);
+        } else {
+          c = sqrt((gamma + beta) / (gamma * 2));
+          sn = p / (gamma * c * 2);
+        }
         const double t0 = c * u[i] + sn * u[j], t1 = -sn * u[i] + c * u[j];
-        const double w0 = tree16(t0 * t0), w1 = tree16(t1 * t1);
-        u[i] = skip ? u[i] : t0;
-        u[j] = skip ? u[j] : t1;
-        W[i] = skip ? W[i] : w0;
-        W[j] = skip ? W[j] : w1;
-        changed |= !skip;
+        u[i] = t0;
+        u[j] = t1;
+        W[i] = tree16(t0 * t0);
+        W[j] = tree16(t1 * t1);
+        changed = true;
       }
     if (!changed) break;
   }

@@ -145,15 +145,21 @@ def sim3_align(src, dst):
     return s, R, mu_d - s * R @ mu_s
 
 
-def gauge_invariant_diff(residual_fn, sc, sol_a, sol_b):
+def gauge_invariant_diff(residual_fn, sc, sol_a, sol_b, extent=False):
     """Gauge-invariant distances between two solutions (rot, t, X) of scene
     `sc`: max |r_a - r_b| over observation residuals (pixels), and the max
     relative distance of camera centres + points after a Sim(3) alignment
-    of a onto b (SURVEY.md §7 hard part 2)."""
+    of a onto b (SURVEY.md §7 hard part 2) -- per coordinate (floor 1e-3),
+    or with `extent` as max |a - b| over the scene's RMS radius about its
+    centroid (for scenes whose first camera sits at the origin, where a
+    per-coordinate ratio divides rounding by the floor)."""
     ra = residual_fn(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, *sol_a)
     rb = residual_fn(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, *sol_b)
     pa = np.vstack([camera_centres(sol_a[0], sol_a[1]), sol_a[2]])
     pb = np.vstack([camera_centres(sol_b[0], sol_b[1]), sol_b[2]])
     s, R, t = sim3_align(pa, pb)
     al = s * pa @ R.T + t
+    if extent:
+        radius = float(np.sqrt(np.mean(np.sum((pb - pb.mean(axis=0)) ** 2, axis=1))))
+        return float(np.max(np.abs(ra - rb))), float(np.max(np.linalg.norm(al - pb, axis=1)) / radius)
     return float(np.max(np.abs(ra - rb))), float(np.max(np.abs(al - pb) / np.maximum(np.abs(pb), 1e-3)))

