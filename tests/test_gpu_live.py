@@ -167,27 +167,29 @@ def test_live_path_on_device_brisk_detections(run_brisk):
         # after a Sim(3) alignment
         sc_ = type("S", (), dict(uv=rec["uv"], cam_idx=rec["cam_idx"], pt_idx=rec["pt_idx"], K=rec["K"]))
         res, al = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]), (r, t, X), extent=True)
-        _, sens_al = L.gauge_invariant_diff(_residuals, sc_, (rp, tp, Xp), (r, t, X), extent=True)
+        sens_res, sens_al = L.gauge_invariant_diff(_residuals, sc_, (rp, tp, Xp), (r, t, X), extent=True)
         table.append(dict(ba=k, obs=len(rec["uv"]), iterations=sm_o["num_iterations"],
                           termination=sm_o["termination_type"], cost_rel=d, cost_sensitivity=sens, X_rel=dx,
-                          X_sensitivity=sens_x, residual_max_px=res, sim3_aligned_rel=al,
-                          sim3_aligned_sensitivity=sens_al))
+                          X_sensitivity=sens_x, residual_max_px=res, residual_sensitivity_px=sens_res,
+                          sim3_aligned_rel=al, sim3_aligned_sensitivity=sens_al))
         print(f"keyframe BA {k}: {len(rec['uv'])} obs, iterations {sm_o['num_iterations']} "
               f"({sm_o['termination_type']}), cost rel diff {d:.2e} (oracle rounding sensitivity {sens:.2e}), "
-              f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e}), residuals {res:.1e} px, Sim(3)-aligned {al:.1e}")
+              f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e}), residuals {res:.1e} px, Sim(3)-aligned {al:.1e} (sensitivity {sens_res:.1e} px, {sens_al:.1e})")
         assert rec["summary"].num_iterations == sm_o["num_iterations"]
-        # (measured: BA 0-2 agree to 3e-14 in cost / 3e-7 in X; BA 3 runs
-        # into the 50-iteration cap along a flat direction, where 2 ulp of
-        # start perturbation move the oracle's own result by 8e-9 in cost).
-        # The rounding-sensitivity allowance is capped: cost 1e-6, X 1e-5
-        # relative whatever the sensitivity (north-star tolerance 1e-6).
+        # (measured round 4: BA 0-2 agree to 1e-13 in cost / 3e-7 in X; BA 3
+        # runs into the 50-iteration cap drifting along the free 7-DoF gauge,
+        # where 2 ulp of start perturbation move the oracle's OWN raw X by
+        # 1e-4 -- a raw-X cap below that no implementation meets, the
+        # reference run twice included -- while its gauge-invariant distances
+        # stay at 2e-5 px / 9e-6 of the scene radius.)
+        # Every allowance is 20x the oracle's own rounding sensitivity, capped:
+        #   cost (north-star tolerance)            1e-6 relative
+        #   residuals, Sim(3)-aligned distance     1e-4 px, 1e-5 of the radius
+        #   raw X (gauge-dependent)                1e-3 relative
         assert d <= min(1e-6, max(1e-9, 20 * sens)), (k, d, sens)
-        assert dx <= min(1e-5, max(1e-6, 20 * sens_x)), (k, dx, sens_x)
-        # Sim(3)-aligned distance over the scene radius: the same capped
-        # allowance as X (measured round 4: BA 2 at 3e-7 X rel, which a
-        # per-coordinate ratio at the origin camera read as 1.7e-4)
-        assert res <= 1e-6, (k, res)
-        assert al <= min(1e-5, max(1e-6, 20 * sens_al)), (k, al, sens_al)
+        assert res <= min(1e-4, max(1e-8, 20 * sens_res)), (k, res, sens_res)
+        assert al <= min(1e-5, max(1e-9, 20 * sens_al)), (k, al, sens_al)
+        assert dx <= min(1e-3, max(1e-6, 20 * sens_x)), (k, dx, sens_x)
     # the per-keyframe table (committed as profiles/r04_live_brisk_ba_parity.json)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, "live_brisk_ba_parity.json"), "w") as f:

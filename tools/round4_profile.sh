@@ -16,3 +16,5 @@ timeout -k 10 900 bash $R/tools/pmc_traffic.sh > $O/pmc_traffic.txt 2>&1 || exit
 python3 $R/tools/pmc_json.py $R/gpurun_out/pmc_traffic $O/pmc_c3.json > $O/pmc_json.txt 2>&1 || exit 1
 timeout -k 10 200 bash $R/tools/pmc_mfma.sh > $O/pmc_mfma.txt 2>&1 || exit 1
 cp $R/gpurun_out/pmc_mfma/pmc_mfma.json $O/pmc_mfma_c3.json
+timeout -k 10 200 bash $R/tools/pmc_stall.sh > $O/pmc_stall.txt 2>&1 || exit 1
+cp $R/gpurun_out/pmc_stall/pmc_stall.json $O/pmc_stall_c3.json
