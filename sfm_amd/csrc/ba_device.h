@@ -78,6 +78,7 @@ struct DevProblem {
   int32_t* cm_p = nullptr;     // [N_pad] point index at camera-major position i
   int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
   int32_t n_jchunks = 0;
+  int32_t xcd_slice_max = 0;   // chunks of the largest of the 8 point slices (host copy)
   int32_t* jgrp = nullptr;     // [9] chunk-table offsets of the 8 point slices (one per XCD)
   int32_t jac_blocks = 1;      // persistent grid of k_jacobian in the solve (cost partials)
   int32_t jac_blocks_rec = 1;  // ... of the record-writing variant (evaluate API, bench roofline)
@@ -193,8 +194,12 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = tr
 // grid of the XCD-ordered observation passes (k_obs_prep_rc, k_backsub_a_rc):
 // one workgroup per 4 chunks, a multiple of 8 (one point slice per XCD)
 inline int obs_xcd_blocks(const DevProblem& d) {
-  const int64_t nb = (d.N_pad / 64 + 3) / 4;
-  return int(8 * std::max<int64_t>(1, (nb + 7) / 8));
+  // one wave per chunk of the LARGEST slice (slices differ by ~5% at C3; a
+  // grid sized by the mean left the largest slice's excess chunks to a
+  // second round of waves: 45.6 -> 50.0 us for k_obs_prep_rc)
+  const int64_t per = d.xcd_slice_max > 0 ? (int64_t(d.xcd_slice_max) + 3) / 4
+                                          : ((d.N_pad / 64 + 3) / 4 + 7) / 8;
+  return int(8 * std::max<int64_t>(1, per));
 }
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]

@@ -1180,8 +1180,17 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
   // (into the stage: stream order puts it after the upload that reads the stage)
   HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  // and the 8 slices' chunk offsets: the observation passes size their grids
+  // by the largest slice (obs_xcd_blocks)
+  HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HCHK(hipStreamSynchronize(s));
   std::memcpy(&n_pairs, stg, sizeof(int64_t));
+  {
+    int32_t g[9];
+    std::memcpy(g, stg + 8, sizeof(g));
+    d.xcd_slice_max = 0;
+    for (int i = 0; i < 8; ++i) d.xcd_slice_max = std::max(d.xcd_slice_max, g[i + 1] - g[i]);
+  }
   timer.mark("layouts (device)");
   if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
   d.n_blk = int64_t(C) * (C + 1) / 2;
