@@ -697,10 +697,13 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(const int32_t* __restr
                                                           double* __restrict__ dpart, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const XcdChunks xc = xcd_chunks(grp_off, wv);
-  for (int t = xc.t; t < xc.end; t += xc.stride) {  // wave-uniform, no barriers below
-  const int4 ch = chunks[t];
-  const int64_t i0 = ch.y;
+  // ONE chunk per wave: the grid covers the largest slice (obs_xcd_blocks).
+  // (A loop over the slice's chunks took the kernel from 74 to 105 VGPRs,
+  // 6 -> 4 waves per SIMD: 45.6 -> 49.5 us at C3.)
+  const XcdChunks xc = xcd_chunks(grp_off, wave_uniform(wv));
+  if (xc.t >= xc.end) return;  // wave-uniform, no barriers below
+  const int4 ch = chunks[xc.t];
+  const int64_t i0 = __builtin_amdgcn_readfirstlane(ch.y);
   const int64_t i = i0 + l;
   const int c = __builtin_amdgcn_readfirstlane(ch.x);
   ObsRC o;
@@ -728,7 +731,6 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(const int32_t* __restr
   for (int e = 27; e < 32; ++e) v[e] = 0.0;
   const double tot = wave_sum32(v, l);
   if (!(l & 1) && (l >> 1) < 27) dpart[size_t(i0 / 64) * 27 + (l >> 1)] = tot;
-  }
 }
 
 // Back substitution pass A (see k_backsub_b): e = J_c y_c, u = M^T e, and
@@ -750,10 +752,10 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(const int32_t* __rest
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double model = 0.0;
-  const XcdChunks xc = xcd_chunks(grp_off, wv);
+  const XcdChunks xc = xcd_chunks(grp_off, wave_uniform(wv));
   for (int t = xc.t; t < xc.end; t += xc.stride) {  // wave-uniform
     const int4 ch = chunks[t];
-    const int64_t i = int64_t(ch.y) + l;
+    const int64_t i = int64_t(__builtin_amdgcn_readfirstlane(ch.y)) + l;
     const int c = __builtin_amdgcn_readfirstlane(ch.x);
     ObsRC o;
     obs_recompute(c, cm_p[i], ld2(uv_cm + 2 * i), camR, cam, Kc, scale_c, ptS, o);
