@@ -960,10 +960,104 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
   if (wave0() && timed_out) atomicOr(fail, 2);
 }
 
+// Small systems (nblk <= 2: n <= 127, keyframe-sized BAs of up to 21
+// cameras): the factorisation AND the back substitution in ONE workgroup,
+// no flags, tickets or global round trips.  At nblk <= 2 the persistent
+// launch is two walker steps plus its start-up and the back substitution a
+// second launch (C1: 37.6 + 4.7 us per step solve, each a few us of work).
+// The tile operations and their order are k_chol_fused's walker (the
+// helpers' partial tiles are the input tiles: no earlier column exists) and
+// k_backsolve's arithmetic: bitwise the same L, W and y.
+__global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A, int ld, int n, int nb,
+                                                    double* __restrict__ y, int* __restrict__ fail,
+                                                    const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  __shared__ double T[NB * TS];    // diagonal tile being factored, then L_jj
+  __shared__ double Wl[NB * TS];   // W_j of the current step
+  __shared__ double Ls[NB * TS];   // L_10
+  __shared__ double W0[NB * TS];   // W_0 (kept for the back substitution)
+  __shared__ double scr[4][256];
+  __shared__ double v[NB];
+  __shared__ double yl[NB];        // y_1
+  __shared__ int rdy;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // ---- step 0: POTRF of tile (0, 0) ----
+  load_tile(T, A, ld, 0, 0);
+  __syncthreads();
+  const bool bad0 = (NB <= n) ? potrf_tile<true>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, &rdy)
+                              : potrf_tile<false>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, &rdy);
+  bool bad = bad0;
+  if (nb > 1) {
+    // W_0 kept; L_10 = A_10 W_0^T (the walker's TRSM of the subdiagonal tile)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = t + 256 * q, c = e >> 6, r = e & 63;
+      W0[c * TS + r] = Wl[c * TS + r];
+      T[c * TS + r] = A[size_t(c) * ld + NB + r];
+    }
+    __syncthreads();
+    f64x4 x[4];
+    trsm_lds(T, Wl, x, lane);
+    put_tile(Ls, x, lane);
+    __syncthreads();
+    // ---- step 1: T_11 -= L_10 L_10^T (column block 0 here, the rest inside
+    // the POTRF's panel 0, as the walker), POTRF of tile (1, 1) ----
+    load_tile(T, A, ld, NB, NB);
+    __syncthreads();
+    {
+      const int Ib[1] = {w}, Jb[1] = {0};
+      last_update<1>(T, Ls, Ib, Jb, 1, lane);
+    }
+    __syncthreads();
+    bad |= (2 * NB <= n) ? potrf_tile<true>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, &rdy)
+                         : potrf_tile<false>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, &rdy);
+  }
+  if (bad && t == 0) atomicOr(fail, 1);
+  // ---- back substitution L^T y = z, z = row n of the factor (k_backsolve's
+  // arithmetic, block rows nb_real - 1 .. 0) ----
+  const int nb_real = (n + NB - 1) / NB;
+  const int col = t >> 2, seg = t & 3, rn = n & (NB - 1);
+  // tile (n / 64, b) of the factor holding row n: L_00 (T, nb == 1), L_10
+  // (Ls) and L_11 (T) (nb == 2)
+  for (int b = nb_real - 1; b >= 0; --b) {
+    const int k0 = b * NB;
+    const int nreal = (n - k0) < NB ? (n - k0) : NB;
+    const double* Zt = (nb == 1 || b == 1) ? T : Ls;
+    const double* Wb = (nb == 1 || b == 1) ? Wl : W0;
+    const double zc = (seg == 0 && col < nreal) ? Zt[col * TS + rn] : 0.0;
+    double acc = 0.0;
+    if (b == 0 && nb_real == 2) {
+      // k = 1: L_10^T y_1 (column col of L_10, rows 16 seg .. +16)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc = fma(Ls[col * TS + 16 * seg + i], yl[16 * seg + i], acc);
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (seg == 0) v[col] = (col < nreal) ? zc - acc : 0.0;
+    __syncthreads();
+    double p4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p4[i & 3] = fma(Wb[col * TS + 16 * seg + i], v[16 * seg + i], p4[i & 3]);
+    double sum = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+    sum += __shfl_xor(sum, 1);
+    sum += __shfl_xor(sum, 2);
+    if (seg == 0) {
+      const double yv = col < nreal ? sum : 0.0;
+      y[k0 + col] = yv;
+      if (b == 1) yl[col] = yv;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
+  if (d.nblk <= 2) {  // factor + back substitution in one workgroup
+    k_chol_small<<<1, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.ysol, d.fail, d.gate);
+    return;
+  }
   const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (roles by start order: a partly resident
   // grid still finishes)
@@ -974,7 +1068,7 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
   const int nb_real = (d.n + NB - 1) / NB;
-  if (nb_real <= 0) return;
+  if (nb_real <= 0 || d.nblk <= 2) return;  // (nblk <= 2: k_chol_small solved too)
   // the sentinel in every entry of y the launch produces (ld >= 64 nb_real;
   // the solve's k_pad_init writes it, saving a launch)
   if (!sentinel_set)
