@@ -79,6 +79,11 @@ struct DevProblem {
   int4* jchunks = nullptr;     // [n_jchunks] (camera, first position, count, 0): k_jacobian work units
   int32_t n_jchunks = 0;
   int32_t xcd_slice_max = 0;   // chunks of the largest of the 8 point slices (host copy)
+  // Schur / Cholesky overlap (compute_step_enqueue): per 64x64 tile of S the
+  // camera blocks landed so far and the count that completes it
+  int32_t* tile_cnt = nullptr;  // [nblk * nblk], zeroed before each Schur pass
+  int32_t* tile_exp = nullptr;  // [nblk * nblk], from set_problem
+  int32_t overlap = 0;          // k_chol_fused waits on tile_cnt (and leaves CUs to k_schur_pts)
   int32_t* jgrp = nullptr;     // [9] chunk-table offsets of the 8 point slices (one per XCD)
   int32_t jac_blocks = 1;      // persistent grid of k_jacobian in the solve (cost partials)
   int32_t jac_blocks_rec = 1;  // ... of the record-writing variant (evaluate API, bench roofline)
@@ -185,6 +190,11 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 void launch_point_prep(const DevProblem& d, double radius, hipStream_t s);
 void launch_point_factor(const DevProblem& d, double radius, hipStream_t s);
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
+// its two parts: the diagonal blocks + rhs (k_schur_diag_sum) and the
+// off-diagonal blocks (k_schur_pts; tile_cnt != nullptr: overlapped with the
+// factorisation, blocks counted per 64x64 tile as they land)
+void launch_schur_diag(const DevProblem& d, double radius, bool add_diag, hipStream_t s);
+void launch_schur_offdiag(const DevProblem& d, int* tile_cnt, hipStream_t s);
 void launch_pad_init(const DevProblem& d, hipStream_t s);
 void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
 // dst = scale * src unless *gate == 0 (gate may be nullptr)

@@ -301,16 +301,24 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
         // e into the run's last chunk slot, the run's other slots get zeros
         // (k_cam_sum adds a camera's slots in order) -- no second pass over
         // the records
+        // padding lanes: their 12 J_c entries and 2 residuals zeroed once,
+        // so each product sum adds an exact 0 (bitwise the masked sum, 14
+        // selects instead of 27)
         const bool real = l < cnt;
-        const double* j0 = rec + kJC;
-        const double* j1 = rec + kJC + 6;
+        double j0[6], j1[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          j0[a] = real ? rec[kJC + a] : 0.0;
+          j1[a] = real ? rec[kJC + 6 + a] : 0.0;
+        }
+        const double r0 = real ? rec[kRes] : 0.0, r1 = real ? rec[kRes + 1] : 0.0;
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a)
 #pragma unroll
-          for (int b = a; b < 6; ++b, ++q) acc[q] += real ? j0[a] * j0[b] + j1[a] * j1[b] : 0.0;
+          for (int b = a; b < 6; ++b, ++q) acc[q] += j0[a] * j0[b] + j1[a] * j1[b];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) acc[21 + a] += real ? j0[a] * rec[kRes] + j1[a] * rec[kRes + 1] : 0.0;
+        for (int a = 0; a < 6; ++a) acc[21 + a] += j0[a] * r0 + j1[a] * r1;
         double tot = 0.0;
         if (t + 1 >= n_chunks || ch_n.x != c) {  // wave-uniform
           tot = wave_sum32(acc, l);
@@ -869,7 +877,8 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
                                                         const double* __restrict__ cam, const double* __restrict__ Kc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int ld,
-                                                        const int32_t* __restrict__ bperm, const int* __restrict__ gate) {
+                                                        const int32_t* __restrict__ bperm, const int* __restrict__ gate,
+                                                        int* __restrict__ tile_cnt, int nbt) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   static_assert(kWpb == 1 || (kWpb == kThreads / 64 && kSub == 64), "4 waves per block take 64 lanes each");
   constexpr int kPer = 64 / kSub;  // blocks per wave
@@ -1021,7 +1030,10 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
     auto put = [&](int e, double v) {
       double* q = Sb + size_t(e / 6) * ld + e % 6;
       v = v * sc1[e / 6] * sc2[e % 6];
-      *q = add ? *q - v : -v;
+      v = add ? *q - v : -v;
+      // overlapped with the factorisation: write-through, counted per tile
+      if (tile_cnt) __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *q = v;
     };
     constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
     if (kSub == 64) {
@@ -1031,6 +1043,19 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
       for (int r = 0; r < kR; ++r) put(kR * sl + r, v32[r]);
     }
     if (sl < 4) put(32 + sl, sl == 0 ? t32 : sl == 1 ? t33 : sl == 2 ? t34 : t35);
+  }
+  if (tile_cnt) {
+    // Schur/Cholesky overlap: the block's entries are out (write-through,
+    // drained by this wave), then one lane per block counts it into every
+    // 64x64 tile its 6x6 footprint touches; a helper of k_chol_fused reads a
+    // tile once its count is complete (set_problem's tile_exp)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (own && sl == 0) {
+      const int r0 = 6 * cc.y, c0 = 6 * cc.x;
+      for (int I = r0 / 64; I <= (r0 + 5) / 64; ++I)
+        for (int J = c0 / 64; J <= (c0 + 5) / 64; ++J)
+          __hip_atomic_fetch_add(tile_cnt + I * nbt + J, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1437,20 +1462,31 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
   // the off-diagonal blocks, which add a block's same-camera duplicate pairs
+  launch_schur_diag(d, radius, add_diag, s);
+  launch_schur_offdiag(d, nullptr, s);
+}
+void launch_schur_diag(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   if (d.C)
     k_schur_diag_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, add_diag ? 1 : 0, d.S, d.ld,
                                         d.n, 1, d.gate, d.radius_dev, d.fail,
                                         reinterpret_cast<unsigned long long*>(d.ysol), (d.n + kNB - 1) / kNB * kNB);
+}
+// tile_cnt != nullptr: overlapped with k_chol_fused (compute_step_enqueue):
+// the blocks in their plain order (camera-major: the factor's tile columns
+// complete left to right) and counted per tile
+void launch_schur_offdiag(const DevProblem& d, int* tile_cnt, hipStream_t s) {
   if (!d.n_blk) return;
+  const int64_t n_slots = tile_cnt ? d.n_blk : d.n_bslots;
+  const int32_t* bperm = tile_cnt ? nullptr : d.bperm;
   const int sub = d.schur_pts_sub, per = 64 / sub * (kThreads / 64);
-  const int nb = int((d.n_bslots + per - 1) / per);
+  const int nb = int((n_slots + per - 1) / per);
 #define SFM_PTS(S_)                                                                                           \
-  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                          d.S, d.ld, d.bperm, d.gate)
+  k_schur_pts<S_><<<nb, kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
+                                          d.S, d.ld, bperm, d.gate, tile_cnt, d.nblk)
   if (d.schur_wg_blocks) {  // small systems: one block per workgroup
-    k_schur_pts<64, kThreads / 64><<<int(d.n_bslots), kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS,
-                                                                       d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
-                                                                       d.bperm, d.gate);
+    k_schur_pts<64, kThreads / 64><<<int(n_slots), kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS,
+                                                                    d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
+                                                                    bperm, d.gate, tile_cnt, d.nblk);
     return;
   }
   if (sub == 8) SFM_PTS(8);

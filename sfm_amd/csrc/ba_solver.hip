@@ -116,6 +116,10 @@ struct sfm_ba_handle {
   // candidate current (k_lm_accept folded in; its grid covers the copy)
   int accept_grid = 0;
   int n_cu = 0;  // compute units of the device (queried once)
+  // Schur / Cholesky overlap (DevProblem::overlap): the factorisation's
+  // stream and the two events that fork and join it
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ov_ev[2] = {nullptr, nullptr};
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -213,7 +217,7 @@ void free_problem(sfm_ba_handle* h) {
 }
 
 // ---- phase timing (HIP events on the solver stream; read at the per-iteration sync)
-void mark_begin(sfm_ba_handle* h, int ph) {
+void mark_begin(sfm_ba_handle* h, int ph, hipStream_t on = nullptr) {
   if (!h->profiling) return;
   if (h->ev_used + 2 > int(h->ev.size())) {
     const size_t old = h->ev.size();
@@ -221,12 +225,12 @@ void mark_begin(sfm_ba_handle* h, int ph) {
     for (size_t i = old; i < h->ev.size(); ++i) hipEventCreate(&h->ev[i]);
   }
   h->ev_marks.push_back({ph, h->ev_used});
-  hipEventRecord(h->ev[h->ev_used], h->stream);
+  hipEventRecord(h->ev[h->ev_used], on ? on : h->stream);
   h->ev_used += 2;
 }
-void mark_end(sfm_ba_handle* h) {
+void mark_end(sfm_ba_handle* h, hipStream_t on = nullptr) {
   if (!h->profiling) return;
-  hipEventRecord(h->ev[h->ev_marks.back().second + 1], h->stream);
+  hipEventRecord(h->ev[h->ev_marks.back().second + 1], on ? on : h->stream);
 }
 void collect_marks(sfm_ba_handle* h) {
   if (!h->profiling) return;
@@ -636,7 +640,36 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
   hipStream_t s = h->stream;
   int rc;
   const int nbP = std::max(1, blocks_for(d.P, 256)), nbC = std::max(1, blocks_for(d.C, 256));
-  if (h->mode == SFM_BA_STRUCT_AND_POSE) {
+  if (h->mode == SFM_BA_STRUCT_AND_POSE && d.overlap && d.C && !sharded(h) && !h->force_pack) {
+    // Schur / Cholesky overlap: the diagonal blocks and rhs first, then the
+    // factorisation on its own stream with half the CUs while k_schur_pts
+    // fills the off-diagonal blocks on the other half, in camera-major order
+    // (the factor's tile columns complete left to right); a helper reads an
+    // S tile once k_schur_pts has counted all its camera blocks in
+    mark_begin(h, kPhPtPrep);
+    launch_point_prep(d, radius, s);
+    mark_end(h);
+    if (!h->stream2) {
+      HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&h->ov_ev[0], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&h->ov_ev[1], hipEventDisableTiming));
+    }
+    mark_begin(h, kPhSchur);
+    HIPCHK(hipMemsetAsync(d.tile_cnt, 0, sizeof(int32_t) * size_t(d.nblk) * d.nblk, s));
+    launch_schur_diag(d, radius, h->rank == 0, s);
+    HIPCHK(hipEventRecord(h->ov_ev[0], s));
+    HIPCHK(hipStreamWaitEvent(h->stream2, h->ov_ev[0], 0));
+    mark_begin(h, kPhChol, h->stream2);
+    launch_cholesky(d, ++h->chol_epoch, h->stream2, false);
+    mark_end(h, h->stream2);
+    launch_schur_offdiag(d, d.tile_cnt, s);
+    HIPCHK(hipEventRecord(h->ov_ev[1], h->stream2));
+    HIPCHK(hipStreamWaitEvent(s, h->ov_ev[1], 0));
+    mark_end(h);  // (ended after the join: the Schur phase spans the overlapped factor)
+    mark_begin(h, kPhBack);
+    launch_backsolve(d, ++h->bs_epoch, s, true);
+    mark_end(h);
+  } else if (h->mode == SFM_BA_STRUCT_AND_POSE) {
     mark_begin(h, kPhPtPrep);
     launch_point_prep(d, radius, s);
     mark_end(h);
@@ -927,6 +960,12 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_trace) hipFree(h->lm_trace);
   if (h->stage) hipHostFree(h->stage);
   if (h->ar_tmp) hipFree(h->ar_tmp);
+  if (h->stream2) {
+    hipStreamSynchronize(h->stream2);
+    hipStreamDestroy(h->stream2);
+    hipEventDestroy(h->ov_ev[0]);
+    hipEventDestroy(h->ov_ev[1]);
+  }
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -1319,6 +1358,20 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);
   ALLOC(d.cticket, 3);  // task ticket, walker-role ticket, back-substitution role ticket
+  // Schur / Cholesky overlap (SFM_OVERLAP=1; unsharded, more than two tiles):
+  // per 64x64 tile of S the number of camera blocks (c1 <= c2, stored at
+  // rows 6 c2.., columns 6 c1..) whose 6x6 footprint touches it
+  d.overlap = env_flag("SFM_OVERLAP") && d.nblk > 2 && !sharded(h) ? 1 : 0;
+  if (d.overlap) {
+    ALLOC(d.tile_cnt, size_t(d.nblk) * d.nblk);
+    ALLOC(d.tile_exp, size_t(d.nblk) * d.nblk);
+    std::vector<int32_t> te(size_t(d.nblk) * d.nblk, 0);
+    for (int c1 = 0; c1 < C; ++c1)
+      for (int c2 = c1; c2 < C; ++c2)
+        for (int I = 6 * c2 / kNB; I <= (6 * c2 + 5) / kNB; ++I)
+          for (int J = 6 * c1 / kNB; J <= (6 * c1 + 5) / kNB; ++J) ++te[size_t(I) * d.nblk + J];
+    HCHK(hipMemcpy(d.tile_exp, te.data(), sizeof(int32_t) * te.size(), hipMemcpyHostToDevice));
+  }
   ALLOC(d.ysol, size_t(d.ld));
   ALLOC(d.fail, size_t(1));
   ALLOC(d.partials, size_t(kNumPartialSlots) * d.max_blocks);

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include "ba_device.h"
 #include "ba_common.h"
 
@@ -416,6 +417,40 @@ __device__ __forceinline__ int ready_bound(const int* F, int nb, int i, int j, i
   return b;
 }
 
+// Schur / Cholesky overlap (DevProblem::tile_cnt): tile (i, j) of S is
+// complete once k_schur_pts has counted every camera block of it in.  Its
+// blocks are stored write-through and drained before each count, so wave 0
+// polls the count (relaxed), then acquires as after a flag.
+__device__ __forceinline__ bool tile_ready_poll(const int* cnt, int exp, int* sh) {
+  if (wave0()) {
+    const bool r = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= exp;
+    if (r) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sh[1] = r ? 1 : 0;
+  }
+  __syncthreads();
+  const int r = __builtin_amdgcn_readfirstlane(sh[1]);
+  __syncthreads();
+  return r != 0;
+}
+__device__ __forceinline__ void tile_wait(const int* cnt, int exp, int* fail) {
+  if (wave0()) {
+    long spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < exp) {
+      if (++spins > kFlagSpins) {
+        atomicOr(fail, 4);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 // The helpers' TRSM X = T W^T for U stacked tiles (T_u in LDS, W = L_jj^-1
 // lower triangular in global memory, column-major: W(c, m) at m*NB + c).
 // Wave w takes row block w of every tile and forms X^T (column block C) =
@@ -466,7 +501,8 @@ __device__ __forceinline__ void put_rows(double* __restrict__ A, int ld, int i0,
 // column (lane & 15) walks the tile's rows (128-B column runs of A).
 __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld, int nb, const double* __restrict__ Winv,
                                   int* __restrict__ F, int* __restrict__ Pf, int epoch, int i, int j, double* T,
-                                  int* sh, int* __restrict__ fail) {
+                                  int* sh, int* __restrict__ fail, const int* __restrict__ tile_cnt,
+                                  const int* __restrict__ tile_exp) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -474,14 +510,19 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
   const bool diag = i == j;
   const bool skipq = diag && cb > rb;        // strictly upper quadrant: never read
   const int K = diag ? j - 2 : j - 1;        // updates k = 0..K by the helper
+  // S tile (i, j): read here, or (overlapped with the Schur pass and not yet
+  // complete) after the updates
+  const bool early = tile_cnt == nullptr || tile_ready_poll(tile_cnt + i * nb + j, tile_exp[i * nb + j], sh);
   double cv[2][2][4];
+  if (early) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int bb = 0; bb < 2; ++bb)
+      for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        cv[a][bb][reg] = skipq ? 0.0 : A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr];
+        for (int reg = 0; reg < 4; ++reg)
+          cv[a][bb][reg] = skipq ? 0.0 : A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr];
+  }
   f64x4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -508,6 +549,16 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb)
           acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
+  }
+  if (!early) {
+    tile_wait(tile_cnt + i * nb + j, tile_exp[i * nb + j], fail);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+          cv[a][bb][reg] = skipq ? 0.0 : A[size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr];
   }
   if (i <= j + 1) {
     // partial tile for the diagonal walker (its diagonal update / TRSM)
@@ -550,7 +601,8 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
 __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld, int nb,
                                                   const double* __restrict__ Winv, int* __restrict__ F, int epoch,
                                                   int i, int j, double* T0, double* T1, int* sh,
-                                                  int* __restrict__ fail) {
+                                                  int* __restrict__ fail, const int* __restrict__ tile_cnt,
+                                                  const int* __restrict__ tile_exp) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -588,6 +640,10 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
 #pragma unroll
           for (int bb = 0; bb < 2; ++bb)
             acc[u][a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[u][bb][ks], acc[u][a][bb], 0, 0, 0);
+  }
+  if (tile_cnt) {  // overlapped with the Schur pass: both S tiles complete
+    tile_wait(tile_cnt + i * nb + j, tile_exp[i * nb + j], fail);
+    tile_wait(tile_cnt + (i + 1) * nb + j, tile_exp[(i + 1) * nb + j], fail);
   }
   // T_u = A - acc -> LDS
 #pragma unroll
@@ -791,7 +847,8 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
                                                     int epoch, int nhelp, int* __restrict__ fail,
-                                                    const int* __restrict__ gate) {
+                                                    const int* __restrict__ gate, const int* __restrict__ tile_cnt,
+                                                    const int* __restrict__ tile_exp) {
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
@@ -846,11 +903,11 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     int j = 0, r = tk;
     while (r >= col_tasks(nb, j)) { r -= col_tasks(nb, j); ++j; }
     if (r < 3) {
-      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail);
+      fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, j + r, j, T, sh, fail, tile_cnt, tile_exp);
     } else {
       const int i = j + 3 + 2 * (r - 3);
-      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail);
-      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail);
+      if (i + 1 < nb) fused_helper_pair(A, ld, nb, Winv, F, epoch, i, j, T, Wl, sh, fail, tile_cnt, tile_exp);
+      else fused_helper_tile(A, ld, nb, Winv, F, Pf, epoch, i, j, T, sh, fail, tile_cnt, tile_exp);
     }
   }
 }
@@ -1061,9 +1118,20 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (roles by start order: a partly resident
   // grid still finishes)
-  const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+  // (SFM_CHOL_HELPERS: a smaller helper grid, for measurements)
+  static const int helpers_env = [] {
+    const char* e = std::getenv("SFM_CHOL_HELPERS");
+    return e ? std::atoi(e) : 0;
+  }();
+  // (overlapped with the Schur pass: half the CUs, the other half runs
+  // k_schur_pts, whose blocks the helpers await -- at n = 3000 127 helpers
+  // factor as fast as 255, 63 take 1.37x)
+  const int full = d.overlap ? d.n_cu / 2 - 1 : d.n_cu - 1;
+  const int cap = helpers_env > 0 ? std::min(helpers_env, full) : full;
+  const int nhelp = std::max(1, std::min(ntask, cap));
+  const int* tc = d.overlap ? d.tile_cnt : nullptr;
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
-                                         epoch, nhelp, d.fail, d.gate);
+                                         epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
 }
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
