@@ -217,8 +217,8 @@ void free_problem(sfm_ba_handle* h) {
 }
 
 // ---- phase timing (HIP events on the solver stream; read at the per-iteration sync)
-void mark_begin(sfm_ba_handle* h, int ph, hipStream_t on = nullptr) {
-  if (!h->profiling) return;
+int mark_begin(sfm_ba_handle* h, int ph, hipStream_t on = nullptr) {
+  if (!h->profiling) return -1;
   if (h->ev_used + 2 > int(h->ev.size())) {
     const size_t old = h->ev.size();
     h->ev.resize(old + 256);
@@ -227,10 +227,13 @@ void mark_begin(sfm_ba_handle* h, int ph, hipStream_t on = nullptr) {
   h->ev_marks.push_back({ph, h->ev_used});
   hipEventRecord(h->ev[h->ev_used], on ? on : h->stream);
   h->ev_used += 2;
+  return int(h->ev_marks.size()) - 1;
 }
-void mark_end(sfm_ba_handle* h, hipStream_t on = nullptr) {
+// ends mark `m` (default: the last one begun)
+void mark_end(sfm_ba_handle* h, hipStream_t on = nullptr, int m = -1) {
   if (!h->profiling) return;
-  hipEventRecord(h->ev[h->ev_marks.back().second + 1], on ? on : h->stream);
+  const auto& mk = m < 0 ? h->ev_marks.back() : h->ev_marks[size_t(m)];
+  hipEventRecord(h->ev[mk.second + 1], on ? on : h->stream);
 }
 void collect_marks(sfm_ba_handle* h) {
   if (!h->profiling) return;
@@ -654,7 +657,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
       HIPCHK(hipEventCreateWithFlags(&h->ov_ev[0], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&h->ov_ev[1], hipEventDisableTiming));
     }
-    mark_begin(h, kPhSchur);
+    const int m_schur = mark_begin(h, kPhSchur);
     HIPCHK(hipMemsetAsync(d.tile_cnt, 0, sizeof(int32_t) * size_t(d.nblk) * d.nblk, s));
     launch_schur_diag(d, radius, h->rank == 0, s);
     HIPCHK(hipEventRecord(h->ov_ev[0], s));
@@ -665,7 +668,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     launch_schur_offdiag(d, d.tile_cnt, s);
     HIPCHK(hipEventRecord(h->ov_ev[1], h->stream2));
     HIPCHK(hipStreamWaitEvent(s, h->ov_ev[1], 0));
-    mark_end(h);  // (ended after the join: the Schur phase spans the overlapped factor)
+    mark_end(h, nullptr, m_schur);  // (after the join: the Schur phase spans the overlapped factor)
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s, true);
     mark_end(h);
