@@ -1364,7 +1364,13 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // Schur / Cholesky overlap (SFM_OVERLAP=1; unsharded, more than two tiles):
   // per 64x64 tile of S the number of camera blocks (c1 <= c2, stored at
   // rows 6 c2.., columns 6 c1..) whose 6x6 footprint touches it
-  d.overlap = env_flag("SFM_OVERLAP") && d.nblk > 2 && !sharded(h) ? 1 : 0;
+  // (2: the factorisation's full helper grid, its workgroups placed as the
+  // Schur pass's retire)
+  {
+    const char* ov = std::getenv("SFM_OVERLAP");
+    const int v = ov ? std::atoi(ov) : 0;
+    d.overlap = v > 0 && d.nblk > 2 && !sharded(h) ? (v >= 2 ? 2 : 1) : 0;
+  }
   if (d.overlap) {
     ALLOC(d.tile_cnt, size_t(d.nblk) * d.nblk);
     ALLOC(d.tile_exp, size_t(d.nblk) * d.nblk);
