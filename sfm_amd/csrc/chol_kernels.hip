@@ -1111,7 +1111,13 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
 
 void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
-  if (d.nblk <= 2) {  // factor + back substitution in one workgroup
+  // (SFM_CHOL_NO_SMALL=1: the persistent pair at every size, for the
+  // bitwise comparison in tests/test_gpu_parity.py)
+  static const bool no_small = [] {
+    const char* e = std::getenv("SFM_CHOL_NO_SMALL");
+    return e && e[0] == '1';
+  }();
+  if (d.nblk <= 2 && !no_small) {  // factor + back substitution in one workgroup
     k_chol_small<<<1, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.ysol, d.fail, d.gate);
     return;
   }
@@ -1136,7 +1142,11 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
   const int nb_real = (d.n + NB - 1) / NB;
-  if (nb_real <= 0 || d.nblk <= 2) return;  // (nblk <= 2: k_chol_small solved too)
+  static const bool no_small = [] {
+    const char* e = std::getenv("SFM_CHOL_NO_SMALL");
+    return e && e[0] == '1';
+  }();
+  if (nb_real <= 0 || (d.nblk <= 2 && !no_small)) return;  // (nblk <= 2: k_chol_small solved too)
   // the sentinel in every entry of y the launch produces (ld >= 64 nb_real;
   // the solve's k_pad_init writes it, saving a launch)
   if (!sentinel_set)

@@ -123,3 +123,33 @@ def test_dense_cholesky_reports_indefinite(n, path, monkeypatch):
     A[n // 2, n // 2] = -1.0
     _, _, fl = dense_spd_solve(A, np.ones(n))
     assert fl == 1
+
+
+def test_small_system_factor_bitwise_equals_persistent():
+    """k_chol_small (nblk <= 2: factor + back substitution in one workgroup)
+    repeats the persistent walker's and k_backsolve's arithmetic in the same
+    order: y bitwise equal to the persistent pair's (SFM_CHOL_NO_SMALL=1, a
+    child process: the knob is read once per process)."""
+    import json, os, subprocess, sys
+    from sfm_amd.ba import dense_spd_solve
+    sizes = [6, 63, 64, 100, 127]
+    code = ("import json, numpy as np\n"
+            "from sfm_amd.ba import dense_spd_solve\n"
+            "out = {}\n"
+            f"for n in {sizes}:\n"
+            "    rng = np.random.default_rng(n)\n"
+            "    M = rng.standard_normal((n, n)); A = M @ M.T + n * np.eye(n); b = rng.standard_normal(n)\n"
+            "    out[n] = dense_spd_solve(A, b)[0].tobytes().hex()\n"
+            "print(json.dumps(out))\n")
+    env = dict(os.environ, SFM_CHOL_NO_SMALL="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref = json.loads(r.stdout.strip().splitlines()[-1])
+    for n in sizes:
+        rng = np.random.default_rng(n)
+        M = rng.standard_normal((n, n))
+        A = M @ M.T + n * np.eye(n)
+        b = rng.standard_normal(n)
+        y = dense_spd_solve(A, b)[0]
+        assert y.tobytes().hex() == ref[str(n)], n

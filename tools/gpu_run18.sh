@@ -7,6 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r04h
 rm -rf $O && mkdir -p $O
 cd $R
+timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -x -q -k "small_system or dense_cholesky" --timeout 150 --timeout-method thread > $O/small_tests.log 2>&1 || { tail -30 $O/small_tests.log; exit 1; }
 SFM_OVERLAP=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_scale.py -x -q -k "baseline_sizes or reproducible or c4_single" --timeout 200 --timeout-method thread > $O/ov_tests.log 2>&1 || { tail -30 $O/ov_tests.log; exit 1; }
 for rep in 1 2; do
   for ov in 0 2; do
