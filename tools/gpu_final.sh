@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-end check: the whole GPU suite and smoke() from this tree.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/final
+rm -rf $O && mkdir -p $O
+cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
