@@ -111,11 +111,35 @@ __device__ __forceinline__ double tree16(double v) {
   return v;
 }
 
+// One Jacobi sweep in OpenCV's order (0,1), (0,2), ..., (10,11), scheduled
+// by row dependencies into 23 passes of up to 4 rotations on disjoint rows
+// (rotation (i, j) waits only for the rotations before it on rows i and j;
+// the critical path is 21 of them): the wave's four 16-lane rows each hold
+// the whole 12-row state and take one rotation of a pass, then exchange the
+// rotated rows.  Every rotation is the same arithmetic on the same values as
+// in the sequential sweep, so the result is bitwise OpenCV's order.  (A
+// branch-free sequential sweep, for the scheduler to overlap, measured
+// slower: 0.375-0.388 vs 0.313 ms per PnP call.)  Unused slots repeat slot 0.
+constexpr int kSvdPasses = 23;
+constexpr int kSvdN[kSvdPasses] = {1, 1, 2, 2, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 4, 3, 3, 3, 3, 2, 2, 1, 1};
+constexpr int kSvdI[kSvdPasses][4] = {
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 1, 0, 0}, {0, 1, 0, 0}, {0, 1, 2, 0}, {0, 1, 2, 0}, {0, 1, 2, 3}, {0, 1, 2, 3},
+    {0, 1, 2, 3}, {4, 0, 1, 2}, {3, 4, 0, 1}, {2, 3, 4, 5}, {1, 2, 3, 4}, {5, 2, 3, 4}, {5, 6, 3, 4}, {5, 6, 4, 5},
+    {5, 6, 7, 5}, {5, 6, 7, 5}, {6, 7, 8, 6}, {7, 8, 7, 7}, {8, 9, 8, 8}, {9, 9, 9, 9}, {10, 10, 10, 10}};
+constexpr int kSvdJ[kSvdPasses][4] = {
+    {1, 1, 1, 1}, {2, 2, 2, 2}, {3, 2, 3, 3}, {4, 3, 4, 4}, {5, 4, 3, 5}, {6, 5, 4, 6}, {7, 6, 5, 4}, {8, 7, 6, 5},
+    {9, 8, 7, 6}, {5, 10, 9, 8}, {7, 6, 11, 10}, {9, 8, 7, 6}, {11, 10, 9, 8}, {7, 11, 10, 9}, {8, 7, 11, 10},
+    {9, 8, 11, 9}, {10, 9, 8, 10}, {11, 10, 9, 11}, {11, 10, 9, 11}, {11, 10, 11, 11}, {11, 10, 11, 11},
+    {11, 11, 11, 11}, {11, 11, 11, 11}};
+__device__ __forceinline__ double sel4(int g, double a0, double a1, double a2, double a3) {
+  return g == 0 ? a0 : g == 1 ? a1 : g == 2 ? a2 : a3;
+}
+
 // u[i] = At[i][lane & 15] on entry (M^T M is symmetric); on return the
 // four left singular vectors of the smallest singular values are in
 // ut[q] = OpenCV's ut row 11 - q, every lane holding all 12 entries.
 __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]) {
-  const int k = threadIdx.x & 15;
+  const int k = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
   double W[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) W[i] = tree16(u[i] * u[i]);
@@ -123,30 +147,48 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
   for (int iter = 0; iter < 30; ++iter) {
     bool changed = false;
 #pragma unroll
-    for (int i = 0; i < 11; ++i)
-#pragma unroll
-      for (int j = i + 1; j < 12; ++j) {
-        const double a = W[i], b = W[j];
-        double p = tree16(u[i] * u[j]);
-        if (fabs(p) <= eps * sqrt(a * b)) continue;
-        p *= 2;
-        const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-        double c, sn;
-        if (beta < 0) {
-          const double delta = (gamma - beta) * 0.5;
-          sn = sqrt(delta / gamma);
-          c = p / (gamma * sn * 2);
-        } else {
-          c = sqrt((gamma + beta) / (gamma * 2));
-          sn = p / (gamma * c * 2);
-        }
-        const double t0 = c * u[i] + sn * u[j], t1 = -sn * u[i] + c * u[j];
-        u[i] = t0;
-        u[j] = t1;
-        W[i] = tree16(t0 * t0);
-        W[j] = tree16(t1 * t1);
-        changed = true;
+    for (int ps = 0; ps < kSvdPasses; ++ps) {
+      const int n = kSvdN[ps];
+      const int* I = kSvdI[ps];
+      const int* J = kSvdJ[ps];
+      // row g's rotation (I[g], J[g]); rows g >= n idle
+      const double ui = sel4(g, u[I[0]], u[I[1]], u[I[2]], u[I[3]]);
+      const double uj = sel4(g, u[J[0]], u[J[1]], u[J[2]], u[J[3]]);
+      const double a = sel4(g, W[I[0]], W[I[1]], W[I[2]], W[I[3]]);
+      const double b = sel4(g, W[J[0]], W[J[1]], W[J[2]], W[J[3]]);
+      double p = tree16(ui * uj);
+      const bool act = g < n && !(fabs(p) <= eps * sqrt(a * b));
+      if (__builtin_amdgcn_ballot_w64(act) == 0) continue;  // every rotation of the pass skipped
+      changed = true;
+      p *= 2;
+      const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+      double c, sn;
+      if (beta < 0) {
+        const double delta = (gamma - beta) * 0.5;
+        sn = sqrt(delta / gamma);
+        c = p / (gamma * sn * 2);
+      } else {
+        c = sqrt((gamma + beta) / (gamma * 2));
+        sn = p / (gamma * c * 2);
       }
+      double t0 = c * ui + sn * uj, t1 = -sn * ui + c * uj;
+      double w0 = tree16(t0 * t0), w1 = tree16(t1 * t1);
+      t0 = act ? t0 : ui;
+      t1 = act ? t1 : uj;
+      w0 = act ? w0 : a;
+      w1 = act ? w1 : b;
+      // every row takes every rotated pair of the pass (lane k of row q holds
+      // column k of rows I[q], J[q])
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q >= n) break;
+        const int src = 16 * q + k;
+        u[I[q]] = __shfl(t0, src);
+        u[J[q]] = __shfl(t1, src);
+        W[I[q]] = __shfl(w0, src);
+        W[J[q]] = __shfl(w1, src);
+      }
+    }
     if (!changed) break;
   }
   int ord[12];
