@@ -819,6 +819,7 @@ struct PnPCtx {
   double* img = nullptr;
   int* inl = nullptr;
   int* sub = nullptr;
+  int sub_n = -1, sub_iters = -1;  // the (n, iterations) whose subsets `sub` holds
   double* model = nullptr;
   int* cnt = nullptr;
   int* res = nullptr;
@@ -888,7 +889,13 @@ extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, cons
   if (hipMemcpyAsync(c->obj, obj, sizeof(double) * 3 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(c->img, img, sizeof(double) * 2 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess)
     return pfail(SFM_EIO, "upload failed");
-  k_pnp_subsets<<<1, 64, 0, s>>>(n, iters, c->sub);
+  // the subsets depend on (n, iterations) alone (cv::RNG(-1) restarted per
+  // call): drawn once per pair, then reused
+  if (c->sub_n != n || c->sub_iters != iters) {
+    k_pnp_subsets<<<1, 64, 0, s>>>(n, iters, c->sub);
+    c->sub_n = n;
+    c->sub_iters = iters;
+  }
   k_pnp_epnp<<<iters, 192, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
   k_pnp_count<<<iters, 256, 0, s>>>(n, c->obj, c->img, c->model, k, thr, c->cnt);
   k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->res, c->inl);
