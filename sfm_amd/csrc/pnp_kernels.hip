@@ -138,8 +138,17 @@ __device__ __forceinline__ double sel4(int g, double a0, double a1, double a2, d
 // u[i] = At[i][lane & 15] on entry (M^T M is symmetric); on return the
 // four left singular vectors of the smallest singular values are in
 // ut[q] = OpenCV's ut row 11 - q, every lane holding all 12 entries.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// lds: this wave's kSvdLds doubles (the pass exchange, then ut)
+constexpr int kSvdLds = 2 * 64 + 2 * 4;
 __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]) {
   const int k = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
+  double2* xt = reinterpret_cast<double2*>(lds);   // [4 rows][16 lanes] (t0, t1)
+  double2* xw = reinterpret_cast<double2*>(lds + 128);  // [4 rows] (W_i, W_j)
   double W[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) W[i] = tree16(u[i] * u[i]);
@@ -178,16 +187,22 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
       w0 = act ? w0 : a;
       w1 = act ? w1 : b;
       // every row takes every rotated pair of the pass (lane k of row q holds
-      // column k of rows I[q], J[q])
+      // column k of rows I[q], J[q]) through the wave's LDS slice: one
+      // 16-B write per lane, one 16-B read per rotation (the W pair a
+      // broadcast read), instead of 8 ds_bpermute per rotation
+      xt[16 * g + k] = make_double2(t0, t1);
+      if (k == 0) xw[g] = make_double2(w0, w1);
+      wave_sync();
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (q >= n) break;
-        const int src = 16 * q + k;
-        u[I[q]] = __shfl(t0, src);
-        u[J[q]] = __shfl(t1, src);
-        W[I[q]] = __shfl(w0, src);
-        W[J[q]] = __shfl(w1, src);
+        const double2 tq = xt[16 * q + k], wq = xw[q];
+        u[I[q]] = tq.x;
+        u[J[q]] = tq.y;
+        W[I[q]] = wq.x;
+        W[J[q]] = wq.y;
       }
+      wave_sync();  // (the reads done before the next pass writes)
     }
     if (!changed) break;
   }
@@ -241,6 +256,7 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
     const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
     row[i] *= sc;
   }
+  wave_sync();  // (the last pass's exchange reads done)
   if (k < 12 && (threadIdx.x & 63) < 16)
 #pragma unroll
     for (int q = 0; q < 4; ++q) lds[q * 12 + k] = row[11 - q];
@@ -690,7 +706,7 @@ __global__ void k_pnp_subsets(int n, int iters, int* __restrict__ sub) {
 // does (err[1] < err[0], then err[2] < err[N]).
 __global__ __launch_bounds__(192) void k_pnp_epnp(const double* __restrict__ obj, const double* __restrict__ img,
                                                   const int* __restrict__ sub, PnPCam k, double* __restrict__ model) {
-  __shared__ double lds[3][48];
+  __shared__ __attribute__((aligned(16))) double lds[3][kSvdLds];
   __shared__ double res[3][13];
   const int it = blockIdx.x;
   const int w = threadIdx.x >> 6;
