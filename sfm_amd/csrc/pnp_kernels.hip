@@ -811,6 +811,9 @@ __global__ __launch_bounds__(64) void k_pnp_select(int n, int iters, double conf
   }
   if (lane == 0) { res[0] = best >= 0 ? 1 : 0; res[1] = best; res[2] = best >= 0 ? max_good : 0; }
   if (best < 0) return;
+  // the winner's model next to the counts (res + 4: 16-B aligned), so one
+  // download returns counts, model and inliers
+  if (lane < 6) reinterpret_cast<double*>(res + 4)[lane] = model[6 * best + lane];
   if (n == kModel) {  // run() with count == modelPoints: the mask is all ones
     if (lane < kModel) inl[lane] = lane;
     return;
@@ -833,15 +836,20 @@ struct PnPCtx {
   size_t cap = 0;
   double* obj = nullptr;
   double* img = nullptr;
+  // one device block returned by ONE download: counts (4 ints), the
+  // winner's model (6 doubles), the inlier list (cap ints)
+  int* out = nullptr;
   int* inl = nullptr;
+  uint8_t* pin = nullptr;  // pinned staging: the points up, the block down
+  size_t pin_cap = 0;
   int* sub = nullptr;
   int sub_n = -1, sub_iters = -1;  // the (n, iterations) whose subsets `sub` holds
   double* model = nullptr;
   int* cnt = nullptr;
-  int* res = nullptr;
   ~PnPCtx() {
     if (stream) hipStreamSynchronize(stream);
-    hipFree(obj); hipFree(img); hipFree(inl); hipFree(sub); hipFree(model); hipFree(cnt); hipFree(res);
+    hipFree(obj); hipFree(img); hipFree(out); hipFree(sub); hipFree(model); hipFree(cnt);
+    if (pin) hipHostFree(pin);
     if (stream) hipStreamDestroy(stream);
   }
 };
@@ -886,24 +894,39 @@ extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, cons
     }
     if (hipMalloc(&c->sub, sizeof(int) * kModel * kMaxIters) != hipSuccess ||
         hipMalloc(&c->model, sizeof(double) * 6 * kMaxIters) != hipSuccess ||
-        hipMalloc(&c->cnt, sizeof(int) * kMaxIters) != hipSuccess || hipMalloc(&c->res, sizeof(int) * 4) != hipSuccess)
+        hipMalloc(&c->cnt, sizeof(int) * kMaxIters) != hipSuccess)
       return pfail(SFM_ENOMEM, "hipMalloc failed");
   }
+  // result block: counts (4 ints = 16 B) | winner's model (6 doubles) | inliers
+  constexpr size_t kOutHead = 16 + 6 * sizeof(double);
   if (size_t(n) > c->cap) {
-    hipFree(c->obj); hipFree(c->img); hipFree(c->inl);
-    c->obj = nullptr; c->img = nullptr; c->inl = nullptr; c->cap = 0;
+    hipFree(c->obj); hipFree(c->img); hipFree(c->out);
+    c->obj = nullptr; c->img = nullptr; c->out = nullptr; c->inl = nullptr; c->cap = 0;
+    if (c->pin) hipHostFree(c->pin);
+    c->pin = nullptr;
     const size_t cap = std::max<size_t>(size_t(n), 1024);
     if (hipMalloc(&c->obj, sizeof(double) * 3 * cap) != hipSuccess ||
-        hipMalloc(&c->img, sizeof(double) * 2 * cap) != hipSuccess || hipMalloc(&c->inl, sizeof(int) * cap) != hipSuccess)
+        hipMalloc(&c->img, sizeof(double) * 2 * cap) != hipSuccess ||
+        hipMalloc(&c->out, kOutHead + sizeof(int) * cap) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->pin), sizeof(double) * 5 * cap + kOutHead + sizeof(int) * cap) !=
+            hipSuccess)
       return pfail(SFM_ENOMEM, "hipMalloc failed");
+    c->inl = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(c->out) + kOutHead);
     c->cap = cap;
   }
   const PnPCam k{K9[0], K9[4], K9[2], K9[5]};
   const int iters = iterations > 0 ? iterations : 1;
   const float thr = float(reproj_err * reproj_err);
   hipStream_t s = c->stream;
-  if (hipMemcpyAsync(c->obj, obj, sizeof(double) * 3 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(c->img, img, sizeof(double) * 2 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess)
+  // the points through the pinned stage (the previous call has drained the
+  // stream: it synchronised before returning)
+  double* pin_obj = reinterpret_cast<double*>(c->pin);
+  double* pin_img = pin_obj + 3 * size_t(n);
+  uint8_t* pin_out = c->pin + sizeof(double) * 5 * c->cap;
+  std::memcpy(pin_obj, obj, sizeof(double) * 3 * size_t(n));
+  std::memcpy(pin_img, img, sizeof(double) * 2 * size_t(n));
+  if (hipMemcpyAsync(c->obj, pin_obj, sizeof(double) * 3 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(c->img, pin_img, sizeof(double) * 2 * size_t(n), hipMemcpyHostToDevice, s) != hipSuccess)
     return pfail(SFM_EIO, "upload failed");
   // the subsets depend on (n, iterations) alone (cv::RNG(-1) restarted per
   // call): drawn once per pair, then reused
@@ -914,15 +937,18 @@ extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, cons
   }
   k_pnp_epnp<<<iters, 192, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
   k_pnp_count<<<iters, 256, 0, s>>>(n, c->obj, c->img, c->model, k, thr, c->cnt);
-  k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->res, c->inl);
-  int res[4] = {0, -1, 0, 0};
+  k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->out, c->inl);
+  // ONE download: counts, model and (up to n) inliers
+  const size_t down = kOutHead + (inliers ? sizeof(int) * size_t(n) : 0);
+  if (hipMemcpyAsync(pin_out, c->out, down, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return pfail(SFM_EIO, "PnP kernels failed");
+  int res[4];
   double mdl[6];
-  hipMemcpyAsync(res, c->res, sizeof(int) * 4, hipMemcpyDeviceToHost, s);
-  if (hipStreamSynchronize(s) != hipSuccess) return pfail(SFM_EIO, "PnP kernels failed");
+  std::memcpy(res, pin_out, sizeof(res));
   if (!res[0]) return 0;
-  hipMemcpyAsync(mdl, c->model + 6 * res[1], sizeof(double) * 6, hipMemcpyDeviceToHost, s);
-  if (inliers && res[2] > 0) hipMemcpyAsync(inliers, c->inl, sizeof(int) * res[2], hipMemcpyDeviceToHost, s);
-  if (hipStreamSynchronize(s) != hipSuccess) return pfail(SFM_EIO, "PnP download failed");
+  std::memcpy(mdl, pin_out + 16, sizeof(mdl));
+  if (inliers && res[2] > 0) std::memcpy(inliers, pin_out + kOutHead, sizeof(int) * size_t(res[2]));
   for (int i = 0; i < 3; ++i) { rvec[i] = mdl[i]; tvec[i] = mdl[3 + i]; }
   *n_inliers = res[2];
   *found = 1;
