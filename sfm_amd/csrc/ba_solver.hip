@@ -1036,6 +1036,8 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     free_problem(h);
     return code;
   };
+// observations up to which set_problem checks and counts them on the host
+constexpr int64_t kHostCheckMaxObs = 65536;
 #define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) return bail(rc)
 #define TMP(ptr, cnt) if ((rc = dalloc_tmp(h, &(ptr), (cnt)))) return bail(rc)
 #define HCHK(expr)                                                                                \
@@ -1050,12 +1052,23 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   // ---- the caller's observation arrays go up as they are (packed into the
   // pinned stage: one DMA); the O(N) layout work runs on the device
   // (ba_setup.hip) ----
+  // keyframe-sized problems: the checks and the camera / point counts on
+  // the host, their point counts riding in the same upload -- no validation
+  // launch and no round trip before the layout (C1: ~60 us of set_problem)
+  const bool host_check = N <= kHostCheckMaxObs;
   StageLayout up;
   const size_t o_uv = up.add(sizeof(double) * 2 * size_t(N)), o_cam = up.add(sizeof(int32_t) * size_t(N)),
-               o_pt = up.add(sizeof(int32_t) * size_t(N));
+               o_pt = up.add(sizeof(int32_t) * size_t(N)),
+               o_pc = host_check ? up.add(sizeof(int32_t) * (size_t(P) + 1)) : 0;
   const size_t in_bytes = up.bytes;
   const bool stage_in = in_bytes <= kStageMaxBytes;
-  if ((rc = stage_reserve(h, std::max(stage_in ? in_bytes : 0, sizeof(int32_t) * (size_t(C) + 4))))) return bail(rc);
+  // (host checks: the camera-run blob below is staged AFTER the input blob,
+  // which is still in flight -- no synchronisation in between -- so the
+  // stage holds both from here: 2 C + chunks + ... ints, bounded)
+  const size_t il_base = host_check && stage_in ? (in_bytes + 255) / 256 * 256 : 0;
+  const size_t il_bound = host_check && stage_in ? 64 * (size_t(C) + 1) + 2 * size_t(N) + 1024 : 0;
+  if ((rc = stage_reserve(h, std::max(stage_in ? il_base + il_bound : 0, sizeof(int32_t) * (size_t(C) + 4)))))
+    return bail(rc);
   stg = h->stage;
   uint8_t* in_blob = nullptr;
   TMP(in_blob, in_bytes);
@@ -1063,9 +1076,35 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   in_cam = reinterpret_cast<int32_t*>(in_blob + o_cam);
   in_pt = reinterpret_cast<int32_t*>(in_blob + o_pt);
   int32_t* err = nullptr;
-  TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
-  int32_t* cnt_c = err + 4;
-  TMP(cnt_p, size_t(P) + 1);
+  int32_t* cnt_c = nullptr;
+  if (host_check && stage_in) {
+    // k_validate's checks and counts, in observation order
+    int32_t first[3] = {INT32_MAX, INT32_MAX, INT32_MAX};
+    std::fill(cam_cnt.begin(), cam_cnt.end(), 0);
+    int32_t* pc = reinterpret_cast<int32_t*>(stg + o_pc);
+    std::fill(pc, pc + size_t(P) + 1, 0);
+    for (int64_t i = 0; i < N; ++i) {
+      const int32_t c = cam_idx[i], p = pt_idx[i];
+      const bool cok = c >= 0 && c < C, pok = p >= 0 && p < P;
+      const bool uok = std::isfinite(obs_uv[2 * i]) && std::isfinite(obs_uv[2 * i + 1]);
+      if (!cok && first[0] == INT32_MAX) first[0] = int32_t(i);
+      if (!pok && first[1] == INT32_MAX) first[1] = int32_t(i);
+      if (!uok && first[2] == INT32_MAX) first[2] = int32_t(i);
+      if (cok && pok) {
+        ++cam_cnt[4 + size_t(c)];
+        ++pc[p];
+      }
+    }
+    cam_cnt[0] = first[0];
+    cam_cnt[1] = first[1];
+    cam_cnt[2] = first[2];
+    cam_cnt[3] = INT32_MAX;
+    cnt_p = reinterpret_cast<int32_t*>(in_blob + o_pc);
+  } else {
+    TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
+    cnt_c = err + 4;
+    TMP(cnt_p, size_t(P) + 1);
+  }
   if (N && stage_in) {
     std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
     std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
@@ -1076,20 +1115,22 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(in_pt, pt_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
   }
-  {
-    Fill32Set fs;
-    fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
-    fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
-    fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
-    launch_fill32(fs, s);
+  if (!(host_check && stage_in)) {
+    {
+      Fill32Set fs;
+      fs.add(err, 4 * sizeof(int32_t), uint32_t(INT32_MAX));
+      fs.add(cnt_c, sizeof(int32_t) * (size_t(C) + 1), 0);
+      fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
+      launch_fill32(fs, s);
+    }
+    launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+    // one round trip: the first bad observation and the per-camera counts
+    // (the host lays out the C camera runs and the wavefront chunk table);
+    // the readback lands in the stage after the upload has read it (stream order)
+    HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
+    HCHK(hipStreamSynchronize(s));
+    std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
   }
-  launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
-  // one round trip: the first bad observation and the per-camera counts
-  // (the host lays out the C camera runs and the wavefront chunk table);
-  // the readback lands in the stage after the upload has read it (stream order)
-  HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
-  HCHK(hipStreamSynchronize(s));
-  std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
   timer.mark("upload + validate");
   {
     const int32_t e0 = cam_cnt[0], e1 = cam_cnt[1], e2 = cam_cnt[2];
@@ -1187,15 +1228,17 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
     StageLayout il;
     const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
                  o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
-    if ((rc = stage_reserve(h, il.bytes))) return bail(rc);
+    if (il_base && il.bytes > il_bound) return bail(fail(SFM_EIO, "internal: camera-run blob above its bound"));
+    if ((rc = stage_reserve(h, il_base + il.bytes))) return bail(rc);  // (never regrows with il_base > 0)
     stg = h->stage;
     uint8_t* ib = nullptr;
     ALLOC(ib, il.bytes);
-    std::memcpy(stg + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
-    std::memcpy(stg + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
-    std::memcpy(stg + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
-    if (nch) std::memcpy(stg + o_ch, chunks.data(), sizeof(int4) * chunks.size());
-    HCHK(hipMemcpyAsync(ib, stg, il.bytes, hipMemcpyHostToDevice, s));
+    uint8_t* sb = stg + il_base;
+    std::memcpy(sb + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
+    std::memcpy(sb + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
+    std::memcpy(sb + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
+    if (nch) std::memcpy(sb + o_ch, chunks.data(), sizeof(int4) * chunks.size());
+    HCHK(hipMemcpyAsync(ib, sb, il.bytes, hipMemcpyHostToDevice, s));
     d.cam_rng = reinterpret_cast<int32_t*>(ib + o_rng);
     d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
     d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
