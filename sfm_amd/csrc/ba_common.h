@@ -2,6 +2,8 @@
 // (ba_kernels.hip, chol_kernels.hip, ba_setup.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cmath>
 #include <cstdint>
 #include "ba_device.h"
 
@@ -38,6 +40,94 @@ __device__ __forceinline__ void reduce_batch_job(const double* __restrict__ part
     scal[j.dst] = r;
     if (fail) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
   }
+}
+// Fixed-order block reduction; result valid in thread 0.  `sh` >= 4 doubles.
+__device__ __forceinline__ double block_reduce(double v, double* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    r = sh[0];
+    for (int i = 1; i < nw; ++i) r = is_max ? fmax(r, sh[i]) : r + sh[i];
+  }
+  return r;
+}
+
+// Rotation matrix R(w) with the branch of ceres::AngleAxisRotatePoint:
+// theta^2 > DBL_EPSILON -> Rodrigues; otherwise the first-order map I + [w]x.
+// Optionally dR/dw_k (k-major, 3 x row-major 3x3), differentiated through
+// the same expressions the Jet evaluation of the reference functor uses.
+__device__ void rotation(const double w[3], double R[9], double* dR) {
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (th2 > DBL_EPSILON) {
+    const double th = sqrt(th2);
+    double s, c;
+    sincos(th, &s, &c);
+    const double ith = 1.0 / th;
+    const double u[3] = {w[0] * ith, w[1] * ith, w[2] * ith};
+    const double omc = 1.0 - c;
+    R[0] = c + omc * u[0] * u[0];        R[1] = -s * u[2] + omc * u[0] * u[1]; R[2] = s * u[1] + omc * u[0] * u[2];
+    R[3] = s * u[2] + omc * u[1] * u[0]; R[4] = c + omc * u[1] * u[1];        R[5] = -s * u[0] + omc * u[1] * u[2];
+    R[6] = -s * u[1] + omc * u[2] * u[0]; R[7] = s * u[0] + omc * u[2] * u[1]; R[8] = c + omc * u[2] * u[2];
+    if (dR) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double dc = -s * u[k], ds = c * u[k], domc = s * u[k];
+        double du[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) du[i] = ((i == k ? 1.0 : 0.0) - u[i] * u[k]) * ith;
+        double* D = dR + 9 * k;
+        // d/dw_k of: c I + s [u]x + omc u u^T
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            D[3 * i + j] = (i == j ? dc : 0.0) + domc * u[i] * u[j] + omc * (du[i] * u[j] + u[i] * du[j]);
+        // skew parts: [a]x = [[0,-a2,a1],[a2,0,-a0],[-a1,a0,0]] with a = ds*u + s*du
+        const double a0 = ds * u[0] + s * du[0], a1 = ds * u[1] + s * du[1], a2 = ds * u[2] + s * du[2];
+        D[1] -= a2; D[2] += a1; D[3] += a2; D[5] -= a0; D[6] -= a1; D[7] += a0;
+      }
+    }
+  } else {
+    R[0] = 1.0;   R[1] = -w[2]; R[2] = w[1];
+    R[3] = w[2];  R[4] = 1.0;   R[5] = -w[0];
+    R[6] = -w[1]; R[7] = w[0];  R[8] = 1.0;
+    if (dR) {
+      for (int i = 0; i < 27; ++i) dR[i] = 0.0;
+      // d([w]x)/dw_k = [e_k]x
+      dR[0 * 9 + 5] = -1.0; dR[0 * 9 + 7] = 1.0;
+      dR[1 * 9 + 2] = 1.0;  dR[1 * 9 + 6] = -1.0;
+      dR[2 * 9 + 1] = -1.0; dR[2 * 9 + 3] = 1.0;
+    }
+  }
+}
+
+// One camera of the LM step (k_cam_update, and k_chol_small's tail for
+// small systems): x_new = x - scale * y, the step's squared length and a
+// non-finite flag accumulated into st / bad, the new pose and its rotation
+// matrix (camRn: R 9 | t 3).
+__device__ __forceinline__ void cam_update_one(int c, const double* __restrict__ cam, const double* __restrict__ ysol,
+                                               const double* __restrict__ scale_c, double* __restrict__ cam_new,
+                                               double* __restrict__ camRn, double& st, double& bad) {
+  double xn[6];
+  for (int k = 0; k < 6; ++k) {
+    const double y = ysol[6 * c + k];
+    if (!isfinite(y)) bad = 1.0;
+    const double dx = scale_c[6 * c + k] * (-y);
+    xn[k] = cam[6 * c + k] + dx;
+    const double d = cam[6 * c + k] - xn[k];
+    st += d * d;
+    cam_new[6 * c + k] = xn[k];
+  }
+  double R[9];
+  rotation(xn, R, nullptr);
+  double* o = camRn + 12 * size_t(c);
+  for (int i = 0; i < 9; ++i) o[i] = R[i];
+  o[9] = xn[3]; o[10] = xn[4]; o[11] = xn[5];
 }
 // Wave sums of 32 values at once by recursive halving (reduce-scatter): at
 // each of the 5 exchange distances 32..2 a lane keeps half of its values and

@@ -643,6 +643,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
   hipStream_t s = h->stream;
   int rc;
   const int nbP = std::max(1, blocks_for(d.P, 256)), nbC = std::max(1, blocks_for(d.C, 256));
+  bool cam_done = false;  // the camera step taken by the small-system factor
   if (h->mode == SFM_BA_STRUCT_AND_POSE && d.overlap && d.C && !sharded(h) && !h->force_pack) {
     // Schur / Cholesky overlap: the diagonal blocks and rhs first, then the
     // factorisation on its own stream with half the CUs while k_schur_pts
@@ -689,7 +690,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     // the cleared failure flag; without cameras the separate launch does)
     if (!d.C) launch_pad_init(d, s);
     mark_begin(h, kPhChol);
-    launch_cholesky(d, ++h->chol_epoch, s, false);
+    cam_done = launch_cholesky(d, ++h->chol_epoch, s, false, h->rank == 0 ? 1 : 0);
     mark_end(h);
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s, true);
@@ -711,7 +712,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     }
     hipMemsetAsync(d.ysol, 0, sizeof(double) * 6 * size_t(d.C), s);
   }
-  launch_cam_update(d, h->rank == 0 && h->mode != SFM_BA_STRUCT_ONLY, s);
+  if (!cam_done) launch_cam_update(d, h->rank == 0 && h->mode != SFM_BA_STRUCT_ONLY, s);
   mark_begin(h, kPhBacksub);
   launch_point_backsub(d, s, h->mode != SFM_BA_STRUCT_ONLY, h->mode != SFM_BA_POSE_ONLY);
   mark_end(h);

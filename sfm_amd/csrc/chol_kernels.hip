@@ -1025,9 +1025,15 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
 // The tile operations and their order are k_chol_fused's walker (the
 // helpers' partial tiles are the input tiles: no earlier column exists) and
 // k_backsolve's arithmetic: bitwise the same L, W and y.
+// With cam != nullptr it also takes k_cam_update's step (C <= 256: that
+// launch's single workgroup, the same arithmetic and reductions).
 __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A, int ld, int n, int nb,
                                                     double* __restrict__ y, int* __restrict__ fail,
-                                                    const int* __restrict__ gate) {
+                                                    const int* __restrict__ gate, int C,
+                                                    const double* __restrict__ cam,
+                                                    const double* __restrict__ scale_c, double* __restrict__ cam_new,
+                                                    double* __restrict__ camRn, double* __restrict__ part_step,
+                                                    double* __restrict__ part_bad) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double T[NB * TS];    // diagonal tile being factored, then L_jj
   __shared__ double Wl[NB * TS];   // W_j of the current step
@@ -1105,11 +1111,19 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
     }
     __syncthreads();
   }
+  if (cam) {  // the camera step (y written above, by this workgroup)
+    double st = 0.0, bd = 0.0;
+    if (t < C) cam_update_one(t, cam, y, scale_c, cam_new, camRn, st, bd);
+    const double rs = block_reduce(st, v, false);
+    if (t == 0 && part_step) part_step[0] = rs;
+    const double rb = block_reduce(bd, v, true);
+    if (t == 0) part_bad[0] = rb;
+  }
 }
 
 }  // namespace
 
-void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail) {
+bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int cam_step) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   // (SFM_CHOL_NO_SMALL=1: the persistent pair at every size, for the
   // bitwise comparison in tests/test_gpu_parity.py)
@@ -1118,8 +1132,13 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
     return e && e[0] == '1';
   }();
   if (d.nblk <= 2 && !no_small) {  // factor + back substitution in one workgroup
-    k_chol_small<<<1, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.ysol, d.fail, d.gate);
-    return;
+    const bool fold = cam_step >= 0 && d.C <= 256;
+    double* part = d.partials;
+    k_chol_small<<<1, 256, 0, s>>>(d.S, d.ld, d.n, d.nblk, d.ysol, d.fail, d.gate, d.C, fold ? d.cam : nullptr,
+                                   d.scale_c, d.cam_new, d.camRn,
+                                   fold && cam_step > 0 ? part + size_t(kPStepCam) * d.max_blocks : nullptr,
+                                   part + size_t(kPBadCam) * d.max_blocks);
+    return fold;
   }
   const int nb = d.nblk, ntask = chol_tasks(nb);
   // one persistent workgroup per CU (roles by start order: a partly resident
@@ -1138,6 +1157,7 @@ void launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int* tc = d.overlap ? d.tile_cnt : nullptr;
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
                                          epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
+  return false;
 }
 
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set) {
