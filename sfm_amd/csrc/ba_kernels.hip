@@ -723,6 +723,78 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(const int32_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+// Camera c's diagonal block and rhs (64 lanes t of one wave; no barrier):
+// k_schur_diag_sum's body, also run by k_schur_pts<64, 4> for a small
+// system's diagonal blocks (one launch fewer per LM iteration).
+__device__ __forceinline__ void schur_diag_body(int c, int C, int t, const int32_t* __restrict__ cam_rng,
+                                                const double* __restrict__ dpart, const double* __restrict__ Ucam,
+                                                const double* __restrict__ diag_c, double radius, int add_diag,
+                                                double* __restrict__ S, int ld, int n, int init,
+                                                int* __restrict__ fail, unsigned long long* __restrict__ ysol,
+                                                int n_y) {
+  // k_pad_init folded in (one launch fewer per LM iteration): the identity
+  // padding below row n of this camera's six columns and y's sentinel
+  // there; the last camera also takes columns n.. (the identity block, the
+  // pivot (n, n) = 1), the rest of the sentinel and the failure flag.  None
+  // of these entries is written by the Schur passes.
+  for (int j = 6 * c; j < 6 * c + 6; ++j) {
+    for (int i = n + 1 + t; i < ld; i += 64) S[size_t(j) * ld + i] = 0.0;
+    if (t == 0 && j < n_y) ysol[j] = kYSentinel;  // k_backsolve's "not yet produced"
+  }
+  if (c == C - 1) {
+    for (int j = n; j < ld; ++j) {
+      for (int i = (j > n ? j : n + 1) + t; i < ld; i += 64) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
+      if (t == 0 && j < n_y) ysol[j] = kYSentinel;
+    }
+    if (t == 0) {
+      S[size_t(n) * ld + n] = 1.0;
+      *fail = 0;
+    }
+  }
+  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+  // lane t sums waves w0 + t, w0 + t + 64, ... (coalesced 216-B rows), then
+  // one reduce-scatter over the wave: lane 2e ends with entry e
+  double v[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v[e] = 0.0;
+  for (int w = w0 + t; w < w1; w += 64) {
+    const double* src = dpart + size_t(w) * 27;
+#pragma unroll
+    for (int e = 0; e < 27; ++e) v[e] += src[e];
+  }
+  const double sum = wave_sum32(v, t);
+  // every lane takes part in the shuffle (a source lane must be active):
+  // lanes < 36 fetch their S_cc entry, lanes 36..41 the rhs entries
+  const int tu = t < 36 ? t / 6 : 0, tv = t < 36 ? t % 6 : 0;
+  const int src = t < 36 ? up6(tu, tv) : (t < 42 ? 21 + (t - 36) : 0);
+  const double tot = __shfl(sum, 2 * src);
+  if (t < 36) {
+    const int u = tu, vv = tv, q = src;
+    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + vv;
+    double val = (init ? 0.0 : *sp) - tot;  // init: before the off-diagonal launch (k_schur_pts adds its part)
+    if (add_diag) {
+      val += Ucam[size_t(kUcam) * c + q];
+      if (u == vv) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
+    }
+    *sp = val;
+  } else if (t < 42) {
+    S[size_t(6 * c + (t - 36)) * ld + n] = tot;
+  }
+}
+
+// What k_schur_pts<64, 4> needs to run k_schur_diag_sum's body itself.
+struct DiagFold {
+  const int32_t* cam_rng;
+  const double* dpart;
+  const double* Ucam;
+  const double* diag_c;
+  double radius;
+  const double* radius_dev;
+  int add_diag, C, n, n_y;
+  int* fail;
+  unsigned long long* ysol;
+};
+
 // k_schur_pts: the off-diagonal Schur blocks WITHOUT the F gathers.  A pair
 // (o1, o2) of block (c1, c2) shares its point p, and
 //   F_o1 F_o2^T = J_c1^T M_1 M_2^T J_c2,   M_i = J_X,i L_p^-T,
@@ -813,7 +885,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int ld,
                                                         const int32_t* __restrict__ bperm, const int* __restrict__ gate,
-                                                        int* __restrict__ tile_cnt, int nbt) {
+                                                        int* __restrict__ tile_cnt, int nbt, const DiagFold df) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   static_assert(kWpb == 1 || (kWpb == kThreads / 64 && kSub == 64), "4 waves per block take 64 lanes each");
   constexpr int kPer = 64 / kSub;  // blocks per wave
@@ -844,6 +916,15 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
     stage_cam(cst[wv][q] + kCamS, cq.y, camR, cam, Kc, scale_c, l);
   }
   wave_lds_sync();
+  if (kWpb > 1 && df.C > 0 && own && cc.x == cc.y && wv == 0) {
+    // small system, k_schur_diag_sum folded in (df.C > 0): camera cc.x's
+    // diagonal block and rhs first, by the wave that later adds this block's
+    // duplicate pairs to it (its stores drained before those loads)
+    const double radius = df.radius_dev ? *df.radius_dev : df.radius;
+    schur_diag_body(cc.x, df.C, l, df.cam_rng, df.dpart, df.Ucam, df.diag_c, radius, df.add_diag, S, ld, df.n, 1,
+                    df.fail, df.ysol, df.n_y);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   const int kb = seg[b], ke = own ? seg[b + 1] : kb;
   double acc[36];
 #pragma unroll
@@ -1006,55 +1087,8 @@ __global__ __launch_bounds__(64) void k_schur_diag_sum(const int32_t* __restrict
                                                        int* __restrict__ fail, unsigned long long* __restrict__ ysol, int n_y) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   if (radius_dev) radius = *radius_dev;  // the device LM loop's current radius
-  const int c = blockIdx.x, t = threadIdx.x;
-  // k_pad_init folded in (one launch fewer per LM iteration): the identity
-  // padding below row n of this camera's six columns and y's sentinel
-  // there; the last camera also takes columns n.. (the identity block, the
-  // pivot (n, n) = 1), the rest of the sentinel and the failure flag.  None
-  // of these entries is written by the Schur passes.
-  for (int j = 6 * c; j < 6 * c + 6; ++j) {
-    for (int i = n + 1 + t; i < ld; i += 64) S[size_t(j) * ld + i] = 0.0;
-    if (t == 0 && j < n_y) ysol[j] = kYSentinel;  // k_backsolve's "not yet produced"
-  }
-  if (c == gridDim.x - 1) {
-    for (int j = n; j < ld; ++j) {
-      for (int i = (j > n ? j : n + 1) + t; i < ld; i += 64) S[size_t(j) * ld + i] = (i == j) ? 1.0 : 0.0;
-      if (t == 0 && j < n_y) ysol[j] = kYSentinel;
-    }
-    if (t == 0) {
-      S[size_t(n) * ld + n] = 1.0;
-      *fail = 0;
-    }
-  }
-  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
-  // lane t sums waves w0 + t, w0 + t + 64, ... (coalesced 216-B rows), then
-  // one reduce-scatter over the wave: lane 2e ends with entry e
-  double v[32];
-#pragma unroll
-  for (int e = 0; e < 32; ++e) v[e] = 0.0;
-  for (int w = w0 + t; w < w1; w += 64) {
-    const double* src = dpart + size_t(w) * 27;
-#pragma unroll
-    for (int e = 0; e < 27; ++e) v[e] += src[e];
-  }
-  const double sum = wave_sum32(v, t);
-  // every lane takes part in the shuffle (a source lane must be active):
-  // lanes < 36 fetch their S_cc entry, lanes 36..41 the rhs entries
-  const int tu = t < 36 ? t / 6 : 0, tv = t < 36 ? t % 6 : 0;
-  const int src = t < 36 ? up6(tu, tv) : (t < 42 ? 21 + (t - 36) : 0);
-  const double tot = __shfl(sum, 2 * src);
-  if (t < 36) {
-    const int u = tu, vv = tv, q = src;
-    double* sp = S + size_t(6 * c + u) * ld + 6 * size_t(c) + vv;
-    double val = (init ? 0.0 : *sp) - tot;  // init: before the off-diagonal launch (k_schur_pts adds its part)
-    if (add_diag) {
-      val += Ucam[size_t(kUcam) * c + q];
-      if (u == vv) { const double dd = sqrt(diag_c[6 * size_t(c) + u] / radius); val += dd * dd; }
-    }
-    *sp = val;
-  } else if (t < 42) {
-    S[size_t(6 * c + (t - 36)) * ld + n] = tot;
-  }
+  schur_diag_body(blockIdx.x, gridDim.x, threadIdx.x, cam_rng, dpart, Ucam, diag_c, radius, add_diag, S, ld, n, init,
+                  fail, ysol, n_y);
 }
 
 // Packed form of the reduced system for the cross-rank all-reduce: row i
@@ -1380,7 +1414,17 @@ void launch_point_prep(const DevProblem& d, double radius, hipStream_t s) {
 }
 void launch_schur(const DevProblem& d, double radius, bool add_diag, hipStream_t s) {
   // diagonal blocks + rhs first (k_obs_prep_rc's per-wave partials), then
-  // the off-diagonal blocks, which add a block's same-camera duplicate pairs
+  // the off-diagonal blocks, which add a block's same-camera duplicate pairs;
+  // a small system's block-per-workgroup pass does the first part itself
+  // (DiagFold: the workgroup of each diagonal block)
+  if (d.schur_wg_blocks && d.n_blk && d.C) {
+    const DiagFold f{d.cam_rng, d.dpart, d.Ucam, d.diag_c, radius, d.radius_dev, add_diag ? 1 : 0, d.C, d.n,
+                     (d.n + kNB - 1) / kNB * kNB, d.fail, reinterpret_cast<unsigned long long*>(d.ysol)};
+    k_schur_pts<64, kThreads / 64><<<int(d.n_bslots), kThreads, 0, s>>>(d.n_bslots, d.blk, d.seg, d.bpts, d.ptS,
+                                                                       d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
+                                                                       d.bperm, d.gate, nullptr, d.nblk, f);
+    return;
+  }
   launch_schur_diag(d, radius, add_diag, s);
   launch_schur_offdiag(d, nullptr, s);
 }
@@ -1401,11 +1445,11 @@ void launch_schur_offdiag(const DevProblem& d, int* tile_cnt, hipStream_t s) {
   const int nb = int((n_slots + per - 1) / per);
 #define SFM_PTS(S_)                                                                                           \
   k_schur_pts<S_><<<nb, kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, d.scale_c, \
-                                          d.S, d.ld, bperm, d.gate, tile_cnt, d.nblk)
+                                          d.S, d.ld, bperm, d.gate, tile_cnt, d.nblk, DiagFold{})
   if (d.schur_wg_blocks) {  // small systems: one block per workgroup
     k_schur_pts<64, kThreads / 64><<<int(n_slots), kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS,
                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
-                                                                    bperm, d.gate, tile_cnt, d.nblk);
+                                                                    bperm, d.gate, tile_cnt, d.nblk, DiagFold{});
     return;
   }
   if (sub == 8) SFM_PTS(8);
