@@ -200,6 +200,9 @@ void launch_pack_upper(const DevProblem& d, bool unpack, hipStream_t s);
 // dst = scale * src unless *gate == 0 (gate may be nullptr)
 void launch_gated_copy(const double* src, double* dst, int64_t n, double scale, const int32_t* gate, hipStream_t s);
 void launch_cam_update(const DevProblem& d, bool count_norm, hipStream_t s);
+// small systems (C <= 64): the point pass and the camera sums + finalisation
+// (k_cam_sum_finalize's work) in one launch; false when not applicable
+bool launch_point_eval_with_cams(const DevProblem& d, int mode, bool count_grad, hipStream_t s);
 void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var = true, bool pts_var = true);
 // grid of the XCD-ordered observation passes (k_obs_prep_rc, k_backsub_a_rc):
 // one workgroup per 4 chunks, a multiple of 8 (one point slice per XCD)

@@ -303,39 +303,50 @@ __global__ __launch_bounds__(64) void k_cam_sum(const int32_t* __restrict__ cam_
 // take their column's diagonal and gradient entries by shuffle, and the
 // camera's gradient max-norm goes to partial slot c (the max over cameras
 // is order-free: the same result as k_cam_finalize's per-block partials).
-__global__ __launch_bounds__(64) void k_cam_sum_finalize(const int32_t* __restrict__ cam_rng,
-                                                         const double* __restrict__ jpart, double* __restrict__ Ucam,
-                                                         double* __restrict__ scale_c, double* __restrict__ diag_c,
-                                                         double min_diag, double max_diag, int mode,
-                                                         double* __restrict__ part_grad,
-                                                         const int* __restrict__ gate) {
-  if (gate && *gate == 0) return;  // device LM loop: phase skipped
-  const int c = blockIdx.x, t = threadIdx.x;
-  const int w0 = cam_rng[2 * c] / 64, w1 = (cam_rng[2 * c + 1] + 63) / 64;
+// Camera c's U_c / b_c sums and their finalisation (64 lanes t of one wave,
+// no barrier): k_cam_sum_finalize's body, also run by k_point_eval_lds<64>'s
+// trailing workgroups for small systems (CamFold: one launch fewer).
+struct CamFold {
+  const int32_t* cam_rng;
+  const double* jpart;
+  double* Ucam;
+  double* scale_c;
+  double* diag_c;
+  double min_diag, max_diag;
+  int mode, C;
+  double* part_grad;
+};
+__device__ __forceinline__ void cam_sum_body(int c, int t, const CamFold& f) {
+  const int w0 = f.cam_rng[2 * c] / 64, w1 = (f.cam_rng[2 * c + 1] + 63) / 64;
   double v[32];
 #pragma unroll
   for (int e = 0; e < 32; ++e) v[e] = 0.0;
   for (int w = w0 + t; w < w1; w += 64) {
-    const double* src = jpart + size_t(w) * 27;
+    const double* src = f.jpart + size_t(w) * 27;
 #pragma unroll
     for (int e = 0; e < 27; ++e) v[e] += src[e];
   }
   const double sum = wave_sum32(v, t);
-  if (!(t & 1) && (t >> 1) < 27) Ucam[size_t(kUcam) * c + (t >> 1)] = sum;
+  if (!(t & 1) && (t >> 1) < 27) f.Ucam[size_t(kUcam) * c + (t >> 1)] = sum;
   const int a = t < 6 ? t : 0;
   const double cn = __shfl(sum, 2 * up6(a, a)), ga = __shfl(sum, 2 * (21 + a));
   double g = 0.0;
   if (t < 6) {
-    if (mode == 0) {
-      scale_c[6 * c + a] = 1.0 / (1.0 + sqrt(cn));
+    if (f.mode == 0) {
+      f.scale_c[6 * c + a] = 1.0 / (1.0 + sqrt(cn));
     } else {
-      diag_c[6 * c + a] = fmin(fmax(cn, min_diag), max_diag);
-      g = fabs(ga / scale_c[6 * c + a]);
+      f.diag_c[6 * c + a] = fmin(fmax(cn, f.min_diag), f.max_diag);
+      g = fabs(ga / f.scale_c[6 * c + a]);
     }
   }
 #pragma unroll
   for (int off = 4; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off));
-  if (t == 0 && part_grad) part_grad[c] = g;
+  if (t == 0 && f.part_grad) f.part_grad[c] = g;
+}
+
+__global__ __launch_bounds__(64) void k_cam_sum_finalize(const CamFold f, const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  cam_sum_body(blockIdx.x, threadIdx.x, f);
 }
 
 __global__ __launch_bounds__(kThreads) void k_cam_finalize(int C, const double* __restrict__ Ucam,
@@ -474,8 +485,15 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_lds(int P, int C, const
                                                              double* __restrict__ scale_p, double* __restrict__ diag_p,
                                                              double* __restrict__ ptV, double min_diag, double max_diag,
                                                              int mode, int reuse, double* __restrict__ part_grad,
-                                                             double* __restrict__ part_xn, const int* __restrict__ gate) {
+                                                             double* __restrict__ part_xn, const int* __restrict__ gate,
+                                                             const CamFold cf) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  const int nbp = (P + kThreads - 1) / kThreads;
+  if (int(blockIdx.x) >= nbp) {  // (cf.C > 0) the camera sums: one camera per wave, no barrier
+    const int c = (int(blockIdx.x) - nbp) * (kThreads / 64) + int(threadIdx.x >> 6);
+    if (c < cf.C) cam_sum_body(c, threadIdx.x & 63, cf);
+    return;
+  }
   __shared__ double sh[4];
   __shared__ double cst[kMaxC * kCamE];
   for (int i = threadIdx.x; i < C * kCamE; i += blockDim.x) {
@@ -1376,10 +1394,21 @@ void launch_jacobian(const DevProblem& d, bool scaled, hipStream_t s, bool write
 void launch_cam_reduce(const DevProblem& d, hipStream_t s) {
   if (d.C) k_cam_sum<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.gate);
 }
+static CamFold cam_fold(const DevProblem& d, int mode, bool count_grad) {
+  return CamFold{d.cam_rng, d.jpart, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode, d.C,
+                 count_grad ? slot(d, kPGradCam) : nullptr};
+}
 void launch_cam_sum_finalize(const DevProblem& d, int mode, bool count_grad, hipStream_t s) {
-  if (d.C)
-    k_cam_sum_finalize<<<d.C, 64, 0, s>>>(d.cam_rng, d.jpart, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
-                                          count_grad ? slot(d, kPGradCam) : nullptr, d.gate);
+  if (d.C) k_cam_sum_finalize<<<d.C, 64, 0, s>>>(cam_fold(d, mode, count_grad), d.gate);
+}
+bool launch_point_eval_with_cams(const DevProblem& d, int mode, bool count_grad, hipStream_t s) {
+  if (d.P == 0 || d.C == 0 || d.C > 64) return false;
+  const int nb = blocks_for(d.P, kThreads) + (d.C + kThreads / 64 - 1) / (kThreads / 64);
+  k_point_eval_lds<64><<<nb, kThreads, 0, s>>>(d.P, d.C, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X,
+                                               d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag, mode, 0,
+                                               slot(d, kPGradPt), slot(d, kPXNormPt), d.gate,
+                                               cam_fold(d, mode, count_grad));
+  return true;
 }
 void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool count_grad, hipStream_t s) {
   k_cam_finalize<<<blocks_for(d.C, kThreads), kThreads, 0, s>>>(d.C, d.Ucam, d.scale_c, d.diag_c, d.min_diag, d.max_diag, mode,
@@ -1393,7 +1422,8 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
 #define SFM_PE_LDS(M_)                                                                                              \
   k_point_eval_lds<M_><<<nb, kThreads, 0, s>>>(d.P, d.C, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X,      \
                                                d.scale_p, d.diag_p, d.ptV, d.min_diag, d.max_diag, mode,           \
-                                               reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt), d.gate)
+                                               reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt), d.gate,    \
+                                               CamFold{})
   if (d.C <= 64) SFM_PE_LDS(64);
   else if (d.C <= 512) SFM_PE_LDS(512);
   else

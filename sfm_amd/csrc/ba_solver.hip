@@ -573,24 +573,36 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   mark_end(h);
   // unsharded: the U_c sums and their finalisation in one launch
   const bool fuse_cam = !sharded(h);
+  // small systems (C <= 64): the camera sums ride in the point pass's launch
+  const bool fold_cams = fuse_cam && cams_var && pts_var && d.P > 0 && d.C > 0 && d.C <= 64;
   if (first && jacobi_scaling) {
-    if (cams_var) {
-      mark_begin(h, kPhCamRed);
-      if (fuse_cam) {
-        launch_cam_sum_finalize(d, 0, false, s);
-      } else {
-        launch_cam_reduce(d, s);
-        if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
-        launch_cam_finalize(d, 0, false, false, s);
-      }
+    if (fold_cams) {
+      mark_begin(h, kPhPtEval);
+      launch_point_eval_with_cams(d, 0, false, s);
       mark_end(h);
+    } else {
+      if (cams_var) {
+        mark_begin(h, kPhCamRed);
+        if (fuse_cam) {
+          launch_cam_sum_finalize(d, 0, false, s);
+        } else {
+          launch_cam_reduce(d, s);
+          if ((rc = allreduce(h, d.Ucam, size_t(kUcam) * d.C, ncclSum))) return rc;
+          launch_cam_finalize(d, 0, false, false, s);
+        }
+        mark_end(h);
+      }
+      if (pts_var) launch_point_eval(d, 0, false, s);
     }
-    if (pts_var) launch_point_eval(d, 0, false, s);
     mark_begin(h, kPhJac);
     launch_jacobian(d, true, s);
     mark_end(h);
   }
-  if (cams_var) {
+  if (fold_cams) {
+    mark_begin(h, kPhPtEval);
+    launch_point_eval_with_cams(d, 1, true, s);
+    mark_end(h);
+  } else if (cams_var) {
     mark_begin(h, kPhCamRed);
     if (fuse_cam) {
       launch_cam_sum_finalize(d, 1, true, s);
@@ -604,7 +616,9 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
     hipMemsetAsync(d.partials + size_t(kPGradCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
     hipMemsetAsync(d.partials + size_t(kPXNormCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
   }
-  if (pts_var) {
+  if (fold_cams) {
+    // (done above, with the camera sums)
+  } else if (pts_var) {
     mark_begin(h, kPhPtEval);
     launch_point_eval(d, 1, false, s);
     mark_end(h);
