@@ -114,7 +114,8 @@ struct sfm_ba_handle {
   bool fuse_lm = false;
   // device LM loop: the evaluation's k_cam_prep also makes the accepted
   // candidate current (k_lm_accept folded in; its grid covers the copy)
-  int accept_grid = 0;
+  int accept_grid = 0;  // < 0: done by the deciding reduction (AcceptFold)
+  bool accept_fold = false;
   int n_cu = 0;  // compute units of the device (queried once)
   // Schur / Cholesky overlap (DevProblem::overlap): the factorisation's
   // stream and the two events that fork and join it
@@ -446,11 +447,29 @@ __global__ void k_lm_init(LmCtl* c, const double* __restrict__ scal) { lm_init(c
 // workgroup resets it.  Gated like the reduction: with the phase skipped the
 // bookkeeping is a no-op too (run_step = 0 only once done, run_eval = 0).
 enum LmTail { kTailDecide = 0, kTailPost = 1, kTailInit = 2 };
+// Small problems (C <= 256, few points): the accepted step's copy and camera
+// preparation -- k_cam_prep with cam_src, the evaluation's first launch --
+// run in the deciding workgroup right after lm_decide, when it accepted the
+// step.  Same per-camera arithmetic; the |x|^2 partial is the one-workgroup
+// sum (the 12 extra waves add +0.0).  C == 0: not folded.
+struct AcceptFold {
+  int C;
+  int64_t n_x;
+  double* cam;
+  double* camR;
+  double* part_xn;
+  const double* cam_src;
+  const double* X_src;
+  double* X_dst;
+};
+constexpr int kAcceptFoldMaxCams = 256;
+constexpr int64_t kAcceptFoldMaxX = 3 * 8192;
 template <int kTail>
 __global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restrict__ partials, int64_t max_blocks,
                                                           ReduceBatch b, double* __restrict__ scal,
                                                           const int* __restrict__ fail, const int* __restrict__ gate,
-                                                          LmCtl* c, sfm_ba_iteration* trace, int cap) {
+                                                          LmCtl* c, sfm_ba_iteration* trace, int cap,
+                                                          const AcceptFold af) {
   if (gate && *gate == 0) return;
   __shared__ double sh[16];
   __shared__ double sc[kNumScalars + 1];
@@ -472,6 +491,28 @@ __global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restri
     else if (kTail == kTailInit) lm_init(c, sc);
     else lm_decide(c, sc, trace, cap);
   }
+  if (kTail != kTailDecide || af.C == 0) return;
+  __shared__ int accepted;
+  if (threadIdx.x == 0) accepted = c->run_eval;
+  __syncthreads();
+  if (!accepted) return;
+  for (int64_t i = threadIdx.x; i < af.n_x; i += blockDim.x) af.X_dst[i] = af.X_src[i];
+  double xn = 0.0;
+  const int cc = threadIdx.x;
+  if (cc < af.C) {
+    double x6[6];
+    for (int k = 0; k < 6; ++k) x6[k] = af.cam_src[6 * cc + k];
+    for (int k = 0; k < 6; ++k) af.cam[6 * cc + k] = x6[k];
+    const double w[3] = {x6[0], x6[1], x6[2]};
+    double R[9], dR[27];
+    rotation(w, R, dR);
+    double* o = af.camR + size_t(kCamR) * cc;
+    for (int i = 0; i < 9; ++i) o[i] = R[i];
+    for (int i = 0; i < 27; ++i) o[9 + i] = dR[i];
+    for (int k = 0; k < 6; ++k) xn += x6[k] * x6[k];
+  }
+  const double r = block_reduce(xn, sh, false);
+  if (threadIdx.x == 0 && af.part_xn) af.part_xn[0] = r;
 }
 
 // Reduced systems with more camera blocks than this take the XCD-aware
@@ -544,10 +585,17 @@ void reduce_phase(sfm_ba_handle* h, const ReduceBatch& rb, bool copy_fail, int t
 #define SFM_RB_LM(T_)                                                                                      \
   k_reduce_batch_lm<T_><<<rb.n, 1024, 0, h->stream>>>(d.partials, d.max_blocks, rb, d.scal,                 \
                                                       copy_fail ? d.fail : nullptr, d.gate, h->lm_ctl,      \
-                                                      h->lm_trace, h->lm_trace_cap)
+                                                      h->lm_trace, h->lm_trace_cap, af)
+    AcceptFold af{};
     if (tail == kTailPost) SFM_RB_LM(kTailPost);
     else if (tail == kTailInit) SFM_RB_LM(kTailInit);
-    else SFM_RB_LM(kTailDecide);
+    else {
+      if (h->accept_fold)
+        af = AcceptFold{d.C, 3 * int64_t(d.P), d.cam, d.camR,
+                        h->mode != SFM_BA_STRUCT_ONLY ? d.partials + size_t(kPXNormCam) * d.max_blocks : nullptr,
+                        d.cam_new, d.X_new, d.X};
+      SFM_RB_LM(kTailDecide);
+    }
 #undef SFM_RB_LM
     return;
   }
@@ -567,7 +615,8 @@ int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
   const int nbP = std::max(1, blocks_for(d.P, 256)),
             nbC = std::max(1, blocks_for(d.C, 256));
   if (h->accept_grid > 0) launch_cam_prep_accept(d, cams_var, h->accept_grid, s);
-  else launch_cam_prep(d, d.cam, cams_var, s);
+  else if (h->accept_grid == 0) launch_cam_prep(d, d.cam, cams_var, s);
+  // accept_grid < 0: done by the deciding workgroup (AcceptFold)
   mark_begin(h, kPhJac);
   launch_jacobian(d, !first || !jacobi_scaling ? true : false, s);
   mark_end(h);
@@ -844,6 +893,8 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   // without a collective between a phase's reduction and the bookkeeping,
   // the two are one launch (k_reduce_batch_lm)
   h->fuse_lm = !sharded(h) && !env_flag("SFM_LM_UNFUSED");
+  h->accept_fold = h->fuse_lm && d.C > 0 && d.C <= kAcceptFoldMaxCams && 3 * int64_t(d.P) <= kAcceptFoldMaxX &&
+                   !env_flag("SFM_NO_ACCEPT_FOLD");
   // the initial evaluation (Jacobi scaling on first use); its scalars
   // initialise the loop state on the device
   d.gate = nullptr;
@@ -856,7 +907,9 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
       d.gate = nullptr;
       if (!h->fuse_lm) k_lm_decide<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
       d.gate = &h->lm_ctl->run_eval;
-      h->accept_grid = acc_blocks;  // k_lm_accept's copy inside the evaluation's k_cam_prep
+      // k_lm_accept's copy inside the evaluation's k_cam_prep, or already
+      // done in the deciding workgroup
+      h->accept_grid = h->accept_fold ? -1 : acc_blocks;
       rc = evaluate_enqueue(h, false, jac_scaling);
       h->accept_grid = 0;
       if (rc) break;
@@ -876,6 +929,7 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   d.gate = nullptr;
   d.radius_dev = nullptr;
   h->fuse_lm = false;
+  h->accept_fold = false;
   if (rc) return rc;
   if (c.error & 4) return fail(SFM_EIO, "Cholesky tile hand-off timed out (persistent grid made no progress)");
   if (c.error & 2) return fail(SFM_EIO, "back-substitution hand-off timed out (persistent grid made no progress)");
