@@ -20,6 +20,52 @@ pytestmark = pytest.mark.gpu
 C, P, VIEWS, SEED = 40, 6000, 8, 0x5F3D2017 + 21
 
 
+def _collect(procs, q, world, timeout):
+    """Each worker's result from the queue; a worker that raised puts
+    ("error", rank, traceback) instead, and then (or at the deadline) the
+    workers -- the ones left waiting in a collective -- are ended, so a
+    failing rank fails the test at once instead of hanging it."""
+    import queue
+    import time
+    deadline = time.monotonic() + timeout
+    res = []
+    try:
+        while len(res) < world:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise AssertionError(f"only {len(res)} of {world} ranks reported within {timeout} s")
+            try:
+                r = q.get(timeout=min(left, 5.0))
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                if dead:
+                    raise AssertionError(f"a rank exited with {dead[0]} before reporting")
+                continue
+            if r[0] == "error":
+                raise AssertionError(f"rank {r[1]} failed:\n{r[2]}")
+            res.append(r)
+    except BaseException:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        for p in procs:
+            p.join(10)
+        raise
+    return sorted(res, key=lambda r: r[0])
+
+
+def _guarded(fn):
+    """Worker body wrapper: an exception goes into the queue (last arg)."""
+    def run(rank, *args):
+        try:
+            fn(rank, *args)
+        except BaseException:
+            import traceback
+            args[-1].put(("error", rank, traceback.format_exc()))
+            raise
+    return run
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -29,6 +75,10 @@ def _free_port():
 
 
 def _worker(rank, world, port, q, mode):
+    _guarded(_worker_body)(rank, world, port, mode, q)
+
+
+def _worker_body(rank, world, port, mode, q):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch
@@ -71,7 +121,7 @@ def test_sharded_solve_on_one_gpu_matches_single(world, mode):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda r: r[0])
+    res = _collect(procs, q, world, 150)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -96,6 +146,10 @@ C4_SEED = 0x5F3D2017 + 4          # scene.config("C4")
 
 
 def _c4_worker(rank, world, port, q):
+    _guarded(_c4_worker_body)(rank, world, port, q)
+
+
+def _c4_worker_body(rank, world, port, q):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch
@@ -151,7 +205,7 @@ def test_c4_two_rank_sharded_solve_matches_single_rank():
     procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=540) for _ in range(world)], key=lambda r: r[0])
+    res = _collect(procs, q, world, 540)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
