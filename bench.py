@@ -421,23 +421,15 @@ def oneshot_leg(sc, reps: int = 3) -> dict:
 
 def stream_copy_gbs(device: int) -> float:
     """Measured device-to-device copy bandwidth (STREAM copy: read + write
-    bytes / time) of a 4 GiB buffer, best of 5, beside the 8 TB/s spec."""
-    import torch
-    n = 1 << 29  # doubles: 4 GiB per buffer
-    a = torch.ones(n, dtype=torch.float64, device=f"cuda:{device}")
-    b = torch.empty_like(a)
-    best = 0.0
-    for _ in range(6):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        best = max(best, 2 * 8 * n / (e0.elapsed_time(e1) * 1e-3) / 1e9)
-    del a, b
-    torch.cuda.empty_cache()
-    return best
+    bytes / time) of a 4 GiB buffer with 16-B accesses (sfm_bench_stream_copy:
+    the best of a few grid / unroll shapes, 5 timed launches each), beside the
+    8 TB/s spec; MI355X_MICROARCH.md measures 6.29 TB/s this way."""
+    import ctypes
+    import sfm_amd
+    from sfm_amd._ffi import check
+    gbs = ctypes.c_double(0.0)
+    check(sfm_amd.lib().sfm_bench_stream_copy(device, 1 << 32, 5, ctypes.byref(gbs)), "sfm_bench_stream_copy")
+    return gbs.value
 
 
 def matcher_leg(device: int, steps: int, cpu: bool) -> dict:

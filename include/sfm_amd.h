@@ -355,6 +355,10 @@ int sfm_triangulate_points(int32_t device, int32_t n, const int32_t* cam0, const
  * factor+solve; *chol_fail = 1 if a pivot was not positive. */
 int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double* b, double* y, int32_t reps,
                         double* ms, int32_t* chol_fail);
+/* Measurement plumbing (bench.py, not a reference interface): the best
+ * STREAM-copy bandwidth (read + write bytes / s, 16-B accesses) over a few
+ * launch shapes, `bytes` per buffer, `reps` timed launches each. */
+int sfm_bench_stream_copy(int32_t device, int64_t bytes, int32_t reps, double* best_gbs);
 
 /* ---- Pyramidal Lucas-Kanade tracker -------------- */
 typedef struct sfm_klt_params {

@@ -61,7 +61,14 @@ __device__ __forceinline__ double block_reduce(double v, double* sh, bool is_max
 // theta^2 > DBL_EPSILON -> Rodrigues; otherwise the first-order map I + [w]x.
 // Optionally dR/dw_k (k-major, 3 x row-major 3x3), differentiated through
 // the same expressions the Jet evaluation of the reference functor uses.
+//
+// Contraction is pinned here (not left to the translation unit's flags):
+// k_cam_prep (ba_kernels.hip) and the device LM loop's accept fold
+// (ba_solver.hip) both call this, and the device loop must equal the host
+// loop bitwise.  `on` fuses within one expression only, so inlining into
+// different callers cannot change which products are fused.
 __device__ void rotation(const double w[3], double R[9], double* dR) {
+#pragma clang fp contract(on)
   const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   if (th2 > DBL_EPSILON) {
     const double th = sqrt(th2);
@@ -113,6 +120,7 @@ __device__ void rotation(const double w[3], double R[9], double* dR) {
 __device__ __forceinline__ void cam_update_one(int c, const double* __restrict__ cam, const double* __restrict__ ysol,
                                                const double* __restrict__ scale_c, double* __restrict__ cam_new,
                                                double* __restrict__ camRn, double& st, double& bad) {
+#pragma clang fp contract(on)  // (as rotation(): k_cam_update and k_chol_small must agree bitwise)
   double xn[6];
   for (int k = 0; k < 6; ++k) {
     const double y = ysol[6 * c + k];

@@ -223,8 +223,11 @@ int blocks_for(int64_t n, int threads);
 // ---- dense Cholesky (chol_kernels.hip) ----
 // cam_step >= 0: a small system's one-workgroup factor also takes the
 // camera step (k_cam_update; cam_step > 0: with its step-length partial);
-// returns whether it did
-bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true, int cam_step = -1);
+// returns whether it did.  overlap: d.overlap when the factor runs beside
+// k_schur_pts (its helpers then await tile_cnt and take the overlap's grid),
+// 0 otherwise -- only the overlapped branch zeroes and fills tile_cnt
+bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail = true, int cam_step = -1,
+                     int overlap = 0);
 // W_k granules back to the sentinel (k_schur_diag_sum does this in the solve)
 // sentinel_set: y already holds kYSentinel (k_pad_init wrote it)
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set = false);

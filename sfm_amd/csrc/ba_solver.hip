@@ -727,7 +727,7 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     HIPCHK(hipEventRecord(h->ov_ev[0], s));
     HIPCHK(hipStreamWaitEvent(h->stream2, h->ov_ev[0], 0));
     mark_begin(h, kPhChol, h->stream2);
-    launch_cholesky(d, ++h->chol_epoch, h->stream2, false);
+    launch_cholesky(d, ++h->chol_epoch, h->stream2, false, -1, d.overlap);
     mark_end(h, h->stream2);
     launch_schur_offdiag(d, d.tile_cnt, s);
     HIPCHK(hipEventRecord(h->ov_ev[1], h->stream2));
@@ -1174,10 +1174,14 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     cnt_c = err + 4;
     TMP(cnt_p, size_t(P) + 1);
   }
-  if (N && stage_in) {
-    std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
-    std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
-    std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
+  // (host checks: the point counts ride in this upload, so it goes up even
+  // without observations -- the zero counts then reach cnt_p)
+  if ((N || host_check) && stage_in) {
+    if (N) {
+      std::memcpy(stg + o_uv, obs_uv, sizeof(double) * 2 * size_t(N));
+      std::memcpy(stg + o_cam, cam_idx, sizeof(int32_t) * size_t(N));
+      std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
+    }
     HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
   } else if (N) {
     HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));

@@ -1123,7 +1123,7 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
 
 }  // namespace
 
-bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int cam_step) {
+bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int cam_step, int overlap) {
   if (clear_fail) (void)hipMemsetAsync(d.fail, 0, sizeof(int), s);
   // (SFM_CHOL_NO_SMALL=1: the persistent pair at every size, for the
   // bitwise comparison in tests/test_gpu_parity.py)
@@ -1151,10 +1151,10 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   // (overlapped with the Schur pass: half the CUs, the other half runs
   // k_schur_pts, whose blocks the helpers await -- at n = 3000 127 helpers
   // factor as fast as 255, 63 take 1.37x)
-  const int full = d.overlap == 1 ? d.n_cu / 2 - 1 : d.n_cu - 1;
+  const int full = overlap == 1 ? d.n_cu / 2 - 1 : d.n_cu - 1;
   const int cap = helpers_env > 0 ? std::min(helpers_env, full) : full;
   const int nhelp = std::max(1, std::min(ntask, cap));
-  const int* tc = d.overlap ? d.tile_cnt : nullptr;
+  const int* tc = overlap ? d.tile_cnt : nullptr;
   k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
                                          epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
   return false;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the C1 keyframe-sized one-shot latency (tools/c1_latency.py) between
 # library builds / environments on one box, alternating:
-#   bash tools/ab_c1.sh head=tools/var_head.so new= devsetup=:SFM_HOST_SETUP=0
+#   bash tools/ab_c1.sh head=abvar/var_head.so new= devsetup=:SFM_HOST_SETUP=0
 # (label=LIB[:VAR=VALUE ...]; an empty LIB is the in-tree library)
 R=$GRAFT_REPO_ROOT
 for pass in 1 2; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the fused Cholesky's hand-off forms (SFM_CHOL_OPT bits) on one box:
-# walker phase stamps (tools/var_stamps.so) and the production factor time.
+# walker phase stamps (abvar/var_stamps.so) and the production factor time.
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R
 for rep in 1 2; do

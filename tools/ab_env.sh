@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B kernel stats of tools/ab_solve.py (C3 solve) under environment variants:
-#   bash tools/ab_env.sh base='' j128='SFM_JAC_WG_PER_XCD=128' head='SFM_AMD_LIB=tools/var_head.so' ...
+#   bash tools/ab_env.sh base='' j128='SFM_JAC_WG_PER_XCD=128' head='SFM_AMD_LIB=abvar/var_head.so' ...
 # each variant twice in alternation (same box); prints the final cost and the
 # top kernels of each run.
 R=$GRAFT_REPO_ROOT

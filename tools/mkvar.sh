@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build an ablation variant: tools/mkvar.sh NAME 'python patch' [file] -> tools/var_NAME.so
+# Build an ablation variant: tools/mkvar.sh NAME 'python patch' [file] -> abvar/var_NAME.so (git-ignored; delete after the A/B so it stops shipping)
 # The patch is python code run with s = the file's text (default ba_kernels.hip); it must change s.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -15,4 +15,4 @@ exec(code)
 assert s != s0, "patch changed nothing"
 open(path, 'w').write(s)
 PY
-make -s -C $V/sfm_amd/csrc -j8 OUT=$R/tools/var_$name.so
+make -s -C $V/sfm_amd/csrc -j8 OUT=$R/abvar/var_$name.so

@@ -1,5 +1,5 @@
 """Diagonal-walker phase times of the fused Cholesky from the stamped
-variant tools/var_stamps.so (tools/chol_stamps.sh).  Usage:
+variant abvar/var_stamps.so (tools/chol_stamps.sh).  Usage:
   SFM_CHOL_OPT=<bits> python tools/walker_phases.py [n]"""
 import ctypes, os, sys
 import numpy as np
