@@ -173,39 +173,61 @@ def test_live_path_on_device_brisk_detections(run_brisk):
         # after a Sim(3) alignment, over the scene radius
         res, al = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]), (r, t, X),
                                          extent=True)
-        table.append(dict(ba=k, obs=len(rec["uv"]), iterations=sm_o["num_iterations"],
-                          gpu_iterations=rec["summary"].num_iterations,
-                          termination=sm_o["termination_type"], cost_rel=d, cost_sensitivity=sens, X_rel=dx,
-                          X_sensitivity=sens_x, residual_max_px=res, residual_sensitivity_px=sens_res,
-                          sim3_aligned_rel=al, sim3_aligned_sensitivity=sens_al))
+        row = dict(ba=k, obs=len(rec["uv"]), iterations=sm_o["num_iterations"],
+                   gpu_iterations=rec["summary"].num_iterations,
+                   termination=sm_o["termination_type"], cost_rel=d, cost_sensitivity=sens, X_rel=dx,
+                   X_sensitivity=sens_x, residual_max_px=res, residual_sensitivity_px=sens_res,
+                   sim3_aligned_rel=al, sim3_aligned_sensitivity=sens_al)
+        if sm_o["termination_type"] == 1:
+            # the oracle in the device solver's association of the reduced
+            # matrix's diagonal blocks (oracle order=1: the same arithmetic,
+            # U_c summed first, then + D^2, then the outer products)
+            r1, t1, X1 = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
+            sm_1, _ = O.solve(rec["uv"], rec["cam_idx"], rec["pt_idx"], rec["K"], r1, t1, X1, order=1)
+            res1, al1 = L.gauge_invariant_diff(_residuals, sc_, (rec["rot_out"], rec["t_out"], rec["X_out"]),
+                                               (r1, t1, X1), extent=True)
+            row.update(order1_iterations=sm_1["num_iterations"],
+                       order1_cost_rel=abs(rec["summary"].final_cost - sm_1["final_cost"]) / sm_1["final_cost"],
+                       order1_X_rel=_rel(rec["X_out"], X1), order1_residual_max_px=res1, order1_sim3_aligned_rel=al1)
+        table.append(row)
         print(f"keyframe BA {k}: {len(rec['uv'])} obs, iterations {sm_o['num_iterations']} "
               f"({sm_o['termination_type']}), cost rel diff {d:.2e} (oracle rounding sensitivity {sens:.2e}), "
               f"X rel diff {dx:.2e} (sensitivity {sens_x:.2e}), residuals {res:.1e} px, Sim(3)-aligned {al:.1e} "
-              f"(sensitivity {sens_res:.1e} px, {sens_al:.1e})")
-    # the per-keyframe table (committed as profiles/r04_live_brisk_ba_parity.json)
+              f"(sensitivity {sens_res:.1e} px, {sens_al:.1e})"
+              + ("" if "order1_X_rel" not in row else
+                 f"; vs the oracle in the device association: cost {row['order1_cost_rel']:.2e}, X "
+                 f"{row['order1_X_rel']:.2e}, residuals {row['order1_residual_max_px']:.1e} px, aligned "
+                 f"{row['order1_sim3_aligned_rel']:.1e}"))
+    # the per-keyframe table (committed as profiles/r05_live_brisk_ba_parity.json)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, "live_brisk_ba_parity.json"), "w") as f:
         json.dump(table, f, indent=1)
-    # Every allowance is 20x the oracle's own rounding spread, capped.
-    # Converged runs (Ceres' function tolerance): cost 1e-6 relative (the
-    # north-star tolerance), residuals 1e-4 px, Sim(3)-aligned distance 1e-5
-    # of the scene radius, raw X 1e-3 (gauge-dependent).  A run stopped by
-    # the 50-iteration cap (NO_CONVERGENCE, termination 1) ends at an
-    # arbitrary point of a slow drift along the free 7-DoF gauge: measured
-    # round 4, BA 3 of this stream, the oracle's own raw X moves 1e-5..1e-4
-    # under 2 ulp of start perturbation and the GPU's end point sits 5e-4
-    # away, 3e-5 of the radius after alignment, at the same cost to 1e-8;
-    # there the cost keeps the 1e-6 cap (floor 1e-7), residuals / aligned
-    # distance / raw X are capped at 1e-3 px / 1e-4 / 1e-2.
+    # Converged runs (Ceres' function tolerance): the north-star tolerance
+    # flat -- cost, raw X and the Sim(3)-aligned distance (over the scene
+    # radius) within 1e-6 relative, residuals within 1e-6 px (measured round
+    # 5: X 6.9e-7, aligned 8.4e-11, residuals 3.1e-9 px at most).
+    # A run stopped by the 50-iteration cap (NO_CONVERGENCE, termination 1)
+    # ends at an arbitrary point of a slow drift along the free 7-DoF gauge,
+    # where the reference algorithm itself moves by its own rounding: 2 ulp
+    # of start perturbation move the oracle's end point (BA 3 of this stream)
+    # by 2e-3 in raw X and 4e-4 of the radius after alignment.  There the
+    # GPU's end point must lie within TWICE that spread of the oracle's in
+    # every quantity (cost also <= 1e-6), both in Ceres' summation order and
+    # in the device's association of the diagonal blocks (oracle order=1).
     for row in table:
-        k, capped = row["ba"], row["termination"] == 1
         assert row["gpu_iterations"] == row["iterations"], row
-        assert row["cost_rel"] <= min(1e-6, max(1e-7 if capped else 1e-9, 20 * row["cost_sensitivity"])), row
-        assert row["residual_max_px"] <= min(1e-3 if capped else 1e-4,
-                                             max(1e-8, 20 * row["residual_sensitivity_px"])), row
-        assert row["sim3_aligned_rel"] <= min(1e-4 if capped else 1e-5,
-                                              max(1e-9, 20 * row["sim3_aligned_sensitivity"])), row
-        assert row["X_rel"] <= min(1e-2 if capped else 1e-3, max(1e-6, 20 * row["X_sensitivity"])), row
+        if row["termination"] != 1:
+            assert row["cost_rel"] <= 1e-6, row
+            assert row["X_rel"] <= 1e-6, row
+            assert row["sim3_aligned_rel"] <= 1e-6, row
+            assert row["residual_max_px"] <= 1e-6, row
+            continue
+        assert row["order1_iterations"] == row["iterations"], row
+        for pre in ("", "order1_"):
+            assert row[pre + "cost_rel"] <= min(1e-6, max(1e-9, 2 * row["cost_sensitivity"])), row
+            assert row[pre + "X_rel"] <= max(1e-6, 2 * row["X_sensitivity"]), row
+            assert row[pre + "sim3_aligned_rel"] <= max(1e-9, 2 * row["sim3_aligned_sensitivity"]), row
+            assert row[pre + "residual_max_px"] <= max(1e-8, 2 * row["residual_sensitivity_px"]), row
     # The scene is one textured plane at depth 10 seen over 0.1-0.3-unit
     # baselines, where a lateral translation and a small rotation move the
     # image almost alike: the camera centres alone are weakly determined

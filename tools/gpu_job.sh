@@ -25,14 +25,14 @@ while [ $# -ge 2 ]; do
     tests) cmd="python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread" ;;
     tests:*) cmd="python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k '${cmd#tests:}'" ;;
     bench) cmd="python bench.py > $O/bench.json" ;;
-    kstats) cmd="rocprofv3 --kernel-trace --stats -d $O/kt -o run -- python3 bench.py --steps 10 --warmup 3 --no-tracker --no-cpu-baseline --no-oneshot > $O/kt_bench.json" ;;
+    kstats) cmd="rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 10 --warmup 3 --no-tracker --no-cpu-baseline --no-oneshot > $O/kt_bench.json" ;;
   esac
   echo "== step $k (${secs}s): $cmd" | tee -a "$O/steps.txt"
   start=$(date +%s.%N)
   timeout -k 10 "$secs" bash -c "$cmd" > "$O/$k.log" 2>&1
   rc=$?
   end=$(date +%s.%N)
-  echo "   rc=$rc  $(echo "$end - $start" | bc) s" | tee -a "$O/steps.txt"
+  echo "   rc=$rc  $(awk "BEGIN{printf \"%.1f\", $end - $start}") s" | tee -a "$O/steps.txt"
   if [ $rc -ne 0 ]; then
     tail -40 "$O/$k.log"
     exit $rc
