@@ -133,6 +133,8 @@ _SIGNATURES = {
     "sfm_comm_unique_id": (c_int, [c_void_p]),
     "sfm_ba_set_comm": (c_int, [c_void_p, c_int32, c_int32, c_void_p]),
     "sfm_ba_set_host_comm": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "sfm_ba_set_host_collectives": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "sfm_ba_set_distributed_factor": (c_int, [c_void_p, c_int32]),
     "sfm_match_features": (c_int, [c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                    c_double, c_double, c_double, c_void_p, c_void_p, POINTER(c_int32)]),
     "sfm_knn2_hamming": (c_int, [c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p, c_void_p,

@@ -102,6 +102,36 @@ class BundleAdjuster:
         check(lib().sfm_ba_set_host_comm(self._h, nranks, rank, ctypes.cast(self._host_cb, c_void_p), None),
               "sfm_ba_set_host_comm")
 
+    COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int32, ctypes.POINTER(c_double),
+                                     ctypes.POINTER(c_double), ctypes.c_int64, ctypes.c_int32, c_void_p)
+
+    def set_host_collectives(self, nranks: int, rank: int, allreduce, broadcast, reduce_scatter) -> None:
+        """The host hook with the distributed factor's collectives as well
+        (sfm_ba_set_host_collectives): allreduce(buf, op) and broadcast(buf,
+        root) in place on a float64 array; reduce_scatter(buf, out) with buf
+        holding nranks segments of len(out), this rank's summed segment into
+        out."""
+        def _cb(kind, buf, out, count, arg, user):
+            try:
+                n = int(count)
+                if kind == 2:
+                    reduce_scatter(np.ctypeslib.as_array(buf, (n * nranks,)), np.ctypeslib.as_array(out, (n,)))
+                elif kind == 1:
+                    broadcast(np.ctypeslib.as_array(buf, (n,)), int(arg))
+                else:
+                    allreduce(np.ctypeslib.as_array(buf, (n,)), int(arg))
+                return 0
+            except Exception:
+                return 1
+        self._host_cb = BundleAdjuster.COLLECTIVE_FN(_cb)  # kept alive with the handle
+        check(lib().sfm_ba_set_host_collectives(self._h, nranks, rank, ctypes.cast(self._host_cb, c_void_p), None),
+              "sfm_ba_set_host_collectives")
+
+    def set_distributed_factor(self, panel_tiles: int) -> None:
+        """0: replicated reduced-camera factor (all-reduce of the packed
+        system); k > 0: 1-D block-cyclic panels of k 64-column tiles."""
+        check(lib().sfm_ba_set_distributed_factor(self._h, int(panel_tiles)), "sfm_ba_set_distributed_factor")
+
     # ---- problem ---------------------------------------------------------
     def set_problem(self, uv, cam_idx, pt_idx, K9, rot, t, X) -> None:
         uv, K9, rot, t, X = _f64(uv), _f64(K9), _f64(rot), _f64(t), _f64(X)

@@ -232,4 +232,18 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
 // sentinel_set: y already holds kYSentinel (k_pad_init wrote it)
 void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentinel_set = false);
 
+// ---- distributed factor: 1-D block-cyclic column panels of pt tiles
+// (panel J on rank J % nranks; chol_kernels.hip) ----
+// panel k of the trailing matrix factored in place (L, W_k) by its owner
+int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStream_t s);
+// this rank's panels after k updated with panel k's L
+void launch_panel_update(const DevProblem& d, int k, int pt, int nranks, int rank, hipStream_t s);
+int panel_update_tiles(int nblk, int pt, int k, int nranks, int rank);
+// panel rectangles (columns col0..col1-1, rows c0_J..n) to / from buf at
+// off[J] (device array; nullptr: every panel at off1)
+void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,
+                       double* buf, hipStream_t s);
+// the failure flag into (put) or OR-ed from a broadcast buffer's slot
+void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s);
+
 }  // namespace sfm

@@ -86,7 +86,26 @@ struct sfm_ba_handle {
   // path with several ranks on one GPU, where RCCL allows one rank per GPU)
   sfm_allreduce_fn host_fn = nullptr;
   void* host_user = nullptr;
-  std::vector<double> host_buf;
+  std::vector<double> host_buf, host_buf2;
+  // ... with broadcast and reduce-scatter too (sfm_ba_set_host_collectives);
+  // without it the distributed factor builds both from host_fn's all-reduce
+  sfm_collective_fn coll_fn = nullptr;
+  void* coll_user = nullptr;
+  // distributed reduced-camera factor (sfm_ba_set_distributed_factor): 1-D
+  // block-cyclic column panels of dist_pt 64-column tiles; 0 = every rank
+  // factors the all-reduced system (replicated)
+  int dist_pt = 0;
+  struct DistBufs {
+    int pt = 0, nblk = 0, n = 0, nranks = 0, rank = 0;  // the layout below was made for
+    int64_t seg = 0;                  // per-rank segment of the reduce-scatter (doubles)
+    int64_t bcast_cap = 0;            // largest broadcast (doubles)
+    std::vector<int64_t> count;       // per panel: rectangle doubles
+    double* send = nullptr;           // [nranks][seg]
+    double* recv = nullptr;           // [seg]
+    double* bcast = nullptr;          // [bcast_cap]
+    int64_t* off_send = nullptr;      // [np] panel offset in send (device)
+    int64_t* off_recv = nullptr;      // [np] own panels' offset in recv, -1 others (device)
+  } dist;
   // out-of-place target of the collectives enqueued inside a gated phase of
   // the device LM loop (allreduce below); grown on demand
   double* ar_tmp = nullptr;
@@ -566,6 +585,132 @@ int allreduce(sfm_ba_handle* h, double* buf, size_t count, ncclRedOp_t op) {
   return 0;
 }
 
+// Host-callback collective of kind SFM_COLL_* on device buffers (D2H, the
+// callback, H2D; synchronous).  For a plain all-reduce hook the other two
+// are built from it: a broadcast is the sum of the root's buffer and the
+// others' zeros (exact), a reduce-scatter the all-reduced segments' own.
+int host_collective(sfm_ba_handle* h, int kind, double* buf, double* out, int64_t count, int arg) {
+  const int64_t in_n = kind == SFM_COLL_REDUCE_SCATTER ? count * h->nranks : count;
+  h->host_buf.resize(size_t(in_n));
+  HIPCHK(hipMemcpyAsync(h->host_buf.data(), buf, sizeof(double) * size_t(in_n), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  int rc = 0;
+  double* res = h->host_buf.data();
+  if (h->coll_fn) {
+    if (kind == SFM_COLL_REDUCE_SCATTER) {
+      h->host_buf2.resize(size_t(count));
+      res = h->host_buf2.data();
+    }
+    rc = h->coll_fn(kind, h->host_buf.data(), res, count, arg, h->coll_user);
+  } else if (kind == SFM_COLL_BROADCAST) {
+    if (h->rank != arg) std::fill(h->host_buf.begin(), h->host_buf.end(), 0.0);
+    rc = h->host_fn(h->host_buf.data(), count, 0, h->host_user);
+  } else if (kind == SFM_COLL_REDUCE_SCATTER) {
+    rc = h->host_fn(h->host_buf.data(), in_n, 0, h->host_user);
+    res = h->host_buf.data() + size_t(h->rank) * size_t(count);
+  } else {
+    rc = h->host_fn(h->host_buf.data(), count, arg, h->host_user);
+  }
+  if (rc != 0) return fail(SFM_EIO, "host collective callback failed");
+  HIPCHK(hipMemcpyAsync(kind == SFM_COLL_REDUCE_SCATTER ? out : buf, res, sizeof(double) * size_t(count),
+                        hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int broadcast(sfm_ba_handle* h, double* buf, int64_t count, int root) {
+  if (h->host_fn || h->coll_fn) return host_collective(h, SFM_COLL_BROADCAST, buf, nullptr, count, root);
+  if (!h->comm) return 0;
+  NCCLCHK(ncclBroadcast(buf, buf, size_t(count), ncclDouble, root, h->comm, h->stream));
+  return 0;
+}
+
+int reduce_scatter(sfm_ba_handle* h, double* send, double* recv, int64_t count) {
+  if (h->host_fn || h->coll_fn) return host_collective(h, SFM_COLL_REDUCE_SCATTER, send, recv, count, 0);
+  if (!h->comm) return 0;
+  NCCLCHK(ncclReduceScatter(send, recv, size_t(count), ncclDouble, ncclSum, h->comm, h->stream));
+  return 0;
+}
+
+// The panel layout of the distributed factor and its buffers (remade when
+// the problem size, the panel width or the rank layout changed).
+int dist_prepare(sfm_ba_handle* h) {
+  DevProblem& d = h->d;
+  auto& D = h->dist;
+  const int pt = h->dist_pt;
+  if (D.send && D.pt == pt && D.nblk == d.nblk && D.n == d.n && D.nranks == h->nranks && D.rank == h->rank) return 0;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (void* p : {static_cast<void*>(D.send), static_cast<void*>(D.recv), static_cast<void*>(D.bcast),
+                  static_cast<void*>(D.off_send), static_cast<void*>(D.off_recv)})
+    if (p) (void)hipFree(p);
+  D = sfm_ba_handle::DistBufs();
+  const int np = (d.nblk + pt - 1) / pt, N = h->nranks;
+  std::vector<int64_t> local(static_cast<size_t>(np)), tot(static_cast<size_t>(N), 0);
+  D.count.assign(size_t(np), 0);
+  for (int J = 0; J < np; ++J) {
+    const int c0 = J * pt * kNB, c1 = std::min((J + 1) * pt * kNB, d.n + 1);
+    D.count[J] = c1 > c0 ? int64_t(c1 - c0) * (d.n + 1 - c0) : 0;
+    local[J] = tot[J % N];
+    tot[J % N] += D.count[J];
+    D.bcast_cap = std::max<int64_t>(D.bcast_cap, D.count[J] + int64_t(pt) * kNB * kNB + 1);
+  }
+  D.seg = std::max<int64_t>(1, *std::max_element(tot.begin(), tot.end()));
+  std::vector<int64_t> os(static_cast<size_t>(np)), orv(static_cast<size_t>(np));
+  for (int J = 0; J < np; ++J) {
+    os[J] = int64_t(J % N) * D.seg + local[J];
+    orv[J] = J % N == h->rank ? local[J] : -1;
+  }
+  auto grab = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
+  if (!grab(reinterpret_cast<void**>(&D.send), sizeof(double) * size_t(D.seg) * N) ||
+      !grab(reinterpret_cast<void**>(&D.recv), sizeof(double) * size_t(D.seg)) ||
+      !grab(reinterpret_cast<void**>(&D.bcast), sizeof(double) * size_t(D.bcast_cap)) ||
+      !grab(reinterpret_cast<void**>(&D.off_send), sizeof(int64_t) * np) ||
+      !grab(reinterpret_cast<void**>(&D.off_recv), sizeof(int64_t) * np))
+    return fail(SFM_ENOMEM, "hipMalloc failed (distributed factor buffers)");
+  HIPCHK(hipMemcpy(D.off_send, os.data(), sizeof(int64_t) * np, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(D.off_recv, orv.data(), sizeof(int64_t) * np, hipMemcpyHostToDevice));
+  HIPCHK(hipMemsetAsync(D.send, 0, sizeof(double) * size_t(D.seg) * N, h->stream));
+  D.pt = pt; D.nblk = d.nblk; D.n = d.n; D.nranks = N; D.rank = h->rank;
+  return 0;
+}
+
+// The reduced camera system's factor, distributed:
+// reduce-scatter of the ranks' partial systems into block-cyclic column
+// panels; per panel k its owner factors it and broadcasts L (+ its W_k
+// tiles and failure bits), every rank applies it to its own later panels;
+// then every rank holds the whole factor and back-substitutes (replicated).
+int dist_factor_enqueue(sfm_ba_handle* h) {
+  DevProblem& d = h->d;
+  hipStream_t s = h->stream;
+  int rc;
+  if ((rc = dist_prepare(h))) return rc;
+  auto& D = h->dist;
+  const int pt = D.pt, N = h->nranks, np = int(D.count.size());
+  launch_panel_copy(d, true, pt, 0, d.n + 1, D.off_send, 0, D.send, s);
+  if ((rc = reduce_scatter(h, D.send, D.recv, D.seg))) return rc;
+  launch_panel_copy(d, false, pt, 0, d.n + 1, D.off_recv, 0, D.recv, s);
+  for (int k = 0; k < np; ++k) {
+    const int owner = k % N, t0 = k * pt, ncols = std::min(pt, d.nblk - t0);
+    const int c0 = t0 * kNB, c1 = c0 + ncols * kNB;
+    const int64_t nw = int64_t(ncols) * kNB * kNB, cnt = D.count[k] + nw + 1;
+    double* wt = D.bcast + D.count[k];
+    if (h->rank == owner) {
+      launch_cholesky_panel(d, k, pt, ++h->chol_epoch, s);
+      launch_panel_copy(d, true, pt, c0, c1, nullptr, 0, D.bcast, s);
+      HIPCHK(hipMemcpyAsync(wt, d.invL + size_t(t0) * kNB * kNB, sizeof(double) * size_t(nw), hipMemcpyDeviceToDevice, s));
+      launch_fail_slot(d, true, wt + nw, s);
+    }
+    if (N > 1 && (rc = broadcast(h, D.bcast, cnt, owner))) return rc;
+    if (h->rank != owner) {
+      launch_panel_copy(d, false, pt, c0, c1, nullptr, 0, D.bcast, s);
+      HIPCHK(hipMemcpyAsync(d.invL + size_t(t0) * kNB * kNB, wt, sizeof(double) * size_t(nw), hipMemcpyDeviceToDevice, s));
+      launch_fail_slot(d, false, wt + nw, s);
+    }
+    launch_panel_update(d, k, pt, N, h->rank, s);
+  }
+  return 0;
+}
+
 // D2H of the scalar block + stream sync.
 int fetch_scalars(sfm_ba_handle* h) {
   HIPCHK(hipMemcpyAsync(h->d.scal_host, h->d.scal, sizeof(double) * (kNumScalars + 1), hipMemcpyDeviceToHost,
@@ -743,18 +888,24 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
     mark_begin(h, kPhSchur);
     launch_schur(d, radius, h->rank == 0, s);
     mark_end(h);
-    if (sharded(h) || h->force_pack) {
-      // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
-      launch_pack_upper(d, false, s);
-      if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
-      launch_pack_upper(d, true, s);
-    }
     // (k_schur_diag_sum also wrote the identity padding, y's sentinel and
     // the cleared failure flag; without cameras the separate launch does)
     if (!d.C) launch_pad_init(d, s);
-    mark_begin(h, kPhChol);
-    cam_done = launch_cholesky(d, ++h->chol_epoch, s, false, h->rank == 0 ? 1 : 0);
-    mark_end(h);
+    if (sharded(h) && h->dist_pt > 0) {
+      mark_begin(h, kPhChol);
+      if ((rc = dist_factor_enqueue(h))) return rc;
+      mark_end(h);
+    } else {
+      if (sharded(h) || h->force_pack) {
+        // all-reduce only the packed upper triangle + rhs (half the ld^2 image)
+        launch_pack_upper(d, false, s);
+        if ((rc = allreduce(h, d.Spack, packed_size(d.n), ncclSum))) return rc;
+        launch_pack_upper(d, true, s);
+      }
+      mark_begin(h, kPhChol);
+      cam_done = launch_cholesky(d, ++h->chol_epoch, s, false, h->rank == 0 ? 1 : 0);
+      mark_end(h);
+    }
     mark_begin(h, kPhBack);
     launch_backsolve(d, ++h->bs_epoch, s, true);
     mark_end(h);
@@ -1032,6 +1183,10 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->lm_trace) hipFree(h->lm_trace);
   if (h->stage) hipHostFree(h->stage);
   if (h->ar_tmp) hipFree(h->ar_tmp);
+  for (void* p : {static_cast<void*>(h->dist.send), static_cast<void*>(h->dist.recv),
+                  static_cast<void*>(h->dist.bcast), static_cast<void*>(h->dist.off_send),
+                  static_cast<void*>(h->dist.off_recv)})
+    if (p) hipFree(p);
   if (h->stream2) {
     hipStreamSynchronize(h->stream2);
     hipStreamDestroy(h->stream2);
@@ -1058,6 +1213,7 @@ int sfm_ba_set_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, const uint8_
   HIPCHK(hipSetDevice(h->device));
   if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
   h->host_fn = nullptr;
+  h->coll_fn = nullptr;
   h->nranks = nranks;
   h->rank = rank;
   // a one-rank communicator is created too: it runs every collective of the
@@ -1077,6 +1233,34 @@ int sfm_ba_set_host_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_all
   h->rank = rank;
   h->host_fn = fn;
   h->host_user = user;
+  h->coll_fn = nullptr;
+  h->coll_user = nullptr;
+  return 0;
+}
+
+// An all-reduce hook built from the general one (kind SFM_COLL_ALLREDUCE).
+namespace {
+int coll_as_allreduce(double* buf, int64_t count, int32_t op, void* user) {
+  auto* h = static_cast<sfm_ba_handle*>(user);
+  return h->coll_fn(SFM_COLL_ALLREDUCE, buf, buf, count, op, h->coll_user);
+}
+}  // namespace
+
+int sfm_ba_set_host_collectives(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_collective_fn fn, void* user) {
+  if (!h || nranks < 1 || rank < 0 || rank >= nranks || !fn) return fail(SFM_EINVAL, "bad communicator arguments");
+  if (h->comm) { ncclCommDestroy(h->comm); h->comm = nullptr; }
+  h->nranks = nranks;
+  h->rank = rank;
+  h->coll_fn = fn;
+  h->coll_user = user;
+  h->host_fn = coll_as_allreduce;  // the sharded path's all-reduces
+  h->host_user = h;
+  return 0;
+}
+
+int sfm_ba_set_distributed_factor(sfm_ba_handle* h, int32_t panel_tiles) {
+  if (!h || panel_tiles < 0 || panel_tiles > 64) return fail(SFM_EINVAL, "panel_tiles must be in [0, 64]");
+  h->dist_pt = panel_tiles;
   return 0;
 }
 
@@ -1649,7 +1833,10 @@ int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32
   if (mode == SFM_BA_STRUCT_ONLY && d.C) HIPCHK(hipMemsetAsync(d.scale_c, 0, sizeof(double) * 6 * d.C, h->stream));
   if (mode == SFM_BA_POSE_ONLY && d.P) HIPCHK(hipMemsetAsync(d.scale_p, 0, sizeof(double) * 3 * d.P, h->stream));
   double* sc = d.scal_host;
-  if (!h->host_fn && !env_flag("SFM_HOST_LM")) {
+  // (the distributed factor's panel loop runs in the host-driven loop: its
+  // collectives are not gated; at the sizes it is for, a host round trip per
+  // phase is noise)
+  if (!h->host_fn && !h->coll_fn && !(sharded(h) && h->dist_pt > 0) && !env_flag("SFM_HOST_LM")) {
     // the same loop with its decisions on the device (k_lm_init /
     // k_lm_decide / k_lm_post): the initial evaluation and the iterations
     // are enqueued in batches, one host synchronisation per batch instead

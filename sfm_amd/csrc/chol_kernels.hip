@@ -295,9 +295,9 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
-      if (w == 3 && pf_sub != nullptr)
+      if (w == 3 && pf_sub != nullptr)  // (pf_diag nullptr: a panel's last column, no next diagonal tile)
         *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+               (pf_diag == nullptr || __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
     }
     __syncthreads();
     // ---- trailing update of column block b+1 (the next panel's); the
@@ -682,9 +682,11 @@ __host__ __device__ __forceinline__ int col_tasks(int nb, int j) {
   const int m = nb - j;
   return m <= 2 ? m : 3 + (m - 3) / 2 + ((m - 3) & 1);
 }
-__host__ __device__ __forceinline__ int chol_tasks(int nb) {
+// (ncols < nb: a column panel -- the first ncols tile columns of an nb-row
+// trailing matrix, finished as L; the tiles right of it are not touched)
+__host__ __device__ __forceinline__ int chol_tasks(int nb, int ncols) {
   int s = 0;
-  for (int j = 0; j < nb; ++j) s += col_tasks(nb, j);
+  for (int j = 0; j < ncols; ++j) s += col_tasks(nb, j);
   return s;
 }
 
@@ -737,7 +739,8 @@ __device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
-__device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, double* __restrict__ Winv,
+__device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, int ncols,
+                             double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
                              double* Ls, double (*scr)[256], int* rdy, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -749,7 +752,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
     nx[q] = A[size_t(c) * ld + r];
   }
-  for (int j = 0; j < nb; ++j) {
+  for (int j = 0; j < ncols; ++j) {
     const int j0 = j * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -767,10 +770,11 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       block_publish_wt(F + j * nb + j - 1, epoch);
     }
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
-    const bool more = j + 1 < nb;
+    const bool more = j + 1 < nb;      // a tile below the diagonal
+    const bool next = j + 1 < ncols;   // ... and the walker's next diagonal tile (a panel ends before it)
     const int i0 = j0 + NB;
     const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
-    const int* fdiag = more ? Pf + (j + 1) * nb + j + 1 : nullptr;
+    const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : nullptr;
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
                                     : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
     if (bad) atomicOr(fail, 1);
@@ -782,7 +786,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       for (int q = 0; q < 16; ++q) {
         const int e = t + 256 * q, c = e >> 6, r = e & 63;
         sub[q] = A[size_t(j0 + c) * ld + i0 + r];
-        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        if (next) nx[q] = A[size_t(i0 + c) * ld + i0 + r];
       }
     }
     double* Wk = Winv + size_t(j) * NB * NB;
@@ -823,11 +827,13 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       // the poll missed: wait for the partial tiles here
       block_wait(Pf + (j + 1) * nb + j, epoch, fail);
       load_tile(T, A, ld, i0, j0);
-      block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
+      if (next) {
+        block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        for (int q = 0; q < 16; ++q) {
+          const int e = t + 256 * q, c = e >> 6, r = e & 63;
+          nx[q] = A[size_t(i0 + c) * ld + i0 + r];
+        }
       }
     }
     // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
@@ -840,13 +846,22 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
       st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
     }
+    if (!next) {
+      // a panel's last column: L_j+1,j is final (no next step publishes it)
+      block_publish_wt(F + (j + 1) * nb + j, epoch);
+      break;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb,
+// ncols < nb: one column panel of a distributed factor (launch_cholesky_panel);
+// tepoch: the ticket epoch (the flag epoch `epoch` for a whole factor; 1 for
+// a panel, whose tickets are zeroed before its launch -- its task count
+// differs from panel to panel)
+__global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb, int ncols,
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
-                                                    int epoch, int nhelp, int* __restrict__ fail,
+                                                    int epoch, int tepoch, int nhelp, int* __restrict__ fail,
                                                     const int* __restrict__ gate, const int* __restrict__ tile_cnt,
                                                     const int* __restrict__ tile_exp) {
   __shared__ double T[NB * TS];
@@ -859,7 +874,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
     // (epoch - 1) (ntask + nhelp) and (epoch - 1) (1 + nhelp)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      atomicAdd(ticket, (unsigned long long)(chol_tasks(nb) + nhelp));
+      atomicAdd(ticket, (unsigned long long)(chol_tasks(nb, ncols) + nhelp));
       atomicAdd(ticket + 1, (unsigned long long)(1 + nhelp));
     }
     return;
@@ -872,18 +887,18 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     const unsigned long long v = atomicAdd(ticket + 1, threadIdx.x == 0 ? 1ULL : 0ULL);
     const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
     const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
-    sh[1] = int(((unsigned long long)hi << 32 | lo) - (unsigned long long)(epoch - 1) * (unsigned long long)(1 + nhelp));
+    sh[1] = int(((unsigned long long)hi << 32 | lo) - (unsigned long long)(tepoch - 1) * (unsigned long long)(1 + nhelp));
   }
   __syncthreads();
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker(A, ld, n, nb, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
+    fused_walker(A, ld, n, nb, ncols, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
     return;
   }
-  const int ntask = chol_tasks(nb);
+  const int ntask = chol_tasks(nb, ncols);
   // every launch takes exactly ntask + nhelp tickets (one failing grab per helper)
-  const unsigned long long base = (unsigned long long)(epoch - 1) * (unsigned long long)(ntask + nhelp);
+  const unsigned long long base = (unsigned long long)(tepoch - 1) * (unsigned long long)(ntask + nhelp);
   while (true) {
     if (wave0()) {
       // one increment per wave (lane 0 adds 1, the others 0); every lane
@@ -1121,6 +1136,114 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
   }
 }
 
+// ---------------------------------------------------------------------------
+// Distributed factor (1-D block-cyclic column panels over the ranks; see
+// DESIGN.md §7).  Panel J = tile columns [pt J, pt J + pt); rank J % N owns
+// it.  Per panel k: its owner factors it (k_chol_fused with ncols = pt on
+// the trailing matrix), every rank receives it by broadcast and applies it
+// to its own later panels (k_panel_update), so at the end every rank holds
+// the whole L (and every W_k) and the back substitution runs replicated.
+
+// Own tile columns after panel k, in order: panels j = k+1.. with
+// j % nranks == rank, tile columns [pt j, min(pt j + pt, nblk)); column jt
+// holds the nblk - jt tiles (jt .. nblk-1, jt).
+__device__ __forceinline__ bool panel_task(int task, int nblk, int pt, int k, int nranks, int rank, int* it, int* jt) {
+  int j = k + 1 + ((rank - (k + 1)) % nranks + nranks) % nranks;
+  for (; j * pt < nblk; j += nranks) {
+    for (int c = j * pt; c < min(j * pt + pt, nblk); ++c) {
+      const int cnt = nblk - c;
+      if (task < cnt) {
+        *jt = c;
+        *it = c + task;
+        return true;
+      }
+      task -= cnt;
+    }
+  }
+  return false;
+}
+
+// S tile (it, jt) -= L_it,k L_jt,k^T over panel k's columns [kc0, kc0 + kw):
+// one tile per workgroup, wave w the 32x32 quadrant (c in cb.., r in rb..)
+// accumulated transposed as in fused_helper_tile (the strictly upper
+// quadrant of a diagonal tile is skipped: never read).  Every tile keeps its
+// k order (the panel's columns ascending), the order the single-GPU factor
+// applies them in.
+__global__ __launch_bounds__(256) void k_panel_update(double* __restrict__ A, int ld, int nblk, int pt, int k,
+                                                      int kc0, int kw, int nranks, int rank) {
+  int it = 0, jt = 0;
+  if (!panel_task(blockIdx.x, nblk, pt, k, nranks, rank, &it, &jt)) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
+  const int lr = lane & 15, lk = lane >> 4;
+  const int i0 = it * NB, j0 = jt * NB;
+  if (it == jt && cb > rb) return;  // wave-uniform; no barrier in this kernel
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) acc[a][bb] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = kc0; k0 < kc0 + kw; k0 += NB) {
+    double xa[2][16], yb[2][16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const size_t colbase = size_t(k0 + 4 * ks + lk) * ld;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) xa[a][ks] = A[colbase + j0 + cb + 16 * a + lr];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) yb[bb][ks] = A[colbase + i0 + rb + 16 * bb + lr];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+          acc[a][bb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a][ks], yb[bb][ks], acc[a][bb], 0, 0, 0);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        double* q = A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr;
+        *q -= acc[a][bb][reg];
+      }
+}
+
+// Panel rectangles <-> a contiguous buffer: column c (c0_J <= c < c1_J of
+// panel J, c <= n) rows [c0_J, n] at buf + off[J] + (c - c0_J)(n + 1 - c0_J)
+// (off[J] < 0: panel J skipped).  One workgroup per column.  Rows beyond n
+// (identity padding, zero in every real column) and columns beyond n never
+// travel: every rank writes them itself (k_schur_diag_sum).
+template <bool kPack>
+__global__ __launch_bounds__(256) void k_panel_copy(double* __restrict__ A, int ld, int n, int pcols, int col0,
+                                                    const int64_t* __restrict__ off, int64_t off1,
+                                                    double* __restrict__ buf) {
+  const int c = col0 + blockIdx.x;
+  const int J = c / pcols, c0 = J * pcols;
+  const int64_t o = off ? off[J] : off1;
+  if (o < 0) return;
+  const int rows = n + 1 - c0;
+  double* b = buf + o + int64_t(c - c0) * rows;
+  double* col = A + size_t(c) * ld + c0;
+  for (int r = threadIdx.x; r < rows; r += 256) {
+    if (kPack) b[r] = col[r];
+    else col[r] = b[r];
+  }
+}
+
+// A broadcast panel's tail: its failure bits (one double slot) OR-ed into
+// this rank's flag.
+__global__ void k_fail_or(const double* __restrict__ slot, int* __restrict__ fail) {
+  const int v = int(__builtin_bit_cast(uint64_t, *slot) & 0x7fffffffu);
+  if (v) atomicOr(fail, v);
+}
+__global__ void k_fail_put(const int* __restrict__ fail, double* __restrict__ slot) {
+  *slot = __builtin_bit_cast(double, uint64_t(uint32_t(*fail)));
+}
+
 }  // namespace
 
 bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int cam_step, int overlap) {
@@ -1140,7 +1263,7 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
                                    part + size_t(kPBadCam) * d.max_blocks);
     return fold;
   }
-  const int nb = d.nblk, ntask = chol_tasks(nb);
+  const int nb = d.nblk, ntask = chol_tasks(nb, nb);
   // one persistent workgroup per CU (roles by start order: a partly resident
   // grid still finishes)
   // (SFM_CHOL_HELPERS: a smaller helper grid, for measurements)
@@ -1155,8 +1278,8 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int cap = helpers_env > 0 ? std::min(helpers_env, full) : full;
   const int nhelp = std::max(1, std::min(ntask, cap));
   const int* tc = overlap ? d.tile_cnt : nullptr;
-  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb, d.cticket,
-                                         epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
+  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
+                                         d.cticket, epoch, epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
   return false;
 }
 
@@ -1172,6 +1295,49 @@ void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentin
   if (!sentinel_set)
     (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.ysol), int(kYSentinelWord), size_t(nb_real) * NB * 2, s);
   k_backsolve<<<nb_real, 256, 0, s>>>(d.S, d.ld, d.n, nb_real, d.invL, d.ysol, d.fail, d.gate, d.cticket + 2, epoch);
+}
+
+int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStream_t s) {
+  const int t0 = k * pt, nb = d.nblk - t0, ncols = std::min(pt, nb);
+  if (ncols <= 0) return 0;
+  const int c0 = t0 * NB;
+  const int ntask = chol_tasks(nb, ncols);
+  const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
+  // the panel's own tickets (ntask differs per panel): zeroed, ticket epoch 1
+  (void)hipMemsetAsync(d.cticket + 3, 0, 2 * sizeof(unsigned long long), s);
+  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S + size_t(c0) * d.ld + c0, d.ld, d.n - c0, nb, ncols,
+                                         d.invL + size_t(t0) * NB * NB, d.cflags, d.cflags + size_t(nb) * nb,
+                                         d.cticket + 3, epoch, 1, nhelp, d.fail, nullptr, nullptr, nullptr);
+  return 0;
+}
+
+int panel_update_tiles(int nblk, int pt, int k, int nranks, int rank) {
+  int n = 0;
+  for (int j = k + 1; j * pt < nblk; ++j) {
+    if (j % nranks != rank) continue;
+    for (int c = j * pt; c < std::min(j * pt + pt, nblk); ++c) n += nblk - c;
+  }
+  return n;
+}
+
+void launch_panel_update(const DevProblem& d, int k, int pt, int nranks, int rank, hipStream_t s) {
+  const int tiles = panel_update_tiles(d.nblk, pt, k, nranks, rank);
+  if (tiles <= 0) return;
+  const int kc0 = k * pt * NB, kw = std::min(pt, d.nblk - k * pt) * NB;
+  k_panel_update<<<tiles, 256, 0, s>>>(d.S, d.ld, d.nblk, pt, k, kc0, kw, nranks, rank);
+}
+
+void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,
+                       double* buf, hipStream_t s) {
+  col1 = std::min(col1, d.n + 1);
+  if (col1 <= col0) return;
+  if (pack) k_panel_copy<true><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
+  else k_panel_copy<false><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
+}
+
+void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s) {
+  if (put) k_fail_put<<<1, 1, 0, s>>>(d.fail, slot);
+  else k_fail_or<<<1, 1, 0, s>>>(slot, d.fail);
 }
 
 }  // namespace sfm
