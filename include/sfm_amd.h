@@ -378,6 +378,16 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
  * STREAM-copy bandwidth (read + write bytes / s, 16-B accesses) over a few
  * launch shapes, `bytes` per buffer, `reps` timed launches each. */
 int sfm_bench_stream_copy(int32_t device, int64_t bytes, int32_t reps, double* best_gbs);
+/* Measurement plumbing (tools/dist_factor_model.py): the device work of
+ * the distributed factor (sfm_ba_set_distributed_factor) of an n x n system
+ * at nranks ranks, each rank's share timed on this one GPU (no collective
+ * runs; the broadcasts' bytes are the model's).  Per panel k (np panels):
+ * fac_ms[k] its owner's factor, pack_ms[k] the owner's pack of it,
+ * unpack_ms[k] a receiver's unpack, upd_ms[r * np + k] rank r's updates of
+ * its later panels; misc_ms[5] = reduce-scatter pack, unpack, the back
+ * substitution, failure bits, panel-image doubles. */
+int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t panel_tiles, double* fac_ms,
+                            double* pack_ms, double* unpack_ms, double* upd_ms, double* misc_ms);
 
 /* ---- Pyramidal Lucas-Kanade tracker -------------- */
 typedef struct sfm_klt_params {

@@ -179,6 +179,8 @@ _SIGNATURES = {
     "sfm_dense_spd_solve": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double),
                                     POINTER(c_int32)]),
     "sfm_bench_stream_copy": (c_int, [c_int32, c_int64, c_int32, POINTER(c_double)]),
+    "sfm_dist_factor_profile": (c_int, [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
     "sfm_klt_default_params": (None, [POINTER(KLTParams)]),
     "sfm_klt_create": (c_int, [c_int32, c_int32, c_int32, POINTER(KLTParams), POINTER(c_void_p)]),
     "sfm_klt_destroy": (c_int, [c_void_p]),

@@ -126,8 +126,9 @@ struct DevProblem {
                               //     4: Cholesky tile hand-off timeout
   int32_t* flags = nullptr;   // [nblk] back-substitution hand-off flags (epoch-stamped)
   int32_t* cflags = nullptr;  // [2][nblk][nblk] fused Cholesky: final (F) and partial (P) tile flags
-  unsigned long long* cticket = nullptr;  // [3] fused Cholesky tile ticket, its walker-role ticket, the back
-                                          // substitution's row ticket (all monotone across launches)
+  unsigned long long* cticket = nullptr;  // [5] fused Cholesky tile ticket, its walker-role ticket, the back
+                                          // substitution's row ticket (all monotone across launches); a
+                                          // distributed factor panel's two (zeroed per panel)
   int32_t n_cu = 0;           // compute units (co-residency bound of the persistent grids)
   // LM diagonal clamp of the running solve (sfm_ba_options min/max_lm_diagonal)
   double min_diag = 1e-6, max_diag = 1e32;
@@ -245,5 +246,7 @@ void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col
                        double* buf, hipStream_t s);
 // the failure flag into (put) or OR-ed from a broadcast buffer's slot
 void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s);
+// a diagonally dominant augmented system (timing of the distributed factor)
+void launch_spd_fill(double* A, int ld, int n, unsigned seed, hipStream_t s);
 
 }  // namespace sfm

@@ -1660,7 +1660,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   ALLOC(d.invL, size_t(d.nblk) * kNB * kNB);
   ALLOC(d.flags, size_t(d.nblk));
   ALLOC(d.cflags, 2 * size_t(d.nblk) * d.nblk);
-  ALLOC(d.cticket, 3);  // task ticket, walker-role ticket, back-substitution role ticket
+  ALLOC(d.cticket, 5);  // task ticket, walker-role ticket, back-substitution role ticket, a panel's two
   // Schur / Cholesky overlap (SFM_OVERLAP=1; unsharded, more than two tiles):
   // per 64x64 tile of S the number of camera blocks (c1 <= c2, stored at
   // rows 6 c2.., columns 6 c1..) whose 6x6 footprint touches it
@@ -1719,7 +1719,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     fs.add(d.invL, sizeof(double) * size_t(d.nblk) * kNB * kNB, 0);
     fs.add(d.flags, sizeof(int32_t) * size_t(d.nblk), 0);
     fs.add(d.cflags, sizeof(int32_t) * 2 * size_t(d.nblk) * d.nblk, 0);
-    fs.add(d.cticket, 3 * sizeof(unsigned long long), 0);
+    fs.add(d.cticket, 5 * sizeof(unsigned long long), 0);
     fs.add(d.partials, sizeof(double) * size_t(kNumPartialSlots) * d.max_blocks, 0);
     launch_fill32(fs, s);
   }
@@ -2067,6 +2067,115 @@ int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
   return 0;
 }
 
+int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t panel_tiles, double* fac_ms,
+                            double* pack_ms, double* unpack_ms, double* upd_ms, double* misc_ms) {
+  if (n <= 0 || nranks < 1 || panel_tiles < 1 || !fac_ms || !pack_ms || !unpack_ms || !upd_ms || !misc_ms)
+    return fail(SFM_EINVAL, "bad arguments");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return fail(SFM_ENODEV, "no device");
+  HIPCHK(hipSetDevice(device));
+  DevProblem d;
+  d.n = n;
+  d.ld = ((n + 1 + kNB - 1) / kNB) * kNB;
+  d.nblk = d.ld / kNB;
+  const int pt = panel_tiles, np = (d.nblk + pt - 1) / pt;
+  const size_t bytes = sizeof(double) * size_t(d.ld) * d.ld;
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreate(&s));
+  double *S = nullptr, *invd = nullptr, *ys = nullptr, *buf = nullptr;
+  int *fl = nullptr, *flags = nullptr;
+  const size_t nflag = d.nblk + 2 * size_t(d.nblk) * d.nblk + 16;
+  HIPCHK(hipMalloc(&S, bytes));
+  HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
+  HIPCHK(hipMemset(invd, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB));
+  HIPCHK(hipMalloc(&flags, sizeof(int) * nflag));
+  HIPCHK(hipMemset(flags, 0, sizeof(int) * nflag));
+  HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
+  HIPCHK(hipMalloc(&fl, sizeof(int)));
+  HIPCHK(hipMemset(fl, 0, sizeof(int)));
+  // one panel rectangle (the broadcast buffer) / the whole lower image (the
+  // reduce-scatter's send buffer)
+  HIPCHK(hipMalloc(&buf, bytes));
+  HIPCHK(hipMemset(buf, 0, bytes));
+  d.S = S; d.invL = invd; d.ysol = ys; d.fail = fl; d.flags = flags;
+  d.cflags = flags + d.nblk;
+  d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk);
+  if (reinterpret_cast<uintptr_t>(d.cticket) % 8) d.cticket = reinterpret_cast<unsigned long long*>(flags + d.nblk + 2 * size_t(d.nblk) * d.nblk + 1);
+  d.n_cu = device_cus(device);
+  std::vector<hipEvent_t> ev(4 * size_t(np) + 8);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  auto el = [&](hipEvent_t a, hipEvent_t b) {
+    float m = 0.f;
+    (void)hipEventElapsedTime(&m, a, b);
+    return double(m);
+  };
+  // offsets of every panel in a whole-image buffer (the reduce-scatter pack)
+  std::vector<int64_t> off(static_cast<size_t>(np));
+  int64_t tot = 0;
+  for (int J = 0; J < np; ++J) {
+    off[J] = tot;
+    const int c0 = J * pt * kNB, c1 = std::min((J + 1) * pt * kNB, n + 1);
+    tot += c1 > c0 ? int64_t(c1 - c0) * (n + 1 - c0) : 0;
+  }
+  int64_t* doff = nullptr;
+  HIPCHK(hipMalloc(&doff, sizeof(int64_t) * np));
+  HIPCHK(hipMemcpy(doff, off.data(), sizeof(int64_t) * np, hipMemcpyHostToDevice));
+  int epoch = 0;
+  for (int rank = 0; rank < nranks; ++rank) {
+    launch_spd_fill(S, d.ld, n, 12345u, s);
+    if (rank == 0) {  // reduce-scatter pack + unpack of the whole image, the back substitution
+      HIPCHK(hipEventRecord(ev[0], s));
+      launch_panel_copy(d, true, pt, 0, n + 1, doff, 0, buf, s);
+      HIPCHK(hipEventRecord(ev[1], s));
+      launch_panel_copy(d, false, pt, 0, n + 1, doff, 0, buf, s);
+      HIPCHK(hipEventRecord(ev[2], s));
+    }
+    for (int k = 0; k < np; ++k) {
+      const int owner = k % nranks, t0 = k * pt, ncols = std::min(pt, d.nblk - t0);
+      const int c0 = t0 * kNB, c1 = c0 + ncols * kNB;
+      HIPCHK(hipEventRecord(ev[8 + 4 * k], s));
+      if (owner == rank) {
+        launch_cholesky_panel(d, k, pt, ++epoch, s);
+        HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
+        launch_panel_copy(d, true, pt, c0, c1, nullptr, tot, buf, s);
+      } else {
+        // (from the owner's last packed L, or zeros: every pivot stays positive)
+        HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
+        launch_panel_copy(d, false, pt, c0, c1, nullptr, tot, buf, s);
+      }
+      HIPCHK(hipEventRecord(ev[8 + 4 * k + 2], s));
+      launch_panel_update(d, k, pt, nranks, rank, s);
+      HIPCHK(hipEventRecord(ev[8 + 4 * k + 3], s));
+    }
+    if (rank == 0) {
+      HIPCHK(hipMemsetAsync(ys, 0xFF, sizeof(double) * d.ld, s));
+      HIPCHK(hipEventRecord(ev[3], s));
+      launch_backsolve(d, 1, s);
+      HIPCHK(hipEventRecord(ev[4], s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    for (int k = 0; k < np; ++k) {
+      const bool own = k % nranks == rank;
+      if (own) fac_ms[k] = el(ev[8 + 4 * k], ev[8 + 4 * k + 1]);
+      (own ? pack_ms : unpack_ms)[k] = el(ev[8 + 4 * k + 1], ev[8 + 4 * k + 2]);
+      upd_ms[size_t(rank) * np + k] = el(ev[8 + 4 * k + 2], ev[8 + 4 * k + 3]);
+    }
+    if (rank == 0) {
+      misc_ms[0] = el(ev[0], ev[1]);  // reduce-scatter pack
+      misc_ms[1] = el(ev[1], ev[2]);  // unpack
+      misc_ms[2] = el(ev[3], ev[4]);  // back substitution
+    }
+  }
+  int f = 0;
+  HIPCHK(hipMemcpy(&f, fl, sizeof(int), hipMemcpyDeviceToHost));
+  misc_ms[3] = f;
+  misc_ms[4] = double(tot);  // doubles of the whole panel image
+  for (auto e : ev) hipEventDestroy(e);
+  hipFree(S); hipFree(invd); hipFree(flags); hipFree(ys); hipFree(fl); hipFree(buf); hipFree(doff);
+  hipStreamDestroy(s);
+  return 0;
+}
+
 int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double* b, double* y, int32_t reps,
                         double* ms, int32_t* chol_fail) {
   if (n <= 0 || !A || !b || !y || reps < 1) return fail(SFM_EINVAL, "bad arguments");
@@ -2092,8 +2201,8 @@ int sfm_dense_spd_solve(int32_t device, int32_t n, const double* A, const double
   HIPCHK(hipMalloc(&S0, bytes));
   HIPCHK(hipMalloc(&invd, sizeof(double) * size_t(d.nblk) * kNB * kNB));
   HIPCHK(hipMemset(invd, 0, sizeof(double) * size_t(d.nblk) * kNB * kNB));
-  HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 8)));
-  HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 8)));
+  HIPCHK(hipMalloc(&flags, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 16)));
+  HIPCHK(hipMemset(flags, 0, sizeof(int) * (d.nblk + 2 * size_t(d.nblk) * d.nblk + 16)));
   HIPCHK(hipMalloc(&ys, sizeof(double) * d.ld));
   HIPCHK(hipMalloc(&fl, sizeof(int)));
   HIPCHK(hipMemcpy(S0, img.data(), bytes, hipMemcpyHostToDevice));

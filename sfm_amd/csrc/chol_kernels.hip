@@ -1244,6 +1244,23 @@ __global__ void k_fail_put(const int* __restrict__ fail, double* __restrict__ sl
   *slot = __builtin_bit_cast(double, uint64_t(uint32_t(*fail)));
 }
 
+// A diagonally dominant (so SPD) augmented system made on the device, for
+// the distributed factor's component timing (sfm_dist_factor_profile): the
+// timings do not depend on the values, a 12000^2 host matrix would cost
+// seconds to make and upload.
+__global__ void k_spd_fill(double* __restrict__ A, int ld, int n, unsigned seed) {
+  const int j = blockIdx.x;
+  for (int i = threadIdx.x; i < ld; i += blockDim.x) {
+    uint64_t z = (uint64_t(seed) << 40) ^ (uint64_t(j) * 0x9E3779B97F4A7C15ull) ^ (uint64_t(i) * 0xBF58476D1CE4E5B9ull);
+    z ^= z >> 31; z *= 0x94D049BB133111EBull; z ^= z >> 29;
+    const double u = double(z >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+    double v = 0.0;
+    if (j < n) v = i < j ? 0.0 : (i == j ? 1.0 + 0.5 * n : (i <= n ? u : 0.0));
+    else v = i == j ? 1.0 : 0.0;
+    A[size_t(j) * ld + i] = v;
+  }
+}
+
 }  // namespace
 
 bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_fail, int cam_step, int overlap) {
@@ -1338,6 +1355,10 @@ void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col
 void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s) {
   if (put) k_fail_put<<<1, 1, 0, s>>>(d.fail, slot);
   else k_fail_or<<<1, 1, 0, s>>>(slot, d.fail);
+}
+
+void launch_spd_fill(double* A, int ld, int n, unsigned seed, hipStream_t s) {
+  k_spd_fill<<<ld, 256, 0, s>>>(A, ld, n, seed);
 }
 
 }  // namespace sfm

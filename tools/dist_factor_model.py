@@ -1,0 +1,167 @@
+"""Predicted C4 strong-scaling curve (BASELINE config 4) of the two multi-GPU
+designs, from parts MEASURED on one MI355X:
+
+* the replicated design: every rank factors the all-reduced 12000^2 system
+  (its factor time is the measured single-GPU one);
+* the distributed design (sfm_ba_set_distributed_factor): reduce-scatter into
+  1-D block-cyclic panels, per panel the owner's factor + broadcast, every
+  rank's updates of its own later panels.  Each rank's device work at N ranks
+  is timed on this GPU by sfm_dist_factor_profile (per panel: the owner's
+  factor and pack, a receiver's unpack, every rank's updates);
+* the sharded rest of the solve (point passes, Schur, Jacobian ...) from a
+  measured C4 N=1 solve's phase times, divided by N.
+
+Only the collectives are not measured (no second GPU is ever available to
+this build): they are modelled from the published xGMI figures, as two
+scenarios -- "ring": one 153 GB/s link per hop (RCCL ring), "mesh": the
+~300 GB/s bus bandwidth RCCL reaches over the fully connected 8-GPU xGMI
+mesh -- each with 20 us per collective.
+
+  python tools/dist_factor_model.py [--out gpurun_out/dist_model.json]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+LAT_S = 20e-6
+SCEN = {"ring": 153e9, "mesh": 300e9}
+N_SYS = 12000          # C4 reduced system (6 x 2000 cameras)
+ITERS = 3              # LM iterations of the C4 solve (= factorisations per solve)
+
+
+_CACHE = {}
+
+
+def profile(n, nranks, pt):
+    if (n, nranks, pt) in _CACHE:
+        return _CACHE[(n, nranks, pt)]
+    import sfm_amd
+    nblk = (n + 1 + 63) // 64
+    np_ = (nblk + pt - 1) // pt
+    fac = np.zeros(np_)
+    pack = np.zeros(np_)
+    unpack = np.zeros(np_)
+    upd = np.zeros((nranks, np_))
+    misc = np.zeros(5)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    rc = sfm_amd.lib().sfm_dist_factor_profile(0, n, nranks, pt, p(fac), p(pack), p(unpack), p(upd), p(misc))
+    if rc != 0:
+        raise RuntimeError(sfm_amd.lib().sfm_last_error())
+    _CACHE[(n, nranks, pt)] = (fac, pack, unpack, upd, misc)
+    return _CACHE[(n, nranks, pt)]
+
+
+def panel_bytes(n, pt):
+    nblk = (n + 1 + 63) // 64
+    out = []
+    for J in range((nblk + pt - 1) // pt):
+        c0, c1 = J * pt * 64, min((J + 1) * pt * 64, n + 1)
+        ncols = min(pt, nblk - J * pt)
+        out.append(8 * ((c1 - c0) * (n + 1 - c0) + ncols * 64 * 64 + 1))
+    return np.array(out, dtype=np.float64)
+
+
+def own_tiles_after(nblk, pt, k, nranks, rank):
+    """tiles rank updates after panel k: (its panels j > k)."""
+    tot, first = 0, 0
+    for j in range(k + 1, (nblk + pt - 1) // pt):
+        if j % nranks != rank:
+            continue
+        t = sum(nblk - c for c in range(j * pt, min(j * pt + pt, nblk)))
+        if j == k + 1:
+            first = t
+        tot += t
+    return tot, first
+
+
+def factor_model(n, nranks, pt, bw):
+    """One distributed factorisation (seconds) for the two schedules:
+    sequential (per panel: every rank's updates of the previous panel, the
+    owner's factor + pack, the broadcast, the unpack) and look-ahead (the
+    owner of k+1 updates panel k+1 first, factors and broadcasts it while
+    the bulk updates run beside it: the chain is update-next + factor + pack
+    + broadcast, the bulk bounded by each rank's total updates)."""
+    fac, pack, unpack, upd, misc = profile(n, nranks, pt)
+    ms = 1e-3
+    nblk = (n + 1 + 63) // 64
+    np_ = len(fac)
+    pb = panel_bytes(n, pt)
+    bcast = LAT_S + pb / bw if nranks > 1 else np.zeros(np_)
+    rs_bytes = 8 * misc[4]
+    rs = (LAT_S + (nranks - 1) / nranks * rs_bytes / bw) if nranks > 1 else 0.0
+    rs_copy = (misc[0] + misc[1]) * ms / nranks + misc[0] * ms   # pack all, unpack own share
+    seq = rs + rs_copy
+    for k in range(np_):
+        prev = upd[:, k - 1].max() * ms if k > 0 else 0.0
+        seq += prev + (fac[k] + pack[k]) * ms + bcast[k] + (unpack[k] * ms if nranks > 1 else 0.0)
+    seq += upd[:, np_ - 1].max() * ms + misc[2] * ms
+    chain = 0.0
+    for k in range(np_):
+        own = k % nranks
+        if k > 0:
+            tot, first = own_tiles_after(nblk, pt, k - 1, nranks, own)
+            chain += upd[own, k - 1] * ms * (first / tot if tot else 0.0)
+        chain += (fac[k] + pack[k]) * ms + bcast[k] + (unpack[k] * ms if nranks > 1 else 0.0)
+    bulk = upd.sum(axis=1).max() * ms + sum(fac[k] for k in range(np_)) * ms / nranks
+    look = rs + rs_copy + max(chain, bulk) + misc[2] * ms
+    return {"sequential_s": seq, "lookahead_s": look, "chain_s": chain, "bulk_s": bulk,
+            "reduce_scatter_s": rs, "broadcast_s": float(bcast.sum()), "factor_s_sum": float(fac.sum() * ms),
+            "updates_s_max_rank": float(upd.sum(axis=1).max() * ms), "backsub_s": misc[2] * ms,
+            "fail_bits": int(misc[3])}
+
+
+def c4_n1_phases():
+    """Phase times of a C4 solve on this GPU (bench.measure_ba, 3 solves)."""
+    import bench
+    args = argparse.Namespace(steps=3, warmup=1)
+    m = bench.measure_ba(2000, 1_000_000, 0, 1_000_000, bench.SEED + 1, True, args, 1, 0, 0, None, False)
+    m["ba"].close()
+    ph = {k: v["ms"] / 3 for k, v in m["phases"].items()}
+    return m["elapsed"] / 3, ph, m["iters"] / 3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "dist_model.json"))
+    ap.add_argument("--pt", type=int, nargs="*", default=[2, 4])
+    a = ap.parse_args()
+    solve_s, ph, iters = c4_n1_phases()
+    chol1 = ph["cholesky"] * 1e-3                       # per solve, 3 factorisations
+    backsolve1 = ph["backsolve"] * 1e-3
+    rest = solve_s - chol1 - backsolve1                 # sharded (points) + replicated small work
+    print(f"C4 N=1: {solve_s * 1e3:.1f} ms per solve ({iters:.0f} LM iterations), factor {chol1 * 1e3:.1f} ms, "
+          f"back substitution {backsolve1 * 1e3:.2f} ms, rest {rest * 1e3:.1f} ms", flush=True)
+    out = {"c4_n1": {"solve_ms": solve_s * 1e3, "phases_ms": ph, "lm_iterations": iters},
+           "latency_s": LAT_S, "scenarios_Bps": SCEN, "curves": {}}
+    packed = 8 * (N_SYS * (N_SYS + 1) // 2 + N_SYS)
+    for name, bw in SCEN.items():
+        for N in (1, 2, 4, 8):
+            ar = 0.0 if N == 1 else LAT_S + 2 * (N - 1) / N * packed / bw
+            rep = chol1 + backsolve1 + ITERS * ar + rest / N
+            key = f"{name}_N{N}"
+            out["curves"][key] = {"replicated_ms": rep * 1e3, "replicated_speedup": solve_s / rep}
+            for pt in a.pt:
+                f = factor_model(N_SYS, N, pt, bw)
+                for sch in ("sequential", "lookahead"):
+                    t = ITERS * f[f"{sch}_s"] + rest / N
+                    out["curves"][key][f"dist_pt{pt}_{sch}_ms"] = t * 1e3
+                    out["curves"][key][f"dist_pt{pt}_{sch}_speedup"] = solve_s / t
+                out["curves"][key][f"dist_pt{pt}_parts"] = f
+            print(key, json.dumps({k: (round(v, 3) if isinstance(v, float) else v)
+                                   for k, v in out["curves"][key].items() if not k.endswith("parts")}), flush=True)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
