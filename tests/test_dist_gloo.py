@@ -81,3 +81,137 @@ def test_sharded_reduced_system_equals_global():
                                     1.0 / (1.0 + np.sqrt(cp)), np.full(6 * C, 0.05), np.full(3 * P, 0.02), True)
     assert np.allclose(S_sh, S, rtol=1e-11, atol=1e-12 * np.abs(S).max())
     assert np.allclose(rhs_sh, rhs, rtol=1e-11, atol=1e-12 * np.abs(rhs).max())
+
+
+# ---- the distributed reduced-camera factor (sfm_ba_set_distributed_factor,
+# ba_solver.hip dist_factor_enqueue): the same protocol on the host, numpy
+# for the device kernels, gloo for the collectives ----
+def _panel_layout(n, pw, world):
+    """Panel J = columns [pw J, pw J + pw) of the augmented (n+1)-row system,
+    rows c0_J..n; owner J % world; per-owner segment offsets (the
+    reduce-scatter's send layout) -- dist_prepare's arithmetic."""
+    npan = (n + 1 + pw - 1) // pw
+    count, local, tot = [], [], [0] * world
+    for J in range(npan):
+        c0, c1 = J * pw, min((J + 1) * pw, n + 1)
+        count.append((c1 - c0) * (n + 1 - c0))
+        local.append(tot[J % world])
+        tot[J % world] += count[-1]
+    return npan, count, local, max(tot)
+
+
+def _pack(A, n, pw, J, buf, off):
+    c0, c1 = J * pw, min((J + 1) * pw, n + 1)
+    rows = n + 1 - c0
+    for c in range(c0, c1):
+        buf[off + (c - c0) * rows: off + (c - c0 + 1) * rows] = A[c0:n + 1, c]
+
+
+def _unpack(A, n, pw, J, buf, off):
+    c0, c1 = J * pw, min((J + 1) * pw, n + 1)
+    rows = n + 1 - c0
+    for c in range(c0, c1):
+        A[c0:n + 1, c] = buf[off + (c - c0) * rows: off + (c - c0 + 1) * rows]
+
+
+def _dist_worker(rank, world, port, q, pw):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from sfm_amd import scene
+    from oracle import ffi as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    C, P = 8, 240
+    lo, hi = rank * P // world, (rank + 1) * P // world
+    sh = scene.generate(C, P, views=4, seed=99, p_begin=lo, p_end=hi)
+    scale_c, scale_p = np.full((C, 6), 0.5), np.full((hi - lo, 3), 0.5)
+    S, rhs, _, _ = O.reduced_system(sh.uv, sh.cam_idx, sh.pt_idx, sh.K, sh.rot, sh.t, sh.X, scale_c, scale_p,
+                                    np.full(6 * C, 0.05), np.full(3 * (hi - lo), 0.02), add_cam_diag=(rank == 0))
+    n = 6 * C
+    # this rank's partial augmented system: lower triangle, row n = rhs
+    A = np.zeros((n + 1, n + 1))
+    A[:n, :n] = np.tril(S)
+    A[n, :n] = rhs
+    A[n, n] = 1.0
+    npan, count, local, seg = _panel_layout(n, pw, world)
+    send = np.zeros(world * seg)
+    for J in range(npan):
+        _pack(A, n, pw, J, send, (J % world) * seg + local[J])
+    recv = torch.zeros(seg, dtype=torch.float64)
+    dist.reduce_scatter_tensor(recv, torch.from_numpy(send))
+    for J in range(npan):
+        if J % world == rank:
+            _unpack(A, n, pw, J, recv.numpy(), local[J])
+    for k in range(npan):
+        c0, c1 = k * pw, min((k + 1) * pw, n + 1)
+        buf = torch.zeros(count[k], dtype=torch.float64)
+        if k % world == rank:
+            # the owner factors its (fully updated) panel: diagonal block,
+            # then the rows below against it (pivot n forced to 1, as the
+            # device factor takes it)
+            D = A[c0:c1, c0:c1]
+            L = np.linalg.cholesky(np.tril(D) + np.tril(D, -1).T) if c1 <= n else None
+            if L is None:  # the last panel holds row n: factor the real part, z below it
+                m = n - c0
+                Lr = np.linalg.cholesky(np.tril(D[:m, :m]) + np.tril(D[:m, :m], -1).T)
+                A[c0:n, c0:n] = Lr
+                A[n, c0:n] = np.linalg.solve(Lr, A[n, c0:n])
+                A[n, n] = 1.0
+            else:
+                A[c0:c1, c0:c1] = L
+                A[c1:n + 1, c0:c1] = np.linalg.solve(L, A[c1:n + 1, c0:c1].T).T
+            _pack(A, n, pw, k, buf.numpy(), 0)
+        dist.broadcast(buf, src=k % world)
+        if k % world != rank:
+            _unpack(A, n, pw, k, buf.numpy(), 0)
+        # this rank's later panels take panel k's update
+        Lk = A[c0:n + 1, c0:c1]
+        for J in range(k + 1, npan):
+            if J % world != rank:
+                continue
+            j0, j1 = J * pw, min((J + 1) * pw, n + 1)
+            A[j0:n + 1, j0:j1] -= Lk[j0 - c0:, :] @ Lk[j0 - c0:j1 - c0, :].T
+    # replicated back substitution L^T y = z
+    L = np.tril(A[:n, :n])
+    y = np.linalg.solve(L.T, A[n, :n])
+    q.put((rank, L, y))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,pw", [(2, 8), (2, 16), (3, 8)])
+def test_distributed_factor_protocol_equals_global_solve(world, pw):
+    """Reduce-scatter of the ranks' partial systems into block-cyclic panels,
+    per panel the owner's factor + a broadcast, every rank updating its own
+    later panels: every rank ends with the factor of the global system and
+    the same solution as np.linalg.solve on it."""
+    from sfm_amd import scene
+    from oracle import ffi as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, q, pw)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    C, P = 8, 240
+    full = scene.generate(C, P, views=4, seed=99)
+    S, rhs, _, _ = O.reduced_system(full.uv, full.cam_idx, full.pt_idx, full.K, full.rot, full.t, full.X,
+                                    np.full((C, 6), 0.5), np.full((P, 3), 0.5), np.full(6 * C, 0.05),
+                                    np.full(3 * P, 0.02), True)
+    # (the reduced system of a free-gauge BA is ill-conditioned: the factor
+    # is checked by its reconstruction and the solution by its residual, both
+    # backward-stable quantities, plus a loose forward comparison)
+    L_ref = np.linalg.cholesky(S)
+    y_ref = np.linalg.solve(S, rhs)
+    for _, L, y in res:
+        assert np.abs(L @ L.T - S).max() <= 1e-12 * np.abs(S).max()
+        assert np.abs(S @ y - rhs).max() <= 1e-10 * np.abs(rhs).max()
+        assert np.allclose(L, L_ref, rtol=1e-6, atol=1e-9 * np.abs(L_ref).max())
+        assert np.allclose(y, y_ref, rtol=1e-5, atol=1e-9 * np.abs(y_ref).max())
+        assert np.array_equal(L, res[0][1]) and np.array_equal(y, res[0][2])  # every rank the same factor
