@@ -517,6 +517,18 @@ def self_launch(argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def factor_layout(args, world: int, strong: bool) -> int:
+    """Panel width (64-column tiles) of the distributed reduced-camera factor,
+    0 = replicated (sfm_ba_set_distributed_factor).  Auto: the distributed
+    factor for the strong-scaling C4 headline at N >= 4, where the model built
+    on this GPU's measured parts predicts it ahead of the replicated factor
+    (tools/dist_factor_model.py); replicated at N = 2 and for
+    the weak C3-per-GPU line (a 3000^2 system: one 36-MB all-reduce)."""
+    if args.dist_pt >= 0:
+        return args.dist_pt
+    return 4 if (world >= 4 and strong) else 0
+
+
 def measure_ba(cams: int, P_total: int, p_begin: int, p_end: int, seed: int, strong: bool, args, world: int,
                rank: int, local_rank: int, dist, comm: bool) -> dict:
     """One BA workload: the scene's landmark shard [p_begin, p_end) set up
@@ -536,6 +548,9 @@ def measure_ba(cams: int, P_total: int, p_begin: int, p_end: int, seed: int, str
         ba.set_comm(world, rank, uid[0])
     elif comm:
         ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+    dist_pt = factor_layout(args, world, strong) if (world > 1 or comm) else 0
+    if dist_pt:
+        ba.set_distributed_factor(dist_pt)
     t0 = time.perf_counter()
     ba.set_problem(sc.uv, sc.cam_idx, sc.pt_idx, sc.K, sc.rot, sc.t, sc.X)
     ba.sync()
@@ -593,7 +608,7 @@ def measure_ba(cams: int, P_total: int, p_begin: int, p_end: int, seed: int, str
     res_only = evals - jevals       # residual-only (candidate) evaluations
     return {"ba": ba, "sc": sc, "elapsed": elapsed, "iters": iters, "evals": evals, "jevals": jevals, "last": last,
             "phases": phases, "setup_s": setup_s, "n_obs_total": n_obs_total, "n_pts_total": P_total,
-            "res_only": res_only, "value": n_obs_total * res_only / elapsed, "strong": strong}
+            "res_only": res_only, "value": n_obs_total * res_only / elapsed, "strong": strong, "dist_pt": dist_pt}
 
 
 def ba_summary(m: dict, args, world: int) -> dict:
@@ -614,7 +629,11 @@ def ba_summary(m: dict, args, world: int) -> dict:
         "phase_ms_per_solve": {k: round(v["ms"] / args.steps, 4) for k, v in phases.items()},
         "workload": {"cams": sc.n_cams, "points": m["n_pts_total"], "observations": m["n_obs_total"],
                      "points_per_gpu": sc.n_pts, "obs_per_gpu": sc.n_obs, "views_per_point": VIEWS,
-                     "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU"},
+                     "parallelism": f"landmark-sharded x{world}" if world > 1 else "single GPU",
+                     "reduced_camera_factor": (f"distributed: 1-D block-cyclic panels of {m['dist_pt']} tiles"
+                                               if m["dist_pt"] else
+                                               ("replicated (all-reduce of the packed system)" if world > 1
+                                                else "single GPU"))},
     }
 
 
@@ -637,6 +656,9 @@ def main() -> int:
                     help="N=1: also measure BASELINE C4 on this GPU (the N=1 point of the strong-scaling curve the "
                          "N>1 lines report; off by default so that a kernel trace of the default command holds the "
                          "C3 headline's kernels only)")
+    ap.add_argument("--dist-pt", type=int, default=-1,
+                    help="reduced-camera factor at N>1: 0 replicated, k>0 distributed panels of k 64-column tiles, "
+                         "-1 auto (distributed for the C4 headline at N>=4)")
     ap.add_argument("--comm", action="store_true",
                     help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
     ap.add_argument("--dry-run", action="store_true",

@@ -215,6 +215,13 @@ inline int obs_xcd_blocks(const DevProblem& d) {
                                           : ((d.N_pad / 64 + 3) / 4 + 7) / 8;
   return int(8 * std::max<int64_t>(1, per));
 }
+// grid of the XCD-ordered point pass of the back substitution (k_backsub_b):
+// workgroup b serves point slice b % 8 -- the points whose observations the
+// XCD-ordered passes ran on XCD b % 8 -- in blocks of kThreads points
+inline int pt_xcd_blocks(const DevProblem& d) {
+  const int64_t per_slice = (int64_t(d.P) + 7) / 8;
+  return int(8 * std::max<int64_t>(1, (per_slice + kThreads - 1) / kThreads));
+}
 void launch_cam_solve(const DevProblem& d, double radius, hipStream_t s);
 // sum (op 0) or max (op 1) of `nb` partials in slot into scal[dst]
 void launch_reduce(const DevProblem& d, int slot, int nb, int op, int dst, hipStream_t s);

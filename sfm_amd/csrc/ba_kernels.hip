@@ -1248,9 +1248,15 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
                                                         double* __restrict__ part_model, const int* __restrict__ gate) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  // XCD point-slice order (pt_xcd_blocks): workgroups go round-robin to the
+  // 8 XCDs, so workgroup b takes points of slice b % 8, the slice whose
+  // observations k_backsub_a_rc ran (and wrote u) on that XCD; X_new / y_p
+  // land in the L2 that k_backsub_c's same-slice chunks read them from
+  const int x = blockIdx.x & 7;
+  const int pb = int((int64_t(x) * P + 7) / 8), pe = int((int64_t(x + 1) * P + 7) / 8);
+  const int p = pb + (blockIdx.x >> 3) * blockDim.x + threadIdx.x;
   double st = 0.0, bad = 0.0, model = 0.0;
-  if (p < P) {
+  if (p < pe) {
     const double* L = ptL + size_t(kPtL) * p;
     const double l00 = L[0], l10 = L[1], l11 = L[2], l20 = L[3], l21 = L[4], l22 = L[5];
     double w0 = L[6], w1 = L[7], w2 = L[8];
@@ -1302,7 +1308,10 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
   if (threadIdx.x == 0) part_model[blockIdx.x] = r;
 }
 
-__global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int32_t* __restrict__ wcam,
+// (chunks in the XCD point-slice order of k_obs_prep_rc, one per wave: the
+// X_new gathers stay in the slice k_backsub_b wrote on this XCD)
+__global__ __launch_bounds__(kThreads) void k_backsub_c(const int32_t* __restrict__ grp_off,
+                                                        const int4* __restrict__ chunks,
                                                         const int32_t* __restrict__ cam_obs,
                                                         const int32_t* __restrict__ cm_p,
                                                         const double* __restrict__ uv_cm,
@@ -1313,11 +1322,12 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(int64_t N_pad, const int
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
   __shared__ double sh[4];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i0 = int64_t(blockIdx.x) * kThreads + 64 * wv;
+  const XcdChunks xc = xcd_chunks(grp_off, wave_uniform(wv));
   double ncost = 0.0;
-  if (i0 < N_pad) {
-    const int64_t i = i0 + l;
-    const int c = __builtin_amdgcn_readfirstlane(wcam[i0 >> 6]);  // wave-uniform: scalar camera loads
+  if (xc.t < xc.end) {  // wave-uniform
+    const int4 ch = chunks[xc.t];
+    const int64_t i = int64_t(__builtin_amdgcn_readfirstlane(ch.y)) + l;
+    const int c = __builtin_amdgcn_readfirstlane(ch.x);  // wave-uniform: scalar camera loads
     const bool real = cam_obs[i] >= 0;
     const int p = cm_p[i];
     // candidate residual at (cam_new, X_new)
@@ -1523,13 +1533,13 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
     (void)hipMemsetAsync(slot(d, kPModel), 0, sizeof(double) * size_t(obs_xcd_blocks(d)), s);
   }
   if (d.P && pts_var) {
-    k_backsub_b<<<blocks_for(d.P, kThreads), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.eu_cm ? d.pos : nullptr,
+    k_backsub_b<<<pt_xcd_blocks(d), kThreads, 0, s>>>(d.P, d.pt_off, d.eu, d.eu_cm ? d.pos : nullptr,
                                                                d.ptL, d.ptV, d.scale_p,
                                                                d.X, d.X_new, d.ypt, slot(d, kPStepPt),
                                                                slot(d, kPBadBack), slot(d, kPModelPt), d.gate);
   } else if (d.P) {
     // points constant (POSE_ONLY): y_p = 0, X_new = X, no step, no bad flag
-    const size_t nbP = size_t(blocks_for(d.P, kThreads));
+    const size_t nbP = size_t(pt_xcd_blocks(d));
     (void)hipMemsetAsync(d.ypt, 0, sizeof(double) * 3 * size_t(d.P), s);
     (void)hipMemcpyAsync(d.X_new, d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToDevice, s);
     (void)hipMemsetAsync(slot(d, kPStepPt), 0, sizeof(double) * nbP, s);
@@ -1537,8 +1547,8 @@ void launch_point_backsub(const DevProblem& d, hipStream_t s, bool cams_var, boo
     (void)hipMemsetAsync(slot(d, kPModelPt), 0, sizeof(double) * nbP, s);
   }
   if (d.N_pad)
-    k_backsub_c<<<blocks_for(d.N_pad, kThreads), kThreads, 0, s>>>(d.N_pad, d.wcam, d.cam_obs, d.cm_p, d.uv_cm, d.Kc,
-                                                                   d.X_new, d.camRn, slot(d, kPNewCost), d.gate);
+    k_backsub_c<<<obs_xcd_blocks(d), kThreads, 0, s>>>(d.jgrp, d.jchunks, d.cam_obs, d.cm_p, d.uv_cm, d.Kc, d.X_new,
+                                                       d.camRn, slot(d, kPNewCost), d.gate);
 }
 void launch_reduce(const DevProblem& d, int sl, int nb, int op, int dst, hipStream_t s) {
   k_reduce<<<1, 1024, 0, s>>>(slot(d, sl), nb, op, d.scal + dst);

@@ -936,17 +936,18 @@ int compute_step_enqueue(sfm_ba_handle* h, double radius) {
   }
   if (h->rank != 0 || h->mode == SFM_BA_STRUCT_ONLY)
     hipMemsetAsync(d.partials + size_t(kPStepCam) * d.max_blocks, 0, sizeof(double) * nbC, s);
-  const int nbI = std::max(1, blocks_for(d.N_pad, 256));  // k_backsub_c grid
+  const int nbI = d.N_pad ? obs_xcd_blocks(d) : 1;  // k_backsub_a_rc / k_backsub_c grid
+  const int nbB = d.P ? pt_xcd_blocks(d) : 1;       // k_backsub_b grid
   ReduceBatch rb;
-  rb.add(kPModel, d.N_pad ? obs_xcd_blocks(d) : 1, 0, kModelChange);  // k_backsub_a_rc grid
+  rb.add(kPModel, nbI, 0, kModelChange);
   rb.add(kPNewCost, nbI, 0, kNewCost);
-  rb.add(kPStepPt, nbP, 0, kStep2Pt);
+  rb.add(kPStepPt, nbB, 0, kStep2Pt);
   rb.add(kPStepCam, nbC, 0, kStep2Cam);
   // bad-step flags: max over point_prep, cam_update and backsub partials
   rb.add(kPBad, nbP, 1, kBadStep);
   rb.add(kPBadCam, nbC, 1, kBadCam);
-  rb.add(kPBadBack, nbP, 1, kBadBack);
-  rb.add(kPModelPt, nbP, 0, kModelChangePt);
+  rb.add(kPBadBack, nbB, 1, kBadBack);
+  rb.add(kPModelPt, nbB, 0, kModelChangePt);
   // ... and the Cholesky failure flag (an int) into the slot after the scalars
   reduce_phase(h, rb, true, kTailDecide);
   if (sharded(h)) {
@@ -1621,7 +1622,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   d.ld = ((d.n + 1 + kNB - 1) / kNB) * kNB;
   d.nblk = d.ld / kNB;
   d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
-                           d.jac_blocks_rec, blocks_for(npad, 256), obs_xcd_blocks(d)});
+                           d.jac_blocks_rec, blocks_for(npad, 256), obs_xcd_blocks(d), pt_xcd_blocks(d)});
   {
     uint8_t* pb = nullptr;
     ALLOC(pb, pl.bytes);

@@ -17,7 +17,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));  // one 16-B access
 // Each thread moves kU 16-B elements per round, all loads issued before the
 // stores; consecutive lanes take consecutive 16-B elements (fully coalesced
 // 1-KiB wave accesses).
-template <int kU>
+template <int kU, bool kNT>
 __global__ __launch_bounds__(256) void k_stream_copy(const v4f* __restrict__ a, v4f* __restrict__ b, int64_t n) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x * kU;
   for (int64_t base = int64_t(blockIdx.x) * blockDim.x * kU + threadIdx.x; base < n; base += stride) {
@@ -25,12 +25,15 @@ __global__ __launch_bounds__(256) void k_stream_copy(const v4f* __restrict__ a, 
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int64_t i = base + int64_t(u) * blockDim.x;
-      if (i < n) v[u] = __builtin_nontemporal_load(a + i);
+      if (i < n) v[u] = kNT ? __builtin_nontemporal_load(a + i) : a[i];
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int64_t i = base + int64_t(u) * blockDim.x;
-      if (i < n) __builtin_nontemporal_store(v[u], b + i);
+      if (i < n) {
+        if (kNT) __builtin_nontemporal_store(v[u], b + i);
+        else b[i] = v[u];
+      }
     }
   }
 }
@@ -65,13 +68,15 @@ extern "C" int sfm_bench_stream_copy(int32_t device, int64_t bytes, int32_t reps
   double best = 0.0;
   // a few grid / unroll shapes, best of `reps` each (the figure is the best
   // copy the device sustains, not a property of one launch shape)
-  const int grids[3] = {cus * 4, cus * 8, cus * 16};
+  const int grids[4] = {cus * 2, cus * 4, cus * 8, cus * 16};
   for (int g : grids)
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 4; ++u)
       for (int r = 0; r <= reps; ++r) {
         (void)hipEventRecord(e0, s);
-        if (u == 0) k_stream_copy<4><<<g, 256, 0, s>>>(a, b, n);
-        else k_stream_copy<8><<<g, 256, 0, s>>>(a, b, n);
+        if (u == 0) k_stream_copy<4, true><<<g, 256, 0, s>>>(a, b, n);
+        else if (u == 1) k_stream_copy<8, true><<<g, 256, 0, s>>>(a, b, n);
+        else if (u == 2) k_stream_copy<4, false><<<g, 256, 0, s>>>(a, b, n);
+        else k_stream_copy<8, false><<<g, 256, 0, s>>>(a, b, n);
         (void)hipEventRecord(e1, s);
         (void)hipEventSynchronize(e1);
         float ms = 0.f;

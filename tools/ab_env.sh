@@ -16,6 +16,6 @@ for spec in "$@"; do
     timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ab_${label}_$pass -- python3 $R/tools/ab_solve.py > $R/gpurun_out/ab_${label}_$pass.log 2>&1
   ) || { echo "$label failed"; tail $R/gpurun_out/ab_${label}_$pass.log; exit 1; }
   grep final_cost $R/gpurun_out/ab_${label}_$pass.log | sed "s/^/$label /"
-  python3 $R/tools/kstats.py $R/gpurun_out/ab_${label}_$pass | grep -E "k_jacobian|k_obs_prep|k_cam_sum|k_schur_diag|k_chol|k_schur_pts" | sed "s/^/$label /"
+  python3 $R/tools/kstats.py $R/gpurun_out/ab_${label}_$pass | grep -E "${KRX:-k_jacobian|k_obs_prep|k_cam_sum|k_schur_diag|k_chol|k_schur_pts}" | sed "s/^/$label /"
 done
 done
