@@ -520,13 +520,14 @@ def self_launch(argv) -> int:
 def factor_layout(args, world: int, strong: bool) -> int:
     """Panel width (64-column tiles) of the distributed reduced-camera factor,
     0 = replicated (sfm_ba_set_distributed_factor).  Auto: the distributed
-    factor for the strong-scaling C4 headline at N >= 4, where the model built
-    on this GPU's measured parts predicts it ahead of the replicated factor
-    (tools/dist_factor_model.py); replicated at N = 2 and for
-    the weak C3-per-GPU line (a 3000^2 system: one 36-MB all-reduce)."""
+    factor with 8-tile panels for the strong-scaling C4 headline, which the
+    model built on this GPU's measured parts predicts ahead of the replicated
+    factor at every N > 1 (tools/dist_factor_model.py, DESIGN.md §7);
+    replicated for the weak C3-per-GPU line (a 3000^2 system: one 36-MB
+    all-reduce per LM iteration)."""
     if args.dist_pt >= 0:
         return args.dist_pt
-    return 4 if (world >= 4 and strong) else 0
+    return 8 if (world > 1 and strong) else 0
 
 
 def measure_ba(cams: int, P_total: int, p_begin: int, p_end: int, seed: int, strong: bool, args, world: int,
@@ -658,7 +659,7 @@ def main() -> int:
                          "C3 headline's kernels only)")
     ap.add_argument("--dist-pt", type=int, default=-1,
                     help="reduced-camera factor at N>1: 0 replicated, k>0 distributed panels of k 64-column tiles, "
-                         "-1 auto (distributed for the C4 headline at N>=4)")
+                         "-1 auto (8-tile panels for the C4 headline)")
     ap.add_argument("--comm", action="store_true",
                     help="use an RCCL communicator even at N=1 (exercises the sharded path's collectives)")
     ap.add_argument("--dry-run", action="store_true",

@@ -244,9 +244,9 @@ void launch_backsolve(const DevProblem& d, int epoch, hipStream_t s, bool sentin
 // (panel J on rank J % nranks; chol_kernels.hip) ----
 // panel k of the trailing matrix factored in place (L, W_k) by its owner
 int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStream_t s);
-// this rank's panels after k updated with panel k's L
-void launch_panel_update(const DevProblem& d, int k, int pt, int nranks, int rank, hipStream_t s);
-int panel_update_tiles(int nblk, int pt, int k, int nranks, int rank);
+// this rank's panels j in [j0, j1] (j > k) updated with panel k's L
+void launch_panel_update(const DevProblem& d, int k, int j0, int j1, int pt, int nranks, int rank, hipStream_t s);
+int panel_update_tiles(int nblk, int pt, int j0, int j1, int nranks, int rank);
 // panel rectangles (columns col0..col1-1, rows c0_J..n) to / from buf at
 // off[J] (device array; nullptr: every panel at off1)
 void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,

@@ -102,7 +102,9 @@ struct sfm_ba_handle {
     std::vector<int64_t> count;       // per panel: rectangle doubles
     double* send = nullptr;           // [nranks][seg]
     double* recv = nullptr;           // [seg]
-    double* bcast = nullptr;          // [bcast_cap]
+    double* bcast = nullptr;          // [2][bcast_cap]: panel k travels in half k % 2
+    hipStream_t cstream = nullptr;    // RCCL: the broadcasts' own stream (look-ahead)
+    hipEvent_t ev_packed = nullptr, ev_free[2] = {nullptr, nullptr}, ev_arrived[2] = {nullptr, nullptr};
     int64_t* off_send = nullptr;      // [np] panel offset in send (device)
     int64_t* off_recv = nullptr;      // [np] own panels' offset in recv, -1 others (device)
   } dist;
@@ -643,7 +645,16 @@ int dist_prepare(sfm_ba_handle* h) {
   for (void* p : {static_cast<void*>(D.send), static_cast<void*>(D.recv), static_cast<void*>(D.bcast),
                   static_cast<void*>(D.off_send), static_cast<void*>(D.off_recv)})
     if (p) (void)hipFree(p);
+  const hipStream_t cs = D.cstream;
+  const hipEvent_t evs[5] = {D.ev_packed, D.ev_free[0], D.ev_free[1], D.ev_arrived[0], D.ev_arrived[1]};
   D = sfm_ba_handle::DistBufs();
+  D.cstream = cs;  // (kept for the handle's life)
+  D.ev_packed = evs[0]; D.ev_free[0] = evs[1]; D.ev_free[1] = evs[2]; D.ev_arrived[0] = evs[3]; D.ev_arrived[1] = evs[4];
+  if (!D.cstream) {
+    HIPCHK(hipStreamCreateWithFlags(&D.cstream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&D.ev_packed, &D.ev_free[0], &D.ev_free[1], &D.ev_arrived[0], &D.ev_arrived[1]})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
   const int np = (d.nblk + pt - 1) / pt, N = h->nranks;
   std::vector<int64_t> local(static_cast<size_t>(np)), tot(static_cast<size_t>(N), 0);
   D.count.assign(size_t(np), 0);
@@ -663,7 +674,7 @@ int dist_prepare(sfm_ba_handle* h) {
   auto grab = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
   if (!grab(reinterpret_cast<void**>(&D.send), sizeof(double) * size_t(D.seg) * N) ||
       !grab(reinterpret_cast<void**>(&D.recv), sizeof(double) * size_t(D.seg)) ||
-      !grab(reinterpret_cast<void**>(&D.bcast), sizeof(double) * size_t(D.bcast_cap)) ||
+      !grab(reinterpret_cast<void**>(&D.bcast), 2 * sizeof(double) * size_t(D.bcast_cap)) ||
       !grab(reinterpret_cast<void**>(&D.off_send), sizeof(int64_t) * np) ||
       !grab(reinterpret_cast<void**>(&D.off_recv), sizeof(int64_t) * np))
     return fail(SFM_ENOMEM, "hipMalloc failed (distributed factor buffers)");
@@ -679,34 +690,86 @@ int dist_prepare(sfm_ba_handle* h) {
 // panels; per panel k its owner factors it and broadcasts L (+ its W_k
 // tiles and failure bits), every rank applies it to its own later panels;
 // then every rank holds the whole factor and back-substitutes (replicated).
+// Look-ahead order: having panel k, the owner of panel k+1 first updates
+// that panel alone, factors and packs it, and only then applies panel k to
+// its other panels -- with RCCL the broadcast of k+1 runs on its own stream
+// beside those bulk updates (two broadcast buffers, panel k in half k % 2;
+// events order a half's reuse after its last reader).  Every panel still
+// takes its updates in panel order, so the factor is bitwise the sequential
+// loop's.
 int dist_factor_enqueue(sfm_ba_handle* h) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
   if ((rc = dist_prepare(h))) return rc;
   auto& D = h->dist;
-  const int pt = D.pt, N = h->nranks, np = int(D.count.size());
+  const int pt = D.pt, N = h->nranks, me = h->rank, np = int(D.count.size());
+  // (SFM_DIST_OVERLAP=1: the broadcast stream and its events even on one
+  // rank, where RCCL's broadcast is a local no-op -- the one-GPU test of the
+  // look-ahead plumbing, tests/test_gpu_scale.py)
+  static const bool force_overlap = env_flag("SFM_DIST_OVERLAP");
+  const bool overlap = h->comm != nullptr && (N > 1 || force_overlap);
   launch_panel_copy(d, true, pt, 0, d.n + 1, D.off_send, 0, D.send, s);
   if ((rc = reduce_scatter(h, D.send, D.recv, D.seg))) return rc;
   launch_panel_copy(d, false, pt, 0, d.n + 1, D.off_recv, 0, D.recv, s);
+  if (overlap) {  // both broadcast halves free from here (the last factor's readers are before this on s)
+    HIPCHK(hipEventRecord(D.ev_free[0], s));
+    HIPCHK(hipEventRecord(D.ev_free[1], s));
+  }
+  auto geom = [&](int k, int* t0, int* c0, int* c1, int64_t* nw) {
+    *t0 = k * pt;
+    const int ncols = std::min(pt, d.nblk - *t0);
+    *c0 = *t0 * kNB;
+    *c1 = *c0 + ncols * kNB;
+    *nw = int64_t(ncols) * kNB * kNB;
+  };
+  auto half = [&](int k) { return D.bcast + size_t(k & 1) * size_t(D.bcast_cap); };
+  // the owner's part: factor panel k, pack L + W_k tiles + failure bits
+  auto factor_pack = [&](int k) -> int {
+    int t0, c0, c1;
+    int64_t nw;
+    geom(k, &t0, &c0, &c1, &nw);
+    double* b = half(k);
+    launch_cholesky_panel(d, k, pt, ++h->chol_epoch, s);
+    launch_panel_copy(d, true, pt, c0, c1, nullptr, 0, b, s);
+    HIPCHK(hipMemcpyAsync(b + D.count[k], d.invL + size_t(t0) * kNB * kNB, sizeof(double) * size_t(nw),
+                          hipMemcpyDeviceToDevice, s));
+    launch_fail_slot(d, true, b + D.count[k] + nw, s);
+    if (overlap) HIPCHK(hipEventRecord(D.ev_packed, s));
+    return 0;
+  };
+  if (np > 0 && me == 0 && (rc = factor_pack(0))) return rc;
   for (int k = 0; k < np; ++k) {
-    const int owner = k % N, t0 = k * pt, ncols = std::min(pt, d.nblk - t0);
-    const int c0 = t0 * kNB, c1 = c0 + ncols * kNB;
-    const int64_t nw = int64_t(ncols) * kNB * kNB, cnt = D.count[k] + nw + 1;
-    double* wt = D.bcast + D.count[k];
-    if (h->rank == owner) {
-      launch_cholesky_panel(d, k, pt, ++h->chol_epoch, s);
-      launch_panel_copy(d, true, pt, c0, c1, nullptr, 0, D.bcast, s);
-      HIPCHK(hipMemcpyAsync(wt, d.invL + size_t(t0) * kNB * kNB, sizeof(double) * size_t(nw), hipMemcpyDeviceToDevice, s));
-      launch_fail_slot(d, true, wt + nw, s);
+    const int owner = k % N;
+    int t0, c0, c1;
+    int64_t nw;
+    geom(k, &t0, &c0, &c1, &nw);
+    double* b = half(k);
+    const int64_t cnt = D.count[k] + nw + 1;
+    if (N > 1 || overlap) {
+      if (overlap) {
+        // the half is packed (owner) / no longer read by panel k-2's unpack
+        if (me == owner) HIPCHK(hipStreamWaitEvent(D.cstream, D.ev_packed, 0));
+        else HIPCHK(hipStreamWaitEvent(D.cstream, D.ev_free[k & 1], 0));
+        NCCLCHK(ncclBroadcast(b, b, size_t(cnt), ncclDouble, owner, h->comm, D.cstream));
+        HIPCHK(hipEventRecord(D.ev_arrived[k & 1], D.cstream));
+        HIPCHK(hipStreamWaitEvent(s, D.ev_arrived[k & 1], 0));
+      } else if ((rc = broadcast(h, b, cnt, owner))) {
+        return rc;
+      }
     }
-    if (N > 1 && (rc = broadcast(h, D.bcast, cnt, owner))) return rc;
-    if (h->rank != owner) {
-      launch_panel_copy(d, false, pt, c0, c1, nullptr, 0, D.bcast, s);
-      HIPCHK(hipMemcpyAsync(d.invL + size_t(t0) * kNB * kNB, wt, sizeof(double) * size_t(nw), hipMemcpyDeviceToDevice, s));
-      launch_fail_slot(d, false, wt + nw, s);
+    if (me != owner) {
+      launch_panel_copy(d, false, pt, c0, c1, nullptr, 0, b, s);
+      HIPCHK(hipMemcpyAsync(d.invL + size_t(t0) * kNB * kNB, b + D.count[k], sizeof(double) * size_t(nw),
+                            hipMemcpyDeviceToDevice, s));
+      launch_fail_slot(d, false, b + D.count[k] + nw, s);
+      if (overlap) HIPCHK(hipEventRecord(D.ev_free[k & 1], s));
     }
-    launch_panel_update(d, k, pt, N, h->rank, s);
+    if (k + 1 < np && (k + 1) % N == me) {
+      launch_panel_update(d, k, k + 1, k + 1, pt, N, me, s);  // the next panel first (look-ahead)
+      if ((rc = factor_pack(k + 1))) return rc;
+    }
+    launch_panel_update(d, k, k + 2, INT32_MAX / 2, pt, N, me, s);  // (k+1 is not ours unless updated above)
   }
   return 0;
 }
@@ -1188,6 +1251,13 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
                   static_cast<void*>(h->dist.bcast), static_cast<void*>(h->dist.off_send),
                   static_cast<void*>(h->dist.off_recv)})
     if (p) hipFree(p);
+  if (h->dist.cstream) {
+    hipStreamSynchronize(h->dist.cstream);
+    hipStreamDestroy(h->dist.cstream);
+    for (hipEvent_t e : {h->dist.ev_packed, h->dist.ev_free[0], h->dist.ev_free[1], h->dist.ev_arrived[0],
+                         h->dist.ev_arrived[1]})
+      hipEventDestroy(e);
+  }
   if (h->stream2) {
     hipStreamSynchronize(h->stream2);
     hipStreamDestroy(h->stream2);
@@ -2145,7 +2215,7 @@ int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t p
         launch_panel_copy(d, false, pt, c0, c1, nullptr, tot, buf, s);
       }
       HIPCHK(hipEventRecord(ev[8 + 4 * k + 2], s));
-      launch_panel_update(d, k, pt, nranks, rank, s);
+      launch_panel_update(d, k, k + 1, INT32_MAX / 2, pt, nranks, rank, s);
       HIPCHK(hipEventRecord(ev[8 + 4 * k + 3], s));
     }
     if (rank == 0) {

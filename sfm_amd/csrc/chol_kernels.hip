@@ -1144,12 +1144,13 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
 // to its own later panels (k_panel_update), so at the end every rank holds
 // the whole L (and every W_k) and the back substitution runs replicated.
 
-// Own tile columns after panel k, in order: panels j = k+1.. with
-// j % nranks == rank, tile columns [pt j, min(pt j + pt, nblk)); column jt
-// holds the nblk - jt tiles (jt .. nblk-1, jt).
-__device__ __forceinline__ bool panel_task(int task, int nblk, int pt, int k, int nranks, int rank, int* it, int* jt) {
-  int j = k + 1 + ((rank - (k + 1)) % nranks + nranks) % nranks;
-  for (; j * pt < nblk; j += nranks) {
+// Own tile columns of panels j in [j0, j1], in order (j % nranks == rank),
+// tile columns [pt j, min(pt j + pt, nblk)); column jt holds the nblk - jt
+// tiles (jt .. nblk-1, jt).
+__device__ __forceinline__ bool panel_task(int task, int nblk, int pt, int j0, int j1, int nranks, int rank, int* it,
+                                           int* jt) {
+  int j = j0 + ((rank - j0) % nranks + nranks) % nranks;
+  for (; j <= j1 && j * pt < nblk; j += nranks) {
     for (int c = j * pt; c < min(j * pt + pt, nblk); ++c) {
       const int cnt = nblk - c;
       if (task < cnt) {
@@ -1169,10 +1170,10 @@ __device__ __forceinline__ bool panel_task(int task, int nblk, int pt, int k, in
 // quadrant of a diagonal tile is skipped: never read).  Every tile keeps its
 // k order (the panel's columns ascending), the order the single-GPU factor
 // applies them in.
-__global__ __launch_bounds__(256) void k_panel_update(double* __restrict__ A, int ld, int nblk, int pt, int k,
-                                                      int kc0, int kw, int nranks, int rank) {
+__global__ __launch_bounds__(256) void k_panel_update(double* __restrict__ A, int ld, int nblk, int pt, int pj0,
+                                                      int pj1, int kc0, int kw, int nranks, int rank) {
   int it = 0, jt = 0;
-  if (!panel_task(blockIdx.x, nblk, pt, k, nranks, rank, &it, &jt)) return;
+  if (!panel_task(blockIdx.x, nblk, pt, pj0, pj1, nranks, rank, &it, &jt)) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cb = 32 * (w >> 1), rb = 32 * (w & 1);
   const int lr = lane & 15, lk = lane >> 4;
@@ -1328,20 +1329,20 @@ int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStre
   return 0;
 }
 
-int panel_update_tiles(int nblk, int pt, int k, int nranks, int rank) {
+int panel_update_tiles(int nblk, int pt, int j0, int j1, int nranks, int rank) {
   int n = 0;
-  for (int j = k + 1; j * pt < nblk; ++j) {
+  for (int j = j0; j <= j1 && j * pt < nblk; ++j) {
     if (j % nranks != rank) continue;
     for (int c = j * pt; c < std::min(j * pt + pt, nblk); ++c) n += nblk - c;
   }
   return n;
 }
 
-void launch_panel_update(const DevProblem& d, int k, int pt, int nranks, int rank, hipStream_t s) {
-  const int tiles = panel_update_tiles(d.nblk, pt, k, nranks, rank);
+void launch_panel_update(const DevProblem& d, int k, int j0, int j1, int pt, int nranks, int rank, hipStream_t s) {
+  const int tiles = panel_update_tiles(d.nblk, pt, j0, j1, nranks, rank);
   if (tiles <= 0) return;
   const int kc0 = k * pt * NB, kw = std::min(pt, d.nblk - k * pt) * NB;
-  k_panel_update<<<tiles, 256, 0, s>>>(d.S, d.ld, d.nblk, pt, k, kc0, kw, nranks, rank);
+  k_panel_update<<<tiles, 256, 0, s>>>(d.S, d.ld, d.nblk, pt, j0, j1, kc0, kw, nranks, rank);
 }
 
 void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,

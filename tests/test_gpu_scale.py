@@ -155,6 +155,57 @@ def test_one_rank_rccl_communicator_at_c4_is_exact():
         assert np.array_equal(a, b)
 
 
+def _dist_one_rank(s, pt, overlap):
+    env = os.environ.get("SFM_DIST_OVERLAP")
+    if overlap:
+        os.environ["SFM_DIST_OVERLAP"] = "1"
+    try:
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_comm(1, 0, sfm_amd.BundleAdjuster.unique_id())
+            ba.set_distributed_factor(pt)
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            p = ba.parameters()
+    finally:
+        if env is None:
+            os.environ.pop("SFM_DIST_OVERLAP", None)
+        else:
+            os.environ["SFM_DIST_OVERLAP"] = env
+    return sm, tr, p
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cfg,pt", [("C2", 1), ("C2", 4), ("C3", 4)])
+def test_distributed_factor_on_one_rank(cfg, pt):
+    """The distributed reduced-camera factor (sfm_ba_set_distributed_factor)
+    through a one-rank RCCL communicator: reduce-scatter into panels, every
+    panel factored (k_chol_fused on a column panel) and applied to the later
+    ones by k_panel_update, the replicated back substitution.  Against the
+    single-launch factor: same LM path, cost 1e-9, parameters 1e-6 (a
+    different update order, so not bitwise).  With SFM_DIST_OVERLAP=1 the
+    broadcasts run on their own stream with the look-ahead events (a no-op
+    broadcast on one rank): bitwise the plain loop."""
+    s = scene.config(cfg)
+    with sfm_amd.BundleAdjuster() as ba:
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm1, tr1 = ba.solve()
+        p1 = ba.parameters()
+    sm2, tr2, p2 = _dist_one_rank(s, pt, False)
+    sm3, tr3, p3 = _dist_one_rank(s, pt, True)
+
+    def rel(a, b):
+        return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-3)))
+
+    assert sm2.num_iterations == sm1.num_iterations
+    assert [t["step_is_successful"] for t in tr2] == [t["step_is_successful"] for t in tr1]
+    assert abs(sm2.final_cost - sm1.final_cost) <= 1e-9 * sm1.final_cost
+    for a, b in zip(p2, p1):
+        assert rel(a, b) < 1e-6
+    assert sm3.final_cost == sm2.final_cost
+    for a, b in zip(p3, p2):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("kind", ["cam", "pt", "uv"])
 def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
     """The device-side validation of sfm_ba_set_problem (ba_setup.hip
