@@ -239,14 +239,24 @@ __global__ __launch_bounds__(kThreads) void k_jacobian(const int32_t* __restrict
         // padding lanes: their 12 J_c entries and 2 residuals zeroed once,
         // so each product sum adds an exact 0 (bitwise the masked sum, 14
         // selects instead of 27)
-        const bool real = l < cnt;
-        double j0[6], j1[6];
+        // (only a camera's last chunk has padding lanes: the masks sit behind
+        // a wave-uniform branch, 28 selects off the full chunks' path)
+        double j0[6], j1[6], r0 = rec[kRes], r1 = rec[kRes + 1];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-          j0[a] = real ? rec[kJC + a] : 0.0;
-          j1[a] = real ? rec[kJC + 6 + a] : 0.0;
+          j0[a] = rec[kJC + a];
+          j1[a] = rec[kJC + 6 + a];
         }
-        const double r0 = real ? rec[kRes] : 0.0, r1 = real ? rec[kRes + 1] : 0.0;
+        if (cnt < 64) {
+          const bool real = l < cnt;
+#pragma unroll
+          for (int a = 0; a < 6; ++a) {
+            j0[a] = real ? j0[a] : 0.0;
+            j1[a] = real ? j1[a] : 0.0;
+          }
+          r0 = real ? r0 : 0.0;
+          r1 = real ? r1 : 0.0;
+        }
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a)
@@ -677,15 +687,25 @@ __global__ __launch_bounds__(kThreads) void k_obs_prep_rc(const int32_t* __restr
     F[3 * u + 1] = jc[u] * o.M[1] + jc[6 + u] * o.M[4];
     F[3 * u + 2] = jc[u] * o.M[2] + jc[6 + u] * o.M[5];
   }
-  const bool real = cam_obs[i] >= 0;
-  const double r0 = real ? o.rec[kRes] - o.h0 : 0.0, r1 = real ? o.rec[kRes + 1] - o.h1 : 0.0;
+  // padding slots (cam_obs < 0) only in a camera's last chunk (count ch.z <
+  // 64): their F and r are zeroed behind a wave-uniform branch, so every
+  // product sums an exact 0 (bitwise the masked sums; 24 selects off the full
+  // chunks' path instead of 54 on every one)
+  double r0 = o.rec[kRes] - o.h0, r1 = o.rec[kRes + 1] - o.h1;
+  if (__builtin_amdgcn_readfirstlane(ch.z) < 64) {
+    const bool real = cam_obs[i] >= 0;
+#pragma unroll
+    for (int e = 0; e < 18; ++e) F[e] = real ? F[e] : 0.0;
+    r0 = real ? r0 : 0.0;
+    r1 = real ? r1 : 0.0;
+  }
   double v[32];
   int q = 0;
 #pragma unroll
   for (int u = 0; u < 6; ++u)
 #pragma unroll
     for (int w = u; w < 6; ++w, ++q)
-      v[q] = real ? F[3 * u] * F[3 * w] + F[3 * u + 1] * F[3 * w + 1] + F[3 * u + 2] * F[3 * w + 2] : 0.0;
+      v[q] = F[3 * u] * F[3 * w] + F[3 * u + 1] * F[3 * w + 1] + F[3 * u + 2] * F[3 * w + 2];
 #pragma unroll
   for (int u = 0; u < 6; ++u) v[21 + u] = jc[u] * r0 + jc[6 + u] * r1;
 #pragma unroll

@@ -295,9 +295,9 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       w_row3_sum(T, Wl, scr[w], w - 1, lane);
-      if (w == 3 && pf_sub != nullptr)  // (pf_diag nullptr: a panel's last column, no next diagonal tile)
+      if (w == 3 && pf_sub != nullptr)
         *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-               (pf_diag == nullptr || __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
+               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     }
     __syncthreads();
     // ---- trailing update of column block b+1 (the next panel's); the
@@ -739,6 +739,7 @@ __device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
+template <bool kPanel>  // a column panel (ncols < nb possible) or the whole factor (ncols == nb)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, int ncols,
                              double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
@@ -752,7 +753,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
     nx[q] = A[size_t(c) * ld + r];
   }
-  for (int j = 0; j < ncols; ++j) {
+  for (int j = 0; j < (kPanel ? ncols : nb); ++j) {
     const int j0 = j * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -771,10 +772,12 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     }
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
     const bool more = j + 1 < nb;      // a tile below the diagonal
-    const bool next = j + 1 < ncols;   // ... and the walker's next diagonal tile (a panel ends before it)
+    const bool next = kPanel ? j + 1 < ncols : more;  // ... and the walker's next diagonal tile (a panel ends before it)
     const int i0 = j0 + NB;
     const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
-    const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : nullptr;
+    // (a panel's last column has no next diagonal tile: its poll checks the
+    // sub-diagonal flag twice)
+    const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : fsub;
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
                                     : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
     if (bad) atomicOr(fail, 1);
@@ -846,7 +849,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       const int e = t + 256 * q, c = e >> 6, r = e & 63;
       st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
     }
-    if (!next) {
+    if (kPanel && !next) {
       // a panel's last column: L_j+1,j is final (no next step publishes it)
       block_publish_wt(F + (j + 1) * nb + j, epoch);
       break;
@@ -858,6 +861,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
 // tepoch: the ticket epoch (the flag epoch `epoch` for a whole factor; 1 for
 // a panel, whose tickets are zeroed before its launch -- its task count
 // differs from panel to panel)
+template <bool kPanel>
 __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int ld, int n, int nb, int ncols,
                                                     double* __restrict__ Winv, int* __restrict__ F,
                                                     int* __restrict__ Pf, unsigned long long* __restrict__ ticket,
@@ -874,7 +878,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
     // (epoch - 1) (ntask + nhelp) and (epoch - 1) (1 + nhelp)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      atomicAdd(ticket, (unsigned long long)(chol_tasks(nb, ncols) + nhelp));
+      atomicAdd(ticket, (unsigned long long)(chol_tasks(nb, kPanel ? ncols : nb) + nhelp));
       atomicAdd(ticket + 1, (unsigned long long)(1 + nhelp));
     }
     return;
@@ -887,18 +891,20 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
     const unsigned long long v = atomicAdd(ticket + 1, threadIdx.x == 0 ? 1ULL : 0ULL);
     const unsigned lo = __builtin_amdgcn_readfirstlane(unsigned(v));
     const unsigned hi = __builtin_amdgcn_readfirstlane(unsigned(v >> 32));
-    sh[1] = int(((unsigned long long)hi << 32 | lo) - (unsigned long long)(tepoch - 1) * (unsigned long long)(1 + nhelp));
+    const unsigned long long te = kPanel ? tepoch : epoch;
+    sh[1] = int(((unsigned long long)hi << 32 | lo) - (unsigned long long)(te - 1) * (unsigned long long)(1 + nhelp));
   }
   __syncthreads();
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker(A, ld, n, nb, ncols, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
+    fused_walker<kPanel>(A, ld, n, nb, ncols, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
     return;
   }
-  const int ntask = chol_tasks(nb, ncols);
+  const int ntask = chol_tasks(nb, kPanel ? ncols : nb);
   // every launch takes exactly ntask + nhelp tickets (one failing grab per helper)
-  const unsigned long long base = (unsigned long long)(tepoch - 1) * (unsigned long long)(ntask + nhelp);
+  const unsigned long long base =
+      (unsigned long long)((kPanel ? tepoch : epoch) - 1) * (unsigned long long)(ntask + nhelp);
   while (true) {
     if (wave0()) {
       // one increment per wave (lane 0 adds 1, the others 0); every lane
@@ -1296,7 +1302,7 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   const int cap = helpers_env > 0 ? std::min(helpers_env, full) : full;
   const int nhelp = std::max(1, std::min(ntask, cap));
   const int* tc = overlap ? d.tile_cnt : nullptr;
-  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
+  k_chol_fused<false><<<1 + nhelp, 256, 0, s>>>(d.S, d.ld, d.n, nb, nb, d.invL, d.cflags, d.cflags + size_t(nb) * nb,
                                          d.cticket, epoch, epoch, nhelp, d.fail, d.gate, tc, d.tile_exp);
   return false;
 }
@@ -1323,7 +1329,7 @@ int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStre
   const int nhelp = std::max(1, std::min(ntask, d.n_cu - 1));
   // the panel's own tickets (ntask differs per panel): zeroed, ticket epoch 1
   (void)hipMemsetAsync(d.cticket + 3, 0, 2 * sizeof(unsigned long long), s);
-  k_chol_fused<<<1 + nhelp, 256, 0, s>>>(d.S + size_t(c0) * d.ld + c0, d.ld, d.n - c0, nb, ncols,
+  k_chol_fused<true><<<1 + nhelp, 256, 0, s>>>(d.S + size_t(c0) * d.ld + c0, d.ld, d.n - c0, nb, ncols,
                                          d.invL + size_t(t0) * NB * NB, d.cflags, d.cflags + size_t(nb) * nb,
                                          d.cticket + 3, epoch, 1, nhelp, d.fail, nullptr, nullptr, nullptr);
   return 0;
