@@ -161,6 +161,36 @@ __device__ __forceinline__ double wave_sum32(double (&v)[32], int l) {
   return v[0] + __shfl_xor(v[0], 1);
 }
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+// IEEE divisions by one shared denominator: the compiler's f64 division is
+// v_div_scale (denominator) -> v_rcp -> two Newton steps -> v_div_scale
+// (numerator) -> q = n r -> e = n - q z -> v_div_fmas (q + e r) ->
+// v_div_fixup, i.e. ~11 instructions, the reciprocal part repeated for every
+// numerator.  For operands in the normal range div_scale, div_fmas' scaling
+// and div_fixup are identities, so refining the reciprocal once and running
+// only the numerator's three steps gives the same bits (an observation's
+// x/z, y/z and 1/z: 13 instructions instead of ~33).  Outside that range --
+// z = 0, denormal or near-overflow operands -- the result differs from the
+// division's (NaN for inf at z = 0), and is non-finite or meaningless alike:
+// the LM treats either as an invalid step.
+struct SharedDiv {
+  double z, r;
+};
+__device__ __forceinline__ SharedDiv shared_div(double z) {
+  double r = __builtin_amdgcn_rcp(z);
+  double e = fma(-z, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-z, r, 1.0);
+  r = fma(r, e, r);
+  return SharedDiv{z, r};
+}
+__device__ __forceinline__ double sdiv(const SharedDiv& d, double n) {
+  const double q = n * d.r;
+  const double e = fma(-d.z, q, n);
+  return fma(e, d.r, q);
+}
+// 1 / z (q = 1 * r = r)
+__device__ __forceinline__ double srcp(const SharedDiv& d) { return fma(fma(-d.z, d.r, 1.0), d.r, d.r); }
 __device__ __forceinline__ void st2(double* p, double a, double b) {
   *reinterpret_cast<double2*>(p) = make_double2(a, b);
 }

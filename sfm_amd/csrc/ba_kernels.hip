@@ -96,10 +96,12 @@ __device__ __forceinline__ double jac_record(const double* cr, double tc0, doubl
   const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc0;
   const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc1;
   const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc2;
-  const double xp = pc0 / pc2, yp = pc1 / pc2;
+  // pc0 / pc2, pc1 / pc2, 1 / pc2 bitwise the divisions, one reciprocal
+  const SharedDiv dz = shared_div(pc2);
+  const double xp = sdiv(dz, pc0), yp = sdiv(dz, pc1);
   const double r0 = fx * xp + sk * yp + cx - uvo.x;
   const double r1 = fy * yp + cy - uvo.y;
-  const double iz = 1.0 / pc2;
+  const double iz = srcp(dz);
   // d r / d pc
   const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
   const double b1 = fy * iz, b2 = -fy * yp * iz;
@@ -420,10 +422,11 @@ __device__ __forceinline__ void point_eval_body(int p, const int32_t* __restrict
     const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
     const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc[1];
     const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc[2];
-    const double xp = pc0 / pc2, yp = pc1 / pc2;
+    const SharedDiv dz = shared_div(pc2);  // (bitwise the three divisions)
+    const double xp = sdiv(dz, pc0), yp = sdiv(dz, pc1);
     const double r0 = fx * xp + sk * yp + cx - uvo.x;
     const double r1 = fy * yp + cy - uvo.y;
-    const double iz = 1.0 / pc2;
+    const double iz = srcp(dz);
     const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
     const double b1 = fy * iz, b2 = -fy * yp * iz;
     double u[3], v[3];
@@ -604,7 +607,7 @@ __device__ __forceinline__ void obs_recompute(int c, int p, double2 uvo, const d
   const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + tc[0];
   const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + tc[1];
   const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + tc[2];
-  const double iz = 1.0 / pc2, xp = pc0 * iz, yp = pc1 * iz;
+  const double iz = srcp(shared_div(pc2)), xp = pc0 * iz, yp = pc1 * iz;  // (iz bitwise 1.0 / pc2)
   double* rec = o.rec;
   rec[kRes] = fx * xp + sk * yp + cx - uvo.x;
   rec[kRes + 1] = fy * yp + cy - uvo.y;
@@ -868,7 +871,7 @@ __device__ __forceinline__ void pair_side_m(const double* cs, const double Xp[3]
   const double pc0 = cr[0] * Xp[0] + cr[1] * Xp[1] + cr[2] * Xp[2] + cs[36];
   const double pc1 = cr[3] * Xp[0] + cr[4] * Xp[1] + cr[5] * Xp[2] + cs[37];
   const double pc2 = cr[6] * Xp[0] + cr[7] * Xp[1] + cr[8] * Xp[2] + cs[38];
-  const double iz = 1.0 / pc2, xp = pc0 * iz, yp = pc1 * iz;
+  const double iz = srcp(shared_div(pc2)), xp = pc0 * iz, yp = pc1 * iz;  // (iz bitwise 1.0 / pc2)
   const double a0 = fx * iz, a1 = sk * iz, a2 = -(fx * xp + sk * yp) * iz;
   const double b1 = fy * iz, b2 = -fy * yp * iz;
   ab[0] = a0; ab[1] = a1; ab[2] = a2; ab[3] = b1; ab[4] = b2;
@@ -1356,7 +1359,8 @@ __global__ __launch_bounds__(kThreads) void k_backsub_c(const int32_t* __restric
     double pc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) pc[k] = Rn[3 * k] * Xn0 + Rn[3 * k + 1] * Xn1 + Rn[3 * k + 2] * Xn2 + Rn[9 + k];
-    const double xp = pc[0] / pc[2], ypj = pc[1] / pc[2];
+    const SharedDiv dz = shared_div(pc[2]);  // (bitwise the two divisions)
+    const double xp = sdiv(dz, pc[0]), ypj = sdiv(dz, pc[1]);
     const double* k5 = Kc + 5 * size_t(c);
     const double2 uvo = ld2(uv_cm + 2 * i);
     const double rn0 = k5[0] * xp + k5[1] * ypj + k5[2] - uvo.x;
