@@ -432,6 +432,21 @@ def stream_copy_gbs(device: int) -> float:
     return gbs.value
 
 
+def stream_copy_sizes(device: int) -> dict:
+    """The same copy at several buffer sizes: below ~256 MiB the Infinity
+    Cache (MALL) holds part of the working set, so only the 4-GiB figure is
+    the HBM one."""
+    import ctypes
+    import sfm_amd
+    from sfm_amd._ffi import check
+    out = {}
+    for mib in (64, 256, 1024, 4096):
+        gbs = ctypes.c_double(0.0)
+        check(sfm_amd.lib().sfm_bench_stream_copy(device, mib << 20, 5, ctypes.byref(gbs)), "sfm_bench_stream_copy")
+        out[f"{mib}MiB"] = round(gbs.value, 1)
+    return out
+
+
 def matcher_leg(device: int, steps: int, cpu: bool) -> dict:
     """The per-frame matcher of CSfM::tracking (CSfM.cpp:518 ->
     CTracker::matchFeatures(prevIdx, currIdx, ...), CTracker.cpp:368-417):
@@ -824,6 +839,7 @@ def main() -> int:
         ba = None
     if rank == 0 and world == 1:
         out["stream_copy_gbs"] = round(stream_copy_gbs(local_rank), 1)
+        out["stream_copy_gbs_by_buffer"] = stream_copy_sizes(local_rank)
     if rank == 0 and world == 1 and not args.no_oneshot:
         ba.close()  # the one-shot path keeps its own cached handle
         out["oneshot"] = oneshot_leg(sc)
