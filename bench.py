@@ -668,6 +668,8 @@ def main() -> int:
     ap.add_argument("--phases", action="store_true", help="print the per-phase breakdown to stderr")
     ap.add_argument("--no-tracker", action="store_true", help="skip the C5 tracker / matcher / keyframe legs")
     ap.add_argument("--no-oneshot", action="store_true", help="skip the one-shot C3 leg")
+    ap.add_argument("--no-stream-copy", action="store_true",
+                    help="skip the STREAM-copy reference (kernel traces of the BA kernels alone)")
     ap.add_argument("--c4-n1", action="store_true",
                     help="N=1: also measure BASELINE C4 on this GPU (the N=1 point of the strong-scaling curve the "
                          "N>1 lines report; off by default so that a kernel trace of the default command holds the "
@@ -837,7 +839,7 @@ def main() -> int:
         out["weak_c3_per_gpu"] = wk
         mw["ba"].close()
         ba = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_stream_copy:
         out["stream_copy_gbs"] = round(stream_copy_gbs(local_rank), 1)
         out["stream_copy_gbs_by_buffer"] = stream_copy_sizes(local_rank)
     if rank == 0 and world == 1 and not args.no_oneshot:

@@ -25,7 +25,7 @@ while [ $# -ge 2 ]; do
     tests) cmd="python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread" ;;
     tests:*) cmd="python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k '${cmd#tests:}'" ;;
     bench) cmd="python bench.py > $O/bench.json" ;;
-    kstats) cmd="rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 10 --warmup 3 --no-tracker --no-cpu-baseline --no-oneshot > $O/kt_bench.json" ;;
+    kstats) cmd="rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 10 --warmup 3 --no-tracker --no-cpu-baseline --no-oneshot --no-stream-copy > $O/kt_bench.json" ;;
   esac
   echo "== step $k (${secs}s): $cmd" | tee -a "$O/steps.txt"
   start=$(date +%s.%N)
