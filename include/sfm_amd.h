@@ -189,19 +189,23 @@ int sfm_ba_set_host_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_all
  *   SFM_COLL_ALLREDUCE       in place on buf[count], arg = op (0 sum, 1 max);
  *   SFM_COLL_BROADCAST       in place on buf[count] from rank `arg`;
  *   SFM_COLL_REDUCE_SCATTER  buf[nranks * count] in rank-segment order; the
- *                            sum of this rank's segment into out[count].
+ *                            sum of this rank's segment into out[count];
+ *   SFM_COLL_REDUCE          the sum over the ranks of buf[count] into buf
+ *                            on rank `arg` (the others' buf is unspecified).
  * (With sfm_ba_set_host_comm's all-reduce alone, the library builds the
- * other two from it.) */
+ * others from it.) */
 #define SFM_COLL_ALLREDUCE 0
 #define SFM_COLL_BROADCAST 1
 #define SFM_COLL_REDUCE_SCATTER 2
+#define SFM_COLL_REDUCE 3
 typedef int (*sfm_collective_fn)(int32_t kind, double* buf, double* out, int64_t count, int32_t arg, void* user);
 int sfm_ba_set_host_collectives(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_collective_fn fn, void* user);
 /* Reduced-camera factor of a sharded solve: 0 (default) =
  * all-reduce of the packed system and a replicated factor on every rank;
- * k > 0 = reduce-scatter into 1-D block-cyclic panels of k 64-column tiles,
- * each panel factored by its owner and broadcast (the same Ceres DENSE_SCHUR
- * LLT, distributed; replaces the solve at CTracker.cpp:700-701). */
+ * k > 0 = 1-D block-cyclic panels of k 64-column tiles, each panel's partial
+ * systems reduced into its owner, factored there and broadcast (the same
+ * Ceres DENSE_SCHUR LLT, distributed; replaces the solve at
+ * CTracker.cpp:700-701). */
 int sfm_ba_set_distributed_factor(sfm_ba_handle* h, int32_t panel_tiles);
 
 /* Hamming 2-NN matcher + the reference's sequential acceptance rule.

@@ -105,16 +105,18 @@ class BundleAdjuster:
     COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int32, ctypes.POINTER(c_double),
                                      ctypes.POINTER(c_double), ctypes.c_int64, ctypes.c_int32, c_void_p)
 
-    def set_host_collectives(self, nranks: int, rank: int, allreduce, broadcast, reduce_scatter) -> None:
+    def set_host_collectives(self, nranks: int, rank: int, allreduce, broadcast, reduce_scatter, reduce) -> None:
         """The host hook with the distributed factor's collectives as well
-        (sfm_ba_set_host_collectives): allreduce(buf, op) and broadcast(buf,
-        root) in place on a float64 array; reduce_scatter(buf, out) with buf
-        holding nranks segments of len(out), this rank's summed segment into
-        out."""
+        (sfm_ba_set_host_collectives): allreduce(buf, op), broadcast(buf, root)
+        and reduce(buf, root) in place on a float64 array; reduce_scatter(buf,
+        out) with buf holding nranks segments of len(out), this rank's summed
+        segment into out."""
         def _cb(kind, buf, out, count, arg, user):
             try:
                 n = int(count)
-                if kind == 2:
+                if kind == 3:
+                    reduce(np.ctypeslib.as_array(buf, (n,)), int(arg))
+                elif kind == 2:
                     reduce_scatter(np.ctypeslib.as_array(buf, (n * nranks,)), np.ctypeslib.as_array(out, (n,)))
                 elif kind == 1:
                     broadcast(np.ctypeslib.as_array(buf, (n,)), int(arg))

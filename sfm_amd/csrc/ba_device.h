@@ -247,9 +247,11 @@ int launch_cholesky_panel(const DevProblem& d, int k, int pt, int epoch, hipStre
 // this rank's panels j in [j0, j1] (j > k) updated with panel k's L
 void launch_panel_update(const DevProblem& d, int k, int j0, int j1, int pt, int nranks, int rank, hipStream_t s);
 int panel_update_tiles(int nblk, int pt, int j0, int j1, int nranks, int rank);
-// panel rectangles (columns col0..col1-1, rows c0_J..n) to / from buf at
-// off[J] (device array; nullptr: every panel at off1)
-void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,
+// panel rectangles (columns col0..col1-1, rows c0_J..n) and buf at off[J]
+// (device array, < 0: skipped; nullptr: every panel at off1); mode 0 packs
+// S into buf, 1 unpacks buf into S, 2 adds buf into S
+constexpr int kPanelPack = 0, kPanelUnpack = 1, kPanelAdd = 2;
+void launch_panel_copy(const DevProblem& d, int mode, int pt, int col0, int col1, const int64_t* off, int64_t off1,
                        double* buf, hipStream_t s);
 // the failure flag into (put) or OR-ed from a broadcast buffer's slot
 void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s);

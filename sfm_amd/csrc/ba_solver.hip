@@ -97,16 +97,18 @@ struct sfm_ba_handle {
   int dist_pt = 0;
   struct DistBufs {
     int pt = 0, nblk = 0, n = 0, nranks = 0, rank = 0;  // the layout below was made for
-    int64_t seg = 0;                  // per-rank segment of the reduce-scatter (doubles)
+    int64_t total = 0;                // doubles of all panel rectangles
     int64_t bcast_cap = 0;            // largest broadcast (doubles)
-    std::vector<int64_t> count;       // per panel: rectangle doubles
-    double* send = nullptr;           // [nranks][seg]
-    double* recv = nullptr;           // [seg]
+    std::vector<int64_t> count, poff; // per panel: rectangle doubles, offset in the panel image
+    double* send = nullptr;           // [total] this rank's partial panels (own ones: zeros)
+    double* recv = nullptr;           // [total] the other ranks' sums of the own panels
     double* bcast = nullptr;          // [2][bcast_cap]: panel k travels in half k % 2
-    hipStream_t cstream = nullptr;    // RCCL: the broadcasts' own stream (look-ahead)
+    hipStream_t cstream = nullptr;    // RCCL: the collectives' own stream (look-ahead)
     hipEvent_t ev_packed = nullptr, ev_free[2] = {nullptr, nullptr}, ev_arrived[2] = {nullptr, nullptr};
-    int64_t* off_send = nullptr;      // [np] panel offset in send (device)
-    int64_t* off_recv = nullptr;      // [np] own panels' offset in recv, -1 others (device)
+    hipEvent_t ev_sent = nullptr;     // the partial panels are packed
+    std::vector<hipEvent_t> ev_red;   // [np] panel k's reduce has landed (owner)
+    int64_t* off_send = nullptr;      // [np] panel offset in send, -1 for own panels (device)
+    int64_t* off_recv = nullptr;      // (unused)
   } dist;
   // out-of-place target of the collectives enqueued inside a gated phase of
   // the device LM loop (allreduce below); grown on demand
@@ -634,6 +636,26 @@ int reduce_scatter(sfm_ba_handle* h, double* send, double* recv, int64_t count) 
   return 0;
 }
 
+// Sum of count doubles at send over the ranks, into recv on rank `root`.
+int reduce_to(sfm_ba_handle* h, double* send, double* recv, int64_t count, int root, hipStream_t st) {
+  if (h->host_fn || h->coll_fn) {
+    h->host_buf.resize(size_t(count));
+    HIPCHK(hipMemcpyAsync(h->host_buf.data(), send, sizeof(double) * size_t(count), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int rc = h->coll_fn ? h->coll_fn(SFM_COLL_REDUCE, h->host_buf.data(), h->host_buf.data(), count, root, h->coll_user)
+                        : h->host_fn(h->host_buf.data(), count, 0, h->host_user);  // (an all-reduce: root keeps it)
+    if (rc != 0) return fail(SFM_EIO, "host collective callback failed");
+    if (h->rank == root) {
+      HIPCHK(hipMemcpyAsync(recv, h->host_buf.data(), sizeof(double) * size_t(count), hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    return 0;
+  }
+  if (!h->comm) return 0;
+  NCCLCHK(ncclReduce(send, recv, size_t(count), ncclDouble, ncclSum, root, h->comm, st));
+  return 0;
+}
+
 // The panel layout of the distributed factor and its buffers (remade when
 // the problem size, the panel width or the rank layout changed).
 int dist_prepare(sfm_ba_handle* h) {
@@ -647,7 +669,11 @@ int dist_prepare(sfm_ba_handle* h) {
     if (p) (void)hipFree(p);
   const hipStream_t cs = D.cstream;
   const hipEvent_t evs[5] = {D.ev_packed, D.ev_free[0], D.ev_free[1], D.ev_arrived[0], D.ev_arrived[1]};
+  std::vector<hipEvent_t> ev_red = std::move(D.ev_red);
+  const hipEvent_t ev_sent = D.ev_sent;
   D = sfm_ba_handle::DistBufs();
+  D.ev_red = std::move(ev_red);
+  D.ev_sent = ev_sent;
   D.cstream = cs;  // (kept for the handle's life)
   D.ev_packed = evs[0]; D.ev_free[0] = evs[1]; D.ev_free[1] = evs[2]; D.ev_arrived[0] = evs[3]; D.ev_arrived[1] = evs[4];
   if (!D.cstream) {
@@ -656,47 +682,56 @@ int dist_prepare(sfm_ba_handle* h) {
       HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   const int np = (d.nblk + pt - 1) / pt, N = h->nranks;
-  std::vector<int64_t> local(static_cast<size_t>(np)), tot(static_cast<size_t>(N), 0);
   D.count.assign(size_t(np), 0);
+  D.poff.assign(size_t(np), 0);
   for (int J = 0; J < np; ++J) {
     const int c0 = J * pt * kNB, c1 = std::min((J + 1) * pt * kNB, d.n + 1);
     D.count[J] = c1 > c0 ? int64_t(c1 - c0) * (d.n + 1 - c0) : 0;
-    local[J] = tot[J % N];
-    tot[J % N] += D.count[J];
+    D.poff[J] = D.total;
+    D.total += D.count[J];
     D.bcast_cap = std::max<int64_t>(D.bcast_cap, D.count[J] + int64_t(pt) * kNB * kNB + 1);
   }
-  D.seg = std::max<int64_t>(1, *std::max_element(tot.begin(), tot.end()));
-  std::vector<int64_t> os(static_cast<size_t>(np)), orv(static_cast<size_t>(np));
-  for (int J = 0; J < np; ++J) {
-    os[J] = int64_t(J % N) * D.seg + local[J];
-    orv[J] = J % N == h->rank ? local[J] : -1;
-  }
+  std::vector<int64_t> os(static_cast<size_t>(np));
+  for (int J = 0; J < np; ++J) os[J] = J % N == h->rank ? -1 : D.poff[J];
   auto grab = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
-  if (!grab(reinterpret_cast<void**>(&D.send), sizeof(double) * size_t(D.seg) * N) ||
-      !grab(reinterpret_cast<void**>(&D.recv), sizeof(double) * size_t(D.seg)) ||
+  if (!grab(reinterpret_cast<void**>(&D.send), sizeof(double) * size_t(D.total)) ||
+      !grab(reinterpret_cast<void**>(&D.recv), sizeof(double) * size_t(D.total)) ||
       !grab(reinterpret_cast<void**>(&D.bcast), 2 * sizeof(double) * size_t(D.bcast_cap)) ||
-      !grab(reinterpret_cast<void**>(&D.off_send), sizeof(int64_t) * np) ||
-      !grab(reinterpret_cast<void**>(&D.off_recv), sizeof(int64_t) * np))
+      !grab(reinterpret_cast<void**>(&D.off_send), sizeof(int64_t) * np))
     return fail(SFM_ENOMEM, "hipMalloc failed (distributed factor buffers)");
   HIPCHK(hipMemcpy(D.off_send, os.data(), sizeof(int64_t) * np, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(D.off_recv, orv.data(), sizeof(int64_t) * np, hipMemcpyHostToDevice));
-  HIPCHK(hipMemsetAsync(D.send, 0, sizeof(double) * size_t(D.seg) * N, h->stream));
+  // the own panels' regions of send stay zero: the owner's partial is
+  // updated in place and the others' sum is added just before its factor
+  HIPCHK(hipMemsetAsync(D.send, 0, sizeof(double) * size_t(D.total), h->stream));
+  while (int(D.ev_red.size()) < np) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    D.ev_red.push_back(e);
+  }
+  if (!D.ev_sent) HIPCHK(hipEventCreateWithFlags(&D.ev_sent, hipEventDisableTiming));
   D.pt = pt; D.nblk = d.nblk; D.n = d.n; D.nranks = N; D.rank = h->rank;
   return 0;
 }
 
 // The reduced camera system's factor, distributed:
-// reduce-scatter of the ranks' partial systems into block-cyclic column
-// panels; per panel k its owner factors it and broadcasts L (+ its W_k
-// tiles and failure bits), every rank applies it to its own later panels;
-// then every rank holds the whole factor and back-substitutes (replicated).
-// Look-ahead order: having panel k, the owner of panel k+1 first updates
-// that panel alone, factors and packs it, and only then applies panel k to
-// its other panels -- with RCCL the broadcast of k+1 runs on its own stream
-// beside those bulk updates (two broadcast buffers, panel k in half k % 2;
-// events order a half's reuse after its last reader).  Every panel still
-// takes its updates in panel order, so the factor is bitwise the sequential
-// loop's.
+// the ranks' partial systems are summed per column panel into its owner (a
+// reduce per panel, not one reduce-scatter up front), per panel k its owner
+// factors it and broadcasts L (+ its W_k tiles and failure bits), every rank
+// applies it to its own later panels; then every rank holds the whole factor
+// and back-substitutes (replicated).
+// * The owner updates its OWN partial of a panel in place and adds the other
+//   ranks' sum (its own region of the send buffer is zero) just before
+//   factoring it: the updates are linear, so the panels' reduces can run
+//   beside the factorisation instead of ahead of it.
+// * Look-ahead: having panel k, the owner of k+1 first updates that panel
+//   alone, adds its reduce, factors and packs it, and only then applies
+//   panel k to its other panels.
+// * Under RCCL the collectives run on a second stream of the handle in the
+//   order reduce 0, reduce 1, then per k: broadcast k, reduce k+2 -- so the
+//   reduce of a panel lands one step before its owner needs it, and the
+//   broadcast of k+1 overlaps the bulk updates (two broadcast buffers,
+//   events order each buffer's reuse after its last reader).
+// Every panel takes its updates in panel order on every rank count.
 int dist_factor_enqueue(sfm_ba_handle* h) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
@@ -704,18 +739,27 @@ int dist_factor_enqueue(sfm_ba_handle* h) {
   if ((rc = dist_prepare(h))) return rc;
   auto& D = h->dist;
   const int pt = D.pt, N = h->nranks, me = h->rank, np = int(D.count.size());
-  // (SFM_DIST_OVERLAP=1: the broadcast stream and its events even on one
-  // rank, where RCCL's broadcast is a local no-op -- the one-GPU test of the
+  // (SFM_DIST_OVERLAP=1: the collective stream and its events even on one
+  // rank, where RCCL's collectives are local -- the one-GPU test of the
   // look-ahead plumbing, tests/test_gpu_scale.py)
   static const bool force_overlap = env_flag("SFM_DIST_OVERLAP");
   const bool overlap = h->comm != nullptr && (N > 1 || force_overlap);
-  launch_panel_copy(d, true, pt, 0, d.n + 1, D.off_send, 0, D.send, s);
-  if ((rc = reduce_scatter(h, D.send, D.recv, D.seg))) return rc;
-  launch_panel_copy(d, false, pt, 0, d.n + 1, D.off_recv, 0, D.recv, s);
-  if (overlap) {  // both broadcast halves free from here (the last factor's readers are before this on s)
+  const bool comm = N > 1 || overlap;
+  hipStream_t cs = overlap ? D.cstream : s;
+  launch_panel_copy(d, kPanelPack, pt, 0, d.n + 1, D.off_send, 0, D.send, s);
+  if (overlap) {
+    HIPCHK(hipEventRecord(D.ev_sent, s));
+    HIPCHK(hipStreamWaitEvent(cs, D.ev_sent, 0));
+    // both broadcast halves free from here (the last factor's readers are before this on s)
     HIPCHK(hipEventRecord(D.ev_free[0], s));
     HIPCHK(hipEventRecord(D.ev_free[1], s));
   }
+  auto reduce_panel = [&](int k) -> int {
+    if (!comm || k >= np) return 0;
+    if (int e = reduce_to(h, D.send + D.poff[k], D.recv + D.poff[k], D.count[k], k % N, cs)) return e;
+    if (overlap && k % N == me) HIPCHK(hipEventRecord(D.ev_red[k], cs));
+    return 0;
+  };
   auto geom = [&](int k, int* t0, int* c0, int* c1, int64_t* nw) {
     *t0 = k * pt;
     const int ncols = std::min(pt, d.nblk - *t0);
@@ -724,20 +768,26 @@ int dist_factor_enqueue(sfm_ba_handle* h) {
     *nw = int64_t(ncols) * kNB * kNB;
   };
   auto half = [&](int k) { return D.bcast + size_t(k & 1) * size_t(D.bcast_cap); };
-  // the owner's part: factor panel k, pack L + W_k tiles + failure bits
+  // the owner's part: the other ranks' sum into its updated partial, factor
+  // panel k, pack L + W_k tiles + failure bits
   auto factor_pack = [&](int k) -> int {
     int t0, c0, c1;
     int64_t nw;
     geom(k, &t0, &c0, &c1, &nw);
+    if (comm) {
+      if (overlap) HIPCHK(hipStreamWaitEvent(s, D.ev_red[k], 0));
+      launch_panel_copy(d, kPanelAdd, pt, c0, c1, nullptr, D.poff[k], D.recv, s);
+    }
     double* b = half(k);
     launch_cholesky_panel(d, k, pt, ++h->chol_epoch, s);
-    launch_panel_copy(d, true, pt, c0, c1, nullptr, 0, b, s);
+    launch_panel_copy(d, kPanelPack, pt, c0, c1, nullptr, 0, b, s);
     HIPCHK(hipMemcpyAsync(b + D.count[k], d.invL + size_t(t0) * kNB * kNB, sizeof(double) * size_t(nw),
                           hipMemcpyDeviceToDevice, s));
     launch_fail_slot(d, true, b + D.count[k] + nw, s);
     if (overlap) HIPCHK(hipEventRecord(D.ev_packed, s));
     return 0;
   };
+  if ((rc = reduce_panel(0)) || (rc = reduce_panel(1))) return rc;
   if (np > 0 && me == 0 && (rc = factor_pack(0))) return rc;
   for (int k = 0; k < np; ++k) {
     const int owner = k % N;
@@ -746,20 +796,21 @@ int dist_factor_enqueue(sfm_ba_handle* h) {
     geom(k, &t0, &c0, &c1, &nw);
     double* b = half(k);
     const int64_t cnt = D.count[k] + nw + 1;
-    if (N > 1 || overlap) {
+    if (comm) {
       if (overlap) {
         // the half is packed (owner) / no longer read by panel k-2's unpack
-        if (me == owner) HIPCHK(hipStreamWaitEvent(D.cstream, D.ev_packed, 0));
-        else HIPCHK(hipStreamWaitEvent(D.cstream, D.ev_free[k & 1], 0));
-        NCCLCHK(ncclBroadcast(b, b, size_t(cnt), ncclDouble, owner, h->comm, D.cstream));
-        HIPCHK(hipEventRecord(D.ev_arrived[k & 1], D.cstream));
-        HIPCHK(hipStreamWaitEvent(s, D.ev_arrived[k & 1], 0));
+        if (me == owner) HIPCHK(hipStreamWaitEvent(cs, D.ev_packed, 0));
+        else HIPCHK(hipStreamWaitEvent(cs, D.ev_free[k & 1], 0));
+        NCCLCHK(ncclBroadcast(b, b, size_t(cnt), ncclDouble, owner, h->comm, cs));
+        HIPCHK(hipEventRecord(D.ev_arrived[k & 1], cs));
       } else if ((rc = broadcast(h, b, cnt, owner))) {
         return rc;
       }
+      if ((rc = reduce_panel(k + 2))) return rc;
+      if (overlap) HIPCHK(hipStreamWaitEvent(s, D.ev_arrived[k & 1], 0));
     }
     if (me != owner) {
-      launch_panel_copy(d, false, pt, c0, c1, nullptr, 0, b, s);
+      launch_panel_copy(d, kPanelUnpack, pt, c0, c1, nullptr, 0, b, s);
       HIPCHK(hipMemcpyAsync(d.invL + size_t(t0) * kNB * kNB, b + D.count[k], sizeof(double) * size_t(nw),
                             hipMemcpyDeviceToDevice, s));
       launch_fail_slot(d, false, b + D.count[k] + nw, s);
@@ -1258,6 +1309,8 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
                          h->dist.ev_arrived[1]})
       hipEventDestroy(e);
   }
+  for (hipEvent_t e : h->dist.ev_red) hipEventDestroy(e);
+  if (h->dist.ev_sent) hipEventDestroy(h->dist.ev_sent);
   if (h->stream2) {
     hipStreamSynchronize(h->stream2);
     hipStreamDestroy(h->stream2);
@@ -2196,9 +2249,9 @@ int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t p
     launch_spd_fill(S, d.ld, n, 12345u, s);
     if (rank == 0) {  // reduce-scatter pack + unpack of the whole image, the back substitution
       HIPCHK(hipEventRecord(ev[0], s));
-      launch_panel_copy(d, true, pt, 0, n + 1, doff, 0, buf, s);
+      launch_panel_copy(d, kPanelPack, pt, 0, n + 1, doff, 0, buf, s);
       HIPCHK(hipEventRecord(ev[1], s));
-      launch_panel_copy(d, false, pt, 0, n + 1, doff, 0, buf, s);
+      launch_panel_copy(d, kPanelAdd, pt, 0, n + 1, doff, 0, buf, s);
       HIPCHK(hipEventRecord(ev[2], s));
     }
     for (int k = 0; k < np; ++k) {
@@ -2208,11 +2261,11 @@ int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t p
       if (owner == rank) {
         launch_cholesky_panel(d, k, pt, ++epoch, s);
         HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
-        launch_panel_copy(d, true, pt, c0, c1, nullptr, tot, buf, s);
+        launch_panel_copy(d, kPanelPack, pt, c0, c1, nullptr, tot, buf, s);
       } else {
         // (from the owner's last packed L, or zeros: every pivot stays positive)
         HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
-        launch_panel_copy(d, false, pt, c0, c1, nullptr, tot, buf, s);
+        launch_panel_copy(d, kPanelUnpack, pt, c0, c1, nullptr, tot, buf, s);
       }
       HIPCHK(hipEventRecord(ev[8 + 4 * k + 2], s));
       launch_panel_update(d, k, k + 1, INT32_MAX / 2, pt, nranks, rank, s);

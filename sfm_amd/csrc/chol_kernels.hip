@@ -1224,7 +1224,8 @@ __global__ __launch_bounds__(256) void k_panel_update(double* __restrict__ A, in
 // (off[J] < 0: panel J skipped).  One workgroup per column.  Rows beyond n
 // (identity padding, zero in every real column) and columns beyond n never
 // travel: every rank writes them itself (k_schur_diag_sum).
-template <bool kPack>
+// kMode: 0 pack (S -> buf), 1 unpack (buf -> S), 2 accumulate (S += buf).
+template <int kMode>
 __global__ __launch_bounds__(256) void k_panel_copy(double* __restrict__ A, int ld, int n, int pcols, int col0,
                                                     const int64_t* __restrict__ off, int64_t off1,
                                                     double* __restrict__ buf) {
@@ -1236,8 +1237,9 @@ __global__ __launch_bounds__(256) void k_panel_copy(double* __restrict__ A, int 
   double* b = buf + o + int64_t(c - c0) * rows;
   double* col = A + size_t(c) * ld + c0;
   for (int r = threadIdx.x; r < rows; r += 256) {
-    if (kPack) b[r] = col[r];
-    else col[r] = b[r];
+    if (kMode == 0) b[r] = col[r];
+    else if (kMode == 1) col[r] = b[r];
+    else col[r] += b[r];
   }
 }
 
@@ -1351,12 +1353,13 @@ void launch_panel_update(const DevProblem& d, int k, int j0, int j1, int pt, int
   k_panel_update<<<tiles, 256, 0, s>>>(d.S, d.ld, d.nblk, pt, j0, j1, kc0, kw, nranks, rank);
 }
 
-void launch_panel_copy(const DevProblem& d, bool pack, int pt, int col0, int col1, const int64_t* off, int64_t off1,
+void launch_panel_copy(const DevProblem& d, int mode, int pt, int col0, int col1, const int64_t* off, int64_t off1,
                        double* buf, hipStream_t s) {
   col1 = std::min(col1, d.n + 1);
   if (col1 <= col0) return;
-  if (pack) k_panel_copy<true><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
-  else k_panel_copy<false><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
+  if (mode == 0) k_panel_copy<0><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
+  else if (mode == 1) k_panel_copy<1><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
+  else k_panel_copy<2><<<col1 - col0, 256, 0, s>>>(d.S, d.ld, d.n, pt * NB, col0, off, off1, buf);
 }
 
 void launch_fail_slot(const DevProblem& d, bool put, double* slot, hipStream_t s) {

@@ -86,18 +86,18 @@ def test_sharded_reduced_system_equals_global():
 # ---- the distributed reduced-camera factor (sfm_ba_set_distributed_factor,
 # ba_solver.hip dist_factor_enqueue): the same protocol on the host, numpy
 # for the device kernels, gloo for the collectives ----
-def _panel_layout(n, pw, world):
+def _panel_layout(n, pw):
     """Panel J = columns [pw J, pw J + pw) of the augmented (n+1)-row system,
-    rows c0_J..n; owner J % world; per-owner segment offsets (the
-    reduce-scatter's send layout) -- dist_prepare's arithmetic."""
+    rows c0_J..n, owner J % world, at offset poff[J] of the panel image --
+    dist_prepare's arithmetic."""
     npan = (n + 1 + pw - 1) // pw
-    count, local, tot = [], [], [0] * world
+    count, poff, tot = [], [], 0
     for J in range(npan):
         c0, c1 = J * pw, min((J + 1) * pw, n + 1)
         count.append((c1 - c0) * (n + 1 - c0))
-        local.append(tot[J % world])
-        tot[J % world] += count[-1]
-    return npan, count, local, max(tot)
+        poff.append(tot)
+        tot += count[-1]
+    return npan, count, poff, tot
 
 
 def _pack(A, n, pw, J, buf, off):
@@ -112,6 +112,13 @@ def _unpack(A, n, pw, J, buf, off):
     rows = n + 1 - c0
     for c in range(c0, c1):
         A[c0:n + 1, c] = buf[off + (c - c0) * rows: off + (c - c0 + 1) * rows]
+
+
+def _unpack_add(A, n, pw, J, buf, off):
+    c0, c1 = J * pw, min((J + 1) * pw, n + 1)
+    rows = n + 1 - c0
+    for c in range(c0, c1):
+        A[c0:n + 1, c] += buf[off + (c - c0) * rows: off + (c - c0 + 1) * rows]
 
 
 def _dist_worker(rank, world, port, q, pw):
@@ -134,44 +141,63 @@ def _dist_worker(rank, world, port, q, pw):
     A[:n, :n] = np.tril(S)
     A[n, :n] = rhs
     A[n, n] = 1.0
-    npan, count, local, seg = _panel_layout(n, pw, world)
-    send = np.zeros(world * seg)
+    npan, count, poff, tot = _panel_layout(n, pw)
+    # every rank's partial panels, its own ones left zero: the owner updates
+    # its partial in place and adds the others' sum just before its factor
+    send = np.zeros(tot)
     for J in range(npan):
-        _pack(A, n, pw, J, send, (J % world) * seg + local[J])
-    recv = torch.zeros(seg, dtype=torch.float64)
-    dist.reduce_scatter_tensor(recv, torch.from_numpy(send))
-    for J in range(npan):
-        if J % world == rank:
-            _unpack(A, n, pw, J, recv.numpy(), local[J])
-    for k in range(npan):
+        if J % world != rank:
+            _pack(A, n, pw, J, send, poff[J])
+    recv = {}
+
+    def reduce_panel(k):
+        if k < npan:
+            t = torch.from_numpy(send[poff[k]:poff[k] + count[k]].copy())
+            dist.reduce(t, dst=k % world)
+            if k % world == rank:
+                recv[k] = t.numpy()
+
+    def factor(k):
         c0, c1 = k * pw, min((k + 1) * pw, n + 1)
+        _unpack_add(A, n, pw, k, recv.pop(k), 0)
+        D = A[c0:c1, c0:c1]
+        if c1 <= n:
+            L = np.linalg.cholesky(np.tril(D) + np.tril(D, -1).T)
+            A[c0:c1, c0:c1] = L
+            A[c1:n + 1, c0:c1] = np.linalg.solve(L, A[c1:n + 1, c0:c1].T).T
+        else:  # the last panel holds row n: factor the real part, z below it
+            m = n - c0
+            Lr = np.linalg.cholesky(np.tril(D[:m, :m]) + np.tril(D[:m, :m], -1).T)
+            A[c0:n, c0:n] = Lr
+            A[n, c0:n] = np.linalg.solve(Lr, A[n, c0:n])
+            A[n, n] = 1.0
+
+    def update(k, J):
+        c0, c1 = k * pw, min((k + 1) * pw, n + 1)
+        j0, j1 = J * pw, min((J + 1) * pw, n + 1)
+        Lk = A[c0:n + 1, c0:c1]
+        A[j0:n + 1, j0:j1] -= Lk[j0 - c0:, :] @ Lk[j0 - c0:j1 - c0, :].T
+
+    reduce_panel(0)
+    reduce_panel(1)
+    if rank == 0:
+        factor(0)
+    for k in range(npan):
+        c0 = k * pw
         buf = torch.zeros(count[k], dtype=torch.float64)
         if k % world == rank:
-            # the owner factors its (fully updated) panel: diagonal block,
-            # then the rows below against it (pivot n forced to 1, as the
-            # device factor takes it)
-            D = A[c0:c1, c0:c1]
-            L = np.linalg.cholesky(np.tril(D) + np.tril(D, -1).T) if c1 <= n else None
-            if L is None:  # the last panel holds row n: factor the real part, z below it
-                m = n - c0
-                Lr = np.linalg.cholesky(np.tril(D[:m, :m]) + np.tril(D[:m, :m], -1).T)
-                A[c0:n, c0:n] = Lr
-                A[n, c0:n] = np.linalg.solve(Lr, A[n, c0:n])
-                A[n, n] = 1.0
-            else:
-                A[c0:c1, c0:c1] = L
-                A[c1:n + 1, c0:c1] = np.linalg.solve(L, A[c1:n + 1, c0:c1].T).T
             _pack(A, n, pw, k, buf.numpy(), 0)
         dist.broadcast(buf, src=k % world)
+        reduce_panel(k + 2)
         if k % world != rank:
             _unpack(A, n, pw, k, buf.numpy(), 0)
-        # this rank's later panels take panel k's update
-        Lk = A[c0:n + 1, c0:c1]
-        for J in range(k + 1, npan):
-            if J % world != rank:
-                continue
-            j0, j1 = J * pw, min((J + 1) * pw, n + 1)
-            A[j0:n + 1, j0:j1] -= Lk[j0 - c0:, :] @ Lk[j0 - c0:j1 - c0, :].T
+        # look-ahead: the next owner's panel first, then the rest
+        if k + 1 < npan and (k + 1) % world == rank:
+            update(k, k + 1)
+            factor(k + 1)
+        for J in range(k + 2, npan):
+            if J % world == rank:
+                update(k, J)
     # replicated back substitution L^T y = z
     L = np.tril(A[:n, :n])
     y = np.linalg.solve(L.T, A[n, :n])
@@ -183,10 +209,12 @@ def _dist_worker(rank, world, port, q, pw):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,pw", [(2, 8), (2, 16), (3, 8)])
 def test_distributed_factor_protocol_equals_global_solve(world, pw):
-    """Reduce-scatter of the ranks' partial systems into block-cyclic panels,
-    per panel the owner's factor + a broadcast, every rank updating its own
-    later panels: every rank ends with the factor of the global system and
-    the same solution as np.linalg.solve on it."""
+    """The ranks' partial systems reduced panel by panel into the owners of
+    block-cyclic panels (the owner's own partial updated in place, the
+    others' sum added just before its factor), per panel the owner's factor
+    + a broadcast, every rank updating its own later panels in look-ahead
+    order: every rank ends with the factor of the global system and the same
+    solution as np.linalg.solve on it."""
     from sfm_amd import scene
     from oracle import ffi as O
     ctx = mp.get_context("spawn")

@@ -97,7 +97,12 @@ def _gloo_collectives(dist, torch, calls=None):
             calls["reduce_scatter"] = calls.get("reduce_scatter", 0) + 1
         dist.reduce_scatter_tensor(torch.from_numpy(out), torch.from_numpy(buf))
 
-    return allreduce, broadcast, reduce_scatter
+    def reduce(arr, root):
+        if calls is not None:
+            calls["reduce"] = calls.get("reduce", 0) + 1
+        dist.reduce(torch.from_numpy(arr), dst=root)
+
+    return allreduce, broadcast, reduce_scatter, reduce
 
 
 def _worker_body(rank, world, port, mode, dist_pt, q):
@@ -211,7 +216,7 @@ def _c4_worker_body(rank, world, port, dist_pt, q):
         rot, t, X = ba.parameters()
     if dist_pt:
         calls = {"n": dcalls.get("allreduce", 0), "max_count": dcalls.get("max_count", 0),
-                 "broadcast": dcalls.get("broadcast", 0), "reduce_scatter": dcalls.get("reduce_scatter", 0)}
+                 "broadcast": dcalls.get("broadcast", 0), "reduce": dcalls.get("reduce", 0)}
     q.put((rank, sm.num_iterations, sm.final_cost, [x["step_is_successful"] for x in tr],
            [x["cost"] for x in tr], rot, t, X, calls["n"], calls["max_count"], calls, sm.num_linear_solves))
     dist.barrier()
@@ -249,9 +254,9 @@ def _run_c4_ranks(world, dist_pt):
 def test_c4_distributed_factor_matches_single_rank(c4_single, world):
     """C4 in 2 / 3 landmark shards on one GPU with the DISTRIBUTED reduced-
     camera factor: the ranks' partial 12000x12000
-    systems reduce-scattered into 1-D block-cyclic panels of 4 tiles (47
-    panels), each factored by its owner and broadcast, every rank updating its
-    own later panels, the back substitution replicated.  Against the single-
+    systems reduced panel by panel into the owners of 1-D block-cyclic panels
+    of 4 tiles (47 panels), each factored by its owner and broadcast, every
+    rank updating its own later panels, the back substitution replicated.  Against the single-
     rank solve: the same accept/reject sequence, per-iteration and final
     cost within 1e-9, parameters within 1e-6, cameras bitwise equal across
     the ranks -- and no packed-S all-reduce went through the hook."""
@@ -267,7 +272,7 @@ def test_c4_distributed_factor_matches_single_rank(c4_single, world):
     for r in res:
         calls = r[10]
         assert r[9] <= 28 * C4_C                    # only the camera sums (U_c, b_c) and scalars were all-reduced
-        assert calls["reduce_scatter"] == r[11]     # one per linear solve
+        assert calls["reduce"] == r[11] * panels    # one per panel and linear solve
         assert calls["broadcast"] == r[11] * panels
         assert r[1] == sm.num_iterations
         assert r[3] == [x["step_is_successful"] for x in tr]

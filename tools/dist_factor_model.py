@@ -3,9 +3,11 @@ designs, from parts MEASURED on one MI355X:
 
 * the replicated design: every rank factors the all-reduced 12000^2 system
   (its factor time is the measured single-GPU one);
-* the distributed design (sfm_ba_set_distributed_factor): reduce-scatter into
-  1-D block-cyclic panels, per panel the owner's factor + broadcast, every
-  rank's updates of its own later panels.  Each rank's device work at N ranks
+* the distributed design (sfm_ba_set_distributed_factor): 1-D block-cyclic
+  panels, per panel the owner's factor + broadcast, every rank's updates of
+  its own later panels; three schedules: "sequential" and "lookahead" with an
+  up-front reduce-scatter (round 5's first two versions), "pipelined" with
+  the per-panel reduces on the collective stream (what is built).  Each rank's device work at N ranks
   is timed on this GPU by sfm_dist_factor_profile (per panel: the owner's
   factor and pack, a receiver's unpack, every rank's updates);
 * the sharded rest of the solve (point passes, Schur, Jacobian ...) from a
@@ -113,8 +115,30 @@ def factor_model(n, nranks, pt, bw):
         chain += (fac[k] + pack[k]) * ms + bcast[k] + (unpack[k] * ms if nranks > 1 else 0.0)
     bulk = upd.sum(axis=1).max() * ms + sum(fac[k] for k in range(np_)) * ms / nranks
     look = rs + rs_copy + max(chain, bulk) + misc[2] * ms
-    return {"sequential_s": seq, "lookahead_s": look, "chain_s": chain, "bulk_s": bulk,
-            "reduce_scatter_s": rs, "broadcast_s": float(bcast.sum()), "factor_s_sum": float(fac.sum() * ms),
+    # what is built (round 5): the partial panels reduced one by one into
+    # their owners on the collective stream (reduce 0, reduce 1, then per k:
+    # broadcast k, reduce k+2), the owner adding the others' sum just before
+    # it factors the panel; the up-front reduce-scatter leaves the chain.
+    # Step k: broadcast k, then the longer of reduce k+2 (collective stream)
+    # and the next owner's unpack + update of its panel + add + factor + pack.
+    red = LAT_S + (pb - 8.0 * (pt * 64 * 64 + 1)) / bw if nranks > 1 else np.zeros(np_)
+    add = 1.5 * unpack
+    pipe = misc[0] * ms                                  # packing the partial panels (all of them)
+    if np_:
+        pipe += (red[0] if nranks > 1 else 0.0) + (add[0] * ms if nranks > 1 else 0.0) + (fac[0] + pack[0]) * ms
+    for k in range(np_):
+        nxt = 0.0
+        if k + 1 < np_:
+            own = (k + 1) % nranks
+            tot, first = own_tiles_after(nblk, pt, k, nranks, own)
+            nxt = ((unpack[k] if nranks > 1 else 0.0) + upd[own, k] * (first / tot if tot else 0.0)
+                   + (add[k + 1] if nranks > 1 else 0.0) + fac[k + 1] + pack[k + 1]) * ms
+        r2 = red[k + 2] if (nranks > 1 and k + 2 < np_) else 0.0
+        pipe += bcast[k] + max(r2, nxt)
+    pipe = max(pipe, bulk) + misc[2] * ms
+    return {"sequential_s": seq, "lookahead_s": look, "pipelined_s": pipe, "chain_s": chain, "bulk_s": bulk,
+            "reduce_scatter_s": rs, "broadcast_s": float(bcast.sum()), "panel_reduces_s": float(np.sum(red)),
+            "factor_s_sum": float(fac.sum() * ms),
             "updates_s_max_rank": float(upd.sum(axis=1).max() * ms), "backsub_s": misc[2] * ms,
             "fail_bits": int(misc[3])}
 
@@ -151,7 +175,7 @@ def main():
             out["curves"][key] = {"replicated_ms": rep * 1e3, "replicated_speedup": solve_s / rep}
             for pt in a.pt:
                 f = factor_model(N_SYS, N, pt, bw)
-                for sch in ("sequential", "lookahead"):
+                for sch in ("sequential", "lookahead", "pipelined"):
                     t = ITERS * f[f"{sch}_s"] + rest / N
                     out["curves"][key][f"dist_pt{pt}_{sch}_ms"] = t * 1e3
                     out["curves"][key][f"dist_pt{pt}_{sch}_speedup"] = solve_s / t
