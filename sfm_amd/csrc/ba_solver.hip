@@ -2257,13 +2257,16 @@ int sfm_dist_factor_profile(int32_t device, int32_t n, int32_t nranks, int32_t p
     for (int k = 0; k < np; ++k) {
       const int owner = k % nranks, t0 = k * pt, ncols = std::min(pt, d.nblk - t0);
       const int c0 = t0 * kNB, c1 = c0 + ncols * kNB;
+      if (owner != rank) {  // a zero L for the panels this rank receives: its own panels stay SPD
+        const int64_t cols = std::min(c1, n + 1) - c0;
+        HIPCHK(hipMemsetAsync(buf + tot, 0, sizeof(double) * (cols * (n + 1 - c0) + int64_t(ncols) * kNB * kNB + 1), s));
+      }
       HIPCHK(hipEventRecord(ev[8 + 4 * k], s));
       if (owner == rank) {
         launch_cholesky_panel(d, k, pt, ++epoch, s);
         HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
         launch_panel_copy(d, kPanelPack, pt, c0, c1, nullptr, tot, buf, s);
       } else {
-        // (from the owner's last packed L, or zeros: every pivot stays positive)
         HIPCHK(hipEventRecord(ev[8 + 4 * k + 1], s));
         launch_panel_copy(d, kPanelUnpack, pt, c0, c1, nullptr, tot, buf, s);
       }
