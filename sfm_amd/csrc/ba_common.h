@@ -144,11 +144,38 @@ __device__ __forceinline__ void cam_update_one(int c, const double* __restrict__
 // trades the other half with its partner, then the two lanes of a pair add
 // once more.  32 shuffles instead of 32 x 6; lane l returns the sum of
 // value l >> 1 over the wave (fixed order: deterministic).
+// Distances 32 and 16 (24 of the 31 traded values) go through gfx950's
+// half-wave / row swaps: swapping the upper half of v[j] with the lower half
+// of v[h + j] leaves each lane its own kept value and its partner's in the
+// two registers, so no select and no LDS crossbar; the sum is the same pair
+// of values either way.  Distances 8..2 trade through ds_bpermute.
 // (The halves are picked with bit masks: a select between two array
 // elements becomes a select of addresses and pushes the array to scratch.)
+__device__ __forceinline__ void swap_halves32(double& x, double& y) {  // x lanes 32..63 <-> y lanes 0..31
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(y), false, false);
+  x = __hiloint2double(hi[0], lo[0]);
+  y = __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ void swap_rows16(double& x, double& y) {  // x odd 16-lane rows <-> y even rows
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(y), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(y), false, false);
+  x = __hiloint2double(hi[0], lo[0]);
+  y = __hiloint2double(hi[1], lo[1]);
+}
 __device__ __forceinline__ double wave_sum32(double (&v)[32], int l) {
 #pragma unroll
-  for (int h = 16; h >= 1; h >>= 1) {
+  for (int j = 0; j < 16; ++j) {  // distance 32: lanes 0..31 keep v[0..16), 32..63 v[16..32)
+    swap_halves32(v[j], v[16 + j]);
+    v[j] = v[j] + v[16 + j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // distance 16: even rows keep v[0..8), odd rows v[8..16)
+    swap_rows16(v[j], v[8 + j]);
+    v[j] = v[j] + v[8 + j];
+  }
+#pragma unroll
+  for (int h = 4; h >= 1; h >>= 1) {
     const uint64_t m = (l & (2 * h)) ? ~0ull : 0ull;  // exchange distance 2h
 #pragma unroll
     for (int j = 0; j < h; ++j) {

@@ -9,6 +9,8 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <utility>
+#include "svd_schedule.h"
 
 namespace sfm {
 namespace {
@@ -29,19 +31,10 @@ __host__ __device__ __forceinline__ unsigned cv_rng_next(uint64_t& state) {
 // In place on At (= A^T, N rows of length M); kV = false skips the right
 // singular vectors (Vt is then not touched): EPnP needs only U of M^T M,
 // and without the second 12x12 array the kernel stays in registers.
+// The sweeps (until one rotates nothing, at most max(M, 30)), in OpenCV's
+// order, one rotation after another.
 template <int M, int N, bool kV>
-__host__ __device__ void cv_svd_at(double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
-  double W[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double sd = 0.0;
-#pragma unroll
-    for (int k = 0; k < M; ++k) sd += U[i][k] * U[i][k];
-    W[i] = sd;
-    if (kV)
-#pragma unroll
-      for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
-  }
+__host__ __device__ void cv_svd_sweeps(double (&U)[N][M], double (&W)[N], double (&Vt)[N][N]) {
   const double eps = kDblEps * 10;
   for (int iter = 0; iter < (M > 30 ? M : 30); ++iter) {
     bool changed = false;
@@ -85,6 +78,188 @@ __host__ __device__ void cv_svd_at(double (&U)[N][M], double (&w)[N], double (&V
       }
     if (!changed) break;
   }
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The same sweeps with one row per lane (lane r < N holds row r of At, of
+// Vt and W_r), for the 4- and 5-row SVDs of the EPnP beta cases: two
+// rotations on disjoint rows per pass, the tail of sweep s overlapped with
+// the head of sweep s + 1 once sweep s has rotated something
+// (svd_schedule.h, tools/svd_schedule.py; the 12x12 of pnp_kernels.hip
+// cv_svd12_lanes does the same with four 16-lane rotations).  Both lanes of
+// a rotation fetch the partner's row and compute the same p, c, s (the
+// products commute, the sums keep OpenCV's order); lane i keeps c*U_i +
+// s*U_j, lane j -s*U_i + c*U_j, exactly the sequential rotation's values.
+template <int N, int S>
+struct LaneSched;
+#define SFM_LANE_SCHED(NR, SS, NAME)                         \
+  template <>                                                \
+  struct LaneSched<NR, SS> {                                 \
+    static constexpr int P = kSvd##NAME##Passes;             \
+    static constexpr const int* Nr = kSvd##NAME##N;          \
+    static constexpr const int (*I)[2] = kSvd##NAME##I;      \
+    static constexpr const int (*J)[2] = kSvd##NAME##J;      \
+    static constexpr const int (*T)[2] = kSvd##NAME##T;      \
+  };
+SFM_LANE_SCHED(4, 0, L4Pro)
+SFM_LANE_SCHED(4, 1, L4Per)
+SFM_LANE_SCHED(4, 2, L4Epi)
+SFM_LANE_SCHED(5, 0, L5Pro)
+SFM_LANE_SCHED(5, 1, L5Per)
+SFM_LANE_SCHED(5, 2, L5Epi)
+#undef SFM_LANE_SCHED
+
+__device__ __forceinline__ void cvl_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int M, int N, int S, int ps>
+__device__ __forceinline__ void lane_pass(int r, double (&u)[M], double (&v)[N], double& wr, bool (&ch)[2]) {
+  using Sc = LaneSched<N, S>;
+  constexpr int n = Sc::Nr[ps];
+  constexpr int i0 = Sc::I[ps][0], j0 = Sc::J[ps][0], i1 = Sc::I[ps][1], j1 = Sc::J[ps][1];
+  constexpr uint64_t kTag1 = (Sc::T[ps][0] ? (1ull << i0) | (1ull << j0) : 0) |
+                             (n > 1 && Sc::T[ps][1] ? (1ull << i1) | (1ull << j1) : 0);
+  int partner = r;
+  bool lo = false;
+  if (r == i0) { partner = j0; lo = true; }
+  if (r == j0) partner = i0;
+  if (n > 1 && r == i1) { partner = j1; lo = true; }
+  if (n > 1 && r == j1) partner = i1;
+  double pu[M], pv[N];
+#pragma unroll
+  for (int k = 0; k < M; ++k) pu[k] = __shfl(u[k], partner);
+#pragma unroll
+  for (int k = 0; k < N; ++k) pv[k] = __shfl(v[k], partner);
+  const double pw = __shfl(wr, partner);
+  double p = 0.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) p += u[k] * pu[k];
+  const double a = lo ? wr : pw, b = lo ? pw : wr;
+  const bool act = partner != r && !(fabs(p) <= kDblEps * 10 * sqrt(a * b));
+  const uint64_t turned = __builtin_amdgcn_ballot_w64(act);
+  if (turned == 0) return;
+  if (turned & kTag1) ch[1] = true;
+  if (turned & ~kTag1) ch[0] = true;
+  p *= 2;
+  const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+  // the two cases of the rotation with their operands selected (see
+  // cv_svd_sweeps): the same operations on the same values either way
+  const bool neg = beta < 0;
+  const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+  const double den = neg ? gamma : gamma * 2;
+  const double s1 = sqrt(num / den);
+  const double o = p / (gamma * s1 * 2);
+  const double c = neg ? o : s1, s = neg ? s1 : o;
+  const double ca = lo ? c : -s, cb = lo ? s : c;  // lane i: c U_i + s U_j; lane j: -s U_i + c U_j
+  double nu[M], nv[N], nw = 0.0;
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    const double t = ca * (lo ? u[k] : pu[k]) + cb * (lo ? pu[k] : u[k]);
+    nu[k] = t;
+    nw += t * t;
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) nv[k] = ca * (lo ? v[k] : pv[k]) + cb * (lo ? pv[k] : v[k]);
+  if (act) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) u[k] = nu[k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = nv[k];
+    wr = nw;
+  }
+}
+template <int M, int N, int S, int... ps>
+__device__ __forceinline__ void lane_run(int r, double (&u)[M], double (&v)[N], double& wr, bool (&ch)[2],
+                                         std::integer_sequence<int, ps...>) {
+  (lane_pass<M, N, S, ps>(r, u, v, wr, ch), ...);
+}
+template <int M, int N, int S>
+__device__ __forceinline__ void lane_run(int r, double (&u)[M], double (&v)[N], double& wr, bool (&ch)[2]) {
+  lane_run<M, N, S>(r, u, v, wr, ch, std::make_integer_sequence<int, LaneSched<N, S>::P>{});
+}
+
+// lds: N (M + N) doubles of this wave's LDS
+template <int M, int N>
+__device__ void cv_svd_sweeps_lanes(double (&U)[N][M], double (&W)[N], double (&Vt)[N][N], double* lds) {
+  const int r = threadIdx.x & 63;
+  double u[M], v[N], wr = W[0];
+#pragma unroll
+  for (int k = 0; k < M; ++k) u[k] = U[0][k];
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    wr = r == i ? W[i] : wr;
+#pragma unroll
+    for (int k = 0; k < M; ++k) u[k] = r == i ? U[i][k] : u[k];
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = r == k ? 1.0 : 0.0;  // (Vt = I on entry)
+  constexpr int kSweeps = M > 30 ? M : 30;
+  bool ch[2] = {false, false}, head = true;
+  for (int s = 0;;) {
+    if (head) lane_run<M, N, 0>(r, u, v, wr, ch);  // head of sweep s (tag 1)
+    head = false;
+    if (ch[1] && s + 1 < kSweeps) {  // sweep s has turned: its tail with sweep s + 1's head
+      ch[0] = ch[1] = false;
+      lane_run<M, N, 1>(r, u, v, wr, ch);
+      ++s;
+    } else {
+      const bool turned = ch[1];
+      ch[0] = false;
+      lane_run<M, N, 2>(r, u, v, wr, ch);  // tail of sweep s (tag 0)
+      if (!(turned || ch[0]) || ++s >= kSweeps) break;
+      ch[1] = false;
+      head = true;
+    }
+  }
+  cvl_wave_sync();  // (earlier readers of this LDS slice done)
+  if (r < N) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) lds[r * (M + N) + k] = u[k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) lds[r * (M + N) + M + k] = v[k];
+  }
+  cvl_wave_sync();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) U[i][k] = lds[i * (M + N) + k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) Vt[i][k] = lds[i * (M + N) + M + k];
+  }
+  cvl_wave_sync();  // (read before the slice is reused)
+}
+#endif
+
+// lds (device, kV, N = 4 or 5): the sweeps one row per lane through this
+// wave's LDS slice of N (M + N) doubles; nullptr: one rotation after another.
+template <int M, int N, bool kV>
+__host__ __device__ void cv_svd_at(double (&U)[N][M], double (&w)[N], double (&Vt)[N][N], double* lds = nullptr) {
+  double W[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double sd = 0.0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) sd += U[i][k] * U[i][k];
+    W[i] = sd;
+    if (kV)
+#pragma unroll
+      for (int k = 0; k < N; ++k) Vt[i][k] = i == k ? 1.0 : 0.0;
+  }
+  const double eps = kDblEps * 10;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kV && (N == 4 || N == 5)) {
+    if (lds) cv_svd_sweeps_lanes<M, N>(U, W, Vt, lds);
+    else cv_svd_sweeps<M, N, kV>(U, W, Vt);
+  } else {
+    cv_svd_sweeps<M, N, kV>(U, W, Vt);
+  }
+#else
+  (void)lds;
+  cv_svd_sweeps<M, N, kV>(U, W, Vt);
+#endif
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double sd = 0.0;
@@ -149,20 +324,22 @@ __host__ __device__ void cv_svd_at(double (&U)[N][M], double (&w)[N], double (&V
 
 // cv::SVD of A itself (A is copied transposed into U first).
 template <int M, int N>
-__host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], double (&w)[N], double (&Vt)[N][N]) {
+__host__ __device__ void cv_svd(const double (&A)[M][N], double (&U)[N][M], double (&w)[N], double (&Vt)[N][N],
+                                double* lds = nullptr) {
 #pragma unroll
   for (int i = 0; i < N; ++i)
 #pragma unroll
     for (int k = 0; k < M; ++k) U[i][k] = A[k][i];
-  cv_svd_at<M, N, true>(U, w, Vt);
+  cv_svd_at<M, N, true>(U, w, Vt, lds);
 }
 
 // cv::solve(A, b, x, DECOMP_SVD) = SVBkSb: x = sum over w_i > 2 DBL_EPSILON
 // sum(w) of (u_i . b / w_i) v_i, in descending-w order.
 template <int M, int N>
-__host__ __device__ void cv_lstsq(const double (&A)[M][N], const double (&b)[M], double (&x)[N]) {
+__host__ __device__ void cv_lstsq(const double (&A)[M][N], const double (&b)[M], double (&x)[N],
+                                  double* lds = nullptr) {
   double U[N][M], w[N], Vt[N][N];
-  cv_svd<M, N>(A, U, w, Vt);
+  cv_svd<M, N>(A, U, w, Vt, lds);
   double thr = 0.0;
 #pragma unroll
   for (int i = 0; i < N; ++i) thr += w[i];

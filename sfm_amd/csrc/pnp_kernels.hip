@@ -21,6 +21,7 @@
 // bound only shrinks, so evaluating the full bound and replaying gives the
 // sequential result exactly) and compacts the winner's inliers in order.
 #include <hip/hip_runtime.h>
+#include <utility>
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -98,8 +99,9 @@ __host__ __device__ void rodrigues_m2v(const double R[9], double r[3]) {
 // trip.
 template <int kCtrl>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), kCtrl, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), kCtrl, 0xF, 0xF, false);
+  // (every lane of a row rotation is written: no "old" operand to set up)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), kCtrl, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double tree16(double v) {
@@ -111,28 +113,89 @@ __device__ __forceinline__ double tree16(double v) {
   return v;
 }
 
-// One Jacobi sweep in OpenCV's order (0,1), (0,2), ..., (10,11), scheduled
-// by row dependencies into 23 passes of up to 4 rotations on disjoint rows
-// (rotation (i, j) waits only for the rotations before it on rows i and j;
-// the critical path is 21 of them): the wave's four 16-lane rows each hold
-// the whole 12-row state and take one rotation of a pass, then exchange the
-// rotated rows.  Every rotation is the same arithmetic on the same values as
-// in the sequential sweep, so the result is bitwise OpenCV's order.  (A
+// The Jacobi sweeps in OpenCV's order (0,1), (0,2), ..., (10,11), sweep
+// after sweep, scheduled by row dependencies (a rotation (i, j) waits only
+// for the latest earlier rotation on row i and on row j, in its own sweep or
+// the one before) into passes of up to 4 rotations on disjoint rows
+// (svd_schedule.h, tools/svd_schedule.py): the wave's four 16-lane rows each
+// hold the whole 12-row state and take one rotation of a pass, then exchange
+// the rotated rows.  Every rotation is the same arithmetic on the same
+// values as in the sequential order, so the result is bitwise OpenCV's.  (A
 // branch-free sequential sweep, for the scheduler to overlap, measured
-// slower: 0.375-0.388 vs 0.313 ms per PnP call.)  Unused slots repeat slot 0.
-constexpr int kSvdPasses = 23;
-constexpr int kSvdN[kSvdPasses] = {1, 1, 2, 2, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 4, 3, 3, 3, 3, 2, 2, 1, 1};
-constexpr int kSvdI[kSvdPasses][4] = {
-    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 1, 0, 0}, {0, 1, 0, 0}, {0, 1, 2, 0}, {0, 1, 2, 0}, {0, 1, 2, 3}, {0, 1, 2, 3},
-    {0, 1, 2, 3}, {4, 0, 1, 2}, {3, 4, 0, 1}, {2, 3, 4, 5}, {1, 2, 3, 4}, {5, 2, 3, 4}, {5, 6, 3, 4}, {5, 6, 4, 5},
-    {5, 6, 7, 5}, {5, 6, 7, 5}, {6, 7, 8, 6}, {7, 8, 7, 7}, {8, 9, 8, 8}, {9, 9, 9, 9}, {10, 10, 10, 10}};
-constexpr int kSvdJ[kSvdPasses][4] = {
-    {1, 1, 1, 1}, {2, 2, 2, 2}, {3, 2, 3, 3}, {4, 3, 4, 4}, {5, 4, 3, 5}, {6, 5, 4, 6}, {7, 6, 5, 4}, {8, 7, 6, 5},
-    {9, 8, 7, 6}, {5, 10, 9, 8}, {7, 6, 11, 10}, {9, 8, 7, 6}, {11, 10, 9, 8}, {7, 11, 10, 9}, {8, 7, 11, 10},
-    {9, 8, 11, 9}, {10, 9, 8, 10}, {11, 10, 9, 11}, {11, 10, 9, 11}, {11, 10, 11, 11}, {11, 10, 11, 11},
-    {11, 11, 11, 11}, {11, 11, 11, 11}};
-__device__ __forceinline__ double sel4(int g, double a0, double a1, double a2, double a3) {
-  return g == 0 ? a0 : g == 1 ? a1 : g == 2 ? a2 : a3;
+// slower: 0.375-0.388 vs 0.313 ms per PnP call.)  One sweep alone is 23
+// passes; the tail of sweep s with the head of sweep s + 1 (run once sweep s
+// has rotated something, i.e. once sweep s + 1 is certain) is 18 for 66
+// rotations.  The slots of a pass with fewer than 4 rotations repeat (n = 1:
+// slot 0 everywhere, n = 2: 0 1 0 1, n = 3: 0 1 2 0), so a row pair / the
+// whole wave already agrees on them.
+// (svd_schedule.h comes with cv_linalg.h)
+template <int S>
+struct SvdSched;
+template <>
+struct SvdSched<0> {  // head of a sweep
+  static constexpr int P = kSvdProPasses;
+  static constexpr const int* N = kSvdProN;
+  static constexpr const int (*I)[4] = kSvdProI;
+  static constexpr const int (*J)[4] = kSvdProJ;
+  static constexpr const int (*T)[4] = kSvdProT;
+};
+template <>
+struct SvdSched<1> {  // tail of sweep s + head of sweep s + 1
+  static constexpr int P = kSvdPerPasses;
+  static constexpr const int* N = kSvdPerN;
+  static constexpr const int (*I)[4] = kSvdPerI;
+  static constexpr const int (*J)[4] = kSvdPerJ;
+  static constexpr const int (*T)[4] = kSvdPerT;
+};
+template <>
+struct SvdSched<2> {  // tail of a sweep
+  static constexpr int P = kSvdEpiPasses;
+  static constexpr const int* N = kSvdEpiN;
+  static constexpr const int (*I)[4] = kSvdEpiI;
+  static constexpr const int (*J)[4] = kSvdEpiJ;
+  static constexpr const int (*T)[4] = kSvdEpiT;
+};
+// row g's value of four: three independent selects on the row's masks
+// (a nested g == 0 ? : g == 1 ? ... became divergent branches)
+struct RowSel {
+  bool s1, s2, s3;
+};
+__device__ __forceinline__ double sel4(const RowSel& m, double a0, double a1, double a2, double a3) {
+  double r = m.s1 ? a1 : a0;
+  r = m.s2 ? a2 : r;
+  return m.s3 ? a3 : r;
+}
+
+// The rotated rows change hands across the wave's 16-lane rows with gfx950's
+// row swaps (lane k of one row with lane k of another, no LDS round trip):
+// pair16(x) = (x of the even, x of the odd row of my row pair), pair32(x) =
+// (x of my row in the lower, in the upper half of the wave).
+__device__ __forceinline__ double2 pair16(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return make_double2(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
+}
+__device__ __forceinline__ double2 pair32(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return make_double2(__hiloint2double(rh[0], rl[0]), __hiloint2double(rh[1], rl[1]));
+}
+// x of rows 0..3 at my lane (mod 16), for a pass of n rotations
+template <int n>
+__device__ __forceinline__ void gather_rows(double x, double (&v)[4]) {
+  if constexpr (n == 1) {
+    v[0] = v[1] = v[2] = v[3] = x;
+  } else if constexpr (n == 2) {
+    const double2 e = pair16(x);
+    v[0] = v[2] = e.x;
+    v[1] = v[3] = e.y;
+  } else {
+    const double2 e = pair16(x);
+    const double2 a = pair32(e.x), b = pair32(e.y);
+    v[0] = a.x; v[2] = a.y; v[1] = b.x; v[3] = b.y;
+  }
 }
 
 // u[i] = At[i][lane & 15] on entry (M^T M is symmetric); on return the
@@ -143,68 +206,91 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// lds: this wave's kSvdLds doubles (the pass exchange, then ut)
-constexpr int kSvdLds = 2 * 64 + 2 * 4;
+// lds: this wave's kSvdLds doubles (ut at the end of the 12x12; the rows of
+// the beta cases' 6x5 / 6x4 SVDs, cv_linalg.h cv_svd_sweeps_lanes)
+constexpr int kSvdLds = 5 * (6 + 5);
+// One pass of schedule S; ch[t] |= a rotation of tag t turned.
+template <int S, int ps>
+__device__ __forceinline__ void svd_pass(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2]) {
+  using Sc = SvdSched<S>;
+  constexpr int n = Sc::N[ps];
+  constexpr int I0 = Sc::I[ps][0], I1 = Sc::I[ps][1], I2 = Sc::I[ps][2], I3 = Sc::I[ps][3];
+  constexpr int J0 = Sc::J[ps][0], J1 = Sc::J[ps][1], J2 = Sc::J[ps][2], J3 = Sc::J[ps][3];
+  constexpr uint64_t kTag1 = (Sc::T[ps][0] ? 0xFFFFull : 0) | (Sc::T[ps][1] ? 0xFFFFull << 16 : 0) |
+                             (Sc::T[ps][2] ? 0xFFFFull << 32 : 0) | (Sc::T[ps][3] ? 0xFFFFull << 48 : 0);
+  // row g's rotation (I[g], J[g])
+  const double ui = sel4(g, u[I0], u[I1], u[I2], u[I3]);
+  const double uj = sel4(g, u[J0], u[J1], u[J2], u[J3]);
+  const double a = sel4(g, W[I0], W[I1], W[I2], W[I3]);
+  const double b = sel4(g, W[J0], W[J1], W[J2], W[J3]);
+  double p = tree16(ui * uj);
+  const bool act = !(fabs(p) <= eps * sqrt(a * b));
+  const uint64_t turned = __builtin_amdgcn_ballot_w64(act);
+  if (turned == 0) return;  // every rotation of the pass skipped
+  if (turned & kTag1) ch[1] = true;
+  if (turned & ~kTag1) ch[0] = true;
+  p *= 2;
+  const double beta = a - b, gamma = sqrt(p * p + beta * beta);
+  // JacobiSVDImpl_'s two cases with their operands selected, not branched
+  // (rows of the wave take either): beta < 0: sn = sqrt(((gamma - beta) *
+  // 0.5) / gamma), c = p / (gamma * sn * 2); else c = sqrt((gamma + beta) /
+  // (gamma * 2)), sn = p / (gamma * c * 2) -- the same operations on the
+  // same values either way.
+  const bool neg = beta < 0;
+  const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+  const double den = neg ? gamma : gamma * 2;
+  const double s1 = sqrt(num / den);
+  const double o = p / (gamma * s1 * 2);
+  const double c = neg ? o : s1, sn = neg ? s1 : o;
+  double t0 = c * ui + sn * uj, t1 = -sn * ui + c * uj;
+  double w0 = tree16(t0 * t0), w1 = tree16(t1 * t1);
+  t0 = act ? t0 : ui;
+  t1 = act ? t1 : uj;
+  w0 = act ? w0 : a;
+  w1 = act ? w1 : b;
+  double vt0[4], vt1[4], vw0[4], vw1[4];
+  gather_rows<n>(t0, vt0);
+  gather_rows<n>(t1, vt1);
+  gather_rows<n>(w0, vw0);
+  gather_rows<n>(w1, vw1);
+  u[I0] = vt0[0]; u[J0] = vt1[0]; W[I0] = vw0[0]; W[J0] = vw1[0];
+  if constexpr (n > 1) { u[I1] = vt0[1]; u[J1] = vt1[1]; W[I1] = vw0[1]; W[J1] = vw1[1]; }
+  if constexpr (n > 2) { u[I2] = vt0[2]; u[J2] = vt1[2]; W[I2] = vw0[2]; W[J2] = vw1[2]; }
+  if constexpr (n > 3) { u[I3] = vt0[3]; u[J3] = vt1[3]; W[I3] = vw0[3]; W[J3] = vw1[3]; }
+}
+template <int S, int... ps>
+__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2],
+                                        std::integer_sequence<int, ps...>) {
+  (svd_pass<S, ps>(g, u, W, eps, ch), ...);
+}
+template <int S>
+__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2]) {
+  svd_run<S>(g, u, W, eps, ch, std::make_integer_sequence<int, SvdSched<S>::P>{});
+}
 __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]) {
   const int k = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
-  double2* xt = reinterpret_cast<double2*>(lds);   // [4 rows][16 lanes] (t0, t1)
-  double2* xw = reinterpret_cast<double2*>(lds + 128);  // [4 rows] (W_i, W_j)
+  const RowSel gs{g == 1, g == 2, g == 3};
   double W[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) W[i] = tree16(u[i] * u[i]);
   const double eps = kDblEps * 10;
-  for (int iter = 0; iter < 30; ++iter) {
-    bool changed = false;
-#pragma unroll
-    for (int ps = 0; ps < kSvdPasses; ++ps) {
-      const int n = kSvdN[ps];
-      const int* I = kSvdI[ps];
-      const int* J = kSvdJ[ps];
-      // row g's rotation (I[g], J[g]); rows g >= n idle
-      const double ui = sel4(g, u[I[0]], u[I[1]], u[I[2]], u[I[3]]);
-      const double uj = sel4(g, u[J[0]], u[J[1]], u[J[2]], u[J[3]]);
-      const double a = sel4(g, W[I[0]], W[I[1]], W[I[2]], W[I[3]]);
-      const double b = sel4(g, W[J[0]], W[J[1]], W[J[2]], W[J[3]]);
-      double p = tree16(ui * uj);
-      const bool act = g < n && !(fabs(p) <= eps * sqrt(a * b));
-      if (__builtin_amdgcn_ballot_w64(act) == 0) continue;  // every rotation of the pass skipped
-      changed = true;
-      p *= 2;
-      const double beta = a - b, gamma = sqrt(p * p + beta * beta);
-      double c, sn;
-      if (beta < 0) {
-        const double delta = (gamma - beta) * 0.5;
-        sn = sqrt(delta / gamma);
-        c = p / (gamma * sn * 2);
-      } else {
-        c = sqrt((gamma + beta) / (gamma * 2));
-        sn = p / (gamma * c * 2);
-      }
-      double t0 = c * ui + sn * uj, t1 = -sn * ui + c * uj;
-      double w0 = tree16(t0 * t0), w1 = tree16(t1 * t1);
-      t0 = act ? t0 : ui;
-      t1 = act ? t1 : uj;
-      w0 = act ? w0 : a;
-      w1 = act ? w1 : b;
-      // every row takes every rotated pair of the pass (lane k of row q holds
-      // column k of rows I[q], J[q]) through the wave's LDS slice: one
-      // 16-B write per lane, one 16-B read per rotation (the W pair a
-      // broadcast read), instead of 8 ds_bpermute per rotation
-      xt[16 * g + k] = make_double2(t0, t1);
-      if (k == 0) xw[g] = make_double2(w0, w1);
-      wave_sync();
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q >= n) break;
-        const double2 tq = xt[16 * q + k], wq = xw[q];
-        u[I[q]] = tq.x;
-        u[J[q]] = tq.y;
-        W[I[q]] = wq.x;
-        W[J[q]] = wq.y;
-      }
-      wave_sync();  // (the reads done before the next pass writes)
+  // sweep s runs iff s < 30 and sweeps 0..s-1 each rotated something
+  bool ch[2] = {false, false}, head = true;
+  for (int s = 0;;) {
+    if (head) svd_run<0>(gs, u, W, eps, ch);  // head of sweep s (tag 1)
+    head = false;
+    if (ch[1] && s + 1 < 30) {  // sweep s has turned: its tail with sweep s + 1's head
+      ch[0] = ch[1] = false;
+      svd_run<1>(gs, u, W, eps, ch);
+      ++s;
+    } else {
+      const bool turned = ch[1];
+      ch[0] = false;
+      svd_run<2>(gs, u, W, eps, ch);  // tail of sweep s (tag 0)
+      if (!(turned || ch[0]) || ++s >= 30) break;
+      ch[1] = false;
+      head = true;
     }
-    if (!changed) break;
   }
   int ord[12];
 #pragma unroll
@@ -256,13 +342,10 @@ __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]
     const double sc = sd > kDblMin ? 1.0 / sd : 0.0;
     row[i] *= sc;
   }
-  wave_sync();  // (the last pass's exchange reads done)
   if (k < 12 && (threadIdx.x & 63) < 16)
 #pragma unroll
     for (int q = 0; q < 4; ++q) lds[q * 12 + k] = row[11 - q];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_sync();
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -555,17 +638,25 @@ __host__ __device__ void epnp5_common(const EpnpIn& in, const PnPCam& k, double*
 #if defined(__HIP_DEVICE_COMPILE__)
     // lane col (mod 16) holds column col of M^T M = entry col of every row of At
     const int col = threadIdx.x & 15;
+    double mc1[kModel], mc2[kModel];  // this lane's column of M (row p of M1 / M2)
+#pragma unroll
+    for (int p = 0; p < kModel; ++p) {
+      mc1[p] = 0.0;
+      mc2[p] = 0.0;
+#pragma unroll
+      for (int c = 0; c < 12; ++c) {
+        mc1[p] = c == col ? M1[p][c] : mc1[p];
+        mc2[p] = c == col ? M2[p][c] : mc2[p];
+      }
+    }
     double u[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       double acc = 0.0;
 #pragma unroll
       for (int p = 0; p < kModel; ++p) {
-        double mc1 = 0.0, mc2 = 0.0;
-#pragma unroll
-        for (int c = 0; c < 12; ++c) { mc1 = c == col ? M1[p][c] : mc1; mc2 = c == col ? M2[p][c] : mc2; }
-        acc = acc + M1[p][i] * mc1;
-        acc = acc + M2[p][i] * mc2;
+        acc = acc + M1[p][i] * mc1[p];
+        acc = acc + M2[p][i] * mc2[p];
       }
       u[i] = col < 12 ? acc : 0.0;
     }
@@ -610,7 +701,7 @@ __host__ __device__ void epnp5_common(const EpnpIn& in, const PnPCam& k, double*
 }
 
 __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, const EpnpCommon& cm, double R[9],
-                                      double t[3]) {
+                                      double t[3], double* lds = nullptr) {
   const double (&alpha)[kModel][4] = cm.alpha;
   const double (&ut)[4][12] = cm.ut;
   const double (&L)[6][10] = cm.L;
@@ -619,7 +710,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     double A4[6][4], b4[4];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { A4[i][0] = L[i][0]; A4[i][1] = L[i][1]; A4[i][2] = L[i][3]; A4[i][3] = L[i][6]; }
-    cv_lstsq<6, 4>(A4, rho, b4);
+    cv_lstsq<6, 4>(A4, rho, b4, lds);
     double be[4];
     if (b4[0] < 0) {
       be[0] = sqrt(-b4[0]); be[1] = -b4[1] / be[0]; be[2] = -b4[2] / be[0]; be[3] = -b4[3] / be[0];
@@ -632,7 +723,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     double A3[6][3], b3[3];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { A3[i][0] = L[i][0]; A3[i][1] = L[i][1]; A3[i][2] = L[i][2]; }
-    cv_lstsq<6, 3>(A3, rho, b3);
+    cv_lstsq<6, 3>(A3, rho, b3, lds);
     double be[4];
     if (b3[0] < 0) { be[0] = sqrt(-b3[0]); be[1] = b3[2] < 0 ? sqrt(-b3[2]) : 0.0; }
     else { be[0] = sqrt(b3[0]); be[1] = b3[2] > 0 ? sqrt(b3[2]) : 0.0; }
@@ -646,7 +737,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = 0; j < 5; ++j) A5[i][j] = L[i][j];
-    cv_lstsq<6, 5>(A5, rho, b5);
+    cv_lstsq<6, 5>(A5, rho, b5, lds);
     double be[4];
     if (b5[0] < 0) { be[0] = sqrt(-b5[0]); be[1] = b5[2] < 0 ? sqrt(-b5[2]) : 0.0; }
     else { be[0] = sqrt(b5[0]); be[1] = b5[2] > 0 ? sqrt(b5[2]) : 0.0; }
@@ -725,7 +816,7 @@ __global__ __launch_bounds__(192) void k_pnp_epnp(const double* __restrict__ obj
   EpnpCommon cm;
   epnp5_common(in, k, lds[w], cm);
   double R[9], t[3], r[3];
-  const double e = epnp5_case(w, in, k, cm, R, t);
+  const double e = epnp5_case(w, in, k, cm, R, t, lds[w]);
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) res[w][i] = R[i];
