@@ -133,10 +133,14 @@ __device__ __forceinline__ void lane_pass(int r, double (&u)[M], double (&v)[N],
   for (int k = 0; k < M; ++k) pu[k] = __shfl(u[k], partner);
 #pragma unroll
   for (int k = 0; k < N; ++k) pv[k] = __shfl(v[k], partner);
-  const double pw = __shfl(wr, partner);
-  double p = 0.0;
+  // the partner's W is the sum of squares of its row in order (as set after
+  // its last rotation, or initially): recomputed here, not fetched
+  double p = 0.0, pw = 0.0;
 #pragma unroll
-  for (int k = 0; k < M; ++k) p += u[k] * pu[k];
+  for (int k = 0; k < M; ++k) {
+    p += u[k] * pu[k];
+    pw += pu[k] * pu[k];
+  }
   const double a = lo ? wr : pw, b = lo ? pw : wr;
   const bool act = partner != r && !(fabs(p) <= kDblEps * 10 * sqrt(a * b));
   const uint64_t turned = __builtin_amdgcn_ballot_w64(act);
@@ -153,16 +157,18 @@ __device__ __forceinline__ void lane_pass(int r, double (&u)[M], double (&v)[N],
   const double s1 = sqrt(num / den);
   const double o = p / (gamma * s1 * 2);
   const double c = neg ? o : s1, s = neg ? s1 : o;
-  const double ca = lo ? c : -s, cb = lo ? s : c;  // lane i: c U_i + s U_j; lane j: -s U_i + c U_j
+  // lane i: c U_i + s U_j; lane j: -s U_i + c U_j = c U_j + (-s) U_i (the
+  // sum commutes): both c * own + cb * partner, no per-entry select
+  const double cb = lo ? s : -s;
   double nu[M], nv[N], nw = 0.0;
 #pragma unroll
   for (int k = 0; k < M; ++k) {
-    const double t = ca * (lo ? u[k] : pu[k]) + cb * (lo ? pu[k] : u[k]);
+    const double t = c * u[k] + cb * pu[k];
     nu[k] = t;
     nw += t * t;
   }
 #pragma unroll
-  for (int k = 0; k < N; ++k) nv[k] = ca * (lo ? v[k] : pv[k]) + cb * (lo ? pv[k] : v[k]);
+  for (int k = 0; k < N; ++k) nv[k] = c * v[k] + cb * pv[k];
   if (act) {
 #pragma unroll
     for (int k = 0; k < M; ++k) u[k] = nu[k];

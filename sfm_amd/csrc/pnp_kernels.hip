@@ -208,10 +208,15 @@ __device__ __forceinline__ void wave_sync() {
 }
 // lds: this wave's kSvdLds doubles (ut at the end of the 12x12; the rows of
 // the beta cases' 6x5 / 6x4 SVDs, cv_linalg.h cv_svd_sweeps_lanes)
-constexpr int kSvdLds = 5 * (6 + 5);
+constexpr int kSvdLds = 6 * 10 + 6;  // (>= 5 (6 + 5): also L and rho for the Gauss-Newton rows)
 // One pass of schedule S; ch[t] |= a rotation of tag t turned.
+// JacobiSVDImpl_ keeps W_i = |row i|^2, set from the row itself after every
+// rotation of row i (and at the start), so W_i is always tree16(u_i * u_i)
+// of the current row, bitwise: the pass recomputes a = W_i and b = W_j from
+// the rows (two trees beside p's) instead of carrying W through the
+// exchange -- two trees fewer after the rotation, W never exchanged.
 template <int S, int ps>
-__device__ __forceinline__ void svd_pass(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2]) {
+__device__ __forceinline__ void svd_pass(const RowSel& g, double (&u)[12], double eps, bool (&ch)[2]) {
   using Sc = SvdSched<S>;
   constexpr int n = Sc::N[ps];
   constexpr int I0 = Sc::I[ps][0], I1 = Sc::I[ps][1], I2 = Sc::I[ps][2], I3 = Sc::I[ps][3];
@@ -221,8 +226,7 @@ __device__ __forceinline__ void svd_pass(const RowSel& g, double (&u)[12], doubl
   // row g's rotation (I[g], J[g])
   const double ui = sel4(g, u[I0], u[I1], u[I2], u[I3]);
   const double uj = sel4(g, u[J0], u[J1], u[J2], u[J3]);
-  const double a = sel4(g, W[I0], W[I1], W[I2], W[I3]);
-  const double b = sel4(g, W[J0], W[J1], W[J2], W[J3]);
+  const double a = tree16(ui * ui), b = tree16(uj * uj);
   double p = tree16(ui * uj);
   const bool act = !(fabs(p) <= eps * sqrt(a * b));
   const uint64_t turned = __builtin_amdgcn_ballot_w64(act);
@@ -243,58 +247,91 @@ __device__ __forceinline__ void svd_pass(const RowSel& g, double (&u)[12], doubl
   const double o = p / (gamma * s1 * 2);
   const double c = neg ? o : s1, sn = neg ? s1 : o;
   double t0 = c * ui + sn * uj, t1 = -sn * ui + c * uj;
-  double w0 = tree16(t0 * t0), w1 = tree16(t1 * t1);
   t0 = act ? t0 : ui;
   t1 = act ? t1 : uj;
-  w0 = act ? w0 : a;
-  w1 = act ? w1 : b;
-  double vt0[4], vt1[4], vw0[4], vw1[4];
+  double vt0[4], vt1[4];
   gather_rows<n>(t0, vt0);
   gather_rows<n>(t1, vt1);
-  gather_rows<n>(w0, vw0);
-  gather_rows<n>(w1, vw1);
-  u[I0] = vt0[0]; u[J0] = vt1[0]; W[I0] = vw0[0]; W[J0] = vw1[0];
-  if constexpr (n > 1) { u[I1] = vt0[1]; u[J1] = vt1[1]; W[I1] = vw0[1]; W[J1] = vw1[1]; }
-  if constexpr (n > 2) { u[I2] = vt0[2]; u[J2] = vt1[2]; W[I2] = vw0[2]; W[J2] = vw1[2]; }
-  if constexpr (n > 3) { u[I3] = vt0[3]; u[J3] = vt1[3]; W[I3] = vw0[3]; W[J3] = vw1[3]; }
+  u[I0] = vt0[0]; u[J0] = vt1[0];
+  if constexpr (n > 1) { u[I1] = vt0[1]; u[J1] = vt1[1]; }
+  if constexpr (n > 2) { u[I2] = vt0[2]; u[J2] = vt1[2]; }
+  if constexpr (n > 3) { u[I3] = vt0[3]; u[J3] = vt1[3]; }
 }
 template <int S, int... ps>
-__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2],
+__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double eps, bool (&ch)[2],
                                         std::integer_sequence<int, ps...>) {
-  (svd_pass<S, ps>(g, u, W, eps, ch), ...);
+  (svd_pass<S, ps>(g, u, eps, ch), ...);
 }
 template <int S>
-__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double (&W)[12], double eps, bool (&ch)[2]) {
-  svd_run<S>(g, u, W, eps, ch, std::make_integer_sequence<int, SvdSched<S>::P>{});
+__device__ __forceinline__ void svd_run(const RowSel& g, double (&u)[12], double eps, bool (&ch)[2]) {
+  svd_run<S>(g, u, eps, ch, std::make_integer_sequence<int, SvdSched<S>::P>{});
 }
 __device__ void cv_svd12_lanes(double (&u)[12], double* lds, double (&ut)[4][12]) {
   const int k = threadIdx.x & 15, g = (threadIdx.x & 63) >> 4;
   const RowSel gs{g == 1, g == 2, g == 3};
-  double W[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) W[i] = tree16(u[i] * u[i]);
   const double eps = kDblEps * 10;
   // sweep s runs iff s < 30 and sweeps 0..s-1 each rotated something
   bool ch[2] = {false, false}, head = true;
   for (int s = 0;;) {
-    if (head) svd_run<0>(gs, u, W, eps, ch);  // head of sweep s (tag 1)
+    if (head) svd_run<0>(gs, u, eps, ch);  // head of sweep s (tag 1)
     head = false;
     if (ch[1] && s + 1 < 30) {  // sweep s has turned: its tail with sweep s + 1's head
       ch[0] = ch[1] = false;
-      svd_run<1>(gs, u, W, eps, ch);
+      svd_run<1>(gs, u, eps, ch);
       ++s;
     } else {
       const bool turned = ch[1];
       ch[0] = false;
-      svd_run<2>(gs, u, W, eps, ch);  // tail of sweep s (tag 0)
+      svd_run<2>(gs, u, eps, ch);  // tail of sweep s (tag 0)
       if (!(turned || ch[0]) || ++s >= 30) break;
       ch[1] = false;
       head = true;
     }
   }
   int ord[12];
+  double W[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) { W[i] = sqrt(tree16(u[i] * u[i])); ord[i] = i; }
+  {
+    // Fast path: every W distinct and > DBL_MIN -- the selection sort below is
+    // then the descending order and completes nothing, and only rows 8..11
+    // (the four smallest) are kept: lane k < 12 ranks W_k, the rows of ranks
+    // 11..8 are picked by ballot, normalised and published.  (Ties or zero
+    // singular values -- e.g. planar points -- take the full path.)
+    double wk = W[0];
+#pragma unroll
+    for (int i = 1; i < 12; ++i) wk = k == i ? W[i] : wk;
+    int rank = 0;
+    bool tie = false;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      rank += W[i] > wk ? 1 : 0;
+      tie = tie || (i != k && W[i] == wk);
+    }
+    if (__builtin_amdgcn_ballot_w64(k < 12 && (tie || !(wk > kDblMin))) == 0) {
+      double rq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int src = __builtin_ctzll(__builtin_amdgcn_ballot_w64(k < 12 && rank == 11 - q) & 0xFFFull);
+        double x = u[0], sd = W[0];
+#pragma unroll
+        for (int c = 1; c < 12; ++c) {
+          x = src == c ? u[c] : x;
+          sd = src == c ? W[c] : sd;
+        }
+        rq[q] = x * (1.0 / sd);
+      }
+      if (k < 12 && (threadIdx.x & 63) < 16)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds[q * 12 + k] = rq[q];
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < 12; ++m) ut[q][m] = lds[q * 12 + m];
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 11; ++i) {
     int j = i;
@@ -515,24 +552,88 @@ __host__ __device__ double r_and_t(const EpnpIn& in, const double (&alpha)[kMode
   return sum / kModel;
 }
 
-__host__ __device__ void gauss_newton(const double (&L)[6][10], const double (&rho)[6], double b[4]) {
+// One row of epnp::compute_A_and_b_gauss_newton: A row i (4) and b_i.
+__host__ __device__ __forceinline__ void gn_row(const double* l, double rho_i, const double b[4], double A[4],
+                                                double& r) {
+  A[0] = 2 * l[0] * b[0] + l[1] * b[1] + l[3] * b[2] + l[6] * b[3];
+  A[1] = l[1] * b[0] + 2 * l[2] * b[1] + l[4] * b[2] + l[7] * b[3];
+  A[2] = l[3] * b[0] + l[4] * b[1] + 2 * l[5] * b[2] + l[8] * b[3];
+  A[3] = l[6] * b[0] + l[7] * b[1] + l[8] * b[2] + 2 * l[9] * b[3];
+  r = rho_i - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] + l[3] * b[0] * b[2] +
+               l[4] * b[1] * b[2] + l[5] * b[2] * b[2] + l[6] * b[0] * b[3] + l[7] * b[1] * b[3] +
+               l[8] * b[2] * b[3] + l[9] * b[3] * b[3]);
+}
+
+// epnp::gauss_newton: 5 iterations of compute_A_and_b + qr_solve.  lds
+// (device): the six rows of A and b are built one per lane (the same
+// arithmetic per row) and gathered through this wave's LDS slice (30
+// doubles), the wave-uniform QR solve then reads them -- a sixth of the
+// row-building instructions of the issue-bound wave.
+__host__ __device__ void gauss_newton(const double (&L)[6][10], const double (&rho)[6], double b[4],
+                                      double* lds = nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  {  // (every device caller passes its wave's slice)
+    const int ln = threadIdx.x & 63, i = ln < 6 ? ln : 0;
+    // lane i's row of L through the slice (a select chain over the rows
+    // becomes a dynamically indexed L, i.e. scratch)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (earlier readers of the slice done)
+    if (ln == 0) {
+#pragma unroll
+      for (int row = 0; row < 6; ++row) {
+#pragma unroll
+        for (int q = 0; q < 10; ++q) lds[10 * row + q] = L[row][q];
+        lds[60 + row] = rho[row];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double l[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) l[q] = lds[10 * i + q];
+    const double rho_i = lds[60 + i];
+    for (int it = 0; it < 5; ++it) {
+      double Ai[4], ri;
+      gn_row(l, rho_i, b, Ai, ri);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (the previous iteration's reads done)
+      if (ln < 6) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lds[5 * ln + q] = Ai[q];
+        lds[5 * ln + 4] = ri;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double A[6][4], r[6], x[4];
+#pragma unroll
+      for (int row = 0; row < 6; ++row) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[row][q] = lds[5 * row + q];
+        r[row] = lds[5 * row + 4];
+      }
+      if (!qr_solve(A, r, x)) break;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] += x[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (read before the slice is reused)
+  }
+#else
+  (void)lds;
   for (int it = 0; it < 5; ++it) {
     double A[6][4], r[6], x[4];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const double* l = L[i];
-      A[i][0] = 2 * l[0] * b[0] + l[1] * b[1] + l[3] * b[2] + l[6] * b[3];
-      A[i][1] = l[1] * b[0] + 2 * l[2] * b[1] + l[4] * b[2] + l[7] * b[3];
-      A[i][2] = l[3] * b[0] + l[4] * b[1] + 2 * l[5] * b[2] + l[8] * b[3];
-      A[i][3] = l[6] * b[0] + l[7] * b[1] + l[8] * b[2] + 2 * l[9] * b[3];
-      r[i] = rho[i] - (l[0] * b[0] * b[0] + l[1] * b[0] * b[1] + l[2] * b[1] * b[1] + l[3] * b[0] * b[2] +
-                       l[4] * b[1] * b[2] + l[5] * b[2] * b[2] + l[6] * b[0] * b[3] + l[7] * b[1] * b[3] +
-                       l[8] * b[2] * b[3] + l[9] * b[3] * b[3]);
-    }
+    for (int i = 0; i < 6; ++i) gn_row(L[i], rho[i], b, A[i], r[i]);
     if (!qr_solve(A, r, x)) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] += x[i];
   }
+#endif
 }
 
 // EPnP of one 5-point subset, in three parts: the control points, the
@@ -717,7 +818,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     } else {
       be[0] = sqrt(b4[0]); be[1] = b4[1] / be[0]; be[2] = b4[2] / be[0]; be[3] = b4[3] / be[0];
     }
-    gauss_newton(L, rho, be);
+    gauss_newton(L, rho, be, lds);
     return r_and_t(in, alpha, ut, be, k, R, t);
   } else if (N == 1) {
     double A3[6][3], b3[3];
@@ -729,7 +830,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     else { be[0] = sqrt(b3[0]); be[1] = b3[2] > 0 ? sqrt(b3[2]) : 0.0; }
     if (b3[1] < 0) be[0] = -be[0];
     be[2] = 0.0; be[3] = 0.0;
-    gauss_newton(L, rho, be);
+    gauss_newton(L, rho, be, lds);
     return r_and_t(in, alpha, ut, be, k, R, t);
   } else {
     double A5[6][5], b5[5];
@@ -744,7 +845,7 @@ __host__ __device__ double epnp5_case(int N, const EpnpIn& in, const PnPCam& k, 
     if (b5[1] < 0) be[0] = -be[0];
     be[2] = b5[3] / be[0];
     be[3] = 0.0;
-    gauss_newton(L, rho, be);
+    gauss_newton(L, rho, be, lds);
     return r_and_t(in, alpha, ut, be, k, R, t);
   }
 }
