@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include "ba_device.h"
 #include "ba_common.h"
 
@@ -486,9 +487,15 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_rc(int P, const int32_t
 // up to 64 cache lines: the texture-address path, not latency, bounds it
 // (index/constant prefetching measured no change).  From LDS the same values,
 // in the same arithmetic, are bitwise identical.
+// kGroups > 1 (C3-sized camera sets, whose 68-KB copy caps a 256-thread
+// workgroup at 2 waves per SIMD): one workgroup of kGroups x 256 threads
+// shares one copy, group g running the 256 points of virtual block
+// blockIdx.x * kGroups + g exactly as a 256-thread workgroup would (same
+// points, same per-block partials, reduced over its own four waves in
+// order), i.e. twice the waves per LDS copy and half the copies.
 constexpr int kCamE = 17;
-template <int kMaxC>
-__global__ __launch_bounds__(kThreads) void k_point_eval_lds(int P, int C, const int32_t* __restrict__ pt_off,
+template <int kMaxC, int kGroups = 1>
+__global__ __launch_bounds__(kThreads * kGroups) void k_point_eval_lds(int P, int C, const int32_t* __restrict__ pt_off,
                                                              const int32_t* __restrict__ cam_pm,
                                                              const double* __restrict__ uv_pm,
                                                              const double* __restrict__ camR,
@@ -501,29 +508,47 @@ __global__ __launch_bounds__(kThreads) void k_point_eval_lds(int P, int C, const
                                                              double* __restrict__ part_xn, const int* __restrict__ gate,
                                                              const CamFold cf) {
   if (gate && *gate == 0) return;  // device LM loop: phase skipped
+  static_assert(kGroups == 1 || kMaxC > 64, "the camera fold runs with one group per workgroup");
   const int nbp = (P + kThreads - 1) / kThreads;
-  if (int(blockIdx.x) >= nbp) {  // (cf.C > 0) the camera sums: one camera per wave, no barrier
+  if (kGroups == 1 && int(blockIdx.x) >= nbp) {  // (cf.C > 0) the camera sums: one camera per wave, no barrier
     const int c = (int(blockIdx.x) - nbp) * (kThreads / 64) + int(threadIdx.x >> 6);
     if (c < cf.C) cam_sum_body(c, threadIdx.x & 63, cf);
     return;
   }
-  __shared__ double sh[4];
+  __shared__ double sh[4 * kGroups];
   __shared__ double cst[kMaxC * kCamE];
   for (int i = threadIdx.x; i < C * kCamE; i += blockDim.x) {
     const int c = i / kCamE, j = i - c * kCamE;
     cst[i] = j < 9 ? camR[size_t(kCamR) * c + j] : j < 12 ? cam[6 * size_t(c) + 3 + (j - 9)] : Kc[5 * size_t(c) + (j - 12)];
   }
   __syncthreads();
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = int(threadIdx.x) / kThreads, tg = int(threadIdx.x) % kThreads;
+  const int vb = int(blockIdx.x) * kGroups + grp;  // the 256-thread block this group stands for
+  const int p = vb * kThreads + tg;
   double g = 0.0, xn = 0.0;
   if (p < P)
     point_eval_body(p, pt_off, cam_pm, uv_pm, CamView{cst, cst + 9, cst + 12, kCamE, kCamE, kCamE}, X, scale_p,
                     diag_p, ptV, min_diag, max_diag, mode, reuse, g, xn);
   if (mode == 1) {
-    const double rg = block_reduce(g, sh, true);
-    if (threadIdx.x == 0) part_grad[blockIdx.x] = rg;
-    const double rx = block_reduce(xn, sh, false);
-    if (threadIdx.x == 0) part_xn[blockIdx.x] = rx;
+    // block_reduce per group: its four waves' values combined in wave order
+    const int w = int(threadIdx.x) >> 6, l = int(threadIdx.x) & 63;
+    const double wg = wave_max(g), wx = wave_sum(xn);
+    if (l == 0) sh[w] = wg;
+    __syncthreads();
+    double rg = 0.0;
+    if (tg == 0) {
+      rg = sh[4 * grp];
+      for (int i = 1; i < 4; ++i) rg = fmax(rg, sh[4 * grp + i]);
+    }
+    __syncthreads();
+    if (l == 0) sh[w] = wx;
+    __syncthreads();
+    if (tg == 0 && vb < nbp) {
+      double rx = sh[4 * grp];
+      for (int i = 1; i < 4; ++i) rx = rx + sh[4 * grp + i];
+      part_grad[vb] = rg;
+      part_xn[vb] = rx;
+    }
   }
 }
 
@@ -1449,6 +1474,11 @@ void launch_cam_finalize(const DevProblem& d, int mode, bool reuse_diag, bool co
                                                                reuse_diag ? 1 : 0,
                                                                count_grad ? slot(d, kPGradCam) : nullptr, d.gate);
 }
+// A/B switch, read once (SFM_PE_GROUPS1=1: the 256-thread point pass).
+static bool env_flag_k(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '1';
+}
 void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream_t s) {
   if (d.P == 0) return;
   const int nb = blocks_for(d.P, kThreads);
@@ -1459,6 +1489,10 @@ void launch_point_eval(const DevProblem& d, int mode, bool reuse_diag, hipStream
                                                reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt), d.gate,    \
                                                CamFold{})
   if (d.C <= 64) SFM_PE_LDS(64);
+  else if (d.C <= 512 && !env_flag_k("SFM_PE_GROUPS1"))
+    k_point_eval_lds<512, 2><<<blocks_for(d.P, 2 * kThreads), 2 * kThreads, 0, s>>>(
+        d.P, d.C, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X, d.scale_p, d.diag_p, d.ptV, d.min_diag,
+        d.max_diag, mode, reuse_diag ? 1 : 0, slot(d, kPGradPt), slot(d, kPXNormPt), d.gate, CamFold{});
   else if (d.C <= 512) SFM_PE_LDS(512);
   else
     k_point_eval_rc<<<nb, kThreads, 0, s>>>(d.P, d.pt_off, d.cam_pm, d.uv_pm, d.camR, d.cam, d.Kc, d.X, d.scale_p,
