@@ -90,6 +90,25 @@ def test_solves_are_bitwise_reproducible():
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_grouped_point_pass_is_bitwise_the_single_group_pass(cfg, monkeypatch):
+    """k_point_eval_lds<512, 2> (two 256-thread groups sharing one camera
+    copy) against the 256-thread workgroups (SFM_PE_GROUPS1=1): the same
+    points and per-block partials, so the whole solve is bitwise the same."""
+    s = scene.config(cfg)
+    assert 64 < s.K.shape[0] <= 512
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SFM_PE_GROUPS1", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            out.append((sm.final_cost, tr, ba.parameters()))
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    for a, b in zip(out[0][2], out[1][2]):
+        assert np.array_equal(a, b)
+
+
 def test_packed_allreduce_path_is_exact(monkeypatch):
     s = scene.config("C1")
     with sfm_amd.BundleAdjuster() as ba:
