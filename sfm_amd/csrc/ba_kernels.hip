@@ -413,9 +413,16 @@ __device__ __forceinline__ void point_eval_body(int p, const int32_t* __restrict
   if (mode == 1)
     for (int k = 0; k < 3; ++k) sp[k] = scale_p[3 * size_t(p) + k];
   const int q0 = pt_off[p], q1 = pt_off[p + 1];
+  // the next observation's camera index and uv are loaded one step ahead
+  int c_n = q0 < q1 ? cam_pm[q0] : 0;
+  double2 uv_n = q0 < q1 ? ld2(uv_pm + 2 * size_t(q0)) : make_double2(0.0, 0.0);
   for (int q = q0; q < q1; ++q) {
-    const int c = cam_pm[q];
-    const double2 uvo = ld2(uv_pm + 2 * size_t(q));
+    const int c = c_n;
+    const double2 uvo = uv_n;
+    if (q + 1 < q1) {
+      c_n = cam_pm[q + 1];
+      uv_n = ld2(uv_pm + 2 * size_t(q + 1));
+    }
     const double* cr = cv.R + size_t(cv.sR) * c;
     const double* k5 = cv.K + size_t(cv.sK) * c;
     const double* tc = cv.t + size_t(cv.sT) * c;
@@ -1310,8 +1317,33 @@ __global__ __launch_bounds__(kThreads) void k_backsub_b(int P, const int32_t* __
     double w0 = L[6], w1 = L[7], w2 = L[8];
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;  // sum of u = L^-1 J_X^T e
     const int q0 = pt_off[p], q1 = pt_off[p + 1];
-    for (int q = q0; q < q1; ++q) {
-      // pass A's u: at the point-major slot, or (eu_pos) at the camera-major position
+    // pass A's u: at the point-major slot, or (eu_pos) at the camera-major
+    // position.  Four observations' positions, then their u, are loaded
+    // before any is summed (two memory round trips per four instead of two
+    // per observation: what bounds keyframe-sized problems); the sums still
+    // run in observation order.
+    int q = q0;
+    for (; q + 4 <= q1; q += 4) {
+      int ps[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ps[j] = eu_pos ? eu_pos[q + j] : q + j;
+      double2 a[4];
+      double b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double* u = eu + 4 * size_t(ps[j]);
+        a[j] = ld2(u);
+        b[j] = u[2];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w0 -= a[j].x;
+        w1 -= a[j].y;
+        w2 -= b[j];
+        s0 += a[j].x; s1 += a[j].y; s2 += b[j];
+      }
+    }
+    for (; q < q1; ++q) {
       const double* u = eu + 4 * (eu_pos ? size_t(eu_pos[q]) : size_t(q));
       const double2 u01 = ld2(u);
       const double u2 = u[2];
