@@ -294,6 +294,215 @@ __global__ __launch_bounds__(kT) void k_fill32(Fill32Set fs) {
   for (int64_t i = 4 * n4 + t0; i < f.n; i += st) f.p[i] = f.v;
 }
 
+// ---- keyframe-sized problems (set_problem's small path) ----
+// The same layouts without radix sorts.  The host knows every count, so
+// each order is a scatter into its known segments -- an integer atomic only
+// picks a slot -- followed by ordering each segment on its own: the final
+// order within a segment is the sorted one whatever slots the atomics gave,
+// so every output is the sorted path's, bit for bit (tests/test_gpu_scale.py).
+
+// Observation i into its point's segment (any slot).
+__global__ __launch_bounds__(kT) void k_small_pm_scatter(int64_t N, const int32_t* __restrict__ pt,
+                                                         const int32_t* __restrict__ pt_off,
+                                                         int32_t* __restrict__ fill, int32_t* __restrict__ tmp) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i >= N) return;
+  const int p = pt[i];
+  tmp[pt_off[p] + atomicAdd(fill + p, 1)] = int32_t(i);
+}
+// Each observation's rank in its point's segment by (camera, caller index)
+// -- the stable (point, camera) sort's order -- and the point-major gathers
+// at that position (k_gather_pm's).  Segments are short (the host bounds
+// them): every lane scans its own.
+__global__ __launch_bounds__(kT) void k_small_pm_rank(int64_t N, const int32_t* __restrict__ pt_off,
+                                                      const int32_t* __restrict__ tmp,
+                                                      const int32_t* __restrict__ cam, const int32_t* __restrict__ pt,
+                                                      const double* __restrict__ uv, int32_t* __restrict__ order,
+                                                      double* __restrict__ uv_pm, int32_t* __restrict__ cam_pm,
+                                                      int32_t* __restrict__ pt_s) {
+  const int64_t s = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (s >= N) return;
+  const int32_t i = tmp[s];
+  const int p = pt[i], c = cam[i];
+  const int q0 = pt_off[p], q1 = pt_off[p + 1];
+  int rank = 0;
+  for (int q = q0; q < q1; ++q) {
+    const int32_t j = tmp[q];
+    const int cj = cam[j];
+    rank += (cj < c || (cj == c && j < i)) ? 1 : 0;
+  }
+  const int dst = q0 + rank;
+  order[dst] = i;
+  reinterpret_cast<double2*>(uv_pm)[dst] = reinterpret_cast<const double2*>(uv)[i];
+  cam_pm[dst] = c;
+  pt_s[dst] = p;
+}
+// Point-major id q into its camera's segment (any slot).
+__global__ __launch_bounds__(kT) void k_small_cm_scatter(int64_t N, const int32_t* __restrict__ cam_pm,
+                                                         const int32_t* __restrict__ cam_off,
+                                                         int32_t* __restrict__ fill, int32_t* __restrict__ tmp) {
+  const int64_t q = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (q >= N) return;
+  const int c = cam_pm[q];
+  tmp[cam_off[c] + atomicAdd(fill + c, 1)] = int32_t(q);
+}
+// One workgroup per camera: its point-major ids ascending (the stable sort
+// by camera of the point-major order), bitonic in LDS (<= kSmallCamObs).
+constexpr int kSmallCamObs = 4096;
+__global__ __launch_bounds__(kT) void k_small_cm_sort(const int32_t* __restrict__ cam_off,
+                                                      const int32_t* __restrict__ tmp,
+                                                      int32_t* __restrict__ cm_order) {
+  __shared__ int32_t v[kSmallCamObs];
+  const int c = blockIdx.x;
+  const int o = cam_off[c], n = cam_off[c + 1] - o;
+  int m = 1;
+  while (m < n) m <<= 1;
+  for (int k = threadIdx.x; k < m; k += kT) v[k] = k < n ? tmp[o + k] : INT_MAX;
+  __syncthreads();
+  for (int size = 2; size <= m; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int k = threadIdx.x; k < m; k += kT) {
+        const int partner = k ^ stride;
+        if (partner > k) {
+          const bool up = (k & size) == 0;
+          const int a = v[k], b = v[partner];
+          if ((a > b) == up) { v[k] = b; v[partner] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int k = threadIdx.x; k < n; k += kT) cm_order[o + k] = v[k];
+}
+// The chunk table grouped by point slice (k_chunk_keys' key), stable: one
+// wave, 64 chunks at a time, each key's rank by ballot.
+__global__ __launch_bounds__(64) void k_small_chunks(int n, const int4* __restrict__ ch,
+                                                     const int32_t* __restrict__ cm_order,
+                                                     const int32_t* __restrict__ pt_s, int P, int4* __restrict__ out,
+                                                     int32_t* __restrict__ grp) {
+  const int l = threadIdx.x;
+  const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  auto key_of = [&](int t) { return int(int64_t(pt_s[cm_order[ch[t].w]]) * 8 / max(1, P)); };
+  int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int b = 0; b < n; b += 64) {
+    const int t = b + l, k = t < n ? key_of(t) : -1;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) cnt[g] += __popcll(__builtin_amdgcn_ballot_w64(k == g));
+  }
+  int start[9];
+  start[0] = 0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) start[g + 1] = start[g] + cnt[g];
+  if (l <= 8) {
+    int v = 0;
+#pragma unroll
+    for (int g = 0; g <= 8; ++g) v = l == g ? start[g] : v;
+    grp[l] = v;
+  }
+  for (int b = 0; b < n; b += 64) {
+    const int t = b + l, k = t < n ? key_of(t) : -1;
+    int dst = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(k == g);
+      if (k == g) dst = start[g] + __popcll(m & lt);
+      start[g] += __popcll(m);
+    }
+    if (t < n) {
+      const int4 v = ch[t];
+      out[dst] = make_int4(v.x, v.y, v.z, 0);
+    }
+  }
+}
+// Block b = (c1, c2), c1 <= c2 (row-major over the upper triangle, k_blk's).
+__device__ __forceinline__ int2 small_block(int64_t b, int C) {
+  int c1 = 0;
+  while (c1 + 1 < C && int64_t(c1 + 1) * C - int64_t(c1 + 1) * c1 / 2 <= b) ++c1;
+  const int64_t rs = int64_t(c1) * C - int64_t(c1) * (c1 - 1) / 2 - c1;
+  return make_int2(c1, int(b - rs));
+}
+// This lane's share of block (c1, c2)'s pairs: camera-major entry i of c1
+// (o1, point p) against the point's observations o2 of camera c2, o2 != o1.
+__device__ __forceinline__ int small_pairs_of(int i, int c2, const int32_t* __restrict__ cm_order,
+                                              const int32_t* __restrict__ cam_pm, const int32_t* __restrict__ pt_s,
+                                              const int32_t* __restrict__ pt_off, int32_t* __restrict__ out) {
+  const int32_t o1 = cm_order[i];
+  const int p = pt_s[o1];
+  int k = 0;
+  for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
+    if (cam_pm[o2] == c2 && o2 != o1) {
+      if (out) out[k] = p;
+      ++k;
+    }
+  return k;
+}
+// One workgroup per block: its pair count.
+__global__ __launch_bounds__(kT) void k_small_pair_count(int C, const int32_t* __restrict__ cam_off,
+                                                         const int32_t* __restrict__ cm_order,
+                                                         const int32_t* __restrict__ cam_pm,
+                                                         const int32_t* __restrict__ pt_s,
+                                                         const int32_t* __restrict__ pt_off, int32_t* __restrict__ cnt) {
+  __shared__ int sh[kT / 64];
+  const int2 cc = small_block(blockIdx.x, C);
+  int k = 0;
+  for (int i = cam_off[cc.x] + threadIdx.x; i < cam_off[cc.x + 1]; i += kT)
+    k += small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, nullptr);
+  for (int off = 32; off > 0; off >>= 1) k += __shfl_xor(k, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+// seg = exclusive sum of the n block counts (seg[n] = total), one workgroup.
+__global__ __launch_bounds__(1024) void k_small_scan(int64_t n, const int32_t* __restrict__ cnt,
+                                                     int32_t* __restrict__ seg) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024, a = std::min<int64_t>(n, t * per), e = std::min<int64_t>(n, a + per);
+  int32_t sum = 0;
+  for (int64_t i = a; i < e; ++i) sum += cnt[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int32_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int32_t run = part[t] - sum;
+  for (int64_t i = a; i < e; ++i) {
+    seg[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023) seg[n] = part[t];
+}
+// One workgroup per block: its list in (o1 camera-major, o2 point-major)
+// order, 256 camera-major entries at a time, positions by a prefix sum.
+__global__ __launch_bounds__(kT) void k_small_pair_fill(int C, const int32_t* __restrict__ cam_off,
+                                                        const int32_t* __restrict__ cm_order,
+                                                        const int32_t* __restrict__ cam_pm,
+                                                        const int32_t* __restrict__ pt_s,
+                                                        const int32_t* __restrict__ pt_off,
+                                                        const int32_t* __restrict__ seg, int32_t* __restrict__ bpts) {
+  __shared__ int sc[kT];
+  const int2 cc = small_block(blockIdx.x, C);
+  const int t = threadIdx.x, i0 = cam_off[cc.x], i1 = cam_off[cc.x + 1];
+  int run = seg[blockIdx.x];
+  for (int b = i0; b < i1; b += kT) {
+    const int i = b + t;
+    const int k = i < i1 ? small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, nullptr) : 0;
+    sc[t] = k;
+    __syncthreads();
+    for (int off = 1; off < kT; off <<= 1) {
+      const int v = t >= off ? sc[t - off] : 0;
+      __syncthreads();
+      sc[t] += v;
+      __syncthreads();
+    }
+    if (k) small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, bpts + run + sc[t] - k);
+    run += sc[kT - 1];
+    __syncthreads();
+  }
+}
+
 int bits_for(uint64_t max_key) {
   int b = 1;
   while (b < 64 && (max_key >> b) != 0) ++b;
@@ -386,6 +595,35 @@ void launch_fill32(const Fill32Set& fs, hipStream_t s) {
 }
 void launch_blk(int C, int2* blk, hipStream_t s) {
   if (C > 0) k_blk<<<dim3(unsigned((C + kT - 1) / kT), unsigned(C)), kT, 0, s>>>(C, blk);
+}
+void launch_small_pm(int64_t N, const int32_t* pt, const int32_t* cam, const double* uv, const int32_t* pt_off,
+                     int32_t* fill, int32_t* tmp, int32_t* order, double* uv_pm, int32_t* cam_pm, int32_t* pt_s,
+                     hipStream_t s) {
+  if (N <= 0) return;
+  k_small_pm_scatter<<<nblocks(N), kT, 0, s>>>(N, pt, pt_off, fill, tmp);
+  k_small_pm_rank<<<nblocks(N), kT, 0, s>>>(N, pt_off, tmp, cam, pt, uv, order, uv_pm, cam_pm, pt_s);
+}
+void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* fill, int32_t* tmp,
+                     int32_t* cm_order, hipStream_t s) {
+  if (N <= 0 || C <= 0) return;
+  k_small_cm_scatter<<<nblocks(N), kT, 0, s>>>(N, cam_pm, cam_off, fill, tmp);
+  k_small_cm_sort<<<C, kT, 0, s>>>(cam_off, tmp, cm_order);
+}
+void launch_small_chunks(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, int4* out,
+                         int32_t* grp, hipStream_t s) {
+  k_small_chunks<<<1, 64, 0, s>>>(n, ch, cm_order, pt_s, P, out, grp);
+}
+void launch_small_pairs_count(int C, int64_t n_blk, const int32_t* cam_off, const int32_t* cm_order,
+                              const int32_t* cam_pm, const int32_t* pt_s, const int32_t* pt_off, int32_t* cnt,
+                              int32_t* seg, hipStream_t s) {
+  if (n_blk <= 0) return;
+  k_small_pair_count<<<unsigned(n_blk), kT, 0, s>>>(C, cam_off, cm_order, cam_pm, pt_s, pt_off, cnt);
+  k_small_scan<<<1, 1024, 0, s>>>(n_blk, cnt, seg);
+}
+void launch_small_pairs_fill(int C, int64_t n_blk, const int32_t* cam_off, const int32_t* cm_order,
+                             const int32_t* cam_pm, const int32_t* pt_s, const int32_t* pt_off, const int32_t* seg,
+                             int32_t* bpts, hipStream_t s) {
+  if (n_blk > 0) k_small_pair_fill<<<unsigned(n_blk), kT, 0, s>>>(C, cam_off, cm_order, cam_pm, pt_s, pt_off, seg, bpts);
 }
 int64_t bperm_slots_bound(int64_t n_blk, int per) { return std::max<int64_t>(1, (n_blk + per - 1) / per) * 8 * per; }
 hipError_t launch_bperm(int C, int64_t n_blk, int64_t n_pairs, const int32_t* seg, const int2* blk, int per,

@@ -1443,7 +1443,8 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // which is still in flight -- no synchronisation in between -- so the
   // stage holds both from here: 2 C + chunks + ... ints, bounded)
   const size_t il_base = host_check && stage_in ? (in_bytes + 255) / 256 * 256 : 0;
-  const size_t il_bound = host_check && stage_in ? 64 * (size_t(C) + 1) + 2 * size_t(N) + 1024 : 0;
+  const size_t il_bound =
+      host_check && stage_in ? 64 * (size_t(C) + 1) + 2 * size_t(N) + 8 * (size_t(P) + 1) + 4 * size_t(C) + 2048 : 0;
   if ((rc = stage_reserve(h, std::max(stage_in ? il_base + il_bound : 0, sizeof(int32_t) * (size_t(C) + 4)))))
     return bail(rc);
   stg = h->stage;
@@ -1557,6 +1558,23 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     const int v = std::atoi(jw);
     if (v > 0) d.jac_blocks = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, v));
   }
+  // keyframe-sized problems: the layouts without radix sorts (ba_setup.hip
+  // small path; the same arrays bit for bit), when the host has the counts
+  // and the segments fit its bounds (SFM_SMALL_SETUP=0: the sorted path)
+  // (C (C + 1) / 2 <= kSchurXcdMinBlocks: the plain k_schur_pts block order,
+  // as the sorted path takes for these sizes)
+  bool small = host_check && stage_in && N > 0 && C > 0 && C <= kSmallSetupMaxC &&
+               int64_t(C) * (C + 1) / 2 <= kSchurXcdMinBlocks;
+  if (small) {
+    const char* ss = std::getenv("SFM_SMALL_SETUP");
+    if (ss && ss[0] == '0') small = false;
+  }
+  if (small)
+    for (int c = 0; c < C && small; ++c) small = cam_cnt[4 + c] <= kSmallSetupMaxCamObs;
+  if (small) {
+    const int32_t* pc = reinterpret_cast<const int32_t*>(stg + o_pc);
+    for (int p = 0; p < P && small; ++p) small = pc[p] <= kSmallSetupMaxPtObs;
+  }
   std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
   for (int c = 0; c < C; ++c) {
     const double* k = K9 + 9 * size_t(c);
@@ -1570,7 +1588,8 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   int64_t* poff = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_bytes = 0;
-  ALLOC(d.pt_off, size_t(P) + 1);
+  int32_t* small_fill = nullptr;  // small path: the scatters' slot counters (P | C), zeroed in the camera-run blob
+  if (!small) ALLOC(d.pt_off, size_t(P) + 1);  // (small path: in the camera-run blob)
   ALLOC(d.order, size_t(N));
   ALLOC(d.uv_pm, 2 * size_t(N));
   ALLOC(d.cam_pm, size_t(N));
@@ -1609,6 +1628,10 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     StageLayout il;
     const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
                  o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
+    // small path: pt_off (the host's scan of the point counts, resident) and
+    // the zeroed slot counters of the point / camera scatters
+    const size_t o_poff = small ? il.add(sizeof(int32_t) * (size_t(P) + 1)) : 0,
+                 o_fill = small ? il.add(sizeof(int32_t) * (size_t(P) + size_t(C))) : 0;
     if (il_base && il.bytes > il_bound) return bail(fail(SFM_EIO, "internal: camera-run blob above its bound"));
     if ((rc = stage_reserve(h, il_base + il.bytes))) return bail(rc);  // (never regrows with il_base > 0)
     stg = h->stage;
@@ -1619,12 +1642,41 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     std::memcpy(sb + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
     std::memcpy(sb + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
     if (nch) std::memcpy(sb + o_ch, chunks.data(), sizeof(int4) * chunks.size());
+    if (small) {
+      const int32_t* pc = reinterpret_cast<const int32_t*>(stg + o_pc);
+      int32_t* po = reinterpret_cast<int32_t*>(sb + o_poff);
+      po[0] = 0;
+      for (int p = 0; p < P; ++p) po[p + 1] = po[p] + pc[p];
+      std::memset(sb + o_fill, 0, sizeof(int32_t) * (size_t(P) + size_t(C)));
+    }
     HCHK(hipMemcpyAsync(ib, sb, il.bytes, hipMemcpyHostToDevice, s));
+    if (small) {
+      d.pt_off = reinterpret_cast<int32_t*>(ib + o_poff);
+      small_fill = reinterpret_cast<int32_t*>(ib + o_fill);
+    }
     d.cam_rng = reinterpret_cast<int32_t*>(ib + o_rng);
     d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
     d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
     ch_in = reinterpret_cast<int4*>(ib + o_ch);
   }
+  int32_t* small_cnt = nullptr;  // small path: per-block pair counts
+  if (small) {
+    // the same layouts without radix sorts (ba_setup.hip small path):
+    // point-major by (point, camera, caller index), camera-major by (camera,
+    // point-major id), the chunk table by slice, the pair counts per block
+    // (seg = their exclusive sum, seg[n_blk] = the pair total)
+    d.n_blk = int64_t(C) * (C + 1) / 2;
+    ALLOC(d.seg, size_t(d.n_blk) + 1);
+    TMP(small_cnt, std::max<size_t>(1, size_t(d.n_blk)));
+    launch_small_pm(N, in_pt, in_cam, in_uv, d.pt_off, small_fill, reinterpret_cast<int32_t*>(k32a), d.order,
+                    d.uv_pm, d.cam_pm, pt_s, s);
+    launch_small_cm(N, C, d.cam_pm, d_cam_off, small_fill + P, reinterpret_cast<int32_t*>(k32b), cm_order, s);
+    launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
+    launch_small_chunks(int(nch), ch_in, cm_order, pt_s, P, d.jchunks, d.jgrp, s);
+    launch_small_pairs_count(C, d.n_blk, d_cam_off, cm_order, d.cam_pm, pt_s, d.pt_off, small_cnt, d.seg, s);
+    // (into the stage: stream order puts it after the upload that reads the stage)
+    HCHK(hipMemcpyAsync(stg, d.seg + d.n_blk, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  } else {
   // point-major order: stable sort by (point, camera)
   launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
   HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
@@ -1646,11 +1698,18 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
   // (into the stage: stream order puts it after the upload that reads the stage)
   HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  }
   // and the 8 slices' chunk offsets: the observation passes size their grids
   // by the largest slice (obs_xcd_blocks)
   HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HCHK(hipStreamSynchronize(s));
-  std::memcpy(&n_pairs, stg, sizeof(int64_t));
+  if (small) {
+    int32_t np32 = 0;
+    std::memcpy(&np32, stg, sizeof(int32_t));
+    n_pairs = np32;
+  } else {
+    std::memcpy(&n_pairs, stg, sizeof(int64_t));
+  }
   {
     int32_t g[9];
     std::memcpy(g, stg + 8, sizeof(g));
@@ -1690,9 +1749,14 @@ constexpr int64_t kHostCheckMaxObs = 65536;
                o_c0 = pl.add(sizeof(double) * 6 * size_t(C)), o_X = pl.add(sizeof(double) * 3 * size_t(P)),
                o_X0 = pl.add(sizeof(double) * 3 * size_t(P));
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
-  ALLOC(d.seg, size_t(d.n_blk) + 1);
+  if (!small) ALLOC(d.seg, size_t(d.n_blk) + 1);
   ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
-  {
+  if (small) {
+    launch_small_pairs_fill(C, d.n_blk, d_cam_off, cm_order, d.cam_pm, pt_s, d.pt_off, d.seg, d.bpts, s);
+    launch_blk(C, d.blk, s);
+    d.bperm = nullptr;
+    d.n_bslots = d.n_blk;
+  } else {
     uint32_t *bk_a = nullptr, *bk_b = nullptr;
     int32_t* bv = nullptr;
     const int64_t nk = std::max<int64_t>({n_pairs, d.n_blk, 1});

@@ -272,6 +272,45 @@ def test_device_layout_keeps_caller_order_of_duplicates():
     _assert_parity(o, g)
 
 
+def _small_setup_scenes():
+    out = [("C1", scene.config("C1"))]
+    s = scene.generate(12, 400, views=4, seed=23)  # duplicates, shuffled caller order
+    rng = np.random.default_rng(5)
+    dup = rng.choice(len(s.pt_idx), 40, replace=False)
+    _append_obs(s, s.cam_idx[dup], s.pt_idx[dup], s.uv[dup] + rng.normal(0, 0.3, (40, 2)))
+    perm = rng.permutation(len(s.pt_idx))
+    s.uv, s.cam_idx, s.pt_idx = s.uv[perm], s.cam_idx[perm], s.pt_idx[perm]
+    out.append(("dup-shuffled", s))
+    s = scene.generate(40, 3000, views=6, seed=31)  # an empty camera and single-view points
+    keep = (s.cam_idx != 7) & ~((s.pt_idx % 97 == 0) & (np.arange(len(s.pt_idx)) % 3 != 0))
+    s.uv, s.cam_idx, s.pt_idx = s.uv[keep], s.cam_idx[keep], s.pt_idx[keep]
+    out.append(("empty-camera", s))
+    return out
+
+
+@pytest.mark.parametrize("idx", range(3))
+def test_small_setup_path_is_bitwise_the_sorted_path(idx, monkeypatch):
+    """Keyframe-sized problems build their layouts without radix sorts
+    (ba_setup.hip small path: scatter into the host-known segments, then each
+    segment ordered on its own); SFM_SMALL_SETUP=0 takes the sorted path.
+    Both must give the same evaluate() outputs and the same solve, bit for
+    bit (caller-order duplicates, an empty camera, single-view points)."""
+    name, s = _small_setup_scenes()[idx]
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SFM_SMALL_SETUP", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            ev = ba.evaluate()
+            sm, tr = ba.solve()
+            out.append((ev, sm.final_cost, tr, ba.parameters()))
+    (ev0, c0, tr0, p0), (ev1, c1, tr1, p1) = out
+    assert ev0[0] == ev1[0] and np.array_equal(ev0[1], ev1[1]) and np.array_equal(ev0[2], ev1[2]), name
+    assert c0 == c1 and tr0 == tr1, name
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b), name
+
+
 def test_one_shot_solves_reuse_the_cached_handle():
     """sfm_ba_solve keeps one handle per device and thread (buffers pooled):
     back-to-back one-shot solves of different sizes give the resident
