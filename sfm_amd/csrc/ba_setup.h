@@ -51,18 +51,19 @@ void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm,
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s);
 void launch_blk(int C, int2* blk, hipStream_t s);
 // Keyframe-sized problems: the same layouts without radix sorts (scatter into
-// the host-known segments, then each segment ordered on its own).  fill /
-// tmp: zeroed counters (P / C) and N-item scratch.  Bounds (the host checks):
-// a camera's observations <= kSmallCamObs (4096), C <= 256 (the pair passes
-// run a workgroup per camera block), short point segments.
+// the host-known point segments then ranks within each, per-camera stable
+// compactions, run lengths of the camera-sorted point segments for the pair
+// lists).  fill / tmp: zeroed point counters (P) and N-item scratch.  Bounds
+// (the host checks): C <= 256, at most kSmallChunks chunks, short point
+// segments.
 constexpr int kSmallSetupMaxC = 256;
-constexpr int kSmallSetupMaxCamObs = 4096;
+constexpr int kSmallSetupMaxChunks = 2048;
 constexpr int kSmallSetupMaxPtObs = 64;
 void launch_small_pm(int64_t N, const int32_t* pt, const int32_t* cam, const double* uv, const int32_t* pt_off,
                      int32_t* fill, int32_t* tmp, int32_t* order, double* uv_pm, int32_t* cam_pm, int32_t* pt_s,
                      hipStream_t s);
-void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* fill, int32_t* tmp,
-                     int32_t* cm_order, hipStream_t s);
+void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* cm_order,
+                     hipStream_t s);
 void launch_small_chunks(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, int4* out,
                          int32_t* grp, hipStream_t s);
 // cnt (n_blk) per block, seg (n_blk + 1) their exclusive sum

@@ -337,54 +337,51 @@ __global__ __launch_bounds__(kT) void k_small_pm_rank(int64_t N, const int32_t* 
   cam_pm[dst] = c;
   pt_s[dst] = p;
 }
-// Point-major id q into its camera's segment (any slot).
-__global__ __launch_bounds__(kT) void k_small_cm_scatter(int64_t N, const int32_t* __restrict__ cam_pm,
-                                                         const int32_t* __restrict__ cam_off,
-                                                         int32_t* __restrict__ fill, int32_t* __restrict__ tmp) {
-  const int64_t q = int64_t(blockIdx.x) * kT + threadIdx.x;
-  if (q >= N) return;
-  const int c = cam_pm[q];
-  tmp[cam_off[c] + atomicAdd(fill + c, 1)] = int32_t(q);
-}
 // One workgroup per camera: its point-major ids ascending (the stable sort
-// by camera of the point-major order), bitonic in LDS (<= kSmallCamObs).
-constexpr int kSmallCamObs = 4096;
-__global__ __launch_bounds__(kT) void k_small_cm_sort(const int32_t* __restrict__ cam_off,
-                                                      const int32_t* __restrict__ tmp,
-                                                      int32_t* __restrict__ cm_order) {
-  __shared__ int32_t v[kSmallCamObs];
-  const int c = blockIdx.x;
-  const int o = cam_off[c], n = cam_off[c + 1] - o;
-  int m = 1;
-  while (m < n) m <<= 1;
-  for (int k = threadIdx.x; k < m; k += kT) v[k] = k < n ? tmp[o + k] : INT_MAX;
-  __syncthreads();
-  for (int size = 2; size <= m; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int k = threadIdx.x; k < m; k += kT) {
-        const int partner = k ^ stride;
-        if (partner > k) {
-          const bool up = (k & size) == 0;
-          const int a = v[k], b = v[partner];
-          if ((a > b) == up) { v[k] = b; v[partner] = a; }
-        }
-      }
-      __syncthreads();
+// by camera of the point-major order) by a stable compaction -- 1024 ids
+// at a time, each wave's matches ranked by ballot, the waves in order.
+__global__ __launch_bounds__(1024) void k_small_cm_compact(int64_t N, const int32_t* __restrict__ cam_pm,
+                                                           const int32_t* __restrict__ cam_off,
+                                                           int32_t* __restrict__ cm_order) {
+  __shared__ int wcnt[16];
+  const int c = blockIdx.x, t = threadIdx.x, l = t & 63, w = t >> 6;
+  const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  int run = cam_off[c];
+  for (int64_t base = 0; base < N; base += 1024) {
+    const int64_t q = base + t;
+    const bool hit = q < N && cam_pm[q] == c;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+    if (l == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      before += v < w ? wcnt[v] : 0;
+      total += wcnt[v];
     }
-  for (int k = threadIdx.x; k < n; k += kT) cm_order[o + k] = v[k];
+    if (hit) cm_order[run + before + __popcll(m & lt)] = int32_t(q);
+    run += total;
+    __syncthreads();
+  }
 }
-// The chunk table grouped by point slice (k_chunk_keys' key), stable: one
-// wave, 64 chunks at a time, each key's rank by ballot.
-__global__ __launch_bounds__(64) void k_small_chunks(int n, const int4* __restrict__ ch,
-                                                     const int32_t* __restrict__ cm_order,
-                                                     const int32_t* __restrict__ pt_s, int P, int4* __restrict__ out,
-                                                     int32_t* __restrict__ grp) {
+// The chunk table grouped by point slice (k_chunk_keys' key), stable: the
+// keys by the whole workgroup into LDS, then wave 0 ranks them, 64 chunks at
+// a time, by ballot.
+constexpr int kSmallChunks = 2048;
+__global__ __launch_bounds__(1024) void k_small_chunks(int n, const int4* __restrict__ ch,
+                                                       const int32_t* __restrict__ cm_order,
+                                                       const int32_t* __restrict__ pt_s, int P, int4* __restrict__ out,
+                                                       int32_t* __restrict__ grp) {
+  __shared__ unsigned char key[kSmallChunks];
+  for (int t = threadIdx.x; t < n; t += 1024)
+    key[t] = (unsigned char)(int64_t(pt_s[cm_order[ch[t].w]]) * 8 / max(1, P));
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
   const int l = threadIdx.x;
   const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
-  auto key_of = [&](int t) { return int(int64_t(pt_s[cm_order[ch[t].w]]) * 8 / max(1, P)); };
   int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int b = 0; b < n; b += 64) {
-    const int t = b + l, k = t < n ? key_of(t) : -1;
+    const int t = b + l, k = t < n ? int(key[t]) : -1;
 #pragma unroll
     for (int g = 0; g < 8; ++g) cnt[g] += __popcll(__builtin_amdgcn_ballot_w64(k == g));
   }
@@ -399,7 +396,7 @@ __global__ __launch_bounds__(64) void k_small_chunks(int n, const int4* __restri
     grp[l] = v;
   }
   for (int b = 0; b < n; b += 64) {
-    const int t = b + l, k = t < n ? key_of(t) : -1;
+    const int t = b + l, k = t < n ? int(key[t]) : -1;
     int dst = 0;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
@@ -420,20 +417,26 @@ __device__ __forceinline__ int2 small_block(int64_t b, int C) {
   const int64_t rs = int64_t(c1) * C - int64_t(c1) * (c1 - 1) / 2 - c1;
   return make_int2(c1, int(b - rs));
 }
-// This lane's share of block (c1, c2)'s pairs: camera-major entry i of c1
-// (o1, point p) against the point's observations o2 of camera c2, o2 != o1.
-__device__ __forceinline__ int small_pairs_of(int i, int c2, const int32_t* __restrict__ cm_order,
+// Camera-major entry i of c1 (o1, point p) in block (c1, c2): the pairs are
+// the observations o2 of p with camera c2, o2 != o1.  A point's point-major
+// segment is sorted by camera, so they are one run; its length (minus o1
+// itself when c2 == c1) is the count, and every pair stores p.  The segment
+// is read four entries at a time (independent loads).
+__device__ __forceinline__ int small_pairs_of(int i, int c1, int c2, const int32_t* __restrict__ cm_order,
                                               const int32_t* __restrict__ cam_pm, const int32_t* __restrict__ pt_s,
-                                              const int32_t* __restrict__ pt_off, int32_t* __restrict__ out) {
+                                              const int32_t* __restrict__ pt_off, int& p) {
   const int32_t o1 = cm_order[i];
-  const int p = pt_s[o1];
+  p = pt_s[o1];
+  const int q0 = pt_off[p], q1 = pt_off[p + 1];
   int k = 0;
-  for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2)
-    if (cam_pm[o2] == c2 && o2 != o1) {
-      if (out) out[k] = p;
-      ++k;
-    }
-  return k;
+  for (int q = q0; q < q1; q += 4) {
+    int cj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cj[j] = cam_pm[min(q + j, q1 - 1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k += (q + j < q1 && cj[j] == c2) ? 1 : 0;
+  }
+  return k - (c2 == c1 ? 1 : 0);
 }
 // One workgroup per block: its pair count.
 __global__ __launch_bounds__(kT) void k_small_pair_count(int C, const int32_t* __restrict__ cam_off,
@@ -443,9 +446,9 @@ __global__ __launch_bounds__(kT) void k_small_pair_count(int C, const int32_t* _
                                                          const int32_t* __restrict__ pt_off, int32_t* __restrict__ cnt) {
   __shared__ int sh[kT / 64];
   const int2 cc = small_block(blockIdx.x, C);
-  int k = 0;
+  int k = 0, p;
   for (int i = cam_off[cc.x] + threadIdx.x; i < cam_off[cc.x + 1]; i += kT)
-    k += small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, nullptr);
+    k += small_pairs_of(i, cc.x, cc.y, cm_order, cam_pm, pt_s, pt_off, p);
   for (int off = 32; off > 0; off >>= 1) k += __shfl_xor(k, off);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
   __syncthreads();
@@ -488,7 +491,8 @@ __global__ __launch_bounds__(kT) void k_small_pair_fill(int C, const int32_t* __
   int run = seg[blockIdx.x];
   for (int b = i0; b < i1; b += kT) {
     const int i = b + t;
-    const int k = i < i1 ? small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, nullptr) : 0;
+    int p = 0;
+    const int k = i < i1 ? small_pairs_of(i, cc.x, cc.y, cm_order, cam_pm, pt_s, pt_off, p) : 0;
     sc[t] = k;
     __syncthreads();
     for (int off = 1; off < kT; off <<= 1) {
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(kT) void k_small_pair_fill(int C, const int32_t* __
       sc[t] += v;
       __syncthreads();
     }
-    if (k) small_pairs_of(i, cc.y, cm_order, cam_pm, pt_s, pt_off, bpts + run + sc[t] - k);
+    for (int j = 0; j < k; ++j) bpts[run + sc[t] - k + j] = p;
     run += sc[kT - 1];
     __syncthreads();
   }
@@ -603,15 +607,14 @@ void launch_small_pm(int64_t N, const int32_t* pt, const int32_t* cam, const dou
   k_small_pm_scatter<<<nblocks(N), kT, 0, s>>>(N, pt, pt_off, fill, tmp);
   k_small_pm_rank<<<nblocks(N), kT, 0, s>>>(N, pt_off, tmp, cam, pt, uv, order, uv_pm, cam_pm, pt_s);
 }
-void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* fill, int32_t* tmp,
-                     int32_t* cm_order, hipStream_t s) {
+void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* cm_order,
+                     hipStream_t s) {
   if (N <= 0 || C <= 0) return;
-  k_small_cm_scatter<<<nblocks(N), kT, 0, s>>>(N, cam_pm, cam_off, fill, tmp);
-  k_small_cm_sort<<<C, kT, 0, s>>>(cam_off, tmp, cm_order);
+  k_small_cm_compact<<<C, 1024, 0, s>>>(N, cam_pm, cam_off, cm_order);
 }
 void launch_small_chunks(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, int4* out,
                          int32_t* grp, hipStream_t s) {
-  k_small_chunks<<<1, 64, 0, s>>>(n, ch, cm_order, pt_s, P, out, grp);
+  k_small_chunks<<<1, 1024, 0, s>>>(n, ch, cm_order, pt_s, P, out, grp);
 }
 void launch_small_pairs_count(int C, int64_t n_blk, const int32_t* cam_off, const int32_t* cm_order,
                               const int32_t* cam_pm, const int32_t* pt_s, const int32_t* pt_off, int32_t* cnt,

@@ -1403,6 +1403,7 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   HIPCHK(hipStreamSynchronize(h->stream));
   free_problem(h);
   DevProblem& d = h->d;
+  timer.mark("sync + free");
   const int64_t N = n_obs;
   const int C = n_cams, P = n_pts;
   d.C = C; d.P = P; d.N = N;
@@ -1478,6 +1479,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     cam_cnt[2] = first[2];
     cam_cnt[3] = INT32_MAX;
     cnt_p = reinterpret_cast<int32_t*>(in_blob + o_pc);
+    timer.mark("host checks + counts");
   } else {
     TMP(err, 4 + size_t(C) + 1);  // first bad observation (4) | per-camera counts (C + 1)
     cnt_c = err + 4;
@@ -1492,6 +1494,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
       std::memcpy(stg + o_pt, pt_idx, sizeof(int32_t) * size_t(N));
     }
     HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
+    timer.mark("stage copy + upload");
   } else if (N) {
     HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
@@ -1569,8 +1572,11 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     const char* ss = std::getenv("SFM_SMALL_SETUP");
     if (ss && ss[0] == '0') small = false;
   }
-  if (small)
-    for (int c = 0; c < C && small; ++c) small = cam_cnt[4 + c] <= kSmallSetupMaxCamObs;
+  if (small) {
+    int64_t nch_small = 0;
+    for (int c = 0; c < C; ++c) nch_small += (cam_cnt[4 + c] + 63) / 64;
+    small = nch_small <= kSmallSetupMaxChunks;
+  }
   if (small) {
     const int32_t* pc = reinterpret_cast<const int32_t*>(stg + o_pc);
     for (int p = 0; p < P && small; ++p) small = pc[p] <= kSmallSetupMaxPtObs;
@@ -1668,15 +1674,17 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     d.n_blk = int64_t(C) * (C + 1) / 2;
     ALLOC(d.seg, size_t(d.n_blk) + 1);
     TMP(small_cnt, std::max<size_t>(1, size_t(d.n_blk)));
+    timer.mark("allocs + camera-run blob");
     launch_small_pm(N, in_pt, in_cam, in_uv, d.pt_off, small_fill, reinterpret_cast<int32_t*>(k32a), d.order,
                     d.uv_pm, d.cam_pm, pt_s, s);
-    launch_small_cm(N, C, d.cam_pm, d_cam_off, small_fill + P, reinterpret_cast<int32_t*>(k32b), cm_order, s);
+    launch_small_cm(N, C, d.cam_pm, d_cam_off, cm_order, s);
     launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
     launch_small_chunks(int(nch), ch_in, cm_order, pt_s, P, d.jchunks, d.jgrp, s);
     launch_small_pairs_count(C, d.n_blk, d_cam_off, cm_order, d.cam_pm, pt_s, d.pt_off, small_cnt, d.seg, s);
     // (into the stage: stream order puts it after the upload that reads the stage)
     HCHK(hipMemcpyAsync(stg, d.seg + d.n_blk, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   } else {
+  timer.mark("allocs + camera-run blob");
   // point-major order: stable sort by (point, camera)
   launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
   HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
@@ -1702,6 +1710,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // and the 8 slices' chunk offsets: the observation passes size their grids
   // by the largest slice (obs_xcd_blocks)
   HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  timer.mark("layout launches");
   HCHK(hipStreamSynchronize(s));
   if (small) {
     int32_t np32 = 0;
@@ -1914,6 +1923,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   h->chol_epoch = 0;
   h->bs_epoch = 0;
   d.n_cu = h->n_cu;
+  timer.mark("pairs + params launches");
   HCHK(hipStreamSynchronize(s));
   if (bperm_per) {
     int64_t m_max = 1;
