@@ -787,8 +787,9 @@ __global__ __launch_bounds__(kThreads) void k_backsub_a_rc(const int32_t* __rest
       // streams a point's u contiguously instead of gathering 48-B records
       const double* M = o.M;
       double* dst = eu + 4 * (eu_cm ? size_t(i) : size_t(qo));
+      // (the whole 32-B slot, padding included: full-line writes, 59 -> 51 us at C3)
       st2(dst, M[0] * e0 + M[3] * e1, M[1] * e0 + M[4] * e1);
-      dst[2] = M[2] * e0 + M[5] * e1;
+      st2(dst + 2, M[2] * e0 + M[5] * e1, 0.0);
     }
   }
   const double r = block_reduce(model, sh, false);
