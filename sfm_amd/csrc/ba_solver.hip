@@ -286,14 +286,16 @@ int device_cus(int device) {
   return prop.multiProcessorCount;
 }
 
-// SFM_TIMING=1: host phase times of sfm_ba_set_problem on stderr.
+// SFM_TIMING=1: host phase times of sfm_ba_set_problem and of the device LM
+// loop's batches on stderr.
 struct HostTimer {
   bool on = env_flag("SFM_TIMING");
+  const char* tag = "set_problem";
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   void mark(const char* what) {
     if (!on) return;
     const auto t1 = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[set_problem] %-22s %8.3f ms\n", what,
+    std::fprintf(stderr, "[%s] %-22s %8.3f ms\n", tag, what,
                  std::chrono::duration<double, std::milli>(t1 - t0).count());
     t0 = t1;
   }
@@ -505,20 +507,26 @@ __global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restri
   __syncthreads();
   if (!last) return;
   __threadfence();
+  // The bookkeeping runs on an LDS copy of the control block, loaded and
+  // stored back by the whole workgroup: its branches read and write the
+  // block field by field, one dependent memory round trip each in place.
+  __shared__ LmCtl lc;
+  static_assert(sizeof(LmCtl) % 4 == 0, "LmCtl is copied as 32-bit words");
+  constexpr int kCtlWords = int(sizeof(LmCtl) / 4);
+  static_assert(kCtlWords <= 1024, "one word per thread");
   if (threadIdx.x <= kNumScalars)
     sc[threadIdx.x] = __hip_atomic_load(scal + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kCtlWords) reinterpret_cast<int*>(&lc)[threadIdx.x] = reinterpret_cast<const int*>(c)[threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0) {
-    c->red_count = 0;
-    if (kTail == kTailPost) lm_post(c, sc, trace, cap);
-    else if (kTail == kTailInit) lm_init(c, sc);
-    else lm_decide(c, sc, trace, cap);
+    lc.red_count = 0;
+    if (kTail == kTailPost) lm_post(&lc, sc, trace, cap);
+    else if (kTail == kTailInit) lm_init(&lc, sc);
+    else lm_decide(&lc, sc, trace, cap);
   }
-  if (kTail != kTailDecide || af.C == 0) return;
-  __shared__ int accepted;
-  if (threadIdx.x == 0) accepted = c->run_eval;
   __syncthreads();
-  if (!accepted) return;
+  if (threadIdx.x < kCtlWords) reinterpret_cast<int*>(c)[threadIdx.x] = reinterpret_cast<const int*>(&lc)[threadIdx.x];
+  if (kTail != kTailDecide || af.C == 0 || !lc.run_eval) return;
   for (int64_t i = threadIdx.x; i < af.n_x; i += blockDim.x) af.X_dst[i] = af.X_src[i];
   double xn = 0.0;
   const int cc = threadIdx.x;
@@ -1112,6 +1120,8 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
                   bool* nonfinite) {
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
+  HostTimer timer;
+  timer.tag = "solve";
   if (!h->lm_ctl) {
     if (hipMalloc(reinterpret_cast<void**>(&h->lm_ctl), sizeof(LmCtl)) != hipSuccess) {
       h->lm_ctl = nullptr;
@@ -1183,11 +1193,13 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
       if (!h->fuse_lm) k_lm_post<<<1, 1, 0, s>>>(h->lm_ctl, d.scal, h->lm_trace, h->lm_trace_cap);
     }
     if (rc) break;
+    timer.mark("batch enqueued");
     if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = fail(SFM_EIO, "LM control readback failed");
       break;
     }
+    timer.mark("batch synchronised");
     collect_marks(h);
     if (c.done) break;
     batch = batch_next;

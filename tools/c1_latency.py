@@ -78,6 +78,18 @@ def summarise(d):
     gaps.sort(reverse=True)
     print("gap total per solve (us):", round(sum(g for g, _ in gaps) / 1e3 / nsolve, 1))
     print("largest gaps before:", [(round(g / 1e3, 1), n) for g, n in gaps[:12]])
+    # the last resident solve in order: from the event after its set_problem's
+    # last host-to-device copy to the parameters' download
+    k = len(ev) - 1
+    while k > 0 and ev[k][2] != "C MEMORY_COPY_HOST_TO_DEVICE":
+        k -= 1
+    seq = ev[k + 1:]
+    t0 = seq[0][0] if seq else 0
+    print("last solve timeline (start us, duration us, gap before us):")
+    prev = t0
+    for s_, e_, n in seq:
+        print(f"  {(s_ - t0) / 1e3:8.1f} {(e_ - s_) / 1e3:7.1f} {(s_ - prev) / 1e3:6.1f}  {n}")
+        prev = max(prev, e_)
 
 
 if __name__ == "__main__":
