@@ -1458,7 +1458,17 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   const size_t il_base = host_check && stage_in ? (in_bytes + 255) / 256 * 256 : 0;
   const size_t il_bound =
       host_check && stage_in ? 64 * (size_t(C) + 1) + 2 * size_t(N) + 8 * (size_t(P) + 1) + 4 * size_t(C) + 2048 : 0;
-  if ((rc = stage_reserve(h, std::max(stage_in ? il_base + il_bound : 0, sizeof(int32_t) * (size_t(C) + 4)))))
+  // intrinsics, the parameters and their reset copies: one blob, one DMA
+  StageLayout pl;
+  const size_t o_K = pl.add(sizeof(double) * 5 * size_t(C)), o_c = pl.add(sizeof(double) * 6 * size_t(C)),
+               o_c0 = pl.add(sizeof(double) * 6 * size_t(C)), o_X = pl.add(sizeof(double) * 3 * size_t(P)),
+               o_X0 = pl.add(sizeof(double) * 3 * size_t(P));
+  // host-checked problems stage it behind the camera-run blob and upload it
+  // before the layout round trip (its host copies overlap the layout kernels)
+  const size_t pl_base = (il_base + il_bound + 255) / 256 * 256;
+  const bool early_params = il_base > 0 && (C || P) && pl_base + pl.bytes <= 4 * kStageMaxBytes;
+  if ((rc = stage_reserve(h, std::max({stage_in ? il_base + il_bound : 0, early_params ? pl_base + pl.bytes : 0,
+                                        sizeof(int32_t) * (size_t(C) + 4)}))))
     return bail(rc);
   stg = h->stage;
   uint8_t* in_blob = nullptr;
@@ -1652,6 +1662,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
                  o_fill = small ? il.add(sizeof(int32_t) * (size_t(P) + size_t(C))) : 0;
     if (il_base && il.bytes > il_bound) return bail(fail(SFM_EIO, "internal: camera-run blob above its bound"));
     if ((rc = stage_reserve(h, il_base + il.bytes))) return bail(rc);  // (never regrows with il_base > 0)
+    if (early_params && il_base + il.bytes > pl_base) return bail(fail(SFM_EIO, "internal: stage layout overlap"));
     stg = h->stage;
     uint8_t* ib = nullptr;
     ALLOC(ib, il.bytes);
@@ -1676,6 +1687,24 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     d.wcam = reinterpret_cast<int32_t*>(ib + o_w);
     d_cam_off = reinterpret_cast<int32_t*>(ib + o_off);
     ch_in = reinterpret_cast<int4*>(ib + o_ch);
+  }
+  if (early_params) {
+    uint8_t* pb = nullptr;
+    ALLOC(pb, pl.bytes);
+    d.Kc = reinterpret_cast<double*>(pb + o_K);
+    d.cam = reinterpret_cast<double*>(pb + o_c);
+    d.cam0 = reinterpret_cast<double*>(pb + o_c0);
+    d.X = reinterpret_cast<double*>(pb + o_X);
+    d.X0 = reinterpret_cast<double*>(pb + o_X0);
+    uint8_t* ps = stg + pl_base;
+    std::memcpy(ps + o_K, Kc.data(), sizeof(double) * Kc.size());
+    std::memcpy(ps + o_c, cam.data(), sizeof(double) * cam.size());
+    std::memcpy(ps + o_c0, cam.data(), sizeof(double) * cam.size());
+    if (P) {
+      std::memcpy(ps + o_X, X, sizeof(double) * 3 * size_t(P));
+      std::memcpy(ps + o_X0, X, sizeof(double) * 3 * size_t(P));
+    }
+    HCHK(hipMemcpyAsync(pb, ps, pl.bytes, hipMemcpyHostToDevice, s));
   }
   int32_t* small_cnt = nullptr;  // small path: per-block pair counts
   if (small) {
@@ -1764,11 +1793,6 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // the pinned mirror's 16-slot tail: the k_schur_pts group sizes
   int64_t* grp_host = reinterpret_cast<int64_t*>(d.scal_host + kNumScalars + 1);
   int bperm_per = 0;
-  // intrinsics, the parameters and their reset copies: one blob, one DMA
-  StageLayout pl;
-  const size_t o_K = pl.add(sizeof(double) * 5 * size_t(C)), o_c = pl.add(sizeof(double) * 6 * size_t(C)),
-               o_c0 = pl.add(sizeof(double) * 6 * size_t(C)), o_X = pl.add(sizeof(double) * 3 * size_t(P)),
-               o_X0 = pl.add(sizeof(double) * 3 * size_t(P));
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
   if (!small) ALLOC(d.seg, size_t(d.n_blk) + 1);
   ALLOC(d.bpts, std::max<size_t>(1, size_t(n_pairs)));
@@ -1831,7 +1855,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   d.nblk = d.ld / kNB;
   d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
                            d.jac_blocks_rec, blocks_for(npad, 256), obs_xcd_blocks(d), pt_xcd_blocks(d)});
-  {
+  if (!early_params) {
     uint8_t* pb = nullptr;
     ALLOC(pb, pl.bytes);
     d.Kc = reinterpret_cast<double*>(pb + o_K);
@@ -1897,7 +1921,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
 #undef ALLOC
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
-  if (C || P) {
+  if ((C || P) && !early_params) {
     if (pl.bytes <= kStageMaxBytes) {
       // the stage is free: the n_pairs readback synchronised the stream
       if ((rc = stage_reserve(h, pl.bytes))) return bail(rc);
@@ -1936,15 +1960,22 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   h->bs_epoch = 0;
   d.n_cu = h->n_cu;
   timer.mark("pairs + params launches");
-  HCHK(hipStreamSynchronize(s));
   if (bperm_per) {
+    // the k_schur_pts group sizes come back; the scratch buffers return to
+    // the pool once the stream is through with them
+    HCHK(hipStreamSynchronize(s));
     int64_t m_max = 1;
     for (int x = 0; x < 8; ++x) m_max = std::max<int64_t>(m_max, (grp_host[8 + x] + bperm_per - 1) / bperm_per);
     d.n_bslots = m_max * 8 * bperm_per;
+    retire_tmps(h);
+    timer.mark("pair lists + uploads (device)");
   }
+  // (otherwise no final synchronisation: the pair lists and uploads run on
+  // while the caller enqueues the solve -- stream order covers every reader;
+  // the scratch buffers stay out of the pool until the next set_problem's
+  // free_problem, after its synchronisation, and the pinned stage is next
+  // written by a call that synchronises first)
 #undef HCHK
-  retire_tmps(h);
-  timer.mark("pair lists + uploads (device)");
   h->has_problem = true;
   return 0;
 }

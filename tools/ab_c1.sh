@@ -4,7 +4,7 @@
 #   bash tools/ab_c1.sh head=abvar/var_head.so new= devsetup=:SFM_HOST_SETUP=0
 # (label=LIB[:VAR=VALUE ...]; an empty LIB is the in-tree library)
 R=$GRAFT_REPO_ROOT
-for pass in 1 2; do
+for pass in $(seq 1 ${PASSES:-2}); do
 for spec in "$@"; do
   label=${spec%%=*}; rest=${spec#*=}; lib=${rest%%:*}; envs=""
   [ "$rest" != "$lib" ] && envs=${rest#*:}
