@@ -123,8 +123,17 @@ struct sfm_ba_handle {
   // mirror and the device trace buffer (grown to the iteration cap)
   LmCtl* lm_ctl = nullptr;
   LmCtl* lm_ctl_host = nullptr;
+  // (pinned host memory: the deciding workgroups write the few entries
+  // straight to the host, which reads them after the batch's synchronisation)
   sfm_ba_iteration* lm_trace = nullptr;
   int lm_trace_cap = 0;
+  // one-shot sfm_ba_solve on a small problem: every batch's control readback
+  // also brings the parameters (cam | X) into param_host, so the final
+  // download needs no further round trip (param_host_valid until consumed)
+  bool prefetch_params = false;
+  bool param_host_valid = false;
+  double* param_host = nullptr;
+  size_t param_host_cap = 0;
   // pinned staging for every host <-> device transfer of set_problem,
   // get_parameters and the LM trace: a pageable copy goes through the
   // runtime's own staging (C1: the 320-KB uv upload took 131 us, the 49-KB
@@ -213,6 +222,7 @@ int stage_reserve(sfm_ba_handle* h, size_t bytes) {
 // would run them one after the other (C3 one-shot 7.4 -> 9.2 ms with the
 // 48-MB observation upload staged).
 constexpr size_t kStageMaxBytes = size_t(1) << 20;
+constexpr size_t kParamPrefetchMaxBytes = size_t(1) << 20;  // one-shot solves that prefetch their parameters
 
 // byte offsets of a packed staging layout (256-B aligned pieces)
 struct StageLayout {
@@ -1134,10 +1144,13 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
   }
   const int cap = std::max(1, opts.max_num_iterations + 1);
   if (h->lm_trace_cap < cap) {
-    if (h->lm_trace) (void)hipFree(h->lm_trace);
+    if (h->lm_trace) {
+      (void)hipStreamSynchronize(s);
+      (void)hipHostFree(h->lm_trace);
+    }
     h->lm_trace = nullptr;
     h->lm_trace_cap = 0;
-    if (hipMalloc(reinterpret_cast<void**>(&h->lm_trace), sizeof(sfm_ba_iteration) * size_t(cap)) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->lm_trace), sizeof(sfm_ba_iteration) * size_t(cap)) != hipSuccess) {
       h->lm_trace = nullptr;
       return fail(SFM_ENOMEM, "hipMalloc failed (LM trace)");
     }
@@ -1194,6 +1207,14 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
     }
     if (rc) break;
     timer.mark("batch enqueued");
+    if (h->prefetch_params) {
+      if (hipMemcpyAsync(h->param_host, d.cam, sizeof(double) * 6 * size_t(d.C), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipMemcpyAsync(h->param_host + 6 * size_t(d.C), d.X, sizeof(double) * 3 * size_t(d.P), hipMemcpyDeviceToHost,
+                         s) != hipSuccess) {
+        rc = fail(SFM_EIO, "parameter readback failed");
+        break;
+      }
+    }
     if (hipMemcpyAsync(&c, h->lm_ctl, sizeof(LmCtl), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = fail(SFM_EIO, "LM control readback failed");
@@ -1231,15 +1252,9 @@ int run_device_lm(sfm_ba_handle* h, const sfm_ba_options& opts, double* cost, sf
     push(it0);
   }
   const int n_tr = std::min(c.trace_len, h->lm_trace_cap);
-  if (n_tr) {
-    // (the stream is idle after the last control readback: the stage is free)
-    if (int e = stage_reserve(h, sizeof(sfm_ba_iteration) * size_t(n_tr))) return e;
-    HIPCHK(hipMemcpyAsync(h->stage, h->lm_trace, sizeof(sfm_ba_iteration) * size_t(n_tr), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::vector<sfm_ba_iteration> tr(static_cast<size_t>(n_tr));
-    std::memcpy(tr.data(), h->stage, sizeof(sfm_ba_iteration) * size_t(n_tr));
-    for (int i = 0; i < n_tr; ++i) push(tr[i]);
-  }
+  // (written to pinned host memory, complete at the last batch's synchronisation)
+  for (int i = 0; i < n_tr; ++i) push(h->lm_trace[i]);
+  h->param_host_valid = h->prefetch_params;
   sm->termination_type = c.termination;
   sm->num_iterations = c.iteration;
   sm->num_successful_steps += c.n_succ;
@@ -1307,7 +1322,8 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
   if (h->d.scal_host) hipHostFree(h->d.scal_host);
   if (h->lm_ctl) hipFree(h->lm_ctl);
   if (h->lm_ctl_host) hipHostFree(h->lm_ctl_host);
-  if (h->lm_trace) hipFree(h->lm_trace);
+  if (h->lm_trace) hipHostFree(h->lm_trace);
+  if (h->param_host) hipHostFree(h->param_host);
   if (h->stage) hipHostFree(h->stage);
   if (h->ar_tmp) hipFree(h->ar_tmp);
   for (void* p : {static_cast<void*>(h->dist.send), static_cast<void*>(h->dist.recv),
@@ -2257,7 +2273,39 @@ int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const 
     return rc;
   }
   rc = sfm_ba_set_problem(h, n_obs, obs_uv, cam_idx, pt_idx, n_cams, K9, rot, t, n_pts, X);
+  // small problems: the parameters ride in the solve's last control readback
+  const size_t np = 6 * size_t(std::max(0, n_cams)) + 3 * size_t(std::max(0, n_pts));
+  if (!rc && np * sizeof(double) <= kParamPrefetchMaxBytes) {
+    if (h->param_host_cap < np) {
+      if (h->param_host) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipHostFree(h->param_host);
+      }
+      h->param_host = nullptr;
+      h->param_host_cap = 0;
+      if (hipHostMalloc(reinterpret_cast<void**>(&h->param_host), std::max<size_t>(np, 4096) * sizeof(double)) ==
+          hipSuccess)
+        h->param_host_cap = std::max<size_t>(np, 4096);
+      else
+        h->param_host = nullptr;
+    }
+    h->prefetch_params = h->param_host != nullptr;
+  }
+  h->param_host_valid = false;
   if (!rc) rc = sfm_ba_solve_resident(h, opts, mode, summary, trace, trace_cap, trace_len);
+  h->prefetch_params = false;
+  if (!rc && h->param_host_valid) {
+    const double* cam = h->param_host;
+    for (int c = 0; c < n_cams; ++c)
+      for (int j = 0; j < 3; ++j) {
+        rot[3 * c + j] = cam[6 * c + j];
+        t[3 * c + j] = cam[6 * c + 3 + j];
+      }
+    if (n_pts) std::memcpy(X, h->param_host + 6 * size_t(n_cams), sizeof(double) * 3 * size_t(n_pts));
+    h->param_host_valid = false;
+    return 0;
+  }
+  h->param_host_valid = false;
   if (!rc) rc = sfm_ba_get_parameters(h, rot, t, X);
   return rc;
 }
