@@ -59,6 +59,7 @@ void launch_blk(int C, int2* blk, hipStream_t s);
 constexpr int kSmallSetupMaxC = 256;
 constexpr int kSmallSetupMaxChunks = 2048;
 constexpr int kSmallSetupMaxPtObs = 64;
+constexpr int64_t kSmallSetupMaxObs = 64 * 1024;  // (k_small_cm_compact: 64 steps of 1024)
 void launch_small_pm(int64_t N, const int32_t* pt, const int32_t* cam, const double* uv, const int32_t* pt_off,
                      int32_t* fill, int32_t* tmp, int32_t* order, double* uv_pm, int32_t* cam_pm, int32_t* pt_s,
                      hipStream_t s);

@@ -340,28 +340,50 @@ __global__ __launch_bounds__(kT) void k_small_pm_rank(int64_t N, const int32_t* 
 // One workgroup per camera: its point-major ids ascending (the stable sort
 // by camera of the point-major order) by a stable compaction -- 1024 ids
 // at a time, each wave's matches ranked by ballot, the waves in order.
+constexpr int kSmallCmMaxSteps = int(kSmallSetupMaxObs / 1024);
 __global__ __launch_bounds__(1024) void k_small_cm_compact(int64_t N, const int32_t* __restrict__ cam_pm,
                                                            const int32_t* __restrict__ cam_off,
                                                            int32_t* __restrict__ cm_order) {
-  __shared__ int wcnt[16];
+  // N <= 64 x 1024 (the small path's bound): thread t looks at observations
+  // t, t + 1024, ...; all loads first (one round trip), the hits as bits of
+  // one mask, the per-(step, wave) counts scanned once in LDS, then the
+  // scatter with the ballots recomputed from the masks.
+  __shared__ int cnt[kSmallCmMaxSteps * 16];
   const int c = blockIdx.x, t = threadIdx.x, l = t & 63, w = t >> 6;
   const uint64_t lt = (l == 0) ? 0ull : (~0ull >> (64 - l));
-  int run = cam_off[c];
-  for (int64_t base = 0; base < N; base += 1024) {
-    const int64_t q = base + t;
-    const bool hit = q < N && cam_pm[q] == c;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
-    if (l == 0) wcnt[w] = __popcll(m);
-    __syncthreads();
-    int before = 0, total = 0;
+  const int K = int((N + 1023) / 1024);
+  uint64_t hits = 0;
+#pragma unroll 8
+  for (int k = 0; k < K; ++k) {
+    const int64_t q = int64_t(k) * 1024 + t;
+    if (q < N && cam_pm[q] == c) hits |= 1ull << k;
+  }
+  for (int k = 0; k < K; ++k) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64((hits >> k) & 1);
+    if (l == 0) cnt[16 * k + w] = __popcll(m);
+  }
+  __syncthreads();
+  // exclusive scan of the K x 16 counts in (step, wave) order: thread e
+  // holds entry e (K x 16 <= 1024)
+  __shared__ int wsum[16];
+  const int ne = 16 * K;
+  const int v = t < ne ? cnt[t] : 0;
+  int incl = v;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      before += v < w ? wcnt[v] : 0;
-      total += wcnt[v];
-    }
-    if (hit) cm_order[run + before + __popcll(m & lt)] = int32_t(q);
-    run += total;
-    __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off);
+    if (l >= off) incl += o;
+  }
+  if (l == 63) wsum[w] = incl;
+  __syncthreads();
+  int wbase = 0;
+  for (int u = 0; u < w; ++u) wbase += wsum[u];
+  if (t < ne) cnt[t] = wbase + incl - v;
+  __syncthreads();
+  const int base = cam_off[c];
+  for (int k = 0; k < K; ++k) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64((hits >> k) & 1);
+    if ((hits >> k) & 1) cm_order[base + cnt[16 * k + w] + __popcll(m & lt)] = int32_t(int64_t(k) * 1024 + t);
   }
 }
 // The chunk table grouped by point slice (k_chunk_keys' key), stable: the
@@ -609,7 +631,7 @@ void launch_small_pm(int64_t N, const int32_t* pt, const int32_t* cam, const dou
 }
 void launch_small_cm(int64_t N, int C, const int32_t* cam_pm, const int32_t* cam_off, int32_t* cm_order,
                      hipStream_t s) {
-  if (N <= 0 || C <= 0) return;
+  if (N <= 0 || C <= 0 || N > kSmallSetupMaxObs) return;  // (set_problem's small-path bound)
   k_small_cm_compact<<<C, 1024, 0, s>>>(N, cam_pm, cam_off, cm_order);
 }
 void launch_small_chunks(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, int4* out,

@@ -1638,7 +1638,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // and the segments fit its bounds (SFM_SMALL_SETUP=0: the sorted path)
   // (C (C + 1) / 2 <= kSchurXcdMinBlocks: the plain k_schur_pts block order,
   // as the sorted path takes for these sizes)
-  bool small = host_check && stage_in && N > 0 && C > 0 && C <= kSmallSetupMaxC &&
+  bool small = host_check && stage_in && N > 0 && N <= kSmallSetupMaxObs && C > 0 && C <= kSmallSetupMaxC &&
                int64_t(C) * (C + 1) / 2 <= kSchurXcdMinBlocks;
   if (small) {
     const char* ss = std::getenv("SFM_SMALL_SETUP");
