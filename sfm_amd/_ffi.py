@@ -242,8 +242,10 @@ def check(rc: int, what: str) -> None:
 def ptr(a: np.ndarray | None) -> c_void_p | None:
     if a is None:
         return None
-    assert a.flags["C_CONTIGUOUS"], "arrays passed to the C ABI must be C-contiguous"
-    return a.ctypes.data_as(c_void_p)
+    assert a.flags.c_contiguous, "arrays passed to the C ABI must be C-contiguous"
+    # (the array interface's address: ~1.4 us, where ctypes.data_as takes ~5 us
+    # per array -- 20-30 us of every keyframe solve's call)
+    return c_void_p(a.__array_interface__["data"][0])
 
 
 def default_options() -> BAOptions:

@@ -25,6 +25,26 @@ def run():
         walls.append(time.perf_counter() - t0)
     w = np.array(walls[5:]) * 1e3
     print(f"C1 one-shot: median {np.median(w):.3f} ms, min {w.min():.3f} ms, iterations {sm.num_iterations}")
+    # the same call through the C ABI alone (arguments prepared once, the
+    # parameters reset by copyto outside the clock): what a C++ caller sees
+    import ctypes
+    from sfm_amd import ba as B
+    L = B.lib()
+    opts, smr = B.default_options(), B.BASummary()
+    tr, tl = (B.BAIteration * 128)(), ctypes.c_int32(0)
+    r, t, X = sc.rot.copy(), sc.t.copy(), sc.X.copy()
+    uv, ci, pi, K = B._f64(sc.uv), B._i32(sc.cam_idx), B._i32(sc.pt_idx), B._f64(sc.K)
+    args = (ctypes.byref(opts), B.STRUCT_AND_POSE, int(uv.shape[0]), B.ptr(uv), B.ptr(ci), B.ptr(pi), int(r.shape[0]), B.ptr(K),
+            B.ptr(r), B.ptr(t), int(X.shape[0]), B.ptr(X), ctypes.byref(smr), tr, 128, ctypes.byref(tl))
+    raw = []
+    for k in range(30):
+        np.copyto(r, sc.rot); np.copyto(t, sc.t); np.copyto(X, sc.X)
+        t0 = time.perf_counter()
+        rc = L.sfm_ba_solve(*args)
+        raw.append(time.perf_counter() - t0)
+        assert rc == 0
+    w = np.array(raw[5:]) * 1e3
+    print(f"C1 one-shot, C ABI call only: median {np.median(w):.3f} ms, min {w.min():.3f} ms")
     ba = sfm_amd.BundleAdjuster(0)
     ts, tv, tg = [], [], []
     for k in range(30):
