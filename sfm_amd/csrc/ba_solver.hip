@@ -2010,21 +2010,25 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   h->bs_epoch = 0;
   d.n_cu = h->n_cu;
   timer.mark("pairs + params launches");
-  if (bperm_per) {
-    // the k_schur_pts group sizes come back; the scratch buffers return to
-    // the pool once the stream is through with them
+  // Small problems end without a synchronisation: every host-to-device copy
+  // came from the pinned stage, nothing is read back, so the pair lists and
+  // uploads run on while the caller enqueues the solve (stream order covers
+  // every reader; the scratch buffers stay out of the pool until the next
+  // set_problem's free_problem, after its synchronisation, and the stage is
+  // next written by a call that synchronises first).  Otherwise: the
+  // k_schur_pts group sizes come back, copies from pageable host memory (the
+  // caller's arrays, this call's vectors) complete, and the scratch buffers
+  // return to the pool.
+  if (!(small && early_params && !bperm_per)) {
     HCHK(hipStreamSynchronize(s));
-    int64_t m_max = 1;
-    for (int x = 0; x < 8; ++x) m_max = std::max<int64_t>(m_max, (grp_host[8 + x] + bperm_per - 1) / bperm_per);
-    d.n_bslots = m_max * 8 * bperm_per;
+    if (bperm_per) {
+      int64_t m_max = 1;
+      for (int x = 0; x < 8; ++x) m_max = std::max<int64_t>(m_max, (grp_host[8 + x] + bperm_per - 1) / bperm_per);
+      d.n_bslots = m_max * 8 * bperm_per;
+    }
     retire_tmps(h);
     timer.mark("pair lists + uploads (device)");
   }
-  // (otherwise no final synchronisation: the pair lists and uploads run on
-  // while the caller enqueues the solve -- stream order covers every reader;
-  // the scratch buffers stay out of the pool until the next set_problem's
-  // free_problem, after its synchronisation, and the pinned stage is next
-  // written by a call that synchronises first)
 #undef HCHK
   h->has_problem = true;
   return 0;
