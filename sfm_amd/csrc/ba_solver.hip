@@ -1452,6 +1452,13 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     if (e_ != hipSuccess) return bail(fail(SFM_EIO, std::string(#expr) + ": " + hipGetErrorString(e_))); \
   } while (0)
   std::vector<int32_t> cam_cnt(size_t(C) + 4);
+  // host-checked problems with few cameras: per camera, its observations per
+  // point slice (the 8 XCD slices of k_small_chunks' key p * 8 / P) -- the
+  // chunk table's slice sizes follow from them on the host -- and the pair
+  // total's estimate (no same-camera duplicates): the small path then needs no
+  // round trip before the pair lists
+  std::vector<int32_t> cam_slice;
+  int64_t pairs_est = 0;
   uint8_t* stg = nullptr;
   double* in_uv = nullptr;
   int32_t *in_cam = nullptr, *in_pt = nullptr, *cnt_p = nullptr;
@@ -1509,6 +1516,17 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     uint32_t bad = 0;
     {
       std::vector<int32_t> cc4(4 * (size_t(C) + 1), 0), pc4(4 * (size_t(P) + 1), 0);
+      // slice s = floor(8 p / P) holds p >= ceil(s P / 8): seven comparisons
+      const bool want_slices = C <= kSmallSetupMaxC && P > 0;
+      uint32_t sb[8];
+      for (int k = 1; k < 8; ++k) sb[k] = uint32_t((int64_t(k) * P + 7) / 8);
+      auto slice_of = [&](uint32_t p) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 1; k < 8; ++k) v += uint32_t(p >= sb[k]);
+        return v;
+      };
+      std::vector<int32_t> cs4(want_slices ? 4 * 8 * (size_t(C) + 1) : 0, 0);
       int64_t i = 0;
       for (; i + 4 <= N; i += 4) {
 #pragma unroll
@@ -1519,22 +1537,34 @@ constexpr int64_t kHostCheckMaxObs = 65536;
           bad |= b;
           // (an out-of-range index lands in the spare slot C / P: the counts
           // are discarded with the error anyway)
-          ++cc4[u * (size_t(C) + 1) + (c < uint32_t(C) ? c : uint32_t(C))];
+          const uint32_t cc = c < uint32_t(C) ? c : uint32_t(C);
+          ++cc4[u * (size_t(C) + 1) + cc];
           ++pc4[u * (size_t(P) + 1) + (p < uint32_t(P) ? p : uint32_t(P))];
+          if (want_slices) ++cs4[(u * (size_t(C) + 1) + cc) * 8 + slice_of(p)];
         }
       }
       for (; i < N; ++i) {
         const uint32_t c = uint32_t(cam_idx[i]), p = uint32_t(pt_idx[i]);
         bad |= uint32_t(c >= uint32_t(C)) | uint32_t(p >= uint32_t(P)) | nonfinite(uvb[2 * i]) |
                nonfinite(uvb[2 * i + 1]);
-        ++cc4[c < uint32_t(C) ? c : uint32_t(C)];
+        const uint32_t cc = c < uint32_t(C) ? c : uint32_t(C);
+        ++cc4[cc];
         ++pc4[p < uint32_t(P) ? p : uint32_t(P)];
+        if (want_slices) ++cs4[size_t(cc) * 8 + slice_of(p)];
+      }
+      if (want_slices) {
+        cam_slice.assign(8 * size_t(C), 0);
+        for (size_t e = 0; e < 8 * size_t(C); ++e)
+          cam_slice[e] = cs4[e] + cs4[8 * (size_t(C) + 1) + e] + cs4[16 * (size_t(C) + 1) + e] +
+                         cs4[24 * (size_t(C) + 1) + e];
       }
       for (int c = 0; c < C; ++c)
         cam_cnt[4 + size_t(c)] = cc4[c] + cc4[(size_t(C) + 1) + c] + cc4[2 * (size_t(C) + 1) + c] +
                                  cc4[3 * (size_t(C) + 1) + c];
-      for (int p = 0; p < P; ++p)
+      for (int p = 0; p < P; ++p) {
         pc[p] = pc4[p] + pc4[(size_t(P) + 1) + p] + pc4[2 * (size_t(P) + 1) + p] + pc4[3 * (size_t(P) + 1) + p];
+        pairs_est += int64_t(pc[p]) * (pc[p] - 1) / 2;
+      }
     }
     if (bad) {
       for (int64_t i = 0; i < N; ++i) {
@@ -1773,7 +1803,6 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     launch_small_chunks(int(nch), ch_in, cm_order, pt_s, P, d.jchunks, d.jgrp, s);
     launch_small_pairs_count(C, d.n_blk, d_cam_off, cm_order, d.cam_pm, pt_s, d.pt_off, small_cnt, d.seg, s);
     // (into the stage: stream order puts it after the upload that reads the stage)
-    HCHK(hipMemcpyAsync(stg, d.seg + d.n_blk, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   } else {
   timer.mark("allocs + camera-run blob");
   // point-major order: stable sort by (point, camera)
@@ -1798,28 +1827,44 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // (into the stage: stream order puts it after the upload that reads the stage)
   HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
-  // and the 8 slices' chunk offsets: the observation passes size their grids
-  // by the largest slice (obs_xcd_blocks)
-  HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  timer.mark("layout launches");
-  HCHK(hipStreamSynchronize(s));
   if (small) {
-    int32_t np32 = 0;
-    std::memcpy(&np32, stg, sizeof(int32_t));
-    n_pairs = np32;
+    // no round trip: the pair lists go into a buffer of the pair total's
+    // bound (every ordered pair of a point's observations: twice the
+    // estimate), the chunk table's slice sizes come from the host's
+    // per-camera slice counts (a camera's chunk k starts at its 64 k-th
+    // observation in point order, whose slice the counts' running sum gives)
+    n_pairs = std::max<int64_t>(1, 2 * pairs_est);
+    std::array<int32_t, 8> jcnt{};
+    for (int c = 0; c < C; ++c) {
+      const int32_t n_c = cam_cnt[4 + size_t(c)];
+      int32_t cum = 0;
+      int sl = 0;
+      for (int32_t k = 0; 64 * k < n_c; ++k) {
+        while (sl < 7 && cum + cam_slice[8 * size_t(c) + sl] <= 64 * k) cum += cam_slice[8 * size_t(c) + sl++];
+        ++jcnt[sl];
+      }
+    }
+    d.xcd_slice_max = *std::max_element(jcnt.begin(), jcnt.end());
+    timer.mark("layout launches");
   } else {
+    // and the 8 slices' chunk offsets: the observation passes size their
+    // grids by the largest slice (obs_xcd_blocks)
+    HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    timer.mark("layout launches");
+    HCHK(hipStreamSynchronize(s));
     std::memcpy(&n_pairs, stg, sizeof(int64_t));
-  }
-  {
     int32_t g[9];
     std::memcpy(g, stg + 8, sizeof(g));
     d.xcd_slice_max = 0;
     for (int i = 0; i < 8; ++i) d.xcd_slice_max = std::max(d.xcd_slice_max, g[i + 1] - g[i]);
+    timer.mark("layouts (device)");
   }
-  timer.mark("layouts (device)");
   if (n_pairs >= int64_t(INT32_MAX)) return bail(fail(SFM_EINVAL, "too many Schur pairs for 32-bit offsets"));
   d.n_blk = int64_t(C) * (C + 1) / 2;
-  d.n_pairs = n_pairs;
+  // the Schur pass's shape below follows the mean pair count: the host's
+  // estimate on host-checked problems (either layout path, so both choose
+  // alike), else the device's count
+  d.n_pairs = host_check && stage_in && !cam_slice.empty() ? pairs_est : n_pairs;
   // lanes per Schur block ~ a tenth of the mean pair count, 8..64 (measured
   // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
   if (const char* ss = std::getenv("SFM_SCHUR_PTS_SUB")) {
