@@ -27,6 +27,7 @@
 #include "ba_device.h"
 #include "ba_setup.h"
 #include "ba_common.h"
+#include "ba_host_layout.h"
 #include "../../include/sfm_amd.h"
 
 namespace {
@@ -1479,8 +1480,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // which is still in flight -- no synchronisation in between -- so the
   // stage holds both from here: 2 C + chunks + ... ints, bounded)
   const size_t il_base = host_check && stage_in ? (in_bytes + 255) / 256 * 256 : 0;
-  const size_t il_bound =
-      host_check && stage_in ? 64 * (size_t(C) + 1) + 2 * size_t(N) + 8 * (size_t(P) + 1) + 4 * size_t(C) + 2048 : 0;
+  const size_t il_bound = host_check && stage_in ? hostlayout::runs_blob_bound(C, N, P) : 0;
   // intrinsics, the parameters and their reset copies: one blob, one DMA
   StageLayout pl;
   const size_t o_K = pl.add(sizeof(double) * 5 * size_t(C)), o_c = pl.add(sizeof(double) * 6 * size_t(C)),
@@ -1502,84 +1502,9 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   int32_t* err = nullptr;
   int32_t* cnt_c = nullptr;
   if (host_check && stage_in) {
-    // k_validate's checks and counts.  Fast pass: the checks OR-ed without
-    // branches and the counts in four interleaved histograms (consecutive
-    // observations of one camera would otherwise chain every increment
-    // through a store-to-load dependency: C1's 20k observations took 33 us);
-    // only a problem with a bad observation takes the exact first-index pass.
-    int32_t first[3] = {INT32_MAX, INT32_MAX, INT32_MAX};
-    std::fill(cam_cnt.begin(), cam_cnt.end(), 0);
-    int32_t* pc = reinterpret_cast<int32_t*>(stg + o_pc);
-    std::fill(pc, pc + size_t(P) + 1, 0);
-    const uint64_t* uvb = reinterpret_cast<const uint64_t*>(obs_uv);
-    auto nonfinite = [](uint64_t b) { return uint32_t(((b >> 52) & 0x7ff) == 0x7ff); };
-    uint32_t bad = 0;
-    {
-      std::vector<int32_t> cc4(4 * (size_t(C) + 1), 0), pc4(4 * (size_t(P) + 1), 0);
-      // slice s = floor(8 p / P) holds p >= ceil(s P / 8): seven comparisons
-      const bool want_slices = C <= kSmallSetupMaxC && P > 0;
-      uint32_t sb[8];
-      for (int k = 1; k < 8; ++k) sb[k] = uint32_t((int64_t(k) * P + 7) / 8);
-      auto slice_of = [&](uint32_t p) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 1; k < 8; ++k) v += uint32_t(p >= sb[k]);
-        return v;
-      };
-      std::vector<int32_t> cs4(want_slices ? 4 * 8 * (size_t(C) + 1) : 0, 0);
-      int64_t i = 0;
-      for (; i + 4 <= N; i += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t c = uint32_t(cam_idx[i + u]), p = uint32_t(pt_idx[i + u]);
-          const uint32_t b = uint32_t(c >= uint32_t(C)) | uint32_t(p >= uint32_t(P)) | nonfinite(uvb[2 * (i + u)]) |
-                             nonfinite(uvb[2 * (i + u) + 1]);
-          bad |= b;
-          // (an out-of-range index lands in the spare slot C / P: the counts
-          // are discarded with the error anyway)
-          const uint32_t cc = c < uint32_t(C) ? c : uint32_t(C);
-          ++cc4[u * (size_t(C) + 1) + cc];
-          ++pc4[u * (size_t(P) + 1) + (p < uint32_t(P) ? p : uint32_t(P))];
-          if (want_slices) ++cs4[(u * (size_t(C) + 1) + cc) * 8 + slice_of(p)];
-        }
-      }
-      for (; i < N; ++i) {
-        const uint32_t c = uint32_t(cam_idx[i]), p = uint32_t(pt_idx[i]);
-        bad |= uint32_t(c >= uint32_t(C)) | uint32_t(p >= uint32_t(P)) | nonfinite(uvb[2 * i]) |
-               nonfinite(uvb[2 * i + 1]);
-        const uint32_t cc = c < uint32_t(C) ? c : uint32_t(C);
-        ++cc4[cc];
-        ++pc4[p < uint32_t(P) ? p : uint32_t(P)];
-        if (want_slices) ++cs4[size_t(cc) * 8 + slice_of(p)];
-      }
-      if (want_slices) {
-        cam_slice.assign(8 * size_t(C), 0);
-        for (size_t e = 0; e < 8 * size_t(C); ++e)
-          cam_slice[e] = cs4[e] + cs4[8 * (size_t(C) + 1) + e] + cs4[16 * (size_t(C) + 1) + e] +
-                         cs4[24 * (size_t(C) + 1) + e];
-      }
-      for (int c = 0; c < C; ++c)
-        cam_cnt[4 + size_t(c)] = cc4[c] + cc4[(size_t(C) + 1) + c] + cc4[2 * (size_t(C) + 1) + c] +
-                                 cc4[3 * (size_t(C) + 1) + c];
-      for (int p = 0; p < P; ++p) {
-        pc[p] = pc4[p] + pc4[(size_t(P) + 1) + p] + pc4[2 * (size_t(P) + 1) + p] + pc4[3 * (size_t(P) + 1) + p];
-        pairs_est += int64_t(pc[p]) * (pc[p] - 1) / 2;
-      }
-    }
-    if (bad) {
-      for (int64_t i = 0; i < N; ++i) {
-        const int32_t c = cam_idx[i], p = pt_idx[i];
-        const bool cok = c >= 0 && c < C, pok = p >= 0 && p < P;
-        const bool uok = std::isfinite(obs_uv[2 * i]) && std::isfinite(obs_uv[2 * i + 1]);
-        if (!cok && first[0] == INT32_MAX) first[0] = int32_t(i);
-        if (!pok && first[1] == INT32_MAX) first[1] = int32_t(i);
-        if (!uok && first[2] == INT32_MAX) first[2] = int32_t(i);
-      }
-    }
-    cam_cnt[0] = first[0];
-    cam_cnt[1] = first[1];
-    cam_cnt[2] = first[2];
-    cam_cnt[3] = INT32_MAX;
+    // k_validate's checks and counts on the host (ba_host_layout.h)
+    hostlayout::check_and_count(N, obs_uv, cam_idx, pt_idx, C, P, C <= kSmallSetupMaxC, cam_cnt.data(),
+                                reinterpret_cast<int32_t*>(stg + o_pc), &cam_slice, &pairs_est);
     cnt_p = reinterpret_cast<int32_t*>(in_blob + o_pc);
     timer.mark("host checks + counts");
   } else {
@@ -1631,29 +1556,12 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // ---- camera runs: camera-major, each camera's run padded to a whole
   // number of 64-wide wavefront chunks; the chunk table camera-major
   // (grouped into 8 point slices on the device, one per XCD) ----
-  std::vector<int32_t> cam_off(size_t(C) + 1, 0), cam_rng(2 * size_t(C));
-  int64_t npad = 0;
-  for (int c = 0; c < C; ++c) {
-    const int32_t n_c = cam_cnt[4 + c];
-    cam_off[c + 1] = cam_off[c] + n_c;
-    cam_rng[2 * c] = int32_t(npad);
-    cam_rng[2 * c + 1] = int32_t(npad + n_c);
-    npad += (n_c + 63) / 64 * 64;
-  }
+  hostlayout::Runs runs;
+  hostlayout::camera_runs(C, cam_cnt.data() + 4, &runs);
+  const std::vector<int32_t>&cam_off = runs.cam_off, &cam_rng = runs.cam_rng, &wcam = runs.wcam;
+  const std::vector<hostlayout::Chunk>& chunks = runs.chunks;
+  const int64_t npad = runs.npad;
   d.N_pad = npad;
-  std::vector<int32_t> wcam(size_t(npad / 64) + 1, 0);
-  for (int c = 0; c < C; ++c)
-    for (int64_t w = cam_rng[2 * c] / 64; w < (int64_t(cam_rng[2 * c]) + cam_off[c + 1] - cam_off[c] + 63) / 64; ++w)
-      wcam[w] = c;
-  // (camera, first position, count, first observation's camera-major index),
-  // camera-major: a k_jacobian wave runs through consecutive chunks of a
-  // slice and reduces once per camera
-  std::vector<int4> chunks;
-  for (int c = 0; c < C; ++c) {
-    const int32_t n_c = cam_off[c + 1] - cam_off[c];
-    for (int32_t k = 0; 64 * k < n_c; ++k)
-      chunks.push_back(make_int4(c, cam_rng[2 * c] + 64 * k, std::min<int32_t>(64, n_c - 64 * k), cam_off[c] + 64 * k));
-  }
   d.n_jchunks = int32_t(chunks.size());
   d.jac_blocks_rec = 8 * std::max(1, std::min((d.n_jchunks / 8 + 3) / 4, 128));  // multiple of 8 (one slice per XCD)
   // the record-free pass of the solve (no 160-B stores) prefers a larger
@@ -1735,7 +1643,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     // cam_rng | wcam (resident), cam_off | chunks (read by the setup only)
     StageLayout il;
     const size_t o_rng = il.add(sizeof(int32_t) * cam_rng.size()), o_w = il.add(sizeof(int32_t) * wcam.size()),
-                 o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(int4) * chunks.size());
+                 o_off = il.add(sizeof(int32_t) * cam_off.size()), o_ch = il.add(sizeof(hostlayout::Chunk) * chunks.size());
     // small path: pt_off (the host's scan of the point counts, resident) and
     // the zeroed slot counters of the point / camera scatters
     const size_t o_poff = small ? il.add(sizeof(int32_t) * (size_t(P) + 1)) : 0,
@@ -1750,7 +1658,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     std::memcpy(sb + o_rng, cam_rng.data(), sizeof(int32_t) * cam_rng.size());
     std::memcpy(sb + o_w, wcam.data(), sizeof(int32_t) * wcam.size());
     std::memcpy(sb + o_off, cam_off.data(), sizeof(int32_t) * cam_off.size());
-    if (nch) std::memcpy(sb + o_ch, chunks.data(), sizeof(int4) * chunks.size());
+    if (nch) std::memcpy(sb + o_ch, chunks.data(), sizeof(hostlayout::Chunk) * chunks.size());
     if (small) {
       const int32_t* pc = reinterpret_cast<const int32_t*>(stg + o_pc);
       int32_t* po = reinterpret_cast<int32_t*>(sb + o_poff);
@@ -1834,17 +1742,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     // per-camera slice counts (a camera's chunk k starts at its 64 k-th
     // observation in point order, whose slice the counts' running sum gives)
     n_pairs = std::max<int64_t>(1, 2 * pairs_est);
-    std::array<int32_t, 8> jcnt{};
-    for (int c = 0; c < C; ++c) {
-      const int32_t n_c = cam_cnt[4 + size_t(c)];
-      int32_t cum = 0;
-      int sl = 0;
-      for (int32_t k = 0; 64 * k < n_c; ++k) {
-        while (sl < 7 && cum + cam_slice[8 * size_t(c) + sl] <= 64 * k) cum += cam_slice[8 * size_t(c) + sl++];
-        ++jcnt[sl];
-      }
-    }
-    d.xcd_slice_max = *std::max_element(jcnt.begin(), jcnt.end());
+    d.xcd_slice_max = hostlayout::small_slice_max(C, cam_cnt.data() + 4, cam_slice);
     timer.mark("layout launches");
   } else {
     // and the 8 slices' chunk offsets: the observation passes size their

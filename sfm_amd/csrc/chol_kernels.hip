@@ -16,12 +16,37 @@
 // flag-chained block rows (k_backsolve).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdlib>
 #include "ba_device.h"
 #include "ba_common.h"
 
 namespace sfm {
+#ifdef SFM_CHOL_STAMPS
+// Development build only (tools/chol_stamps.sh): s_memrealtime (100 MHz)
+// stamps of the diagonal walker's phases, g_wstamp[step][slot], and the
+// helpers' publication times of the tiles the walker awaits, g_hstamp[i][j]
+// (slot 0: partial tile, slot 1: final tile).  Read by sfm_debug_stamps.
+__device__ unsigned long long g_wstamp[256 * 16];
+__device__ unsigned long long g_hstamp[128 * 128 * 2];
+#define WSTAMP(j, k)                                                                          \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define WSTAMPV(j, k, v)                                       \
+  do {                                                         \
+    if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = (v); \
+  } while (0)
+#define HSTAMP(i, j, k)                                                                                         \
+  do {                                                                                                          \
+    if (threadIdx.x == 0 && (i) < 128 && (j) < 128) g_hstamp[((i) * 128 + (j)) * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define WSTAMP(j, k) do { } while (0)
+#define WSTAMPV(j, k, v) do { } while (0)
+#define HSTAMP(i, j, k) do { } while (0)
+#endif
 namespace {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -160,14 +185,77 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
 // waves 1-3 apply it while wave 0 factors panel 0, before the trailing
 // update of panel 0 touches those blocks (every block keeps its update
 // order: bitwise the same factor).
-// pf_sub != nullptr: wave 3 polls the flags of the walker's next two
-// partial tiles once during panel 3 and leaves in *rdy whether both are out,
-// so the walker can load them beside W_j's publication (a poll during panel
-// 2 mostly came too early: the tile (j+1, j) waits for L_j,j-1).
-template <bool kFull>  // every pivot of the tile is a real one (k0 + 64 <= n)
+// pf_sub != nullptr: wave 2 (idle in panel 2) polls the flag of the
+// walker's next partial tile (j+1, j) during panel 2 and leaves in rdy[0]
+// whether it is out; if so, waves 1-3 issue their loads of that tile
+// (pre.load(), to registers) at the top of their panel-3 work, and the walker
+// writes them to its LDS image after the POTRF (pre.store()): the memory
+// latency -- 2-3 us under the helpers' traffic, stamped -- runs beside panel
+// 3 and the W row.  Wave 3 polls the next diagonal partial tile's flag
+// (pf_diag) at the top of panel 3 and leaves it in rdy[1].  (The loads are
+// sc1 loads of sc1-stored bytes behind a relaxed poll and a barrier: no agent
+// acquire, MI355X_MICROARCH.md "Valid forms", row 1.)  Panel 3 is peeled out
+// of the panel loop so that the prefetched registers are live from there on
+// only.
+struct NoPrefetch {
+  __device__ void load() {}
+};
+
+// Wave 0's factorisation of panel b >= 1 (columns g0 = 16 b ..): rows r < g0
+// are above the diagonal (don't-care), so lanes 0..15 carry W_bb column r in
+// p itself: the elimination applies the same operations to [A_panel | I] rows
+// (p[j] *= inv, p[c] -= p[j] L(g0+c, g)), so one FMA stream updates both --
+// half the pivot work of the separate wc[] registers.  Their T writes land in
+// the tile's strictly upper part, which nothing reads.
+template <bool kFull>
+__device__ __forceinline__ void panel_w0(double* T, double* Wl, int g0, int k0, int n, int lane, bool& bad) {
+  const int r = lane;
+  const bool wl = r < 16;
+  double p[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) p[j] = wl ? ((j == r) ? 1.0 : 0.0) : T[(g0 + j) * TS + r];
+  double d = bcast(p[0], g0);
+  // column j's LDS-fed updates (p[c], c >= j + 2) are applied one step
+  // late, right before they are first needed, so the LDS round trip
+  // overlaps the next pivot's rsqrt chain; every p[c] still takes its
+  // column updates in column order (bitwise the eager form)
+  double lp = 0.0, lcp[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) lcp[c] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int g = g0 + j;
+    if (kFull || k0 + g < n) bad |= !(d > 0.0);
+    else d = 1.0;
+    const double inv = rsqrt_nr(d);
+    const double l = p[j] * inv;
+    p[j] = l;
+    T[g * TS + r] = l;
+    if (j >= 1 && j < 15) {
+#pragma unroll
+      for (int c = j + 1; c < 16; ++c) p[c] = fma(-lp, lcp[c], p[c]);  // column j - 1
+    }
+    if (j < 15) {
+      const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
+      const double l1 = bcast(l, g + 1);
+      p[j + 1] = fma(-l, l1, p[j + 1]);
+      if (j < 14) {
+#pragma unroll
+        for (int c = j + 2; c < 16; ++c) lcp[c] = T[g * TS + g0 + c];
+      }
+      lp = l;
+      d = dn;
+    }
+  }
+  if (wl)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = p[c];
+}
+
+template <bool kFull, class Pre>  // kFull: every pivot of the tile is a real one (k0 + 64 <= n)
 __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[256], int k0, int n,
                                            const double* Ls, const int* pf_sub, const int* pf_diag, int epoch,
-                                           int* rdy) {
+                                           int* rdy, Pre& pre) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -176,56 +264,10 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   }
   __syncthreads();
   bool bad = false;
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < 3; ++b) {
     const int g0 = 16 * b;
     if (w == 0 && b > 0) {
-      // ---- panels 1..3: rows r < g0 are above the diagonal (don't-care), so
-      // lanes 0..15 carry W_bb column r in p itself: the elimination applies
-      // the same operations to [A_panel | I] rows (p[j] *= inv, p[c] -= p[j]
-      // L(g0+c, g)), so one FMA stream updates both -- half the pivot work of
-      // the separate wc[] registers.  Their T writes land in the tile's
-      // strictly upper part, which nothing reads.
-      const int r = lane;
-      const bool wl = r < 16;
-      double p[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) p[j] = wl ? ((j == r) ? 1.0 : 0.0) : T[(g0 + j) * TS + r];
-      double d = bcast(p[0], g0);
-      // column j's LDS-fed updates (p[c], c >= j + 2) are applied one step
-      // late, right before they are first needed, so the LDS round trip
-      // overlaps the next pivot's rsqrt chain; every p[c] still takes its
-      // column updates in column order (bitwise the eager form)
-      double lp = 0.0, lcp[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) lcp[c] = 0.0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int g = g0 + j;
-        if (kFull || k0 + g < n) bad |= !(d > 0.0);
-        else d = 1.0;
-        const double inv = rsqrt_nr(d);
-        const double l = p[j] * inv;
-        p[j] = l;
-        T[g * TS + r] = l;
-        if (j >= 1 && j < 15) {
-#pragma unroll
-          for (int c = j + 1; c < 16; ++c) p[c] = fma(-lp, lcp[c], p[c]);  // column j - 1
-        }
-        if (j < 15) {
-          const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
-          const double l1 = bcast(l, g + 1);
-          p[j + 1] = fma(-l, l1, p[j + 1]);
-          if (j < 14) {
-#pragma unroll
-            for (int c = j + 2; c < 16; ++c) lcp[c] = T[g * TS + g0 + c];
-          }
-          lp = l;
-          d = dn;
-        }
-      }
-      if (wl)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = p[c];
+      panel_w0<kFull>(T, Wl, g0, k0, n, lane, bad);
     } else if (w == 0) {
       // ---- panel 0 factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
       const int r = lane;
@@ -284,32 +326,46 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     } else if (b == 1) {
       // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
       trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
-    } else if (b == 2 && w == 1) {
+    } else if (w == 1) {
       w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
-    } else if (b == 2 && w == 3) {
+    } else if (w == 3) {
       trail_block(T, 16, 3, 3, lane);  // panel 1's trailing update of block (3,3)
-    } else if (b == 3) {
-      // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
-      if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      w_row3_sum(T, Wl, scr[w], w - 1, lane);
-      if (w == 3 && pf_sub != nullptr)
-        *rdy = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-               __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    } else if (pf_sub != nullptr) {  // (b == 2, wave 2)
+      rdy[0] = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     }
     __syncthreads();
+    WSTAMP(k0 / NB, 2 + b);
     // ---- trailing update of column block b+1 (the next panel's); the
     // blocks right of it follow during the next panel (look-ahead) ----
-    if (b < 3) {
-      if (w < 3 - b) trail_block(T, g0, b + 1 + w, b + 1, lane);
-      __syncthreads();
-    }
+    if (w < 3 - b) trail_block(T, g0, b + 1 + w, b + 1, lane);
+    __syncthreads();
+    WSTAMP(k0 / NB, 6 + b);
   }
+  // ---- panel 3 (peeled) ----
+  if (w == 0) {
+    panel_w0<kFull>(T, Wl, 48, k0, n, lane, bad);
+  } else {
+    // the walker's next partial tiles: the diagonal tile's poll, then the
+    // prefetch's loads go out first (the poll ahead of them: vmcnt is one
+    // in-order counter, so its value waits only for itself), its result is
+    // written at the end
+    int dflag = 0;
+    if (w == 3 && pf_diag != nullptr) dflag = __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pf_sub != nullptr && __builtin_amdgcn_readfirstlane(rdy[0]) != 0) pre.load();
+    // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
+    if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    w_row3_sum(T, Wl, scr[w], w - 1, lane);
+    if (w == 3 && pf_diag != nullptr) rdy[1] = dflag == epoch;
+  }
+  __syncthreads();
+  WSTAMP(k0 / NB, 5);
   // ---- W row 3 off the diagonal: the products with W_33 ----
   if (w >= 1) w_row3_finish(Wl, scr[w], w - 1, lane);
   __syncthreads();
+  WSTAMP(k0 / NB, 9);
   return bad;
 }
 
@@ -572,6 +628,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
             st_wt(A + size_t(j0 + cb + 16 * a + lk + 4 * reg) * ld + i0 + rb + 16 * bb + lr, cv[a][bb][reg] - acc[a][bb][reg]);
     }
     block_publish_wt(Pf + i * nb + j, epoch);
+    HSTAMP(i, j, 0);
     return;
   }
   // final tile: T -> LDS, then X = T W_j^T on MFMA once W_j is out
@@ -589,6 +646,7 @@ __device__ __forceinline__ void fused_helper_tile(double* __restrict__ A, int ld
   trsm_rows<1>(Tp, Wk, x, lane);
   put_rows<1>(A, ld, i0, j0, x, lane);
   block_publish_wt(F + i * nb + j, epoch);
+  HSTAMP(i, j, 1);
 }
 
 // Helper: the vertical pair of final tiles (i, j), (i+1, j) (i >= j + 2).
@@ -672,6 +730,8 @@ __device__ __forceinline__ void fused_helper_pair(double* __restrict__ A, int ld
     __hip_atomic_store(F + i * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F + (i + 1) * nb + j, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  HSTAMP(i, j, 1);
+  HSTAMP(i + 1, j, 1);
 }
 
 // Helper tasks of column j: the diagonal tile, the subdiagonal tile (both
@@ -732,35 +792,145 @@ __device__ __forceinline__ void store_tile(double* __restrict__ A, int ld, int i
 
 // The diagonal walker.  Step j: T_jj -= L_j,j-1 L_j,j-1^T, POTRF (L_jj, W_j),
 // TRSM of the subdiagonal tile L_j+1,j (kept in LDS for the next update).
-// When the POTRF's poll found the partial tiles (j+1, j) and (j+1, j+1)
-// already out, their loads are issued beside W_j's write-through stores and
-// share one drain with them; the stores of L_j+1,j drain during the next
-// step's first update, and their flag goes out after it.
+// The partial tiles the walker takes from the helpers -- (j+1, j) for the
+// TRSM, (j+1, j+1) for the next step -- were stored sc1 and published behind
+// a drain, so the walker reads them with sc1 loads after a relaxed poll and a
+// barrier, with no agent acquire (MI355X_MICROARCH.md "Valid forms", row 1:
+// the acquire's L1 invalidate + wait cost ~1.7 us on the chain).  Tile
+// (j+1, j) is prefetched to registers during panel 3 of the POTRF when wave
+// 2's poll in panel 2 found it out (potrf_tile); tile (j+1, j+1) is loaded
+// after F(j,j)'s publication, its latency under the TRSM and the stores of
+// L_j+1,j.  Those stores drain during the next step's first update, and their
+// flag goes out after it.
 // (Also taking L_j+2,j here, to shorten the helpers' chain W_j -> L_j+2,j ->
 // last update of T_j+2,j+2, measured no better: the extra TRSM costs what
 // the saved hand-off gains.)
+// threadIdx.x through an opaque move: the per-lane offsets derived from it
+// are computed where they are used.  (The walker's loop holds every value
+// the compiler can hoist out of it in registers -- at 512 VGPR + AGPR per
+// lane a hoisted set of 16-22 addresses spills to scratch, and a scratch
+// reload waits vmcnt(0), i.e. for every load in flight.)
+__device__ __forceinline__ int tid_local() {
+  int v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(int(threadIdx.x)));
+  return v;
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wave 0 polls one flag (relaxed, sc1), the block proceeds after the barrier;
+// no acquire: every load of the awaited bytes is ld_sc1.
+__device__ __forceinline__ void block_wait_sc1(const int* f, int epoch, int* fail) {
+  if (wave0()) {
+    if (!spin_until(f, epoch)) atomicOr(fail, 4);
+  }
+  __syncthreads();
+}
+// Waves 1-3 prefetch a 64x64 tile (column-major at src, leading dimension
+// ld) into the LDS image D: 22 sc1 loads per lane (192 lanes, one 512-B
+// column per wave instruction), then the LDS writes.
+// 16-B sc1 loads of a handed-off tile (buffer_load_dwordx4 sc1: aux bit 4;
+// 16-B sc1 loads of 8-B sc1-stored bytes are row 1 of the "Valid forms"
+// table): half the load instructions of 8-B loads -- the walker's tile loads
+// are issue-bound beside its MFMA work.
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const double* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ d2v ld2_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
+  return __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16));
+}
+// Waves 1-3 prefetch a 64x64 tile (column-major at src, leading dimension
+// ld) into the LDS image D: 11 16-B loads per lane (192 lanes; pair e =
+// u + 192 q, u = t - 64, is column (u >> 5) + 6 q, rows 2 (u & 31) and + 1: two
+// 512-B columns per wave instruction), the LDS writes later (store()).  The
+// offsets run through an opaque register at every step: hoisted out of the
+// walker's loop, the per-lane addresses held 44 registers across the whole
+// walk (140 VGPRs spilled, each reload a vmcnt(0) wait).
+struct SubPrefetch {
+  const double* src;
+  int ld;
+  double* D;
+  d2v v[11];
+  __device__ __forceinline__ void load() {
+    const int u = tid_local() - 64;
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(src);
+    uint32_t off = uint32_t(((u >> 5) * ld + 2 * (u & 31)) * 8);
+    const uint32_t step = uint32_t(6 * ld * 8);
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      asm volatile("" : "+v"(off));
+      if (q < 10 || u < 128) v[q] = ld2_sc1(rs, off);
+      off += step;
+    }
+  }
+  __device__ __forceinline__ void store() {
+    const int u = tid_local() - 64;
+    int off = (u >> 5) * TS + 2 * (u & 31);
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      asm volatile("" : "+v"(off));
+      if (q < 10 || u < 128) {
+        D[off] = v[q].x;
+        D[off + 1] = v[q].y;
+      }
+      off += 6 * TS;
+    }
+  }
+};
+// The walker's whole-tile loads, 256 lanes, 8 16-B loads per lane: pair
+// e = t + 256 q is column (t >> 5) + 8 q, rows 2 (t & 31) and + 1; and the
+// matching LDS writes.
+__device__ __forceinline__ void tile_ld2_sc1(d2v (&v)[8], const double* src, int ld) {
+  const int t = tid_local();
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(src);
+  uint32_t off = uint32_t(((t >> 5) * ld + 2 * (t & 31)) * 8);
+  const uint32_t step = uint32_t(8 * ld * 8);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    asm volatile("" : "+v"(off));
+    v[q] = ld2_sc1(rs, off);
+    off += step;
+  }
+}
+__device__ __forceinline__ void tile_put2(double* D, const d2v (&v)[8]) {
+  const int t = tid_local();
+  int off = (t >> 5) * TS + 2 * (t & 31);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    asm volatile("" : "+v"(off));
+    D[off] = v[q].x;
+    D[off + 1] = v[q].y;
+    off += 8 * TS;
+  }
+}
+__device__ __forceinline__ void tile_st_wt(double* dst, int ld, const double* D) {
+  const int t = tid_local();
+  size_t off = size_t(t >> 6) * ld + (t & 63);
+  const size_t step = size_t(4) * ld;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    asm volatile("" : "+v"(off));
+    const int e = t + 256 * q, c = e >> 6, r = e & 63;
+    st_wt(dst + off, D[c * TS + r]);
+    off += step;
+  }
+}
 template <bool kPanel>  // a column panel (ncols < nb possible) or the whole factor (ncols == nb)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, int ncols,
                              double* __restrict__ Winv,
                              int* __restrict__ F, const int* __restrict__ Pf, int epoch, double* T, double* Wl,
-                             double* Ls, double (*scr)[256], int* rdy, int* __restrict__ fail) {
+                             double* Ls, double* Tn, double (*scr)[256], int* rdy, int* __restrict__ fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // the next diagonal tile travels in registers (loaded one step ahead)
-  double nx[16];
-  block_wait(Pf, epoch, fail);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    nx[q] = A[size_t(c) * ld + r];
-  }
+  d2v nx[8];
+  block_wait_sc1(Pf, epoch, fail);
+  tile_ld2_sc1(nx, A, ld);
   for (int j = 0; j < (kPanel ? ncols : nb); ++j) {
     const int j0 = j * NB;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      T[c * TS + r] = nx[q];
-    }
-    if (t == 0) *rdy = 0;
+    WSTAMP(j, 0);
+    tile_put2(T, nx);
+    if (t == 0) rdy[0] = rdy[1] = 0;
     __syncthreads();
     if (j > 0) {
       // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
@@ -770,28 +940,23 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       // L_j,j-1 (stored at the end of the last step) has drained: its flag
       block_publish_wt(F + j * nb + j - 1, epoch);
     }
+    WSTAMP(j, 1);
     const double* dl = j > 0 ? Ls : nullptr;  // the rest of the last update
     const bool more = j + 1 < nb;      // a tile below the diagonal
     const bool next = kPanel ? j + 1 < ncols : more;  // ... and the walker's next diagonal tile (a panel ends before it)
     const int i0 = j0 + NB;
     const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
-    // (a panel's last column has no next diagonal tile: its poll checks the
-    // sub-diagonal flag twice)
-    const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : fsub;
-    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy)
-                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy);
+    // the subdiagonal partial tile, prefetched into Tn during panel 3
+    SubPrefetch pre{A + size_t(j0) * ld + i0, ld, Tn};
+    const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : nullptr;
+    const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre)
+                                    : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre);
     if (bad) atomicOr(fail, 1);
-    const bool early = more && __builtin_amdgcn_readfirstlane(*rdy) != 0;
-    double sub[16];
-    if (early) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        sub[q] = A[size_t(j0 + c) * ld + i0 + r];
-        if (next) nx[q] = A[size_t(i0 + c) * ld + i0 + r];
-      }
-    }
+    const bool early = more && __builtin_amdgcn_readfirstlane(rdy[0]) != 0;
+    const bool diag_out = next && __builtin_amdgcn_readfirstlane(rdy[1]) != 0;
+    // the prefetched subdiagonal tile into Tn (waves 1-3)
+    if (early && w >= 1) pre.store();
+    WSTAMPV(j, 15, early ? 1ull : 0ull);
     double* Wk = Winv + size_t(j) * NB * NB;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -800,18 +965,11 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       // from set_problem (one memset), 37% fewer bytes on the chain
       if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
     }
-    if (early) {
-      // T (L_jj) is read by nobody from here on (see below): it takes the
-      // subdiagonal tile
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = t + 256 * q, c = e >> 6, r = e & 63;
-        T[c * TS + r] = sub[q];
-      }
-    }
+    WSTAMP(j, 10);
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
     block_publish_wt(F + j * nb + j, epoch);
+    WSTAMP(j, 11);
     if (!more) {
       // L_jj is read by nobody (the helpers' TRSMs and the back substitution
       // use W_j; the next Schur pass rewrites the lower triangle) except in
@@ -827,28 +985,28 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
       break;
     }
     if (!early) {
-      // the poll missed: wait for the partial tiles here
-      block_wait(Pf + (j + 1) * nb + j, epoch, fail);
-      load_tile(T, A, ld, i0, j0);
-      if (next) {
-        block_wait(Pf + (j + 1) * nb + j + 1, epoch, fail);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int e = t + 256 * q, c = e >> 6, r = e & 63;
-          nx[q] = A[size_t(i0 + c) * ld + i0 + r];
-        }
-      }
+      // the poll missed: wait for the subdiagonal partial tile here
+      block_wait_sc1(fsub, epoch, fail);
+      d2v sv[8];
+      tile_ld2_sc1(sv, A + size_t(j0) * ld + i0, ld);
+      tile_put2(Tn, sv);
     }
-    // subdiagonal tile: L_j+1,j = T W^T, kept in Ls for the next update
+    if (next) {
+      // the next diagonal partial tile (out long before; wave 3 saw its flag
+      // in panel 3): its loads run under the TRSM and the L_j+1,j stores
+      if (!diag_out) block_wait_sc1(fdiag, epoch, fail);
+      tile_ld2_sc1(nx, A + size_t(i0) * ld + i0, ld);
+    }
+    if (!early || !diag_out) __syncthreads();  // (the Tn writes above: before the TRSM reads them)
+    WSTAMP(j, 12);
+    // subdiagonal tile: L_j+1,j = Tn W^T, kept in Ls for the next update
     f64x4 x[4];
-    trsm_lds(T, Wl, x, lane);
+    trsm_lds(Tn, Wl, x, lane);
     put_tile(Ls, x, lane);
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      st_wt(A + size_t(j0 + c) * ld + i0 + r, Ls[c * TS + r]);
-    }
+    WSTAMP(j, 13);
+    tile_st_wt(A + size_t(j0) * ld + i0, ld, Ls);
+    WSTAMP(j, 14);
     if (kPanel && !next) {
       // a panel's last column: L_j+1,j is final (no next step publishes it)
       block_publish_wt(F + (j + 1) * nb + j, epoch);
@@ -871,6 +1029,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   __shared__ double T[NB * TS];
   __shared__ double Wl[NB * TS];
   __shared__ double Ls[NB * TS];
+  __shared__ double Tn[NB * TS];  // the walker's subdiagonal tile (helpers: unused)
   __shared__ double scr[4][256];
   __shared__ int sh[2];
   if (gate && *gate == 0) {
@@ -898,7 +1057,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   const int role = __builtin_amdgcn_readfirstlane(sh[1]);
   __syncthreads();
   if (role == 0) {
-    fused_walker<kPanel>(A, ld, n, nb, ncols, Winv, F, Pf, epoch, T, Wl, Ls, scr, sh, fail);
+    fused_walker<kPanel>(A, ld, n, nb, ncols, Winv, F, Pf, epoch, T, Wl, Ls, Tn, scr, sh, fail);
     return;
   }
   const int ntask = chol_tasks(nb, kPanel ? ncols : nb);
@@ -1063,13 +1222,14 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
   __shared__ double scr[4][256];
   __shared__ double v[NB];
   __shared__ double yl[NB];        // y_1
-  __shared__ int rdy;
+  __shared__ int rdy[2];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // ---- step 0: POTRF of tile (0, 0) ----
   load_tile(T, A, ld, 0, 0);
   __syncthreads();
-  const bool bad0 = (NB <= n) ? potrf_tile<true>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, &rdy)
-                              : potrf_tile<false>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, &rdy);
+  NoPrefetch nopre;
+  const bool bad0 = (NB <= n) ? potrf_tile<true>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, rdy, nopre)
+                              : potrf_tile<false>(T, Wl, scr, 0, n, nullptr, nullptr, nullptr, 0, rdy, nopre);
   bool bad = bad0;
   if (nb > 1) {
     // W_0 kept; L_10 = A_10 W_0^T (the walker's TRSM of the subdiagonal tile)
@@ -1093,8 +1253,8 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
       last_update<1>(T, Ls, Ib, Jb, 1, lane);
     }
     __syncthreads();
-    bad |= (2 * NB <= n) ? potrf_tile<true>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, &rdy)
-                         : potrf_tile<false>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, &rdy);
+    bad |= (2 * NB <= n) ? potrf_tile<true>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, rdy, nopre)
+                         : potrf_tile<false>(T, Wl, scr, NB, n, Ls, nullptr, nullptr, 0, rdy, nopre);
   }
   if (bad && t == 0) atomicOr(fail, 1);
   // ---- back substitution L^T y = z, z = row n of the factor (k_backsolve's
@@ -1372,3 +1532,15 @@ void launch_spd_fill(double* A, int ld, int n, unsigned seed, hipStream_t s) {
 }
 
 }  // namespace sfm
+
+#ifdef SFM_CHOL_STAMPS
+extern "C" int sfm_debug_stamps(unsigned long long* out, int n, unsigned long long* hout, int hn) {
+  if (n > 256 * 16) n = 256 * 16;
+  if (hn > 128 * 128 * 2) hn = 128 * 128 * 2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_wstamp), sizeof(unsigned long long) * n) != hipSuccess) return -5;
+  if (hout && hn > 0 &&
+      hipMemcpyFromSymbol(hout, HIP_SYMBOL(sfm::g_hstamp), sizeof(unsigned long long) * hn) != hipSuccess)
+    return -5;
+  return 0;
+}
+#endif
