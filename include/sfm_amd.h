@@ -191,7 +191,8 @@ int sfm_ba_set_host_comm(sfm_ba_handle* h, int32_t nranks, int32_t rank, sfm_all
  *   SFM_COLL_REDUCE_SCATTER  buf[nranks * count] in rank-segment order; the
  *                            sum of this rank's segment into out[count];
  *   SFM_COLL_REDUCE          the sum over the ranks of buf[count] into buf
- *                            on rank `arg` (the others' buf is unspecified).
+ *                            on rank `arg` (the others' buf is unspecified;
+ *                            out == buf for this kind).
  * (With sfm_ba_set_host_comm's all-reduce alone, the library builds the
  * others from it.) */
 #define SFM_COLL_ALLREDUCE 0

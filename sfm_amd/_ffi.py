@@ -240,6 +240,12 @@ def check(rc: int, what: str) -> None:
 
 
 def ptr(a: np.ndarray | None) -> c_void_p | None:
+    """The array's data address for a C-ABI call.
+
+    Unlike ctypes' data_as, the returned c_void_p holds NO reference to the
+    array: the caller must keep `a` alive (bound to a local name) until the
+    call returns -- never pass a temporary such as
+    ptr(np.ascontiguousarray(x)) straight into lib().fn(...)."""
     if a is None:
         return None
     assert a.flags.c_contiguous, "arrays passed to the C ABI must be C-contiguous"

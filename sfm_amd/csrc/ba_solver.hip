@@ -189,7 +189,12 @@ int dalloc(sfm_ba_handle* h, T** p, size_t count) {
   *p = static_cast<T*>(q);
   return 0;
 }
-// set_problem scratch: retired into the pool when set_problem returns
+// set_problem scratch: retired into the pool when set_problem returns after
+// its synchronisation, or -- a keyframe-sized set_problem returns without one
+// -- by the next set_problem's free_problem, which synchronises first.  So a
+// pooled buffer is never handed out while a kernel of this stream may still
+// use it: every path that moves tmps into the pool (retire_tmps) runs behind
+// a hipStreamSynchronize of the handle's stream.
 template <typename T>
 int dalloc_tmp(sfm_ba_handle* h, T** p, size_t count) {
   const int rc = dalloc(h, p, count);
@@ -203,10 +208,20 @@ void retire_tmps(sfm_ba_handle* h) {
   h->tmps.clear();
 }
 
-// The pinned staging buffer with room for `bytes` (the caller has synchronised
-// the stream: nothing may still read or write the old buffer).
+// The pinned staging buffer with room for `bytes`.  Growing it frees the old
+// buffer, so nothing may still read or write it: every caller has synchronised
+// the stream (set_problem, get_parameters), and a keyframe-sized set_problem,
+// which returns with its uploads from the stage still in flight, is always
+// followed by a synchronising call before the stage is written again.  The
+// rule is checked here: a stream found busy is drained first (and counted, so
+// a test can see the rule broken).
+std::atomic<int> g_stage_busy_regrows{0};
 int stage_reserve(sfm_ba_handle* h, size_t bytes) {
   if (bytes <= h->stage_cap) return 0;
+  if (h->stage && hipStreamQuery(h->stream) == hipErrorNotReady) {
+    g_stage_busy_regrows.fetch_add(1);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return fail(SFM_EIO, "stream error before the stage regrows");
+  }
   const size_t cap = std::max<size_t>({bytes, size_t(1) << 20, 2 * h->stage_cap});
   if (h->stage) (void)hipHostFree(h->stage);
   h->stage = nullptr;
@@ -758,11 +773,17 @@ int dist_factor_enqueue(sfm_ba_handle* h) {
   if ((rc = dist_prepare(h))) return rc;
   auto& D = h->dist;
   const int pt = D.pt, N = h->nranks, me = h->rank, np = int(D.count.size());
-  // (SFM_DIST_OVERLAP=1: the collective stream and its events even on one
-  // rank, where RCCL's collectives are local -- the one-GPU test of the
-  // look-ahead plumbing, tests/test_gpu_scale.py)
+  // The broadcasts on a second stream of the handle (the collective stream,
+  // two broadcast buffers and the events that order their reuse) only with
+  // SFM_DIST_OVERLAP=1.  Its non-owner branches (the wait on ev_free, the
+  // unpack, a half reused across owners) have never run with more than one
+  // RCCL rank -- no second GPU was ever available to this build, and RCCL
+  // takes one rank per GPU -- so the multi-GPU default is the schedule the
+  // 2-4-rank host-hook tests run (tests/test_gpu_shards.py), the same order
+  // of operations on one stream.  On one rank (RCCL's collectives local) the
+  // flag is the one-GPU test of the look-ahead plumbing, tests/test_gpu_scale.py.
   static const bool force_overlap = env_flag("SFM_DIST_OVERLAP");
-  const bool overlap = h->comm != nullptr && (N > 1 || force_overlap);
+  const bool overlap = h->comm != nullptr && force_overlap;
   const bool comm = N > 1 || overlap;
   hipStream_t cs = overlap ? D.cstream : s;
   launch_panel_copy(d, kPanelPack, pt, 0, d.n + 1, D.off_send, 0, D.send, s);
@@ -1761,7 +1782,11 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   d.n_blk = int64_t(C) * (C + 1) / 2;
   // the Schur pass's shape below follows the mean pair count: the host's
   // estimate on host-checked problems (either layout path, so both choose
-  // alike), else the device's count
+  // alike), else the device's count.  The estimate counts every unordered
+  // pair of a point's observations, so it undercounts when a camera sees a
+  // point twice (a same-camera pair is an ordered pair of the diagonal
+  // block); it picks the lanes per block only -- the pair buffer is sized by
+  // twice the estimate, an upper bound of the true count either way.
   d.n_pairs = host_check && stage_in && !cam_slice.empty() ? pairs_est : n_pairs;
   // lanes per Schur block ~ a tenth of the mean pair count, 8..64 (measured
   // best: C3, 72 pairs per block -> 8; C1 / C2, ~460 -> 64)
@@ -1962,7 +1987,10 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   // k_schur_pts group sizes come back, copies from pageable host memory (the
   // caller's arrays, this call's vectors) complete, and the scratch buffers
   // return to the pool.
-  if (!(small && early_params && !bperm_per)) {
+  // (SFM_SYNC_SETUP=1: always synchronise, so that a fault in a layout kernel
+  // is reported by set_problem itself, not by the next call)
+  static const bool sync_setup = env_flag("SFM_SYNC_SETUP");
+  if (!(small && early_params && !bperm_per) || sync_setup) {
     HCHK(hipStreamSynchronize(s));
     if (bperm_per) {
       int64_t m_max = 1;

@@ -94,14 +94,24 @@ constexpr int TS = NB + 1;  // LDS column stride (doubles) of the tile images
 
 // D (16x16) += sum_{k<16} A(i, k) B(k, j) with A(i, k) = Ap[i*ai + k*ak],
 // B(k, j) = Bp[k*bk + j*bj] (LDS).  Lane l's reg r holds D(4r + (l>>4), l&15).
+// The eight LDS operands are read before the first MFMA (one wait, not one
+// LDS round trip per MFMA: left to itself the compiler interleaved
+// read -> wait -> MFMA under the walker's register pressure); the MFMA
+// order, and so every sum, is unchanged.
 __device__ __forceinline__ f64x4 mfma16(const double* Ap, int ai, int ak, const double* Bp, int bk, int bj, f64x4 acc,
                                         int lane) {
   const int i = lane & 15, kk = lane >> 4;
+  double a[4], b[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int k = 4 * s + kk;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ap[i * ai + k * ak], Bp[k * bk + i * bj], acc, 0, 0, 0);
+    a[s] = Ap[i * ai + k * ak];
+    b[s] = Bp[k * bk + i * bj];
   }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) asm volatile("" : "+v"(a[s]), "+v"(b[s]));
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
   return acc;
 }
 
@@ -151,14 +161,30 @@ __device__ __forceinline__ void last_update(double* T, const double* Ls, const i
 #pragma unroll
   for (int q = 0; q < kMax; ++q) acc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int M = 0; M < 4; ++M)
+  for (int M = 0; M < 4; ++M) {
+    // a column block's operands first, then its MFMAs (same order per block)
+    double a[4][kMax], b[4][kMax];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const double* row = Ls + (16 * M + 4 * s4 + kk) * TS + li;
 #pragma unroll
       for (int q = 0; q < kMax; ++q)
-        if (q < nq) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16 * Ib[q]], row[16 * Jb[q]], acc[q], 0, 0, 0);
+        if (q < nq) {
+          a[s4][q] = row[16 * Ib[q]];
+          b[s4][q] = row[16 * Jb[q]];
+        }
     }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int q = 0; q < kMax; ++q)
+        if (q < nq) asm volatile("" : "+v"(a[s4][q]), "+v"(b[s4][q]));
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int q = 0; q < kMax; ++q)
+        if (q < nq) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4][q], b[s4][q], acc[q], 0, 0, 0);
+  }
 #pragma unroll
   for (int q = 0; q < kMax; ++q)
     if (q < nq)
@@ -759,14 +785,27 @@ __device__ __forceinline__ void trsm_lds(const double* T, const double* Wl, f64x
 #pragma unroll
   for (int Cb = 0; Cb < 4; ++Cb) x[Cb] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int M = 0; M < 4; ++M)
+  for (int M = 0; M < 4; ++M) {
+    // the column block's operands first, then its MFMAs (same order per x[Cb])
+    double a[4], b[4][4];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const int k = 16 * M + 4 * s4 + kk;
-      const double a = T[k * TS + 16 * w + li];
+      a[s4] = T[k * TS + 16 * w + li];
 #pragma unroll
-      for (int Cb = M; Cb < 4; ++Cb) x[Cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * TS + 16 * Cb + li], x[Cb], 0, 0, 0);
+      for (int Cb = M; Cb < 4; ++Cb) b[s4][Cb] = Wl[k * TS + 16 * Cb + li];
     }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      asm volatile("" : "+v"(a[s4]));
+#pragma unroll
+      for (int Cb = M; Cb < 4; ++Cb) asm volatile("" : "+v"(b[s4][Cb]));
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int Cb = M; Cb < 4; ++Cb) x[Cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4][Cb], x[Cb], 0, 0, 0);
+  }
 }
 __device__ __forceinline__ void put_tile(double* D, const f64x4 x[4], int lane) {
   const int w = threadIdx.x >> 6, li = lane & 15, kk = lane >> 4;
@@ -904,15 +943,38 @@ __device__ __forceinline__ void tile_put2(double* D, const d2v (&v)[8]) {
     off += 8 * TS;
   }
 }
-__device__ __forceinline__ void tile_st_wt(double* dst, int ld, const double* D) {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off, d2v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, byte_off, 0, 16);
+}
+// A 64x64 LDS image D -> the tile at dst (leading dimension ld), write-through
+// 16-B sc1 stores; pair e = t + 256 q as tile_ld2_sc1.  Every LDS read is
+// issued before the first store: one wait instead of one LDS round trip per
+// store (the element-wise form compiled to 16 ds_read -> wait -> store
+// sequences, 0.6 us per tile; the W_j publication with its lower-block mask
+// 1.1 us, both on the walker's chain).  kLowerBlocks: only the 16x16 blocks
+// on or below the diagonal (W_k; its upper blocks stay zero from set_problem).
+template <bool kLowerBlocks>
+__device__ __forceinline__ void tile_st2_wt(double* dst, int ld, const double* D) {
   const int t = tid_local();
-  size_t off = size_t(t >> 6) * ld + (t & 63);
-  const size_t step = size_t(4) * ld;
+  d2v v[8];
+  int lo = (t >> 5) * TS + 2 * (t & 31);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < 8; ++q) {
+    v[q].x = D[lo + 8 * TS * q];
+    v[q].y = D[lo + 8 * TS * q + 1];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(v[q]));  // all reads land before the stores start
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(dst);
+  uint32_t off = uint32_t(((t >> 5) * ld + 2 * (t & 31)) * 8);
+  const uint32_t step = uint32_t(8 * ld * 8);
+  const int r16 = (2 * (t & 31)) >> 4;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
     asm volatile("" : "+v"(off));
-    const int e = t + 256 * q, c = e >> 6, r = e & 63;
-    st_wt(dst + off, D[c * TS + r]);
+    const int c16 = ((t >> 5) + 8 * q) >> 4;
+    if (!kLowerBlocks || r16 >= c16) st2_sc1(rs, off, v[q]);
     off += step;
   }
 }
@@ -957,14 +1019,9 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     // the prefetched subdiagonal tile into Tn (waves 1-3)
     if (early && w >= 1) pre.store();
     WSTAMPV(j, 15, early ? 1ull : 0ull);
-    double* Wk = Winv + size_t(j) * NB * NB;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int e = t + 256 * q, c = e >> 6, r = e & 63;
-      // lower 16x16 blocks only: the upper blocks of every W_k stay zero
-      // from set_problem (one memset), 37% fewer bytes on the chain
-      if ((r >> 4) >= (c >> 4)) st_wt(Wk + c * NB + r, Wl[c * TS + r]);
-    }
+    // W_j: lower 16x16 blocks only (the upper blocks of every W_k stay zero
+    // from set_problem, one memset: 37% fewer bytes on the chain)
+    tile_st2_wt<true>(Winv + size_t(j) * NB * NB, NB, Wl);
     WSTAMP(j, 10);
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
@@ -1005,7 +1062,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     put_tile(Ls, x, lane);
     __syncthreads();
     WSTAMP(j, 13);
-    tile_st_wt(A + size_t(j0) * ld + i0, ld, Ls);
+    tile_st2_wt<false>(A + size_t(j0) * ld + i0, ld, Ls);
     WSTAMP(j, 14);
     if (kPanel && !next) {
       // a panel's last column: L_j+1,j is final (no next step publishes it)
