@@ -323,6 +323,23 @@ int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* f
  * point's rows (append order), first on ties.  Every point needs a row. */
 int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,
                                        int32_t* best_row);
+/* CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692) in one call, on the
+ * device: the points seen in the keyframes frame_no[n_frames]
+ * (getPointsInFrames, CSfM.cpp:648), minus the frame's already matched points
+ * existing_pts[n_existing] (CSfM.cpp:651-662), projected with the frame's pose
+ * x = K (R X + t) (R9 row-major rotation, t3, K9 row-major; CSfM.cpp:664-668),
+ * their representative descriptors (CSfM.cpp:669), matched against the
+ * current frame's keypoints train_idx[n_train] of the frame last pushed to
+ * `mt` (sfm_matcher_push_frame) with the (min_distance, max_distance) window
+ * of CSfM.cpp:671 (ratio 0.8, 0, _maxReprErr).  Results: pts3d_match[k] (map
+ * point) and train_match[k] (frame-global keypoint index), *n_matches of them,
+ * in the matcher's order (queries = the new points ascending).  The map and
+ * the matcher must share device and descriptor width. */
+int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int32_t* frame_no, int32_t n_existing,
+                        const int32_t* existing_pts, const double* R9, const double* t3, const double* K9,
+                        int32_t n_train, const int32_t* train_idx, double ratio_test, double min_distance,
+                        double max_distance, int32_t capacity, int32_t* pts3d_match, int32_t* train_match,
+                        int32_t* n_matches);
 
 /* BRISK descriptor (CTracker::detectFeatures' _descriptor->compute,
  * CTracker.cpp:284): BRISK as published in its

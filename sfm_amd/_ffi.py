@@ -172,6 +172,9 @@ _SIGNATURES = {
     "sfm_map_points_in_frame_multi": (c_int, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                               c_void_p]),
     "sfm_map_representative_descriptors": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "sfm_map_match_frame": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int32, c_void_p, c_double, c_double, c_double, c_int32, c_void_p,
+                                    c_void_p, POINTER(c_int32)]),
     "sfm_pnp_ransac": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_double, c_double,
                                c_void_p, c_void_p, c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     "sfm_triangulate_points": (c_int, [c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

@@ -171,6 +171,29 @@ class DeviceMap:
         check(rc, "sfm_map_points_in_frame_multi")
         return [(p3[off3[i]:off3[i + 1]].copy(), p2[off2[i]:off2[i + 1]].copy()) for i in range(nf)]
 
+    def matchFrame(self, matcher, frameNo, existing, R, t, K, train_idx, ratio: float = 0.8, min_distance: float = 0.0,
+                   max_distance: float = 7.0):
+        """CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692) on the device
+        (sfm_map_match_frame): the keyframes' points minus `existing`,
+        projected with (R, t, K), their representative descriptors matched
+        against the keypoints `train_idx` of the frame last pushed to
+        `matcher`.  Returns (map point ids, frame-global keypoint ids)."""
+        fr = np.ascontiguousarray(np.asarray(frameNo, np.int32).reshape(-1))
+        ex = np.ascontiguousarray(np.asarray(existing, np.int32).reshape(-1))
+        tr = np.ascontiguousarray(np.asarray(train_idx, np.int32).reshape(-1))
+        R9 = np.ascontiguousarray(np.asarray(R, np.float64).reshape(9))
+        t3 = np.ascontiguousarray(np.asarray(t, np.float64).reshape(3))
+        K9 = np.ascontiguousarray(np.asarray(K, np.float64).reshape(9))
+        cap = max(1, len(tr))
+        pm = np.zeros(cap, np.int32)
+        km = np.zeros(cap, np.int32)
+        n = ctypes.c_int32(0)
+        check(lib().sfm_map_match_frame(self._h, matcher._h, len(fr), ptr(fr), len(ex), ptr(ex), ptr(R9), ptr(t3),
+                                        ptr(K9), len(tr), ptr(tr), float(ratio), float(min_distance),
+                                        float(max_distance), cap, ptr(pm), ptr(km), ctypes.byref(n)),
+              "sfm_map_match_frame")
+        return pm[:n.value].copy(), km[:n.value].copy()
+
     def getRepresentativeDescriptors(self, pts3DIdx, return_best: bool = False):
         a = np.ascontiguousarray(np.asarray(pts3DIdx, np.int32).reshape(-1))
         out = np.zeros((max(1, len(a)), self.desc_bytes), np.uint8)

@@ -1149,6 +1149,143 @@ __global__ __launch_bounds__(kThreads, 3) void k_schur_pts(int64_t n_slots, cons
   }
 }
 
+// A register-lighter form of k_schur_pts (built to be
+// measured; SFM_SCHUR_HALVES=1): two passes over every pair list, pass kHalf
+// accumulating only rows 3 kHalf .. 3 kHalf + 2 of the 6x6 block (18 sums
+// instead of 36, 36 VGPRs fewer), at __launch_bounds__(kThreads, 4) for a
+// fourth wave per SIMD.  Pass 1's rows [H Q_2 | H] need no Q_1; pass 0 does
+// everything but half of the accumulation.  Every entry takes the full
+// kernel's operations in its order, and the lane reduction pairs lanes in the
+// same tree, so S is bitwise the one-pass kernel's.
+template <int kSub, int kHalf>
+__global__ __launch_bounds__(kThreads, 4) void k_schur_pts_half(int64_t n_slots, const int2* __restrict__ blk,
+                                                             const int32_t* __restrict__ seg,
+                                                             const int32_t* __restrict__ bpts,
+                                                             const double* __restrict__ ptS,
+                                                             const double* __restrict__ camR,
+                                                             const double* __restrict__ cam,
+                                                             const double* __restrict__ Kc,
+                                                             const double* __restrict__ scale_c, double* __restrict__ S,
+                                                             int ld, const int32_t* __restrict__ bperm,
+                                                             const int* __restrict__ gate) {
+  if (gate && *gate == 0) return;
+  constexpr int kPer = 64 / kSub;
+  __shared__ __attribute__((aligned(16))) double cst[kThreads / 64][kPer][2 * kCamS];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, g = l / kSub, sl = l % kSub;
+  const int64_t wb = (int64_t(blockIdx.x) * (kThreads / 64) + wv) * kPer;
+  auto slot_blk = [&](int64_t k) -> int32_t { return k < n_slots ? (bperm ? bperm[k] : int32_t(k)) : -1; };
+  const int32_t bs = slot_blk(wb + g);
+  const bool own = bs >= 0;
+  const int64_t b = own ? bs : 0;
+  const int2 cc = blk[b];
+  double* cs1 = cst[wv][g];
+  double* cs2 = cs1 + kCamS;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int32_t bq = slot_blk(wb + q);
+    const int2 cq = blk[bq >= 0 ? bq : 0];
+    stage_cam(cst[wv][q], cq.x, camR, cam, Kc, scale_c, l);
+    stage_cam(cst[wv][q] + kCamS, cq.y, camR, cam, Kc, scale_c, l);
+  }
+  wave_lds_sync();
+  const int kb = seg[b], ke = own ? seg[b + 1] : kb;
+  double acc[18];
+#pragma unroll
+  for (int e = 0; e < 18; ++e) acc[e] = 0.0;
+  int len = ke - kb;
+#pragma unroll
+  for (int off = kSub; off < 64; off <<= 1) len = max(len, __shfl_xor(len, off));
+  int p_nx = bpts[kb + sl < ke ? kb + sl : 0];
+  for (int k0 = 0; k0 < len; k0 += kSub) {
+    asm volatile("" ::: "memory");
+    const int k = kb + k0 + sl;
+    const bool valid = k < ke;
+    const int p = p_nx;
+    p_nx = bpts[k + kSub < ke ? k + kSub : 0];
+    const double* r = ptS + size_t(kPtS) * p;
+    double q[12];
+#pragma unroll
+    for (int f = 0; f < 12; f += 2) {
+      const double2 x = ld2(r + f);
+      q[f] = x.x; q[f + 1] = x.y;
+    }
+    const double Xp[3] = {q[0], q[1], q[2]}, sp[3] = {q[3], q[4], q[5]};
+    const double Lp[6] = {q[6], q[7], q[8], q[9], q[10], q[11]};
+    double M1[6], ab1[5], M2[6], ab2[5];
+    pair_side_m(cs1, Xp, sp, Lp, M1, ab1);
+    pair_side_m(cs2, Xp, sp, Lp, M2, ab2);
+    asm volatile("" ::: "memory");
+    const double w = valid ? 1.0 : 0.0;
+    const double g00 = (M1[0] * M2[0] + M1[1] * M2[1] + M1[2] * M2[2]) * w;
+    const double g01 = (M1[0] * M2[3] + M1[1] * M2[4] + M1[2] * M2[5]) * w;
+    const double g10 = (M1[3] * M2[0] + M1[4] * M2[1] + M1[5] * M2[2]) * w;
+    const double g11 = (M1[3] * M2[3] + M1[4] * M2[4] + M1[5] * M2[5]) * w;
+    double H[3][3];
+    {
+      const double t00 = g00 * ab2[0], t01 = g00 * ab2[1] + g01 * ab2[3], t02 = g00 * ab2[2] + g01 * ab2[4];
+      const double t10 = g10 * ab2[0], t11 = g10 * ab2[1] + g11 * ab2[3], t12 = g10 * ab2[2] + g11 * ab2[4];
+      H[0][0] = ab1[0] * t00; H[0][1] = ab1[0] * t01; H[0][2] = ab1[0] * t02;
+      H[1][0] = ab1[1] * t00 + ab1[3] * t10; H[1][1] = ab1[1] * t01 + ab1[3] * t11; H[1][2] = ab1[1] * t02 + ab1[3] * t12;
+      H[2][0] = ab1[2] * t00 + ab1[4] * t10; H[2][1] = ab1[2] * t01 + ab1[4] * t11; H[2][2] = ab1[2] * t02 + ab1[4] * t12;
+    }
+    double HQ[3][3];
+#pragma unroll
+    for (int kq = 0; kq < 3; ++kq) {
+      const double* D = cs2 + 9 + 9 * kq;
+      const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+      const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+      const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) HQ[i][kq] = H[i][0] * q0 + H[i][1] * q1 + H[i][2] * q2;
+    }
+    if (kHalf == 0) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const double* D = cs1 + 9 + 9 * u;
+        const double q0 = D[0] * Xp[0] + D[1] * Xp[1] + D[2] * Xp[2];
+        const double q1 = D[3] * Xp[0] + D[4] * Xp[1] + D[5] * Xp[2];
+        const double q2 = D[6] * Xp[0] + D[7] * Xp[1] + D[8] * Xp[2];
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          acc[6 * u + v] += q0 * HQ[0][v] + q1 * HQ[1][v] + q2 * HQ[2][v];
+          acc[6 * u + 3 + v] += q0 * H[0][v] + q1 * H[1][v] + q2 * H[2][v];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          acc[6 * u + v] += HQ[u][v];
+          acc[6 * u + 3 + v] += H[u][v];
+        }
+    }
+  }
+  double v32[32];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) v32[e] = e < 18 ? acc[e] : 0.0;
+  seg_reduce32<kSub>(v32, l);
+  if (own) {
+    double* Sb = S + size_t(6 * cc.x) * ld + 6 * size_t(cc.y);
+    const bool add = cc.x == cc.y;
+    const double* sc1 = cst[wv][g] + 44;
+    const double* sc2 = sc1 + kCamS;
+    auto put = [&](int e, double v) {
+      double* q = Sb + size_t(e / 6) * ld + e % 6;
+      v = v * sc1[e / 6] * sc2[e % 6];
+      *q = add ? *q - v : -v;
+    };
+    constexpr int kR = kSub >= 32 ? 1 : 32 / kSub;
+    if (kSub == 64) {
+      if (!(sl & 1) && (sl >> 1) < 18) put(18 * kHalf + (sl >> 1), v32[0]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < kR; ++r)
+        if (kR * sl + r < 18) put(18 * kHalf + kR * sl + r, v32[r]);
+    }
+  }
+}
+
 // Diagonal blocks and rhs from k_obs_prep_rc's per-wave partials: camera c's
 // waves are positions cam_rng[2c]/64 .. (run end)/64, summed in order.
 //   S_cc += [rank 0] (U_c + D_c^2) - sum F F^T,   S[c][n] = sum J_c^T (r - h)
@@ -1581,6 +1718,21 @@ void launch_schur_offdiag(const DevProblem& d, int* tile_cnt, hipStream_t s) {
     k_schur_pts<64, kThreads / 64><<<int(n_slots), kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS,
                                                                     d.camR, d.cam, d.Kc, d.scale_c, d.S, d.ld,
                                                                     bperm, d.gate, tile_cnt, d.nblk, DiagFold{});
+    return;
+  }
+  static const bool halves = [] {
+    const char* e = std::getenv("SFM_SCHUR_HALVES");
+    return e && e[0] == '1';
+  }();
+  if (halves && !tile_cnt) {
+#define SFM_PTS_H(S_, H_)                                                                                       \
+  k_schur_pts_half<S_, H_><<<nb, kThreads, 0, s>>>(n_slots, d.blk, d.seg, d.bpts, d.ptS, d.camR, d.cam, d.Kc, \
+                                                   d.scale_c, d.S, d.ld, bperm, d.gate)
+    if (sub == 8) { SFM_PTS_H(8, 0); SFM_PTS_H(8, 1); }
+    else if (sub == 16) { SFM_PTS_H(16, 0); SFM_PTS_H(16, 1); }
+    else if (sub == 32) { SFM_PTS_H(32, 0); SFM_PTS_H(32, 1); }
+    else { SFM_PTS_H(64, 0); SFM_PTS_H(64, 1); }
+#undef SFM_PTS_H
     return;
   }
   if (sub == 8) SFM_PTS(8);

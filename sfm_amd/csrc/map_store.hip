@@ -160,6 +160,11 @@ __global__ __launch_bounds__(64) void k_map_repr(const uint64_t* __restrict__ de
   if (i >= n) return;
   const int p = qpt[i];
   const int r0 = doff[p], k = doff[p + 1] - r0;
+  if (k == 0) {  // no descriptor row (the callers check; reported as -1)
+    if (l == 0) best_local[i] = -1;
+    if (l < W) out[size_t(i) * W + l] = 0;
+    return;
+  }
   unsigned long long key = ~0ull;  // (sum << 32 | local row)
   for (int r = l; r - l < k; r += 64) {
     uint64_t x[W];
@@ -192,6 +197,28 @@ __global__ void k_scatter_points(int n, const int32_t* __restrict__ idx, const d
 
 inline unsigned grid(int64_t n, int b = 256) { return unsigned((n + b - 1) / b); }
 
+__global__ void k_unmark(int n, const int32_t* __restrict__ pts, uint8_t* __restrict__ mark) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) mark[pts[i]] = 0;
+}
+
+// The queried points projected with the frame's pose (CSfM.cpp:664-668, the
+// reference's GeometryUtils::projectPoints with zero distortion, as
+// sfm_amd/live.py's _project): uv = (x / z) f + c.
+__global__ void k_project(int n, const int32_t* __restrict__ qpt, const double* __restrict__ X, double r0, double r1,
+                          double r2, double r3, double r4, double r5, double r6, double r7, double r8, double t0,
+                          double t1, double t2, double fx, double fy, double cx, double cy, double* __restrict__ uv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* x = X + 3 * size_t(qpt[i]);
+  const double x0 = x[0], x1 = x[1], x2 = x[2];
+  const double c0 = r0 * x0 + r1 * x1 + r2 * x2 + t0;
+  const double c1 = r3 * x0 + r4 * x1 + r5 * x2 + t1;
+  const double c2 = r6 * x0 + r7 * x1 + r8 * x2 + t2;
+  uv[2 * size_t(i)] = c0 / c2 * fx + cx;
+  uv[2 * size_t(i) + 1] = c1 / c2 * fy + cy;
+}
+
 template <class T>
 struct DVec {
   T* p = nullptr;
@@ -199,6 +226,11 @@ struct DVec {
 };
 
 }  // namespace
+// match_kernels.hip
+int matcher_match_current(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
+                          const int32_t* train_idx, int n1, double ratio, double mn, double mx, int** res);
+int matcher_words(const sfm_matcher* h);
+int matcher_device(const sfm_matcher* h);
 }  // namespace sfm
 
 using namespace sfm;
@@ -214,6 +246,9 @@ struct sfm_map {
   bool ocsr = false, dcsr = false;         // per-point CSRs current?
   int32_t *orow = nullptr, *ooff = nullptr, *drow = nullptr, *doff = nullptr;
   std::map<std::string, std::pair<void*, size_t>> scratch;
+  hipEvent_t ev = nullptr;                 // sfm_map_match_frame: its queries are ready
+  int32_t* pin = nullptr;                  // sfm_map_match_frame's pinned readback
+  size_t pin_cap = 0;
 };
 
 namespace {
@@ -339,6 +374,8 @@ int sfm_map_destroy(sfm_map* h) {
     if (p) (void)hipFree(p);
   for (auto& e : h->scratch)
     if (e.second.first) (void)hipFree(e.second.first);
+  if (h->ev) (void)hipEventDestroy(h->ev);
+  if (h->pin) (void)hipHostFree(h->pin);
   (void)hipStreamDestroy(h->s);
   delete h;
   return 0;
@@ -658,6 +695,107 @@ int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts
   (void)hipMemcpyAsync(b.data(), best, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
   if (int r = sync(h)) return r;
   if (best_row) std::memcpy(best_row, b.data(), sizeof(int32_t) * size_t(n));
+  return 0;
+}
+
+// CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692) in one call: the
+// points of the keyframes (getPointsInFrames), minus the frame's matched
+// points, projected with the frame's pose, their representative descriptors,
+// matched in the (min, max) window against the current frame's unmatched
+// keypoints, which the matcher holds (sfm_matcher_push_frame).  Everything
+// stays on the device: one readback of the query count, one of the results
+// (the composed calls downloaded every map point and the descriptors, and
+// uploaded them again for the match: ~10 synchronisations per frame).
+int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int32_t* frame_no, int32_t n_existing,
+                        const int32_t* existing_pts, const double* R9, const double* t3, const double* K9,
+                        int32_t n_train, const int32_t* train_idx, double ratio_test, double min_distance,
+                        double max_distance, int32_t capacity, int32_t* pts3d_match, int32_t* train_match,
+                        int32_t* n_matches) {
+  if (!h || !mt || !n_matches) return mapfail(SFM_EINVAL, "NULL handle");
+  *n_matches = 0;
+  if (n_frames < 0 || n_existing < 0 || n_train < 0) return mapfail(SFM_EINVAL, "negative size");
+  if ((n_frames && !frame_no) || (n_existing && !existing_pts) || (n_train && !train_idx) || !R9 || !t3 || !K9)
+    return mapfail(SFM_EINVAL, "NULL argument");
+  if (matcher_words(mt) != h->W || matcher_device(mt) != h->device)
+    return mapfail(SFM_EINVAL, "the map and the matcher differ in descriptor width or device");
+  if (int rc = check_pts(h, n_existing, existing_pts)) return rc;
+  if (n_frames == 0 || h->n_pts == 0 || h->ob_pt.n == 0 || n_train < 2) return 0;
+  if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
+  int rc = 0;
+  const int P = h->n_pts;
+  std::vector<int32_t> fs(frame_no, frame_no + n_frames);
+  std::sort(fs.begin(), fs.end());
+  fs.erase(std::unique(fs.begin(), fs.end()), fs.end());
+  if (!h->dcsr) {
+    if (int r = build_csr(h, "de", h->desc_pt.p, h->desc.n / h->W, &h->drow, &h->doff)) return r;
+    h->dcsr = true;
+  }
+  auto* fset = static_cast<int32_t*>(scratch(h, "fset", sizeof(int32_t) * (fs.size() + size_t(n_existing)), &rc));
+  auto* mark = static_cast<uint8_t*>(scratch(h, "mark", size_t(P), &rc));
+  auto* out = static_cast<int32_t*>(scratch(h, "pout", sizeof(int32_t) * size_t(P), &rc));
+  auto* dn = static_cast<int32_t*>(scratch(h, "pn", sizeof(int32_t), &rc));
+  if (rc) return rc;
+  if (h->pin_cap < 2 * size_t(P) + 1) {
+    if (h->pin) { (void)hipStreamSynchronize(h->s); (void)hipHostFree(h->pin); }
+    h->pin = nullptr;
+    h->pin_cap = 0;
+    const size_t cap = std::max<size_t>(2 * size_t(P) + 1, 8192) * 3 / 2;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int32_t) * cap) != hipSuccess)
+      return mapfail(SFM_ENOMEM, "hipHostMalloc failed");
+    h->pin_cap = cap;
+  }
+  if (!h->ev && hipEventCreateWithFlags(&h->ev, hipEventDisableTiming) != hipSuccess)
+    return mapfail(SFM_EIO, "hipEventCreate failed");
+  // frames + the frame's matched points in one upload
+  (void)hipStreamSynchronize(h->s);  // (the pinned block may feed an earlier copy)
+  std::memcpy(h->pin, fs.data(), sizeof(int32_t) * fs.size());
+  if (n_existing) std::memcpy(h->pin + fs.size(), existing_pts, sizeof(int32_t) * size_t(n_existing));
+  (void)hipMemcpyAsync(fset, h->pin, sizeof(int32_t) * (fs.size() + size_t(n_existing)), hipMemcpyHostToDevice, h->s);
+  (void)hipMemsetAsync(mark, 0, size_t(P), h->s);
+  k_mark_frames<<<grid(h->ob_pt.n), 256, 0, h->s>>>(h->ob_pt.n, h->ob_pt.p, h->ob_frame.p, fset, int(fs.size()), mark);
+  if (n_existing) k_unmark<<<grid(n_existing), 256, 0, h->s>>>(n_existing, fset + fs.size(), mark);
+  hipcub::CountingInputIterator<int32_t> it(0);
+  size_t bytes = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, bytes, it, mark, out, dn, P, h->s);
+  void* tmp = scratch(h, "psel", bytes, &rc);
+  if (rc) return rc;
+  if (hipcub::DeviceSelect::Flagged(tmp, bytes, it, mark, out, dn, P, h->s) != hipSuccess)
+    return mapfail(SFM_EIO, "select failed");
+  (void)hipMemcpyAsync(h->pin, dn, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  const int n_new = h->pin[0];
+  if (n_new == 0) return 0;
+  // the queries: representative descriptors and projections of the new points
+  auto* best = static_cast<int32_t*>(scratch(h, "mb", sizeof(int32_t) * size_t(n_new), &rc));
+  auto* qd = static_cast<uint64_t*>(scratch(h, "mq", sizeof(uint64_t) * size_t(n_new) * h->W, &rc));
+  auto* uv = static_cast<double*>(scratch(h, "muv", sizeof(double) * 2 * size_t(n_new), &rc));
+  if (rc) return rc;
+  switch (h->W) {
+#define CASE(w) case w: k_map_repr<w><<<n_new, 64, 0, h->s>>>(h->desc.p, h->drow, h->doff, out, n_new, best, qd); break;
+    CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
+#undef CASE
+    default: return mapfail(SFM_EINVAL, "descriptor width");
+  }
+  k_project<<<grid(n_new), 256, 0, h->s>>>(n_new, out, h->X.p, R9[0], R9[1], R9[2], R9[3], R9[4], R9[5], R9[6], R9[7],
+                                           R9[8], t3[0], t3[1], t3[2], K9[0], K9[4], K9[2], K9[5], uv);
+  (void)hipMemcpyAsync(h->pin, out, sizeof(int32_t) * size_t(n_new), hipMemcpyDeviceToHost, h->s);
+  (void)hipMemcpyAsync(h->pin + n_new, best, sizeof(int32_t) * size_t(n_new), hipMemcpyDeviceToHost, h->s);
+  if (hipEventRecord(h->ev, h->s) != hipSuccess) return mapfail(SFM_EIO, "hipEventRecord failed");
+  int* res = nullptr;
+  if ((rc = matcher_match_current(mt, h->ev, qd, uv, n_new, train_idx, n_train, ratio_test, min_distance,
+                                  max_distance, &res)))
+    return rc;
+  if (int r = sync(h)) return r;
+  for (int i = 0; i < n_new; ++i)
+    if (h->pin[n_new + i] < 0)
+      return mapfail(SFM_EINVAL, "point " + std::to_string(h->pin[i]) + " has no descriptor row");
+  const int m = res[2 * n_new];
+  if (m > capacity) return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(m));
+  for (int k = 0; k < m; ++k) {
+    pts3d_match[k] = h->pin[res[k]];
+    train_match[k] = train_idx[res[n_new + k]];
+  }
+  *n_matches = m;
   return 0;
 }
 

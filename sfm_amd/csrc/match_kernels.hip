@@ -360,6 +360,38 @@ bool ok_ratio_window(double ratio, double mn, double mx) {
 
 extern "C" {
 
+}  // extern "C"
+
+namespace sfm {
+// For sfm_map_match_frame (map_store.hip): queries already on the device
+// (descriptor words q, positions p0; produced on another stream, ordered
+// after the event `after`) against a subset of the CURRENT frame's keypoints
+// (train_idx, host, frame-local); the (query, train) pairs in subset-local
+// indices, as sfm_matcher_match returns them, in *res (pinned, valid after
+// this call).
+int matcher_match_current(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
+                          const int32_t* train_idx, int n1, double ratio, double mn, double mx, int** res) {
+  if (h->frames_pushed < 1) return mfail(SFM_EINVAL, "push the current frame first");
+  const MatchFrame& fc = h->frame[h->cur];
+  for (int i = 0; i < n1; ++i)
+    if (train_idx[i] < 0 || train_idx[i] >= fc.n) return mfail(SFM_EINVAL, "train index out of range");
+  if (!ok_ratio_window(ratio, mn, mx)) return mfail(SFM_EINVAL, "non-finite threshold");
+  int rc = 0;
+  int* ix = pbuf<int>(h, "idx", size_t(n1), &rc);
+  int* dix = dbuf<int>(h, "didx", size_t(n1), &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);  // (the pinned index stage may feed an earlier copy)
+  std::memcpy(ix, train_idx, sizeof(int) * size_t(n1));
+  hipMemcpyAsync(dix, ix, sizeof(int) * size_t(n1), hipMemcpyHostToDevice, h->stream);
+  if (after && hipStreamWaitEvent(h->stream, after, 0) != hipSuccess) return mfail(SFM_EIO, "stream wait failed");
+  return run_match(h, q, nullptr, p0, n0, fc.desc, dix, fc.pts, n1, ratio, mn, mx, res);
+}
+int matcher_words(const sfm_matcher* h) { return h->W; }
+int matcher_device(const sfm_matcher* h) { return h->device; }
+}  // namespace sfm
+
+extern "C" {
+
 int sfm_matcher_create(int32_t device, int32_t desc_bytes, sfm_matcher** out) {
   if (!out) return mfail(SFM_EINVAL, "out is NULL");
   *out = nullptr;

@@ -222,6 +222,7 @@ class LiveSfM:
         self.stats = {"frames": 0, "tracked": 0, "pnp_inliers": 0, "map_matches": 0, "new_points": 0}
         self.times = {"stream": 0.0, "track": 0.0, "map_match": 0.0, "mapping": 0.0, "ba": 0.0}
         self._pending: _Frame | None = None
+        self.fused_find = True
 
     # ---- driver --------------------------------------------------------------
     def run(self, n_frames: int) -> None:
@@ -308,7 +309,20 @@ class LiveSfM:
         self.prev = cur
 
     def _find_map_points(self, cur: _Frame) -> None:
-        """CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692)."""
+        """CSfM::findMapPointsInCurrentFrame (CSfM.cpp:634-692): one device call
+        (sfm_map_match_frame) -- the composed form below (self.fused_find =
+        False) is the same query as separate map / matcher calls, kept as the
+        test's reference."""
+        if self.fused_find:
+            un = np.flatnonzero(cur.pt3d < 0).astype(np.int32)
+            if len(un) < 2:
+                return
+            existing = cur.pt3d[cur.pt3d >= 0].astype(np.int32)
+            pm, km = self.map.matchFrame(self.matcher, [f.no for f in self.kfs], existing, _rodrigues(cur.rot),
+                                         cur.t, self.K, un, 0.8, 0.0, MAX_REPR_ERR)
+            cur.pt3d[km] = pm
+            self.stats["map_matches"] += len(pm)
+            return
         cov = self.map.getPointsInFrames([f.no for f in self.kfs])
         existing = np.unique(cur.pt3d[cur.pt3d >= 0])
         new = np.setdiff1d(cov, existing, assume_unique=True).astype(np.int32)

@@ -67,6 +67,40 @@ def test_live_path_tracks_every_frame_and_grows_the_map(run80):
     assert len(s.ba_log) == len(s.kfs) - 1
 
 
+class _BothFinds(LiveSfM):
+    """findMapPointsInCurrentFrame both ways on every tracked frame's state:
+    the fused device call (sfm_map_match_frame) and the composed map /
+    matcher calls; the composed result is the one kept."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.cmp = []
+
+    def _find_map_points(self, cur):
+        base = cur.pt3d.copy()
+        self.fused_find = True
+        super()._find_map_points(cur)
+        fused = cur.pt3d.copy()
+        cur.pt3d[:] = base
+        self.fused_find = False
+        super()._find_map_points(cur)
+        self.cmp.append((cur.no, fused, cur.pt3d.copy()))
+
+
+def test_fused_find_map_points_equals_the_composed_calls():
+    s = _BothFinds(KeypointStream())
+    try:
+        s.run(45)
+        assert len(s.cmp) >= 35
+        found = 0
+        for no, fused, comp in s.cmp:
+            assert np.array_equal(fused, comp), f"frame {no}: {np.flatnonzero(fused != comp)[:10]}"
+            found += int((comp >= 0).sum())
+        assert found > 0
+    finally:
+        s.close()
+
+
 def test_every_keyframe_ba_matches_oracle(run80):
     for rec in run80.ba_log:
         r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
