@@ -30,6 +30,7 @@ namespace sfm {
 // (slot 0: partial tile, slot 1: final tile).  Read by sfm_debug_stamps.
 __device__ unsigned long long g_wstamp[256 * 16];
 __device__ unsigned long long g_hstamp[128 * 128 * 2];
+__device__ unsigned long long g_pstamp[256 * 4];  // per wave: the end of its panel-3 work
 #define WSTAMP(j, k)                                                                          \
   do {                                                                                        \
     if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -37,6 +38,10 @@ __device__ unsigned long long g_hstamp[128 * 128 * 2];
 #define WSTAMPV(j, k, v)                                       \
   do {                                                         \
     if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = (v); \
+  } while (0)
+#define PSTAMP(j, w)                                                                                      \
+  do {                                                                                                    \
+    if ((threadIdx.x & 63) == 0 && (j) < 256) g_pstamp[(j) * 4 + (w)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define HSTAMP(i, j, k)                                                                                         \
   do {                                                                                                          \
@@ -46,6 +51,7 @@ __device__ unsigned long long g_hstamp[128 * 128 * 2];
 #define WSTAMP(j, k) do { } while (0)
 #define WSTAMPV(j, k, v) do { } while (0)
 #define HSTAMP(i, j, k) do { } while (0)
+#define PSTAMP(j, w) do { } while (0)
 #endif
 namespace {
 
@@ -132,6 +138,25 @@ __device__ __forceinline__ void w_offdiag(const double* T, double* Wl, double* s
   for (int rr = 0; rr < 4; ++rr) Wl[(16 * J + j) * TS + 16 * I + 4 * rr + kk] = -acc2[rr];
 }
 
+// W_00 = L_00^-1 from the panel-0 factor in T and the pivots' inverses inv
+// [16], lane m < 16 forming column m with the very operations wave 0's panel
+// carried it with before (per entry: the column updates k = 0 .. c-1 as
+// fma(-L(c,k), w_k, .) in k order, then the scaling by inv_c): bitwise the
+// same W_00, off the pivot chain (panel 0 went 2.43 -> see DESIGN.md §5).
+__device__ __forceinline__ void trtri16(const double* T, double* Wl, const double* inv, int lane) {
+  if (lane >= 16) return;
+  double w[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double acc = (c == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < c; ++k) acc = fma(-T[k * TS + c], w[k], acc);
+    w[c] = acc * inv[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) Wl[lane * TS + c] = w[c];
+}
+
 // Row 3 of W in two halves, so that the sum runs during panel 3:
 // scr = sum_{K=J}^{2} L_3K W_KJ (needs only L rows 48.. of panels 0-2 and W
 // rows 0-2), then W_3J = -W_33 scr once panel 3 is out.  Same MFMA order
@@ -154,10 +179,32 @@ __device__ __forceinline__ void w_row3_finish(double* Wl, const double* scr, int
 // The walker's last update T -= Ls Ls^T (Ls = L_j,j-1 in LDS) of the lower
 // 16x16 blocks (I, J) = (Ib[q], Jb[q]), q < nq, by one wavefront; the MFMA
 // chains of the blocks are interleaved (same k order per block as a chain).
+// last_update_acc forms the products only (acc), last_update_apply
+// subtracts them (the walker forms column block 0's at the end of the
+// previous step, beside the drain of L_j,j-1's stores).
+template <int kMax>
+__device__ __forceinline__ void last_update_acc(const double* Ls, const int* Ib, const int* Jb, int nq, int lane,
+                                                f64x4 (&acc)[kMax]);
+template <int kMax>
+__device__ __forceinline__ void last_update_apply(double* T, const int* Ib, const int* Jb, int nq, int lane,
+                                                  const f64x4 (&acc)[kMax]) {
+  const int li = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < kMax; ++q)
+    if (q < nq)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) T[(16 * Jb[q] + li) * TS + 16 * Ib[q] + 4 * rr + kk] -= acc[q][rr];
+}
 template <int kMax>
 __device__ __forceinline__ void last_update(double* T, const double* Ls, const int* Ib, const int* Jb, int nq, int lane) {
-  const int li = lane & 15, kk = lane >> 4;
   f64x4 acc[kMax];
+  last_update_acc<kMax>(Ls, Ib, Jb, nq, lane, acc);
+  last_update_apply<kMax>(T, Ib, Jb, nq, lane, acc);
+}
+template <int kMax>
+__device__ __forceinline__ void last_update_acc(const double* Ls, const int* Ib, const int* Jb, int nq, int lane,
+                                                f64x4 (&acc)[kMax]) {
+  const int li = lane & 15, kk = lane >> 4;
 #pragma unroll
   for (int q = 0; q < kMax; ++q) acc[q] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -185,11 +232,6 @@ __device__ __forceinline__ void last_update(double* T, const double* Ls, const i
       for (int q = 0; q < kMax; ++q)
         if (q < nq) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4][q], b[s4][q], acc[q], 0, 0, 0);
   }
-#pragma unroll
-  for (int q = 0; q < kMax; ++q)
-    if (q < nq)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) T[(16 * Jb[q] + li) * TS + 16 * Ib[q] + 4 * rr + kk] -= acc[q][rr];
 }
 
 // Trailing update of the 16x16 block (I, J) by the panel at columns g0..g0+15,
@@ -295,14 +337,13 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     if (w == 0 && b > 0) {
       panel_w0<kFull>(T, Wl, g0, k0, n, lane, bad);
     } else if (w == 0) {
-      // ---- panel 0 factorisation: lane r = row r; lanes m < 16 carry W_bb column m ----
+      // ---- panel 0 factorisation: lane r = row r.  W_00 is not carried here
+      // (no rows above the panel to carry it in): the pivots' inverses go to
+      // scr[0] and wave 2 forms W_00 during panel 1 (trtri16) ----
       const int r = lane;
-      double p[16], wc[16];
+      double p[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        p[j] = T[(g0 + j) * TS + r];
-        wc[j] = (j == r) ? 1.0 : 0.0;
-      }
+      for (int j = 0; j < 16; ++j) p[j] = T[(g0 + j) * TS + r];
       double d = bcast(p[0], g0);
       double lp = 0.0, lcp[16];  // deferred LDS-fed updates, as in panels 1..3
 #pragma unroll
@@ -316,13 +357,10 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
         const double l = p[j] * inv;  // L(r, g) for r >= g (r == g: sqrt(d))
         p[j] = l;
         T[g * TS + r] = l;
-        wc[j] *= inv;
+        if (r == 0) scr[0][j] = inv;
         if (j >= 1 && j < 15) {
 #pragma unroll
-          for (int c = j + 1; c < 16; ++c) {  // column j - 1
-            p[c] = fma(-lp, lcp[c], p[c]);
-            wc[c] = fma(-lcp[c], wc[j - 1], wc[c]);
-          }
+          for (int c = j + 1; c < 16; ++c) p[c] = fma(-lp, lcp[c], p[c]);  // column j - 1
         }
         if (j < 15) {
           // critical path by readlane only: the next pivot (lane g+1's own
@@ -330,7 +368,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
           const double dn = bcast(fma(-l, l, p[j + 1]), g + 1);
           const double l1 = bcast(l, g + 1);
           p[j + 1] = fma(-l, l1, p[j + 1]);
-          wc[j + 1] = fma(-l1, wc[j], wc[j + 1]);
           if (j < 14) {
 #pragma unroll
             for (int c = j + 2; c < 16; ++c) lcp[c] = T[g * TS + g0 + c];
@@ -339,9 +376,6 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
           d = dn;
         }
       }
-      if (r < 16)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) Wl[(g0 + r) * TS + g0 + c] = wc[c];
     } else if (b == 0) {
       if (Ls != nullptr) {
         // deferred last update: wave 1 blocks (1,1) (2,2), wave 2 (2,1) (3,2),
@@ -352,12 +386,21 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     } else if (b == 1) {
       // panel 0's trailing update of blocks (2,2) (3,2) (3,3) [waves 1, 2, 3]
       trail_block(T, 0, w == 1 ? 2 : 3, w == 3 ? 3 : 2, lane);
+      if (w == 2) trtri16(T, Wl, scr[0], lane);  // W_00 (read by wave 1 in panel 2)
     } else if (w == 1) {
       w_offdiag(T, Wl, scr[w], 1, 0, lane);  // row 1 of W (its diagonal block is done)
     } else if (w == 3) {
       trail_block(T, 16, 3, 3, lane);  // panel 1's trailing update of block (3,3)
     } else if (pf_sub != nullptr) {  // (b == 2, wave 2)
-      rdy[0] = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      // a second poll ~0.55 us later when the first misses: the tile is out
+      // ~5.4 us into the step, panel 2 starts at ~5.1 us (stamped), and a
+      // poll's round trip (~1 us) still ends within the panel (1.8 us)
+      bool f = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (!__builtin_amdgcn_readfirstlane(int(f))) {
+        __builtin_amdgcn_s_sleep(20);
+        f = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      }
+      rdy[0] = f;
     }
     __syncthreads();
     WSTAMP(k0 / NB, 2 + b);
@@ -370,6 +413,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
   // ---- panel 3 (peeled) ----
   if (w == 0) {
     panel_w0<kFull>(T, Wl, 48, k0, n, lane, bad);
+    PSTAMP(k0 / NB, 0);
   } else {
     // the walker's next partial tiles: the diagonal tile's poll, then the
     // prefetch's loads go out first (the poll ahead of them: vmcnt is one
@@ -385,6 +429,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     w_row3_sum(T, Wl, scr[w], w - 1, lane);
     if (w == 3 && pf_diag != nullptr) rdy[1] = dflag == epoch;
+    PSTAMP(k0 / NB, w);
   }
   __syncthreads();
   WSTAMP(k0 / NB, 5);
@@ -986,6 +1031,10 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // the next diagonal tile travels in registers (loaded one step ahead)
   d2v nx[8];
+  // the last update of the next diagonal tile's column block 0 (block (w, 0)),
+  // formed at the end of the previous step
+  f64x4 g0acc[1];
+  g0acc[0] = f64x4{0.0, 0.0, 0.0, 0.0};
   block_wait_sc1(Pf, epoch, fail);
   tile_ld2_sc1(nx, A, ld);
   for (int j = 0; j < (kPanel ? ncols : nb); ++j) {
@@ -995,10 +1044,11 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     if (t == 0) rdy[0] = rdy[1] = 0;
     __syncthreads();
     if (j > 0) {
-      // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0)); the
-      // blocks right of it are updated inside potrf_tile, during panel 0
+      // T -= L_j,j-1 L_j,j-1^T on column block 0 (wave w: block (w, 0); its
+      // products were formed at the end of the last step); the blocks right
+      // of it are updated inside potrf_tile, during panel 0
       const int Ib[1] = {w}, Jb[1] = {0};
-      last_update<1>(T, Ls, Ib, Jb, 1, lane);
+      last_update_apply<1>(T, Ib, Jb, 1, lane, g0acc);
       // L_j,j-1 (stored at the end of the last step) has drained: its flag
       block_publish_wt(F + j * nb + j - 1, epoch);
     }
@@ -1062,6 +1112,12 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     put_tile(Ls, x, lane);
     __syncthreads();
     WSTAMP(j, 13);
+    if (next) {
+      // the next step's column-block-0 update products (its MFMAs run while
+      // the stores below drain)
+      const int Ib[1] = {w}, Jb[1] = {0};
+      last_update_acc<1>(Ls, Ib, Jb, 1, lane, g0acc);
+    }
     tile_st2_wt<false>(A + size_t(j0) * ld + i0, ld, Ls);
     WSTAMP(j, 14);
     if (kPanel && !next) {
@@ -1591,6 +1647,10 @@ void launch_spd_fill(double* A, int ld, int n, unsigned seed, hipStream_t s) {
 }  // namespace sfm
 
 #ifdef SFM_CHOL_STAMPS
+extern "C" int sfm_debug_pstamps(unsigned long long* out, int n) {
+  if (n > 256 * 4) n = 256 * 4;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_pstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
+}
 extern "C" int sfm_debug_stamps(unsigned long long* out, int n, unsigned long long* hout, int hn) {
   if (n > 256 * 16) n = 256 * 16;
   if (hn > 128 * 128 * 2) hn = 128 * 128 * 2;

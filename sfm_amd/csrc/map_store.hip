@@ -197,6 +197,16 @@ __global__ void k_scatter_points(int n, const int32_t* __restrict__ idx, const d
 
 inline unsigned grid(int64_t n, int b = 256) { return unsigned((n + b - 1) / b); }
 
+__global__ void k_gather_points(int n, const int32_t* __restrict__ idx, const double* __restrict__ X,
+                                double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t p = size_t(idx[i]) * 3;
+  out[3 * size_t(i)] = X[p];
+  out[3 * size_t(i) + 1] = X[p + 1];
+  out[3 * size_t(i) + 2] = X[p + 2];
+}
+
 __global__ void k_unmark(int n, const int32_t* __restrict__ pts, uint8_t* __restrict__ mark) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) mark[pts[i]] = 0;
@@ -455,11 +465,30 @@ int sfm_map_get_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, double* 
   if (!pts3d_idx || !pts3d) return mapfail(SFM_EINVAL, "NULL argument");
   if (int rc = check_pts(h, n, pts3d_idx)) return rc;
   if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
-  std::vector<double> all(size_t(h->n_pts) * 3);
-  if (hipMemcpyAsync(all.data(), h->X.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, h->s) != hipSuccess)
+  // gathered on the device: the indices up, n points down (the whole X
+  // array went down before: 140 KB per tracked frame at 6k points)
+  int rc = 0;
+  auto* di = static_cast<int32_t*>(scratch(h, "gi", sizeof(int32_t) * size_t(n), &rc));
+  auto* dv = static_cast<double*>(scratch(h, "gv", sizeof(double) * 3 * size_t(n), &rc));
+  if (rc) return rc;
+  if (h->pin_cap < 8 * size_t(n) + 8) {
+    if (h->pin) { (void)hipStreamSynchronize(h->s); (void)hipHostFree(h->pin); }
+    h->pin = nullptr;
+    h->pin_cap = 0;
+    const size_t cap = std::max<size_t>(8 * size_t(n) + 8, 8192) * 3 / 2;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int32_t) * cap) != hipSuccess)
+      return mapfail(SFM_ENOMEM, "hipHostMalloc failed");
+    h->pin_cap = cap;
+  }
+  (void)hipStreamSynchronize(h->s);  // (the pinned block may feed an earlier copy)
+  std::memcpy(h->pin, pts3d_idx, sizeof(int32_t) * size_t(n));
+  double* pv = reinterpret_cast<double*>(h->pin + ((size_t(n) + 1) & ~size_t(1)));
+  (void)hipMemcpyAsync(di, h->pin, sizeof(int32_t) * size_t(n), hipMemcpyHostToDevice, h->s);
+  k_gather_points<<<grid(n), 256, 0, h->s>>>(n, di, h->X.p, dv);
+  if (hipMemcpyAsync(pv, dv, sizeof(double) * 3 * size_t(n), hipMemcpyDeviceToHost, h->s) != hipSuccess)
     return mapfail(SFM_EIO, "download failed");
-  if (int rc = sync(h)) return rc;
-  for (int32_t i = 0; i < n; ++i) std::memcpy(pts3d + 3 * size_t(i), all.data() + 3 * size_t(pts3d_idx[i]), 24);
+  if (int r = sync(h)) return r;
+  std::memcpy(pts3d, pv, sizeof(double) * 3 * size_t(n));
   return 0;
 }
 

@@ -73,7 +73,13 @@ ev = {
     "potrf end (W_j ready)": [st[j, 9] - st[j, 0] for j in js],
 }
 arr = {k: (round(float(np.median(v)), 2), round(float(np.percentile(v, 90)), 2)) for k, v in ev.items()}
+# per wave: the end of its panel-3 work after the panel's start (slot 8)
+pb = (ctypes.c_ulonglong * (256 * 4))()
+p3w = None
+if hasattr(L, "sfm_debug_pstamps") and L.sfm_debug_pstamps(pb, 256 * 4) == 0:
+    ps = np.array(pb[:], dtype=np.float64).reshape(256, 4) / 100.0
+    p3w = {f"wave{w}": round(float(np.mean([ps[j, w] - st[j, 8] for j in js])), 3) for w in range(4)}
 out = {"n": n, "ms_factor_plus_backsolve": round(ms, 4), "fail": fail, "rel_residual": res,
        "step_us": round(step, 3), "steps": nb, "early_frac": early, "walker_us": walker, "potrf_us": potrf,
-       "arrivals_us_median_p90": arr}
+       "arrivals_us_median_p90": arr, "panel3_work_end_us_per_wave": p3w}
 print(json.dumps(out, indent=1))
