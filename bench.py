@@ -798,7 +798,7 @@ def main() -> int:
             mfma = {}
 
     def traffic(kernel):
-        e = pmc.get(kernel) or {}
+        e = pmc.get(kernel) or pmc.get(kernel + "<false>") or {}
         v = e.get("hbm_bytes_per_launch")
         return None if v is None else int(v)
 
@@ -822,7 +822,8 @@ def main() -> int:
                  "achieved": round(chol_tfs, 3), "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                  "frac": round(chol_tfs / F64_MFMA_PEAK_TFS, 4), "traffic": traffic("k_chol_fused"),
                  "algorithmic_flops": cholesky_flops(n_sys), "avg_ms": round(chol_ms, 4),
-                 "mfma_busy_frac_pmc": (mfma.get("k_chol_fused") or {}).get("mfma_busy_frac")}
+                 "mfma_busy_frac_pmc": (mfma.get("k_chol_fused<false>") or mfma.get("k_chol_fused") or {}).get(
+                     "mfma_busy_frac")}
     roofline = roof_chol if dominant == "cholesky" else roof_jac
 
     wl = head.pop("workload")
