@@ -154,6 +154,9 @@ struct sfm_ba_handle {
   // stream and the two events that fork and join it
   hipStream_t stream2 = nullptr;
   hipEvent_t ov_ev[2] = {nullptr, nullptr};
+  // set_problem's parameter upload beside the layout kernels (large problems)
+  hipStream_t ustream = nullptr;
+  hipEvent_t uev = nullptr;
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -1367,6 +1370,11 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
     hipEventDestroy(h->ov_ev[0]);
     hipEventDestroy(h->ov_ev[1]);
   }
+  if (h->ustream) {
+    hipStreamSynchronize(h->ustream);
+    hipStreamDestroy(h->ustream);
+    hipEventDestroy(h->uev);
+  }
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
   hipStreamDestroy(h->stream);
@@ -1715,6 +1723,36 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     }
     HCHK(hipMemcpyAsync(pb, ps, pl.bytes, hipMemcpyHostToDevice, s));
   }
+  // large problems: the parameters (above the stage's 1 MB) go up from the
+  // caller's pageable arrays on a stream of their own while the layout
+  // kernels run (the host's staging copies took ~0.5 ms at C3 after the
+  // layout round trip, with the device idle); the solve stream waits for them
+  // at the end of set_problem
+  const bool side_params = !early_params && (C || P) && pl.bytes > kStageMaxBytes;
+  if (side_params) {
+    uint8_t* pb = nullptr;
+    ALLOC(pb, pl.bytes);
+    d.Kc = reinterpret_cast<double*>(pb + o_K);
+    d.cam = reinterpret_cast<double*>(pb + o_c);
+    d.cam0 = reinterpret_cast<double*>(pb + o_c0);
+    d.X = reinterpret_cast<double*>(pb + o_X);
+    d.X0 = reinterpret_cast<double*>(pb + o_X0);
+    if (!h->ustream) {
+      HCHK(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
+      HCHK(hipEventCreateWithFlags(&h->uev, hipEventDisableTiming));
+    }
+  }
+  auto upload_params_side = [&]() -> int {
+    hipStream_t u = h->ustream;
+    if (hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, u) != hipSuccess ||
+        hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, u) != hipSuccess ||
+        hipMemcpyAsync(d.cam0, d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToDevice, u) != hipSuccess ||
+        (P && (hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, u) != hipSuccess ||
+               hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, u) != hipSuccess)) ||
+        hipEventRecord(h->uev, u) != hipSuccess)
+      return fail(SFM_EIO, "parameter upload failed");
+    return 0;
+  };
   int32_t* small_cnt = nullptr;  // small path: per-block pair counts
   if (small) {
     // the same layouts without radix sorts (ba_setup.hip small path):
@@ -1770,6 +1808,10 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     // grids by the largest slice (obs_xcd_blocks)
     HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     timer.mark("layout launches");
+    if (side_params) {
+      if ((rc = upload_params_side())) return bail(rc);
+      timer.mark("parameter upload (side stream)");
+    }
     HCHK(hipStreamSynchronize(s));
     std::memcpy(&n_pairs, stg, sizeof(int64_t));
     int32_t g[9];
@@ -1873,7 +1915,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   d.nblk = d.ld / kNB;
   d.max_blocks = std::max({1, C, blocks_for(N, 256), blocks_for(P, 256), d.jac_blocks,
                            d.jac_blocks_rec, blocks_for(npad, 256), obs_xcd_blocks(d), pt_xcd_blocks(d)});
-  if (!early_params) {
+  if (!early_params && !side_params) {
     uint8_t* pb = nullptr;
     ALLOC(pb, pl.bytes);
     d.Kc = reinterpret_cast<double*>(pb + o_K);
@@ -1939,7 +1981,10 @@ constexpr int64_t kHostCheckMaxObs = 65536;
 #undef ALLOC
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
-  if ((C || P) && !early_params) {
+  if (side_params) {
+    if (small && (rc = upload_params_side())) return bail(rc);  // (the small path has no layout round trip)
+    HCHK(hipStreamWaitEvent(s, h->uev, 0));
+  } else if ((C || P) && !early_params) {
     if (pl.bytes <= kStageMaxBytes) {
       // the stage is free: the n_pairs readback synchronised the stream
       if ((rc = stage_reserve(h, pl.bytes))) return bail(rc);
