@@ -267,6 +267,7 @@ __device__ __forceinline__ void trail_block(double* T, int g0, int I, int J, int
 // only.
 struct NoPrefetch {
   __device__ void load() {}
+  __device__ void w_early(const double*, int) {}
 };
 
 // Wave 0's factorisation of panel b >= 1 (columns g0 = 16 b ..): rows r < g0
@@ -330,6 +331,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
     Wl[c * TS + r] = 0.0;
   }
+  if (t == 0) rdy[2] = 0;  // panel 3's W_20 hand-off (wave 3 -> wave 1)
   __syncthreads();
   bool bad = false;
   for (int b = 0; b < 3; ++b) {
@@ -422,19 +424,45 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     int dflag = 0;
     if (w == 3 && pf_diag != nullptr) dflag = __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (pf_sub != nullptr && __builtin_amdgcn_readfirstlane(rdy[0]) != 0) pre.load();
-    // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1)
-    if (w <= 2) w_offdiag(T, Wl, scr[w], 2, w - 1, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    w_row3_sum(T, Wl, scr[w], w - 1, lane);
+    // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1).
+    // W_20 is formed by wave 3 (its own row-3 sum is one product) and handed
+    // to wave 1 by an LDS flag: wave 1 forms its sum's K = 0, 1 products
+    // meanwhile and adds K = 2 last, as the chain always did (bitwise the
+    // same W; wave 1 carried 6 of the panel's 11 16x16x16 products and ended
+    // after wave 0, stamped)
+    if (w == 3) {
+      w_offdiag(T, Wl, scr[3], 2, 0, lane);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&rdy[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      w_row3_sum(T, Wl, scr[3], 2, lane);
+    } else if (w == 2) {
+      w_offdiag(T, Wl, scr[2], 2, 1, lane);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      w_row3_sum(T, Wl, scr[2], 1, lane);
+    } else {
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mfma16(T + 48, 1, TS, Wl, 1, TS, acc, lane);
+      acc = mfma16(T + 16 * TS + 48, 1, TS, Wl + 16, 1, TS, acc, lane);
+      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&rdy[2], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      acc = mfma16(T + 32 * TS + 48, 1, TS, Wl + 32, 1, TS, acc, lane);
+      const int j = lane & 15, kk = lane >> 4;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) scr[1][(4 * rr + kk) * 16 + j] = acc[rr];
+    }
     if (w == 3 && pf_diag != nullptr) rdy[1] = dflag == epoch;
     PSTAMP(k0 / NB, w);
   }
   __syncthreads();
   WSTAMP(k0 / NB, 5);
   // ---- W row 3 off the diagonal: the products with W_33 ----
+  // (wave 0, idle here: the stores of W rows 0-2, final since panel 3)
   if (w >= 1) w_row3_finish(Wl, scr[w], w - 1, lane);
+  else pre.w_early(Wl, lane);
   __syncthreads();
   WSTAMP(k0 / NB, 9);
   return bad;
@@ -931,11 +959,14 @@ __device__ __forceinline__ d2v ld2_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t byte_
 // offsets run through an opaque register at every step: hoisted out of the
 // walker's loop, the per-lane addresses held 44 registers across the whole
 // walk (140 VGPRs spilled, each reload a vmcnt(0) wait).
+__device__ __forceinline__ void w_st_rows012(double* dst, const double* Wl, int lane);
 struct SubPrefetch {
   const double* src;
   int ld;
   double* D;
+  double* wdst;  // W_j's home (its rows 0-2 go out from potrf_tile's end)
   d2v v[11];
+  __device__ __forceinline__ void w_early(const double* Wl, int lane) { w_st_rows012(wdst, Wl, lane); }
   __device__ __forceinline__ void load() {
     const int u = tid_local() - 64;
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(src);
@@ -1023,6 +1054,52 @@ __device__ __forceinline__ void tile_st2_wt(double* dst, int ld, const double* D
     off += step;
   }
 }
+// W_j = Wl (lower 16x16 blocks) -> dst (ld NB), in two parts: blocks (I, J)
+// of rows 0-2 by one wavefront (pair e = lane + 64 h of block q: column
+// 16 J + (e >> 3), rows 16 I + 2 (e & 7) and + 1; 128-B column runs), row 3
+// by the block (pair e = t + 256 h: column e >> 3, rows 48 + 2 (e & 7)).
+__device__ __forceinline__ void w_st_rows012(double* dst, const double* Wl, int lane) {
+  constexpr int BI[6] = {0, 1, 2, 1, 2, 2}, BJ[6] = {0, 0, 0, 1, 1, 2};
+  d2v v[12];
+  const int cl = lane >> 3, rl = 2 * (lane & 7);
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    const int c = 16 * BJ[q >> 1] + 8 * (q & 1) + cl, r = 16 * BI[q >> 1] + rl;
+    v[q].x = Wl[c * TS + r];
+    v[q].y = Wl[c * TS + r + 1];
+  }
+#pragma unroll
+  for (int q = 0; q < 12; ++q) asm volatile("" : "+v"(v[q]));
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(dst);
+  const uint32_t off0 = uint32_t((cl * NB + rl) * 8);
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    uint32_t off = off0 + uint32_t(((16 * BJ[q >> 1] + 8 * (q & 1)) * NB + 16 * BI[q >> 1]) * 8);
+    asm volatile("" : "+v"(off));
+    st2_sc1(rs, off, v[q]);
+  }
+}
+__device__ __forceinline__ void w_st_row3(double* dst, const double* Wl) {
+  const int t = tid_local();
+  d2v v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = t + 256 * h, c = e >> 3, r = 48 + 2 * (e & 7);
+    v[h].x = Wl[c * TS + r];
+    v[h].y = Wl[c * TS + r + 1];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(v[h]));
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(dst);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int e = t + 256 * h;
+    uint32_t off = uint32_t(((e >> 3) * NB + 48 + 2 * (e & 7)) * 8);
+    asm volatile("" : "+v"(off));
+    st2_sc1(rs, off, v[h]);
+  }
+}
+
 template <bool kPanel>  // a column panel (ncols < nb possible) or the whole factor (ncols == nb)
 __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int n, int nb, int ncols,
                              double* __restrict__ Winv,
@@ -1059,7 +1136,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     const int i0 = j0 + NB;
     const int* fsub = more ? Pf + (j + 1) * nb + j : nullptr;
     // the subdiagonal partial tile, prefetched into Tn during panel 3
-    SubPrefetch pre{A + size_t(j0) * ld + i0, ld, Tn};
+    SubPrefetch pre{A + size_t(j0) * ld + i0, ld, Tn, Winv + size_t(j) * NB * NB};
     const int* fdiag = next ? Pf + (j + 1) * nb + j + 1 : nullptr;
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre)
                                     : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre);
@@ -1070,8 +1147,9 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     if (early && w >= 1) pre.store();
     WSTAMPV(j, 15, early ? 1ull : 0ull);
     // W_j: lower 16x16 blocks only (the upper blocks of every W_k stay zero
-    // from set_problem, one memset: 37% fewer bytes on the chain)
-    tile_st2_wt<true>(Winv + size_t(j) * NB * NB, NB, Wl);
+    // from set_problem, one memset: 37% fewer bytes on the chain); rows 0-2
+    // went out from the POTRF's last phase (wave 0), row 3 here
+    w_st_row3(Winv + size_t(j) * NB * NB, Wl);
     WSTAMP(j, 10);
     // W_j out at once: the helpers' TRSMs of column j feed the last updates
     // of the diagonal tiles two steps ahead (a chain as long as a step)
@@ -1144,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_chol_fused(double* __restrict__ A, int 
   __shared__ double Ls[NB * TS];
   __shared__ double Tn[NB * TS];  // the walker's subdiagonal tile (helpers: unused)
   __shared__ double scr[4][256];
-  __shared__ int sh[2];
+  __shared__ int sh[4];
   if (gate && *gate == 0) {
     // device LM loop, phase skipped: the launch still takes its ntask + nhelp
     // tickets and its 1 + nhelp role tickets, so the next epoch's bases stay
@@ -1335,7 +1413,7 @@ __global__ __launch_bounds__(256) void k_chol_small(const double* __restrict__ A
   __shared__ double scr[4][256];
   __shared__ double v[NB];
   __shared__ double yl[NB];        // y_1
-  __shared__ int rdy[2];
+  __shared__ int rdy[4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // ---- step 0: POTRF of tile (0, 0) ----
   load_tile(T, A, ld, 0, 0);
