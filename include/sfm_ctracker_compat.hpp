@@ -288,6 +288,8 @@ class FeatureMatcher {
     return matchFeatures(pts0, desc0, pts1, desc1, matchIdx0, matchIdx1, min_, max_);
   }
 
+  sfm_matcher* handle() const { return h_; }
+
  private:
   sfm_matcher* h_ = nullptr;
   int rc_ = SFM_OK;
@@ -692,6 +694,29 @@ class MapStore {
     const int rc = sfm_map_representative_descriptors(h_, int32_t(n), pts3DIdx.data(), d.data(), nullptr);
     if (rc) return rc;
     descriptors.insert(descriptors.end(), d.begin(), d.end());
+    return SFM_OK;
+  }
+
+  // CSfM::findMapPointsInCurrentFrame's query (CSfM.cpp:634-692) as one
+  // device call (sfm_map_match_frame): the points of keyframes frameNo minus
+  // `existing`, projected by x = K (R X + t) (R9, K9 row-major), matched by
+  // their representative descriptors against keypoints trainIdx of the frame
+  // last pushed to `mt`; appends the (map point, frame keypoint) pairs.
+  int matchFrame(FeatureMatcher& mt, const std::vector<int>& frameNo, const std::vector<int>& existing,
+                 const double* R9, const double* t3, const double* K9, const std::vector<int>& trainIdx,
+                 double ratio, double minDistance, double maxDistance, std::vector<int>& pts3DIdx,
+                 std::vector<int>& kpIdx) {
+    if (!h_) return rc_;
+    if (trainIdx.size() < 2) return SFM_OK;
+    std::vector<int32_t> p3(trainIdx.size()), k2(trainIdx.size());
+    int32_t n = 0;
+    const int rc = sfm_map_match_frame(h_, mt.handle(), int32_t(frameNo.size()), frameNo.data(),
+                                       int32_t(existing.size()), existing.data(), R9, t3, K9,
+                                       int32_t(trainIdx.size()), trainIdx.data(), ratio, minDistance, maxDistance,
+                                       int32_t(trainIdx.size()), p3.data(), k2.data(), &n);
+    if (rc) return rc;
+    pts3DIdx.insert(pts3DIdx.end(), p3.begin(), p3.begin() + n);
+    kpIdx.insert(kpIdx.end(), k2.begin(), k2.begin() + n);
     return SFM_OK;
   }
 
