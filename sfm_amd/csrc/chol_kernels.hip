@@ -31,6 +31,11 @@ namespace sfm {
 __device__ unsigned long long g_wstamp[256 * 16];
 __device__ unsigned long long g_hstamp[128 * 128 * 2];
 __device__ unsigned long long g_pstamp[256 * 4];  // per wave: the end of its panel-3 work
+__device__ unsigned long long g_bstamp[256 * 8];  // k_backsolve per block row (sfm_debug_bstamps)
+#define BSTAMP(b, k)                                                                          \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && (b) < 256) g_bstamp[(b) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define WSTAMP(j, k)                                                                          \
   do {                                                                                        \
     if (threadIdx.x == 0 && (j) < 256) g_wstamp[(j) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -52,6 +57,7 @@ __device__ unsigned long long g_pstamp[256 * 4];  // per wave: the end of its pa
 #define WSTAMPV(j, k, v) do { } while (0)
 #define HSTAMP(i, j, k) do { } while (0)
 #define PSTAMP(j, w) do { } while (0)
+#define BSTAMP(b, k) do { } while (0)
 #endif
 namespace {
 
@@ -1362,8 +1368,10 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
         __builtin_amdgcn_s_sleep(1);
       }
       yb[lane] = yv;
+      if (k == b + 1) BSTAMP(b, 0);
     }
     __syncthreads();
+    if (k == b + 1) BSTAMP(b, 1);
     if (__builtin_amdgcn_readfirstlane(timed_out)) break;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc = fma(lv[i], yb[16 * seg + i], acc);
@@ -1372,7 +1380,9 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
   acc += __shfl_xor(acc, 1);
   acc += __shfl_xor(acc, 2);
   if (seg == 0) v[col] = (col < nreal) ? zc - acc : 0.0;
+  BSTAMP(b, 2);
   __syncthreads();
+  BSTAMP(b, 3);
   // y_b[col] = sum_c W(c, col) v[c]: 16 terms per lane in four chains, then
   // the four segments
   double p4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1385,6 +1395,7 @@ __global__ __launch_bounds__(256) void k_backsolve(const double* __restrict__ A,
   // polls see it when it lands, with nothing to order after it
   if (seg == 0) __hip_atomic_store(y + size_t(k0) + col, col < nreal ? sum : 0.0, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+  BSTAMP(b, 4);
   if (wave0() && timed_out) atomicOr(fail, 2);
 }
 
@@ -1725,6 +1736,10 @@ void launch_spd_fill(double* A, int ld, int n, unsigned seed, hipStream_t s) {
 }  // namespace sfm
 
 #ifdef SFM_CHOL_STAMPS
+extern "C" int sfm_debug_bstamps(unsigned long long* out, int n) {
+  if (n > 256 * 8) n = 256 * 8;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_bstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
+}
 extern "C" int sfm_debug_pstamps(unsigned long long* out, int n) {
   if (n > 256 * 4) n = 256 * 4;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(sfm::g_pstamp), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -5;
