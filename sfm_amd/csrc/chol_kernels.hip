@@ -337,7 +337,7 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     const int e = t + 256 * q, c = e >> 6, r = e & 63;
     Wl[c * TS + r] = 0.0;
   }
-  if (t == 0) rdy[2] = 0;  // panel 3's W_20 hand-off (wave 3 -> wave 1)
+  if (t == 0) rdy[2] = rdy[3] = 0;  // panel 3's W_20 hand-off (wave 3 -> wave 1), its late-poll bits
   __syncthreads();
   bool bad = false;
   for (int b = 0; b < 3; ++b) {
@@ -415,6 +415,9 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     // ---- trailing update of column block b+1 (the next panel's); the
     // blocks right of it follow during the next panel (look-ahead) ----
     if (w < 3 - b) trail_block(T, g0, b + 1 + w, b + 1, lane);
+    // (b = 2: a third poll of the subdiagonal partial tile by idle wave 2)
+    if (b == 2 && w == 2 && pf_sub != nullptr && __builtin_amdgcn_readfirstlane(rdy[0]) == 0)
+      rdy[0] = __hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     __syncthreads();
     WSTAMP(k0 / NB, 6 + b);
   }
@@ -429,7 +432,17 @@ __device__ __forceinline__ bool potrf_tile(double* T, double* Wl, double (*scr)[
     // written at the end
     int dflag = 0;
     if (w == 3 && pf_diag != nullptr) dflag = __hip_atomic_load(pf_diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (pf_sub != nullptr && __builtin_amdgcn_readfirstlane(rdy[0]) != 0) pre.load();
+    if (pf_sub != nullptr) {
+      if (__builtin_amdgcn_readfirstlane(rdy[0]) != 0) {
+        pre.load();
+      } else if (__hip_atomic_load(pf_sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+        // missed by the earlier polls: each wave polls once more and loads its
+        // share; the prefetch counts only if all three saw the tile (bits in
+        // rdy[3]; otherwise the walker reloads it whole)
+        pre.load();
+        if (lane == 0) __hip_atomic_fetch_or(&rdy[3], 1 << w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
     // row 2 of W, then the sums of row 3 (wave w: column block J = w - 1).
     // W_20 is formed by wave 3 (its own row-3 sum is one product) and handed
     // to wave 1 by an LDS flag: wave 1 forms its sum's K = 0, 1 products
@@ -1147,7 +1160,7 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     const bool bad = (j0 + NB <= n) ? potrf_tile<true>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre)
                                     : potrf_tile<false>(T, Wl, scr, j0, n, dl, fsub, fdiag, epoch, rdy, pre);
     if (bad) atomicOr(fail, 1);
-    const bool early = more && __builtin_amdgcn_readfirstlane(rdy[0]) != 0;
+    const bool early = more && (__builtin_amdgcn_readfirstlane(rdy[0]) != 0 || __builtin_amdgcn_readfirstlane(rdy[3]) == 14);
     const bool diag_out = next && __builtin_amdgcn_readfirstlane(rdy[1]) != 0;
     // the prefetched subdiagonal tile into Tn (waves 1-3)
     if (early && w >= 1) pre.store();
@@ -1157,11 +1170,9 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     // went out from the POTRF's last phase (wave 0), row 3 here
     w_st_row3(Winv + size_t(j) * NB * NB, Wl);
     WSTAMP(j, 10);
-    // W_j out at once: the helpers' TRSMs of column j feed the last updates
-    // of the diagonal tiles two steps ahead (a chain as long as a step)
-    block_publish_wt(F + j * nb + j, epoch);
     WSTAMP(j, 11);
     if (!more) {
+      block_publish_wt(F + j * nb + j, epoch);
       // L_jj is read by nobody (the helpers' TRSMs and the back substitution
       // use W_j; the next Schur pass rewrites the lower triangle) except in
       // the tile that holds the augmented row n -- the last one: its z
@@ -1194,7 +1205,10 @@ __device__ __forceinline__ void fused_walker(double* __restrict__ A, int ld, int
     f64x4 x[4];
     trsm_lds(Tn, Wl, x, lane);
     put_tile(Ls, x, lane);
-    __syncthreads();
+    // W_j's flag: its stores drained under the TRSM (the helpers' TRSMs of
+    // column j feed the diagonal tiles two steps ahead, which have the slack:
+    // P(j+1,j) lands ~4.5 us before the walker needs it)
+    block_publish_wt(F + j * nb + j, epoch);
     WSTAMP(j, 13);
     if (next) {
       // the next step's column-block-0 update products (its MFMAs run while
