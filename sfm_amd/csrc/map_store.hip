@@ -237,8 +237,9 @@ struct DVec {
 
 }  // namespace
 // match_kernels.hip
-int matcher_match_current(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
-                          const int32_t* train_idx, int n1, double ratio, double mn, double mx, int** res);
+int matcher_match_current_dev(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
+                              const int32_t* d_train_idx, int n1, double ratio, double mn, double mx, int** res);
+int matcher_current_n(const sfm_matcher* h);
 int matcher_words(const sfm_matcher* h);
 int matcher_device(const sfm_matcher* h);
 }  // namespace sfm
@@ -748,6 +749,10 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
   if (matcher_words(mt) != h->W || matcher_device(mt) != h->device)
     return mapfail(SFM_EINVAL, "the map and the matcher differ in descriptor width or device");
   if (int rc = check_pts(h, n_existing, existing_pts)) return rc;
+  const int n_cur = matcher_current_n(mt);
+  if (n_cur < 0) return mapfail(SFM_EINVAL, "push the current frame to the matcher first");
+  for (int i = 0; i < n_train; ++i)
+    if (train_idx[i] < 0 || train_idx[i] >= n_cur) return mapfail(SFM_EINVAL, "train index out of range");
   if (n_frames == 0 || h->n_pts == 0 || h->ob_pt.n == 0 || n_train < 2) return 0;
   if (hipSetDevice(h->device) != hipSuccess) return mapfail(SFM_ENODEV, "hipSetDevice failed");
   int rc = 0;
@@ -759,27 +764,31 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
     if (int r = build_csr(h, "de", h->desc_pt.p, h->desc.n / h->W, &h->drow, &h->doff)) return r;
     h->dcsr = true;
   }
-  auto* fset = static_cast<int32_t*>(scratch(h, "fset", sizeof(int32_t) * (fs.size() + size_t(n_existing)), &rc));
+  const size_t n_up = fs.size() + size_t(n_existing) + size_t(n_train);
+  auto* fset = static_cast<int32_t*>(scratch(h, "fset", sizeof(int32_t) * n_up, &rc));
   auto* mark = static_cast<uint8_t*>(scratch(h, "mark", size_t(P), &rc));
-  auto* out = static_cast<int32_t*>(scratch(h, "pout", sizeof(int32_t) * size_t(P), &rc));
+  // the selected points, then (after k_map_repr) their representative rows:
+  // one download for both
+  auto* out = static_cast<int32_t*>(scratch(h, "pout", sizeof(int32_t) * 2 * size_t(P), &rc));
   auto* dn = static_cast<int32_t*>(scratch(h, "pn", sizeof(int32_t), &rc));
   if (rc) return rc;
-  if (h->pin_cap < 2 * size_t(P) + 1) {
+  if (h->pin_cap < std::max(2 * size_t(P) + 1, n_up)) {
     if (h->pin) { (void)hipStreamSynchronize(h->s); (void)hipHostFree(h->pin); }
     h->pin = nullptr;
     h->pin_cap = 0;
-    const size_t cap = std::max<size_t>(2 * size_t(P) + 1, 8192) * 3 / 2;
+    const size_t cap = std::max<size_t>(std::max(2 * size_t(P) + 1, n_up), 8192) * 3 / 2;
     if (hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int32_t) * cap) != hipSuccess)
       return mapfail(SFM_ENOMEM, "hipHostMalloc failed");
     h->pin_cap = cap;
   }
   if (!h->ev && hipEventCreateWithFlags(&h->ev, hipEventDisableTiming) != hipSuccess)
     return mapfail(SFM_EIO, "hipEventCreate failed");
-  // frames + the frame's matched points in one upload
+  // frames, the frame's matched points and the train subset in one upload
   (void)hipStreamSynchronize(h->s);  // (the pinned block may feed an earlier copy)
   std::memcpy(h->pin, fs.data(), sizeof(int32_t) * fs.size());
   if (n_existing) std::memcpy(h->pin + fs.size(), existing_pts, sizeof(int32_t) * size_t(n_existing));
-  (void)hipMemcpyAsync(fset, h->pin, sizeof(int32_t) * (fs.size() + size_t(n_existing)), hipMemcpyHostToDevice, h->s);
+  std::memcpy(h->pin + fs.size() + n_existing, train_idx, sizeof(int32_t) * size_t(n_train));
+  (void)hipMemcpyAsync(fset, h->pin, sizeof(int32_t) * n_up, hipMemcpyHostToDevice, h->s);
   (void)hipMemsetAsync(mark, 0, size_t(P), h->s);
   k_mark_frames<<<grid(h->ob_pt.n), 256, 0, h->s>>>(h->ob_pt.n, h->ob_pt.p, h->ob_frame.p, fset, int(fs.size()), mark);
   if (n_existing) k_unmark<<<grid(n_existing), 256, 0, h->s>>>(n_existing, fset + fs.size(), mark);
@@ -795,7 +804,7 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
   const int n_new = h->pin[0];
   if (n_new == 0) return 0;
   // the queries: representative descriptors and projections of the new points
-  auto* best = static_cast<int32_t*>(scratch(h, "mb", sizeof(int32_t) * size_t(n_new), &rc));
+  int32_t* best = out + n_new;
   auto* qd = static_cast<uint64_t*>(scratch(h, "mq", sizeof(uint64_t) * size_t(n_new) * h->W, &rc));
   auto* uv = static_cast<double*>(scratch(h, "muv", sizeof(double) * 2 * size_t(n_new), &rc));
   if (rc) return rc;
@@ -807,12 +816,11 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
   }
   k_project<<<grid(n_new), 256, 0, h->s>>>(n_new, out, h->X.p, R9[0], R9[1], R9[2], R9[3], R9[4], R9[5], R9[6], R9[7],
                                            R9[8], t3[0], t3[1], t3[2], K9[0], K9[4], K9[2], K9[5], uv);
-  (void)hipMemcpyAsync(h->pin, out, sizeof(int32_t) * size_t(n_new), hipMemcpyDeviceToHost, h->s);
-  (void)hipMemcpyAsync(h->pin + n_new, best, sizeof(int32_t) * size_t(n_new), hipMemcpyDeviceToHost, h->s);
+  (void)hipMemcpyAsync(h->pin, out, sizeof(int32_t) * 2 * size_t(n_new), hipMemcpyDeviceToHost, h->s);
   if (hipEventRecord(h->ev, h->s) != hipSuccess) return mapfail(SFM_EIO, "hipEventRecord failed");
   int* res = nullptr;
-  if ((rc = matcher_match_current(mt, h->ev, qd, uv, n_new, train_idx, n_train, ratio_test, min_distance,
-                                  max_distance, &res)))
+  if ((rc = matcher_match_current_dev(mt, h->ev, qd, uv, n_new, fset + fs.size() + n_existing, n_train, ratio_test,
+                                      min_distance, max_distance, &res)))
     return rc;
   if (int r = sync(h)) return r;
   for (int i = 0; i < n_new; ++i)

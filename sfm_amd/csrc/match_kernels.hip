@@ -236,9 +236,9 @@ __global__ __launch_bounds__(64) void k_repr(const uint64_t* __restrict__ d, con
 
 struct MatchFrame {
   int n = 0;
-  uint64_t* desc = nullptr;   // [n][W]
-  double* pts = nullptr;      // [n][2] undistorted (CFrame::getPointsAt)
-  double* ptsd = nullptr;     // [n][2] distorted (CFrame::getPointsDistorted)
+  uint64_t* desc = nullptr;   // [n][W]; one allocation with the two below
+  double* pts = nullptr;      // [n][2] undistorted (CFrame::getPointsAt), right after desc
+  double* ptsd = nullptr;     // [n][2] distorted (CFrame::getPointsDistorted), right after pts
   size_t cap = 0;
 };
 
@@ -366,26 +366,19 @@ namespace sfm {
 // For sfm_map_match_frame (map_store.hip): queries already on the device
 // (descriptor words q, positions p0; produced on another stream, ordered
 // after the event `after`) against a subset of the CURRENT frame's keypoints
-// (train_idx, host, frame-local); the (query, train) pairs in subset-local
-// indices, as sfm_matcher_match returns them, in *res (pinned, valid after
-// this call).
-int matcher_match_current(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
-                          const int32_t* train_idx, int n1, double ratio, double mn, double mx, int** res) {
+// (d_train_idx, frame-local, on the device, checked by the caller against
+// matcher_current_n); the (query, train) pairs in subset-local indices, as
+// sfm_matcher_match returns them, in *res (pinned, valid after this call).
+// No upload and no synchronisation before the kernels.
+int matcher_match_current_dev(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
+                              const int32_t* d_train_idx, int n1, double ratio, double mn, double mx, int** res) {
   if (h->frames_pushed < 1) return mfail(SFM_EINVAL, "push the current frame first");
-  const MatchFrame& fc = h->frame[h->cur];
-  for (int i = 0; i < n1; ++i)
-    if (train_idx[i] < 0 || train_idx[i] >= fc.n) return mfail(SFM_EINVAL, "train index out of range");
   if (!ok_ratio_window(ratio, mn, mx)) return mfail(SFM_EINVAL, "non-finite threshold");
-  int rc = 0;
-  int* ix = pbuf<int>(h, "idx", size_t(n1), &rc);
-  int* dix = dbuf<int>(h, "didx", size_t(n1), &rc);
-  if (rc) return rc;
-  hipStreamSynchronize(h->stream);  // (the pinned index stage may feed an earlier copy)
-  std::memcpy(ix, train_idx, sizeof(int) * size_t(n1));
-  hipMemcpyAsync(dix, ix, sizeof(int) * size_t(n1), hipMemcpyHostToDevice, h->stream);
+  const MatchFrame& fc = h->frame[h->cur];
   if (after && hipStreamWaitEvent(h->stream, after, 0) != hipSuccess) return mfail(SFM_EIO, "stream wait failed");
-  return run_match(h, q, nullptr, p0, n0, fc.desc, dix, fc.pts, n1, ratio, mn, mx, res);
+  return run_match(h, q, nullptr, p0, n0, fc.desc, d_train_idx, fc.pts, n1, ratio, mn, mx, res);
 }
+int matcher_current_n(const sfm_matcher* h) { return h->frames_pushed < 1 ? -1 : h->frame[h->cur].n; }
 int matcher_words(const sfm_matcher* h) { return h->W; }
 int matcher_device(const sfm_matcher* h) { return h->device; }
 }  // namespace sfm
@@ -422,8 +415,6 @@ int sfm_matcher_destroy(sfm_matcher* h) {
   hipStreamSynchronize(h->stream);
   for (auto& f : h->frame) {
     hipFree(f.desc);
-    hipFree(f.pts);
-    hipFree(f.ptsd);
   }
   for (auto& kv : h->dev) hipFree(kv.second.first);
   for (auto& kv : h->pin) hipHostFree(kv.second.first);
@@ -444,16 +435,18 @@ int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_
   int rc = 0;
   if (f.cap < size_t(std::max(n, 1))) {
     hipStreamSynchronize(h->stream);
-    hipFree(f.desc); hipFree(f.pts); hipFree(f.ptsd);
+    hipFree(f.desc);
     f.desc = nullptr; f.pts = f.ptsd = nullptr;
     f.cap = size_t(std::max(n, 1024)) * 3 / 2;
-    if (hipMalloc(&f.desc, f.cap * h->W * 8) != hipSuccess || hipMalloc(&f.pts, f.cap * 16) != hipSuccess ||
-        hipMalloc(&f.ptsd, f.cap * 16) != hipSuccess) {
+    if (hipMalloc(&f.desc, f.cap * (h->W * 8 + 32)) != hipSuccess) {
       f.cap = 0;
       return mfail(SFM_ENOMEM, "hipMalloc failed (matcher frame)");
     }
   }
   f.n = n;
+  // [desc n W | pts 2n | ptsd 2n] as laid out in the stage: one copy
+  f.pts = reinterpret_cast<double*>(f.desc + size_t(n) * h->W);
+  f.ptsd = f.pts + 2 * size_t(n);
   if (n) {
     // staging: one pinned block per frame slot (the previous upload from it
     // may still be in flight only for the other slot)
@@ -466,9 +459,7 @@ int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_
     double* sp = reinterpret_cast<double*>(st + words);
     std::memcpy(sp, pts, 16 * size_t(n));
     std::memcpy(sp + 2 * size_t(n), pts_distorted ? pts_distorted : pts, 16 * size_t(n));
-    hipMemcpyAsync(f.desc, st, words * 8, hipMemcpyHostToDevice, h->stream);
-    hipMemcpyAsync(f.pts, sp, 16 * size_t(n), hipMemcpyHostToDevice, h->stream);
-    hipMemcpyAsync(f.ptsd, sp + 2 * size_t(n), 16 * size_t(n), hipMemcpyHostToDevice, h->stream);
+    hipMemcpyAsync(f.desc, st, words * 8 + 32 * size_t(n), hipMemcpyHostToDevice, h->stream);
   }
   ++h->frames_pushed;
   return 0;
