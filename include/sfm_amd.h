@@ -341,6 +341,24 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
                         double max_distance, int32_t capacity, int32_t* pts3d_match, int32_t* train_match,
                         int32_t* n_matches);
 
+/* CSfM::tracking's pose step (CSfM.cpp:533-565) in one call, replacing
+ * matchFeatures(prevIdx, currIdx) + map->getPointsAtIdx + cv::solvePnPRansac:
+ * the previous frame's keypoints with a map point (prev_pt3d[n_prev], one
+ * entry per keypoint of the frame pushed before the current one, -1 = none)
+ * matched against every keypoint of the current frame of `mt` (undistorted
+ * positions; the reference's (ratio, min, max) = (0.8, 1.5, 40)), their map
+ * points and keypoints gathered on the device and cv::solvePnPRansac run on
+ * them (K9 row-major; the reference's (20, _maxReprErr, 0.99)), with one
+ * upload, one download and one host synchronisation.  *n_matches: the match
+ * count; below min_matches (MIN_FEATURES, CSfM.cpp:545) no PnP runs and
+ * *found = 0.  Found: rvec/tvec and the inliers as (current keypoint,
+ * map point) pairs, *n_inliers of them (capacity >= the number of
+ * prev_pt3d entries >= 0).  Not found: rvec = tvec = 0, no inliers. */
+int sfm_track_pnp(sfm_matcher* mt, sfm_map* map, int32_t n_prev, const int32_t* prev_pt3d, double ratio_test,
+                  double min_distance, double max_distance, int32_t min_matches, const double* K9, int32_t iterations,
+                  double reproj_err, double confidence, double* rvec, double* tvec, int32_t* found,
+                  int32_t* n_matches, int32_t capacity, int32_t* inl_kp, int32_t* inl_pt3d, int32_t* n_inliers);
+
 /* BRISK descriptor (CTracker::detectFeatures' _descriptor->compute,
  * CTracker.cpp:284): BRISK as published in its
  * reference implementation's form (oracle/brisk_oracle.py; the reference's

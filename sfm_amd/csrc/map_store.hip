@@ -837,3 +837,15 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
 }
 
 }  // extern "C"
+
+namespace sfm {
+// The device copy of the map's points for sfm_track_pnp, which reads it on
+// the matcher's stream: the map stream is drained first (its calls already
+// synchronise before returning; this keeps the rule local).
+const double* map_points_dev(sfm_map* h, int32_t* n_pts, int* device) {
+  (void)hipStreamSynchronize(h->s);
+  *n_pts = h->n_pts;
+  *device = h->device;
+  return h->X.p;
+}
+}  // namespace sfm

@@ -324,8 +324,10 @@ int launch_knn(sfm_matcher* h, const uint64_t* q, const int* qidx, int n0, const
 // One match: queries (q, qidx, p0) against trains (tr, tidx, p1) already on
 // the device; results (query, train) in subset-local indices into the pinned
 // buffer `res` ([2 * n0 + 1]: idx0 | idx1 | count) after the stream sync.
-int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
-              const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** res_out) {
+// The kernels alone (no download, no synchronisation): the (query, train)
+// pairs and their count land in the device buffer *out_dev ([2 n0 + 1]).
+int run_match_async(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
+                    const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** out_dev) {
   int rc = 0;
   const int nslice = slices_for(h, n0, n1);
   auto* part = dbuf<unsigned long long>(h, "part", 2 * size_t(n0) * nslice, &rc);
@@ -333,7 +335,6 @@ int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* 
   int* first = dbuf<int>(h, "first", size_t(n1), &rc);
   int* slot = dbuf<int>(h, "slot", size_t(n0), &rc);
   int* out = dbuf<int>(h, "out", 2 * size_t(n0) + 1, &rc);
-  int* res = pbuf<int>(h, "res", 2 * size_t(n0) + 1, &rc);
   if (rc) return rc;
   hipStream_t s = h->stream;
   hipEventRecord(h->ev[0], s);
@@ -344,12 +345,47 @@ int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* 
   sfm::k_mark_first<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
   sfm::k_compact_slots<false><<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
   hipEventRecord(h->ev[2], s);
+  *out_dev = out;
+  return 0;
+}
+
+int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
+              const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** res_out) {
+  int rc = 0;
+  int* res = pbuf<int>(h, "res", 2 * size_t(n0) + 1, &rc);
+  if (rc) return rc;
+  int* out = nullptr;
+  if ((rc = run_match_async(h, q, qidx, p0, n0, tr, tidx, p1, n1, ratio, mn, mx, &out))) return rc;
+  hipStream_t s = h->stream;
   hipMemcpyAsync(res, out, (2 * size_t(n0) + 1) * sizeof(int), hipMemcpyDeviceToHost, s);
   if (hipStreamSynchronize(s) != hipSuccess) return mfail(SFM_EIO, "matcher kernels failed");
   hipEventElapsedTime(&h->last_knn_ms, h->ev[0], h->ev[1]);
   hipEventElapsedTime(&h->last_total_ms, h->ev[0], h->ev[2]);
   *res_out = res;
   return 0;
+}
+
+// sfm_track_pnp: the matches (query k -> prev keypoint pidx[out[k]], its map
+// point pt3d[.]; train -> current keypoint out[n0 + k]) into PnP's object
+// (the map point) and image (the current keypoint) arrays, with the match's
+// map point and keypoint kept for the inlier lists; thread 0 copies the count
+// into the result block's head.
+__global__ void k_track_gather(const int* __restrict__ out, int n0, const int* __restrict__ pidx,
+                               const int* __restrict__ pt3d, const double* __restrict__ X,
+                               const double* __restrict__ pts, double* __restrict__ obj, double* __restrict__ img,
+                               int* __restrict__ m3, int* __restrict__ kp, int* __restrict__ head) {
+  const int m = out[2 * n0];
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 0) head[0] = m;
+  if (k >= m) return;
+  const int p = pt3d[pidx[out[k]]], c = out[n0 + k];
+  obj[3 * k] = X[3 * size_t(p)];
+  obj[3 * k + 1] = X[3 * size_t(p) + 1];
+  obj[3 * k + 2] = X[3 * size_t(p) + 2];
+  img[2 * k] = pts[2 * c];
+  img[2 * k + 1] = pts[2 * c + 1];
+  m3[k] = p;
+  kp[k] = c;
 }
 
 bool ok_ratio_window(double ratio, double mn, double mx) {
@@ -363,6 +399,13 @@ extern "C" {
 }  // extern "C"
 
 namespace sfm {
+// pnp_kernels.hip / map_store.hip (sfm_track_pnp)
+int pnp_ransac_dev(hipStream_t s, const int* d_n, int gate, const double* d_obj, const double* d_img, const double* K9,
+                   int iterations, double reproj_err, double confidence, int* d_sub, double* d_model, int* d_cnt,
+                   int* d_res, int* d_inl);
+int pnp_max_iters();
+int pnp_model_size();
+const double* map_points_dev(sfm_map* h, int32_t* n_pts, int* device);
 // For sfm_map_match_frame (map_store.hip): queries already on the device
 // (descriptor words q, positions p0; produced on another stream, ordered
 // after the event `after`) against a subset of the CURRENT frame's keypoints
@@ -678,4 +721,94 @@ int sfm_representative_descriptors(int32_t device, const uint8_t* desc, const in
   return 0;
 }
 
+
+// CSfM::tracking's pose step (CSfM.cpp:533-565) as one call: the previous
+// frame's keypoints with a map point (prev_pt3d[i] >= 0) matched against the
+// whole current frame (matchFeatures(prevIdx, currIdx), CTracker.cpp:368-417),
+// their map points and keypoints gathered on the device, and
+// cv::solvePnPRansac on them (sfm_pnp_ransac's kernels) -- one upload, one
+// download, one synchronisation.  Fewer than min_matches matches: no PnP
+// (*found = 0; the caller's lost-tracking branch, CSfM.cpp:545-551).  Outputs:
+// *n_matches, the pose (rvec, tvec; zero when not found) and the inliers as
+// (current keypoint, map point) pairs.
+int sfm_track_pnp(sfm_matcher* h, sfm_map* map, int32_t n_prev, const int32_t* prev_pt3d, double ratio_test,
+                  double min_distance, double max_distance, int32_t min_matches, const double* K9, int32_t iterations,
+                  double reproj_err, double confidence, double* rvec, double* tvec, int32_t* found,
+                  int32_t* n_matches, int32_t capacity, int32_t* inl_kp, int32_t* inl_pt3d, int32_t* n_inliers) {
+  if (!h || !map || !found || !n_matches || !n_inliers || !rvec || !tvec || !K9) return mfail(SFM_EINVAL, "NULL argument");
+  *found = 0;
+  *n_matches = 0;
+  *n_inliers = 0;
+  for (int i = 0; i < 3; ++i) rvec[i] = tvec[i] = 0.0;
+  if (h->frames_pushed < 2) return mfail(SFM_EINVAL, "push the previous and the current frame first");
+  if (!ok_ratio_window(ratio_test, min_distance, max_distance)) return mfail(SFM_EINVAL, "non-finite threshold");
+  if (iterations < 0 || iterations > sfm::pnp_max_iters()) return mfail(SFM_EINVAL, "bad iterations");
+  if (!(confidence > 0.0 && confidence < 1.0)) return mfail(SFM_EINVAL, "confidence must lie in (0, 1)");
+  const MatchFrame& fp = h->frame[h->cur ^ 1];
+  const MatchFrame& fc = h->frame[h->cur];
+  if (n_prev != fp.n || (n_prev && !prev_pt3d)) return mfail(SFM_EINVAL, "prev_pt3d must hold one entry per previous keypoint");
+  int32_t P = 0;
+  int mdev = 0;
+  const double* X = sfm::map_points_dev(map, &P, &mdev);
+  if (mdev != h->device) return mfail(SFM_EINVAL, "the map and the matcher are on different devices");
+  std::vector<int32_t> pidx;
+  pidx.reserve(size_t(n_prev));
+  for (int32_t i = 0; i < n_prev; ++i) {
+    if (prev_pt3d[i] >= P) return mfail(SFM_EINVAL, "map point index out of range");
+    if (prev_pt3d[i] >= 0) pidx.push_back(i);
+  }
+  const int n0 = int(pidx.size()), n1 = fc.n;
+  if (n0 == 0 || n1 < 2) return 0;  // (as sfm_matcher_match_subset: no matches)
+  if (capacity < n0) return mfail(SFM_EINVAL, "capacity below the previous frame's matched keypoints");
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int rc = 0;
+  const int iters = iterations > 0 ? iterations : 1;
+  const size_t n_up = size_t(n0) + size_t(n1) + size_t(n_prev);
+  int* ix = pbuf<int>(h, "tidx", n_up, &rc);
+  int* dix = dbuf<int>(h, "dtidx", n_up, &rc);
+  // result block (ints): count, (pad x3) | found, best, inliers, pad | model
+  // (6 doubles) | inliers [n0] | map points [n0] | keypoints [n0]
+  const size_t blk = 8 + 12 + 3 * size_t(n0);
+  int* dblk = dbuf<int>(h, "tblk", blk, &rc);
+  int* hblk = pbuf<int>(h, "tblkh", blk, &rc);
+  double* dobj = dbuf<double>(h, "tobj", 5 * size_t(n0), &rc);
+  int* dsub = dbuf<int>(h, "tsub", size_t(sfm::pnp_model_size()) * iters, &rc);
+  double* dmodel = dbuf<double>(h, "tmodel", 6 * size_t(iters), &rc);
+  int* dcnt = dbuf<int>(h, "tcnt", size_t(iters), &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);  // (the pinned stage may feed an earlier copy)
+  std::memcpy(ix, pidx.data(), sizeof(int) * size_t(n0));
+  for (int i = 0; i < n1; ++i) ix[n0 + i] = i;  // the whole current frame (currIdx)
+  if (n_prev) std::memcpy(ix + n0 + n1, prev_pt3d, sizeof(int) * size_t(n_prev));
+  hipMemcpyAsync(dix, ix, sizeof(int) * n_up, hipMemcpyHostToDevice, h->stream);
+  int* out = nullptr;
+  // undistorted positions (CFrame::getPointsAt, CTracker.cpp:375-376)
+  if ((rc = run_match_async(h, fp.desc, dix, fp.pts, n0, fc.desc, dix + n0, fc.pts, n1, ratio_test, min_distance,
+                            max_distance, &out)))
+    return rc;
+  int* inl = dblk + 20;
+  int* m3 = inl + n0;
+  int* kp = m3 + n0;
+  k_track_gather<<<(n0 + 255) / 256, 256, 0, h->stream>>>(out, n0, dix, dix + n0 + n1, X, fc.pts, dobj,
+                                                          dobj + 3 * size_t(n0), m3, kp, dblk);
+  if ((rc = sfm::pnp_ransac_dev(h->stream, dblk, min_matches, dobj, dobj + 3 * size_t(n0), K9, iterations, reproj_err,
+                           confidence, dsub, dmodel, dcnt, dblk + 4, inl)))
+    return rc;
+  hipMemcpyAsync(hblk, dblk, sizeof(int) * blk, hipMemcpyDeviceToHost, h->stream);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return mfail(SFM_EIO, "tracking kernels failed");
+  const int m = hblk[0];
+  *n_matches = m;
+  if (m < min_matches || !hblk[4]) return 0;
+  const double* mdl = reinterpret_cast<const double*>(hblk + 8);
+  for (int i = 0; i < 3; ++i) { rvec[i] = mdl[i]; tvec[i] = mdl[3 + i]; }
+  const int ni = hblk[6];
+  const int* hin = hblk + 20;
+  for (int i = 0; i < ni; ++i) {
+    inl_kp[i] = hblk[20 + 2 * n0 + hin[i]];
+    inl_pt3d[i] = hblk[20 + n0 + hin[i]];
+  }
+  *n_inliers = ni;
+  *found = 1;
+  return 0;
+}
 }  // extern "C"

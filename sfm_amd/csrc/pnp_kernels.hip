@@ -866,8 +866,15 @@ __host__ __device__ void epnp5(const EpnpIn& in, const PnPCam& k, double* lds, d
 }
 
 // cv::RNG(uint64(-1)) subsets of the whole iteration bound (one thread).
-__global__ void k_pnp_subsets(int n, int iters, int* __restrict__ sub) {
+// nd: the point count on the device (sfm_track_pnp; n otherwise), below
+// `gate` no model is sought (zero subsets keep the later kernels in bounds).
+__global__ void k_pnp_subsets(int n_arg, const int* __restrict__ nd, int gate, int iters, int* __restrict__ sub) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int n = nd ? *nd : n_arg;
+  if (n < gate) {
+    for (int i = 0; i < iters * kModel; ++i) sub[i] = 0;
+    return;
+  }
   uint64_t state = ~0ull;
   auto next = [&]() -> unsigned { return cv_rng_next(state); };
   for (int it = 0; it < iters; ++it) {
@@ -955,10 +962,11 @@ __device__ __forceinline__ bool pnp_inlier(const double* __restrict__ obj, const
   return e <= thr;
 }
 
-__global__ __launch_bounds__(256) void k_pnp_count(int n, const double* __restrict__ obj,
+__global__ __launch_bounds__(256) void k_pnp_count(int n_arg, const int* __restrict__ nd, const double* __restrict__ obj,
                                                    const double* __restrict__ img, const double* __restrict__ model,
                                                    PnPCam k, float thr, int* __restrict__ cnt) {
   __shared__ int sh[4];
+  const int n = nd ? *nd : n_arg;
   const int it = blockIdx.x;
   double R[9], t[3];
   rodrigues_v2m(model + 6 * it, R);
@@ -975,11 +983,17 @@ __global__ __launch_bounds__(256) void k_pnp_count(int n, const double* __restri
 // Replay of RANSACPointSetRegistrator::run's acceptance over the counts, then
 // the winner's inliers in index order.  One wave.  res: [0] found, [1] best
 // iteration, [2] inlier count.
-__global__ __launch_bounds__(64) void k_pnp_select(int n, int iters, double confidence,
-                                                   const double* __restrict__ obj, const double* __restrict__ img,
-                                                   const double* __restrict__ model, const int* __restrict__ cnt,
-                                                   PnPCam k, float thr, int* __restrict__ res, int* __restrict__ inl) {
+__global__ __launch_bounds__(64) void k_pnp_select(int n_arg, const int* __restrict__ nd, int gate, int iters,
+                                                   double confidence, const double* __restrict__ obj,
+                                                   const double* __restrict__ img, const double* __restrict__ model,
+                                                   const int* __restrict__ cnt, PnPCam k, float thr,
+                                                   int* __restrict__ res, int* __restrict__ inl) {
   const int lane = threadIdx.x;
+  const int n = nd ? *nd : n_arg;
+  if (n < gate) {
+    if (lane == 0) { res[0] = 0; res[1] = -1; res[2] = 0; }
+    return;
+  }
   int best = -1, max_good = 0;
   int niters = iters > 1 ? iters : 1;
   for (int it = 0; it < niters && it < iters; ++it) {
@@ -1054,6 +1068,32 @@ int pfail(int code, const char* msg) {
 }  // namespace
 }  // namespace sfm
 
+namespace sfm {
+// cv::solvePnPRansac on points already on the device, their count at d_n
+// (device; below `gate` no model: found = 0), launched on stream s without
+// a synchronisation (sfm_track_pnp).  Scratch from the caller: d_sub
+// [kModel kMaxIters], d_model [6 kMaxIters], d_cnt [kMaxIters]; result block
+// d_res: found, best iteration, inlier count, (pad) | the model (6 doubles,
+// 16-B aligned) | then d_inl [n_cap] the inliers' indices.
+int pnp_ransac_dev(hipStream_t s, const int* d_n, int gate, const double* d_obj, const double* d_img, const double* K9,
+                   int iterations, double reproj_err, double confidence, int* d_sub, double* d_model, int* d_cnt,
+                   int* d_res, int* d_inl) {
+  if (iterations < 0 || iterations > kMaxIters) return pfail(SFM_EINVAL, "bad iterations");
+  if (!(confidence > 0.0 && confidence < 1.0)) return pfail(SFM_EINVAL, "confidence must lie in (0, 1)");
+  const PnPCam k{K9[0], K9[4], K9[2], K9[5]};
+  const int iters = iterations > 0 ? iterations : 1;
+  const float thr = float(reproj_err * reproj_err);
+  gate = gate > kModel ? gate : kModel;
+  k_pnp_subsets<<<1, 64, 0, s>>>(0, d_n, gate, iters, d_sub);
+  k_pnp_epnp<<<iters, 192, 0, s>>>(d_obj, d_img, d_sub, k, d_model);
+  k_pnp_count<<<iters, 256, 0, s>>>(0, d_n, d_obj, d_img, d_model, k, thr, d_cnt);
+  k_pnp_select<<<1, 64, 0, s>>>(0, d_n, gate, iters, confidence, d_obj, d_img, d_model, d_cnt, k, thr, d_res, d_inl);
+  return hipGetLastError() == hipSuccess ? 0 : pfail(SFM_EIO, "PnP launch failed");
+}
+int pnp_max_iters() { return kMaxIters; }
+int pnp_model_size() { return kModel; }
+}  // namespace sfm
+
 using namespace sfm;
 
 extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, const double* img, const double* K9,
@@ -1123,13 +1163,14 @@ extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, cons
   // the subsets depend on (n, iterations) alone (cv::RNG(-1) restarted per
   // call): drawn once per pair, then reused
   if (c->sub_n != n || c->sub_iters != iters) {
-    k_pnp_subsets<<<1, 64, 0, s>>>(n, iters, c->sub);
+    k_pnp_subsets<<<1, 64, 0, s>>>(n, nullptr, kModel, iters, c->sub);
     c->sub_n = n;
     c->sub_iters = iters;
   }
   k_pnp_epnp<<<iters, 192, 0, s>>>(c->obj, c->img, c->sub, k, c->model);
-  k_pnp_count<<<iters, 256, 0, s>>>(n, c->obj, c->img, c->model, k, thr, c->cnt);
-  k_pnp_select<<<1, 64, 0, s>>>(n, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr, c->out, c->inl);
+  k_pnp_count<<<iters, 256, 0, s>>>(n, nullptr, c->obj, c->img, c->model, k, thr, c->cnt);
+  k_pnp_select<<<1, 64, 0, s>>>(n, nullptr, kModel, iters, confidence, c->obj, c->img, c->model, c->cnt, k, thr,
+                                c->out, c->inl);
   // ONE download: counts, model and (up to n) inliers
   const size_t down = kOutHead + (inliers ? sizeof(int) * size_t(n) : 0);
   if (hipMemcpyAsync(pin_out, c->out, down, hipMemcpyDeviceToHost, s) != hipSuccess ||

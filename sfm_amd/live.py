@@ -37,6 +37,7 @@ culling (CSfM.cpp:232-246) are not restated.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -222,7 +223,11 @@ class LiveSfM:
         self.stats = {"frames": 0, "tracked": 0, "pnp_inliers": 0, "map_matches": 0, "new_points": 0}
         self.times = {"stream": 0.0, "track": 0.0, "map_match": 0.0, "mapping": 0.0, "ba": 0.0}
         self._pending: _Frame | None = None
-        self.fused_find = True
+        # the fused device calls (SFM_LIVE_COMPOSED=1: the composed calls,
+        # for A/B timing; the tests compare both forms)
+        composed = os.environ.get("SFM_LIVE_COMPOSED") == "1"
+        self.fused_find = not composed
+        self.fused_track = not composed
 
     # ---- driver --------------------------------------------------------------
     def run(self, n_frames: int) -> None:
@@ -275,22 +280,31 @@ class LiveSfM:
         t0 = time.perf_counter()
         cur = _Frame(k, pts, desc)
         self.matcher.push_frame(pts, desc)
-        prev_idx = np.flatnonzero(self.prev.pt3d >= 0).astype(np.int32)
-        pm, cm = self.matcher.match_subset(prev_idx, np.arange(len(pts), dtype=np.int32))
-        if len(cm) < MIN_FEATURES:
+        if self.fused_track:
+            # matchFeatures + getPointsAtIdx + solvePnPRansac in one device call
+            # (sfm_track_pnp); the composed form below is the test's reference
+            nm, found, r, t, ikp, ipt = self.matcher.track_pnp(self.map, self.prev.pt3d, self.K, MIN_FEATURES, 20,
+                                                               MAX_REPR_ERR, 0.99)
+        else:
+            prev_idx = np.flatnonzero(self.prev.pt3d >= 0).astype(np.int32)
+            pm, cm = self.matcher.match_subset(prev_idx, np.arange(len(pts), dtype=np.int32))
+            nm = len(cm)
+        if nm < MIN_FEATURES:
             # lost: keep matching against the previous frame (no swap)
             self.lost += 1
             self.matcher.push_frame(self.prev.pts, self.prev.desc)
             self.times["track"] += time.perf_counter() - t0
             return
         self.lost = 0
-        m3 = self.prev.pt3d[pm]
-        obj = self.map.getPointsAtIdx(m3)
-        found, r, t, inl = solvePnPRansac(obj, pts[cm], self.K, 20, MAX_REPR_ERR, 0.99, device=self.device)
+        if not self.fused_track:
+            m3 = self.prev.pt3d[pm]
+            obj = self.map.getPointsAtIdx(m3)
+            found, r, t, inl = solvePnPRansac(obj, pts[cm], self.K, 20, MAX_REPR_ERR, 0.99, device=self.device)
+            ikp, ipt = cm[inl], m3[inl]
         cur.rot, cur.t = np.asarray(r, float), np.asarray(t, float)
-        cur.pt3d[cm[inl]] = m3[inl]
+        cur.pt3d[ikp] = ipt
         self.stats["tracked"] += 1
-        self.stats["pnp_inliers"] += len(inl)
+        self.stats["pnp_inliers"] += len(ikp)
         t1 = time.perf_counter()
         self.times["track"] += t1 - t0
         self._find_map_points(cur)

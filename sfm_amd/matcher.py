@@ -83,6 +83,26 @@ class FeatureMatcher:
               "sfm_matcher_match_subset")
         return o0[:nm.value].copy(), o1[:nm.value].copy()
 
+    def track_pnp(self, device_map, prev_pt3d, K, min_matches: int, iterations: int = 20, reproj_err: float = 7.0,
+                  confidence: float = 0.99, ratio=RATIO_TEST, min_distance=MIN_MATCH_DISTANCE,
+                  max_distance=MAX_MATCH_DISTANCE):
+        """CSfM::tracking's pose step as one device call (sfm_track_pnp):
+        matchFeatures(prevIdx, currIdx) of the previous frame's keypoints with
+        a map point (prev_pt3d >= 0) against the whole current frame, then
+        cv::solvePnPRansac on their map points.  -> (n_matches, found, rvec,
+        tvec, inlier keypoints, their map points); no PnP below min_matches."""
+        p3 = np.ascontiguousarray(np.asarray(prev_pt3d).reshape(-1), dtype=np.int32)
+        K9 = np.ascontiguousarray(np.asarray(K, np.float64).reshape(9))
+        cap = max(1, int((p3 >= 0).sum()))
+        kp, pt = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+        rvec, tvec = np.zeros(3), np.zeros(3)
+        found, nm, ni = c_int32(0), c_int32(0), c_int32(0)
+        check(lib().sfm_track_pnp(self._h, device_map._h, len(p3), ptr(p3), ratio, min_distance, max_distance,
+                                  int(min_matches), ptr(K9), int(iterations), float(reproj_err), float(confidence),
+                                  ptr(rvec), ptr(tvec), ctypes.byref(found), ctypes.byref(nm), cap, ptr(kp), ptr(pt),
+                                  ctypes.byref(ni)), "sfm_track_pnp")
+        return nm.value, bool(found.value), rvec, tvec, kp[:ni.value].copy(), pt[:ni.value].copy()
+
     def match_frames(self, distorted: bool = True, ratio=RATIO_TEST, min_distance=MIN_MATCH_DISTANCE,
                      max_distance=MAX_MATCH_DISTANCE):
         """bool CTracker::matchFeatures(): the whole frames (distorted positions) -> (_prevIdx, _currIdx)."""

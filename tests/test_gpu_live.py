@@ -101,6 +101,30 @@ def test_fused_find_map_points_equals_the_composed_calls():
         s.close()
 
 
+def test_fused_tracking_equals_the_composed_calls():
+    """sfm_track_pnp (matchFeatures + getPointsAtIdx + solvePnPRansac in one
+    device call) against the three calls it replaces: the same keyframes,
+    poses, associations, statistics and map, bitwise."""
+    runs = []
+    for fused in (True, False):
+        s = LiveSfM(KeypointStream())
+        s.fused_track = fused
+        try:
+            s.run(60)
+            runs.append(([f.no for f in s.kfs], [(f.rot.copy(), f.t.copy(), f.pt3d.copy()) for f in s.kfs],
+                         dict(s.stats), s.map.size(), s.prev.rot.copy(), s.prev.t.copy(), s.prev.pt3d.copy()))
+        finally:
+            s.close()
+    a, b = runs
+    assert a[0] == b[0] and len(a[0]) >= 3
+    for (r1, t1, p1), (r2, t2, p2) in zip(a[1], b[1]):
+        assert np.array_equal(r1, r2) and np.array_equal(t1, t2) and np.array_equal(p1, p2)
+    assert a[2] == b[2] and a[2]["tracked"] > 40
+    assert a[3] == b[3]
+    for x, y in zip(a[4:], b[4:]):
+        assert np.array_equal(x, y)
+
+
 def test_every_keyframe_ba_matches_oracle(run80):
     for rec in run80.ba_log:
         r, t, X = rec["rot"].copy(), rec["t"].copy(), rec["X"].copy()
