@@ -251,6 +251,21 @@ int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_
 int sfm_matcher_match_subset(sfm_matcher* h, const int32_t* prev_idx, int32_t n_prev, const int32_t* curr_idx,
                              int32_t n_curr, double ratio_test, double min_distance, double max_distance,
                              int32_t* prev_match, int32_t* curr_match, int32_t* n_matches);
+/* Keyframe store (CSfM::mapping's keyframe-pair matching, CSfM.cpp:141-221):
+ * keyframe slot `slot` takes pts [n][2] and desc [n][desc_bytes], resident
+ * on the device until the slot is stored again. */
+int sfm_matcher_store_keyframe(sfm_matcher* h, int32_t slot, const double* pts, const uint8_t* desc, int32_t n);
+/* The (pts0, desc0, pts1, desc1[, min, max]) overload of matchFeatures
+ * (CTracker.cpp:419-477) on stored keyframe rows: query rows q_idx[n_q] of
+ * slot q_slot (positions q_pts [n_q][2] when given -- e.g. projections, as
+ * CSfM.cpp:199-206 passes them; q_idx must not repeat then -- else the
+ * keyframe's own), train rows t_idx[n_t] of slot t_slot.  Subset-local
+ * indices out (into q_idx / t_idx), bitwise sfm_matcher_match on the same
+ * rows; capacity >= min(n_q, n_t). */
+int sfm_matcher_match_keyframes(sfm_matcher* h, int32_t q_slot, const int32_t* q_idx, int32_t n_q, const double* q_pts,
+                                int32_t t_slot, const int32_t* t_idx, int32_t n_t, double ratio_test,
+                                double min_distance, double max_distance, int32_t* idx0, int32_t* idx1,
+                                int32_t* n_matches);
 /* bool CTracker::matchFeatures() (CTracker.cpp:419-477): the two whole
  * frames, DISTORTED positions when distorted != 0 (CTracker.cpp:429-430);
  * fills _prevIdx/_currIdx; the reference's bool is n >= _minFeatures. */

@@ -175,6 +175,10 @@ _SIGNATURES = {
     "sfm_map_match_frame": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_int32, c_void_p, c_double, c_double, c_double, c_int32, c_void_p,
                                     c_void_p, POINTER(c_int32)]),
+    "sfm_matcher_store_keyframe": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int32]),
+    "sfm_matcher_match_keyframes": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_void_p,
+                                            c_int32, c_double, c_double, c_double, c_void_p, c_void_p,
+                                            POINTER(c_int32)]),
     "sfm_track_pnp": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_double, c_double, c_double, c_int32,
                               c_void_p, c_int32, c_double, c_double, c_void_p, c_void_p, POINTER(c_int32),
                               POINTER(c_int32), c_int32, c_void_p, c_void_p, POINTER(c_int32)]),

@@ -303,6 +303,21 @@ int append(sfm_map* h, DVec<T>& v, const T* src, int64_t n) {
   return 0;
 }
 
+// The handle's pinned block, at least n ints (grown while the stream is idle).
+int32_t* pin_reserve(sfm_map* h, size_t n, int* rc) {
+  if (h->pin_cap < n) {
+    if (h->pin) { (void)hipStreamSynchronize(h->s); (void)hipHostFree(h->pin); }
+    h->pin = nullptr;
+    h->pin_cap = 0;
+    const size_t cap = std::max<size_t>(n, 8192) * 3 / 2;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(int32_t) * cap) != hipSuccess) {
+      *rc = mapfail(SFM_ENOMEM, "hipHostMalloc failed");
+      return nullptr;
+    }
+    h->pin_cap = cap;
+  }
+  return h->pin;
+}
 int sync(sfm_map* h) {
   return hipStreamSynchronize(h->s) == hipSuccess ? 0 : mapfail(SFM_EIO, "kernel or copy failed");
 }
@@ -666,8 +681,11 @@ int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* f
   if (hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cnt, eoff, int(N), h->s) != hipSuccess)
     return mapfail(SFM_EIO, "scan failed");
   k_frame_offsets<<<1, 1, 0, h->s>>>(n_frames, fcnt, N, cnt, eoff, offs);
-  std::vector<int32_t> offs_h(2 * (size_t(n_frames) + 1));
-  (void)hipMemcpyAsync(offs_h.data(), offs, sizeof(int32_t) * offs_h.size(), hipMemcpyDeviceToHost, h->s);
+  // (readbacks through the pinned block: a pageable copy is staged by the
+  // runtime, ~2x the time at these sizes)
+  int32_t* offs_h = pin_reserve(h, 2 * (size_t(n_frames) + 1), &rc);
+  if (rc) return rc;
+  (void)hipMemcpyAsync(offs_h, offs, sizeof(int32_t) * 2 * (size_t(n_frames) + 1), hipMemcpyDeviceToHost, h->s);
   if (int r = sync(h)) return r;
   for (int i = 0; i <= n_frames; ++i) {
     off3[i] = offs_h[i];
@@ -683,9 +701,14 @@ int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* f
   if (rc) return rc;
   k_dup_fill<<<grid(n), 256, 0, h->s>>>(n, sel, h->ob_pt.p, h->ob_frame.p, h->ob_idx.p, h->orow, h->ooff, INT32_MIN,
                                         eoff, out3, out2);
-  (void)hipMemcpyAsync(pts3d_idx, out3, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
-  if (n2) (void)hipMemcpyAsync(pts2d_idx, out2, sizeof(int32_t) * size_t(n2), hipMemcpyDeviceToHost, h->s);
-  return sync(h);
+  int32_t* ph = pin_reserve(h, size_t(n) + size_t(n2), &rc);
+  if (rc) return rc;
+  (void)hipMemcpyAsync(ph, out3, sizeof(int32_t) * size_t(n), hipMemcpyDeviceToHost, h->s);
+  if (n2) (void)hipMemcpyAsync(ph + n, out2, sizeof(int32_t) * size_t(n2), hipMemcpyDeviceToHost, h->s);
+  if (int r = sync(h)) return r;
+  std::memcpy(pts3d_idx, ph, sizeof(int32_t) * size_t(n));
+  if (n2) std::memcpy(pts2d_idx, ph + n, sizeof(int32_t) * size_t(n2));
+  return 0;
 }
 
 int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, uint8_t* desc_out,

@@ -243,6 +243,7 @@ struct MatchFrame {
 };
 
 struct sfm_matcher {
+  std::vector<MatchFrame> kf;  // keyframe store (sfm_matcher_store_keyframe)
   int device = 0;
   int desc_bytes = 64, W = 8;
   int n_cu = 256;
@@ -456,6 +457,7 @@ int sfm_matcher_destroy(sfm_matcher* h) {
   if (!h) return 0;
   hipSetDevice(h->device);
   hipStreamSynchronize(h->stream);
+  for (auto& f : h->kf) hipFree(f.desc);
   for (auto& f : h->frame) {
     hipFree(f.desc);
   }
@@ -599,6 +601,97 @@ int sfm_matcher_match(sfm_matcher* h, const double* pts0, const uint8_t* desc0, 
   const int m = res[2 * n0];
   std::memcpy(idx0, res, sizeof(int) * size_t(m));
   std::memcpy(idx1, res + n0, sizeof(int) * size_t(m));
+  *n_matches = m;
+  return 0;
+}
+
+// Keyframe store (CSfM::mapping's keyframe-pair matching, CSfM.cpp:141-221):
+// slot `slot` takes pts [n][2] and desc [n][desc_bytes] once, resident.
+int sfm_matcher_store_keyframe(sfm_matcher* h, int32_t slot, const double* pts, const uint8_t* desc, int32_t n) {
+  if (!h) return mfail(SFM_EINVAL, "handle is NULL");
+  if (slot < 0 || slot > (1 << 20) || n < 0 || (n > 0 && (!pts || !desc))) return mfail(SFM_EINVAL, "bad keyframe arguments");
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  if (size_t(slot) >= h->kf.size()) h->kf.resize(size_t(slot) + 1);
+  MatchFrame& f = h->kf[size_t(slot)];
+  int rc = 0;
+  if (f.cap < size_t(std::max(n, 1))) {
+    hipStreamSynchronize(h->stream);
+    hipFree(f.desc);
+    f.desc = nullptr;
+    f.cap = size_t(std::max(n, 1));
+    if (hipMalloc(&f.desc, f.cap * (h->W * 8 + 16)) != hipSuccess) {
+      f.cap = 0;
+      return mfail(SFM_ENOMEM, "hipMalloc failed (matcher keyframe)");
+    }
+  }
+  f.n = n;
+  f.pts = reinterpret_cast<double*>(f.desc + size_t(n) * h->W);
+  f.ptsd = f.pts;
+  if (n) {
+    const size_t words = size_t(n) * h->W;
+    auto* st = pbuf<uint64_t>(h, "kfstage", words + 2 * size_t(n), &rc);
+    if (rc) return rc;
+    hipStreamSynchronize(h->stream);
+    pack_words(desc, n, h->desc_bytes, h->W, st);
+    std::memcpy(st + words, pts, 16 * size_t(n));
+    hipMemcpyAsync(f.desc, st, words * 8 + 16 * size_t(n), hipMemcpyHostToDevice, h->stream);
+  }
+  return 0;
+}
+
+// sfm_matcher_match on keyframe rows: query rows q_idx of keyframe q_slot
+// (positions q_pts [n_q][2] when given -- then q_idx must not repeat --,
+// else the keyframe's own), train rows t_idx of keyframe t_slot; indices out
+// are subset-local (into q_idx / t_idx), as sfm_matcher_match returns them.
+int sfm_matcher_match_keyframes(sfm_matcher* h, int32_t q_slot, const int32_t* q_idx, int32_t n_q, const double* q_pts,
+                                int32_t t_slot, const int32_t* t_idx, int32_t n_t, double ratio_test,
+                                double min_distance, double max_distance, int32_t* idx0, int32_t* idx1,
+                                int32_t* n_matches) {
+  if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
+  *n_matches = 0;
+  if (q_slot < 0 || t_slot < 0 || size_t(q_slot) >= h->kf.size() || size_t(t_slot) >= h->kf.size())
+    return mfail(SFM_EINVAL, "keyframe slot not stored");
+  if (n_q < 0 || n_t < 0 || (n_q && !q_idx) || (n_t && !t_idx)) return mfail(SFM_EINVAL, "bad index lists");
+  if (!ok_ratio_window(ratio_test, min_distance, max_distance)) return mfail(SFM_EINVAL, "non-finite threshold");
+  const MatchFrame& fq = h->kf[size_t(q_slot)];
+  const MatchFrame& ft = h->kf[size_t(t_slot)];
+  std::vector<char> seen(q_pts ? size_t(fq.n) : 0, 0);
+  for (int32_t i = 0; i < n_q; ++i) {
+    if (q_idx[i] < 0 || q_idx[i] >= fq.n) return mfail(SFM_EINVAL, "query index out of range");
+    if (q_pts) {
+      if (seen[size_t(q_idx[i])]) return mfail(SFM_EINVAL, "query index repeated with given positions");
+      seen[size_t(q_idx[i])] = 1;
+    }
+  }
+  for (int32_t i = 0; i < n_t; ++i)
+    if (t_idx[i] < 0 || t_idx[i] >= ft.n) return mfail(SFM_EINVAL, "train index out of range");
+  if (n_q == 0 || n_t < 2) return 0;  // reference UB with < 2 train rows: no matches
+  if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
+  int rc = 0;
+  // stage: q_idx | t_idx | (8-B aligned) query positions at their rows
+  const size_t ni = (size_t(n_q) + n_t + 1) & ~size_t(1);
+  const size_t np = q_pts ? 2 * size_t(fq.n) : 0;
+  auto* st = pbuf<int>(h, "kfidx", ni + 2 * np, &rc);
+  auto* d = dbuf<int>(h, "dkfidx", ni + 2 * np, &rc);
+  if (rc) return rc;
+  hipStreamSynchronize(h->stream);
+  std::memcpy(st, q_idx, sizeof(int) * size_t(n_q));
+  std::memcpy(st + n_q, t_idx, sizeof(int) * size_t(n_t));
+  double* sp = reinterpret_cast<double*>(st + ni);
+  if (q_pts)
+    for (int32_t i = 0; i < n_q; ++i) {
+      sp[2 * size_t(q_idx[i])] = q_pts[2 * size_t(i)];
+      sp[2 * size_t(q_idx[i]) + 1] = q_pts[2 * size_t(i) + 1];
+    }
+  hipMemcpyAsync(d, st, sizeof(int) * (ni + 2 * np), hipMemcpyHostToDevice, h->stream);
+  const double* p0 = q_pts ? reinterpret_cast<const double*>(d + ni) : fq.pts;
+  int* res = nullptr;
+  if ((rc = run_match(h, fq.desc, d, p0, n_q, ft.desc, d + n_q, ft.pts, n_t, ratio_test, min_distance, max_distance,
+                      &res)))
+    return rc;
+  const int m = res[2 * n_q];
+  std::memcpy(idx0, res, sizeof(int) * size_t(m));
+  std::memcpy(idx1, res + n_q, sizeof(int) * size_t(m));
   *n_matches = m;
   return 0;
 }

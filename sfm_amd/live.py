@@ -228,6 +228,7 @@ class LiveSfM:
         composed = os.environ.get("SFM_LIVE_COMPOSED") == "1"
         self.fused_find = not composed
         self.fused_track = not composed
+        self.resident_kf = not composed  # mapping matches on the matcher's keyframe store
 
     # ---- driver --------------------------------------------------------------
     def run(self, n_frames: int) -> None:
@@ -243,6 +244,7 @@ class LiveSfM:
         if not self.kfs:
             f = _Frame(k, pts, desc)
             self.kfs.append(f)                  # first keyframe at the origin (CFrame.cpp:229-235)
+            self.matcher.store_keyframe(0, pts, desc)
             self.matcher.push_frame(pts, desc)
             self.prev = f
             return
@@ -270,6 +272,7 @@ class LiveSfM:
         f0.pt3d[i0] = idx
         f1.pt3d[i1] = idx
         self.kfs.append(f1.copy())
+        self.matcher.store_keyframe(1, f1.pts, f1.desc)
         self.stats["new_points"] += len(idx)
         self._bundle_adjust()
         self.prev = f1
@@ -312,6 +315,7 @@ class LiveSfM:
         if self._add_keyframe(cur):
             kf = cur.copy()
             self.kfs.append(kf)
+            self.matcher.store_keyframe(len(self.kfs) - 1, kf.pts, kf.desc)
             m = np.flatnonzero(kf.pt3d >= 0)
             self.map.addPointMatches(kf.pt3d[m], m, kf.no)
             self.map.addDescriptors(kf.pt3d[m], kf.desc[m])
@@ -367,7 +371,10 @@ class LiveSfM:
             pu = np.flatnonzero(kf.pt3d < 0)
             if len(cu) < 2 or len(pu) < 2:
                 continue
-            pi, ci = self.matcher.match(kf.pts[pu], kf.desc[pu], new_kf.pts[cu], new_kf.desc[cu])
+            if self.resident_kf:
+                pi, ci = self.matcher.match_keyframes(i, pu, len(self.kfs) - 1, cu)
+            else:
+                pi, ci = self.matcher.match(kf.pts[pu], kf.desc[pu], new_kf.pts[cu], new_kf.desc[cu])
             if not len(pi):
                 continue
             uv0, uv1 = kf.pts[pu[pi]], new_kf.pts[cu[ci]]
@@ -388,8 +395,13 @@ class LiveSfM:
                 if len(uj) < 2:
                     continue
                 uv, _ = _project(self.K, kj.rot, kj.t, Xf)
-                d = pdesc if abs(kj.no - kf.no) < abs(kj.no - new_kf.no) else cdesc
-                m0, m1 = self.matcher.match(uv, d, kj.pts[uj], kj.desc[uj], 0.8, 0.0, MAX_REPR_ERR)
+                near_kf = abs(kj.no - kf.no) < abs(kj.no - new_kf.no)
+                if self.resident_kf:
+                    m0, m1 = self.matcher.match_keyframes(i if near_kf else len(self.kfs) - 1, p2 if near_kf else c2,
+                                                          j, uj, uv, 0.8, 0.0, MAX_REPR_ERR)
+                else:
+                    d = pdesc if near_kf else cdesc
+                    m0, m1 = self.matcher.match(uv, d, kj.pts[uj], kj.desc[uj], 0.8, 0.0, MAX_REPR_ERR)
                 if len(m0):
                     self.map.addPointMatches(idx[m0], uj[m1], kj.no)
                     kj.pt3d[uj[m1]] = idx[m0]

@@ -83,6 +83,32 @@ class FeatureMatcher:
               "sfm_matcher_match_subset")
         return o0[:nm.value].copy(), o1[:nm.value].copy()
 
+    def store_keyframe(self, slot: int, pts, desc) -> None:
+        """Keyframe slot `slot` resident on the device (pts [n][2], desc)."""
+        p = _pts(pts)
+        d = _desc(desc, self.desc_bytes)
+        if d.shape[0] != p.shape[0]:
+            raise ValueError("one descriptor row per keypoint")
+        check(lib().sfm_matcher_store_keyframe(self._h, int(slot), ptr(p), ptr(d), p.shape[0]),
+              "sfm_matcher_store_keyframe")
+
+    def match_keyframes(self, q_slot: int, q_idx, t_slot: int, t_idx, q_pts=None, ratio=RATIO_TEST,
+                        min_distance=MIN_MATCH_DISTANCE, max_distance=MAX_MATCH_DISTANCE):
+        """match(pts0, desc0, pts1, desc1) on stored keyframe rows: query rows
+        q_idx of q_slot (positions q_pts if given), train rows t_idx of
+        t_slot -> subset-local (query, train) indices."""
+        a = np.ascontiguousarray(np.asarray(q_idx).reshape(-1), dtype=np.int32)
+        b = np.ascontiguousarray(np.asarray(t_idx).reshape(-1), dtype=np.int32)
+        qp = None if q_pts is None else _pts(q_pts)
+        if qp is not None and qp.shape[0] != a.size:
+            raise ValueError("one query position per query row")
+        cap = max(1, min(a.size, b.size))
+        o0, o1, nm = np.zeros(cap, np.int32), np.zeros(cap, np.int32), c_int32(0)
+        check(lib().sfm_matcher_match_keyframes(self._h, int(q_slot), ptr(a), a.size, ptr(qp), int(t_slot), ptr(b),
+                                                b.size, ratio, min_distance, max_distance, ptr(o0), ptr(o1),
+                                                ctypes.byref(nm)), "sfm_matcher_match_keyframes")
+        return o0[:nm.value].copy(), o1[:nm.value].copy()
+
     def track_pnp(self, device_map, prev_pt3d, K, min_matches: int, iterations: int = 20, reproj_err: float = 7.0,
                   confidence: float = 0.99, ratio=RATIO_TEST, min_distance=MIN_MATCH_DISTANCE,
                   max_distance=MAX_MATCH_DISTANCE):

@@ -103,12 +103,14 @@ def test_fused_find_map_points_equals_the_composed_calls():
 
 def test_fused_tracking_equals_the_composed_calls():
     """sfm_track_pnp (matchFeatures + getPointsAtIdx + solvePnPRansac in one
-    device call) against the three calls it replaces: the same keyframes,
-    poses, associations, statistics and map, bitwise."""
+    device call) and the mapping's matches on the matcher's keyframe store
+    (sfm_matcher_match_keyframes) against the calls they replace: the same
+    keyframes, poses, associations, statistics and map, bitwise."""
     runs = []
     for fused in (True, False):
         s = LiveSfM(KeypointStream())
         s.fused_track = fused
+        s.resident_kf = fused
         try:
             s.run(60)
             runs.append(([f.no for f in s.kfs], [(f.rot.copy(), f.t.copy(), f.pt3d.copy()) for f in s.kfs],
