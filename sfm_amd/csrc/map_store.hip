@@ -154,10 +154,10 @@ __global__ void k_frame_offsets(int nf, const int32_t* __restrict__ fcnt, int64_
 template <int W>
 __global__ __launch_bounds__(64) void k_map_repr(const uint64_t* __restrict__ desc, const int32_t* __restrict__ drow,
                                                  const int32_t* __restrict__ doff, const int32_t* __restrict__ qpt,
-                                                 int n, int32_t* __restrict__ best_local,
-                                                 uint64_t* __restrict__ out) {
+                                                 int n, const int32_t* __restrict__ n_dev,
+                                                 int32_t* __restrict__ best_local, uint64_t* __restrict__ out) {
   const int i = blockIdx.x, l = threadIdx.x;
-  if (i >= n) return;
+  if (i >= (n_dev ? *n_dev : n)) return;  // (n_dev: the count on the device, n its bound)
   const int p = qpt[i];
   const int r0 = doff[p], k = doff[p + 1] - r0;
   if (k == 0) {  // no descriptor row (the callers check; reported as -1)
@@ -215,11 +215,12 @@ __global__ void k_unmark(int n, const int32_t* __restrict__ pts, uint8_t* __rest
 // The queried points projected with the frame's pose (CSfM.cpp:664-668, the
 // reference's GeometryUtils::projectPoints with zero distortion, as
 // sfm_amd/live.py's _project): uv = (x / z) f + c.
-__global__ void k_project(int n, const int32_t* __restrict__ qpt, const double* __restrict__ X, double r0, double r1,
+__global__ void k_project(int n, const int32_t* __restrict__ n_dev, const int32_t* __restrict__ qpt,
+                          const double* __restrict__ X, double r0, double r1,
                           double r2, double r3, double r4, double r5, double r6, double r7, double r8, double t0,
                           double t1, double t2, double fx, double fy, double cx, double cy, double* __restrict__ uv) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= (n_dev ? *n_dev : n)) return;
   const double* x = X + 3 * size_t(qpt[i]);
   const double x0 = x[0], x1 = x[1], x2 = x[2];
   const double c0 = r0 * x0 + r1 * x1 + r2 * x2 + t0;
@@ -238,7 +239,8 @@ struct DVec {
 }  // namespace
 // match_kernels.hip
 int matcher_match_current_dev(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
-                              const int32_t* d_train_idx, int n1, double ratio, double mn, double mx, int** res);
+                              const int32_t* d_n0, const int32_t* d_train_idx, int n1, double ratio, double mn,
+                              double mx, int** res);
 int matcher_current_n(const sfm_matcher* h);
 int matcher_words(const sfm_matcher* h);
 int matcher_device(const sfm_matcher* h);
@@ -738,7 +740,7 @@ int sfm_map_representative_descriptors(sfm_map* h, int32_t n, const int32_t* pts
   if (rc) return rc;
   (void)hipMemcpyAsync(q, pts3d_idx, sizeof(int32_t) * size_t(n), hipMemcpyHostToDevice, h->s);
   switch (h->W) {
-#define CASE(w) case w: k_map_repr<w><<<n, 64, 0, h->s>>>(h->desc.p, drow, doff, q, n, best, out); break;
+#define CASE(w) case w: k_map_repr<w><<<n, 64, 0, h->s>>>(h->desc.p, drow, doff, q, n, nullptr, best, out); break;
     CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
 #undef CASE
     default: return mapfail(SFM_EINVAL, "descriptor width");  // excluded by sfm_map_create
@@ -822,38 +824,38 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
   if (rc) return rc;
   if (hipcub::DeviceSelect::Flagged(tmp, bytes, it, mark, out, dn, P, h->s) != hipSuccess)
     return mapfail(SFM_EIO, "select failed");
-  (void)hipMemcpyAsync(h->pin, dn, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
-  if (int r = sync(h)) return r;
-  const int n_new = h->pin[0];
-  if (n_new == 0) return 0;
-  // the queries: representative descriptors and projections of the new points
-  int32_t* best = out + n_new;
-  auto* qd = static_cast<uint64_t*>(scratch(h, "mq", sizeof(uint64_t) * size_t(n_new) * h->W, &rc));
-  auto* uv = static_cast<double*>(scratch(h, "muv", sizeof(double) * 2 * size_t(n_new), &rc));
+  // no readback of the count here: the kernels below run on its bound P and
+  // read the count itself (k_map_repr, k_project, the matcher's acceptance)
+  int32_t* best = out + P;
+  auto* qd = static_cast<uint64_t*>(scratch(h, "mq", sizeof(uint64_t) * size_t(P) * h->W, &rc));
+  auto* uv = static_cast<double*>(scratch(h, "muv", sizeof(double) * 2 * size_t(P), &rc));
   if (rc) return rc;
   switch (h->W) {
-#define CASE(w) case w: k_map_repr<w><<<n_new, 64, 0, h->s>>>(h->desc.p, h->drow, h->doff, out, n_new, best, qd); break;
+#define CASE(w) case w: k_map_repr<w><<<P, 64, 0, h->s>>>(h->desc.p, h->drow, h->doff, out, P, dn, best, qd); break;
     CASE(1) CASE(2) CASE(4) CASE(8) CASE(16) CASE(32) CASE(64)
 #undef CASE
     default: return mapfail(SFM_EINVAL, "descriptor width");
   }
-  k_project<<<grid(n_new), 256, 0, h->s>>>(n_new, out, h->X.p, R9[0], R9[1], R9[2], R9[3], R9[4], R9[5], R9[6], R9[7],
-                                           R9[8], t3[0], t3[1], t3[2], K9[0], K9[4], K9[2], K9[5], uv);
-  (void)hipMemcpyAsync(h->pin, out, sizeof(int32_t) * 2 * size_t(n_new), hipMemcpyDeviceToHost, h->s);
+  k_project<<<grid(P), 256, 0, h->s>>>(P, dn, out, h->X.p, R9[0], R9[1], R9[2], R9[3], R9[4], R9[5], R9[6], R9[7],
+                                       R9[8], t3[0], t3[1], t3[2], K9[0], K9[4], K9[2], K9[5], uv);
+  // points, representative rows and the count in one download
+  (void)hipMemcpyAsync(h->pin, out, sizeof(int32_t) * 2 * size_t(P), hipMemcpyDeviceToHost, h->s);
+  (void)hipMemcpyAsync(h->pin + 2 * size_t(P), dn, sizeof(int32_t), hipMemcpyDeviceToHost, h->s);
   if (hipEventRecord(h->ev, h->s) != hipSuccess) return mapfail(SFM_EIO, "hipEventRecord failed");
   int* res = nullptr;
-  if ((rc = matcher_match_current_dev(mt, h->ev, qd, uv, n_new, fset + fs.size() + n_existing, n_train, ratio_test,
+  if ((rc = matcher_match_current_dev(mt, h->ev, qd, uv, P, dn, fset + fs.size() + n_existing, n_train, ratio_test,
                                       min_distance, max_distance, &res)))
     return rc;
   if (int r = sync(h)) return r;
+  const int n_new = h->pin[2 * size_t(P)];
   for (int i = 0; i < n_new; ++i)
-    if (h->pin[n_new + i] < 0)
+    if (h->pin[P + i] < 0)
       return mapfail(SFM_EINVAL, "point " + std::to_string(h->pin[i]) + " has no descriptor row");
-  const int m = res[2 * n_new];
+  const int m = res[2 * P];
   if (m > capacity) return mapfail(SFM_EINVAL, "capacity " + std::to_string(capacity) + " < " + std::to_string(m));
   for (int k = 0; k < m; ++k) {
     pts3d_match[k] = h->pin[res[k]];
-    train_match[k] = train_idx[res[n_new + k]];
+    train_match[k] = train_idx[res[P + k]];
   }
   *n_matches = m;
   return 0;

@@ -152,13 +152,14 @@ __global__ void k_knn2_merge(const unsigned long long* __restrict__ part, int n0
 //   key[j]   = min over accepted queries of (d0 << 32 | i)  -> surviving query
 //   first[j] = min over accepted queries of i               -> slot order
 // Positions are those of rows qidx[i] / tidx[j] (nullptr: i / j).
-__global__ void k_accept(const unsigned long long* __restrict__ part, int n0, int nslice,
+// (n0_dev: the query count on the device, n0 its bound -- sfm_map_match_frame)
+__global__ void k_accept(const unsigned long long* __restrict__ part, int n0, const int* __restrict__ n0_dev, int nslice,
                          const double* __restrict__ p0, const int* __restrict__ qidx, const double* __restrict__ p1,
                          const int* __restrict__ tidx, double ratio_test, double minSq, double maxSq,
                          unsigned long long* __restrict__ key, int* __restrict__ first) {
 #pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n0) return;
+  if (i >= (n0_dev ? *n0_dev : n0)) return;
   unsigned long long k0, k1;
   merge_parts(part, n0, nslice, i, k0, k1);
   if (k0 == kNoKey || k1 == kNoKey) return;  // < 2 train rows: the reference reads past matches[i] (UB)
@@ -328,7 +329,8 @@ int launch_knn(sfm_matcher* h, const uint64_t* q, const int* qidx, int n0, const
 // The kernels alone (no download, no synchronisation): the (query, train)
 // pairs and their count land in the device buffer *out_dev ([2 n0 + 1]).
 int run_match_async(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
-                    const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** out_dev) {
+                    const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** out_dev,
+                    const int* n0_dev = nullptr) {
   int rc = 0;
   const int nslice = slices_for(h, n0, n1);
   auto* part = dbuf<unsigned long long>(h, "part", 2 * size_t(n0) * nslice, &rc);
@@ -342,7 +344,8 @@ int run_match_async(sfm_matcher* h, const uint64_t* q, const int* qidx, const do
   k_reset<<<(std::max(n0, n1) + 255) / 256, 256, 0, s>>>(n1, key, first, n0, slot);
   if ((rc = launch_knn(h, q, qidx, n0, tr, tidx, n1, part, nslice))) return rc;
   hipEventRecord(h->ev[1], s);
-  k_accept<<<(n0 + 255) / 256, 256, 0, s>>>(part, n0, nslice, p0, qidx, p1, tidx, ratio, mn * mn, mx * mx, key, first);
+  k_accept<<<(n0 + 255) / 256, 256, 0, s>>>(part, n0, n0_dev, nslice, p0, qidx, p1, tidx, ratio, mn * mn, mx * mx, key,
+                                             first);
   sfm::k_mark_first<<<(n1 + 255) / 256, 256, 0, s>>>(n1, first, slot);
   sfm::k_compact_slots<false><<<1, 1024, 0, s>>>(n0, slot, key, out, out + n0, out + 2 * n0);
   hipEventRecord(h->ev[2], s);
@@ -351,12 +354,13 @@ int run_match_async(sfm_matcher* h, const uint64_t* q, const int* qidx, const do
 }
 
 int run_match(sfm_matcher* h, const uint64_t* q, const int* qidx, const double* p0, int n0, const uint64_t* tr,
-              const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** res_out) {
+              const int* tidx, const double* p1, int n1, double ratio, double mn, double mx, int** res_out,
+              const int* n0_dev = nullptr) {
   int rc = 0;
   int* res = pbuf<int>(h, "res", 2 * size_t(n0) + 1, &rc);
   if (rc) return rc;
   int* out = nullptr;
-  if ((rc = run_match_async(h, q, qidx, p0, n0, tr, tidx, p1, n1, ratio, mn, mx, &out))) return rc;
+  if ((rc = run_match_async(h, q, qidx, p0, n0, tr, tidx, p1, n1, ratio, mn, mx, &out, n0_dev))) return rc;
   hipStream_t s = h->stream;
   hipMemcpyAsync(res, out, (2 * size_t(n0) + 1) * sizeof(int), hipMemcpyDeviceToHost, s);
   if (hipStreamSynchronize(s) != hipSuccess) return mfail(SFM_EIO, "matcher kernels failed");
@@ -415,12 +419,13 @@ const double* map_points_dev(sfm_map* h, int32_t* n_pts, int* device);
 // sfm_matcher_match returns them, in *res (pinned, valid after this call).
 // No upload and no synchronisation before the kernels.
 int matcher_match_current_dev(sfm_matcher* h, hipEvent_t after, const uint64_t* q, const double* p0, int n0,
-                              const int32_t* d_train_idx, int n1, double ratio, double mn, double mx, int** res) {
+                              const int32_t* d_n0, const int32_t* d_train_idx, int n1, double ratio, double mn,
+                              double mx, int** res) {
   if (h->frames_pushed < 1) return mfail(SFM_EINVAL, "push the current frame first");
   if (!ok_ratio_window(ratio, mn, mx)) return mfail(SFM_EINVAL, "non-finite threshold");
   const MatchFrame& fc = h->frame[h->cur];
   if (after && hipStreamWaitEvent(h->stream, after, 0) != hipSuccess) return mfail(SFM_EIO, "stream wait failed");
-  return run_match(h, q, nullptr, p0, n0, fc.desc, d_train_idx, fc.pts, n1, ratio, mn, mx, res);
+  return run_match(h, q, nullptr, p0, n0, fc.desc, d_train_idx, fc.pts, n1, ratio, mn, mx, res, d_n0);
 }
 int matcher_current_n(const sfm_matcher* h) { return h->frames_pushed < 1 ? -1 : h->frame[h->cur].n; }
 int matcher_words(const sfm_matcher* h) { return h->W; }
