@@ -178,11 +178,27 @@ class _Frame:
         return f
 
     def P(self, K):
-        return K @ np.hstack([_rodrigues(self.rot), self.t.reshape(3, 1)])
+        return K @ np.hstack([_R(self.rot), self.t.reshape(3, 1)])
+
+
+_RCACHE: dict = {}
+
+
+def _R(rot):
+    """_rodrigues(rot), memoised on rot's bytes (a keyframe's pose is asked
+    for by every mapping pass and re-finding; the values are the function's
+    own, the arrays are not to be modified)."""
+    key = np.asarray(rot, np.float64).tobytes()
+    R = _RCACHE.get(key)
+    if R is None:
+        if len(_RCACHE) > 4096:
+            _RCACHE.clear()
+        R = _RCACHE[key] = _rodrigues(rot)
+    return R
 
 
 def _project(K, rot, t, X):
-    Xc = X @ _rodrigues(rot).T + t
+    Xc = X @ _R(rot).T + t
     return Xc[:, :2] / Xc[:, 2:3] * np.array([K[0, 0], K[1, 1]]) + K[:2, 2], Xc[:, 2]
 
 
@@ -190,7 +206,7 @@ def _filter_matches(K, f0, f1, uv0, uv1, X, max_err):
     """filterMatches restated from its call site (CSfM.cpp:164-165): positive
     depth in both keyframes, point-to-epipolar-line distance <= max_err both
     ways (F of the two poses)."""
-    R0, R1 = _rodrigues(f0.rot), _rodrigues(f1.rot)
+    R0, R1 = _R(f0.rot), _R(f1.rot)
     R = R1 @ R0.T
     tt = f1.t - R @ f0.t
     tx = np.array([[0, -tt[2], tt[1]], [tt[2], 0, -tt[0]], [-tt[1], tt[0], 0]])
@@ -336,7 +352,7 @@ class LiveSfM:
             if len(un) < 2:
                 return
             existing = cur.pt3d[cur.pt3d >= 0].astype(np.int32)
-            pm, km = self.map.matchFrame(self.matcher, [f.no for f in self.kfs], existing, _rodrigues(cur.rot),
+            pm, km = self.map.matchFrame(self.matcher, [f.no for f in self.kfs], existing, _R(cur.rot),
                                          cur.t, self.K, un, 0.8, 0.0, MAX_REPR_ERR)
             cur.pt3d[km] = pm
             self.stats["map_matches"] += len(pm)
