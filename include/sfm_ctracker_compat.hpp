@@ -513,6 +513,7 @@ class MapStore {
   MapStore(const MapStore&) = delete;
   MapStore& operator=(const MapStore&) = delete;
   int status() const { return rc_; }
+  sfm_map* handle() const { return h_; }
 
   // CMap::getNPoints (CMap.cpp:114-116)
   int getNPoints() const {
