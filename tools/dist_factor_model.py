@@ -136,7 +136,31 @@ def factor_model(n, nranks, pt, bw):
         r2 = red[k + 2] if (nranks > 1 and k + 2 < np_) else 0.0
         pipe += bcast[k] + max(r2, nxt)
     pipe = max(pipe, bulk) + misc[2] * ms
-    return {"sequential_s": seq, "lookahead_s": look, "pipelined_s": pipe, "chain_s": chain, "bulk_s": bulk,
+    # NOT BUILT, a projection from the same measured parts (VERDICT r5 item
+    # 2): the pipelined schedule with panel k's broadcast in CH row bands and
+    # the next owner's unpack + update of panel k+1 consuming each band as it
+    # lands: per step max(T, P) + min(T, P) / CH instead of T + P (T the
+    # broadcast, each band paying the collective latency; P the unpack +
+    # update), then the add + factor + pack of panel k+1 as before.
+    CH = 4
+    chunked = misc[0] * ms
+    if np_:
+        chunked += (red[0] if nranks > 1 else 0.0) + (add[0] * ms if nranks > 1 else 0.0) + (fac[0] + pack[0]) * ms
+    for k in range(np_):
+        T = (CH * LAT_S + (bcast[k] - LAT_S)) if nranks > 1 else 0.0
+        ov, rest = 0.0, 0.0
+        if k + 1 < np_:
+            own = (k + 1) % nranks
+            tot, first = own_tiles_after(nblk, pt, k, nranks, own)
+            ov = ((unpack[k] if nranks > 1 else 0.0) + upd[own, k] * (first / tot if tot else 0.0)) * ms
+            rest = ((add[k + 1] if nranks > 1 else 0.0) + fac[k + 1] + pack[k + 1]) * ms
+        r2 = red[k + 2] if (nranks > 1 and k + 2 < np_) else 0.0
+        # (the collective stream: the bands, then reduce k+2; the main stream:
+        # the bands' consumption, then add + factor + pack of k+1)
+        chunked += max(T + r2, max(T, ov) + min(T, ov) / CH + rest)
+    chunked = max(chunked, bulk) + misc[2] * ms
+    return {"sequential_s": seq, "lookahead_s": look, "pipelined_s": pipe, "chunked_projection_s": chunked,
+            "chain_s": chain, "bulk_s": bulk,
             "reduce_scatter_s": rs, "broadcast_s": float(bcast.sum()), "panel_reduces_s": float(np.sum(red)),
             "factor_s_sum": float(fac.sum() * ms),
             "updates_s_max_rank": float(upd.sum(axis=1).max() * ms), "backsub_s": misc[2] * ms,
@@ -175,7 +199,7 @@ def main():
             out["curves"][key] = {"replicated_ms": rep * 1e3, "replicated_speedup": solve_s / rep}
             for pt in a.pt:
                 f = factor_model(N_SYS, N, pt, bw)
-                for sch in ("sequential", "lookahead", "pipelined"):
+                for sch in ("sequential", "lookahead", "pipelined", "chunked_projection"):
                     t = ITERS * f[f"{sch}_s"] + rest / N
                     out["curves"][key][f"dist_pt{pt}_{sch}_ms"] = t * 1e3
                     out["curves"][key][f"dist_pt{pt}_{sch}_speedup"] = solve_s / t
