@@ -24,6 +24,7 @@
 #include <vector>
 #include <chrono>
 
+#include "sfm_trace.h"
 #include "ba_device.h"
 #include "ba_setup.h"
 #include "ba_common.h"
@@ -770,6 +771,7 @@ int dist_prepare(sfm_ba_handle* h) {
 //   events order each buffer's reuse after its last reader).
 // Every panel takes its updates in panel order on every rank count.
 int dist_factor_enqueue(sfm_ba_handle* h) {
+  SFM_TRACE("sfm:dist_factor");
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
@@ -907,6 +909,7 @@ void reduce_phase(sfm_ba_handle* h, const ReduceBatch& rb, bool copy_fail, int t
 // Evaluate cost, Jacobian, Jacobi scale (first call), per-block normal
 // equations, LM diagonal and gradient at the current parameters.
 int evaluate_enqueue(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
+  SFM_TRACE("sfm:evaluate");
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
@@ -1004,6 +1007,7 @@ int evaluate(sfm_ba_handle* h, bool first, bool jacobi_scaling) {
 // One trust-region step: factor, Schur, dense Cholesky, back substitution,
 // model cost change and candidate cost.
 int compute_step_enqueue(sfm_ba_handle* h, double radius) {
+  SFM_TRACE("sfm:compute_step");
   DevProblem& d = h->d;
   hipStream_t s = h->stream;
   int rc;
@@ -1449,6 +1453,7 @@ int sfm_ba_set_distributed_factor(sfm_ba_handle* h, int32_t panel_tiles) {
 int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, const int32_t* cam_idx,
                        const int32_t* pt_idx, int32_t n_cams, const double* K9, const double* rot, const double* t,
                        int32_t n_pts, const double* X) {
+  SFM_TRACE("sfm_ba_set_problem");
   if (!h) return fail(SFM_EINVAL, "handle is NULL");
   if (n_obs < 0 || n_cams < 0 || n_pts < 0) return fail(SFM_EINVAL, "negative size");
   if (n_obs > 0 && (!obs_uv || !cam_idx || !pt_idx)) return fail(SFM_EINVAL, "observation arrays are NULL");
@@ -2107,6 +2112,7 @@ int sfm_ba_sync(sfm_ba_handle* h) {
 
 int sfm_ba_solve_resident(sfm_ba_handle* h, const sfm_ba_options* opts_in, int32_t mode, sfm_ba_summary* summary,
                           sfm_ba_iteration* trace, int32_t trace_cap, int32_t* trace_len) {
+  SFM_TRACE("sfm_ba_solve_resident");
   const auto t_start = std::chrono::steady_clock::now();
   auto now_s = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
   if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
@@ -2299,6 +2305,7 @@ int sfm_ba_solve(const sfm_ba_options* opts, int32_t mode, int64_t n_obs, const 
                  const int32_t* cam_idx, const int32_t* pt_idx, int32_t n_cams, const double* K9, double* rot,
                  double* t, int32_t n_pts, double* X, sfm_ba_summary* summary, sfm_ba_iteration* trace,
                  int32_t trace_cap, int32_t* trace_len) {
+  SFM_TRACE("sfm_ba_solve");
   if (mode < 0 || mode > 2 || n_obs == 0) {
     if (summary) { std::memset(summary, 0, sizeof(*summary)); summary->termination_type = SFM_CONVERGENCE; }
     if (trace_len) *trace_len = 0;
@@ -2373,6 +2380,7 @@ static int ensure_records(sfm_ba_handle* h) {
 }
 
 int sfm_ba_evaluate(sfm_ba_handle* h, double* cost, double* res, double* jac) {
+  SFM_TRACE("sfm_ba_evaluate");
   if (!h || !h->has_problem) return fail(SFM_EINVAL, "no problem set");
   HIPCHK(hipSetDevice(h->device));
   DevProblem& d = h->d;

@@ -24,6 +24,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include "sfm_trace.h"
 #include "../../include/sfm_amd.h"
 
 void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
@@ -1033,5 +1034,6 @@ int brisk_detect_describe_impl(int32_t device, const uint8_t* img, bool img_on_d
 extern "C" int sfm_brisk_detect_describe(int32_t device, const uint8_t* img, int32_t w, int32_t h, int32_t threshold,
                                          int32_t octaves, int32_t capacity, float* kps, int32_t* octave,
                                          uint8_t* desc, int32_t* n_out) {
+  SFM_TRACE("sfm_brisk_detect_describe");
   return brisk_detect_describe_impl(device, img, false, w, h, threshold, octaves, capacity, kps, octave, desc, n_out);
 }

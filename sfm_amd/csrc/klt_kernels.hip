@@ -28,6 +28,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include "sfm_trace.h"
 #include "../../include/sfm_amd.h"
 #include "ordered_compact.h"
 #include "klt_internal.h"
@@ -499,6 +500,7 @@ int sfm_klt_destroy(sfm_klt_handle* h) {
 int32_t sfm_klt_num_levels(const sfm_klt_handle* h) { return h ? h->levels + 1 : 0; }
 
 int sfm_klt_push_frame(sfm_klt_handle* h, const uint8_t* grey, int32_t stride) {
+  SFM_TRACE("sfm_klt_push_frame");
   if (!h || !grey) return kfail(SFM_EINVAL, "NULL argument");
   if (stride < h->w) return kfail(SFM_EINVAL, "stride < width");
   hipSetDevice(h->device);

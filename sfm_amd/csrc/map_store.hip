@@ -31,6 +31,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include "sfm_trace.h"
 #include "../../include/sfm_amd.h"
 
 void sfm_internal_set_error(const std::string& msg);  // ba_solver.hip
@@ -419,6 +420,7 @@ int sfm_map_size(sfm_map* h, int32_t* n_pts, int64_t* n_obs, int64_t* n_desc_row
 
 int sfm_map_add_new_points(sfm_map* h, int32_t n_pts, const double* pts3d, int32_t n_frames, const int32_t* frame_no,
                            const int32_t* pts2d_idx, int32_t* pts3d_idx) {
+  SFM_TRACE("sfm_map_add_new_points");
   if (!h) return mapfail(SFM_EINVAL, "NULL handle");
   if (n_pts < 0 || n_frames < 0) return mapfail(SFM_EINVAL, "negative size");
   if (n_pts == 0) return 0;
@@ -478,6 +480,7 @@ int sfm_map_add_descriptors(sfm_map* h, int32_t n, const int32_t* pts3d_idx, con
 }
 
 int sfm_map_get_points(sfm_map* h, int32_t n, const int32_t* pts3d_idx, double* pts3d) {
+  SFM_TRACE("sfm_map_get_points");
   if (!h) return mapfail(SFM_EINVAL, "NULL handle");
   if (n <= 0) return n < 0 ? mapfail(SFM_EINVAL, "negative size") : 0;
   if (!pts3d_idx || !pts3d) return mapfail(SFM_EINVAL, "NULL argument");
@@ -629,6 +632,7 @@ int sfm_map_points_in_frame(sfm_map* h, int32_t frame_no, int32_t capacity, int3
 
 int sfm_map_points_in_frame_multi(sfm_map* h, int32_t n_frames, const int32_t* frame_no, int64_t capacity,
                                   int32_t* pts3d_idx, int32_t* off3, int32_t* pts2d_idx, int32_t* off2) {
+  SFM_TRACE("sfm_map_points_in_frame_multi");
   if (!h || !off3 || !off2 || (n_frames > 0 && !frame_no)) return mapfail(SFM_EINVAL, "NULL argument");
   if (n_frames < 0) return mapfail(SFM_EINVAL, "negative size");
   for (int i = 0; i <= n_frames; ++i) off3[i] = off2[i] = 0;
@@ -766,6 +770,7 @@ int sfm_map_match_frame(sfm_map* h, sfm_matcher* mt, int32_t n_frames, const int
                         int32_t n_train, const int32_t* train_idx, double ratio_test, double min_distance,
                         double max_distance, int32_t capacity, int32_t* pts3d_match, int32_t* train_match,
                         int32_t* n_matches) {
+  SFM_TRACE("sfm_map_match_frame");
   if (!h || !mt || !n_matches) return mapfail(SFM_EINVAL, "NULL handle");
   *n_matches = 0;
   if (n_frames < 0 || n_existing < 0 || n_train < 0) return mapfail(SFM_EINVAL, "negative size");

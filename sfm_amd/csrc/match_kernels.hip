@@ -35,6 +35,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include "sfm_trace.h"
 #include "../../include/sfm_amd.h"
 #include "ordered_compact.h"
 
@@ -476,6 +477,7 @@ int sfm_matcher_destroy(sfm_matcher* h) {
 
 int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_distorted, const uint8_t* desc,
                            int32_t n) {
+  SFM_TRACE("sfm_matcher_push_frame");
   if (!h) return mfail(SFM_EINVAL, "handle is NULL");
   if (n < 0 || (n > 0 && (!pts || !desc))) return mfail(SFM_EINVAL, "bad frame arguments");
   if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
@@ -518,6 +520,7 @@ int sfm_matcher_push_frame(sfm_matcher* h, const double* pts, const double* pts_
 int sfm_matcher_match_subset(sfm_matcher* h, const int32_t* prev_idx, int32_t n_prev, const int32_t* curr_idx,
                              int32_t n_curr, double ratio_test, double min_distance, double max_distance,
                              int32_t* prev_match, int32_t* curr_match, int32_t* n_matches) {
+  SFM_TRACE("sfm_matcher_match_subset");
   if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
   *n_matches = 0;
   if (h->frames_pushed < 2) return mfail(SFM_EINVAL, "push the previous and the current frame first");
@@ -579,6 +582,7 @@ int sfm_matcher_match_frames(sfm_matcher* h, int32_t distorted, double ratio_tes
 int sfm_matcher_match(sfm_matcher* h, const double* pts0, const uint8_t* desc0, int32_t n0, const double* pts1,
                       const uint8_t* desc1, int32_t n1, double ratio_test, double min_distance, double max_distance,
                       int32_t* idx0, int32_t* idx1, int32_t* n_matches) {
+  SFM_TRACE("sfm_matcher_match");
   if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
   *n_matches = 0;
   if (n0 < 0 || n1 < 0) return mfail(SFM_EINVAL, "negative size");
@@ -613,6 +617,7 @@ int sfm_matcher_match(sfm_matcher* h, const double* pts0, const uint8_t* desc0, 
 // Keyframe store (CSfM::mapping's keyframe-pair matching, CSfM.cpp:141-221):
 // slot `slot` takes pts [n][2] and desc [n][desc_bytes] once, resident.
 int sfm_matcher_store_keyframe(sfm_matcher* h, int32_t slot, const double* pts, const uint8_t* desc, int32_t n) {
+  SFM_TRACE("sfm_matcher_store_keyframe");
   if (!h) return mfail(SFM_EINVAL, "handle is NULL");
   if (slot < 0 || slot > (1 << 20) || n < 0 || (n > 0 && (!pts || !desc))) return mfail(SFM_EINVAL, "bad keyframe arguments");
   if (hipSetDevice(h->device) != hipSuccess) return mfail(SFM_EIO, "hipSetDevice failed");
@@ -652,6 +657,7 @@ int sfm_matcher_match_keyframes(sfm_matcher* h, int32_t q_slot, const int32_t* q
                                 int32_t t_slot, const int32_t* t_idx, int32_t n_t, double ratio_test,
                                 double min_distance, double max_distance, int32_t* idx0, int32_t* idx1,
                                 int32_t* n_matches) {
+  SFM_TRACE("sfm_matcher_match_keyframes");
   if (!h || !n_matches) return mfail(SFM_EINVAL, "NULL argument");
   *n_matches = 0;
   if (q_slot < 0 || t_slot < 0 || size_t(q_slot) >= h->kf.size() || size_t(t_slot) >= h->kf.size())
@@ -833,6 +839,7 @@ int sfm_track_pnp(sfm_matcher* h, sfm_map* map, int32_t n_prev, const int32_t* p
                   double min_distance, double max_distance, int32_t min_matches, const double* K9, int32_t iterations,
                   double reproj_err, double confidence, double* rvec, double* tvec, int32_t* found,
                   int32_t* n_matches, int32_t capacity, int32_t* inl_kp, int32_t* inl_pt3d, int32_t* n_inliers) {
+  SFM_TRACE("sfm_track_pnp");
   if (!h || !map || !found || !n_matches || !n_inliers || !rvec || !tvec || !K9) return mfail(SFM_EINVAL, "NULL argument");
   *found = 0;
   *n_matches = 0;

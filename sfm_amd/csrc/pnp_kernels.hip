@@ -29,6 +29,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include "sfm_trace.h"
 #include "../../include/sfm_amd.h"
 #include "cv_linalg.h"
 
@@ -1099,6 +1100,7 @@ using namespace sfm;
 extern "C" int sfm_pnp_ransac(int32_t device, int32_t n, const double* obj, const double* img, const double* K9,
                               int32_t iterations, double reproj_err, double confidence, double* rvec, double* tvec,
                               int32_t* inliers, int32_t* n_inliers, int32_t* found) {
+  SFM_TRACE("sfm_pnp_ransac");
   if (!found || !n_inliers || !rvec || !tvec || !K9) return pfail(SFM_EINVAL, "NULL argument");
   *found = 0;
   *n_inliers = 0;
