@@ -24,9 +24,11 @@ __device__ __forceinline__ double wave_max(double v) {
 // partials; `fail` != nullptr also copies the Cholesky failure int into the
 // slot after the scalars.  k_reduce_batch and the device LM loop's
 // k_reduce_batch_lm (ba_solver.hip) share it.
+// sc1: the results stored write-through (sc1), for a consumer in the same
+// launch that loads them sc1 after the counter (k_reduce_batch_lm).
 __device__ __forceinline__ void reduce_batch_job(const double* __restrict__ partials, int64_t max_blocks,
                                                  const ReduceJob& j, double* __restrict__ scal,
-                                                 const int* __restrict__ fail, double* sh) {
+                                                 const int* __restrict__ fail, double* sh, bool sc1 = false) {
   const double* src = partials + size_t(j.slot) * max_blocks;
   double v = 0.0;
   for (int i = threadIdx.x; i < j.nb; i += 1024) v = j.op ? fmax(v, src[i]) : v + src[i];
@@ -37,8 +39,15 @@ __device__ __forceinline__ void reduce_batch_job(const double* __restrict__ part
   if (threadIdx.x == 0) {
     double r = sh[0];
     for (int i = 1; i < 16; ++i) r = j.op ? fmax(r, sh[i]) : r + sh[i];
-    scal[j.dst] = r;
-    if (fail) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
+    if (sc1) {
+      __hip_atomic_store(scal + j.dst, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (fail)
+        __hip_atomic_store(reinterpret_cast<int*>(scal + kNumScalars), *fail, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      scal[j.dst] = r;
+      if (fail) *reinterpret_cast<int*>(scal + kNumScalars) = *fail;
+    }
   }
 }
 // Fixed-order block reduction; result valid in thread 0.  `sh` >= 4 doubles.

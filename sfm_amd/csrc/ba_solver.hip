@@ -496,10 +496,14 @@ __global__ void k_lm_init(LmCtl* c, const double* __restrict__ scal) { lm_init(c
 // workgroup reduces its job (reduce_batch_job, as k_reduce_batch), and the
 // last one to finish runs k_lm_decide's (kPost: k_lm_post's) body on the
 // reduced scalars -- one launch instead of two, ~4.5 us of dispatch each.
-// The scalars are re-read through agent-scope loads after the count (the
-// other workgroups' stores were fenced before their increment); the count
-// lives in the control block, which the loop's upload zeroes, and the last
-// workgroup resets it.  Gated like the reduction: with the phase skipped the
+// The hand-off is MI355X_MICROARCH.md "Valid forms" row 1 without fences:
+// each workgroup's one storing lane stores its scalars sc1, waits for them
+// (vmcnt(0)) and adds to the count; the workgroup whose add returns the last
+// value re-reads every scalar through sc1 loads after a barrier.  (Two
+// __threadfence()s stood there before -- write-back + invalidate of the XCD
+// L2, ~3.5 us each, the second by all 1024 threads.)  The count lives in the
+// control block, which the loop's upload zeroes, and the last workgroup
+// resets it.  Gated like the reduction: with the phase skipped the
 // bookkeeping is a no-op too (run_step = 0 only once done, run_eval = 0).
 enum LmTail { kTailDecide = 0, kTailPost = 1, kTailInit = 2 };
 // Small problems (C <= 256, few points): the accepted step's copy and camera
@@ -529,14 +533,13 @@ __global__ __launch_bounds__(1024) void k_reduce_batch_lm(const double* __restri
   __shared__ double sh[16];
   __shared__ double sc[kNumScalars + 1];
   __shared__ int last;
-  reduce_batch_job(partials, max_blocks, b.job[blockIdx.x], scal, blockIdx.x == 0 ? fail : nullptr, sh);
+  reduce_batch_job(partials, max_blocks, b.job[blockIdx.x], scal, blockIdx.x == 0 ? fail : nullptr, sh, true);
   if (threadIdx.x == 0) {
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the storing lane's sc1 stores landed)
     last = atomicAdd(&c->red_count, 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   // The bookkeeping runs on an LDS copy of the control block, loaded and
   // stored back by the whole workgroup: its branches read and write the
   // block field by field, one dependent memory round trip each in place.
