@@ -1964,13 +1964,14 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   ALLOC(d.cticket, 5);  // task ticket, walker-role ticket, back-substitution role ticket, a panel's two
   // Schur / Cholesky overlap (SFM_OVERLAP=1; unsharded, more than two tiles):
   // per 64x64 tile of S the number of camera blocks (c1 <= c2, stored at
-  // rows 6 c2.., columns 6 c1..) whose 6x6 footprint touches it
-  // (2: the factorisation's full helper grid, its workgroups placed as the
-  // Schur pass's retire)
+  // rows 6 c2.., columns 6 c1..) whose 6x6 footprint touches it.  (The
+  // round-4 mode 2, a full helper grid placed as the Schur pass retires,
+  // relied on the dispatcher starting the Schur pass's workgroups first:
+  // not guaranteed, and seen to time out the factor, so removed.)
   {
     const char* ov = std::getenv("SFM_OVERLAP");
     const int v = ov ? std::atoi(ov) : 0;
-    d.overlap = v > 0 && d.nblk > 2 && !sharded(h) ? (v >= 2 ? 2 : 1) : 0;
+    d.overlap = v > 0 && d.nblk > 2 && !sharded(h) ? 1 : 0;
   }
   if (d.overlap) {
     ALLOC(d.tile_cnt, size_t(d.nblk) * d.nblk);

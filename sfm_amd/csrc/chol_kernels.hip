@@ -1676,7 +1676,7 @@ bool launch_cholesky(const DevProblem& d, int epoch, hipStream_t s, bool clear_f
   // (overlapped with the Schur pass: half the CUs, the other half runs
   // k_schur_pts, whose blocks the helpers await -- at n = 3000 127 helpers
   // factor as fast as 255, 63 take 1.37x)
-  const int full = overlap == 1 ? d.n_cu / 2 - 1 : d.n_cu - 1;
+  const int full = overlap ? d.n_cu / 2 - 1 : d.n_cu - 1;
   const int cap = helpers_env > 0 ? std::min(helpers_env, full) : full;
   const int nhelp = std::max(1, std::min(ntask, cap));
   const int* tc = overlap ? d.tile_cnt : nullptr;

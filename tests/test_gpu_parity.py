@@ -153,3 +153,22 @@ def test_small_system_factor_bitwise_equals_persistent():
         b = rng.standard_normal(n)
         y = dense_spd_solve(A, b)[0]
         assert y.tobytes().hex() == ref[str(n)], n
+
+
+def test_schur_cholesky_overlap_bitwise(monkeypatch):
+    """SFM_OVERLAP=1 (opt-in, read at set_problem): the off-diagonal Schur
+    pass beside the factorisation on a second stream, half the CUs each.
+    Same S tiles, same factor order: the solve bitwise equal to the default
+    one-stream schedule (60 cameras: a 6-tile reduced system)."""
+    s = scene.generate(60, 3000, views=6, seed=11)
+    runs = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("SFM_OVERLAP", ov)
+        r, t, X = s.copy_params()
+        sm, tr = sfm_amd.solve(s.uv, s.cam_idx, s.pt_idx, s.K, r, t, X)
+        runs.append((sm.final_cost, sm.num_iterations, r, t, X))
+    (c0, n0, *p0), (c1, n1, *p1) = runs
+    assert n0 == n1 and n0 >= 1
+    assert c0 == c1
+    for a, b in zip(p0, p1):
+        assert a.tobytes() == b.tobytes()
