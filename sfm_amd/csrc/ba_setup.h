@@ -26,6 +26,24 @@ struct Fill32Set {
   void add(void* p, size_t bytes, uint32_t v) { job[n++] = Job{static_cast<uint32_t*>(p), int64_t(bytes / 4), v}; }
 };
 void launch_fill32(const Fill32Set& fs, hipStream_t s);
+// small device -> pinned host copies (dst: device-mapped pointers of pinned
+// host memory; 4-B words) by one kernel, not by the copy engine
+struct HostCopySet {
+  int n = 0;
+  int32_t* dst[4];
+  const int32_t* src[4];
+  int words[4];
+  void add(void* d, const void* s, size_t bytes) {
+    dst[n] = static_cast<int32_t*>(d);
+    src[n] = static_cast<const int32_t*>(s);
+    words[n] = int(bytes / 4);
+    ++n;
+  }
+};
+void launch_copy_to_host(const HostCopySet& cs, hipStream_t s);
+// pinned host bytes (a device-mapped pointer; bytes a multiple of 16) copied
+// by a kernel on s, not by the copy engine
+void launch_copy_from_host(void* dst, const void* src_host_mapped, size_t bytes, hipStream_t s);
 
 // err[0..2] = first observation with a bad camera index / point index /
 // non-finite uv (INT32_MAX: none); per-camera and per-point counts of the
@@ -39,6 +57,11 @@ void launch_gather_pm(int64_t N, const int32_t* order, const double* uv, const i
 void launch_fill_cm(int64_t N_pad, const int32_t* wcam, const int32_t* cam_rng, const int32_t* cam_off,
                     const int32_t* cm_order, const int32_t* pt_s, const double* uv_pm, int32_t* cm_p, double* uv_cm,
                     int32_t* cam_obs, int32_t* pos, hipStream_t s);
+// (set_problem's deferred uv: uv_pm and uv_cm from the caller-order uv once
+// it has landed, k_gather_pm / k_fill_cm having run with uv = nullptr)
+void launch_uv_layout(int64_t N, int64_t N_pad, const int32_t* order, const int32_t* wcam, const int32_t* cam_rng,
+                      const int32_t* cam_off, const int32_t* cm_order, const double* uv, double* uv_pm, double* uv_cm,
+                      int32_t* err, hipStream_t s);
 void launch_chunk_keys(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, uint32_t* key,
                        int32_t* iota, hipStream_t s);
 void launch_chunk_gather(int n, const int32_t* perm, const int4* ch, const uint32_t* key, int4* out, int32_t* grp,

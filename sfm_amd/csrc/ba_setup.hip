@@ -51,11 +51,12 @@ __global__ __launch_bounds__(kT) void k_validate(int64_t N, const double* __rest
   for (int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x; i < N; i += int64_t(gridDim.x) * kT) {
     const int c = cam[i], p = pt[i];
     const bool cok = c >= 0 && c < C, pok = p >= 0 && p < P;
-    const double2 u = reinterpret_cast<const double2*>(uv)[i];
-    const bool uok = isfinite(u.x) && isfinite(u.y);
     if (!cok) atomicMin(err + 0, int32_t(i));
     if (!pok) atomicMin(err + 1, int32_t(i));
-    if (!uok) atomicMin(err + 2, int32_t(i));
+    if (uv) {  // (nullptr: uv still in flight, checked by k_uv_layout)
+      const double2 u = reinterpret_cast<const double2*>(uv)[i];
+      if (!(isfinite(u.x) && isfinite(u.y))) atomicMin(err + 2, int32_t(i));
+    }
     if (cok && pok) {
       if (lds) atomicAdd(hist + c, 1);
       else atomicAdd(cam_cnt + c, 1);
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(kT) void k_gather_pm(int64_t N, const int32_t* __re
   const int64_t q = int64_t(blockIdx.x) * kT + threadIdx.x;
   if (q >= N) return;
   const int64_t i = order[q];
-  reinterpret_cast<double2*>(uv_pm)[q] = reinterpret_cast<const double2*>(uv)[i];
+  if (uv) reinterpret_cast<double2*>(uv_pm)[q] = reinterpret_cast<const double2*>(uv)[i];
   const int c = cam[i];
   cam_pm[q] = c;
   pt_s[q] = pt[i];
@@ -110,9 +111,37 @@ __global__ __launch_bounds__(kT) void k_fill_cm(int64_t N_pad, const int32_t* __
   const int32_t n_c = cam_off[c + 1] - cam_off[c];
   const int32_t q = cm_order[cam_off[c] + min(j, n_c - 1)];
   cm_p[i] = pt_s[q];
-  reinterpret_cast<double2*>(uv_cm)[i] = reinterpret_cast<const double2*>(uv_pm)[q];
+  if (uv_pm) reinterpret_cast<double2*>(uv_cm)[i] = reinterpret_cast<const double2*>(uv_pm)[q];
   cam_obs[i] = j < n_c ? q : -1;
   if (j < n_c) pos[q] = int32_t(i);
+}
+
+// Large problems upload uv beside the index layouts (set_problem's deferred
+// uv): k_gather_pm / k_fill_cm ran without it, and this pass makes the same
+// two copies -- uv_pm[q] = uv[order[q]], camera-major slot i the uv of the
+// point-major observation k_fill_cm took (padding: the camera's last one) --
+// and k_validate's finite check (first bad caller index into err[2]).
+__global__ __launch_bounds__(kT) void k_uv_layout(int64_t N, int64_t N_pad, const int32_t* __restrict__ order,
+                                                  const int32_t* __restrict__ wcam,
+                                                  const int32_t* __restrict__ cam_rng,
+                                                  const int32_t* __restrict__ cam_off,
+                                                  const int32_t* __restrict__ cm_order, const double* __restrict__ uv,
+                                                  double* __restrict__ uv_pm, double* __restrict__ uv_cm,
+                                                  int32_t* __restrict__ err) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i < N) {
+    const int32_t o = order[i];
+    const double2 u = reinterpret_cast<const double2*>(uv)[o];
+    reinterpret_cast<double2*>(uv_pm)[i] = u;
+    if (!(isfinite(u.x) && isfinite(u.y))) atomicMin(err + 2, o);
+  }
+  if (i < N_pad) {
+    const int c = wcam[i >> 6];
+    const int32_t j = int32_t(i - cam_rng[2 * c]);
+    const int32_t n_c = cam_off[c + 1] - cam_off[c];
+    const int32_t q = cm_order[cam_off[c] + min(j, n_c - 1)];
+    reinterpret_cast<double2*>(uv_cm)[i] = reinterpret_cast<const double2*>(uv)[order[q]];
+  }
 }
 
 // Chunk t of the (camera-major) chunk list: its XCD group is
@@ -282,6 +311,14 @@ __global__ __launch_bounds__(kT) void k_bperm_fill(int64_t n_blk, const int32_t*
   const int x = row_x[blk[b].x];
   const int64_t i = p - grp[x];
   bperm[((i / per) * 8 + x) * per + i % per] = b;
+}
+
+// Host (pinned, device-mapped) -> device copy by a kernel, 16 B per lane
+// (bytes a multiple of 16): a small upload that must not queue behind a large
+// DMA on the copy engine (set_problem's deferred uv)
+__global__ __launch_bounds__(kT) void k_copy_from_host(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                       int64_t n16) {
+  for (int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x; i < n16; i += int64_t(gridDim.x) * kT) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(kT) void k_fill32(Fill32Set fs) {
@@ -593,6 +630,13 @@ void launch_fill_cm(int64_t N_pad, const int32_t* wcam, const int32_t* cam_rng, 
     k_fill_cm<<<nblocks(N_pad), kT, 0, s>>>(N_pad, wcam, cam_rng, cam_off, cm_order, pt_s, uv_pm, cm_p, uv_cm, cam_obs,
                                             pos);
 }
+void launch_uv_layout(int64_t N, int64_t N_pad, const int32_t* order, const int32_t* wcam, const int32_t* cam_rng,
+                      const int32_t* cam_off, const int32_t* cm_order, const double* uv, double* uv_pm, double* uv_cm,
+                      int32_t* err, hipStream_t s) {
+  const int64_t n = std::max(N, N_pad);
+  if (n > 0)
+    k_uv_layout<<<nblocks(n), kT, 0, s>>>(N, N_pad, order, wcam, cam_rng, cam_off, cm_order, uv, uv_pm, uv_cm, err);
+}
 void launch_chunk_keys(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, uint32_t* key,
                        int32_t* iota, hipStream_t s) {
   if (n > 0) k_chunk_keys<<<nblocks(n), kT, 0, s>>>(n, ch, cm_order, pt_s, P, key, iota);
@@ -611,6 +655,21 @@ void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm,
 }
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s) {
   k_seg<<<nblocks(n_blk + 1), kT, 0, s>>>(n_blk, key, n_pairs, seg);
+}
+void launch_copy_from_host(void* dst, const void* src_host_mapped, size_t bytes, hipStream_t s) {
+  const int64_t n16 = int64_t(bytes / 16);
+  if (n16 > 0)
+    k_copy_from_host<<<int(std::min<int64_t>(nblocks(n16), 256)), kT, 0, s>>>(
+        static_cast<uint4*>(dst), static_cast<const uint4*>(src_host_mapped), n16);
+}
+// up to 4 small device -> pinned host copies (4-B words) by one workgroup:
+// readbacks that must not queue behind a DMA on the copy engine
+__global__ __launch_bounds__(kT) void k_copy_to_host(HostCopySet cs) {
+  for (int k = 0; k < cs.n; ++k)
+    for (int i = threadIdx.x; i < cs.words[k]; i += kT) cs.dst[k][i] = cs.src[k][i];
+}
+void launch_copy_to_host(const HostCopySet& cs, hipStream_t s) {
+  if (cs.n > 0) k_copy_to_host<<<1, kT, 0, s>>>(cs);
 }
 void launch_fill32(const Fill32Set& fs, hipStream_t s) {
   if (fs.n == 0) return;

@@ -155,9 +155,10 @@ struct sfm_ba_handle {
   // stream and the two events that fork and join it
   hipStream_t stream2 = nullptr;
   hipEvent_t ov_ev[2] = {nullptr, nullptr};
-  // set_problem's parameter upload beside the layout kernels (large problems)
+  // set_problem's uploads beside the layout kernels (large problems): the
+  // parameters (uev), and uv from a worker thread (uev_uv)
   hipStream_t ustream = nullptr;
-  hipEvent_t uev = nullptr;
+  hipEvent_t uev = nullptr, uev_uv = nullptr;
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev;
@@ -1381,6 +1382,7 @@ int sfm_ba_destroy(sfm_ba_handle* h) {
     hipStreamSynchronize(h->ustream);
     hipStreamDestroy(h->ustream);
     hipEventDestroy(h->uev);
+    if (h->uev_uv) hipEventDestroy(h->uev_uv);
   }
   for (auto e : h->ev) hipEventDestroy(e);
   if (h->comm) ncclCommDestroy(h->comm);
@@ -1475,13 +1477,29 @@ int sfm_ba_set_problem(sfm_ba_handle* h, int64_t n_obs, const double* obs_uv, co
   d.C = C; d.P = P; d.N = N;
   hipStream_t s = h->stream;
   int rc = 0;
+  // large problems: uv goes up from a worker thread (below); it is joined
+  // before any return (the copy writes a buffer of this call and reads the
+  // caller's array)
+  std::atomic<int> uv_state{0};     // 1: uv's copy and event are enqueued, 2: that failed
+  std::atomic<int> param_state{0};  // the same for the parameters' copies (by that worker)
+  struct Joiner {
+    std::thread t;
+    void join() {
+      if (t.joinable()) t.join();
+    }
+    ~Joiner() { join(); }  // (declared after the states: joined before they go)
+  } uv_worker;
   // Any failure returns through here: the buffers go back to the pool.
   auto bail = [&](int code) {
+    uv_worker.join();
     free_problem(h);
     return code;
   };
 // observations up to which set_problem checks and counts them on the host
 constexpr int64_t kHostCheckMaxObs = 65536;
+// and from which uv (16 B each) goes up from a worker thread beside the index
+// layouts (4 MB: the thread's start-up is noise beside the copy)
+constexpr int64_t kDeferredUvMinObs = 262144;
 #define ALLOC(ptr, cnt) if ((rc = dalloc(h, &(ptr), (cnt)))) return bail(rc)
 #define TMP(ptr, cnt) if ((rc = dalloc_tmp(h, &(ptr), (cnt)))) return bail(rc)
 #define HCHK(expr)                                                                                \
@@ -1513,6 +1531,9 @@ constexpr int64_t kHostCheckMaxObs = 65536;
                o_pc = host_check ? up.add(sizeof(int32_t) * (size_t(P) + 1)) : 0;
   const size_t in_bytes = up.bytes;
   const bool stage_in = in_bytes <= kStageMaxBytes;
+  // large problems: uv uploaded beside the index layouts (SFM_SYNC_UV=1: in
+  // line, as before round 6)
+  const bool deferred_uv = !stage_in && N >= kDeferredUvMinObs && !env_flag("SFM_SYNC_UV");
   // (host checks: the camera-run blob below is staged AFTER the input blob,
   // which is still in flight -- no synchronisation in between -- so the
   // stage holds both from here: 2 C + chunks + ... ints, bounded)
@@ -1536,6 +1557,42 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   in_uv = reinterpret_cast<double*>(in_blob + o_uv);
   in_cam = reinterpret_cast<int32_t*>(in_blob + o_cam);
   in_pt = reinterpret_cast<int32_t*>(in_blob + o_pt);
+  std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
+  for (int c = 0; c < C; ++c) {
+    const double* k = K9 + 9 * size_t(c);
+    Kc[5 * c] = k[0]; Kc[5 * c + 1] = k[1]; Kc[5 * c + 2] = k[2]; Kc[5 * c + 3] = k[4]; Kc[5 * c + 4] = k[5];
+    for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
+  }
+  // large problems: the parameters (above the stage's 1 MB) go up from the
+  // caller's pageable arrays on a stream of their own while the layout
+  // kernels run (with a deferred uv, from its worker, before uv) (the host's staging copies took ~0.5 ms at C3 after the
+  // layout round trip, with the device idle); the solve stream waits for them
+  // at the end of set_problem
+  const bool side_params = !early_params && (C || P) && pl.bytes > kStageMaxBytes;
+  if (side_params) {
+    uint8_t* pb = nullptr;
+    ALLOC(pb, pl.bytes);
+    d.Kc = reinterpret_cast<double*>(pb + o_K);
+    d.cam = reinterpret_cast<double*>(pb + o_c);
+    d.cam0 = reinterpret_cast<double*>(pb + o_c0);
+    d.X = reinterpret_cast<double*>(pb + o_X);
+    d.X0 = reinterpret_cast<double*>(pb + o_X0);
+    if (!h->ustream) {
+      HCHK(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
+      HCHK(hipEventCreateWithFlags(&h->uev, hipEventDisableTiming));
+    }
+  }
+  auto params_copies = [&]() -> bool {
+    hipStream_t u = h->ustream;
+    return hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, u) == hipSuccess &&
+           hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, u) == hipSuccess &&
+           hipMemcpyAsync(d.cam0, d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToDevice, u) == hipSuccess &&
+           (!P || (hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, u) == hipSuccess &&
+                   hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, u) ==
+                       hipSuccess)) &&
+           hipEventRecord(h->uev, u) == hipSuccess;
+  };
+  auto upload_params_side = [&]() -> int { return params_copies() ? 0 : fail(SFM_EIO, "parameter upload failed"); };
   int32_t* err = nullptr;
   int32_t* cnt_c = nullptr;
   if (host_check && stage_in) {
@@ -1560,10 +1617,42 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     HCHK(hipMemcpyAsync(in_blob, stg, in_bytes, hipMemcpyHostToDevice, s));
     timer.mark("stage copy + upload");
   } else if (N) {
-    HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(in_cam, cam_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
     HCHK(hipMemcpyAsync(in_pt, pt_idx, sizeof(int32_t) * size_t(N), hipMemcpyHostToDevice, s));
+    if (deferred_uv) {
+      // the indices are up; uv (two thirds of the bytes) goes up from a
+      // worker thread on the side stream -- a pageable copy holds its thread
+      // until the data has left the caller's array -- while this thread lays
+      // out the indices; k_uv_layout takes it once it has landed
+      if (!h->ustream) {
+        HCHK(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
+        HCHK(hipEventCreateWithFlags(&h->uev, hipEventDisableTiming));
+      }
+      if (!h->uev_uv) HCHK(hipEventCreateWithFlags(&h->uev_uv, hipEventDisableTiming));
+      const int dev = h->device;
+      hipStream_t u = h->ustream;
+      hipEvent_t ue = h->uev_uv;
+      // (the parameters first: 5 MB the solve needs only at its start, off
+      // the copy engine before uv's layouts wait on it)
+      uv_worker.t = std::thread([dev, u, ue, in_uv, obs_uv, N, side_params, &params_copies, &uv_state, &param_state]() {
+        bool ok = hipSetDevice(dev) == hipSuccess;
+        if (side_params) param_state.store(ok && params_copies() ? 1 : 2, std::memory_order_release);
+        ok = ok && hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, u) ==
+                       hipSuccess &&
+             hipEventRecord(ue, u) == hipSuccess;
+        uv_state.store(ok ? 1 : 2, std::memory_order_release);
+      });
+    } else {
+      HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
+    }
   }
+  // the solve stream takes uv once the worker has enqueued its copy
+  auto wait_uv = [&]() -> int {
+    uv_worker.join();
+    if (uv_state.load(std::memory_order_acquire) != 1) return fail(SFM_EIO, "observation upload failed");
+    if (hipStreamWaitEvent(s, h->uev_uv, 0) != hipSuccess) return fail(SFM_EIO, "observation upload wait failed");
+    return 0;
+  };
   if (!(host_check && stage_in)) {
     {
       Fill32Set fs;
@@ -1572,13 +1661,22 @@ constexpr int64_t kHostCheckMaxObs = 65536;
       fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
       launch_fill32(fs, s);
     }
-    launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+    launch_validate(N, deferred_uv ? nullptr : in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
     // one round trip: the first bad observation and the per-camera counts
     // (the host lays out the C camera runs and the wavefront chunk table);
     // the readback lands in the stage after the upload has read it (stream order)
     HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * (size_t(C) + 4), hipMemcpyDeviceToHost, s));
     HCHK(hipStreamSynchronize(s));
     std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * (size_t(C) + 4));
+    if (deferred_uv && std::min(cam_cnt[0], cam_cnt[1]) != INT32_MAX) {
+      // a bad index: the whole check once uv is up, so the error reported is
+      // the first bad observation of any kind, as without the deferral
+      if ((rc = wait_uv())) return bail(rc);
+      launch_validate(N, in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+      HCHK(hipMemcpyAsync(stg, err, sizeof(int32_t) * 4, hipMemcpyDeviceToHost, s));
+      HCHK(hipStreamSynchronize(s));
+      std::memcpy(cam_cnt.data(), stg, sizeof(int32_t) * 4);
+    }
   }
   timer.mark("upload + validate");
   {
@@ -1627,12 +1725,6 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   if (small) {
     const int32_t* pc = reinterpret_cast<const int32_t*>(stg + o_pc);
     for (int p = 0; p < P && small; ++p) small = pc[p] <= kSmallSetupMaxPtObs;
-  }
-  std::vector<double> Kc(5 * size_t(C)), cam(6 * size_t(C));
-  for (int c = 0; c < C; ++c) {
-    const double* k = K9 + 9 * size_t(c);
-    Kc[5 * c] = k[0]; Kc[5 * c + 1] = k[1]; Kc[5 * c + 2] = k[2]; Kc[5 * c + 3] = k[4]; Kc[5 * c + 4] = k[5];
-    for (int j = 0; j < 3; ++j) { cam[6 * c + j] = rot[3 * c + j]; cam[6 * c + 3 + j] = t[3 * c + j]; }
   }
   timer.mark("camera runs (host)");
   // ---- resident arrays of the point-major and camera-major layouts ----
@@ -1703,7 +1795,16 @@ constexpr int64_t kHostCheckMaxObs = 65536;
       for (int p = 0; p < P; ++p) po[p + 1] = po[p] + pc[p];
       std::memset(sb + o_fill, 0, sizeof(int32_t) * (size_t(P) + size_t(C)));
     }
-    HCHK(hipMemcpyAsync(ib, sb, il.bytes, hipMemcpyHostToDevice, s));
+    if (deferred_uv) {
+      // uv's 32-MB DMA is on the copy engine now: this blob, on it, would
+      // wait behind it and hold up the layouts, so a kernel reads it from
+      // the pinned stage instead (il.bytes: 256-B aligned pieces)
+      void* sbd = nullptr;
+      HCHK(hipHostGetDevicePointer(&sbd, sb, 0));
+      launch_copy_from_host(ib, sbd, (il.bytes + 15) / 16 * 16, s);
+    } else {
+      HCHK(hipMemcpyAsync(ib, sb, il.bytes, hipMemcpyHostToDevice, s));
+    }
     if (small) {
       d.pt_off = reinterpret_cast<int32_t*>(ib + o_poff);
       small_fill = reinterpret_cast<int32_t*>(ib + o_fill);
@@ -1731,36 +1832,6 @@ constexpr int64_t kHostCheckMaxObs = 65536;
     }
     HCHK(hipMemcpyAsync(pb, ps, pl.bytes, hipMemcpyHostToDevice, s));
   }
-  // large problems: the parameters (above the stage's 1 MB) go up from the
-  // caller's pageable arrays on a stream of their own while the layout
-  // kernels run (the host's staging copies took ~0.5 ms at C3 after the
-  // layout round trip, with the device idle); the solve stream waits for them
-  // at the end of set_problem
-  const bool side_params = !early_params && (C || P) && pl.bytes > kStageMaxBytes;
-  if (side_params) {
-    uint8_t* pb = nullptr;
-    ALLOC(pb, pl.bytes);
-    d.Kc = reinterpret_cast<double*>(pb + o_K);
-    d.cam = reinterpret_cast<double*>(pb + o_c);
-    d.cam0 = reinterpret_cast<double*>(pb + o_c0);
-    d.X = reinterpret_cast<double*>(pb + o_X);
-    d.X0 = reinterpret_cast<double*>(pb + o_X0);
-    if (!h->ustream) {
-      HCHK(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
-      HCHK(hipEventCreateWithFlags(&h->uev, hipEventDisableTiming));
-    }
-  }
-  auto upload_params_side = [&]() -> int {
-    hipStream_t u = h->ustream;
-    if (hipMemcpyAsync(d.Kc, Kc.data(), sizeof(double) * Kc.size(), hipMemcpyHostToDevice, u) != hipSuccess ||
-        hipMemcpyAsync(d.cam, cam.data(), sizeof(double) * cam.size(), hipMemcpyHostToDevice, u) != hipSuccess ||
-        hipMemcpyAsync(d.cam0, d.cam, sizeof(double) * cam.size(), hipMemcpyDeviceToDevice, u) != hipSuccess ||
-        (P && (hipMemcpyAsync(d.X, X, sizeof(double) * 3 * size_t(P), hipMemcpyHostToDevice, u) != hipSuccess ||
-               hipMemcpyAsync(d.X0, d.X, sizeof(double) * 3 * size_t(P), hipMemcpyDeviceToDevice, u) != hipSuccess)) ||
-        hipEventRecord(h->uev, u) != hipSuccess)
-      return fail(SFM_EIO, "parameter upload failed");
-    return 0;
-  };
   int32_t* small_cnt = nullptr;  // small path: per-block pair counts
   if (small) {
     // the same layouts without radix sorts (ba_setup.hip small path):
@@ -1784,11 +1855,12 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   launch_pm_keys(N, in_cam, in_pt, C, k64a, iota, s);
   HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
                     uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
-  launch_gather_pm(N, d.order, in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
+  launch_gather_pm(N, d.order, deferred_uv ? nullptr : in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
   HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
   // camera-major order of the point-major ids: stable sort by camera
   HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
-  launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, d.uv_pm, d.cm_p, d.uv_cm, d.cam_obs, d.pos, s);
+  launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, deferred_uv ? nullptr : d.uv_pm, d.cm_p,
+                 d.uv_cm, d.cam_obs, d.pos, s);
   // chunk table grouped by point slice (stable: camera-major order kept)
   launch_chunk_keys(int(nch), ch_in, cm_order, pt_s, P, k32a, iota, s);
   HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, perm, nch, 7, s));
@@ -1800,7 +1872,7 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
   HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
   // (into the stage: stream order puts it after the upload that reads the stage)
-  HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  if (!deferred_uv) HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   if (small) {
     // no round trip: the pair lists go into a buffer of the pair total's
@@ -1814,9 +1886,21 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   } else {
     // and the 8 slices' chunk offsets: the observation passes size their
     // grids by the largest slice (obs_xcd_blocks)
-    HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (!deferred_uv) HCHK(hipMemcpyAsync(stg + 8, d.jgrp, 9 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     timer.mark("layout launches");
-    if (side_params) {
+    if (deferred_uv) {
+      // the pair total and the slice offsets read back by a kernel into the
+      // pinned stage: uv's DMA holds the copy engine (uv itself is taken
+      // after the pair lists are enqueued, which do not read it)
+      void* stg_d = nullptr;
+      HCHK(hipHostGetDevicePointer(&stg_d, stg, 0));
+      uint8_t* sd = static_cast<uint8_t*>(stg_d);
+      HostCopySet cs;
+      cs.add(sd, poff + N, sizeof(int64_t));
+      cs.add(sd + 8, d.jgrp, 9 * sizeof(int32_t));
+      launch_copy_to_host(cs, s);
+    }
+    if (side_params && !deferred_uv) {
       if ((rc = upload_params_side())) return bail(rc);
       timer.mark("parameter upload (side stream)");
     }
@@ -1854,12 +1938,14 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   d.schur_wg_blocks = d.schur_pts_sub == 64 && d.n_blk <= 4 * 256 &&
                       (d.n_blk ? double(d.n_pairs) / double(d.n_blk) : 0.0) >= 256.0;
   if (const char* sw = std::getenv("SFM_SCHUR_WG")) d.schur_wg_blocks = sw[0] == '1' && d.schur_pts_sub == 64;
-  if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1 + 16)) != hipSuccess) {
+  if (!d.scal_host && hipHostMalloc(&d.scal_host, sizeof(double) * (kNumScalars + 1 + 17)) != hipSuccess) {
     d.scal_host = nullptr;
     return bail(fail(SFM_ENOMEM, "hipHostMalloc failed"));
   }
-  // the pinned mirror's 16-slot tail: the k_schur_pts group sizes
+  // the pinned mirror's 17-slot tail: the k_schur_pts group sizes (16), then
+  // the deferred uv's finite check (slot 16)
   int64_t* grp_host = reinterpret_cast<int64_t*>(d.scal_host + kNumScalars + 1);
+  int32_t* uv_err_host = reinterpret_cast<int32_t*>(grp_host + 16);
   int bperm_per = 0;
   ALLOC(d.blk, std::max<size_t>(1, size_t(d.n_blk)));
   if (!small) ALLOC(d.seg, size_t(d.n_blk) + 1);
@@ -1990,8 +2076,24 @@ constexpr int64_t kHostCheckMaxObs = 65536;
 #undef ALLOC
 #undef TMP
   release_pool(h);  // earlier problems' buffers this one did not reuse
+  if (deferred_uv) {
+    // uv (and before it the parameters) by now up or nearly: its two
+    // layouts and its finite check behind the pair lists, the check read
+    // back by a kernel with the final synchronisation
+    if ((rc = wait_uv())) return bail(rc);
+    timer.mark("uv upload (worker)");
+    launch_uv_layout(N, npad, d.order, d.wcam, d.cam_rng, d_cam_off, cm_order, in_uv, d.uv_pm, d.uv_cm, err, s);
+    void* ue_d = nullptr;
+    HCHK(hipHostGetDevicePointer(&ue_d, uv_err_host, 0));
+    HostCopySet cs;
+    cs.add(ue_d, err + 2, sizeof(int32_t));
+    launch_copy_to_host(cs, s);
+  }
   if (side_params) {
     if (small && (rc = upload_params_side())) return bail(rc);  // (the small path has no layout round trip)
+    // (deferred uv: its worker, joined above, enqueued them)
+    if (deferred_uv && param_state.load(std::memory_order_acquire) != 1)
+      return bail(fail(SFM_EIO, "parameter upload failed"));
     HCHK(hipStreamWaitEvent(s, h->uev, 0));
   } else if ((C || P) && !early_params) {
     if (pl.bytes <= kStageMaxBytes) {
@@ -2046,6 +2148,8 @@ constexpr int64_t kHostCheckMaxObs = 65536;
   static const bool sync_setup = env_flag("SFM_SYNC_SETUP");
   if (!(small && early_params && !bperm_per) || sync_setup) {
     HCHK(hipStreamSynchronize(s));
+    if (deferred_uv && *uv_err_host != INT32_MAX)
+      return bail(fail(SFM_EINVAL, "non-finite observation at " + std::to_string(*uv_err_host)));
     if (bperm_per) {
       int64_t m_max = 1;
       for (int x = 0; x < 8; ++x) m_max = std::max<int64_t>(m_max, (grp_host[8 + x] + bperm_per - 1) / bperm_per);

@@ -250,6 +250,58 @@ def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
         assert sm.num_iterations > 0
 
 
+def test_large_set_problem_uploads_uv_beside_the_index_layouts(monkeypatch):
+    """Above 262144 observations uv goes up from a worker thread while the
+    index layouts run (ba_solver.hip, deferred uv; k_uv_layout makes uv_pm /
+    uv_cm and the finite check once it has landed).  SFM_SYNC_UV=1 uploads
+    it in line: both give the same evaluate() outputs and solve, bit for bit."""
+    s = scene.config("C2")
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_SYNC_UV", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            ev = ba.evaluate()
+            sm, tr = ba.solve()
+            out.append((ev, sm.final_cost, tr, ba.parameters()))
+    (ev0, c0, tr0, p0), (ev1, c1, tr1, p1) = out
+    assert ev0[0] == ev1[0] and np.array_equal(ev0[1], ev1[1]) and np.array_equal(ev0[2], ev1[2])
+    assert c0 == c1 and tr0 == tr1
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["cam", "uv", "uv_before_cam", "cam_before_uv"])
+def test_large_set_problem_rejects_the_first_bad_observation(kind):
+    """The deferred-uv path checks the indices first and uv once it has
+    landed; the error still names the FIRST bad observation of any kind
+    (a bad index makes it wait for uv and run the whole check)."""
+    s = scene.config("C2")
+    uv, cam = s.uv.copy(), s.cam_idx.copy()
+    if kind == "cam":
+        cam[[400000, 123457]] = s.n_cams
+        want = "cam_idx out of range at 123457"
+    elif kind == "uv":
+        uv[400001, 1] = np.nan
+        uv[300000, 0] = np.inf
+        want = "non-finite observation at 300000"
+    elif kind == "uv_before_cam":
+        uv[200000, 0] = np.nan
+        cam[300000] = -1
+        want = "non-finite observation at 200000"
+    else:
+        uv[300000, 1] = np.inf
+        cam[200000] = s.n_cams + 3
+        want = "cam_idx out of range at 200000"
+    with sfm_amd.BundleAdjuster() as ba:
+        with pytest.raises(sfm_amd.SfmError) as ei:
+            ba.set_problem(uv, cam, s.pt_idx, s.K, s.rot, s.t, s.X)
+        assert want in str(ei.value)
+        ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+        sm, _ = ba.solve()
+        assert sm.num_iterations > 0
+
+
 def test_device_layout_keeps_caller_order_of_duplicates():
     """Observations of one (point, camera) pair keep the caller's order in
     the device-built point-major layout (stable radix sort), so the
