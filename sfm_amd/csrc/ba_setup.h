@@ -62,6 +62,8 @@ void launch_fill_cm(int64_t N_pad, const int32_t* wcam, const int32_t* cam_rng, 
 void launch_uv_layout(int64_t N, int64_t N_pad, const int32_t* order, const int32_t* wcam, const int32_t* cam_rng,
                       const int32_t* cam_off, const int32_t* cm_order, const double* uv, double* uv_pm, double* uv_cm,
                       int32_t* err, hipStream_t s);
+// pt_off (P + 1 entries) from the sorted point-major keys point * C + camera
+void launch_pt_off(int P, const uint64_t* sorted_keys, int64_t N, int C, int32_t* pt_off, hipStream_t s);
 void launch_chunk_keys(int n, const int4* ch, const int32_t* cm_order, const int32_t* pt_s, int P, uint32_t* key,
                        int32_t* iota, hipStream_t s);
 void launch_chunk_gather(int n, const int32_t* perm, const int4* ch, const uint32_t* key, int4* out, int32_t* grp,

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kT) void k_validate(int64_t N, const double* __rest
     if (cok && pok) {
       if (lds) atomicAdd(hist + c, 1);
       else atomicAdd(cam_cnt + c, 1);
-      atomicAdd(pt_cnt + p, 1);
+      if (pt_cnt) atomicAdd(pt_cnt + p, 1);  // (nullptr: pt_off from the sorted keys, k_pt_off)
     }
   }
   __syncthreads();
@@ -176,8 +176,14 @@ __global__ __launch_bounds__(kT) void k_chunk_gather(int n, const int32_t* __res
   }
 }
 
-// Pairs of the camera-major observation list entry i (unpadded): o2 in the
-// point's segment with camera >= c1, o2 != o1.
+// Pairs of observation o1 (entry i of the camera-major list, unpadded; or,
+// cm_order == nullptr, point-major observation i): o2 in the point's segment
+// with camera >= c1, o2 != o1.  The stable sort by block that follows keeps,
+// within a block (c1, c2), the emission order of its o1 -- camera c1's
+// observations, in point-major order either way (the camera-major list holds
+// each camera's run in point-major order) -- so both emissions give the same
+// lists.  Point-major emission reads each point's run from adjacent threads
+// (one gather per run instead of one per observation).
 __global__ __launch_bounds__(kT) void k_pair_count(int64_t N, const int32_t* __restrict__ cm_order,
                                                    const int32_t* __restrict__ cam_pm,
                                                    const int32_t* __restrict__ pt_s,
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(kT) void k_pair_count(int64_t N, const int32_t* __r
   const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
   if (i > N) return;
   if (i == N) { cnt[N] = 0; return; }
-  const int32_t o1 = cm_order[i];
+  const int32_t o1 = cm_order ? cm_order[i] : int32_t(i);
   const int c1 = cam_pm[o1], p = pt_s[o1];
   int64_t k = 0;
   for (int32_t o2 = pt_off[p]; o2 < pt_off[p + 1]; ++o2) k += (cam_pm[o2] >= c1 && o2 != o1) ? 1 : 0;
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(kT) void k_pair_fill(int64_t N, const int32_t* __re
                                                   int C, uint32_t* __restrict__ key, int32_t* __restrict__ val) {
   const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
   if (i >= N) return;
-  const int32_t o1 = cm_order[i];
+  const int32_t o1 = cm_order ? cm_order[i] : int32_t(i);
   const int c1 = cam_pm[o1], p = pt_s[o1];
   const int64_t rs = row_start(c1, C) - c1;
   int64_t k = off[i];
@@ -212,6 +218,22 @@ __global__ __launch_bounds__(kT) void k_pair_fill(int64_t N, const int32_t* __re
       ++k;
     }
   }
+}
+
+// pt_off[p] = first point-major observation of point p: the lower bound of
+// p * C in the sorted (point, camera) keys -- the exclusive sum of the point
+// counts, without k_validate's 2M scattered count atomics.
+__global__ __launch_bounds__(kT) void k_pt_off(int P, const uint64_t* __restrict__ key, int64_t N, int C,
+                                               int32_t* __restrict__ pt_off) {
+  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (p > P) return;
+  const uint64_t t = uint64_t(p) * uint64_t(C);
+  int64_t lo = 0, hi = N;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (key[mid] < t) lo = mid + 1; else hi = mid;
+  }
+  pt_off[p] = int32_t(lo);
 }
 
 // seg[b] = first pair of block b (lower bound of b in the sorted keys).
@@ -652,6 +674,9 @@ void launch_pair_count(int64_t N, const int32_t* cm_order, const int32_t* cam_pm
 void launch_pair_fill(int64_t N, const int32_t* cm_order, const int32_t* cam_pm, const int32_t* pt_s,
                       const int32_t* pt_off, const int64_t* off, int C, uint32_t* key, int32_t* val, hipStream_t s) {
   if (N > 0) k_pair_fill<<<nblocks(N), kT, 0, s>>>(N, cm_order, cam_pm, pt_s, pt_off, off, C, key, val);
+}
+void launch_pt_off(int P, const uint64_t* sorted_keys, int64_t N, int C, int32_t* pt_off, hipStream_t s) {
+  k_pt_off<<<nblocks(int64_t(P) + 1), kT, 0, s>>>(P, sorted_keys, N, C, pt_off);
 }
 void launch_seg(int64_t n_blk, const uint32_t* key, int64_t n_pairs, int32_t* seg, hipStream_t s) {
   k_seg<<<nblocks(n_blk + 1), kT, 0, s>>>(n_blk, key, n_pairs, seg);

@@ -1661,7 +1661,8 @@ constexpr int64_t kDeferredUvMinObs = 262144;
       fs.add(cnt_p, sizeof(int32_t) * (size_t(P) + 1), 0);
       launch_fill32(fs, s);
     }
-    launch_validate(N, deferred_uv ? nullptr : in_uv, in_cam, in_pt, C, P, err, cnt_c, cnt_p, s);
+    // (deferred uv: no point counts either -- pt_off comes from the sorted keys)
+    launch_validate(N, deferred_uv ? nullptr : in_uv, in_cam, in_pt, C, P, err, cnt_c, deferred_uv ? nullptr : cnt_p, s);
     // one round trip: the first bad observation and the per-camera counts
     // (the host lays out the C camera runs and the wavefront chunk table);
     // the readback lands in the stage after the upload has read it (stream order)
@@ -1730,6 +1731,7 @@ constexpr int64_t kDeferredUvMinObs = 262144;
   // ---- resident arrays of the point-major and camera-major layouts ----
   int64_t n_pairs = 0;
   int32_t *pt_s = nullptr, *cm_order = nullptr;
+  const int32_t* pair_order = nullptr;  // the Schur pair lists' emission order (nullptr: point-major)
   int64_t* poff = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_bytes = 0;
@@ -1856,7 +1858,8 @@ constexpr int64_t kDeferredUvMinObs = 262144;
   HCHK(sort_pairs64(sort_tmp, sort_bytes, k64a, k64b, iota, d.order, N,
                     uint64_t(std::max(1, P)) * uint64_t(std::max(1, C)) - 1, s));
   launch_gather_pm(N, d.order, deferred_uv ? nullptr : in_uv, in_cam, in_pt, d.uv_pm, d.cam_pm, pt_s, k32a, iota, s);
-  HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
+  if (deferred_uv) launch_pt_off(P, k64b, N, C, d.pt_off, s);
+  else HCHK(exclusive_sum32(sort_tmp, sort_bytes, cnt_p, d.pt_off, int64_t(P) + 1, s));
   // camera-major order of the point-major ids: stable sort by camera
   HCHK(sort_pairs32(sort_tmp, sort_bytes, k32a, k32b, iota, cm_order, N, uint64_t(std::max(1, C)) - 1, s));
   launch_fill_cm(npad, d.wcam, d.cam_rng, d_cam_off, cm_order, pt_s, deferred_uv ? nullptr : d.uv_pm, d.cm_p,
@@ -1869,7 +1872,9 @@ constexpr int64_t kDeferredUvMinObs = 262144;
   int64_t* pcnt = nullptr;
   TMP(pcnt, size_t(N) + 1);
   TMP(poff, size_t(N) + 1);
-  launch_pair_count(N, cm_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
+  // (point-major emission: the same lists; SFM_PAIRS_CM=1 emits in camera-major order)
+  pair_order = env_flag("SFM_PAIRS_CM") ? cm_order : nullptr;
+  launch_pair_count(N, pair_order, d.cam_pm, pt_s, d.pt_off, pcnt, s);
   HCHK(exclusive_sum64(sort_tmp, sort_bytes, pcnt, poff, N + 1, s));
   // (into the stage: stream order puts it after the upload that reads the stage)
   if (!deferred_uv) HCHK(hipMemcpyAsync(stg, poff + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1969,7 +1974,7 @@ constexpr int64_t kDeferredUvMinObs = 262144;
       sort_tmp = tb;
       sort_bytes = need;
     }
-    launch_pair_fill(N, cm_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
+    launch_pair_fill(N, pair_order, d.cam_pm, pt_s, d.pt_off, poff, C, bk_a, bv, s);
     HCHK(sort_pairs32(sort_tmp, sort_bytes, bk_a, bk_b, bv, d.bpts, n_pairs, uint64_t(std::max<int64_t>(1, d.n_blk)) - 1,
                       s));
     launch_seg(d.n_blk, bk_b, n_pairs, d.seg, s);
@@ -2078,16 +2083,21 @@ constexpr int64_t kDeferredUvMinObs = 262144;
   release_pool(h);  // earlier problems' buffers this one did not reuse
   if (deferred_uv) {
     // uv (and before it the parameters) by now up or nearly: its two
-    // layouts and its finite check behind the pair lists, the check read
-    // back by a kernel with the final synchronisation
-    if ((rc = wait_uv())) return bail(rc);
+    // layouts and its finite check on the side stream, behind its copy and
+    // beside the pair lists (the index layouts they read are complete: the
+    // host synchronised on them), the check read back by a kernel with the
+    // final synchronisation
+    uv_worker.join();
+    if (uv_state.load(std::memory_order_acquire) != 1) return bail(fail(SFM_EIO, "observation upload failed"));
     timer.mark("uv upload (worker)");
-    launch_uv_layout(N, npad, d.order, d.wcam, d.cam_rng, d_cam_off, cm_order, in_uv, d.uv_pm, d.uv_cm, err, s);
+    hipStream_t u = h->ustream;
+    launch_uv_layout(N, npad, d.order, d.wcam, d.cam_rng, d_cam_off, cm_order, in_uv, d.uv_pm, d.uv_cm, err, u);
     void* ue_d = nullptr;
     HCHK(hipHostGetDevicePointer(&ue_d, uv_err_host, 0));
     HostCopySet cs;
     cs.add(ue_d, err + 2, sizeof(int32_t));
-    launch_copy_to_host(cs, s);
+    launch_copy_to_host(cs, u);
+    HCHK(hipEventRecord(h->uev_uv, u));  // (the solve stream waits for it after its own fills, below)
   }
   if (side_params) {
     if (small && (rc = upload_params_side())) return bail(rc);  // (the small path has no layout round trip)
@@ -2146,6 +2156,7 @@ constexpr int64_t kDeferredUvMinObs = 262144;
   // (SFM_SYNC_SETUP=1: always synchronise, so that a fault in a layout kernel
   // is reported by set_problem itself, not by the next call)
   static const bool sync_setup = env_flag("SFM_SYNC_SETUP");
+  if (deferred_uv) HCHK(hipStreamWaitEvent(s, h->uev_uv, 0));
   if (!(small && early_params && !bperm_per) || sync_setup) {
     HCHK(hipStreamSynchronize(s));
     if (deferred_uv && *uv_err_host != INT32_MAX)

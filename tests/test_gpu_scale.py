@@ -271,6 +271,27 @@ def test_large_set_problem_uploads_uv_beside_the_index_layouts(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_point_major_pair_emission_is_bitwise_the_camera_major_one(cfg, monkeypatch):
+    """The Schur pair lists are emitted in point-major order (a point's run
+    read by adjacent threads) and stably sorted by block; within a block the
+    order is camera c1's observations in point-major order either way, so
+    the lists -- and the solve -- are bitwise those of the camera-major
+    emission (SFM_PAIRS_CM=1).  C3 also covers the XCD work order (bperm)."""
+    s = scene.config(cfg)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFM_PAIRS_CM", flag)
+        with sfm_amd.BundleAdjuster() as ba:
+            ba.set_problem(s.uv, s.cam_idx, s.pt_idx, s.K, s.rot, s.t, s.X)
+            sm, tr = ba.solve()
+            out.append((sm.final_cost, tr, ba.parameters()))
+    (c0, tr0, p0), (c1, tr1, p1) = out
+    assert c0 == c1 and tr0 == tr1
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("kind", ["cam", "uv", "uv_before_cam", "cam_before_uv"])
 def test_large_set_problem_rejects_the_first_bad_observation(kind):
     """The deferred-uv path checks the indices first and uv once it has
