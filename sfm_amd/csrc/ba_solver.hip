@@ -1634,14 +1634,20 @@ constexpr int64_t kDeferredUvMinObs = 262144;
       hipEvent_t ue = h->uev_uv;
       // (the parameters first: 5 MB the solve needs only at its start, off
       // the copy engine before uv's layouts wait on it)
-      uv_worker.t = std::thread([dev, u, ue, in_uv, obs_uv, N, side_params, &params_copies, &uv_state, &param_state]() {
+      auto uv_job = [dev, u, ue, in_uv, obs_uv, N, side_params, &params_copies, &uv_state, &param_state]() {
         bool ok = hipSetDevice(dev) == hipSuccess;
         if (side_params) param_state.store(ok && params_copies() ? 1 : 2, std::memory_order_release);
         ok = ok && hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, u) ==
                        hipSuccess &&
              hipEventRecord(ue, u) == hipSuccess;
         uv_state.store(ok ? 1 : 2, std::memory_order_release);
-      });
+      };
+      // (no exception crosses the C ABI: without a thread the copies run here)
+      try {
+        uv_worker.t = std::thread(uv_job);
+      } catch (...) {
+        uv_job();
+      }
     } else {
       HCHK(hipMemcpyAsync(in_uv, obs_uv, sizeof(double) * 2 * size_t(N), hipMemcpyHostToDevice, s));
     }
