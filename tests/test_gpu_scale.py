@@ -250,12 +250,15 @@ def test_set_problem_rejects_bad_observations_at_the_first_index(kind):
         assert sm.num_iterations > 0
 
 
-def test_large_set_problem_uploads_uv_beside_the_index_layouts(monkeypatch):
+@pytest.mark.parametrize("cfg", ["C2", "small-params"])
+def test_large_set_problem_uploads_uv_beside_the_index_layouts(cfg, monkeypatch):
     """Above 262144 observations uv goes up from a worker thread while the
     index layouts run (ba_solver.hip, deferred uv; k_uv_layout makes uv_pm /
     uv_cm and the finite check once it has landed).  SFM_SYNC_UV=1 uploads
-    it in line: both give the same evaluate() outputs and solve, bit for bit."""
-    s = scene.config("C2")
+    it in line: both give the same evaluate() outputs and solve, bit for bit.
+    C2's parameters (2.4 MB) ride with the worker; "small-params" (300k
+    observations, 0.97 MB of parameters) stages them after the layouts."""
+    s = scene.config("C2") if cfg == "C2" else scene.generate(50, 20000, views=15, seed=5)
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("SFM_SYNC_UV", flag)
